@@ -1,0 +1,187 @@
+"""ctypes bindings for the CPU oracle (oracle/liborc.so) and, where present, the
+reference-compiled checker (oracle/_ref/libtbfref.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py -- never by the product package.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+ORC_SO = ROOT / "oracle" / "liborc.so"
+REF_SO = ROOT / "oracle" / "_ref" / "libtbfref.so"
+
+_fp = C.POINTER(C.c_float)
+_dp = C.POINTER(C.c_double)
+_u32p = C.POINTER(C.c_uint32)
+
+
+def _f(a):
+    return None if a is None else a.ctypes.data_as(_fp)
+
+
+def load_oracle():
+    if not ORC_SO.exists():
+        raise FileNotFoundError(f"{ORC_SO} missing -- run `make -C oracle`")
+    lib = C.CDLL(str(ORC_SO))
+    lib.orc_template_new.restype = C.c_void_p
+    lib.orc_template_new.argtypes = [C.c_double, C.c_void_p, C.c_void_p, C.c_uint]
+    lib.orc_template_free.argtypes = [C.c_void_p]
+    lib.orc_template_dump.argtypes = [C.c_void_p, C.c_char_p]
+    lib.orc_template_bank_size.restype = C.c_size_t
+    lib.orc_template_bank_size.argtypes = [C.c_void_p]
+    lib.orc_template_bank.argtypes = [C.c_void_p, _fp, _u32p]
+    lib.orc_template_envs.argtypes = [C.c_void_p, _fp, _fp, _fp]
+    lib.orc_fitwave.restype = C.c_size_t
+    lib.orc_fitwave.argtypes = [C.c_double, C.c_double, C.c_int, C.c_int, C.c_double]
+    lib.orc_get_frequencies.argtypes = [_dp, C.c_void_p]
+    lib.orc_infer_scale_size.argtypes = [_dp, C.POINTER(C.c_int), C.POINTER(C.c_float)]
+    lib.orc_srand.argtypes = [C.c_void_p, C.c_uint]
+    lib.orc_rand_next.restype = C.c_int32
+    lib.orc_rand_next.argtypes = [C.c_void_p]
+    lib.orc_inst_new.restype = C.c_void_p
+    lib.orc_inst_new.argtypes = [C.c_void_p, C.c_uint]
+    lib.orc_inst_free.argtypes = [C.c_void_p]
+    lib.orc_note.argtypes = [C.c_void_p, C.c_int, C.c_int]
+    lib.orc_set_param.argtypes = [C.c_void_p, C.c_int, C.c_double]
+    lib.orc_set_chain.argtypes = [C.c_void_p, C.c_int]
+    lib.orc_render.argtypes = [C.c_void_p, C.c_int, _fp, _fp, _fp, _fp, _fp]
+    for pre in ("orc",):
+        getattr(lib, f"{pre}_whirl_new").restype = C.c_void_p
+        getattr(lib, f"{pre}_whirl_new").argtypes = [C.c_double]
+        getattr(lib, f"{pre}_whirl_rev_option").argtypes = [C.c_void_p, C.c_int]
+        getattr(lib, f"{pre}_whirl_proc3").argtypes = [C.c_void_p, _fp, _fp, _fp, C.c_int]
+        getattr(lib, f"{pre}_whirl_free").argtypes = [C.c_void_p]
+        getattr(lib, f"{pre}_reverb_new").restype = C.c_void_p
+        getattr(lib, f"{pre}_reverb_new").argtypes = [C.c_double, C.c_uint]
+        getattr(lib, f"{pre}_reverb_set_mix").argtypes = [C.c_void_p, C.c_float]
+        getattr(lib, f"{pre}_reverb_proc").argtypes = [C.c_void_p, _fp, _fp, C.c_int]
+        getattr(lib, f"{pre}_reverb_free").argtypes = [C.c_void_p]
+        getattr(lib, f"{pre}_preamp_new").restype = C.c_void_p
+        getattr(lib, f"{pre}_preamp_new").argtypes = [C.c_double, C.c_uint]
+        getattr(lib, f"{pre}_preamp_set").argtypes = [C.c_void_p, C.c_int, C.c_float]
+        getattr(lib, f"{pre}_preamp_proc").argtypes = [C.c_void_p, _fp, _fp, C.c_int]
+        getattr(lib, f"{pre}_preamp_free").argtypes = [C.c_void_p]
+    return lib
+
+
+def load_ref():
+    """The reference-compiled checker; None when not built (e.g. on the GPU box)."""
+    if not REF_SO.exists():
+        return None
+    lib = C.CDLL(str(REF_SO))
+    lib.ref_inst_new.restype = C.c_void_p
+    lib.ref_inst_new.argtypes = [C.c_void_p, C.c_uint]
+    lib.ref_inst_free.argtypes = [C.c_void_p]
+    lib.ref_note.argtypes = [C.c_void_p, C.c_int, C.c_int]
+    lib.ref_set_param.argtypes = [C.c_void_p, C.c_int, C.c_double]
+    lib.ref_set_chain.argtypes = [C.c_void_p, C.c_int]
+    lib.ref_render.argtypes = [C.c_void_p, C.c_int, _fp, _fp, _fp, _fp, _fp]
+    lib.ref_whirl_new.restype = C.c_void_p
+    lib.ref_whirl_new.argtypes = [C.c_double]
+    lib.ref_whirl_rev_option.argtypes = [C.c_void_p, C.c_int]
+    lib.ref_whirl_proc3.argtypes = [C.c_void_p, _fp, _fp, _fp, C.c_int]
+    lib.ref_whirl_free.argtypes = [C.c_void_p]
+    lib.ref_reverb_new.restype = C.c_void_p
+    lib.ref_reverb_new.argtypes = [C.c_double, C.c_uint]
+    lib.ref_reverb_set_mix.argtypes = [C.c_void_p, C.c_float]
+    lib.ref_reverb_proc.argtypes = [C.c_void_p, _fp, _fp, C.c_int]
+    lib.ref_reverb_free.argtypes = [C.c_void_p]
+    lib.ref_preamp_new.restype = C.c_void_p
+    lib.ref_preamp_new.argtypes = [C.c_double, C.c_uint]
+    lib.ref_preamp_set.argtypes = [C.c_void_p, C.c_int, C.c_float]
+    lib.ref_preamp_proc.argtypes = [C.c_void_p, _fp, _fp, C.c_int]
+    lib.ref_preamp_free.argtypes = [C.c_void_p]
+    return lib
+
+
+class Template:
+    """Tonegen template (wave bank + play matrix + envelopes) built by the oracle."""
+
+    def __init__(self, lib, sr=48000.0, mts128=None, ratio9=None, seed=1):
+        self.lib = lib
+        self._mts = None if mts128 is None else np.ascontiguousarray(mts128, dtype=np.float64)
+        self._rat = None if ratio9 is None else np.ascontiguousarray(ratio9, dtype=np.float64)
+        self.ptr = lib.orc_template_new(
+            float(sr),
+            None if self._mts is None else self._mts.ctypes.data,
+            None if self._rat is None else self._rat.ctypes.data,
+            int(seed),
+        )
+        self.sr = sr
+
+    def bank(self):
+        n = self.lib.orc_template_bank_size(self.ptr)
+        out = np.zeros(n, np.float32)
+        lens = np.zeros(256, np.uint32)
+        self.lib.orc_template_bank(self.ptr, _f(out), lens.ctypes.data_as(_u32p))
+        return out, lens
+
+    def envs(self):
+        a = np.zeros((9, 128), np.float32)
+        r = np.zeros((9, 128), np.float32)
+        k = np.zeros(128, np.float32)
+        self.lib.orc_template_envs(self.ptr, _f(a), _f(r), _f(k))
+        return a, r, k
+
+    def dump(self, d):
+        return self.lib.orc_template_dump(self.ptr, str(d).encode())
+
+    def __del__(self):
+        try:
+            self.lib.orc_template_free(self.ptr)
+        except Exception:
+            pass
+
+
+class Chain:
+    """One organ instance driven through either the oracle or the reference checker."""
+
+    def __init__(self, lib, tpl: Template, seed: int, ref: bool = False):
+        self.lib, self.ref = lib, ref
+        p = "ref" if ref else "orc"
+        self._new = getattr(lib, f"{p}_inst_new")
+        self._note = getattr(lib, f"{p}_note")
+        self._param = getattr(lib, f"{p}_set_param")
+        self._chain = getattr(lib, f"{p}_set_chain")
+        self._render = getattr(lib, f"{p}_render")
+        self._free = getattr(lib, f"{p}_inst_free")
+        self.ptr = self._new(tpl.ptr, int(seed))
+        self.tpl = tpl
+
+    def note(self, key, on):
+        self._note(self.ptr, int(key), int(on))
+
+    def param(self, pid, value):
+        self._param(self.ptr, int(pid), float(value))
+
+    def chain(self, mode):
+        self._chain(self.ptr, int(mode))
+
+    def render(self, nblocks, stages=False):
+        n = nblocks * 128
+        L = np.zeros(n, np.float32)
+        R = np.zeros(n, np.float32)
+        if stages:
+            A = np.zeros(n, np.float32)
+            B = np.zeros(n, np.float32)
+            Cc = np.zeros(n, np.float32)
+            self._render(self.ptr, nblocks, _f(L), _f(R), _f(A), _f(B), _f(Cc))
+            return L, R, A, B, Cc
+        self._render(self.ptr, nblocks, _f(L), _f(R), None, None, None)
+        return L, R
+
+    def __del__(self):
+        try:
+            self._free(self.ptr)
+        except Exception:
+            pass
+
+
+def fptr(a):
+    return _f(a)

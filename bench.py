@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""bench.py -- BASELINE.json metric: stereo samples/sec whole-node, full chain
+(tonegen -> vibrato -> overdrive -> reverb -> whirl) at 48 kHz, 4096 organ instances
+per GPU (configs[2] at N=1; configs[3] = 8 x 4096 at N=8, weak scaling), with
+max|err| vs the CPU chain.
+
+A "step" is one kernel pass over the batch: every instance renders `--blocks`
+128-sample blocks (default 64 = 8192 stereo samples per instance).  Inputs are
+synthetic: instance i plays the "Jazz 1 all" registration (pgm/default.pgm:27-36)
+with overdrive character 0.5, reverb 0.1, rotary chorale, chord root 48+(i mod 24)
++ {0,4,7,12}; note-on lands at block 0 of the first warmup step.
+
+Launch: python bench.py --gpus N --steps K --warmup W   (N>1 under torch.distributed.run,
+one rank per GPU; instances shard across ranks, no data-path collective).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests"))
+
+BYTES_PER_STEREO_SAMPLE = 424  # 8 B output + 13 lines x 2 ch x (8 B write + 8 B read)
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=4096, help="instances per GPU")
+    ap.add_argument("--blocks", type=int, default=64, help="128-sample blocks per step")
+    ap.add_argument("--sr", type=float, default=48000.0)
+    ap.add_argument("--check", type=int, default=4, help="instances checked against the CPU oracle")
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--cpu-instances", type=int, default=64)
+    ap.add_argument("--cpu-blocks", type=int, default=375)
+    return ap.parse_args()
+
+
+def setup_events(eng, first_global, n):
+    import scenarios as S
+    for i in range(n):
+        for (_, kind, a, v) in S.bench_scenario(first_global + i):
+            if kind == "note":
+                eng.note(i, a, v)
+            else:
+                eng.set_param(i, a, v)
+
+
+def _cpu_worker(args):
+    """Oracle (CPU restatement) render of a slice of instances; returns samples and seconds."""
+    idx, blocks, sr = args
+    import scenarios as S
+    from orc_bind import Chain, Template, load_oracle
+    lib = load_oracle()
+    tpl = Template(lib, sr=sr, seed=7)
+    chains = []
+    for i in idx:
+        ch = Chain(lib, tpl, 1000 + i)
+        for (_, kind, a, v) in S.bench_scenario(i):
+            (ch.note if kind == "note" else ch.param)(a, v)
+        chains.append(ch)
+    t0 = time.perf_counter()
+    for ch in chains:
+        ch.render(blocks)
+    return len(idx) * blocks * 128, time.perf_counter() - t0
+
+
+def cpu_baseline(n_inst, blocks, sr):
+    import multiprocessing as mp
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, 16, n_inst))
+    parts = [list(range(k, n_inst, cores)) for k in range(cores)]
+    ctx = mp.get_context("spawn")
+    t0 = time.perf_counter()
+    with ctx.Pool(cores) as pool:
+        res = pool.map(_cpu_worker, [(p, blocks, sr) for p in parts])
+    wall = time.perf_counter() - t0
+    samples = sum(r[0] for r in res)
+    busy = max(r[1] for r in res)  # render time of the slowest worker (construction excluded)
+    return {"value": samples / busy, "unit": "stereo samples/s", "cores": cores, "kind": "port",
+            "sample": f"{n_inst} instances x {blocks} blocks ({blocks * 128 / sr:.2f} s audio each), "
+                      f"oracle/ C restatement, {cores} processes, construction excluded (wall {wall:.1f}s)"}
+
+
+def oracle_check(rank_first, n_check, total_blocks, last_blocks, gpu_L, gpu_R, sr):
+    """max|err| of the last step's outputs vs the CPU oracle for the first instances."""
+    import numpy as np
+    import scenarios as S
+    from orc_bind import Chain, Template, load_oracle
+    lib = load_oracle()
+    tpl = Template(lib, sr=sr, seed=7)
+    err, exact, tot = 0.0, 0, 0
+    for i in range(n_check):
+        g = rank_first + i
+        ch = Chain(lib, tpl, 1000 + g)
+        for (_, kind, a, v) in S.bench_scenario(g):
+            (ch.note if kind == "note" else ch.param)(a, v)
+        ch.render(total_blocks - last_blocks)
+        L, R = ch.render(last_blocks)
+        for x, y in ((gpu_L[i], L), (gpu_R[i], R)):
+            d = np.abs(x.astype(np.float64) - y.astype(np.float64))
+            err = max(err, float(d.max()))
+            exact += int(np.sum(x.view(np.uint32) == y.view(np.uint32)))
+            tot += x.size
+    return err, exact / max(tot, 1)
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import numpy as np
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(0)
+    import tunebfree_amd as T
+
+    B = a.batch
+    first_global = rank * B
+    eng = T.Engine(sample_rate=a.sr, device=torch.cuda.current_device())
+    tid = eng.template(seed=7)
+    eng.add_instances([tid] * B, [1000 + first_global + i for i in range(B)])
+    setup_events(eng, first_global, B)
+    nsamp = a.blocks * 128
+    outL = torch.empty((B, nsamp), dtype=torch.float32, device="cuda")
+    outR = torch.empty((B, nsamp), dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream()
+    sptr = stream.cuda_stream
+
+    def step():
+        eng.render_device(a.blocks, outL.data_ptr(), outR.data_ptr(), nsamp, sptr)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    t0 = time.perf_counter()
+    for k in range(a.steps):
+        ev[k][0].record(stream)
+        step()
+        ev[k][1].record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    total_samples = world * B * nsamp * a.steps
+    value = total_samples / elapsed
+
+    # parity on the last step (first --check instances of this rank)
+    gL = outL[: a.check].cpu().numpy()
+    gR = outR[: a.check].cpu().numpy()
+    total_blocks = (a.warmup + a.steps) * a.blocks
+    max_err, exact = oracle_check(first_global, a.check, total_blocks, a.blocks, gL, gR, a.sr) if a.check else (None, None)
+    if dist:
+        e = torch.tensor([max_err or 0.0], dtype=torch.float64, device="cuda")
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        max_err = float(e.item())
+
+    if rank == 0:
+        per_launch_bytes = B * nsamp * BYTES_PER_STEREO_SAMPLE
+        achieved = per_launch_bytes / (kern_ms * 1e-3) / 1e9
+        cpu = cpu_baseline(a.cpu_instances, a.cpu_blocks, a.sr) if (a.cpu_baseline and world == 1) else None
+        line = {
+            "metric": "stereo samples/sec whole-node, batch=4096 full chain @48kHz; max|err| vs CPU",
+            "value": value, "unit": "stereo samples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32 (f64 reverb/overdrive)", "data": "synthetic",
+            "config": {"workload": f"configs[{2 if world == 1 else 3}]: full chain tonegen->vibrato->overdrive->"
+                                   f"reverb->whirl, {B} instances/GPU x {world} GPU(s), {a.sr:.0f} Hz, "
+                                   f"{a.blocks} blocks/step, Jazz-1 registration + 4-note chords",
+                       "batch_per_gpu": B, "blocks_per_step": a.blocks, "sample_rate": a.sr,
+                       "parallelism": f"instance-sharded x{world} (no collective)"},
+            "max_err": max_err, "bit_exact_frac": exact, "checked_instances": a.check,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "tbf_render_kernel", "kernel_ms_per_launch": kern_ms,
+                         "bytes_per_stereo_sample": BYTES_PER_STEREO_SAMPLE},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

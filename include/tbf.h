@@ -1,0 +1,128 @@
+/*
+ * tbf.h -- C-ABI of the MI355X batched render engine for tuneBfree's DSP chain.
+ *
+ * Drop-in boundary.  The reference evaluates one organ per plugin instance through
+ * four per-block calls issued by synthSound (b_synth/lv2.cpp:212-239,
+ * src/clap.cpp:244-270, src/main.cpp:243-292):
+ *     oscGenerateFragment (struct b_tonegen*, float* buf, size_t)     src/tonegen.h:594
+ *     preamp (void* pa, float* in, float* out, size_t)                 src/overdrive.h:35
+ *     b_reverb::reverb (float* in, float* out, int)                    src/reverb.h:30
+ *     whirlProc3 (struct b_whirl*, const float*, float*, float*,
+ *                 float*, float*, size_t)                              src/whirl.h:245-249
+ * tbf_render / tbf_synth_sound replace that quartet for a batch of instances; the
+ * control surface replaces the host-side calls that mutate the DSP structs between
+ * blocks:
+ *     oscKeyOn / oscKeyOff                      src/tonegen.cpp:3096-3166 -> tbf_note
+ *     CLAP setParam (drawbars, vibrato, rotary,
+ *     overdrive, character, reverb, percussion) src/clap.cpp:162-207     -> tbf_set_param
+ *     allocSynth + initSynth                    b_synth/lv2.cpp:336-353, 164-193
+ *                                               -> tbf_template_create + tbf_instances_add
+ * Event timing is the reference's: anything issued between two render calls takes
+ * effect at the next 128-sample block boundary (b_synth/lv2.cpp:1130-1134).
+ *
+ * Conventions: plain C types, 0 on success, negative errno-style codes on failure
+ * (tbf_last_error() has the message); one host thread per engine; no allocation
+ * inside tbf_render_device once the instance set is fixed.
+ */
+#ifndef TBF_H
+#define TBF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TBF_ABI_VERSION 1
+#define TBF_BLOCK_SAMPLES 128
+
+/* parameter ids: CLAP ids of src/clap.cpp:31-48 ... */
+#define TBF_P_DRAWBAR_MIN 0 /* upper manual drawbars 16' .. 1', value 0..8 */
+#define TBF_P_DRAWBAR_MAX 8
+#define TBF_P_VIBRATO 9            /* upper manual through the scanner, 0/1 */
+#define TBF_P_VIBRATO_TYPE 10      /* 0..5 = V1 C1 V2 C2 V3 C3 */
+#define TBF_P_DRUM 11              /* 0 stop, 1 slow, 2 fast */
+#define TBF_P_HORN 12              /* 0 stop, 1 slow, 2 fast */
+#define TBF_P_OVERDRIVE 13         /* 0 clean, 1 overdrive */
+#define TBF_P_CHARACTER 14         /* 0..1 */
+#define TBF_P_REVERB 15            /* reverb mix 0..1 */
+#define TBF_P_PERCUSSION 16        /* 0/1 */
+#define TBF_P_PERCUSSION_VOLUME 17 /* 1 normal, 0 soft (CLAP convention) */
+#define TBF_P_PERCUSSION_DECAY 18  /* 1 fast, 0 slow */
+#define TBF_P_PERCUSSION_HARMONIC 19 /* 1 second (bus A), 0 third (bus B) */
+/* ... plus the setters the LV2/JACK hosts reach through MIDI CCs (src/midi.cpp) */
+#define TBF_P_BUS_DRAWBAR_BASE 100 /* 100 + bus 0..26 (upper, lower, pedal), value 0..8 */
+#define TBF_P_VIBRATO_LOWER 130    /* lower manual through the scanner, 0/1 */
+#define TBF_P_SWELL 131            /* swell pedal 0..1 (setSwellPedal1FromMIDI) */
+#define TBF_P_WHIRL_BYPASS 132     /* whirl.bypass 0/1 */
+
+#define TBF_CHAIN_FULL 0     /* tonegen -> vibrato -> overdrive -> reverb -> whirl */
+#define TBF_CHAIN_TONEGEN 1  /* oscGenerateFragment only, L = R = tonegen output */
+#define TBF_CHAIN_TAP_PREAMP 2 /* parity tap: L = R = preamp output */
+#define TBF_CHAIN_TAP_REVERB 3 /* parity tap: L = R = reverb output */
+
+typedef struct tbf_engine tbf_engine;
+
+typedef struct tbf_engine_config {
+	double   sample_rate; /* Hz, 22050 .. 96000 */
+	int32_t  device;      /* HIP device ordinal */
+	uint32_t chain_mode;  /* TBF_CHAIN_* */
+	uint32_t reserved[4];
+} tbf_engine_config;
+
+int         tbf_abi_version (void);
+const char* tbf_last_error (void);
+
+int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out);
+int tbf_engine_destroy (tbf_engine* e);
+
+/* Tone-generator template (initToneGenerator's shared tables: wave bank, play matrix,
+ * envelopes) for one tuning.  mts128: 128 MTS-ESP note frequencies or NULL for the
+ * no-master 12-TET table; ratio9: drawbar target ratios or NULL for
+ * {0.5,1.5,1,2,3,4,5,6,8}; seed: srand() seed of the template's rand() stream. */
+int tbf_template_create (tbf_engine* e, const double* mts128, const double* ratio9, uint32_t seed,
+                         uint32_t* tpl_id);
+
+/* Add n instances: instance k uses template tpl_ids[k] and per-instance seed seeds[k]
+ * (srand before allocReverb/allocPreamp).  Returns the first new index in *first. */
+int      tbf_instances_add (tbf_engine* e, uint32_t n, const uint32_t* tpl_ids, const uint32_t* seeds,
+                            uint32_t* first);
+uint32_t tbf_instance_count (const tbf_engine* e);
+
+int tbf_note (tbf_engine* e, uint32_t inst, int32_t key, int32_t on);
+int tbf_set_param (tbf_engine* e, uint32_t inst, int32_t param, double value);
+
+/* Render nblocks x 128 samples for every instance.  Host buffers; instance i writes
+ * out[i * stride + 0 .. nblocks*128).  Synchronous. */
+int tbf_render (tbf_engine* e, uint32_t nblocks, float* outL, float* outR, uint64_t stride);
+
+/* Same into device memory on `stream` (hipStream_t, NULL = engine stream); returns
+ * once the work is enqueued.  Outputs stay in HBM. */
+int tbf_render_device (tbf_engine* e, uint32_t nblocks, float* d_outL, float* d_outR, uint64_t stride,
+                       void* stream);
+
+/* synthSound semantics (b_synth/lv2.cpp:212-239): serve nframes per instance out of
+ * the 128-sample block FIFO, rendering blocks as needed. */
+int tbf_synth_sound (tbf_engine* e, uint32_t nframes, float* outL, float* outR, uint64_t stride);
+
+int tbf_synchronize (tbf_engine* e);
+/* bit 0: vibrato scatter took the serial path in some block (informational) */
+int tbf_error_flags (tbf_engine* e, uint32_t* flags);
+/* read back the wave bank of a template (wheels 1..256 concatenated) for checks */
+int tbf_template_bank (tbf_engine* e, uint32_t tpl_id, float* out, uint64_t cap, uint32_t* lens256);
+
+/* ---- test hooks (host only; used by the parity tests to pin the control plane) ---- */
+/* play-matrix entries of one key (keyContrib, src/tonegen.cpp:1122-1213) */
+int tbf_debug_contrib (tbf_engine* e, uint32_t tpl_id, int32_t key, int16_t* wheel, int16_t* bus, float* level,
+                       uint32_t cap);
+/* envelopes (9 x 128 each) and key-compression table (128) of a template */
+int tbf_debug_tables (tbf_engine* e, uint32_t tpl_id, float* attack, float* release, float* keycomp);
+/* run one block of the tonegen control plane for an instance and return the core
+ * program: per entry {wheel, env, row, sg, pg, vg, nsg, npg, nvg} as 9 floats */
+int tbf_debug_step (tbf_engine* e, uint32_t inst, float* entries9, uint32_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -90,6 +90,7 @@ size_t        orc_template_bank_size (const orc_template* t);
 void          orc_template_bank (const orc_template* t, float* out, uint32_t* lens);
 void          orc_template_envs (const orc_template* t, float* attack9x128, float* release9x128, float* keycomp128);
 size_t        orc_fitwave (double hz, double precision, int minS, int maxS, double rate);
+int           orc_template_contrib (const orc_template* t, int key, int16_t* wheel, int16_t* bus, float* level, int cap);
 
 /* ---------------- instances ---------------- */
 typedef struct orc_inst orc_inst;
@@ -106,6 +107,9 @@ void      orc_set_chain (orc_inst* p, int mode);                   /* 0 full, 1 
 /* render nblocks of the synthSound quartet; any output pointer may be NULL.
  * sA/sB/sC receive the tonegen, preamp and reverb stage outputs. */
 void orc_render (orc_inst* p, int nblocks, float* L, float* R, float* sA, float* sB, float* sC);
+/* the core program of the last orc_render block: 9 floats per instruction
+ * {wheel, opr, envRow, sg, pg, vg, nsg, npg, nvg} (wrap-split halves included) */
+int           orc_debug_program (const orc_inst* p, float* out9, int cap);
 
 /* parameter ids (src/clap.cpp:31-48) */
 #define ORC_P_DRAWBAR_MIN 0

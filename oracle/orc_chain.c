@@ -115,3 +115,15 @@ void orc_render (orc_inst* p, int nblocks, float* L, float* R, float* sA, float*
 			memcpy (R + o, p->bufR, sizeof (p->bufR));
 	}
 }
+
+int orc_debug_program (const orc_inst* p, float* out, int cap)
+{
+	int i;
+	for (i = 0; i < p->tg.corePgmLen && i < cap; i++) {
+		const orc_coreins* c = &p->tg.corePgm[i];
+		float*             o = out + 9 * i;
+		o[0] = (float)c->wheel; o[1] = (float)c->opr; o[2] = (float)c->envRow;
+		o[3] = c->sgain; o[4] = c->pgain; o[5] = c->vgain; o[6] = c->nsgain; o[7] = c->npgain; o[8] = c->nvgain;
+	}
+	return p->tg.corePgmLen;
+}

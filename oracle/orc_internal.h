@@ -55,6 +55,7 @@ typedef struct orc_tonegen {
 	float               keyCompTable[128];
 	int                 keyDownCount;
 	orc_coreins         corePgm[256 * 2 + 8];
+	int                 corePgmLen;
 	unsigned int        newRouting, oldRouting;
 	unsigned int        percSendBus, percSendBusA, percSendBusB;
 	unsigned int        upperKeyCount;

@@ -1002,6 +1002,7 @@ void orc_tg_generate (orc_tonegen* t, float* buf)
 		}
 	}
 
+	t->corePgmLen = (int)(cw - t->corePgm);
 	/* core interpreter (3607-3687) */
 	if (cw == t->corePgm) {
 		for (i = 0; i < BSS; i++)
@@ -1110,4 +1111,15 @@ void orc_tg_generate (orc_tonegen* t, float* buf)
 	}
 	if (t->upperKeyCount == 0)
 		t->percEnvGain = t->percEnvGainReset;
+}
+
+int orc_template_contrib (const orc_template* t, int key, int16_t* wheel, int16_t* bus, float* level, int cap)
+{
+	int i;
+	for (i = 0; i < t->keyContrib[key].n && i < cap; i++) {
+		wheel[i] = t->keyContrib[key].v[i].sa;
+		bus[i]   = t->keyContrib[key].v[i].sb;
+		level[i] = t->keyContrib[key].v[i].fc;
+	}
+	return t->keyContrib[key].n;
 }

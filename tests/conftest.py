@@ -1,0 +1,36 @@
+import os
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI)")
+
+
+def gpu_available():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    from orc_bind import load_oracle
+    return load_oracle()
+
+
+@pytest.fixture(scope="session")
+def refchk():
+    from orc_bind import load_ref
+    lib = load_ref()
+    if lib is None:
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    return lib

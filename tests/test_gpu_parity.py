@@ -1,0 +1,71 @@
+"""GPU parity: the HIP render path (through the C-ABI) against the CPU oracle.
+
+Gate (BASELINE.json north_star): max|err| <= 1e-5 per float32 sample vs the CPU
+chain.  The float32 stages are computed in the reference's literal operation order,
+so the expected outcome is bit-identity; the only licensed source of difference is
+FP64 libm (GPU sin/asin vs glibc), reported as the bit-exact fraction.
+"""
+import numpy as np
+import pytest
+
+import scenarios as S
+from enginerun import compare, engine_run, oracle_run
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+
+
+def _engine(chain=0, sr=48000.0):
+    import tunebfree_amd as T
+    return T.Engine(sample_rate=sr, device=0, chain=chain)
+
+
+def _setup(oracle, n, scen_fn, chain=0, tpl_seed=7, sr=48000.0):
+    from orc_bind import Template
+    eng = _engine(chain, sr)
+    tid = eng.template(seed=tpl_seed)
+    seeds = [1000 + 17 * i for i in range(n)]
+    eng.add_instances([tid] * n, seeds)
+    tpl = Template(oracle, sr=sr, seed=tpl_seed)
+    scens = [scen_fn(i) for i in range(n)]
+    return eng, tpl, seeds, scens
+
+
+def test_gpu_tonegen_only_bitexact(oracle):
+    eng, tpl, seeds, scens = _setup(oracle, 8, lambda i: S.bench_scenario(i, full=False), chain=1)
+    L, R = engine_run(eng, scens, 24)
+    oL, oR, oA, _, _ = oracle_run(oracle, tpl, seeds, scens, 24, chain=1)
+    err, exact = compare(L, oA)
+    print(f"tonegen max|err|={err:.3g} bit-exact={exact:.6f}")
+    assert err == 0.0 and exact == 1.0
+    assert np.array_equal(L, R)
+
+
+@pytest.mark.parametrize("tap,idx", [(2, 3), (3, 4)])
+def test_gpu_stage_taps(oracle, tap, idx):
+    eng, tpl, seeds, scens = _setup(oracle, 6, S.bench_scenario, chain=tap)
+    L, _ = engine_run(eng, scens, 32)
+    ref = oracle_run(oracle, tpl, seeds, scens, 32)[idx]
+    err, exact = compare(L, ref)
+    print(f"tap {tap}: max|err|={err:.3g} bit-exact={exact:.6f}")
+    assert err <= TOL
+
+
+def test_gpu_full_chain_bench(oracle):
+    eng, tpl, seeds, scens = _setup(oracle, 8, S.bench_scenario)
+    L, R = engine_run(eng, scens, 64)
+    oL, oR, *_ = oracle_run(oracle, tpl, seeds, scens, 64)
+    eL, xL = compare(L, oL)
+    eR, xR = compare(R, oR)
+    print(f"full chain: max|err| L={eL:.3g} R={eR:.3g} bit-exact L={xL:.6f} R={xR:.6f}")
+    assert max(eL, eR) <= TOL
+
+
+def test_gpu_full_chain_events(oracle):
+    eng, tpl, seeds, scens = _setup(oracle, 6, S.event_scenario)
+    L, R = engine_run(eng, scens, 72)
+    oL, oR, *_ = oracle_run(oracle, tpl, seeds, scens, 72)
+    eL, xL = compare(L, oL)
+    eR, xR = compare(R, oR)
+    print(f"events: max|err| L={eL:.3g} R={eR:.3g} bit-exact L={xL:.6f} R={xR:.6f}")
+    assert max(eL, eR) <= TOL

@@ -1,0 +1,769 @@
+/*
+ * tbf_engine.cpp -- the C-ABI of include/tbf.h: instance construction (LV2 allocSynth /
+ * initSynth protocol with shared tonegen templates), the host control plane, and the
+ * segmentation of a render into kernel launches at block boundaries where control
+ * changes.
+ */
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/tbf.h"
+#include "tbf_host.h"
+#include "tbf_types.h"
+
+extern "C" int tbf_launch_render (const tbf_launch* P, hipStream_t stream);
+
+using namespace tbf;
+
+static thread_local std::string g_err;
+
+static int fail (int code, const std::string& msg)
+{
+	g_err = msg;
+	return code;
+}
+
+#define HIPCHK(x)                                                                        \
+	do {                                                                                 \
+		hipError_t _e = (x);                                                             \
+		if (_e != hipSuccess)                                                            \
+			return fail (-5, std::string (#x ": ") + hipGetErrorString (_e));           \
+	} while (0)
+
+namespace {
+
+struct Instance {
+	uint32_t       tpl = 0;
+	TgControl      tg;
+	tbf_inst_const k;
+	tbf_inst_state s0;
+	tbf_seg_ctl    ctl;
+	double         params[64];
+	/* preamp (struct b_preamp) */
+	int            odClean = 1;
+	float          odA = 0.0f, odB = 0.0f, odC = 1.0f, odD = 0.5f;
+	/* reverb mix */
+	float          rvG = 0.1f;
+	int            whBypass = 0;
+	int            revOpt = -1;
+	bool           ctlDirty = true;
+	bool           progDirty = true;
+	std::vector<tbf_prog_entry> prog;
+};
+
+template <typename T>
+struct DevBuf {
+	T*     p   = nullptr;
+	size_t cap = 0;
+	int    ensure (size_t n)
+	{
+		if (n <= cap)
+			return 0;
+		if (p)
+			(void)hipFree (p);
+		p   = nullptr;
+		cap = 0;
+		if (hipMalloc ((void**)&p, std::max<size_t> (n, 1) * sizeof (T)) != hipSuccess)
+			return -12;
+		cap = n;
+		return 0;
+	}
+	void release ()
+	{
+		if (p)
+			(void)hipFree (p);
+		p   = nullptr;
+		cap = 0;
+	}
+};
+
+} // namespace
+
+struct tbf_engine {
+	tbf_engine_config                       cfg;
+	hipStream_t                             stream = nullptr;
+	WhirlTables                             wt;
+	std::vector<uint32_t>                   vibTab;
+	uint32_t                                statorInc = 0;
+	uint32_t                                wringLen  = 512;
+	std::vector<std::unique_ptr<TgTemplate>> tpls;
+	std::vector<Instance>                   inst;
+	/* reverb ring layout (identical for all instances: A..F are fixed) */
+	uint32_t                                slabLen = 0;
+	/* device side */
+	bool                                    deviceReady = false;
+	uint32_t                                devInst     = 0;
+	DevBuf<float>                           bank;
+	DevBuf<tbf_tpl_desc>                    tplDesc;
+	DevBuf<tbf_inst_const>                  cst;
+	DevBuf<tbf_inst_state>                  st;
+	DevBuf<float>                           wring;
+	DevBuf<double>                          rslab;
+	DevBuf<tbf_seg_ctl>                     ctl;
+	DevBuf<tbf_prog_entry>                  prog;
+	DevBuf<uint32_t>                        vib;
+	DevBuf<float>                           whTab, whBw;
+	DevBuf<uint32_t>                        err;
+	DevBuf<float>                           outL, outR;
+	std::vector<tbf_seg_ctl>                hCtl;
+	std::vector<tbf_prog_entry>             hProg;
+	/* synth_sound FIFO */
+	std::vector<float>                      fifoL, fifoR;
+	uint32_t                                boffset = TBF_BLK;
+};
+
+#define PROG_CAP (TBF_NW + 1)
+
+/* ------------------------------------------------------------------ construction */
+
+static void reverbConsts (tbf_inst_const& k, double sr, float A, float B, float C, float D, float E, float F)
+{
+	/* src/reverb.cpp:283-336 */
+	double bq0  = ((A * 9000.0) + 1000.0) / sr;
+	double b1[3] = {1.618033988749894848204586, 0.618033988749894848204586, 0.5};
+	for (int q = 0; q < 3; q++) {
+		double K    = tan (M_PI * bq0);
+		double norm = 1.0 / (1.0 + K / b1[q] + K * K);
+		k.bq[q][0]  = K * K * norm;
+		k.bq[q][1]  = 2.0 * k.bq[q][0];
+		k.bq[q][2]  = k.bq[q][0];
+		k.bq[q][3]  = 2.0 * (K * K - 1.0) * norm;
+		k.bq[q][4]  = (1.0 - K / b1[q] + K * K) * norm;
+	}
+	double vibSpeed    = 0.06 + C;
+	double vibDepth    = (0.027 + pow (D, 3)) * 100.0;
+	double size        = (pow (E, 2) * 90.0) + 10.0;
+	double depthFactor = 1.0 - pow ((1.0 - (0.82 - ((B * 0.5) + (size * 0.002)))), 4);
+	double blend       = 0.955 - (size * 0.007);
+	double crossmod    = (F - 0.5) * 2.0;
+	crossmod           = pow (crossmod, 3) * 0.5;
+	double regen       = depthFactor * (0.5 - (fabs (crossmod) * 0.031));
+	static const double depth[8] = {0.003251, 0.002999, 0.002917, 0.002749, 0.002503, 0.002423, 0.002146, 0.002088};
+	static const int    dmul[12] = {79, 73, 71, 67, 61, 59, 53, 47, 43, 41, 37, 31};
+	for (int l = 0; l < 8; l++)
+		k.vibDelta[l] = depth[l] * vibSpeed;
+	k.vibDepth      = vibDepth;
+	k.blend         = blend;
+	k.crossmod      = crossmod;
+	k.oneMinusAbsCm = 1.0 - fabs (crossmod);
+	k.regen         = regen;
+	for (int l = 0; l < 12; l++)
+		k.delay[l] = (int)(dmul[l] * size);
+	k.delay[12] = (int)((29 * size) - (56 * size * fabs (crossmod)));
+	uint32_t o  = 0;
+	for (int c = 0; c < 2; c++)
+		for (int l = 0; l < 13; l++) {
+			k.ringOff[c * 13 + l] = o;
+			o += (uint32_t)((k.delay[l] + 1 + 7) & ~7);
+		}
+	k.slabLen = o;
+}
+
+static void whirlConsts (tbf_inst_const& k, const WhirlTables& wt)
+{
+	memcpy (k.hafw, wt.hafw, sizeof (k.hafw));
+	memcpy (k.hbfw, wt.hbfw, sizeof (k.hbfw));
+	memcpy (k.drf, wt.drf, sizeof (k.drf));
+	memcpy (k.hornSpacing, wt.hornSpacing, sizeof (k.hornSpacing));
+	memcpy (k.drumSpacing, wt.drumSpacing, sizeof (k.drumSpacing));
+	memcpy (k.hornPhase, wt.phase, sizeof (k.hornPhase));
+	const float hornLevel = 0.7f, leakLevel = 0.15f, micAngle = 0.0f;
+	k.leakage   = leakLevel * hornLevel;
+	k.hornLevel = hornLevel;
+	/* default mic widths 0 (src/whirl.cpp:113-117): hll dll hrr drr = 1, others 0 */
+	const float mic[8] = {1.0f, 0.0f, 1.0f, 0.0f, 0.0f, 1.0f, 0.0f, 1.0f};
+	memcpy (k.mic, mic, sizeof (mic));
+	k.fwAng = micAngle * .25;
+	k.bwAng = 1. + micAngle * -.25;
+	memcpy (k.lAcc, wt.lAcc, sizeof (k.lAcc));
+	k.deadzone = (.05 / (60.f * wt.sr));
+	memcpy (k.revHorn, wt.revHorn, sizeof (k.revHorn));
+	memcpy (k.revDrum, wt.revDrum, sizeof (k.revDrum));
+	k.hnBrakePos = 0;
+	k.drBrakePos = 0;
+	k.hnHardstop = (float)(10.f / (60.f * wt.sr));
+	k.drHardstop = (float)(8.f / (60.f * wt.sr));
+	k.minspeed   = (float)(3.f / (60.f * wt.sr));
+	k.hnLimit    = (float)(60.f / (60. * wt.sr));
+	k.drLimit    = (float)(100.f / (60. * wt.sr));
+	k.sr         = wt.sr;
+}
+
+/* preamp per-block constants, src/overdrive.cpp:64-84 and the density/out loops */
+static void odCtl (const Instance& in, double sr, tbf_seg_ctl& c)
+{
+	double overallscale = 1.0;
+	overallscale /= 44100.0;
+	overallscale *= sr;
+	double density = in.odA * 4.0;
+	c.odIir        = pow (in.odB, 3) / overallscale;
+	c.odOutput     = in.odC;
+	c.odWet        = in.odD;
+	c.odDry        = 1.0 - c.odWet;
+	double out     = fabs (density);
+	density        = density * fabs (density);
+	double count   = density;
+	int    iter    = 0;
+	while (count > 1.0) {
+		iter++;
+		count = count - 1.0;
+	}
+	while (out > 1.0)
+		out = out - 1.0;
+	c.odIter       = iter;
+	c.odOut        = out;
+	c.odDensityPos = density > 0 ? 1u : 0u;
+	c.odClean      = (uint32_t)in.odClean;
+}
+
+extern "C" {
+
+int tbf_abi_version (void) { return TBF_ABI_VERSION; }
+const char* tbf_last_error (void) { return g_err.c_str (); }
+
+int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
+{
+	if (!cfg || !out)
+		return fail (-22, "null argument");
+	if (!(cfg->sample_rate >= 8000.0 && cfg->sample_rate <= 192000.0))
+		return fail (-22, "sample_rate out of range");
+	/* device -1: host-only engine (table builders and control plane; render refuses) */
+	if (cfg->device != -1) {
+		int ndev = 0;
+		if (hipGetDeviceCount (&ndev) != hipSuccess || ndev <= 0)
+			return fail (-19, "no HIP device available");
+		if (cfg->device < 0 || cfg->device >= ndev)
+			return fail (-19, "device ordinal out of range");
+	}
+	std::unique_ptr<tbf_engine> e (new tbf_engine ());
+	e->cfg = *cfg;
+	if (cfg->device >= 0) {
+		HIPCHK (hipSetDevice (cfg->device));
+		HIPCHK (hipStreamCreateWithFlags (&e->stream, hipStreamNonBlocking));
+	}
+	e->wt.build (cfg->sample_rate);
+	/* compact whirl ring: live window < maxAhead + 2 + one sub-block */
+	e->wringLen = 512;
+	while ((float)e->wringLen < e->wt.maxAhead + 2.0f + TBF_SUB + 2.0f)
+		e->wringLen *= 2;
+	if (e->wringLen > 2048)
+		return fail (-22, "whirl write-ahead exceeds the reference ring");
+	/* vibrato tables (src/vibrato.cpp:91-95, 224-251) */
+	e->vibTab.resize (3 * 2048);
+	const double amp[3] = {3.0, 6.0, 9.0};
+	for (int t = 0; t < 3; t++)
+		for (int i = 0; i < 2048; i++) {
+			double m                  = sin ((2.0 * M_PI * i) / 2048);
+			e->vibTab[t * 2048 + i] = (unsigned int)((1.0 + amp[t] + (m * amp[t])) * 65536.0);
+		}
+	e->statorInc = (unsigned int)(((7.25 * 2048) / cfg->sample_rate) * 65536.0);
+	*out         = e.release ();
+	return 0;
+}
+
+int tbf_engine_destroy (tbf_engine* e)
+{
+	if (!e)
+		return 0;
+	if (e->cfg.device >= 0)
+		(void)hipSetDevice (e->cfg.device);
+	if (e->stream)
+		(void)hipStreamSynchronize (e->stream);
+	e->bank.release ();
+	e->tplDesc.release ();
+	e->cst.release ();
+	e->st.release ();
+	e->wring.release ();
+	e->rslab.release ();
+	e->ctl.release ();
+	e->prog.release ();
+	e->vib.release ();
+	e->whTab.release ();
+	e->whBw.release ();
+	e->err.release ();
+	e->outL.release ();
+	e->outR.release ();
+	if (e->stream)
+		(void)hipStreamDestroy (e->stream);
+	delete e;
+	return 0;
+}
+
+int tbf_template_create (tbf_engine* e, const double* mts128, const double* ratio9, uint32_t seed, uint32_t* id)
+{
+	if (!e || !id)
+		return fail (-22, "null argument");
+	std::unique_ptr<TgTemplate> t (new TgTemplate ());
+	t->build (e->cfg.sample_rate, mts128, ratio9, seed);
+	*id = (uint32_t)e->tpls.size ();
+	e->tpls.push_back (std::move (t));
+	e->deviceReady = false;
+	return 0;
+}
+
+int tbf_template_bank (tbf_engine* e, uint32_t tid, float* out, uint64_t cap, uint32_t* lens)
+{
+	if (!e || tid >= e->tpls.size ())
+		return fail (-22, "bad template id");
+	const TgTemplate& t = *e->tpls[tid];
+	if (lens)
+		for (int i = 1; i <= TBF_NW; i++)
+			lens[i - 1] = t.len[i];
+	if (out) {
+		if (cap < t.bank.size ())
+			return fail (-28, "buffer too small");
+		memcpy (out, t.bank.data (), t.bank.size () * sizeof (float));
+	}
+	return (int)t.bank.size ();
+}
+
+int tbf_instances_add (tbf_engine* e, uint32_t n, const uint32_t* tpl_ids, const uint32_t* seeds, uint32_t* first)
+{
+	if (!e || (n && (!tpl_ids || !seeds)))
+		return fail (-22, "null argument");
+	const double sr = e->cfg.sample_rate;
+	if (first)
+		*first = (uint32_t)e->inst.size ();
+	for (uint32_t q = 0; q < n; q++) {
+		if (tpl_ids[q] >= e->tpls.size ())
+			return fail (-22, "bad template id");
+		e->inst.emplace_back ();
+		Instance& in = e->inst.back ();
+		in.tpl       = tpl_ids[q];
+		memset (&in.k, 0, sizeof (in.k));
+		memset (&in.s0, 0, sizeof (in.s0));
+		memset (&in.ctl, 0, sizeof (in.ctl));
+		memset (in.params, 0, sizeof (in.params));
+		in.k.tpl = in.tpl;
+		/* allocSynth order: allocReverb (rand x16 vib phases, fpdL, fpdR), allocWhirl,
+		 * allocTonegen, allocPreamp (rand fpd)  -- b_synth/lv2.cpp:336-353 */
+		GlibcRand rnd (seeds[q]);
+		for (int c = 0; c < 2; c++)
+			for (int l = 0; l < 8; l++)
+				in.s0.vib[c][l] = rnd.next () - 2147483647 / 2;
+		uint32_t f = 1;
+		while (f < 16386)
+			f = (uint32_t)rnd.next () * 0xFFFFFFFFu;
+		in.s0.fpdL = f;
+		f          = 1;
+		while (f < 16386)
+			f = (uint32_t)rnd.next () * 0xFFFFFFFFu;
+		in.s0.fpdR = f;
+		f          = 1;
+		while (f < 16386)
+			f = (uint32_t)rnd.next () * 0xFFFFFFFFu;
+		in.s0.odFpd  = f;
+		in.s0.fpFlip = 1;
+		for (int l = 0; l < 13; l++)
+			in.s0.count[l] = 1;
+		reverbConsts (in.k, sr, 1.0f, 0.2f, 0.0f, 0.0f, 0.4f, 0.8f);
+		whirlConsts (in.k, e->wt);
+		/* initWhirl -> computeRotationSpeeds -> setRevSelect(0) -> useRevOption(4) */
+		in.s0.hornTarget = e->wt.revHorn[4];
+		in.s0.drumTarget = e->wt.revDrum[4];
+		in.s0.hornAcDc   = in.s0.hornIncr < in.s0.hornTarget ? 1 : (in.s0.hornTarget < in.s0.hornIncr ? -1 : 0);
+		in.s0.drumAcDc   = in.s0.drumIncr < in.s0.drumTarget ? 1 : (in.s0.drumTarget < in.s0.drumIncr ? -1 : 0);
+		/* tonegen + vibrato runtime state (initToneGenerator, reset_vibrato) */
+		in.s0.keyCompLevel = 1.0f;
+		in.s0.percEnvGain  = 0.0f;
+		in.s0.outPos       = 1023 / 2;
+		in.tg.init (e->tpls[in.tpl].get ());
+		if (e->slabLen == 0)
+			e->slabLen = in.k.slabLen;
+		else if (e->slabLen != in.k.slabLen)
+			return fail (-22, "inconsistent reverb geometry");
+	}
+	e->deviceReady = false;
+	return 0;
+}
+
+uint32_t tbf_instance_count (const tbf_engine* e) { return e ? (uint32_t)e->inst.size () : 0; }
+
+int tbf_note (tbf_engine* e, uint32_t i, int32_t key, int32_t on)
+{
+	if (!e || i >= e->inst.size ())
+		return fail (-22, "bad instance");
+	if (key < 0 || key >= 384)
+		return 0; /* oscKeyOn/Off ignore keys >= MAX_KEYS */
+	if (on)
+		e->inst[i].tg.keyOn (key);
+	else
+		e->inst[i].tg.keyOff (key);
+	return 0;
+}
+
+int tbf_set_param (tbf_engine* e, uint32_t i, int32_t index, double v)
+{
+	if (!e || i >= e->inst.size ())
+		return fail (-22, "bad instance");
+	Instance& in    = e->inst[i];
+	float     value = (float)v;
+	if (index >= 0 && index < 64)
+		in.params[index] = value;
+	/* src/clap.cpp:108-121 setToneGenParam + 162-207 setParam */
+	if (index >= TBF_P_DRAWBAR_MIN && index <= TBF_P_DRAWBAR_MAX)
+		in.tg.setDrawBar (index, (unsigned)rint (value));
+	else if (index == TBF_P_VIBRATO)
+		in.tg.setVibratoUpper ((int)rint (value));
+	else if (index == TBF_P_VIBRATO_TYPE)
+		in.tg.setVibratoFromInt ((int)floor (value));
+	else if (index == TBF_P_DRUM || index == TBF_P_HORN)
+		in.revOpt = (int)(floor (in.params[TBF_P_DRUM]) + 3 * floor (in.params[TBF_P_HORN]));
+	else if (index == TBF_P_OVERDRIVE)
+		in.odClean = (int)rint (1.0f - value);
+	else if (index == TBF_P_CHARACTER) {
+		/* fsetCharacter + linseg, src/overdrive.cpp:547-574 */
+		static const double Aval[5] = {0.0, 0.25, 0.50, 0.75, 1.00};
+		static const double Cval[5] = {1.0, 0.70, 0.25, 0.15, 0.13};
+		in.odA                      = value;
+		for (int q = 0; q < 4; q++)
+			if (value <= Aval[q + 1]) {
+				float a = (float)Aval[q], b = (float)Aval[q + 1], p = (float)Cval[q], qq = (float)Cval[q + 1];
+				in.odC  = p + (value - a) * (qq - p) / (b - a);
+				break;
+			}
+	} else if (index == TBF_P_REVERB)
+		in.rvG = value;
+	else if (index == TBF_P_PERCUSSION)
+		in.tg.setPercEnabled ((int)rint (value));
+	else if (index == TBF_P_PERCUSSION_VOLUME)
+		in.tg.setPercVolume ((int)(1 - rint (value)));
+	else if (index == TBF_P_PERCUSSION_DECAY)
+		in.tg.setPercFast ((int)rint (value));
+	else if (index == TBF_P_PERCUSSION_HARMONIC)
+		in.tg.setPercFirst ((int)rint (value));
+	else if (index >= TBF_P_BUS_DRAWBAR_BASE && index < TBF_P_BUS_DRAWBAR_BASE + 27)
+		in.tg.setDrawBar (index - TBF_P_BUS_DRAWBAR_BASE, (unsigned)rint (value));
+	else if (index == TBF_P_VIBRATO_LOWER)
+		in.tg.setVibratoLower ((int)rint (value));
+	else if (index == TBF_P_SWELL) {
+		unsigned char u      = (unsigned char)rint (value * 127.0);
+		in.tg.swellPedalGain = (float)((in.tg.outputLevelTrim * ((double)u)) / 127.0);
+	} else if (index == TBF_P_WHIRL_BYPASS)
+		in.whBypass = (int)rint (value);
+	else if (!(index >= 0 && index < 64))
+		return fail (-22, "unknown parameter id");
+	in.ctlDirty = true;
+	return 0;
+}
+
+} /* extern "C" */
+
+/* ------------------------------------------------------------------ device setup */
+static int ensureDevice (tbf_engine* e)
+{
+	if (e->deviceReady)
+		return 0;
+	if (e->cfg.device < 0)
+		return fail (-19, "host-only engine (device -1) cannot render");
+	HIPCHK (hipSetDevice (e->cfg.device));
+	HIPCHK (hipStreamSynchronize (e->stream));
+	const uint32_t n = (uint32_t)e->inst.size ();
+	/* wave banks + template descriptors */
+	size_t total = 0;
+	for (auto& t : e->tpls)
+		total += t->bank.size ();
+	if (e->bank.ensure (total) || e->tplDesc.ensure (e->tpls.size ()))
+		return fail (-12, "out of device memory (bank)");
+	std::vector<tbf_tpl_desc> desc (e->tpls.size ());
+	size_t                    o = 0;
+	for (size_t q = 0; q < e->tpls.size (); q++) {
+		const TgTemplate& t = *e->tpls[q];
+		HIPCHK (hipMemcpy (e->bank.p + o, t.bank.data (), t.bank.size () * sizeof (float), hipMemcpyHostToDevice));
+		for (int w = 0; w <= TBF_NW; w++) {
+			desc[q].off[w] = (uint32_t)(o + t.off[w]);
+			desc[q].len[w] = t.len[w];
+		}
+		memcpy (desc[q].attackEnv, t.attackEnv, sizeof (desc[q].attackEnv));
+		memcpy (desc[q].releaseEnv, t.releaseEnv, sizeof (desc[q].releaseEnv));
+		o += t.bank.size ();
+	}
+	HIPCHK (hipMemcpy (e->tplDesc.p, desc.data (), desc.size () * sizeof (tbf_tpl_desc), hipMemcpyHostToDevice));
+	/* shared tables */
+	if (e->vib.ensure (e->vibTab.size ()) || e->whTab.ensure (e->wt.displ.size ()) || e->whBw.ensure (e->wt.bw.size ()) ||
+	    e->err.ensure (4))
+		return fail (-12, "out of device memory (tables)");
+	HIPCHK (hipMemcpy (e->vib.p, e->vibTab.data (), e->vibTab.size () * 4, hipMemcpyHostToDevice));
+	HIPCHK (hipMemcpy (e->whTab.p, e->wt.displ.data (), e->wt.displ.size () * 4, hipMemcpyHostToDevice));
+	HIPCHK (hipMemcpy (e->whBw.p, e->wt.bw.data (), e->wt.bw.size () * 4, hipMemcpyHostToDevice));
+	HIPCHK (hipMemset (e->err.p, 0, 16));
+	/* per-instance buffers: new instances start from their initial state, existing
+	 * instances keep their device state */
+	const uint32_t old = e->devInst;
+	if (n > old) {
+		DevBuf<tbf_inst_state> nst;
+		DevBuf<float>          nwr;
+		DevBuf<double>         nsl;
+		if (nst.ensure (n) || nwr.ensure ((size_t)n * 4 * e->wringLen) || nsl.ensure ((size_t)n * e->slabLen))
+			return fail (-12, "out of device memory (instances)");
+		if (old) {
+			HIPCHK (hipMemcpy (nst.p, e->st.p, old * sizeof (tbf_inst_state), hipMemcpyDeviceToDevice));
+			HIPCHK (hipMemcpy (nwr.p, e->wring.p, (size_t)old * 4 * e->wringLen * 4, hipMemcpyDeviceToDevice));
+			HIPCHK (hipMemcpy (nsl.p, e->rslab.p, (size_t)old * e->slabLen * 8, hipMemcpyDeviceToDevice));
+		}
+		std::vector<tbf_inst_state> s0 (n - old);
+		for (uint32_t i = old; i < n; i++)
+			s0[i - old] = e->inst[i].s0;
+		HIPCHK (hipMemcpy (nst.p + old, s0.data (), (n - old) * sizeof (tbf_inst_state), hipMemcpyHostToDevice));
+		HIPCHK (hipMemset (nwr.p + (size_t)old * 4 * e->wringLen, 0, (size_t)(n - old) * 4 * e->wringLen * 4));
+		HIPCHK (hipMemset (nsl.p + (size_t)old * e->slabLen, 0, (size_t)(n - old) * e->slabLen * 8));
+		e->st.release ();
+		e->wring.release ();
+		e->rslab.release ();
+		e->st    = nst;
+		e->wring = nwr;
+		e->rslab = nsl;
+		std::vector<tbf_inst_const> k (n);
+		for (uint32_t i = 0; i < n; i++)
+			k[i] = e->inst[i].k;
+		if (e->cst.ensure (n) || e->ctl.ensure (n) || e->prog.ensure ((size_t)n * PROG_CAP))
+			return fail (-12, "out of device memory (control)");
+		HIPCHK (hipMemcpy (e->cst.p, k.data (), n * sizeof (tbf_inst_const), hipMemcpyHostToDevice));
+		e->hCtl.resize (n);
+		e->hProg.resize ((size_t)n * PROG_CAP);
+		e->devInst = n;
+	}
+	e->deviceReady = true;
+	return 0;
+}
+
+/* control for the next segment; returns true if some instance must be re-stepped at
+ * the following block (env -> steady transition) */
+static bool buildControl (tbf_engine* e, uint32_t& progLo, uint32_t& progHi, bool& ctlChanged)
+{
+	bool           again = false;
+	const uint32_t n     = (uint32_t)e->inst.size ();
+	progLo               = n;
+	progHi               = 0;
+	ctlChanged           = false;
+	for (uint32_t i = 0; i < n; i++) {
+		Instance&    in = e->inst[i];
+		tbf_seg_ctl& c  = e->hCtl[i];
+		const bool   tgDirty = in.tg.dirty ();
+		if (tgDirty) {
+			in.tg.step (in.prog, c);
+			in.progDirty = true;
+			in.ctlDirty  = true;
+			if (in.tg.dirty ())
+				again = true;
+		}
+		if (in.progDirty) {
+			if (in.prog.size () > PROG_CAP)
+				in.prog.resize (PROG_CAP);
+			std::copy (in.prog.begin (), in.prog.end (), e->hProg.begin () + (size_t)i * PROG_CAP);
+			progLo       = std::min (progLo, i);
+			progHi       = std::max (progHi, i + 1);
+			in.progDirty = false;
+		}
+		if (in.ctlDirty || in.revOpt >= 0) {
+			if (!tgDirty) {
+				/* mixdown fields that setters can change without a tonegen step */
+				c.swellPedalGain   = in.tg.swellPedalGain;
+				c.outputGain       = in.tg.swellPedalGain * in.tg.percDrawbarGain;
+				c.percEnvGainDecay = in.tg.percEnvGainDecay;
+				c.percEnvGainReset = in.tg.percEnvGainReset;
+				c.vibTable         = in.tg.vibTable;
+				c.vibMixed         = in.tg.vibMixed;
+			}
+			c.prog_off = i * PROG_CAP;
+			c.prog_len = (uint32_t)in.prog.size ();
+			odCtl (in, e->cfg.sample_rate, c);
+			c.rvWet       = in.rvG;
+			c.whBypass    = (uint32_t)in.whBypass;
+			c.whRevOption = in.revOpt;
+			in.revOpt     = -1;
+			in.ctlDirty   = (c.whRevOption >= 0); /* clear the one-shot next segment */
+			ctlChanged    = true;
+		}
+	}
+	return again;
+}
+
+static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, uint64_t stride, hipStream_t s)
+{
+	int rc = ensureDevice (e);
+	if (rc)
+		return rc;
+	const uint32_t n = (uint32_t)e->inst.size ();
+	if (n == 0 || nblocks == 0)
+		return 0;
+	if (stride < (uint64_t)nblocks * TBF_BLK)
+		return fail (-22, "stride smaller than nblocks*128");
+	tbf_launch P;
+	memset (&P, 0, sizeof (P));
+	P.bank      = e->bank.p;
+	P.tpls      = e->tplDesc.p;
+	P.cst       = e->cst.p;
+	P.st        = e->st.p;
+	P.wring     = e->wring.p;
+	P.rslab     = e->rslab.p;
+	P.ctl       = e->ctl.p;
+	P.prog      = e->prog.p;
+	P.vibTab    = e->vib.p;
+	P.whTab     = e->whTab.p;
+	P.whBw      = e->whBw.p;
+	P.outL      = dL;
+	P.outR      = dR;
+	P.outStride = stride;
+	P.nInst     = n;
+	P.wringLen  = e->wringLen;
+	P.statorInc = e->statorInc;
+	P.chain     = e->cfg.chain_mode;
+	P.slabLen   = e->slabLen;
+	P.errFlags  = e->err.p;
+	uint32_t b0 = 0;
+	while (b0 < nblocks) {
+		uint32_t lo, hi;
+		bool     ctlChanged;
+		bool     again = buildControl (e, lo, hi, ctlChanged);
+		if (ctlChanged)
+			HIPCHK (hipMemcpyAsync (e->ctl.p, e->hCtl.data (), n * sizeof (tbf_seg_ctl), hipMemcpyHostToDevice, s));
+		if (hi > lo)
+			HIPCHK (hipMemcpyAsync (e->prog.p + (size_t)lo * PROG_CAP, e->hProg.data () + (size_t)lo * PROG_CAP,
+			                        (size_t)(hi - lo) * PROG_CAP * sizeof (tbf_prog_entry), hipMemcpyHostToDevice, s));
+		const uint32_t len = again ? 1u : nblocks - b0;
+		P.nBlocks          = len;
+		P.outOffset        = (uint64_t)b0 * TBF_BLK;
+		rc                 = tbf_launch_render (&P, s);
+		if (rc)
+			return fail (rc, std::string ("kernel launch failed: ") + hipGetErrorString (hipGetLastError ()));
+		/* host staging buffers are rewritten by the next buildControl: keep order */
+		if (ctlChanged || hi > lo)
+			HIPCHK (hipStreamSynchronize (s));
+		b0 += len;
+	}
+	return 0;
+}
+
+extern "C" {
+
+int tbf_render_device (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, uint64_t stride, void* stream)
+{
+	if (!e || !dL || !dR)
+		return fail (-22, "null argument");
+	if (e->cfg.device < 0)
+		return fail (-19, "host-only engine (device -1) cannot render");
+	HIPCHK (hipSetDevice (e->cfg.device));
+	return renderImpl (e, nblocks, dL, dR, stride, stream ? (hipStream_t)stream : e->stream);
+}
+
+int tbf_render (tbf_engine* e, uint32_t nblocks, float* outL, float* outR, uint64_t stride)
+{
+	if (!e || !outL || !outR)
+		return fail (-22, "null argument");
+	if (e->cfg.device < 0)
+		return fail (-19, "host-only engine (device -1) cannot render");
+	HIPCHK (hipSetDevice (e->cfg.device));
+	const uint32_t n   = (uint32_t)e->inst.size ();
+	const size_t   per = (size_t)nblocks * TBF_BLK;
+	if (stride < per)
+		return fail (-22, "stride smaller than nblocks*128");
+	if (e->outL.ensure ((size_t)n * per) || e->outR.ensure ((size_t)n * per))
+		return fail (-12, "out of device memory (outputs)");
+	int rc = renderImpl (e, nblocks, e->outL.p, e->outR.p, per, e->stream);
+	if (rc)
+		return rc;
+	HIPCHK (hipMemcpy2DAsync (outL, stride * 4, e->outL.p, per * 4, per * 4, n, hipMemcpyDeviceToHost, e->stream));
+	HIPCHK (hipMemcpy2DAsync (outR, stride * 4, e->outR.p, per * 4, per * 4, n, hipMemcpyDeviceToHost, e->stream));
+	HIPCHK (hipStreamSynchronize (e->stream));
+	return 0;
+}
+
+int tbf_synth_sound (tbf_engine* e, uint32_t nframes, float* outL, float* outR, uint64_t stride)
+{
+	if (!e || !outL || !outR)
+		return fail (-22, "null argument");
+	const uint32_t n = (uint32_t)e->inst.size ();
+	e->fifoL.resize ((size_t)n * TBF_BLK);
+	e->fifoR.resize ((size_t)n * TBF_BLK);
+	uint32_t written = 0;
+	while (written < nframes) {
+		if (e->boffset >= TBF_BLK) {
+			e->boffset = 0;
+			int rc     = tbf_render (e, 1, e->fifoL.data (), e->fifoR.data (), TBF_BLK);
+			if (rc)
+				return rc;
+		}
+		const uint32_t nread = std::min (nframes - written, (uint32_t)TBF_BLK - e->boffset);
+		for (uint32_t i = 0; i < n; i++) {
+			memcpy (outL + (size_t)i * stride + written, e->fifoL.data () + (size_t)i * TBF_BLK + e->boffset, nread * 4);
+			memcpy (outR + (size_t)i * stride + written, e->fifoR.data () + (size_t)i * TBF_BLK + e->boffset, nread * 4);
+		}
+		written += nread;
+		e->boffset += nread;
+	}
+	return 0;
+}
+
+int tbf_synchronize (tbf_engine* e)
+{
+	if (!e)
+		return fail (-22, "null argument");
+	if (e->cfg.device < 0)
+		return 0;
+	HIPCHK (hipSetDevice (e->cfg.device));
+	HIPCHK (hipStreamSynchronize (e->stream));
+	return 0;
+}
+
+int tbf_error_flags (tbf_engine* e, uint32_t* flags)
+{
+	if (!e || !flags)
+		return fail (-22, "null argument");
+	*flags = 0;
+	if (!e->err.p)
+		return 0;
+	HIPCHK (hipMemcpy (flags, e->err.p, 4, hipMemcpyDeviceToHost));
+	return 0;
+}
+
+int tbf_debug_contrib (tbf_engine* e, uint32_t tid, int32_t key, int16_t* wheel, int16_t* bus, float* level,
+                       uint32_t cap)
+{
+	if (!e || tid >= e->tpls.size () || key < 0 || key >= 384)
+		return fail (-22, "bad argument");
+	const auto& v = e->tpls[tid]->keyContrib[key];
+	for (uint32_t i = 0; i < v.size () && i < cap; i++) {
+		wheel[i] = v[i].wheel;
+		bus[i]   = v[i].bus;
+		level[i] = v[i].level;
+	}
+	return (int)v.size ();
+}
+
+int tbf_debug_tables (tbf_engine* e, uint32_t tid, float* attack, float* release, float* keycomp)
+{
+	if (!e || tid >= e->tpls.size ())
+		return fail (-22, "bad argument");
+	const TgTemplate& t = *e->tpls[tid];
+	if (attack) memcpy (attack, t.attackEnv, sizeof (t.attackEnv));
+	if (release) memcpy (release, t.releaseEnv, sizeof (t.releaseEnv));
+	if (keycomp) memcpy (keycomp, t.keyCompTable, sizeof (t.keyCompTable));
+	return 0;
+}
+
+int tbf_debug_step (tbf_engine* e, uint32_t i, float* out, uint32_t cap)
+{
+	if (!e || i >= e->inst.size ())
+		return fail (-22, "bad instance");
+	Instance& in = e->inst[i];
+	tbf_seg_ctl c;
+	memset (&c, 0, sizeof (c));
+	in.tg.step (in.prog, c);
+	in.progDirty = in.ctlDirty = true;
+	for (uint32_t q = 0; q < in.prog.size () && q < cap; q++) {
+		const tbf_prog_entry& p = in.prog[q];
+		float*                o = out + 9 * q;
+		o[0] = p.wheel; o[1] = p.env; o[2] = p.row;
+		o[3] = p.sg; o[4] = p.pg; o[5] = p.vg; o[6] = p.nsg; o[7] = p.npg; o[8] = p.nvg;
+	}
+	return (int)in.prog.size ();
+}
+
+} /* extern "C" */

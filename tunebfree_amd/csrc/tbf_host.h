@@ -1,0 +1,119 @@
+/*
+ * tbf_host.h -- host-side table builders and the tonegen control plane.
+ *
+ * Everything here runs once per template / instance / event on the CPU, in the
+ * reference's FP64/FP32 arithmetic with glibc libm, so the tables the device consumes
+ * are bit-identical to what the reference's init code builds:
+ *   - TgTemplate: initToneGenerator's shared part (src/tonegen.cpp:2905-3066):
+ *     frequencies (src/tuning.cpp:142), play matrix (1122-1213), wave bank
+ *     (1470-1630), key-compression table (1939-1966), envelopes (2562-2728);
+ *   - WhirlTables: computeOffsets/initTables (src/whirl.cpp:534-624, 338-517);
+ *   - TgControl: the message-queue / active-list / routing part of
+ *     oscGenerateFragment (src/tonegen.cpp:3257-3594) which turns key and drawbar
+ *     events into per-block core programs for the device.
+ */
+#ifndef TBF_HOST_H
+#define TBF_HOST_H
+
+#include <stdint.h>
+
+#include <vector>
+
+#include "tbf_types.h"
+
+namespace tbf {
+
+/* glibc rand() (TYPE_3) -- srand(seed) stream of the reference hosts */
+struct GlibcRand {
+	int32_t s[31];
+	int     f = 3, r = 0;
+	explicit GlibcRand (unsigned int seed);
+	int32_t next ();
+};
+
+struct Contrib {
+	int16_t wheel, bus;
+	float   level;
+};
+
+struct TgTemplate {
+	double                            sr = 48000.0;
+	double                            frequency[300];
+	double                            targetRatio[9];
+	int                               envMin = 0, envMax = 0;
+	std::vector<Contrib>              keyContrib[384];
+	std::vector<float>                bank; /* wheels 1..256 concatenated */
+	uint32_t                          off[TBF_NW + 1] = {0};
+	uint32_t                          len[TBF_NW + 1] = {0};
+	float                             keyCompTable[128];
+	float                             attackEnv[9][TBF_BLK];
+	float                             releaseEnv[9][TBF_BLK];
+	void build (double sr, const double* mts128, const double* ratio9, unsigned int seed);
+};
+
+struct WhirlTables {
+	double             sr = 0;
+	std::vector<float> displ; /* hnFwd, hnBwd, drFwd, drBwd: 4 x 16384 */
+	std::vector<float> bw;    /* bfw, bbw: 2 x 16384 x 5 */
+	float              hornSpacing[6], drumSpacing[6];
+	int32_t            phase[6];
+	float              hafw[5], hbfw[5], drf[5];
+	double             revHorn[9], revDrum[9];
+	double             lAcc[4];
+	float              maxAhead; /* largest write-ahead in samples */
+	void build (double sr);
+};
+
+/* per-instance tonegen control state (runtime fields of struct b_tonegen) */
+struct TgControl {
+	struct Aot {
+		float busLevel[27];
+		int   keyCount[27];
+		int   refCount;
+		float sumUpper, sumLower, sumPedal, sumPercn, sumSwell, sumScanr;
+	};
+	const TgTemplate* tpl = nullptr;
+	Aot               aot[TBF_NW + 1];
+	int               activeOscList[TBF_NW + 1];
+	int               activeOscLEnd = 0;
+	int               aclPos[TBF_NW + 1];
+	uint16_t          rflags[TBF_NW + 1];
+	std::vector<uint16_t> msg;
+	int               keyDownCount = 0;
+	unsigned          upperKeyCount = 0;
+	unsigned          newRouting = 0, oldRouting = 0;
+	unsigned          percSendBus = 4, percSendBusA = 3, percSendBusB = 4;
+	float             swellPedalGain = 0.07f, outputLevelTrim = 0.07f;
+	unsigned          activeKeys[384];
+	float             drawBarGain[27];
+	float             drawBarLevel[27][9];
+	uint16_t          drawBarChange = 0;
+	int               percEnabled = 0, percTriggerBus = 8, percTrigRestore = 0, percIsSoft = 0, percIsFast = 0;
+	float             percEnvGainReset = 0, percEnvGainDecay = 0, percEnvScaling = 11.0f;
+	float             percEnvGainResetNorm = 1.0f, percEnvGainResetSoft = 0.5012f;
+	float             percEnvGainDecayFastNorm = 0.9995f, percEnvGainDecayFastSoft = 0.9995f;
+	float             percEnvGainDecaySlowNorm = 0.9999f, percEnvGainDecaySlowSoft = 0.9999f;
+	float             percDrawbarNormalGain = 0.60512f, percDrawbarSoftGain = 1.0f, percDrawbarGain = 1.0f;
+	/* vibrato knob (setVibrato, src/vibrato.cpp:97-129) */
+	uint32_t          vibTable = 2, vibMixed = 0;
+	bool              steadyPending = false; /* last block emitted env entries / removals */
+
+	void init (const TgTemplate* t);
+	void keyOn (int key);
+	void keyOff (int key);
+	void setDrawBar (int bus, unsigned setting);
+	void setVibratoUpper (int on);
+	void setVibratoLower (int on);
+	void setVibratoFromInt (int param);
+	void setPercEnabled (int on);
+	void setPercVolume (int isSoft);
+	void setPercFast (int isFast);
+	void setPercFirst (int isFirst);
+	bool dirty () const;
+	/* one block of control: returns the block's program and mixdown control */
+	void step (std::vector<tbf_prog_entry>& prog, tbf_seg_ctl& ctl);
+};
+
+} // namespace tbf
+
+#endif

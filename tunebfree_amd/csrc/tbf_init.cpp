@@ -1,0 +1,808 @@
+/*
+ * tbf_init.cpp -- host table builders and tonegen control plane (see tbf_host.h).
+ * Each function cites the reference code whose arithmetic it reproduces.
+ */
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <limits>
+
+#include "tbf_host.h"
+
+namespace tbf {
+
+/* glibc srandom_r/random_r TYPE_3 (degree 31, separation 3) */
+GlibcRand::GlibcRand (unsigned int seed)
+{
+	if (seed == 0)
+		seed = 1;
+	int32_t word = (int32_t)seed;
+	s[0]         = word;
+	for (int i = 1; i < 31; ++i) {
+		int64_t hi = word / 127773;
+		int64_t lo = word % 127773;
+		int64_t w  = 16807 * lo - 2836 * hi;
+		if (w < 0)
+			w += 2147483647;
+		word = (int32_t)w;
+		s[i] = word;
+	}
+	f = 3;
+	r = 0;
+	for (int i = 0; i < 310; ++i)
+		next ();
+}
+
+int32_t GlibcRand::next ()
+{
+	uint32_t val = (uint32_t)s[f] + (uint32_t)s[r];
+	s[f]         = (int32_t)val;
+	if (++f >= 31) {
+		f = 0;
+		++r;
+	} else if (++r >= 31) {
+		r = 0;
+	}
+	return (int32_t)(val >> 1);
+}
+
+static double dBToGain (double dB) { return pow (10.0, (dB / 20.0)); }
+
+/* src/tuning.cpp:48-147 */
+static void frequencies (double* f, const double* mts128)
+{
+	for (int i = 0; i < 128; i++)
+		f[i] = mts128 ? mts128[i] : 440. * pow (2., (i - 69.) / 12.);
+	int   scaleSize = -1;
+	float period    = -1.0f;
+	bool  found     = false;
+	for (float p = 2.0f; p < 10.0f && !found; p++)
+		for (int s = 1; s < 128 && !found; s++) {
+			bool mismatch = false;
+			for (int i = 0; i < 128 - s; i++)
+				if (fabs (f[i + s] / f[i] - p) > 1e-6) {
+					mismatch = true;
+					break;
+				}
+			if (!mismatch) {
+				scaleSize = s;
+				period    = p;
+				found     = true;
+			}
+		}
+	for (int s = 1; s < 128 && !found; s++) {
+		float p        = (float)(f[s] / f[0]);
+		bool  mismatch = false;
+		for (int i = 0; i < 128 - s; i++)
+			if (fabs (f[i + s] / f[i] - p) > 1e-6) {
+				mismatch = true;
+				break;
+			}
+		if (!mismatch) {
+			scaleSize = s;
+			period    = p;
+			found     = true;
+		}
+	}
+	for (int i = 128; i < 300; i++)
+		f[i] = scaleSize > 0 ? period * f[i - scaleSize] : f[127];
+}
+
+/* src/tonegen.cpp:502-692 */
+static double taper (int key, int bus)
+{
+	double tp = 0.0;
+	key       = key - 36;
+	switch (bus) {
+		case 0: tp = key < 12 ? -10.0 : key < 17 ? -7.0 : key < 24 ? -3.5 : key < 36 ? 0.0 : key < 48 ? 3.5 : 7.0; break;
+		case 1: tp = key < 15 ? -3.5 : key < 38 ? 0.0 : key < 50 ? 3.5 : 7.0; break;
+		case 2: tp = key < 17 ? -7.0 : key < 22 ? -3.5 : key < 37 ? 0.0 : key < 49 ? 3.5 : 7.0; break;
+		case 3: tp = key < 17 ? -3.5 : key < 39 ? 0.0 : -3.5; break;
+		case 4: tp = key < 14 ? 7.0 : key < 20 ? 3.5 : key < 40 ? 0.0 : key < 50 ? -3.5 : -7.0; break;
+		case 5: tp = key < 12 ? 7.0 : key < 15 ? 3.5 : key < 41 ? 0.0 : key < 54 ? -3.5 : -7.0; break;
+		case 6: tp = key < 14 ? 3.5 : key < 42 ? 0.0 : key < 50 ? -3.5 : -7.0; break;
+		case 7: tp = key < 43 ? 0.0 : key < 48 ? -3.5 : -7.0; break;
+		case 8: tp = key < 43 ? 0.0 : -7.0; break;
+	}
+	return dBToGain (tp);
+}
+
+/* src/tuning.cpp:153-174 (wheel pairs table is reference data) */
+static short pairedWheel (short n)
+{
+	static const short wp[92] = {0, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 59, 60, 61, 62, 63, 64, 65, 66, 67, 68, 69,
+	                             70, 71, 72, 73, 74, 75, 76, 77, 78, 79, 80, 81, 82, 83, 84, 0, 0, 0, 0, 0, 85, 86,
+	                             87, 88, 89, 90, 91, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18,
+	                             19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 42, 43, 44,
+	                             45, 46, 47, 48};
+	return (short)((n / 92) * 92 + wp[n % 92]);
+}
+
+static const short kTerminalStrip[] = {
+	85, 42, 30, 76, 66, 18, 6, 54, 90, 35, 83, 71, 23, 11, 59, 47, 40, 28, 76, 64, 16, 4, 52, 88, 33, 81, 69, 21, 9,
+	57, 45, 34, 26, 74, 62, 14, 2, 50, 86, 43, 31, 79, 67, 19, 7, 55, 91, 36, 84, 72, 24, 12, 60, 48, 41, 29, 77, 65,
+	17, 5, 53, 89, 34, 82, 70, 22, 10, 58, 46, 39, 27, 75, 63, 15, 3, 51, 87, 32, 80, 68, 20, 8, 56, 44, 37, 25, 73,
+	61, 13, 1, 49, 0};
+
+struct Le {
+	short sa, sb;
+	float fc;
+};
+
+/* src/tonegen.cpp:933-1213 applyDefaultConfiguration + compilePlayMatrix */
+static void playMatrix (TgTemplate& t)
+{
+	std::vector<Le> terminalMix[TBF_NW + 1], keyTaper[384], keyCrosstalk[384];
+	for (int i = 1; i <= TBF_NW; i++) {
+		terminalMix[i].push_back ({(short)i, 0, (float)(1.0 - 0.01)});
+		short pw = pairedWheel ((short)i);
+		if (0 < pw && pw <= TBF_NW)
+			terminalMix[i].push_back ({pw, 0, (float)0.01});
+	}
+	for (int i = 1; i <= TBF_NW; i++) {
+		for (int j = 0; kTerminalStrip[j] > 0; j++) {
+			if (kTerminalStrip[j] == (short)i) {
+				int east = j > 0 ? kTerminalStrip[j - 1] : 0;
+				int west = kTerminalStrip[j + 1];
+				if (east > 0)
+					terminalMix[i].push_back ({(short)east, 0, (float)0.01});
+				if (west > 0)
+					terminalMix[i].push_back ({(short)west, 0, (float)0.01});
+				break;
+			}
+		}
+	}
+	/* applyManualDefaults (707-802) */
+	double of[TBF_NW + 1];
+	for (int i = 1; i <= TBF_NW; i++)
+		of[i] = fmin (fmax (t.frequency[i - 1], 12.0), 2.5e10);
+	for (int man = 0; man < 2; man++) {
+		const int keyOffset = man * 128, busOffset = man * 9;
+		for (int k = 0; k < 128; k++) {
+			for (int b = 0; b < 9; b++) {
+				float smallest = std::numeric_limits<float>::infinity ();
+				int   best     = 0;
+				for (int tn = 1; tn <= TBF_NW; tn++) {
+					float ratio    = (float)(of[tn] / t.frequency[k]);
+					float centDiff = (float)(1200 * fabs (log2 (t.targetRatio[b] / ratio)));
+					if (centDiff < smallest) {
+						smallest = centDiff;
+						best     = tn;
+					}
+				}
+				if (best != 1 && best != TBF_NW)
+					keyTaper[k + keyOffset].push_back ({(short)best, (short)(b + busOffset), (float)taper (k, b)});
+			}
+		}
+	}
+	/* applyPedalDefaults (810-841) */
+	static const int PDoffset[9] = {-12, 7, 0, 12, 19, 24, 28, 31, 36};
+	for (int k = 0; k < 32; k++)
+		for (int b = 0; b < 9; b++) {
+			int tn = (k + 1) + PDoffset[b];
+			if (tn < 1 || TBF_NW < tn)
+				continue;
+			keyTaper[k + 256].push_back ({(short)tn, (short)(b + 18), (float)dBToGain (0.0)});
+		}
+	/* applyDefaultCrosstalk (849-879) */
+	for (int man = 0; man < 2; man++)
+		for (int k = 0; k < 128; k++) {
+			const int kn = k + man * 128;
+			for (int b = 0; b < 9; b++) {
+				const int busNumber = man * 9 + b;
+				for (const Le& e : keyTaper[kn]) {
+					if (e.sb == busNumber)
+						continue;
+					keyCrosstalk[kn].push_back ({e.sa, (short)busNumber, (float)((0.01 * e.fc) / abs (busNumber - e.sb))});
+				}
+			}
+		}
+	/* compilePlayMatrix + cpmInsert (1061-1213) */
+	static unsigned char cpmBus[TBF_NW + 1][27];
+	static float         cpmGain[TBF_NW][27];
+	short                wheelNumber[TBF_NW + 1];
+	short                rowLength[TBF_NW];
+	for (int k = 0; k < 384; k++) {
+		int  endRow = 0;
+		auto ins    = [&] (const Le& lep) {
+            const int           terminal = lep.sa;
+            const unsigned char bus      = (unsigned char)lep.sb;
+            for (const Le& tl : terminalMix[terminal]) {
+                float gain = tl.fc * lep.fc;
+                short wnr  = tl.sa;
+                if (gain == 0.0)
+                    continue;
+                int r, b;
+                wheelNumber[endRow] = wnr;
+                for (r = 0; wheelNumber[r] != wnr; r++)
+                    ;
+                if (r == endRow) {
+                    rowLength[r] = 0;
+                    endRow += 1;
+                }
+                int c        = rowLength[r];
+                cpmBus[r][c] = bus;
+                for (b = 0; cpmBus[r][b] != bus; b++)
+                    ;
+                if (b == c) {
+                    rowLength[r] += 1;
+                    cpmGain[r][b] = gain;
+                } else {
+                    cpmGain[r][b] += gain;
+                }
+            }
+		};
+		for (const Le& e : keyTaper[k])
+			ins (e);
+		for (const Le& e : keyCrosstalk[k])
+			ins (e);
+		std::vector<Contrib>& out = t.keyContrib[k];
+		for (int w = 0; w < endRow; w++)
+			for (int c = 0; c < rowLength[w]; c++) {
+				if (cpmGain[w][c] < 0.0000158)
+					continue;
+				Contrib rep {wheelNumber[w], (int16_t)cpmBus[w][c], cpmGain[w][c]};
+				size_t  at = 0;
+				for (; at < out.size (); at++) {
+					if (rep.wheel < out[at].wheel)
+						break;
+					if (rep.wheel == out[at].wheel && rep.bus < out[at].bus)
+						break;
+				}
+				out.insert (out.begin () + (long)at, rep);
+			}
+	}
+}
+
+/* src/tonegen.cpp:1335-1369 */
+static size_t fitWave (double Hz, double precision, int minSamples, int maxSamples, double rate)
+{
+	double minErr = 99999.9, minSpn = 0.0;
+	int    minWaves = (int)ceil ((Hz * (double)minSamples) / rate);
+	int    maxWaves = (int)floor ((Hz * (double)maxSamples) / rate);
+	for (int i = minWaves; i <= maxWaves; i++) {
+		double nws = (rate * i) / Hz;
+		double spn = rint (nws);
+		double err = fabs (nws - spn);
+		if (err < minErr) {
+			minErr = err;
+			minSpn = spn;
+		}
+		if (err < precision)
+			break;
+	}
+	return (size_t)minSpn;
+}
+
+void TgTemplate::build (double rate, const double* mts128, const double* ratio9, unsigned int seed)
+{
+	static const double defaultRatio[9] = {0.5, 1.5, 1, 2, 3, 4, 5, 6, 8};
+	GlibcRand           rnd (seed);
+	sr     = rate;
+	envMin = std::min ((int)floor (sr * 8.0 / 22050.0), TBF_BLK);
+	envMax = std::min ((int)ceil (sr * 40.0 / 22050.0), TBF_BLK);
+	frequencies (frequency, mts128);
+	for (int i = 0; i < 9; i++)
+		targetRatio[i] = ratio9 ? ratio9[i] : defaultRatio[i];
+	for (auto& v : keyContrib)
+		v.clear ();
+	playMatrix (*this);
+
+	/* initOscillators (1470-1630): spline EQ (p1y=1,r1y=0,p4y=1,r4y=0), fitWave,
+	 * writeSamples with one rand() LSB per sample, wheels 1..256 in order */
+	const double fullCircle = 2.0 * M_PI;
+	size_t       total      = 0;
+	double       att[TBF_NW + 1], wf[TBF_NW + 1];
+	size_t       wl[TBF_NW + 1];
+	for (int i = 1; i <= TBF_NW; i++) {
+		double k   = TBF_NW - 1;
+		double tt  = ((double)(i - 1)) / k;
+		double tSq = tt * tt;
+		double tCb = tSq * tt;
+		double r   = 1.0 * (2.0 * tCb - 3.0 * tSq + 1.0) + 1.0 * (-2.0 * tCb + 3.0 * tSq) + 0.0 * (tCb - 2.0 * tSq + tt) +
+		           0.0 * (tCb - tSq);
+		att[i] = (r < 0.0) ? 0.0 : (1.0 < r) ? 1.0 : r;
+		wf[i]  = fmin (fmax (frequency[i - 1], 12.0), 2.5e10);
+		wl[i]  = fitWave (wf[i], 0.001, 3 * TBF_BLK, (int)(ceil (sr / 48000.0) * 4096), sr);
+		total += wl[i];
+	}
+	bank.assign (total, 0.f);
+	size_t o = 0;
+	for (int i = 1; i <= TBF_NW; i++) {
+		off[i]        = (uint32_t)o;
+		len[i]        = (uint32_t)wl[i];
+		double apl[12], plHz[12], aplSum = 0.0;
+		for (int j = 0; j < 12; j++) {
+			apl[j] = j == 0 ? 1.0 : 0.0;
+			aplSum += fabs (apl[j]);
+			plHz[j] = wf[i] * ((double)(j + 1));
+			if ((sr * 0.5) <= plHz[j])
+				apl[j] = 0.0;
+		}
+		const double U = att[i] / aplSum;
+		float*       y = bank.data () + o;
+		for (size_t n = 0; n < wl[i]; n++) {
+			double s = 0.0;
+			for (int j = 0; j < 12; j++)
+				s += apl[j] * sin (remainder ((plHz[j] * fullCircle * (double)n) / sr, fullCircle));
+			float v = (rnd.next () < (2147483647 >> 1)) ? (float)(1.0 / 32767.0) : 0.0f;
+			y[n]    = (float)((double)v + (U * s));
+		}
+		o += wl[i];
+	}
+	/* initKeyCompTable (1939-1966) */
+	{
+		float u = -5.0f, v = -9.0f, m = (float)(1.0 / (128 - 12));
+		keyCompTable[0] = keyCompTable[1] = 1.0f;
+		static const double t2[9] = {-1.1598, -2.0291, -2.4987, -2.9952, -3.5218, -4.0823, -4.6815, -4.9975, -4.9998};
+		for (int i = 0; i < 9; i++)
+			keyCompTable[2 + i] = (float)dBToGain (t2[i]);
+		for (int i = 11; i < 128; i++) {
+			float a         = (float)(i - 11);
+			keyCompTable[i] = (float)dBToGain (u + ((v - u) * a * m));
+		}
+	}
+	/* initEnvelopes (2562-2728): attack ENV_CLICK level 0.5, release ENV_LINEAR */
+	for (int b = 0; b < 9; b++) {
+		int bound = envMax - envMin;
+		if (bound < 1)
+			bound = 1;
+		int burst = envMin + (rnd.next () % bound);
+		if (TBF_BLK <= burst)
+			burst = TBF_BLK - 1;
+		int start = (rnd.next () % (TBF_BLK - burst));
+		int i;
+		for (i = 0; i < start; i++)
+			attackEnv[b][i] = 0.0f;
+		for (; i < start + burst; i++) {
+			double d        = ((double)rnd.next ()) / (double)2147483647;
+			attackEnv[b][i] = (float)(1.0 - (0.50f * d));
+		}
+		for (; i < TBF_BLK; i++)
+			attackEnv[b][i] = 1.0f;
+		attackEnv[b][0] = (float)(attackEnv[b][0] / 2.0);
+		for (i = 1; i < TBF_BLK; i++)
+			attackEnv[b][i] = (float)((float)(attackEnv[b][i - 1] + attackEnv[b][i]) / 2.0);
+		for (i = 0; i < TBF_BLK; i++)
+			releaseEnv[b][i] = ((float)i) / (float)TBF_BLK;
+	}
+}
+
+/* ------------------------------------------------------------------ whirl tables */
+static void ipoldraw (std::vector<float>& bfw, double degrees, double level, int partial, double* ipx, double* ipy)
+{
+	double d = *ipx;
+	while (d < 0.0)
+		d += 360.0;
+	int fromIndex = (int)((d * (double)16384) / 360.0);
+	*ipx          = degrees;
+	double e      = *ipx;
+	while (e < d)
+		e += 360.0;
+	int    toIndex = (int)((e * (double)16384) / 360.0);
+	double range   = (double)(toIndex - fromIndex);
+	for (int i = fromIndex; i <= toIndex; i++) {
+		double x                              = (double)(i - fromIndex);
+		double w                              = (*ipy) + ((x / range) * (level - (*ipy)));
+		bfw[(size_t)(i & 16383) * 5 + partial] = (float)w;
+	}
+	*ipy = level;
+}
+
+/* src/whirl.cpp:366-490 angular impulse-response drawing (reference data) */
+static const double kIr[5][26][2] = {
+	{{-180.0, 1.052}, {-166.4, .881}, {-150.5, .881}, {-135.3, .881}, {-122.4, .792}, {-106.5, .792}, {-91.2, .836}, {-75.8, .881}, {-59.4, .851}, {-44.7, .941}, {-30.0, 1.298}, {-14.7, 2.119}, {0.0, 2.820}, {15.6, 2.313}, {30.0, 1.492}, {44.7, .926}, {60.0, .836}, {74.7, .866}, {90.6, .792}, {100.0, .777}, {105.0, .777}, {120.0, .836}, {135.3, .836}, {150.0, .881}, {164.5, .874}, {180.0, 1.052}},
+	{{-180.0, -0.07}, {-150.0, 0.10}, {-135.0, -0.10}, {-122.2, 0.16}, {-105.0, 0.15}, {-91.2, 0.37}, {-75.3, 0.32}, {-60.1, 0.39}, {-44.5, 0.70}, {-30.0, 0.53}, {-12.0, -0.40}, {0.0, -0.81}, {2.7, -0.77}, {15.0, -0.52}, {33.1, 0.38}, {43.7, 0.68}, {57.7, 0.49}, {74.1, 0.19}, {89.4, 0.33}, {105.0, 0.03}, {120.0, 0.12}, {134.0, -0.13}, {153.3, 0.08}, {180.0, -0.07}},
+	{{-180.0, 0.40}, {-165.0, 0.20}, {-150.0, 0.48}, {-135.0, 0.27}, {-121.2, 0.22}, {-89.2, 0.30}, {-69.2, 0.22}, {-58.0, 0.11}, {-40.2, -0.43}, {-29.0, -0.53}, {-15.6, -0.43}, {0.0, 0.00}, {14.3, -0.44}, {30.3, -0.60}, {60.3, 0.11}, {74.9, 0.32}, {91.5, 0.23}, {104.9, 0.32}, {121.7, 0.19}, {135.0, 0.27}, {150.0, 0.45}, {165.0, 0.20}, {180.0, 0.40}},
+	{{-180.0, -0.08}, {-165.2, -0.19}, {-150.0, 0.00}, {-133.9, -0.20}, {-120.0, -0.15}, {-106.0, 0.09}, {-89.3, -0.15}, {-76.3, 0.00}, {-60.3, 0.29}, {-44.6, -0.02}, {-15.6, -0.22}, {0.0, 0.24}, {14.5, 0.11}, {30.1, -0.10}, {44.6, 0.17}, {60.4, 0.22}, {75.9, 0.16}, {90.4, -0.05}, {104.9, 0.07}, {122.8, -0.07}, {136.2, -0.07}, {150.0, 0.08}, {165.0, -0.19}, {180.0, -0.08}},
+	{{-180.0, 0.13}, {-165.2, 0.00}, {-150.0, 0.17}, {-135.2, -0.20}, {-120.5, 0.00}, {-105.0, 0.00}, {-90.0, 0.04}, {-75.0, -0.09}, {-60.3, -0.14}, {-45.0, 0.16}, {-15.6, 0.00}, {0.0, 0.22}, {15.6, -0.21}, {30.1, -0.09}, {45.0, 0.10}, {60.3, -0.07}, {74.8, -0.15}, {90.4, -0.03}, {104.9, -0.14}, {120.5, 0.00}, {135.2, -0.26}, {150.0, 0.16}, {165.0, -0.02}, {180.0, 0.13}},
+};
+static const int kIrN[5] = {26, 24, 23, 24, 24};
+
+/* RBJ designer, src/eqcomp.cpp:98-203 (only the types the whirl uses by default are
+ * exercised, all nine are kept for configurability) */
+static void eqCompute (int type, double fqHz, double Q, double dbG, double* C, double SampleRateD)
+{
+	double A = pow (10.0, (dbG / 40.0)), omega = (2.0 * M_PI * fqHz) / SampleRateD;
+	double sin_ = sin (omega), cos_ = cos (omega), alpha = sin_ / (2.0 * Q), beta = sqrt (A) / Q;
+	switch (type) {
+		case 0: C[0] = (1.0 - cos_) / 2.0; C[1] = 1.0 - cos_; C[2] = (1.0 - cos_) / 2.0; C[3] = 1.0 + alpha; C[4] = -2.0 * cos_; C[5] = 1.0 - alpha; break;
+		case 1: C[0] = (1.0 + cos_) / 2.0; C[1] = -(1.0 + cos_); C[2] = (1.0 + cos_) / 2.0; C[3] = 1.0 + alpha; C[4] = -2.0 * cos_; C[5] = 1.0 - alpha; break;
+		case 2: C[0] = sin_ / 2.0; C[1] = 0.0; C[2] = -sin_ / 2.0; C[3] = 1.0 + alpha; C[4] = -2.0 * cos_; C[5] = 1.0 - alpha; break;
+		case 3: C[0] = alpha; C[1] = 0.0; C[2] = -alpha; C[3] = 1.0 + alpha; C[4] = -2.0 * cos_; C[5] = 1.0 - alpha; break;
+		case 4: C[0] = 1.0; C[1] = -2.0 * cos_; C[2] = 1.0; C[3] = 1.0 + alpha; C[4] = -2.0 * cos_; C[5] = 1.0 - alpha; break;
+		case 5: C[0] = 1.0 - alpha; C[1] = -2.0 * cos_; C[2] = 1.0 + alpha; C[3] = 1.0 + alpha; C[4] = -2.0 * cos_; C[5] = 1.0 - alpha; break;
+		case 6: C[0] = 1.0 + (alpha * A); C[1] = -2.0 * cos_; C[2] = 1.0 - (alpha * A); C[3] = 1.0 + (alpha / A); C[4] = -2.0 * cos_; C[5] = 1.0 - (alpha / A); break;
+		case 7:
+			C[0] = A * ((A + 1) - ((A - 1) * cos_) + (beta * sin_));
+			C[1] = (2.0 * A) * ((A - 1) - ((A + 1) * cos_));
+			C[2] = A * ((A + 1) - ((A - 1) * cos_) - (beta * sin_));
+			C[3] = (A + 1) + ((A - 1) * cos_) + (beta * sin_);
+			C[4] = -2.0 * ((A - 1) + ((A + 1) * cos_));
+			C[5] = (A + 1) + ((A - 1) * cos_) - (beta * sin_);
+			break;
+		case 8:
+			C[0] = A * ((A + 1) + ((A - 1) * cos_) + (beta * sin_));
+			C[1] = -(2.0 * A) * ((A - 1) + ((A + 1) * cos_));
+			C[2] = A * ((A + 1) + ((A - 1) * cos_) - (beta * sin_));
+			C[3] = (A + 1) - ((A - 1) * cos_) + (beta * sin_);
+			C[4] = 2.0 * ((A - 1) - ((A + 1) * cos_));
+			C[5] = (A + 1) - ((A - 1) * cos_) - (beta * sin_);
+			break;
+	}
+	C[0] /= C[3];
+	C[1] /= C[3];
+	C[2] /= C[3];
+	C[4] /= C[3];
+	C[5] /= C[3];
+}
+
+/* setIIRFilter (src/whirl.cpp:147-172) -> {a1, a2, b0, b1, b2} */
+static void iirCoef (float* W, int T, double F, double Q, double G, double SR)
+{
+	double C[6];
+	W[0] = W[1] = W[2] = W[3] = W[4] = 0.f;
+	if (Q <= 0.1 || Q >= 6.00 || F / SR <= 0.0002 || F / SR >= 0.4998 || G <= -48.0 || G >= 48.0 || T < 0 || T > 8)
+		return;
+	eqCompute (T, F, Q, G, C, SR);
+	W[0] = (float)C[4];
+	W[1] = (float)C[5];
+	W[2] = (float)C[0];
+	W[3] = (float)C[1];
+	W[4] = (float)C[2];
+}
+
+void WhirlTables::build (double rate)
+{
+	sr = rate;
+	displ.assign (4 * 16384, 0.f);
+	bw.assign (2 * 16384 * 5, 0.f);
+	/* initValues (src/whirl.cpp:43-134) geometry and filters */
+	const float  hornRadiusCm = 19.2f, drumRadiusCm = 22.0f, airSpeed = 340.0f, micDistCm = 42.0f;
+	const float  hornXOffsetCm = 0.0f, hornZOffsetCm = 0.0f;
+	const double hornR = (hornRadiusCm * sr / 100.0) / airSpeed;
+	const double drumR = (drumRadiusCm * sr / 100.0) / airSpeed;
+	const double micD  = (micDistCm * sr / 100.0) / airSpeed;
+	const double micX  = (hornXOffsetCm * sr / 100.0) / airSpeed;
+	const double micZ  = (hornZOffsetCm * sr / 100.0) / airSpeed;
+	float*       hnFwd = displ.data (), *hnBwd = hnFwd + 16384, *drFwd = hnBwd + 16384, *drBwd = drFwd + 16384;
+	float        maxhn = 0.f, maxdr = 0.f;
+	for (int i = 0; i < 16384; i++) {
+		double       v    = (2.0 * M_PI * (double)i) / (double)16384;
+		double       a    = micD - (hornR * cos (v));
+		double       b    = micZ + hornR * sin (v);
+		const double dist = sqrt ((a * a) + (b * b));
+		hnFwd[i]                  = (float)(dist + micX);
+		hnBwd[16384 - (i + 1)]    = (float)(dist - micX);
+		a                         = micD - (drumR * cos (v));
+		b                         = drumR * sin (v);
+		drFwd[i]                  = (float)sqrt ((a * a) + (b * b));
+		drBwd[16384 - (i + 1)]    = drFwd[i];
+		maxhn                     = std::max (maxhn, std::max (hnFwd[i], hnBwd[16384 - (i + 1)]));
+		maxdr                     = std::max (maxdr, drFwd[i]);
+	}
+	static const float hs[6] = {12.0f, 18.0f, 53.0f, 50.0f, 106.0f, 116.0f};
+	static const float ds[6] = {36.0f, 39.0f, 79.0f, 86.0f, 123.0f, 116.0f};
+	static const int   ph[6] = {0, 16384 >> 1, (16384 * 2) / 6, (16384 * 5) / 6, (16384 * 1) / 6, (16384 * 4) / 6};
+	maxAhead                 = 0.f;
+	for (int i = 0; i < 6; i++) {
+		hornSpacing[i] = (float)(hs[i] * sr / 22100.0 + hornR + 1.0);
+		drumSpacing[i] = (float)(ds[i] * sr / 22100.0 + drumR + 1.0);
+		phase[i]       = ph[i];
+		maxAhead       = std::max (maxAhead, std::max (hornSpacing[i] + maxhn, drumSpacing[i] + maxdr));
+	}
+	/* initTables (338-517) */
+	std::vector<float> bfw (16384 * 5, 0.f);
+	for (int p = 0; p < 5; p++) {
+		double ipx = kIr[p][0][0], ipy = kIr[p][0][1];
+		for (int i = 1; i < kIrN[p]; i++)
+			ipoldraw (bfw, kIr[p][i][0], kIr[p][i][1], p, &ipx, &ipy);
+	}
+	double sum = 0.0;
+	for (int i = 0; i < 16384; i++) {
+		double colsum = 0.0;
+		for (int j = 0; j < 5; j++)
+			colsum += fabs (bfw[(size_t)i * 5 + j]);
+		if (sum < colsum)
+			sum = colsum;
+	}
+	float* obfw = bw.data ();
+	float* obbw = obfw + 16384 * 5;
+	for (int i = 0; i < 16384; i++)
+		for (int j = 0; j < 5; j++) {
+			float v                                  = (float)(bfw[(size_t)i * 5 + j] * (1.0 / sum));
+			obfw[(size_t)i * 5 + j]                  = v;
+			obbw[(size_t)(16384 - i - 1) * 5 + j] = v;
+		}
+	/* initialize (626-662): drum hi-shelf, horn A low-pass, horn B low-shelf */
+	const float haF = 4500, haQ = 2.7456f, haG = -30.0f, hbF = 300.0f, hbQ = 1.0f, hbG = -30.0f;
+	iirCoef (drf, 8, 811.9695, 1.6016, -38.9291, sr);
+	iirCoef (hafw, 0, haF, haQ, haG, sr);
+	iirCoef (hbfw, 7, hbF, hbQ, hbG, sr);
+	/* computeRotationSpeeds (270-293) */
+	const float  hornRPMslow = (float)(60.0 * 0.672), hornRPMfast = (float)(60.0 * 7.056);
+	const float  drumRPMslow = (float)(60.0 * 0.600), drumRPMfast = (float)(60.0 * 5.955);
+	const double hfast = hornRPMfast / (sr * 60.0), hslow = hornRPMslow / (sr * 60.0);
+	const double dfast = drumRPMfast / (sr * 60.0), dslow = drumRPMslow / (sr * 60.0);
+	const double H[9]  = {0, 0, 0, hslow, hslow, hslow, hfast, hfast, hfast};
+	const double D[9]  = {0, dslow, dfast, 0, dslow, dfast, 0, dslow, dfast};
+	for (int i = 0; i < 9; i++) {
+		revHorn[i] = H[i];
+		revDrum[i] = D[i];
+	}
+	/* speed-ramp factors of whirlProc2 (1255-1257, 1306-1308), block = 128 */
+	const float hornAcc = 0.161f, hornDec = 0.321f, drumAcc = 4.127f, drumDec = 1.371f;
+	const float acc[4]  = {hornAcc, hornDec, drumAcc, drumDec};
+	for (int i = 0; i < 4; i++)
+		lAcc[i] = exp (-1.0 / (sr / (size_t)TBF_BLK * acc[i]));
+}
+
+/* ------------------------------------------------------------------ tonegen control */
+void TgControl::init (const TgTemplate* t)
+{
+	tpl = t;
+	memset (aot, 0, sizeof (aot));
+	for (int i = 0; i <= TBF_NW; i++) {
+		aclPos[i] = -1;
+		rflags[i] = 0;
+	}
+	memset (activeKeys, 0, sizeof (activeKeys));
+	memset (drawBarGain, 0, sizeof (drawBarGain));
+	for (int i = 0; i < 27; i++)
+		for (int s = 0; s < 9; s++) {
+			float u            = (float)s;
+			drawBarLevel[i][s] = (float)(u / 8.0);
+		}
+	/* initToneGenerator temporary drawbars (tonegen.cpp:3006-3015) via setMIDIDrawBar */
+	static const int midiBus[8] = {0, 1, 2, 9, 10, 11, 18, 20};
+	static const int midiVal[8] = {8, 8, 6, 8, 3, 8, 8, 6};
+	for (int i = 0; i < 8; i++)
+		setDrawBar (midiBus[i], (unsigned)rint ((127 - midiVal[i]) * 8.0 / 127.0));
+	setPercFirst (0);
+	setPercVolume (0);
+	setPercFast (1);
+	setPercEnabled (0);
+	/* LV2 initSynth: setDrawBars (inst, 0, {8,8,6,0,...}) (b_synth/lv2.cpp:167-180) */
+	static const unsigned preset[9] = {8, 8, 6, 0, 0, 0, 0, 0, 0};
+	for (int i = 0; i < 9; i++)
+		setDrawBar (i, preset[i]);
+}
+
+/* src/tonegen.cpp:3096-3166 */
+void TgControl::keyOff (int key)
+{
+	if (key < 0 || key >= 384 || !activeKeys[key])
+		return;
+	activeKeys[key] = 0;
+	if (key < 128)
+		upperKeyCount--;
+	keyDownCount--;
+	msg.push_back ((uint16_t)(key & 0x0fff));
+}
+
+void TgControl::keyOn (int key)
+{
+	if (key < 0 || key >= 384)
+		return;
+	if (activeKeys[key])
+		keyOff (key);
+	activeKeys[key] = 1;
+	if (key < 128)
+		upperKeyCount++;
+	keyDownCount++;
+	msg.push_back ((uint16_t)(0x1000 | (key & 0x0fff)));
+}
+
+/* src/tonegen.cpp:2738-2750 */
+void TgControl::setDrawBar (int bus, unsigned setting)
+{
+	if (bus < 0 || bus >= 27 || setting > 8)
+		return;
+	drawBarChange = 1;
+	if (bus == percTriggerBus) {
+		percTrigRestore = (int)setting;
+		if (percEnabled)
+			return;
+	}
+	drawBarGain[bus] = drawBarLevel[bus][setting];
+}
+
+void TgControl::setVibratoUpper (int on) { newRouting = on ? (newRouting | 0x02u) : (newRouting & ~0x02u); }
+void TgControl::setVibratoLower (int on) { newRouting = on ? (newRouting | 0x01u) : (newRouting & ~0x01u); }
+
+/* src/vibrato.cpp:97-129: param 0..5 = V1 C1 V2 C2 V3 C3 */
+void TgControl::setVibratoFromInt (int p)
+{
+	if (p < 0 || p > 5)
+		return;
+	vibTable = (uint32_t)(p / 2);
+	vibMixed = (uint32_t)(p & 1);
+}
+
+/* src/tonegen.cpp:1678-1765 */
+void TgControl::setPercEnabled (int on)
+{
+	if (on) {
+		newRouting |= 0x0C;
+		if (-1 < percTriggerBus) {
+			drawBarGain[percTriggerBus] = 0.0f;
+			drawBarChange               = 1;
+		}
+	} else {
+		newRouting &= ~0x0Cu;
+		if (-1 < percTriggerBus) {
+			drawBarGain[percTriggerBus] = drawBarLevel[percTriggerBus][percTrigRestore];
+			drawBarChange               = 1;
+		}
+	}
+	percEnabled = on;
+}
+
+static void percResets (TgControl& t)
+{
+	if (t.percIsFast)
+		t.percEnvGainDecay = t.percIsSoft ? t.percEnvGainDecayFastSoft : t.percEnvGainDecayFastNorm;
+	else
+		t.percEnvGainDecay = t.percIsSoft ? t.percEnvGainDecaySlowSoft : t.percEnvGainDecaySlowNorm;
+}
+
+void TgControl::setPercFast (int isFast)
+{
+	percIsFast = isFast;
+	percResets (*this);
+}
+
+void TgControl::setPercVolume (int isSoft)
+{
+	percIsSoft       = isSoft;
+	percEnvGainReset = percEnvScaling * (isSoft ? percEnvGainResetSoft : percEnvGainResetNorm);
+	percDrawbarGain  = isSoft ? percDrawbarSoftGain : percDrawbarNormalGain;
+	percResets (*this);
+}
+
+void TgControl::setPercFirst (int isFirst) { percSendBus = isFirst ? percSendBusA : percSendBusB; }
+
+bool TgControl::dirty () const
+{
+	return !msg.empty () || drawBarChange || oldRouting != newRouting || steadyPending;
+}
+
+/* src/tonegen.cpp:3250-3594: message queue, active list + program emission, removal.
+ * The wrap split of each instruction (3376-3402, 3524-3555) is applied on the device
+ * from the wheel position it tracks. */
+void TgControl::step (std::vector<tbf_prog_entry>& prog, tbf_seg_ctl& ctl)
+{
+	prog.clear ();
+	int      removed[TBF_NW + 1];
+	int      removedEnd = 0;
+	bool     anyEnv     = false;
+	for (uint16_t m : msg) {
+		const int kn = m & 0x0fff;
+		if ((m & 0xf000) == 0x1000) {
+			for (const Contrib& c : tpl->keyContrib[kn]) {
+				const int wn = c.wheel;
+				if (aot[wn].refCount == 0) {
+					rflags[wn] = 0x0006;
+					if (aclPos[wn] == -1) {
+						aclPos[wn]                       = activeOscLEnd;
+						activeOscList[activeOscLEnd++] = wn;
+					}
+				} else {
+					rflags[wn] |= 0x0004;
+				}
+				aot[wn].busLevel[c.bus] += c.level;
+				aot[wn].keyCount[c.bus] += 1;
+				aot[wn].refCount += 1;
+			}
+		} else {
+			for (const Contrib& c : tpl->keyContrib[kn]) {
+				const int wn = c.wheel;
+				aot[wn].busLevel[c.bus] -= c.level;
+				aot[wn].keyCount[c.bus] -= 1;
+				aot[wn].refCount -= 1;
+				if (aot[wn].refCount == 0)
+					rflags[wn] = 0x0005;
+				else
+					rflags[wn] |= 0x0004;
+			}
+		}
+	}
+	msg.clear ();
+	const bool recomputeRouting = (oldRouting != newRouting);
+	if (recomputeRouting)
+		oldRouting = newRouting;
+
+	for (int i = 0; i < activeOscLEnd; i++) {
+		const int      on  = activeOscList[i];
+		Aot&           a   = aot[on];
+		tbf_prog_entry e;
+		memset (&e, 0, sizeof (e));
+		e.wheel = (uint16_t)on;
+		if (rflags[on] & 0x0001) {
+			removed[removedEnd++] = on;
+			e.env                 = 2;
+			e.row                 = (uint8_t)(i & 7);
+			e.sg                  = a.sumSwell;
+			e.pg                  = a.sumPercn;
+			e.vg                  = a.sumScanr;
+			e.nsg = e.npg = e.nvg = 0.0f;
+			anyEnv                = true;
+		} else {
+			bool reroute = false;
+			if (rflags[on] & 0x0002) {
+				e.sg = e.pg = e.vg = 0.0f;
+			} else {
+				e.sg = a.sumSwell;
+				e.pg = a.sumPercn;
+				e.vg = a.sumScanr;
+			}
+			if ((rflags[on] & 0x0004) || drawBarChange) {
+				float sum = 0.0f;
+				for (int d = 0; d < 9; d++)
+					sum += a.busLevel[d] * drawBarGain[d];
+				a.sumUpper = sum;
+				sum        = 0.0f;
+				for (int d = 9; d < 18; d++)
+					sum += a.busLevel[d] * drawBarGain[d];
+				a.sumLower = sum;
+				sum        = 0.0f;
+				for (int d = 18; d < 27; d++)
+					sum += a.busLevel[d] * drawBarGain[d];
+				a.sumPedal = sum;
+				reroute    = true;
+			}
+			if (reroute || recomputeRouting) {
+				a.sumPercn = (oldRouting & 0x0C) ? a.busLevel[percSendBus] : 0.0f;
+				a.sumScanr = 0.0f;
+				a.sumSwell = a.sumPedal;
+				if (oldRouting & 0x02)
+					a.sumScanr += a.sumUpper;
+				else
+					a.sumSwell += a.sumUpper;
+				if (oldRouting & 0x01)
+					a.sumScanr += a.sumLower;
+				else
+					a.sumSwell += a.sumLower;
+			}
+			if (rflags[on] & 0x0006) {
+				e.env  = 1;
+				e.row  = (uint8_t)(i & 7);
+				e.nsg  = a.sumSwell;
+				e.npg  = a.sumPercn;
+				e.nvg  = a.sumScanr;
+				anyEnv = true;
+			}
+		}
+		rflags[on] = 0;
+		prog.push_back (e);
+	}
+	drawBarChange = 0;
+	for (int i = 0; i < removedEnd; i++) {
+		const int vic = removed[i];
+		const int act = aclPos[vic];
+		aclPos[vic]   = -1;
+		activeOscLEnd--;
+		if (0 < activeOscLEnd) {
+			const int mov = activeOscList[activeOscLEnd];
+			if (mov != vic) {
+				activeOscList[act] = mov;
+				aclPos[mov]        = act;
+			}
+		}
+	}
+	steadyPending = anyEnv || removedEnd > 0;
+
+	/* mixdown control (3712-3777) */
+	ctl.routing          = oldRouting;
+	ctl.swellPedalGain   = swellPedalGain;
+	ctl.outputGain       = swellPedalGain * percDrawbarGain;
+	ctl.percEnvGainDecay = percEnvGainDecay;
+	ctl.percEnvGainReset = percEnvGainReset;
+	ctl.keyCompTarget    = tpl->keyCompTable[keyDownCount < 0 ? 0 : (keyDownCount > 127 ? 127 : keyDownCount)];
+	ctl.resetPercAtEnd   = upperKeyCount == 0;
+	ctl.vibTable         = vibTable;
+	ctl.vibMixed         = vibMixed;
+}
+
+} // namespace tbf

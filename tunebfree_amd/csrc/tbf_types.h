@@ -1,0 +1,143 @@
+/*
+ * tbf_types.h -- POD layouts shared by the host control plane (tbf_engine.cpp) and
+ * the gfx950 render kernel (tbf_render.hip).
+ *
+ * Naming follows the reference's domain: wheels, buses, programs (the tonegen "core
+ * program", src/tonegen.cpp:3333-3566), delay lines, rings, rotors.
+ */
+#ifndef TBF_TYPES_H
+#define TBF_TYPES_H
+
+#include <stdint.h>
+
+#define TBF_BLK 128   /* BUFFER_SIZE_SAMPLES, src/tonegen.h:53 */
+#define TBF_SUB 64    /* sub-block for reverb/whirl: one sample per lane of a wave64 */
+#define TBF_NW 256    /* NOF_WHEELS, src/tonegen.h:79 */
+#define TBF_VRING 256 /* compact vibrato ring (reference 1024; live window <= 21+128) */
+
+/* one core-program entry = one wheel's contribution for one block
+ * (CoreIns, src/tonegen.h:114-129; wrap splitting is done on the device) */
+typedef struct tbf_prog_entry {
+	uint16_t wheel;
+	uint8_t  env; /* 0 plain (CR_CPY/ADD), 1 attack env, 2 release env */
+	uint8_t  row; /* envelope row i & 7 */
+	float    sg, pg, vg;    /* sgain, pgain, vgain */
+	float    nsg, npg, nvg; /* next gains (env entries) */
+	uint32_t pad;
+} tbf_prog_entry;
+
+/* per instance, per launch segment: control state that is constant over the
+ * segment's blocks (events land on segment boundaries) */
+typedef struct tbf_seg_ctl {
+	uint32_t prog_off, prog_len;
+	uint32_t routing;        /* oldRouting after this block's update */
+	float    outputGain;     /* swellPedalGain * percDrawbarGain */
+	float    swellPedalGain;
+	float    percEnvGainDecay;
+	float    percEnvGainReset;
+	float    keyCompTarget;  /* keyCompTable[keyDownCount] */
+	uint32_t resetPercAtEnd; /* upperKeyCount == 0 */
+	uint32_t vibTable;       /* 0..2 -> offset1/2/3Table */
+	uint32_t vibMixed;       /* chorus */
+	uint32_t odClean;
+	int32_t  odIter;         /* sin iterations of the density loop */
+	uint32_t odDensityPos;   /* density > 0 */
+	uint32_t whBypass;
+	int32_t  whRevOption;    /* >= 0: useRevOption(n) before the first block */
+	double   odOut, odOutput, odWet, odDry, odIir;
+	double   rvWet;
+} tbf_seg_ctl;
+
+/* per instance, constant over its lifetime */
+typedef struct tbf_inst_const {
+	uint32_t tpl;
+	uint32_t vibRingPad;
+	/* reverb (src/reverb.cpp:283-336 per-block constants; A..F never change) */
+	double   bq[3][5]; /* biquadA/B/C [2..6] */
+	double   vibDelta[8];
+	double   vibDepth, blend, crossmod, oneMinusAbsCm, regen;
+	int32_t  delay[13];
+	uint32_t ringOff[26]; /* [c*13 + line] offset (doubles) inside the instance slab */
+	uint32_t slabLen;
+	uint32_t vibClosedForm; /* 1: phase increments have no rounding ties (host-checked) */
+	/* whirl (src/whirl.cpp init) */
+	float    hafw[5], hbfw[5], drf[5]; /* a1, a2, b0, b1, b2 */
+	float    hornSpacing[6], drumSpacing[6];
+	int32_t  hornPhase[6];
+	float    leakage, hornLevel;
+	float    mic[8]; /* hll hlr dll dlr hrl hrr drl drr */
+	double   fwAng, bwAng;
+	double   lAcc[4]; /* exp() speed-ramp factors: horn acc, horn dec, drum acc, drum dec */
+	double   deadzone;
+	double   revHorn[9], revDrum[9];
+	double   hnBrakePos, drBrakePos;
+	float    hnHardstop, drHardstop, minspeed, hnLimit, drLimit;
+	float    pad0;
+	double   sr;
+} tbf_inst_const;
+
+/* per instance device-resident DSP state */
+typedef struct tbf_inst_state {
+	/* tonegen */
+	uint32_t pos[TBF_NW + 1];
+	float    keyCompLevel, percEnvGain, pz;
+	/* vibrato */
+	uint32_t stator, outPos;
+	float    vring[TBF_VRING];
+	/* overdrive */
+	double   iirA, iirB;
+	uint32_t fpFlip, odFpd;
+	/* reverb */
+	int32_t  count[13];
+	uint32_t fpdL, fpdR;
+	double   bq[3][4]; /* [A/B/C][L7, L8, R9, R10] */
+	double   fb[2][8];
+	double   vib[2][8];
+	/* whirl */
+	double   hornAngle, drumAngle, hornIncr, drumIncr, hornTarget, drumTarget;
+	int32_t  hornAcDc, drumAcDc;
+	uint32_t outpos;
+	float    z[4];
+	float    fz[4][2]; /* hafw, hbfw, drfL, drfR: z0, z1 */
+	float    adx[3][8];
+	int32_t  adi[3];
+	int32_t  pad1;
+} tbf_inst_state;
+
+/* per template (tuning x sample rate): offsets into the shared wave bank */
+typedef struct tbf_tpl_desc {
+	uint32_t off[TBF_NW + 1];
+	uint32_t len[TBF_NW + 1];
+	float    attackEnv[8][TBF_BLK];  /* rows 0..7 used (i & 7) */
+	float    releaseEnv[8][TBF_BLK];
+} tbf_tpl_desc;
+
+/* kernel launch parameters */
+typedef struct tbf_launch {
+	const float*          bank;
+	const tbf_tpl_desc*   tpls;
+	const tbf_inst_const* cst;
+	tbf_inst_state*       st;
+	float*                wring; /* [inst][4][wring_len] */
+	double*               rslab; /* [inst][slabLen] */
+	const tbf_seg_ctl*    ctl;
+	const tbf_prog_entry* prog;
+	const uint32_t*       vibTab; /* [3][2048] */
+	const float*          whTab;  /* hnFwd, hnBwd, drFwd, drBwd [4][16384] */
+	const float*          whBw;   /* bfw, bbw [2][16384][5] */
+	float*                outL;
+	float*                outR;
+	uint64_t              outStride; /* floats between instances */
+	uint64_t              outOffset; /* first sample index of this segment */
+	uint32_t              nInst;
+	uint32_t              nBlocks;
+	uint32_t              wringLen;
+	uint32_t              statorInc;
+	uint32_t              chain;     /* 0 full, 1 tonegen only */
+	uint32_t              instBase;
+	uint32_t              slabLen;
+	uint32_t              pad;
+	uint32_t*             errFlags;
+} tbf_launch;
+
+#endif

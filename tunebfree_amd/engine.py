@@ -1,0 +1,152 @@
+"""ctypes mirror of include/tbf.h (the drop-in C-ABI)."""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+
+LIB_PATH = Path(__file__).resolve().parent / "libtbf.so"
+
+_fp = C.POINTER(C.c_float)
+_dp = C.POINTER(C.c_double)
+_u32p = C.POINTER(C.c_uint32)
+
+
+class TbfError(RuntimeError):
+    pass
+
+
+class _Config(C.Structure):
+    _fields_ = [("sample_rate", C.c_double), ("device", C.c_int32), ("chain_mode", C.c_uint32),
+                ("reserved", C.c_uint32 * 4)]
+
+
+# every symbol include/tbf.h declares, with its ctypes signature
+SIGNATURES = {
+    "tbf_abi_version": (C.c_int, []),
+    "tbf_last_error": (C.c_char_p, []),
+    "tbf_engine_create": (C.c_int, [C.POINTER(_Config), C.POINTER(C.c_void_p)]),
+    "tbf_engine_destroy": (C.c_int, [C.c_void_p]),
+    "tbf_template_create": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, _u32p]),
+    "tbf_instances_add": (C.c_int, [C.c_void_p, C.c_uint32, _u32p, _u32p, _u32p]),
+    "tbf_instance_count": (C.c_uint32, [C.c_void_p]),
+    "tbf_note": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int32, C.c_int32]),
+    "tbf_set_param": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int32, C.c_double]),
+    "tbf_render": (C.c_int, [C.c_void_p, C.c_uint32, _fp, _fp, C.c_uint64]),
+    "tbf_render_device": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
+    "tbf_synth_sound": (C.c_int, [C.c_void_p, C.c_uint32, _fp, _fp, C.c_uint64]),
+    "tbf_synchronize": (C.c_int, [C.c_void_p]),
+    "tbf_error_flags": (C.c_int, [C.c_void_p, _u32p]),
+    "tbf_template_bank": (C.c_int, [C.c_void_p, C.c_uint32, _fp, C.c_uint64, _u32p]),
+}
+
+_lib = None
+
+
+def load_library():
+    """Load the in-tree libtbf.so; fails loudly when it has not been built."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise TbfError(f"{LIB_PATH} not built -- run __graft_entry__.build() or `make -C tunebfree_amd`")
+        lib = C.CDLL(str(LIB_PATH))
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype, fn.argtypes = res, args
+        _lib = lib
+    return _lib
+
+
+def _check(rc):
+    if rc < 0:
+        raise TbfError(f"tbf error {rc}: {load_library().tbf_last_error().decode(errors='replace')}")
+    return rc
+
+
+class Engine:
+    """A batch of organ instances on one GPU (one engine per device / rank)."""
+
+    def __init__(self, sample_rate=48000.0, device=0, chain=0):
+        lib = load_library()
+        cfg = _Config(float(sample_rate), int(device), int(chain))
+        h = C.c_void_p()
+        _check(lib.tbf_engine_create(C.byref(cfg), C.byref(h)))
+        self._lib, self._h = lib, h
+        self.sample_rate, self.device = sample_rate, device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.tbf_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def template(self, mts128=None, ratio9=None, seed=1):
+        m = None if mts128 is None else np.ascontiguousarray(mts128, dtype=np.float64)
+        r = None if ratio9 is None else np.ascontiguousarray(ratio9, dtype=np.float64)
+        out = C.c_uint32()
+        _check(self._lib.tbf_template_create(self._h, None if m is None else m.ctypes.data,
+                                             None if r is None else r.ctypes.data, int(seed), C.byref(out)))
+        return out.value
+
+    def template_bank(self, tpl):
+        lens = np.zeros(256, np.uint32)
+        n = _check(self._lib.tbf_template_bank(self._h, int(tpl), None, 0, lens.ctypes.data_as(_u32p)))
+        out = np.zeros(n, np.float32)
+        _check(self._lib.tbf_template_bank(self._h, int(tpl), out.ctypes.data_as(_fp), n, None))
+        return out, lens
+
+    def add_instances(self, tpl_ids, seeds):
+        t = np.ascontiguousarray(tpl_ids, dtype=np.uint32)
+        s = np.ascontiguousarray(seeds, dtype=np.uint32)
+        assert t.shape == s.shape
+        first = C.c_uint32()
+        _check(self._lib.tbf_instances_add(self._h, len(t), t.ctypes.data_as(_u32p), s.ctypes.data_as(_u32p),
+                                           C.byref(first)))
+        return first.value
+
+    @property
+    def n_instances(self):
+        return self._lib.tbf_instance_count(self._h)
+
+    def note(self, inst, key, on):
+        _check(self._lib.tbf_note(self._h, int(inst), int(key), int(on)))
+
+    def set_param(self, inst, pid, value):
+        _check(self._lib.tbf_set_param(self._h, int(inst), int(pid), float(value)))
+
+    def render(self, nblocks):
+        """Synchronous render into host arrays, shape [n_instances, nblocks*128]."""
+        n = self.n_instances
+        L = np.zeros((n, nblocks * 128), np.float32)
+        R = np.zeros((n, nblocks * 128), np.float32)
+        _check(self._lib.tbf_render(self._h, int(nblocks), L.ctypes.data_as(_fp), R.ctypes.data_as(_fp),
+                                    nblocks * 128))
+        return L, R
+
+    def render_device(self, nblocks, outL_ptr, outR_ptr, stride, stream=None):
+        """Enqueue a render into device memory (e.g. torch tensor data_ptr())."""
+        _check(self._lib.tbf_render_device(self._h, int(nblocks), C.c_void_p(int(outL_ptr)),
+                                           C.c_void_p(int(outR_ptr)), int(stride),
+                                           None if stream is None else C.c_void_p(int(stream))))
+
+    def synth_sound(self, nframes):
+        n = self.n_instances
+        L = np.zeros((n, nframes), np.float32)
+        R = np.zeros((n, nframes), np.float32)
+        _check(self._lib.tbf_synth_sound(self._h, int(nframes), L.ctypes.data_as(_fp), R.ctypes.data_as(_fp),
+                                         nframes))
+        return L, R
+
+    def synchronize(self):
+        _check(self._lib.tbf_synchronize(self._h))
+
+    def error_flags(self):
+        f = C.c_uint32()
+        _check(self._lib.tbf_error_flags(self._h, C.byref(f)))
+        return f.value

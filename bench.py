@@ -38,8 +38,9 @@ def parse():
     ap.add_argument("--sr", type=float, default=48000.0)
     ap.add_argument("--check", type=int, default=4, help="instances checked against the CPU oracle")
     ap.add_argument("--cpu-baseline", type=int, default=1)
-    ap.add_argument("--cpu-instances", type=int, default=64)
-    ap.add_argument("--cpu-blocks", type=int, default=375)
+    ap.add_argument("--cpu-instances", type=int, default=128)
+    ap.add_argument("--cpu-blocks", type=int, default=1500)
+    ap.add_argument("--chain", type=int, default=0, help="0 full chain; 1/2/3 stage taps (profiling only)")
     return ap.parse_args()
 
 
@@ -133,14 +134,15 @@ def main():
 
     B = a.batch
     first_global = rank * B
-    eng = T.Engine(sample_rate=a.sr, device=torch.cuda.current_device())
+    eng = T.Engine(sample_rate=a.sr, device=torch.cuda.current_device(), chain=a.chain)
     tid = eng.template(seed=7)
     eng.add_instances([tid] * B, [1000 + first_global + i for i in range(B)])
     setup_events(eng, first_global, B)
     nsamp = a.blocks * 128
     outL = torch.empty((B, nsamp), dtype=torch.float32, device="cuda")
     outR = torch.empty((B, nsamp), dtype=torch.float32, device="cuda")
-    stream = torch.cuda.current_stream()
+    stream = torch.cuda.Stream()  # a real stream: the kernel and the timing events share it
+    torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
 
     def step():

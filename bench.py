@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--check", type=int, default=4, help="instances checked against the CPU oracle")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-instances", type=int, default=128)
-    ap.add_argument("--cpu-blocks", type=int, default=1500)
+    ap.add_argument("--cpu-blocks", type=int, default=12000)
     ap.add_argument("--chain", type=int, default=0, help="0 full chain; 1/2/3 stage taps (profiling only)")
     return ap.parse_args()
 

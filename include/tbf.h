@@ -121,6 +121,13 @@ int tbf_debug_tables (tbf_engine* e, uint32_t tpl_id, float* attack, float* rele
 /* run one block of the tonegen control plane for an instance and return the core
  * program: per entry {wheel, env, row, sg, pg, vg, nsg, npg, nvg} as 9 floats */
 int tbf_debug_step (tbf_engine* e, uint32_t inst, float* entries9, uint32_t cap);
+/* the kernel's exact shortcuts of serial recurrences, evaluated on the host (same source,
+ * csrc/tbf_exact.h): op 0 phase_run (in: v0, d, m -> out: ok, D), op 1 cnt_adv (in: c0,
+ * d, n -> out: count), op 2 wrap1 (in: x, -, - -> out: fmod (x, 1)); n records */
+int tbf_debug_exact (int32_t op, const double* in3, double* out2, uint32_t n);
+/* stage timing: enable 1 zeroes per-instance counters and turns the kernel's marks on;
+ * 0 copies out [inst][32] cycle sums (returns the count); -1 turns the marks off */
+int tbf_debug_profile (tbf_engine* e, int32_t enable, uint64_t* out, uint32_t cap);
 
 #ifdef __cplusplus
 }

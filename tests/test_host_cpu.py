@@ -1,0 +1,319 @@
+"""CPU tests of the product's host side (no GPU needed):
+
+  - the C-ABI library loads and exports every symbol include/tbf.h declares;
+  - a host-only engine (device = -1) builds the same tonegen template as the oracle
+    (wave bank, envelopes, key-compression table, play matrix), bit for bit;
+  - its control plane emits, block by block, the same core programs as the oracle's
+    oscGenerateFragment restatement (src/tonegen.cpp:3218-3566) under an event script;
+  - the render entry points refuse to run without a device (no CPU fallback);
+  - the instance sharding used by bench.py --gpus N covers every instance exactly once
+    (world_size-2 gloo run, one engine per rank).
+"""
+import ctypes as C
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import scenarios as S
+from orc_bind import Template
+
+ROOT = Path(__file__).resolve().parents[1]
+T = pytest.importorskip("tunebfree_amd")
+
+
+def _header_symbols():
+    src = (ROOT / "include" / "tbf.h").read_text()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(tbf_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_abi_exports_every_declared_symbol():
+    lib = T.load_library()
+    names = _header_symbols()
+    assert len(names) >= 18
+    for n in names:
+        assert hasattr(lib, n), n
+    # every non-test entry point has a ctypes signature in the host mirror
+    assert {n for n in names if not n.startswith("tbf_debug_")} == set(T.engine.SIGNATURES)
+    assert lib.tbf_abi_version() == 1
+
+
+def _bind_debug(lib):
+    lib.tbf_debug_contrib.restype = C.c_int
+    lib.tbf_debug_contrib.argtypes = [C.c_void_p, C.c_uint32, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.c_uint32]
+    lib.tbf_debug_tables.restype = C.c_int
+    lib.tbf_debug_tables.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.tbf_debug_step.restype = C.c_int
+    lib.tbf_debug_step.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]
+
+
+def _orc_bind_debug(lib):
+    lib.orc_template_contrib.restype = C.c_int
+    lib.orc_template_contrib.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+    lib.orc_debug_program.restype = C.c_int
+    lib.orc_debug_program.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+
+
+@pytest.mark.parametrize("sr,seed,tuning", [(48000.0, 7, None), (44100.0, 3, "19TET"), (96000.0, 11, "p4")])
+def test_host_template_matches_oracle(oracle, sr, seed, tuning):
+    import json
+    mts = None
+    if tuning:
+        mts = np.array(json.loads((ROOT / "tests" / "golden" / "tunings.json").read_text())[tuning], np.float64)
+    ot = Template(oracle, sr=sr, mts128=mts, seed=seed)
+    eng = T.Engine(sample_rate=sr, device=-1)
+    tid = eng.template(mts128=mts, seed=seed)
+    ob, ol = ot.bank()
+    pb, pl = eng.template_bank(tid)
+    assert np.array_equal(ol, pl)
+    assert np.array_equal(ob.view(np.uint32), pb.view(np.uint32))
+    lib = T.load_library()
+    _bind_debug(lib)
+    _orc_bind_debug(oracle)
+    a, r, k = (np.zeros((9, 128), np.float32), np.zeros((9, 128), np.float32), np.zeros(128, np.float32))
+    assert lib.tbf_debug_tables(eng._h, tid, a.ctypes.data, r.ctypes.data, k.ctypes.data) >= 0
+    oa, orr, ok = ot.envs()
+    for x, y in ((a, oa), (r, orr), (k, ok)):
+        assert np.array_equal(x.view(np.uint32), y.view(np.uint32))
+    cap = 4096
+    for key in list(range(0, 61)) + list(range(64, 125)) + list(range(128, 160)):
+        w1, b1, l1 = np.zeros(cap, np.int16), np.zeros(cap, np.int16), np.zeros(cap, np.float32)
+        w2, b2, l2 = np.zeros(cap, np.int16), np.zeros(cap, np.int16), np.zeros(cap, np.float32)
+        n1 = lib.tbf_debug_contrib(eng._h, tid, key, w1.ctypes.data, b1.ctypes.data, l1.ctypes.data, cap)
+        n2 = oracle.orc_template_contrib(ot.ptr, key, w2.ctypes.data, b2.ctypes.data, l2.ctypes.data, cap)
+        assert n1 == n2, key
+        assert np.array_equal(w1[:n1], w2[:n1]) and np.array_equal(b1[:n1], b2[:n1]), key
+        assert np.array_equal(l1[:n1].view(np.uint32), l2[:n1].view(np.uint32)), key
+    eng.close()
+
+
+def _oracle_program(oracle, inst_ptr):
+    buf = np.zeros(9 * 1100, np.float32)
+    n = oracle.orc_debug_program(inst_ptr, buf.ctypes.data, 1100)
+    e = buf[: 9 * n].reshape(n, 9)
+    out, prev = [], None
+    for row in e:  # fold the wrap-split second halves (same wheel, consecutive)
+        w = int(row[0])
+        if prev is not None and w == prev:
+            continue
+        prev = w
+        er = int(row[2])
+        env, r = (0, 0) if er < 0 else ((1, er) if er < 8 else (2, er - 8))
+        out.append((w, env, r, row[3:9].copy()))
+    return out
+
+
+def _engine_program(lib, eng, i):
+    buf = np.zeros(9 * 600, np.float32)
+    n = lib.tbf_debug_step(eng._h, i, buf.ctypes.data, 600)
+    assert n >= 0
+    return buf[: 9 * n].reshape(n, 9)
+
+
+def _events_by_block(scen):
+    by = {}
+    for (b, kind, a, v) in scen:
+        by.setdefault(b, []).append((kind, a, v))
+    return by
+
+
+def test_control_plane_programs_match_oracle(oracle):
+    """Block-by-block core programs of the host control plane vs the oracle's
+    oscGenerateFragment (active list order, wheel, envelope row, all six gains)."""
+    from orc_bind import Chain
+    _orc_bind_debug(oracle)
+    lib = T.load_library()
+    _bind_debug(lib)
+    tpl = Template(oracle, seed=7)
+    eng = T.Engine(device=-1)
+    tid = eng.template(seed=7)
+    n_inst, nblocks = 3, 64
+    seeds = [1000 + i for i in range(n_inst)]
+    eng.add_instances([tid] * n_inst, seeds)
+    chains = [Chain(oracle, tpl, s) for s in seeds]
+    scens = [_events_by_block(S.event_scenario(i)) for i in range(n_inst)]
+    checked = 0
+    for blk in range(nblocks):
+        for i in range(n_inst):
+            for (kind, a, v) in scens[i].get(blk, []):
+                if kind == "note":
+                    eng.note(i, a, v)
+                    chains[i].note(a, v)
+                else:
+                    eng.set_param(i, a, v)
+                    chains[i].param(a, v)
+            chains[i].render(1)
+            op = _oracle_program(oracle, chains[i].ptr)
+            pp = _engine_program(lib, eng, i)
+            assert len(op) == len(pp), (blk, i)
+            for (w, env, r, g), q in zip(op, pp):
+                assert (w, env) == (int(q[0]), int(q[1])), (blk, i)
+                if env:
+                    assert r == int(q[2]), (blk, i)
+                    assert np.array_equal(g.view(np.uint32), q[3:9].view(np.uint32)), (blk, i, w)
+                else:
+                    assert np.array_equal(g[:3].view(np.uint32), q[3:6].view(np.uint32)), (blk, i, w)
+                checked += 1
+    assert checked > 1000
+    eng.close()
+
+
+def test_render_refuses_without_device():
+    """The product has no CPU path: a host-only engine refuses to render."""
+    eng = T.Engine(device=-1)
+    tid = eng.template(seed=1)
+    eng.add_instances([tid], [1])
+    with pytest.raises(T.TbfError):
+        eng.render(1)
+    with pytest.raises(T.TbfError):
+        eng.synth_sound(64)
+    eng.close()
+
+
+def test_param_and_note_validation():
+    eng = T.Engine(device=-1)
+    tid = eng.template(seed=1)
+    eng.add_instances([tid, tid], [1, 2])
+    with pytest.raises(T.TbfError):
+        eng.note(5, 60, 1)           # no such instance
+    with pytest.raises(T.TbfError):
+        eng.set_param(0, 9999, 1.0)  # unknown parameter id
+    with pytest.raises(T.TbfError):
+        eng.add_instances([77], [1])  # unknown template
+    eng.note(0, 60, 1)
+    eng.set_param(1, S.P_DRAWBAR + 2, 4)
+    assert eng.n_instances == 2
+    eng.close()
+
+
+# ---------------------------------------------------------------- N>1 sharding (gloo)
+def _digest(lib, eng, n, steps):
+    import hashlib
+    out = []
+    for i in range(n):
+        h = hashlib.sha256()
+        for _ in range(steps):
+            h.update(_engine_program(lib, eng, i).tobytes())
+        out.append(h.hexdigest())
+    return out
+
+
+def _rank_main(rank, world, port, n_total, q):
+    import os
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tunebfree_amd.shard import shard
+    lib = T.load_library()
+    _bind_debug(lib)
+    first, cnt = shard(n_total, rank, world)
+    eng = T.Engine(device=-1)
+    tid = eng.template(seed=7)
+    eng.add_instances([tid] * cnt, [1000 + first + i for i in range(cnt)])
+    for i in range(cnt):
+        for (_, kind, a, v) in S.bench_scenario(first + i):
+            (eng.note if kind == "note" else eng.set_param)(i, a, v)
+    dig = _digest(lib, eng, cnt, 3)
+    got = [None] * world
+    dist.all_gather_object(got, (first, cnt, dig))
+    if rank == 0:
+        q.put(got)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_world2_gloo():
+    import multiprocessing as mp
+    import socket
+    from tunebfree_amd.shard import shard
+    n_total = 7
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_rank_main, args=(r, 2, port, n_total, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = q.get(timeout=240)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    covered = sorted(i for (f, c, _) in got for i in range(f, f + c))
+    assert covered == list(range(n_total))
+    # each rank's instances are exactly the single-process engine's instances
+    lib = T.load_library()
+    _bind_debug(lib)
+    eng = T.Engine(device=-1)
+    tid = eng.template(seed=7)
+    eng.add_instances([tid] * n_total, [1000 + i for i in range(n_total)])
+    for i in range(n_total):
+        for (_, kind, a, v) in S.bench_scenario(i):
+            (eng.note if kind == "note" else eng.set_param)(i, a, v)
+    ref = _digest(lib, eng, n_total, 3)
+    merged = [d for (f, c, dig) in sorted(got) for d in dig]
+    assert merged == ref
+    assert shard(8 * 4096, 3, 8) == (3 * 4096, 4096)
+
+
+# ---------------------------------------------------------------- exact shortcuts
+def _exact(op, rows):
+    lib = T.load_library()
+    lib.tbf_debug_exact.restype = C.c_int
+    lib.tbf_debug_exact.argtypes = [C.c_int32, C.c_void_p, C.c_void_p, C.c_uint32]
+    a = np.ascontiguousarray(rows, np.float64).reshape(-1, 3)
+    out = np.zeros((len(a), 2), np.float64)
+    assert lib.tbf_debug_exact(op, a.ctypes.data, out.ctypes.data, len(a)) == 0
+    return out
+
+
+def test_phase_closed_form_is_exact():
+    """csrc/tbf_exact.h phase_run: when it accepts a run, v0 + j*D equals the reference's
+    repeated `vib += depth * vibSpeed` (src/reverb.cpp:479-496) for every j <= m."""
+    rng = np.random.default_rng(5)
+    depth = np.array([0.003251, 0.002999, 0.002917, 0.002749, 0.002503, 0.002423, 0.002146, 0.002088])
+    ds = list(depth * 0.06) + list(depth * 1.06) + list(rng.uniform(1e-7, 0.5, 40))
+    v0s = list(rng.integers(-2 ** 31, 2 ** 31, 200).astype(np.float64) - 1073741823.0)
+    for k in range(-20, 32):  # values hugging binade edges, both signs
+        for eps in (0.0, 1e-16, 3e-16, 1e-12, 1e-6, 1e-3):
+            for sg in (1.0, -1.0):
+                v0s += [sg * 2.0 ** k * (1 + eps), sg * 2.0 ** k * (1 - eps / 2)]
+    rows = [(v, d, 64) for v in v0s for d in ds]
+    out = _exact(0, rows)
+    accepted = 0
+    for (v0, d, m), (ok, D) in zip(rows, out):
+        if not ok:
+            continue
+        accepted += 1
+        v = np.float64(v0)
+        for j in range(1, int(m) + 1):
+            v = v + np.float64(d)
+            assert v == np.float64(v0) + np.float64(j) * np.float64(D), (v0, d, j)
+    # the kernel's fast path covers the reference's own phases (rand() - RAND_MAX/2 seeds)
+    real = [(v, d, 64) for v in v0s[:200] for d in ds[:16]]
+    assert _exact(0, real)[:, 0].mean() > 0.99
+    assert 0.1 * len(rows) < accepted < len(rows)  # both outcomes exercised
+
+
+def test_count_and_wrap_shortcuts():
+    rows, want = [], []
+    for d in (560, 756, 1007, 3):
+        for c0 in (-1, 0, 1, d - 64, d - 1, d, d + 1, d + 50):
+            for n in (0, 1, 63, 64, 65, 128):
+                c = c0
+                for _ in range(n):  # src/reverb.cpp: count++; if (count < 0 || count > d) count = 0
+                    c += 1
+                    if c < 0 or c > d:
+                        c = 0
+                rows.append((c0, d, n))
+                want.append(c)
+    assert [int(x) for x in _exact(1, rows)[:, 0]] == want
+    xs = np.array([0.0, 0.25, 0.999999999, 1.0, 1.5, 1.9999999, 2.0, 2.5, -0.25, 7.75, np.nan, np.inf])
+    got = _exact(2, [(x, 0, 0) for x in xs])[:, 0]
+    ref = np.fmod(xs, 1.0)
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    assert np.array_equal(got[~np.isnan(ref)], ref[~np.isnan(ref)])

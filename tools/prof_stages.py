@@ -1,0 +1,60 @@
+"""Per-stage wave-clock breakdown of the render kernel (tbf_debug_profile marks).
+usage: python tools/prof_stages.py [--batch 4096] [--blocks 32]
+Marks add a workgroup barrier each, so totals run ~10% above the unprofiled kernel."""
+import argparse
+import ctypes as C
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests"))
+
+NAMES = {0: "tg interpreter", 1: "tg vibrato", 2: "tg mixdown", 3: "od serial", 4: "od parallel",
+         5: "rv fpd serial", 6: "rv reads+taps", 7: "rv pd write + A/B chains", 8: "rv ap/line writes + asin",
+         9: "rv C chain", 10: "rv out + counts", 11: "wh speed", 12: "wh serial filt+angles", 13: "wh FILTER_C",
+         14: "wh ring rd + drum shelves", 15: "wh motions", 16: "wh accumulate", 17: "wh out + carry",
+         18: "state load", 19: "state store"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--blocks", type=int, default=32)
+    a = ap.parse_args()
+    import torch
+    import tunebfree_amd as T
+    import scenarios as S
+    eng = T.Engine(sample_rate=48000.0, device=0)
+    tid = eng.template(seed=7)
+    B = a.batch
+    eng.add_instances([tid] * B, [1000 + i for i in range(B)])
+    for i in range(B):
+        for (_, kind, x, v) in S.bench_scenario(i):
+            (eng.note if kind == "note" else eng.set_param)(i, x, v)
+    n = a.blocks * 128
+    oL = torch.empty((B, n), dtype=torch.float32, device="cuda")
+    oR = torch.empty((B, n), dtype=torch.float32, device="cuda")
+    eng.render_device(a.blocks, oL.data_ptr(), oR.data_ptr(), n)
+    eng.synchronize()
+    lib = T.load_library()
+    lib.tbf_debug_profile.restype = C.c_int
+    lib.tbf_debug_profile.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_uint32]
+    assert lib.tbf_debug_profile(eng._h, 1, None, 0) == 0
+    eng.render_device(a.blocks, oL.data_ptr(), oR.data_ptr(), n)
+    eng.synchronize()
+    buf = np.zeros(B * 32, np.uint64)
+    assert lib.tbf_debug_profile(eng._h, 0, buf.ctypes.data, buf.size) >= 0
+    lib.tbf_debug_profile(eng._h, -1, None, 0)
+    per = buf.reshape(B, 32).astype(np.float64).mean(axis=0) / a.blocks
+    tot = per.sum()
+    print(f"wave-clock cycles per 128-sample block (mean over {B} instances), total {tot:.0f}")
+    for k in range(32):
+        if per[k] > 0:
+            print(f"  {k:2d} {NAMES.get(k, '?'):28s} {per[k]:10.0f}  {100 * per[k] / tot:5.1f}%")
+
+
+if __name__ == "__main__":
+    main()

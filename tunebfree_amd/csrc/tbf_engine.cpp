@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../include/tbf.h"
+#include "tbf_exact.h"
 #include "tbf_host.h"
 #include "tbf_types.h"
 
@@ -110,6 +111,8 @@ struct tbf_engine {
 	DevBuf<uint32_t>                        vib;
 	DevBuf<float>                           whTab, whBw;
 	DevBuf<uint32_t>                        err;
+	DevBuf<uint64_t>                        prof; /* tbf_debug_profile */
+	bool                                    profOn = false;
 	DevBuf<float>                           outL, outR;
 	std::vector<tbf_seg_ctl>                hCtl;
 	std::vector<tbf_prog_entry>             hProg;
@@ -617,6 +620,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 	P.chain     = e->cfg.chain_mode;
 	P.slabLen   = e->slabLen;
 	P.errFlags  = e->err.p;
+	P.prof      = e->profOn ? e->prof.p : nullptr;
 	uint32_t b0 = 0;
 	while (b0 < nblocks) {
 		uint32_t lo, hi;
@@ -764,6 +768,56 @@ int tbf_debug_step (tbf_engine* e, uint32_t i, float* out, uint32_t cap)
 		o[3] = p.sg; o[4] = p.pg; o[5] = p.vg; o[6] = p.nsg; o[7] = p.npg; o[8] = p.nvg;
 	}
 	return (int)in.prog.size ();
+}
+
+int tbf_debug_profile (tbf_engine* e, int32_t enable, uint64_t* out, uint32_t cap)
+{
+	if (!e)
+		return fail (-22, "null engine");
+	const size_t n = (size_t)e->inst.size () * TBF_PROF_SLOTS;
+	if (enable == 1) {
+		if (e->cfg.device < 0)
+			return fail (-19, "host-only engine");
+		HIPCHK (hipSetDevice (e->cfg.device));
+		if (e->prof.ensure (n))
+			return fail (-12, "out of device memory");
+		HIPCHK (hipMemset (e->prof.p, 0, n * sizeof (uint64_t)));
+		e->profOn = true;
+		return 0;
+	}
+	if (enable == 0) {
+		if (!e->profOn)
+			return fail (-22, "profiling not enabled");
+		HIPCHK (hipStreamSynchronize (e->stream));
+		HIPCHK (hipDeviceSynchronize ());
+		const size_t m = std::min<size_t> (n, cap);
+		if (out && m)
+			HIPCHK (hipMemcpy (out, e->prof.p, m * sizeof (uint64_t), hipMemcpyDeviceToHost));
+		return (int)n;
+	}
+	e->profOn = false;
+	return 0;
+}
+
+int tbf_debug_exact (int32_t op, const double* in, double* out, uint32_t n)
+{
+	if (!in || !out || op < 0 || op > 2)
+		return fail (-22, "bad arguments");
+	for (uint32_t i = 0; i < n; i++) {
+		const double* a = in + 3 * i;
+		double*       o = out + 2 * i;
+		o[0] = o[1] = 0.0;
+		if (op == 0) {
+			double D = 0.0;
+			o[0]     = phase_run (a[0], a[1], (int)a[2], D) ? 1.0 : 0.0;
+			o[1]     = D;
+		} else if (op == 1) {
+			o[0] = cnt_adv ((int)a[0], (int)a[1], (int)a[2]);
+		} else {
+			o[0] = wrap1 (a[0]);
+		}
+	}
+	return 0;
 }
 
 } /* extern "C" */

@@ -1,0 +1,60 @@
+/*
+ * tbf_exact.h -- exact shortcuts for serial recurrences of the reference, shared by the
+ * kernel and a host test hook (tbf_debug_exact) so CPU tests can check them against
+ * the literal recurrences.
+ */
+#ifndef TBF_EXACT_H
+#define TBF_EXACT_H
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#define TBF_HD __host__ __device__ __forceinline__
+
+/* count after n increments of `count++; if (count < 0 || count > d) count = 0` */
+TBF_HD int cnt_adv (int c0, int d, int n)
+{
+	if (c0 >= 0 && c0 <= d && n <= d + 1) { /* steady state: one wrap at most */
+		const int v = c0 + n;
+		return v > d ? v - d - 1 : v;
+	}
+	if (n == 0)
+		return c0;
+	if (c0 > d || c0 < 0)
+		return (n - 1) % (d + 1);
+	return (c0 + n) % (d + 1);
+}
+
+/* Exact closed form of `v += d` repeated (src/reverb.cpp:479-496 vibrato phases).
+ * Inside one binade [2^(e-1), 2^e) of |v| every sum lands on the grid u = 2^(e-53), so
+ * fl(v + d) = v + D with D = rint(d/u)*u, unless d/u is a tie.  Valid for a run of m
+ * steps when the first and last values stay at least one grid step inside the binade
+ * (the exact sums then never reach a binade edge).  Returns false otherwise. */
+TBF_HD bool phase_run (double v0, double d, int m, double& D)
+{
+	if (!(d >= 0.0) || !(fabs (v0) > 0.0) || !isfinite (v0))
+		return false;
+	int e;
+	frexp (v0, &e);
+	const double u  = ldexp (1.0, e - 53);
+	const double lo = ldexp (1.0, e - 1) + u, hi = ldexp (1.0, e) - u;
+	const double k  = d / u;
+	const double r  = rint (k);
+	if (fabs (k - r) == 0.5)
+		return false;
+	D              = r * u;
+	const double w = v0 + (double)m * D;
+	const double a0 = fabs (v0), a1 = fabs (w);
+	return a0 >= lo && a0 <= hi && a1 >= lo && a1 <= hi && ((v0 < 0) == (w < 0));
+}
+
+/* fmod (x, 1.0) for the rotor angle update (src/whirl.cpp:1428-1429): for x in [0, 2)
+ * fmod is x or x - 1, the latter exact by Sterbenz; anything else takes libm. */
+TBF_HD double wrap1 (double x)
+{
+	if (x >= 0.0 && x < 2.0)
+		return x >= 1.0 ? x - 1.0 : x;
+	return fmod (x, 1.0);
+}
+
+#endif

@@ -13,6 +13,7 @@
 #define TBF_BLK 128   /* BUFFER_SIZE_SAMPLES, src/tonegen.h:53 */
 #define TBF_SUB 64    /* sub-block for reverb/whirl: one sample per lane of a wave64 */
 #define TBF_NW 256    /* NOF_WHEELS, src/tonegen.h:79 */
+#define TBF_PROF_SLOTS 32
 #define TBF_VRING 256 /* compact vibrato ring (reference 1024; live window <= 21+128) */
 
 /* one core-program entry = one wheel's contribution for one block
@@ -138,6 +139,7 @@ typedef struct tbf_launch {
 	uint32_t              slabLen;
 	uint32_t              pad;
 	uint32_t*             errFlags;
+	uint64_t*             prof;      /* [inst][TBF_PROF_SLOTS] stage cycle sums, or NULL */
 } tbf_launch;
 
 #endif

@@ -60,6 +60,46 @@ def event_scenario(i):
     return ev
 
 
+class GlibcRand:
+    """glibc srand()/rand() (TYPE_3 additive generator), for event scripts that follow
+    the reference's rand()-driven control code."""
+
+    def __init__(self, seed):
+        seed = seed or 1
+        r = [0] * 34
+        r[0] = seed & 0x7FFFFFFF if seed < 2 ** 31 else seed - 2 ** 32
+        for i in range(1, 31):
+            hi, lo = divmod(r[i - 1], 127773) if r[i - 1] >= 0 else (-((-r[i - 1]) // 127773), -((-r[i - 1]) % 127773))
+            w = 16807 * lo - 2836 * hi
+            r[i] = w + 2147483647 if w < 0 else w
+        for i in range(31, 34):
+            r[i] = r[i - 31]
+        self.r = [x & 0xFFFFFFFF for x in r]
+        for _ in range(310):
+            self._step()
+
+    def _step(self):
+        v = (self.r[-31] + self.r[-3]) & 0xFFFFFFFF
+        self.r.append(v)
+        del self.r[0]
+        return v >> 1
+
+    def next(self):
+        return self._step()
+
+
+def random_drawbar_scenario(i, seed=None):
+    """BASELINE config 5: upper drawbars from randomizeDrawbars (`rand() % 9` x 9,
+    src/program.cpp:716-729) after srand(seed), rest of the Jazz-1 registration,
+    chord root 48+(i mod 24) + {0,4,7,12}."""
+    g = GlibcRand(1 + i if seed is None else seed)
+    bars = [g.next() % 9 for _ in range(9)]
+    ev = [(0, k, a, b) for (k, a, b) in jazz1_params()]
+    ev += [(0, "param", P_DRAWBAR + j, v) for j, v in enumerate(bars)]
+    ev += [(0, "note", k, 1) for k in chord_for(i)]
+    return ev
+
+
 def run(chain, scenario, nblocks, stages=False):
     """Apply events at block boundaries and render; returns concatenated arrays."""
     import numpy as np

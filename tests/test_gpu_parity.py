@@ -69,3 +69,62 @@ def test_gpu_full_chain_events(oracle):
     eR, xR = compare(R, oR)
     print(f"events: max|err| L={eL:.3g} R={eR:.3g} bit-exact L={xL:.6f} R={xR:.6f}")
     assert max(eL, eR) <= TOL
+
+
+def test_gpu_vs_committed_reference_vectors():
+    """The HIP engine against the reference's own compiled chain (committed vectors,
+    tests/golden/ref_vectors.npz): 44.1/48/96 kHz (whirl ring W=512/1024), 12-TET /
+    19-TET / p4 / bagpipe4 templates, event scripts, config-5 random drawbars."""
+    import json
+    from pathlib import Path
+    import tunebfree_amd as T
+    from golden.make_ref_vectors import scenario
+    gold = Path(__file__).resolve().parent / "golden"
+    z = np.load(gold / "ref_vectors.npz")
+    tunings = json.loads((gold / "tunings.json").read_text())
+    worst = 0.0
+    for c in json.loads(str(z["cases"])):
+        eng = T.Engine(sample_rate=c["sr"], device=0, chain=c["chain"])
+        m = None if c["tuning"] is None else np.array(tunings[c["tuning"]], np.float64)
+        tid = eng.template(mts128=m, seed=c["tpl_seed"])
+        eng.add_instances([tid], [c["inst_seed"]])
+        L, R = engine_run(eng, [scenario(*c["scenario"])], c["nblocks"])
+        for got, k in ((L[0], "L"), (R[0], "R")):
+            err, exact = compare(got, z[f"{c['name']}/{k}"])
+            print(f"{c['name']}/{k}: max|err|={err:.3g} bit-exact={exact:.6f}")
+            worst = max(worst, err)
+        eng.close()
+    assert worst <= TOL
+
+
+def test_gpu_config5_mixed_tunings_96k(oracle):
+    """BASELINE config 5 shape at test size: 96 kHz, one shared template per tuning
+    (7 tunings of the reference's tests), per-instance random drawbars, several
+    templates interleaved inside one launch."""
+    import json
+    from pathlib import Path
+    import tunebfree_amd as T
+    from orc_bind import Template
+    tunings = json.loads((Path(__file__).resolve().parent / "golden" / "tunings.json").read_text())
+    names = sorted(tunings, key=lambda k: (tunings[k] is not None, k))
+    eng = T.Engine(sample_rate=96000.0, device=0)
+    tids, tpls = {}, {}
+    for j, nm in enumerate(names):
+        m = None if tunings[nm] is None else np.array(tunings[nm], np.float64)
+        tids[nm] = eng.template(mts128=m, seed=100 + j)
+        tpls[nm] = Template(oracle, sr=96000.0, mts128=m, seed=100 + j)
+    n = 2 * len(names)
+    pick = [names[(5 * i) % len(names)] for i in range(n)]
+    seeds = [7000 + i for i in range(n)]
+    eng.add_instances([tids[p] for p in pick], seeds)
+    scens = [S.random_drawbar_scenario(i) for i in range(n)]
+    L, R = engine_run(eng, scens, 24)
+    worst, ex = 0.0, []
+    for i in range(n):
+        oL, oR, *_ = oracle_run(oracle, tpls[pick[i]], [seeds[i]], [scens[i]], 24)
+        for a, b in ((L[i], oL[0]), (R[i], oR[0])):
+            e, x = compare(a, b)
+            worst = max(worst, e)
+            ex.append(x)
+    print(f"config5: {n} instances, {len(names)} tunings, max|err|={worst:.3g} bit-exact={min(ex):.6f}")
+    assert worst <= TOL

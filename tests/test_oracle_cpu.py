@@ -186,3 +186,37 @@ def test_stage_units_vs_reference(oracle, refchk, sr):
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
         oracle.orc_preamp_free(po)
         refchk.ref_preamp_free(pr)
+
+
+# --------------------------------------------------------------------------- committed vectors
+def _golden_cases():
+    z = np.load(GOLD / "ref_vectors.npz")
+    return z, json.loads(str(z["cases"]))
+
+
+def test_glibc_rand_python_mirror():
+    """scenarios.GlibcRand (used by the config-5 random-drawbar scripts) == libc rand()."""
+    libc = C.CDLL(None)
+    for seed in (1, 3, 12345, 0, 2 ** 31 + 5):
+        libc.srand(C.c_uint(seed))
+        a = [libc.rand() for _ in range(500)]
+        g = S.GlibcRand(seed)
+        assert a == [g.next() for _ in range(500)], seed
+
+
+def test_oracle_vs_committed_reference_vectors(oracle, tunings):
+    """The oracle reproduces, bit for bit and at every stage tap, the outputs of the
+    reference's own compiled TUs committed in tests/golden/ref_vectors.npz (generator:
+    tests/golden/make_ref_vectors.py) -- 44.1/48/96 kHz, 4 tunings, event scripts."""
+    from golden.make_ref_vectors import scenario
+    z, cases = _golden_cases()
+    assert len(cases) >= 6
+    for c in cases:
+        m = None if c["tuning"] is None else np.array(tunings[c["tuning"]], np.float64)
+        tpl = Template(oracle, sr=c["sr"], mts128=m, seed=c["tpl_seed"])
+        ch = Chain(oracle, tpl, c["inst_seed"])
+        ch.chain(c["chain"])
+        got = S.run(ch, scenario(*c["scenario"]), c["nblocks"], stages=True)
+        for k, v in zip("LRABC", got):
+            ref = z[f"{c['name']}/{k}"]
+            assert np.array_equal(v.view(np.uint32), ref.view(np.uint32)), (c["name"], k)

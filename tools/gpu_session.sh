@@ -25,7 +25,7 @@ BENCHP="--steps 3 --warmup 1 --cpu-baseline 0 --check 0 --blocks 16"
 for s in $STEPS; do
 	case $s in
 	list) run counters 120 rocprofv3 -L ;;
-	tests) run tests 900 python3 -m pytest tests -x -q -m gpu ;;
+	tests) run tests 900 python3 -u -m pytest tests -x -v -s -m gpu --timeout 300 --timeout-method thread ;;
 	bench) run bench 900 python3 bench.py ;;
 	prof) run prof 300 python3 tools/prof_stages.py ;;
 	ablate) for c in 1 2 3 0; do run ablate$c 300 python3 bench.py --chain $c --steps 3 --warmup 1 --cpu-baseline 0 --check 0; done ;;
@@ -40,6 +40,10 @@ for s in $STEPS; do
 		for c in 1 2 3 0; do
 			run pmcc$c 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU -d "$OUT/pmcc$c" -o run --output-format csv -- python3 bench.py $BENCHP --chain $c
 		done ;;
+	calib)
+		run calib_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/calib_fetch" -o run --output-format csv -- python3 tools/calib_pmc.py
+		run calib_write 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/calib_write" -o run --output-format csv -- python3 tools/calib_pmc.py
+		;;
 	*) echo "unknown step $s" ;;
 	esac
 done

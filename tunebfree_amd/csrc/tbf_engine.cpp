@@ -19,6 +19,7 @@
 #include "tbf_types.h"
 
 extern "C" int tbf_launch_render (const tbf_launch* P, hipStream_t stream);
+extern "C" int tbf_launch_calibrate (int op, void* buf, uint64_t n, hipStream_t s);
 
 using namespace tbf;
 
@@ -818,6 +819,14 @@ int tbf_debug_exact (int32_t op, const double* in, double* out, uint32_t n)
 		}
 	}
 	return 0;
+}
+
+int tbf_debug_calibrate (int32_t op, void* buf, uint64_t n, void* stream)
+{
+	if (!buf || (op != 0 && op != 1))
+		return fail (-22, "bad arguments");
+	int rc = tbf_launch_calibrate (op, buf, n, (hipStream_t)stream);
+	return rc ? fail (rc, "calibration launch failed") : 0;
 }
 
 } /* extern "C" */

@@ -40,6 +40,11 @@ for s in $STEPS; do
 		for c in 1 2 3 0; do
 			run pmcc$c 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU -d "$OUT/pmcc$c" -o run --output-format csv -- python3 bench.py $BENCHP --chain $c
 		done ;;
+	quick) run quick 600 python3 bench.py --cpu-baseline 0 --check 2 --steps 3 --warmup 1 ;;
+	variants)
+		for v in tunebfree_amd/_variants/libtbf_*.so; do
+			run "var_$(basename $v .so)" 300 env TBF_LIB=$v python3 bench.py --cpu-baseline 0 --check 2 --steps 3 --warmup 1
+		done ;;
 	calib)
 		run calib_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/calib_fetch" -o run --output-format csv -- python3 tools/calib_pmc.py
 		run calib_write 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/calib_write" -o run --output-format csv -- python3 tools/calib_pmc.py

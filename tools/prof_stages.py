@@ -12,11 +12,12 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "tests"))
 
-NAMES = {0: "tg interpreter", 1: "tg vibrato", 2: "tg mixdown", 3: "od serial", 4: "od parallel",
-         5: "rv fpd serial", 6: "rv reads+taps", 7: "rv pd write + A/B chains", 8: "rv ap/line writes + asin",
-         9: "rv C chain", 10: "rv out + counts", 11: "wh speed", 12: "wh serial filt+angles", 13: "wh FILTER_C",
-         14: "wh ring rd + drum shelves", 15: "wh motions", 16: "wh accumulate", 17: "wh out + carry",
-         18: "state load", 19: "state store"}
+NAMES = {0: "tg state load + interpreter", 1: "tg vibrato", 2: "tg mixdown", 3: "od serial", 4: "od parallel",
+         18: "tg state store",
+         5: "rv state load + fpd serial", 6: "rv reads+taps", 7: "rv pd write + A/B chains",
+         8: "rv ap/line writes + asin", 9: "rv C chain", 10: "rv out + counts",
+         17: "wh state + ring load", 11: "wh speed", 12: "wh ring rd + serial filt+angles", 13: "wh FILTER_C",
+         14: "wh motions", 15: "wh accumulate", 16: "wh out + carry", 19: "wh state + ring store"}
 
 
 def main():

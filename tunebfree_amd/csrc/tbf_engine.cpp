@@ -115,6 +115,7 @@ struct tbf_engine {
 	DevBuf<uint64_t>                        prof; /* tbf_debug_profile */
 	bool                                    profOn = false;
 	DevBuf<float>                           outL, outR;
+	DevBuf<float>                           mid1, mid2; /* inter-stage blocks of one launch chunk */
 	std::vector<tbf_seg_ctl>                hCtl;
 	std::vector<tbf_prog_entry>             hProg;
 	/* synth_sound FIFO */
@@ -123,6 +124,9 @@ struct tbf_engine {
 };
 
 #define PROG_CAP (TBF_NW + 1)
+/* blocks per kernel launch chunk: bounds the inter-stage buffers to
+ * n_inst x TBF_CHUNK x 128 floats each (134 MB at 4096 instances) */
+#define TBF_CHUNK 64
 
 /* ------------------------------------------------------------------ construction */
 
@@ -293,6 +297,8 @@ int tbf_engine_destroy (tbf_engine* e)
 	e->err.release ();
 	e->outL.release ();
 	e->outR.release ();
+	e->mid1.release ();
+	e->mid2.release ();
 	if (e->stream)
 		(void)hipStreamDestroy (e->stream);
 	delete e;
@@ -350,33 +356,34 @@ int tbf_instances_add (tbf_engine* e, uint32_t n, const uint32_t* tpl_ids, const
 		GlibcRand rnd (seeds[q]);
 		for (int c = 0; c < 2; c++)
 			for (int l = 0; l < 8; l++)
-				in.s0.vib[c][l] = rnd.next () - 2147483647 / 2;
+				in.s0.rv.vib[c][l] = rnd.next () - 2147483647 / 2;
 		uint32_t f = 1;
 		while (f < 16386)
 			f = (uint32_t)rnd.next () * 0xFFFFFFFFu;
-		in.s0.fpdL = f;
+		in.s0.rv.fpdL = f;
 		f          = 1;
 		while (f < 16386)
 			f = (uint32_t)rnd.next () * 0xFFFFFFFFu;
-		in.s0.fpdR = f;
+		in.s0.rv.fpdR = f;
 		f          = 1;
 		while (f < 16386)
 			f = (uint32_t)rnd.next () * 0xFFFFFFFFu;
-		in.s0.odFpd  = f;
-		in.s0.fpFlip = 1;
+		in.s0.tg.odFpd  = f;
+		in.s0.tg.fpFlip = 1;
 		for (int l = 0; l < 13; l++)
-			in.s0.count[l] = 1;
+			in.s0.rv.count[l] = 1;
 		reverbConsts (in.k, sr, 1.0f, 0.2f, 0.0f, 0.0f, 0.4f, 0.8f);
 		whirlConsts (in.k, e->wt);
 		/* initWhirl -> computeRotationSpeeds -> setRevSelect(0) -> useRevOption(4) */
-		in.s0.hornTarget = e->wt.revHorn[4];
-		in.s0.drumTarget = e->wt.revDrum[4];
-		in.s0.hornAcDc   = in.s0.hornIncr < in.s0.hornTarget ? 1 : (in.s0.hornTarget < in.s0.hornIncr ? -1 : 0);
-		in.s0.drumAcDc   = in.s0.drumIncr < in.s0.drumTarget ? 1 : (in.s0.drumTarget < in.s0.drumIncr ? -1 : 0);
+		tbf_wh_state& w  = in.s0.wh;
+		w.hornTarget     = e->wt.revHorn[4];
+		w.drumTarget     = e->wt.revDrum[4];
+		w.hornAcDc       = w.hornIncr < w.hornTarget ? 1 : (w.hornTarget < w.hornIncr ? -1 : 0);
+		w.drumAcDc       = w.drumIncr < w.drumTarget ? 1 : (w.drumTarget < w.drumIncr ? -1 : 0);
 		/* tonegen + vibrato runtime state (initToneGenerator, reset_vibrato) */
-		in.s0.keyCompLevel = 1.0f;
-		in.s0.percEnvGain  = 0.0f;
-		in.s0.outPos       = 1023 / 2;
+		in.s0.tg.keyCompLevel = 1.0f;
+		in.s0.tg.percEnvGain  = 0.0f;
+		in.s0.tg.outPos       = 1023 / 2;
 		in.tg.init (e->tpls[in.tpl].get ());
 		if (e->slabLen == 0)
 			e->slabLen = in.k.slabLen;
@@ -622,6 +629,14 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 	P.slabLen   = e->slabLen;
 	P.errFlags  = e->err.p;
 	P.prof      = e->profOn ? e->prof.p : nullptr;
+	if (e->cfg.chain_mode != TBF_CHAIN_TONEGEN) {
+		const size_t need = (size_t)n * TBF_CHUNK * TBF_BLK;
+		if (e->mid1.ensure (need) || e->mid2.ensure (need))
+			return fail (-12, "out of device memory (stage buffers)");
+	}
+	P.mid1      = e->mid1.p;
+	P.mid2      = e->mid2.p;
+	P.midStride = (uint64_t)TBF_CHUNK * TBF_BLK;
 	uint32_t b0 = 0;
 	while (b0 < nblocks) {
 		uint32_t lo, hi;
@@ -632,14 +647,32 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		if (hi > lo)
 			HIPCHK (hipMemcpyAsync (e->prog.p + (size_t)lo * PROG_CAP, e->hProg.data () + (size_t)lo * PROG_CAP,
 			                        (size_t)(hi - lo) * PROG_CAP * sizeof (tbf_prog_entry), hipMemcpyHostToDevice, s));
-		const uint32_t len = again ? 1u : nblocks - b0;
-		P.nBlocks          = len;
-		P.outOffset        = (uint64_t)b0 * TBF_BLK;
-		rc                 = tbf_launch_render (&P, s);
-		if (rc)
-			return fail (rc, std::string ("kernel launch failed: ") + hipGetErrorString (hipGetLastError ()));
+		const uint32_t len      = again ? 1u : nblocks - b0;
+		bool           needSync = ctlChanged || hi > lo;
+		/* the segment runs in chunks; only the first chunk may apply a rotary one-shot */
+		for (uint32_t c0 = 0; c0 < len; c0 += TBF_CHUNK) {
+			P.nBlocks   = std::min<uint32_t> (TBF_CHUNK, len - c0);
+			P.outOffset = (uint64_t)(b0 + c0) * TBF_BLK;
+			if (c0 > 0 && ctlChanged) {
+				/* clear the rev-option one-shot for the following chunks */
+				bool any = false;
+				for (uint32_t i = 0; i < n; i++)
+					if (e->hCtl[i].whRevOption >= 0) {
+						e->hCtl[i].whRevOption = -1;
+						any                    = true;
+					}
+				if (any) {
+					HIPCHK (hipStreamSynchronize (s));
+					HIPCHK (hipMemcpyAsync (e->ctl.p, e->hCtl.data (), n * sizeof (tbf_seg_ctl), hipMemcpyHostToDevice, s));
+				}
+				ctlChanged = false;
+			}
+			rc = tbf_launch_render (&P, s);
+			if (rc)
+				return fail (rc, std::string ("kernel launch failed: ") + hipGetErrorString (hipGetLastError ()));
+		}
 		/* host staging buffers are rewritten by the next buildControl: keep order */
-		if (ctlChanged || hi > lo)
+		if (needSync)
 			HIPCHK (hipStreamSynchronize (s));
 		b0 += len;
 	}

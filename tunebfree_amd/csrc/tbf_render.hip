@@ -1,17 +1,23 @@
 /*
- * tbf_render.hip -- gfx950 render kernel for the tuneBfree block quartet
+ * tbf_render.hip -- gfx950 render kernels for the tuneBfree block quartet
  *   oscGenerateFragment -> preamp -> b_reverb::reverb -> whirlProc3
  * (src/tonegen.cpp:3218, src/overdrive.cpp:329, src/reverb.cpp:274, src/whirl.cpp:1653).
  *
- * Mapping: one workgroup = one wave64 = one organ instance; the kernel loops over the
- * segment's 128-sample blocks with the instance's DSP state resident in LDS.
- *   - tonegen:   lane = sample (2 samples/lane), wheel loop in active-list order
- *   - vibrato:   lane-parallel scatter recast as an ordered per-slot gather
- *   - overdrive, reverb, whirl: sub-blocks of 64 samples, lane = sample; every ring
- *     read of a sub-block happens before its ring writes (write-after-read), which is
- *     exact because every ring delay exceeds the sub-block (reverb >= 560, whirl >= 79
- *     samples ahead); per-sample IIR/phase recurrences run on single lanes in the
- *     reference's literal operation order.
+ * Three kernels per launch chunk, each one wave64 per organ instance looping over the
+ * chunk's 128-sample blocks with that stage's state resident in LDS:
+ *   k_tonegen  tonegen + vibrato + mixdown + overdrive   -> mid1 [inst][block*128]
+ *   k_reverb   MatrixVerb (FP64)                         -> mid2
+ *   k_whirl    horn/drum rotors + mic mix                -> outL / outR
+ * Every stage is causal, so running all blocks of stage k before stage k+1 is exact.
+ * Splitting the stages gives each kernel its own register and LDS budget (occupancy
+ * 3-4 waves/SIMD instead of 2 for the fused kernel); mid1/mid2 add 16 B per stereo
+ * sample of HBM traffic against the reverb's 416 B.
+ *
+ * Inside a stage: lane = sample (tonegen: 2 samples/lane; reverb/whirl: 64-sample
+ * sub-blocks).  Every ring read of a sub-block happens before its ring writes, which is
+ * exact because every ring delay exceeds the sub-block (reverb >= 560, whirl >= 79
+ * samples ahead).  Per-sample IIR/phase recurrences run on single lanes in the
+ * reference's literal operation order.
  * Float discipline: compiled with -ffp-contract=off, no fast-math, denormals kept;
  * every expression follows the reference's evaluation order so results are
  * bit-identical to the strict-IEEE oracle except for FP64 libm (sin/asin) ulps.
@@ -20,72 +26,80 @@
 #include <math.h>
 #include <stdint.h>
 
+#include "../../include/tbf.h"
 #include "tbf_types.h"
 #include "tbf_exact.h"
 
 #define NL 64
 
-struct TgScratch {
-	float swl[TBF_BLK];
-	float vin[TBF_BLK];
-	float prc[TBF_BLK];
+/* occupancy targets (waves per SIMD); LDS and VGPR budgets are sized for them */
+#ifndef TG_WAVES
+#define TG_WAVES 4
+#endif
+#ifndef RV_WAVES
+#define RV_WAVES 2
+#endif
+#ifndef WH_WAVES
+#define WH_WAVES 3
+#endif
+
+/* ------------------------------------------------------------------ LDS layouts */
+struct TgLds {
+	tbf_tg_state st;
+	float        bufA[TBF_BLK];
+	float        bufB[TBF_BLK];
+	float        swl[TBF_BLK];
+	float        vin[TBF_BLK];
+	float        prc[TBF_BLK];
 	union {
 		struct { /* core-program entries resolved by the interpreter prologue */
 			uint32_t base[TBF_NW + 8]; /* bank index of the wheel's current sample */
 			uint32_t lim[TBF_NW + 8];  /* samples before the wheel's wrap */
 			uint32_t len[TBF_NW + 8];  /* wheel length */
 		} ent;
-		struct {
-			float    vout[TBF_BLK];
-			float    va[TBF_BLK];
-			float    vg[TBF_BLK];
-			int32_t  vh[TBF_BLK];
-			float    pe[TBF_BLK];
-			float    kc[TBF_BLK];
+		struct { /* vibrato + mixdown */
+			float   vout[TBF_BLK];
+			float   va[TBF_BLK];
+			float   vg[TBF_BLK];
+			int32_t vh[TBF_BLK];
+			float   pe[TBF_BLK];
+			float   kc[TBF_BLK];
+		} v;
+		struct { /* overdrive */
 			double   odx[TBF_BLK];
 			double   odh[TBF_BLK];
 			uint32_t fpd[TBF_BLK + 1];
-		};
-	};
+		} od;
+	} u;
+	unsigned long long prof[TBF_PROF_SLOTS];
+	unsigned long long plast;
 };
 
-struct RvScratch {
-	double   a[2][TBF_SUB]; /* predelay output -> biquadA output */
-	double   b[2][TBF_SUB]; /* tap mix -> biquadB -> asin -> biquadC output */
-	double   t[8][TBF_SUB]; /* one channel's vibrato offsets */
-	double   vn[2][8];      /* vibrato phases after the sub-block */
-	double   fbn[2][8];     /* feedback of the sub-block's last sample */
-	uint32_t fpd[2][TBF_SUB + 1];
-};
-
-struct WhScratch {
-	double   ang[2][TBF_SUB];
-	float    xx[TBF_SUB + 1];
-	float    xf[TBF_SUB + 4];
-	float    x1[TBF_SUB + 4];
-	float    x2[TBF_SUB + 4];
-	float    xd1[TBF_SUB + 1];
-	float    xd2[TBF_SUB];
-	float    rd[2][TBF_SUB];
-	float    y[2][TBF_SUB];
-	float    ma[3][TBF_SUB];
-	float    mb[3][TBF_SUB];
-	int32_t  mu[3][TBF_SUB]; /* unwrapped write slot (outpos wrap folded in) */
+struct RvLds {
+	tbf_rv_state st;
+	float        in[TBF_BLK];
+	double       a[2][TBF_SUB]; /* predelay output -> biquadA output */
+	double       b[2][TBF_SUB]; /* tap mix -> biquadB -> asin -> biquadC output */
+	double       t[8][TBF_SUB]; /* one channel's vibrato offsets */
+	double       vn[2][8];      /* vibrato phases after the sub-block */
+	double       fbn[2][8];     /* feedback of the sub-block's last sample */
+	uint32_t     fpd[2][TBF_SUB + 1];
+	unsigned long long prof[TBF_PROF_SLOTS];
+	unsigned long long plast;
 };
 
 template <int W>
-struct Lds {
-	tbf_inst_state st;
-	float          wring[4][W];
-	float          bufA[TBF_BLK];
-	float          bufB[TBF_BLK];
-	float          bufC[TBF_BLK];
-	union {
-		TgScratch tg;
-		RvScratch rv;
-		WhScratch wh;
-	} u;
-	int brake;
+struct WhLds {
+	tbf_wh_state st;
+	float        wring[4][W];
+	double       ang[2][TBF_SUB];
+	float        xx[TBF_SUB + 1];
+	float        xf[TBF_SUB + 4];
+	float        x1[TBF_SUB + 4];
+	float        x2[TBF_SUB + 4];
+	float        xd1[TBF_SUB + 1];
+	float        rd[2][TBF_SUB]; /* drum ring outputs -> drum shelf outputs (in place) */
+	int          brake;
 	unsigned long long prof[TBF_PROF_SLOTS];
 	unsigned long long plast;
 };
@@ -103,6 +117,35 @@ struct Lds {
 			__syncthreads ();                                                            \
 		}                                                                                \
 	} while (0)
+
+template <typename L>
+__device__ __forceinline__ void prof_begin (const tbf_launch& P, L& sm)
+{
+	if (P.prof) {
+		if (threadIdx.x < TBF_PROF_SLOTS)
+			sm.prof[threadIdx.x] = 0;
+		if (threadIdx.x == 0)
+			sm.plast = __builtin_amdgcn_s_memtime ();
+	}
+}
+
+template <typename L>
+__device__ __forceinline__ void prof_end (const tbf_launch& P, L& sm, uint32_t inst)
+{
+	if (P.prof && threadIdx.x < TBF_PROF_SLOTS)
+		P.prof[(size_t)inst * TBF_PROF_SLOTS + threadIdx.x] += sm.prof[threadIdx.x];
+}
+
+/* copy a state sub-struct between HBM and LDS, one dword per lane */
+template <typename T>
+__device__ __forceinline__ void copy_words (T* dst, const T* src)
+{
+	static_assert (sizeof (T) % 4 == 0, "state structs are dword-sized");
+	const uint32_t* s = (const uint32_t*)src;
+	uint32_t*       d = (uint32_t*)dst;
+	for (uint32_t i = threadIdx.x; i < sizeof (T) / 4; i += NL)
+		d[i] = s[i];
+}
 
 __device__ __forceinline__ uint32_t xorshift (uint32_t s)
 {
@@ -126,7 +169,6 @@ __device__ __forceinline__ int wave_max (int v)
 	return v;
 }
 
-
 /* Airwindows 32-bit dither term, src/overdrive.cpp:153-159 / src/reverb.cpp:775-783.
  * The reference multiplies by a long double literal; FP64 here (the
  * difference reaches the float output with probability ~1e-17 per sample). */
@@ -148,37 +190,39 @@ __device__ __forceinline__ float frac1 (float x)
 	return fmodf (x, 1.f);
 }
 
-/* RBJ biquad, Direct Form II in float (EQ_IIR, src/whirl.cpp:1479-1485) */
-__device__ __forceinline__ float eq_iir (const float* c, float& z0, float& z1, float x)
+/* RBJ biquad, Direct Form II in float (EQ_IIR, src/whirl.cpp:1479-1485); coefficients
+ * a1 a2 b0 b1 b2 in registers */
+__device__ __forceinline__ float eq_iir (float c0, float c1, float c2, float c3, float c4, float& z0, float& z1,
+                                         float x)
 {
-	float temp = x - (c[0] * z0) - (c[1] * z1);
-	float y    = (temp * c[2]) + (c[3] * z0) + (c[4] * z1);
+	float temp = x - (c0 * z0) - (c1 * z1);
+	float y    = (temp * c2) + (c3 * z0) + (c4 * z1);
 	z1         = z0;
 	z0         = temp;
 	return y;
 }
 
-/* ------------------------------------------------------------------ tonegen */
-template <int W>
-__device__ void stage_tonegen (const tbf_launch& P, Lds<W>& sm, const tbf_seg_ctl& G, const tbf_tpl_desc* T)
-{
-	const int        lane = threadIdx.x;
-	TgScratch&       s    = sm.u.tg;
-	tbf_inst_state&  st   = sm.st;
-	const tbf_prog_entry* __restrict__ prog = P.prog + G.prog_off;
-	const int        np   = (int)G.prog_len;
-	float            sw0 = 0.f, sw1 = 0.f, vb0 = 0.f, vb1 = 0.f, pc0 = 0.f, pc1 = 0.f;
+/* ================================================================== k_tonegen */
 
-	/* core interpreter, src/tonegen.cpp:3607-3687 (wrap split folded into the index).
-	 * Prologue, lane per entry: resolve the wheel's bank position and advance st.pos
-	 * (each wheel appears once per program). */
+/* oscGenerateFragment core interpreter + vibratoProc + mixdown, src/tonegen.cpp:3607-3777 */
+__device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl& G, const tbf_tpl_desc* T)
+{
+	const int             lane = threadIdx.x;
+	tbf_tg_state&         st   = sm.st;
+	const tbf_prog_entry* __restrict__ prog = P.prog + G.prog_off;
+	const int             np   = (int)G.prog_len;
+	float                 sw0 = 0.f, sw1 = 0.f, vb0 = 0.f, vb1 = 0.f, pc0 = 0.f, pc1 = 0.f;
+
+	/* core interpreter (wrap split folded into the index).  Prologue, lane per entry:
+	 * resolve the wheel's bank position and advance st.pos (each wheel appears once per
+	 * program). */
 	for (int e = lane; e < np; e += NL) {
 		const uint32_t w   = prog[e].wheel;
 		const uint32_t pos = st.pos[w];
 		const uint32_t len = T->len[w];
-		s.ent.base[e]      = T->off[w] + pos;
-		s.ent.lim[e]       = len - pos;
-		s.ent.len[e]       = len;
+		sm.u.ent.base[e]   = T->off[w] + pos;
+		sm.u.ent.lim[e]    = len - pos;
+		sm.u.ent.len[e]    = len;
 		st.pos[w]          = (len < pos + TBF_BLK) ? pos + TBF_BLK - len : pos + TBF_BLK;
 	}
 	__syncthreads ();
@@ -187,14 +231,14 @@ __device__ void stage_tonegen (const tbf_launch& P, Lds<W>& sm, const tbf_seg_ct
 #pragma unroll 4
 	for (int e = 0; e < np; e++) {
 		const tbf_prog_entry E    = prog[e];
-		const uint32_t       base = s.ent.base[e];
-		const uint32_t       lim  = s.ent.lim[e];
-		const uint32_t       len  = s.ent.len[e];
+		const uint32_t       base = sm.u.ent.base[e];
+		const uint32_t       lim  = sm.u.ent.lim[e];
+		const uint32_t       len  = sm.u.ent.len[e];
 		const uint32_t       i0   = (uint32_t)lane < lim ? base + lane : base + lane - len;
 		const uint32_t       i1   = (uint32_t)(lane + NL) < lim ? base + lane + NL : base + lane + NL - len;
 		const float          x0   = P.bank[i0];
 		const float          x1   = P.bank[i1];
-		float       a0, a1, b0, b1, c0, c1;
+		float                a0, a1, b0, b1, c0, c1;
 		if (E.env) {
 			const float* ep = (E.env == 1 ? T->attackEnv[E.row] : T->releaseEnv[E.row]);
 			const float  e0 = ep[lane], e1 = ep[lane + NL];
@@ -220,31 +264,31 @@ __device__ void stage_tonegen (const tbf_launch& P, Lds<W>& sm, const tbf_seg_ct
 		}
 	}
 	__syncthreads (); /* the entry table is overwritten below */
-	s.swl[lane] = sw0; s.swl[lane + NL] = sw1;
-	s.vin[lane] = vb0; s.vin[lane + NL] = vb1;
-	s.prc[lane] = pc0; s.prc[lane + NL] = pc1;
+	sm.swl[lane] = sw0; sm.swl[lane + NL] = sw1;
+	sm.vin[lane] = vb0; sm.vin[lane + NL] = vb1;
+	sm.prc[lane] = pc0; sm.prc[lane + NL] = pc1;
 	__syncthreads ();
 
 	const uint32_t routing = G.routing;
 	TBF_MARK (0);
 	/* vibrato scanner, src/vibrato.cpp:365-411 */
 	if (routing & 0x03) {
-		const uint32_t* otab   = P.vibTab + 2048u * G.vibTable;
-		const uint32_t  out0   = st.outPos;
-		const uint32_t  stat0  = st.stator;
-		const float     fnorm  = (float)(1.0 / 65536.0);
+		const uint32_t* otab  = P.vibTab + 2048u * G.vibTable;
+		const uint32_t  out0  = st.outPos;
+		const uint32_t  stat0 = st.stator;
+		const float     fnorm = (float)(1.0 / 65536.0);
 		for (int k = 0; k < 2; k++) {
-			const int      n   = lane + k * NL;
-			const uint32_t op  = (out0 + n) & 0x3FFu;
-			const uint32_t sn  = (stat0 + (uint32_t)n * P.statorInc) & 0x07ffffffu;
-			const uint32_t j   = ((op << 16) + otab[sn >> 16]) & 0x03FFFFFFu;
-			const int      h   = (int)(j >> 16);
-			const float    f   = fnorm * ((float)(j & 0xFFFF));
-			const float    x   = s.vin[n];
-			const float    g   = f * x;
-			s.va[n] = x - g;
-			s.vg[n] = g;
-			s.vh[n] = n + (int)(((uint32_t)h - op) & 0x3FFu); /* slot offset from out0 */
+			const int      n  = lane + k * NL;
+			const uint32_t op = (out0 + n) & 0x3FFu;
+			const uint32_t sn = (stat0 + (uint32_t)n * P.statorInc) & 0x07ffffffu;
+			const uint32_t j  = ((op << 16) + otab[sn >> 16]) & 0x03FFFFFFu;
+			const int      h  = (int)(j >> 16);
+			const float    f  = fnorm * ((float)(j & 0xFFFF));
+			const float    x  = sm.vin[n];
+			const float    g  = f * x;
+			sm.u.v.va[n] = x - g;
+			sm.u.v.vg[n] = g;
+			sm.u.v.vh[n] = n + (int)(((uint32_t)h - op) & 0x3FFu); /* slot offset from out0 */
 		}
 		__syncthreads ();
 		/* ordered gather: slot W_o collects, in sample order, x-g from samples with
@@ -252,10 +296,10 @@ __device__ void stage_tonegen (const tbf_launch& P, Lds<W>& sm, const tbf_seg_ct
 		 * within 32 ahead (checked; lane 0 replays serially otherwise) */
 		int bad = 0, dmn = 1 << 20, dmx = -(1 << 20);
 		for (int k = 0; k < 2; k++) {
-			const int n  = lane + k * NL;
-			const int d  = s.vh[n] - n;
+			const int n = lane + k * NL;
+			const int d = sm.u.v.vh[n] - n;
 			if (d < 1 || d > 31) bad = 1;
-			if (n > 0 && s.vh[n] < s.vh[n - 1]) bad = 1;
+			if (n > 0 && sm.u.v.vh[n] < sm.u.v.vh[n - 1]) bad = 1;
 			dmn = min (dmn, d);
 			dmx = max (dmx, d);
 		}
@@ -270,16 +314,16 @@ __device__ void stage_tonegen (const tbf_launch& P, Lds<W>& sm, const tbf_seg_ct
 				const int      m0   = wo - 1 - dmx < 0 ? 0 : wo - 1 - dmx;
 				const int      m1   = wo - dmn > TBF_BLK - 1 ? TBF_BLK - 1 : wo - dmn;
 				for (int m = m0; m <= m1; m++) {
-					const int hm = s.vh[m];
+					const int hm = sm.u.v.vh[m];
 					if (hm == wo)
-						v += s.va[m];
+						v += sm.u.v.va[m];
 					else if (hm + 1 == wo)
-						v += s.vg[m];
+						v += sm.u.v.vg[m];
 				}
 				if (wo < TBF_BLK) {
-					const float x = s.vin[wo];
-					s.vout[wo]    = G.vibMixed ? (x + v) * (float)0.7071067811865475 : v;
-					st.vring[slot] = 0.f;
+					const float x     = sm.vin[wo];
+					sm.u.v.vout[wo]   = G.vibMixed ? (x + v) * (float)0.7071067811865475 : v;
+					st.vring[slot]    = 0.f;
 				} else {
 					st.vring[slot] = v;
 				}
@@ -289,13 +333,13 @@ __device__ void stage_tonegen (const tbf_launch& P, Lds<W>& sm, const tbf_seg_ct
 				atomicOr (P.errFlags, 1u);
 				for (int n = 0; n < TBF_BLK; n++) {
 					const uint32_t op = (out0 + n) & 0x3FFu;
-					const int      h  = (int)((op + (uint32_t)(s.vh[n] - n)) & 0x3FFu);
+					const int      h  = (int)((op + (uint32_t)(sm.u.v.vh[n] - n)) & 0x3FFu);
 					const int      k2 = (h + 1) & 0x3FF;
-					st.vring[h & (TBF_VRING - 1)] += s.va[n];
-					st.vring[k2 & (TBF_VRING - 1)] += s.vg[n];
-					const float x = s.vin[n];
+					st.vring[h & (TBF_VRING - 1)] += sm.u.v.va[n];
+					st.vring[k2 & (TBF_VRING - 1)] += sm.u.v.vg[n];
+					const float x = sm.vin[n];
 					const float v = st.vring[op & (TBF_VRING - 1)];
-					s.vout[n]     = G.vibMixed ? (x + v) * (float)0.7071067811865475 : v;
+					sm.u.v.vout[n] = G.vibMixed ? (x + v) * (float)0.7071067811865475 : v;
 					st.vring[op & (TBF_VRING - 1)] = 0.f;
 				}
 			}
@@ -315,7 +359,7 @@ __device__ void stage_tonegen (const tbf_launch& P, Lds<W>& sm, const tbf_seg_ct
 		const bool  perc         = (routing & 0x0C) != 0;
 		const float dec          = G.percEnvGainDecay;
 		float       v            = lane == 0 ? st.keyCompLevel : st.percEnvGain;
-		float*      out          = lane == 0 ? s.kc : s.pe;
+		float*      out          = lane == 0 ? sm.u.v.kc : sm.u.v.pe;
 		for (int i0 = 0; i0 < TBF_BLK; i0 += 8) {
 			float o[8];
 #pragma unroll
@@ -337,48 +381,46 @@ __device__ void stage_tonegen (const tbf_launch& P, Lds<W>& sm, const tbf_seg_ct
 	__syncthreads ();
 	for (int k = 0; k < 2; k++) {
 		const int   n = lane + k * NL;
-		const float x = s.swl[n];
+		const float x = sm.swl[n];
 		float       y;
 		if (routing & 0x0C) {
 			/* HIPASS_PERCUSSION first difference, tonegen.cpp:3719-3731 */
-			const float p = (n == 0 ? st.pz : s.prc[n - 1]) - s.prc[n];
+			const float p = (n == 0 ? st.pz : sm.prc[n - 1]) - sm.prc[n];
 			if (routing & 0x03)
-				y = (G.outputGain * s.kc[n] * ((x + s.vout[n]) + (p * s.pe[n])));
+				y = (G.outputGain * sm.u.v.kc[n] * ((x + sm.u.v.vout[n]) + (p * sm.u.v.pe[n])));
 			else
-				y = (G.outputGain * s.kc[n] * (x + (p * s.pe[n])));
+				y = (G.outputGain * sm.u.v.kc[n] * (x + (p * sm.u.v.pe[n])));
 		} else if (routing & 0x03) {
-			y = (G.swellPedalGain * s.kc[n] * (x + s.vout[n]));
+			y = (G.swellPedalGain * sm.u.v.kc[n] * (x + sm.u.v.vout[n]));
 		} else {
-			y = (G.swellPedalGain * s.kc[n] * x);
+			y = (G.swellPedalGain * sm.u.v.kc[n] * x);
 		}
 		sm.bufA[n] = y;
 	}
 	__syncthreads ();
 	if (lane == 0 && (routing & 0x0C))
-		st.pz = s.prc[TBF_BLK - 1];
+		st.pz = sm.prc[TBF_BLK - 1];
 	__syncthreads ();
 	TBF_MARK (2);
 }
 
-/* ------------------------------------------------------------------ overdrive */
-template <int W>
-__device__ void stage_overdrive (const tbf_launch& P, Lds<W>& sm, const tbf_seg_ctl& G)
+/* preamp / airwindows_density, src/overdrive.cpp:60-170 (FP64) */
+__device__ void stage_overdrive (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl& G)
 {
-	const int       lane = threadIdx.x;
-	TgScratch&      s    = sm.u.tg;
-	tbf_inst_state& st   = sm.st;
+	const int     lane = threadIdx.x;
+	tbf_tg_state& st   = sm.st;
 	if (G.odClean) {
 		sm.bufB[lane]      = sm.bufA[lane];
 		sm.bufB[lane + NL] = sm.bufA[lane + NL];
 		__syncthreads ();
 		return;
 	}
-	/* src/overdrive.cpp:89-168; serial: xorshift sequence + alternating one-pole HPF */
+	/* serial: xorshift sequence + alternating one-pole HPF */
 	{
 		/* xorshift dither sequence F[0..128] on the scalar unit, written into lanes */
-		uint32_t f  = __builtin_amdgcn_readfirstlane (st.odFpd);
+		uint32_t       f  = __builtin_amdgcn_readfirstlane (st.odFpd);
 		const uint32_t f0 = f;
-		uint32_t lo = 0, hi = 0;
+		uint32_t       lo = 0, hi = 0;
 		for (int i = 0; i < NL; i++) {
 			f  = xorshift (f);
 			lo = (lane == i) ? f : lo;
@@ -387,11 +429,12 @@ __device__ void stage_overdrive (const tbf_launch& P, Lds<W>& sm, const tbf_seg_
 			f  = xorshift (f);
 			hi = (lane == i) ? f : hi;
 		}
-		s.fpd[lane + 1]      = lo;
-		s.fpd[lane + 1 + NL] = hi;
+		sm.u.od.fpd[lane + 1]      = lo;
+		sm.u.od.fpd[lane + 1 + NL] = hi;
+		__syncthreads (); /* all lanes have read st.odFpd */
 		if (lane == 0) {
-			s.fpd[0] = f0;
-			st.odFpd = f;
+			sm.u.od.fpd[0] = f0;
+			st.odFpd       = f;
 		}
 	}
 	__syncthreads ();
@@ -399,8 +442,8 @@ __device__ void stage_overdrive (const tbf_launch& P, Lds<W>& sm, const tbf_seg_
 		const int n = lane + k * NL;
 		double    x = (double)sm.bufA[n];
 		if (fabs (x) < 1.18e-23)
-			x = s.fpd[n] * 1.18e-17;
-		s.odx[n] = x;
+			x = sm.u.od.fpd[n] * 1.18e-17;
+		sm.u.od.odx[n] = x;
 	}
 	__syncthreads ();
 	if (lane < 2) {
@@ -413,11 +456,11 @@ __device__ void stage_overdrive (const tbf_launch& P, Lds<W>& sm, const tbf_seg_
 			double xv[8];
 #pragma unroll
 			for (int k = 0; k < 8; k++)
-				xv[k] = s.odx[start + 2 * (i0 + k)];
+				xv[k] = sm.u.od.odx[start + 2 * (i0 + k)];
 #pragma unroll
 			for (int k = 0; k < 8; k++) {
-				iir                           = (iir * (1.0 - a)) + (xv[k] * a);
-				s.odh[start + 2 * (i0 + k)] = xv[k] - iir;
+				iir                                = (iir * (1.0 - a)) + (xv[k] * a);
+				sm.u.od.odh[start + 2 * (i0 + k)] = xv[k] - iir;
 			}
 		}
 		if (lane == 0)
@@ -429,8 +472,8 @@ __device__ void stage_overdrive (const tbf_launch& P, Lds<W>& sm, const tbf_seg_
 	TBF_MARK (3);
 	for (int k = 0; k < 2; k++) {
 		const int n   = lane + k * NL;
-		double    x   = s.odh[n];
-		double    dry = s.odx[n];
+		double    x   = sm.u.od.odh[n];
+		double    dry = sm.u.od.odx[n];
 		double    br;
 		for (int c = 0; c < G.odIter; c++) {
 			br = fabs (x) * 1.57079633;
@@ -451,18 +494,59 @@ __device__ void stage_overdrive (const tbf_launch& P, Lds<W>& sm, const tbf_seg_
 			x *= G.odOutput;
 		if (G.odWet < 1.0)
 			x = (dry * G.odDry) + (x * G.odWet);
-		x = dither_add (x, s.fpd[n + 1]);
+		x = dither_add (x, sm.u.od.fpd[n + 1]);
 		sm.bufB[n] = (float)x;
 	}
 	__syncthreads ();
 	TBF_MARK (4);
 }
 
-/* ------------------------------------------------------------------ reverb */
+__global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL), amdgpu_waves_per_eu (TG_WAVES)))
+k_tonegen (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl, const tbf_tpl_desc* __restrict__ tpls,
+           const tbf_inst_const* __restrict__ cst)
+{
+	__shared__ TgLds sm;
+	const int      lane = threadIdx.x;
+	const uint32_t inst = blockIdx.x + P.instBase;
+	if (inst >= P.nInst)
+		return;
+	const tbf_seg_ctl&  G = ctl[inst];
+	const tbf_tpl_desc* T = tpls + cst[inst].tpl;
+	tbf_tg_state*       S = &P.st[inst].tg;
+	prof_begin (P, sm);
+	copy_words (&sm.st, S);
+	__syncthreads ();
+	for (uint32_t blk = 0; blk < P.nBlocks; blk++) {
+		stage_tonegen (P, sm, G, T);
+		if (P.chain == TBF_CHAIN_TONEGEN) {
+			float* oL = P.outL + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
+			float* oR = P.outR + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
+			oL[lane] = oR[lane] = sm.bufA[lane];
+			oL[lane + NL] = oR[lane + NL] = sm.bufA[lane + NL];
+			continue;
+		}
+		stage_overdrive (P, sm, G);
+		float* o = P.mid1 + (size_t)inst * P.midStride + (size_t)blk * TBF_BLK;
+		o[lane]      = sm.bufB[lane];
+		o[lane + NL] = sm.bufB[lane + NL];
+		if (P.chain == TBF_CHAIN_TAP_PREAMP) {
+			float* oL = P.outL + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
+			float* oR = P.outR + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
+			oL[lane] = oR[lane] = sm.bufB[lane];
+			oL[lane + NL] = oR[lane + NL] = sm.bufB[lane + NL];
+		}
+	}
+	__syncthreads ();
+	copy_words (S, &sm.st);
+	TBF_MARK (18);
+	prof_end (P, sm, inst);
+}
+
+/* ================================================================== k_reverb */
 
 /* Serial IIR chains of one sub-block on lanes 0..nch-1: lane j runs the biquad
- * coefficient set q[j] with state (s7, s8) over 64 samples of its LDS row, in place. */
-__device__ __forceinline__ void rv_chains (const tbf_inst_const& K, tbf_inst_state& st, double* row, int q, int c)
+ * coefficient set q with state (s7, s8) over 64 samples of its LDS row, in place. */
+__device__ __forceinline__ void rv_chains (const tbf_inst_const& K, tbf_rv_state& st, double* row, int q, int c)
 {
 	const double* cf = K.bq[q];
 	const double  c0 = cf[0], c1 = cf[1], c2 = cf[2], c3 = cf[3], c4 = cf[4];
@@ -488,66 +572,65 @@ __device__ __forceinline__ void rv_chains (const tbf_inst_const& K, tbf_inst_sta
 /* b_reverb::reverb (src/reverb.cpp:274-794), 64-sample sub-blocks, lane = sample.
  * All 13 rings are >= 560 samples long (the reference's fixed A..F settings), so every
  * ring read of a sub-block precedes the ring writes of that sub-block.  Serial parts:
- * the two dither sequences (lanes 0,1); biquadA (predelay output) and biquadB (tap mix)
- * of both channels together on lanes 0..3 -- their inputs are known once the reads are
- * done; biquadC on lanes 0,1. */
-template <int W>
-__device__ void stage_reverb (const tbf_launch& P, Lds<W>& sm, const tbf_seg_ctl& G, const tbf_inst_const& K,
-                              double* __restrict__ slab)
+ * the two dither sequences (scalar unit); biquadA (predelay output) and biquadB (tap
+ * mix) of both channels together on lanes 0..3 -- their inputs are known once the reads
+ * are done; biquadC on lanes 0,1. */
+__device__ void stage_reverb (const tbf_launch& P, RvLds& sm, const tbf_seg_ctl& G, const tbf_inst_const& K,
+                              double* __restrict__ slab, float* __restrict__ out)
 {
-	const int       lane = threadIdx.x;
-	RvScratch&      s    = sm.u.rv;
-	tbf_inst_state& st   = sm.st;
-	const double    wet  = G.rvWet;
+	const int     lane = threadIdx.x;
+	tbf_rv_state& st   = sm.st;
+	const double  wet  = G.rvWet;
 
 #pragma unroll 1
 	for (int sb = 0; sb < TBF_BLK / TBF_SUB; sb++) {
 		const int n = lane; /* sample within the sub-block */
 		/* dither sequences (src/reverb.cpp:775-783) on the scalar unit, into lanes */
 		{
-			uint32_t fL = __builtin_amdgcn_readfirstlane (st.fpdL);
-			uint32_t fR = __builtin_amdgcn_readfirstlane (st.fpdR);
+			uint32_t       fL = __builtin_amdgcn_readfirstlane (st.fpdL);
+			uint32_t       fR = __builtin_amdgcn_readfirstlane (st.fpdR);
 			const uint32_t gL = fL, gR = fR;
-			uint32_t nL = 0, nR = 0;
+			uint32_t       nL = 0, nR = 0;
 			for (int i = 0; i < TBF_SUB; i++) {
 				fL = xorshift (fL);
 				fR = xorshift (fR);
 				nL = (lane == i) ? fL : nL;
 				nR = (lane == i) ? fR : nR;
 			}
-			s.fpd[0][lane + 1] = nL;
-			s.fpd[1][lane + 1] = nR;
+			sm.fpd[0][lane + 1] = nL;
+			sm.fpd[1][lane + 1] = nR;
 			__syncthreads (); /* all lanes have read st.fpdL/R */
 			if (lane == 0) {
-				s.fpd[0][0] = gL;
-				s.fpd[1][0] = gR;
-				st.fpdL     = fL;
-				st.fpdR     = fR;
+				sm.fpd[0][0] = gL;
+				sm.fpd[1][0] = gR;
+				st.fpdL      = fL;
+				st.fpdR      = fR;
 			}
 		}
 		TBF_MARK (5);
-		const double inS = (double)sm.bufB[sb * TBF_SUB + n];
+		const double inS = (double)sm.in[sb * TBF_SUB + n];
 		/* ---- predelay M (line 12) ---- */
 		const int dM  = K.delay[12];
 		const int cMn = cnt_adv (st.count[12], dM, n);     /* write slot */
 		const int cMr = cnt_adv (st.count[12], dM, n + 1); /* read slot  */
 		double*   mL  = slab + K.ringOff[12];
 		double*   mR  = slab + K.ringOff[13 + 12];
-		s.a[0][n]     = mL[cMr];
-		s.a[1][n]     = mR[cMr];
+		sm.a[0][n]    = mL[cMr];
+		sm.a[1][n]    = mR[cMr];
 		/* ---- allpass reads (lines 8..11) ---- */
 		double apOld[2][4];
 		int    apW[4];
 		for (int l = 8; l < 12; l++) {
-			const int d  = K.delay[l];
-			const int cr = cnt_adv (st.count[l], d, n + 1);
-			apW[l - 8]   = cnt_adv (st.count[l], d, n);
+			const int d     = K.delay[l];
+			const int cr    = cnt_adv (st.count[l], d, n + 1);
+			apW[l - 8]      = cnt_adv (st.count[l], d, n);
 			apOld[0][l - 8] = slab[K.ringOff[l] + cr];
 			apOld[1][l - 8] = slab[K.ringOff[13 + l] + cr];
 		}
 		/* ---- delay-line taps (lines 0..7) with the vibrato offsets; Householder
 		 * feedback and tap mix (src/reverb.cpp:479-560, 686-724) ---- */
 		double fb[2][8];
+#pragma unroll
 		for (int c = 0; c < 2; c++) {
 			/* pass 1: vibrato phases and offsets (one sin per line) -> LDS */
 #pragma unroll 1
@@ -561,31 +644,27 @@ __device__ void stage_reverb (const tbf_launch& P, Lds<W>& sm, const tbf_seg_ctl
 					for (int i = 0; i <= n; i++)
 						v += dl;
 				}
-				s.t[l][n] = (sin (v) + 1.0) * K.vibDepth;
+				sm.t[l][n] = (sin (v) + 1.0) * K.vibDepth;
 				if (n == TBF_SUB - 1)
-					s.vn[c][l] = v;
+					sm.vn[c][l] = v;
 			}
-			/* pass 2: all 16 tap loads of the channel in flight together */
-			double r0[8], r1[8], fr[8];
+			/* pass 2: the 16 two-tap reads of the channel and their interpolation */
+			double I[8];
 #pragma unroll
 			for (int l = 0; l < 8; l++) {
 				const int     d   = K.delay[l];
 				const int     cn  = cnt_adv (st.count[l], d, n + 1);
-				const double  off = s.t[l][n];
+				const double  off = sm.t[l][n];
 				const int     wk  = (int)(cn + off);
 				const int     w0  = wk - ((wk > d) ? d + 1 : 0);
 				const int     w1  = wk + 1 - ((wk + 1 > d) ? d + 1 : 0);
 				const double* a   = slab + K.ringOff[c * 13 + l];
-				fr[l]             = off - floor (off);
-				r0[l]             = a[w0];
-				r1[l]             = a[w1];
-			}
-			double I[8];
-#pragma unroll
-			for (int l = 0; l < 8; l++) {
-				double x = (r0[l] * (1 - fr[l]));
-				x += (r1[l] * fr[l]);
-				I[l] = ((1.0 - K.blend) * x) + (r0[l] * K.blend);
+				const double  fr  = off - floor (off);
+				const double  r0  = a[w0];
+				const double  r1  = a[w1];
+				double        x   = (r0 * (1 - fr));
+				x += (r1 * fr);
+				I[l] = ((1.0 - K.blend) * x) + (r0 * K.blend);
 			}
 			I[0]     = (I[0] * K.oneMinusAbsCm) + (I[4] * K.crossmod);
 			I[4]     = (I[4] * K.oneMinusAbsCm) + (I[0] * K.crossmod);
@@ -597,27 +676,29 @@ __device__ void stage_reverb (const tbf_launch& P, Lds<W>& sm, const tbf_seg_ctl
 			fb[c][5] = (I[5] - (I[4] + I[6] + I[7])) * K.regen;
 			fb[c][6] = (I[6] - (I[4] + I[5] + I[7])) * K.regen;
 			fb[c][7] = (I[7] - (I[4] + I[5] + I[6])) * K.regen;
-			s.b[c][n] = (I[0] + I[1] + I[2] + I[3] + I[4] + I[5] + I[6] + I[7]) / 8.0;
+			sm.b[c][n] = (I[0] + I[1] + I[2] + I[3] + I[4] + I[5] + I[6] + I[7]) / 8.0;
 		}
 		TBF_MARK (6);
 		__syncthreads (); /* all ring reads of the sub-block are complete */
 		if (lane < 16)
-			st.vib[lane >> 3][lane & 7] = s.vn[lane >> 3][lane & 7];
+			st.vib[lane >> 3][lane & 7] = sm.vn[lane >> 3][lane & 7];
+#pragma unroll
 		for (int c = 0; c < 2; c++) {
 			double x = inS;
 			if (fabs (x) < 1.18e-23)
-				x = s.fpd[c][n] * 1.18e-17;
+				x = sm.fpd[c][n] * 1.18e-17;
 			(c ? mR : mL)[cMn] = x;
 		}
 		/* ---- biquadA (predelay out) and biquadB (tap mix), both channels, lanes 0..3 ---- */
 		if (lane < 4)
-			rv_chains (K, st, lane < 2 ? s.a[lane] : s.b[lane - 2], lane >> 1, lane & 1);
+			rv_chains (K, st, lane < 2 ? sm.a[lane] : sm.b[lane - 2], lane >> 1, lane & 1);
 		__syncthreads ();
 		TBF_MARK (7);
 		/* ---- allpasses and delay-line writes; clamp + asin of the biquadB output ---- */
 		static const int srcAp[8] = {3, 2, 1, 0, 0, 1, 2, 3};
+#pragma unroll
 		for (int c = 0; c < 2; c++) {
-			const double a0 = sin (s.a[c][n] * wet);
+			const double a0 = sin (sm.a[c][n] * wet);
 			double       ap[4];
 			for (int l = 0; l < 4; l++) {
 				double a = a0;
@@ -633,34 +714,35 @@ __device__ void stage_reverb (const tbf_launch& P, Lds<W>& sm, const tbf_seg_ctl
 					prev = st.fb[c][l];
 				slab[K.ringOff[c * 13 + l] + cnt_adv (st.count[l], K.delay[l], n)] = ap[srcAp[l]] + prev;
 				if (lane == NL - 1)
-					s.fbn[c][l] = fb[c][l];
+					sm.fbn[c][l] = fb[c][l];
 			}
-			double y = s.b[c][n];
+			double y = sm.b[c][n];
 			if (y > 1.0) y = 1.0;
 			if (y < -1.0) y = -1.0;
-			s.b[c][n] = asin (y);
+			sm.b[c][n] = asin (y);
 		}
 		__syncthreads ();
 		if (lane < 16)
-			st.fb[lane >> 3][lane & 7] = s.fbn[lane >> 3][lane & 7];
+			st.fb[lane >> 3][lane & 7] = sm.fbn[lane >> 3][lane & 7];
 		TBF_MARK (8);
 		/* ---- biquadC, lanes 0,1 ---- */
 		if (lane < 2)
-			rv_chains (K, st, s.b[lane], 2, lane);
+			rv_chains (K, st, sm.b[lane], 2, lane);
 		__syncthreads ();
 		TBF_MARK (9);
 		double o[2];
+#pragma unroll
 		for (int c = 0; c < 2; c++) {
-			double x = s.b[c][n];
+			double x = sm.b[c][n];
 			if (wet != 1.0) {
 				double dry = inS;
 				if (fabs (dry) < 1.18e-23)
-					dry = s.fpd[c][n] * 1.18e-17;
+					dry = sm.fpd[c][n] * 1.18e-17;
 				x += (dry * (1.0 - wet));
 			}
-			o[c] = dither_add (x, s.fpd[c][n + 1]);
+			o[c] = dither_add (x, sm.fpd[c][n + 1]);
 		}
-		sm.bufC[sb * TBF_SUB + n] = (float)(0.7071067811865476 * (o[0] + o[1]));
+		out[sb * TBF_SUB + n] = (float)(0.7071067811865476 * (o[0] + o[1]));
 		__syncthreads ();
 		if (lane < 13)
 			st.count[lane] = cnt_adv (st.count[lane], K.delay[lane], TBF_SUB);
@@ -669,8 +751,43 @@ __device__ void stage_reverb (const tbf_launch& P, Lds<W>& sm, const tbf_seg_ctl
 	}
 }
 
-/* ------------------------------------------------------------------ whirl */
-__device__ void whirl_speed (tbf_inst_state& st, const tbf_inst_const& K, int revOpt, int& brake)
+__global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL), amdgpu_waves_per_eu (RV_WAVES)))
+k_reverb (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_seg_ctl* __restrict__ ctl)
+{
+	__shared__ RvLds sm;
+	const int      lane = threadIdx.x;
+	const uint32_t inst = blockIdx.x + P.instBase;
+	if (inst >= P.nInst)
+		return;
+	const tbf_inst_const& K    = cst[inst];
+	const tbf_seg_ctl&    G    = ctl[inst];
+	tbf_rv_state*         S    = &P.st[inst].rv;
+	double*               slab = P.rslab + (size_t)inst * P.slabLen;
+	prof_begin (P, sm);
+	copy_words (&sm.st, S);
+	__syncthreads ();
+	for (uint32_t blk = 0; blk < P.nBlocks; blk++) {
+		const float* in = P.mid1 + (size_t)inst * P.midStride + (size_t)blk * TBF_BLK;
+		sm.in[lane]      = in[lane];
+		sm.in[lane + NL] = in[lane + NL];
+		__syncthreads ();
+		float* out = P.chain == TBF_CHAIN_TAP_REVERB
+		                 ? P.outL + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK
+		                 : P.mid2 + (size_t)inst * P.midStride + (size_t)blk * TBF_BLK;
+		stage_reverb (P, sm, G, K, slab, out);
+		if (P.chain == TBF_CHAIN_TAP_REVERB) {
+			float* oR = P.outR + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
+			oR[lane]      = out[lane];
+			oR[lane + NL] = out[lane + NL];
+		}
+	}
+	__syncthreads ();
+	copy_words (S, &sm.st);
+	prof_end (P, sm, inst);
+}
+
+/* ================================================================== k_whirl */
+__device__ void whirl_speed (tbf_wh_state& st, const tbf_inst_const& K, int revOpt, int& brake)
 {
 	/* useRevOption (src/whirl.cpp:174-196) for an event landing before this block */
 	if (revOpt >= 0) {
@@ -766,99 +883,71 @@ __device__ void whirl_speed (tbf_inst_state& st, const tbf_inst_const& K, int re
 	}
 }
 
-
-/* Ordered ring accumulation of one 64-sample sub-block (HN_MOTION / DR_MOTION adds,
- * src/whirl.cpp:1432-1469).  The reference adds, sample by sample and motion by motion
- * in source order, a into slot U and b into slot U+1.  Per slot this is a sequence of
- * float adds whose order must be kept; it is rebuilt lane-parallel:
- *   - a motion's slot U_n is non-decreasing in n with steps 0..2 and stays within 2 of
- *     U_0 + n, so slot t receives its a/b terms from samples n in [t-U_0-4, t-U_0+3],
- *     in sample order;
- *   - inside one ring the motion with the larger spacing is >= 2 slots ahead of the
- *     next at every sample, so every slot it shares with that motion got that motion's
- *     terms from earlier samples: running the motions as passes, farthest first,
- *     reproduces the per-slot order.
- * Both properties are checked per ring and sub-block (wave vote); when either fails the
- * serial replay runs instead, so the result is bit-identical in all cases.  s.mu/ma/mb
- * hold the ring's three motions in source order (q = 0, 1, 2 -> motion (r&1) + 2q). */
+/* One motion's ordered adds into a ring for a 64-sample sub-block (HN_MOTION /
+ * DR_MOTION, src/whirl.cpp:1432-1469): sample n adds a_n into slot U_n and b_n into
+ * slot U_n + 1, in sample order.  With U non-decreasing, the samples sharing a slot
+ * value form a group G(u) and slot t receives, in order, b of G(t-1) then a of G(t).
+ * Groups have at most 2 samples (checked by the caller), so the first lane of each
+ * group owns slot t = U (and slot t + 1 when no group sits at t + 1) and finds its
+ * neighbours' terms with lane shifts; owners never share a slot. */
 template <int W>
-__device__ void ring_accumulate (float* ring, WhScratch& s, int lane)
+__device__ __forceinline__ void motion_add (float* ring, int U, float a, float b, int lane)
 {
-	const uint32_t WM = (uint32_t)W - 1u;
-	int ok = 1;
-	for (int q = 0; q < 3; q++) {
-		const int u  = s.mu[q][lane];
-		const int u0 = s.mu[q][0];
-		const int up = lane ? s.mu[q][lane - 1] : u;
-		const int dv = u - u0 - lane;
-		if (u - up < 0 || u - up > 2 || dv < -2 || dv > 2)
-			ok = 0;
-		if (q < 2 && u + 2 > s.mu[q + 1][lane])
-			ok = 0;
-	}
-	if (__all (ok)) {
-		for (int q = 2; q >= 0; q--) { /* farthest motion first */
-			const int u0 = s.mu[q][0];
-			const int ns = s.mu[q][TBF_SUB - 1] + 2 - u0; /* slots u0 .. U_63+1 (<= 67) */
-			for (int o = lane; o < ns; o += NL) {
-				/* slot t = u0 + o takes terms from samples o-3 .. o+2 (|U_m - u0 - m| <= 2) */
-				const int t = u0 + o;
-				int       um[6];
-				float     ta[6], tb[6];
-#pragma unroll
-				for (int j = 0; j < 6; j++) {
-					const int m  = o - 3 + j;
-					const int mc = m < 0 ? 0 : (m > TBF_SUB - 1 ? TBF_SUB - 1 : m);
-					um[j]        = (m == mc) ? s.mu[q][mc] : INT32_MIN;
-					ta[j]        = s.ma[q][mc];
-					tb[j]        = s.mb[q][mc];
-				}
-				float v = ring[(uint32_t)t & WM];
-#pragma unroll
-				for (int j = 0; j < 6; j++) {
-					if (um[j] == t - 1)
-						v += tb[j];
-					else if (um[j] == t)
-						v += ta[j];
-				}
-				ring[(uint32_t)t & WM] = v;
-			}
-			__syncthreads ();
+	const uint32_t WM  = (uint32_t)W - 1u;
+	const int      Up  = __shfl_up (U, 1);
+	const int      Up2 = __shfl_up (U, 2);
+	const int      Un  = __shfl_down (U, 1);
+	const int      Un2 = __shfl_down (U, 2);
+	const float    bp1 = __shfl_up (b, 1);
+	const float    bp2 = __shfl_up (b, 2);
+	const float    an  = __shfl_down (a, 1);
+	const float    bn  = __shfl_down (b, 1);
+	const bool     first = lane == 0 || U != Up;
+	if (first) {
+		const bool     pair = lane < NL - 1 && Un == U;
+		const uint32_t t    = (uint32_t)U;
+		float          v    = ring[t & WM];
+		if (lane > 0 && Up == U - 1) {
+			if (lane > 1 && Up2 == Up)
+				v += bp2;
+			v += bp1;
 		}
-	} else {
-		/* serial replay in the reference order: sample-major, motions in source order */
-		if (lane == 0) {
-			for (int i = 0; i < TBF_SUB; i++) {
-				for (int q = 0; q < 3; q++) {
-					const uint32_t sl = (uint32_t)s.mu[q][i] & WM;
-					ring[sl] += s.ma[q][i];
-					ring[(sl + 1) & WM] += s.mb[q][i];
-				}
-			}
+		v += a;
+		if (pair)
+			v += an;
+		ring[t & WM] = v;
+		const bool nextExists = pair ? lane < NL - 2 : lane < NL - 1;
+		const int  Unx        = pair ? Un2 : Un;
+		if (!nextExists || Unx != U + 1) {
+			float w = ring[(t + 1) & WM];
+			w += b;
+			if (pair)
+				w += bn;
+			ring[(t + 1) & WM] = w;
 		}
-		__syncthreads ();
 	}
 }
 
+/* whirlProc2 (src/whirl.cpp:1191-1638) + whirlProc3 mic mix (1653-1681) */
 template <int W>
-__device__ void stage_whirl (const tbf_launch& P, Lds<W>& sm, const tbf_seg_ctl& G, const tbf_inst_const& K,
-                             int firstBlock, float* __restrict__ oL, float* __restrict__ oR)
+__device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ctl& G, const tbf_inst_const& K,
+                             int firstBlock, const float* __restrict__ in, float* __restrict__ oL,
+                             float* __restrict__ oR)
 {
-	const int       lane = threadIdx.x;
-	WhScratch&      s    = sm.u.wh;
-	tbf_inst_state& st   = sm.st;
-	const float*    hnFwd = P.whTab;
-	const float*    hnBwd = P.whTab + 16384;
-	const float*    drFwd = P.whTab + 2 * 16384;
-	const float*    drBwd = P.whTab + 3 * 16384;
-	const float*    bfw   = P.whBw;
-	const float*    bbw   = P.whBw + 16384 * 5;
+	const int     lane  = threadIdx.x;
+	tbf_wh_state& st    = sm.st;
+	const float*  hnFwd = P.whTab;
+	const float*  hnBwd = P.whTab + 16384;
+	const float*  drFwd = P.whTab + 2 * 16384;
+	const float*  drBwd = P.whTab + 3 * 16384;
+	const float*  bfw   = P.whBw;
+	const float*  bbw   = P.whBw + 16384 * 5;
 
 	if (G.whBypass) {
 		/* whirlProc2 bypass (src/whirl.cpp:1197-1215) + whirlProc3 mix */
 		for (int k = 0; k < 2; k++) {
 			const int   n = lane + k * NL;
-			const float x = sm.bufC[n];
+			const float x = in[n];
 			oL[n] = x * K.mic[0] + x * K.mic[1] + 0.f * K.mic[2] + 0.f * K.mic[3];
 			oR[n] = x * K.mic[4] + x * K.mic[5] + 0.f * K.mic[6] + 0.f * K.mic[7];
 		}
@@ -871,60 +960,62 @@ __device__ void stage_whirl (const tbf_launch& P, Lds<W>& sm, const tbf_seg_ctl&
 	}
 	__syncthreads ();
 	TBF_MARK (11);
-	const double hornIncr = st.hornIncr, drumIncr = st.drumIncr;
-	const uint32_t WM     = (uint32_t)W - 1u;
+	const double   hornIncr = st.hornIncr, drumIncr = st.drumIncr;
+	const uint32_t WM       = (uint32_t)W - 1u;
+	/* serial filter coefficients: lane 0 horn A, lanes 1-2 drum shelf */
+	const float* cfa = lane == 0 ? K.hafw : K.drf;
+	const float  fa0 = cfa[0], fa1 = cfa[1], fa2 = cfa[2], fa3 = cfa[3], fa4 = cfa[4];
+	const float  hb0 = K.hbfw[0], hb1 = K.hbfw[1], hb2 = K.hbfw[2], hb3 = K.hbfw[3], hb4 = K.hbfw[4];
 
 #pragma unroll 1
 	for (int sb = 0; sb < TBF_BLK / TBF_SUB; sb++) {
 		const int      n      = lane;
 		const uint32_t outpos = (st.outpos + (uint32_t)n) & 2047u;
 		const int32_t  unwrap = (int32_t)(st.outpos + (uint32_t)n - outpos); /* 0 or 2048 */
-		const float    xin    = (float)((double)sm.bufC[sb * TBF_SUB + n] + 1e-14);
-		s.xx[n + 1]           = xin;
+		const float    xin    = (float)((double)in[sb * TBF_SUB + n] + 1e-14);
+		sm.xx[n + 1]          = xin;
 		if (lane == 0)
-			s.xx[0] = st.z[2];
-		__syncthreads ();
+			sm.xx[0] = st.z[2];
 		/* ring reads + clear at outpos: before this sub-block's writes, which land >= 79
 		 * slots ahead (src/whirl.cpp:1585-1600) */
 		const uint32_t o   = outpos & WM;
 		const float    hlv = sm.wring[0][o], hrv = sm.wring[1][o];
-		s.rd[0][n]         = sm.wring[2][o];
-		s.rd[1][n]         = sm.wring[3][o];
+		sm.rd[0][n]        = sm.wring[2][o];
+		sm.rd[1][n]        = sm.wring[3][o];
 		sm.wring[0][o]     = 0.f;
 		sm.wring[1][o]     = 0.f;
 		sm.wring[2][o]     = 0.f;
 		sm.wring[3][o]     = 0.f;
 		if (lane < 4) {
 			const int i = lane;
-			s.xf[i] = st.adx[0][(st.adi[0] + 3 - i) & 7];
-			s.x1[i] = st.adx[1][(st.adi[1] + 3 - i) & 7];
-			s.x2[i] = st.adx[2][(st.adi[2] + 3 - i) & 7];
+			sm.xf[i] = st.adx[0][(st.adi[0] + 3 - i) & 7];
+			sm.x1[i] = st.adx[1][(st.adi[1] + 3 - i) & 7];
+			sm.x2[i] = st.adx[2][(st.adi[2] + 3 - i) & 7];
 		}
 		__syncthreads ();
 		/* independent serial biquads as lane chains: lane 0 horn filter A (hafw), lanes
-		 * 1, 2 drum shelves (drfL, drfR); then lane 0 horn filter B (hbfw) while lanes 1, 2
-		 * step the rotor angles */
+		 * 1, 2 drum shelves (drfL, drfR, in place on rd); then lane 0 horn filter B
+		 * (hbfw) while lanes 1, 2 step the rotor angles */
 		if (lane < 3) {
-			const float* c  = lane == 0 ? K.hafw : K.drf;
 			const int    fi = lane == 0 ? 0 : lane + 1;
-			const float* in = lane == 0 ? s.xx + 1 : s.rd[lane - 1];
-			float*       ou = lane == 0 ? s.xf + 4 : s.y[lane - 1];
+			const float* ip = lane == 0 ? sm.xx + 1 : sm.rd[lane - 1];
+			float*       ou = lane == 0 ? sm.xf + 4 : sm.rd[lane - 1];
 			float        z0 = st.fz[fi][0], z1 = st.fz[fi][1];
 			for (int i0 = 0; i0 < TBF_SUB; i0 += 8) {
 				float xv[8];
 #pragma unroll
 				for (int k = 0; k < 8; k++)
-					xv[k] = in[i0 + k];
+					xv[k] = ip[i0 + k];
 #pragma unroll
 				for (int k = 0; k < 8; k++)
-					ou[i0 + k] = eq_iir (c, z0, z1, xv[k]);
+					ou[i0 + k] = eq_iir (fa0, fa1, fa2, fa3, fa4, z0, z1, xv[k]);
 			}
 			st.fz[fi][0] = z0;
 			st.fz[fi][1] = z1;
 		}
 		if (lane == 0) {
 			float  z0 = st.fz[1][0], z1 = st.fz[1][1];
-			float* io = s.xf + 4;
+			float* io = sm.xf + 4;
 			for (int i0 = 0; i0 < TBF_SUB; i0 += 8) {
 				float xv[8];
 #pragma unroll
@@ -932,7 +1023,7 @@ __device__ void stage_whirl (const tbf_launch& P, Lds<W>& sm, const tbf_seg_ctl&
 					xv[k] = io[i0 + k];
 #pragma unroll
 				for (int k = 0; k < 8; k++)
-					io[i0 + k] = eq_iir (K.hbfw, z0, z1, xv[k]);
+					io[i0 + k] = eq_iir (hb0, hb1, hb2, hb3, hb4, z0, z1, xv[k]);
 			}
 			st.fz[1][0] = z0;
 			st.fz[1][1] = z1;
@@ -948,88 +1039,129 @@ __device__ void stage_whirl (const tbf_launch& P, Lds<W>& sm, const tbf_seg_ctl&
 				}
 #pragma unroll
 				for (int k = 0; k < 8; k++)
-					s.ang[lane - 1][i0 + k] = av[k];
+					sm.ang[lane - 1][i0 + k] = av[k];
 			}
-			if (lane == 1) st.hornAngle = a; else st.drumAngle = a;
+			if (lane == 1)
+				st.hornAngle = a;
+			else
+				st.drumAngle = a;
 		}
 		__syncthreads ();
 		TBF_MARK (12);
 		/* reflection filters FILTER_C (src/whirl.cpp:1472-1477), lane-parallel */
-		const float xf   = s.xf[n + 4];
-		const float xfp  = n == 0 ? st.z[0] : s.xf[n + 3];
+		const float xf   = sm.xf[n + 4];
+		const float xfp  = n == 0 ? st.z[0] : sm.xf[n + 3];
 		const float x1v  = (float)((0.4 * xf) + (0.4 * xfp));
-		s.x1[n + 4]      = x1v;
-		const float xdp  = s.xx[n];
+		sm.x1[n + 4]     = x1v;
+		const float xdp  = sm.xx[n];
 		const float xd1v = (float)((0.4 * xin) + (0.4 * xdp));
-		s.xd1[n + 1]     = xd1v;
+		sm.xd1[n + 1]    = xd1v;
 		if (lane == 0)
-			s.xd1[0] = st.z[3];
+			sm.xd1[0] = st.z[3];
 		__syncthreads ();
-		const float x1p  = n == 0 ? st.z[1] : s.x1[n + 3];
+		const float x1p  = n == 0 ? st.z[1] : sm.x1[n + 3];
 		const float x2v  = (float)((0.4 * x1v) + (0.4 * x1p));
-		s.x2[n + 4]      = x2v;
-		const float xd2v = (float)((0.4 * xd1v) + (0.4 * s.xd1[n]));
+		sm.x2[n + 4]     = x2v;
+		const float xd2v = (float)((0.4 * xd1v) + (0.4 * sm.xd1[n]));
 		__syncthreads ();
-
 		TBF_MARK (13);
-		TBF_MARK (14);
+
 		/* ---- per ring (HL, HR, DL, DR): its three motions, then the ordered adds ---- */
-		const double ha = s.ang[0][n];
-		const double da = s.ang[1][n];
+		const double ha = sm.ang[0][n];
+		const double da = sm.ang[1][n];
 #pragma unroll 1
 		for (int r = 0; r < 4; r++) {
+			int   mu[3];
+			float ma[3], mb[3];
+#pragma unroll
 			for (int q = 0; q < 3; q++) {
-				const int p = (r & 1) + 2 * q;
+				const int  p   = (r & 1) + 2 * q;
 				const bool fwd = (p == 0 || p == 3 || p == 4);
-				float xa, t;
+				float      xa, t;
 				if (r < 2) {
 					/* HN_MOTION, src/whirl.cpp:1432-1453 */
-					const float*  hist = p < 2 ? s.xf : (p < 4 ? s.x1 : s.x2);
-					const float*  dsp  = fwd ? hnFwd : hnBwd;
-					const float*  bw   = fwd ? bbw : bfw;
-					const double  ang  = ha + ((p & 1) ? K.bwAng : K.fwAng);
-					const float   h1   = (float)(ang * (unsigned int)16384 + K.hornPhase[p]);
-					const float   hd   = frac1 (h1);
-					const unsigned hl  = ((unsigned int)floorf (h1)) & 16383u;
-					const unsigned hh  = (hl + 1) & 16383u;
-					const float   intp = dsp[hl] * (1.f - hd) + hd * dsp[hh];
-					const unsigned kk  = ((unsigned int)roundf (h1)) & 16383u;
-					t                  = K.hornSpacing[p] + intp + (float)outpos;
-					const float*  b    = bw + 5 * kk;
-					xa                 = b[0] * hist[n + 4];
+					const float*   hist = p < 2 ? sm.xf : (p < 4 ? sm.x1 : sm.x2);
+					const float*   dsp  = fwd ? hnFwd : hnBwd;
+					const float*   bw   = fwd ? bbw : bfw;
+					const double   ang  = ha + ((p & 1) ? K.bwAng : K.fwAng);
+					const float    h1   = (float)(ang * (unsigned int)16384 + K.hornPhase[p]);
+					const float    hd   = frac1 (h1);
+					const unsigned hl   = ((unsigned int)floorf (h1)) & 16383u;
+					const unsigned hh   = (hl + 1) & 16383u;
+					const float    intp = dsp[hl] * (1.f - hd) + hd * dsp[hh];
+					const unsigned kk   = ((unsigned int)roundf (h1)) & 16383u;
+					t                   = K.hornSpacing[p] + intp + (float)outpos;
+					const float* b      = bw + 5 * kk;
+					xa                  = b[0] * hist[n + 4];
 					xa += b[1] * hist[n + 3];
 					xa += b[2] * hist[n + 2];
 					xa += b[3] * hist[n + 1];
 					xa += b[4] * hist[n + 0];
 				} else {
 					/* DR_MOTION, src/whirl.cpp:1455-1469 */
-					xa                = p < 2 ? xin : (p < 4 ? xd1v : xd2v);
-					const float* dsp  = fwd ? drFwd : drBwd;
-					const float  d1   = (float)(da * (unsigned int)16384 + K.hornPhase[p]);
-					const float  dd   = frac1 (d1);
-					const unsigned dl = ((unsigned int)floorf (d1)) & 16383u;
-					const unsigned dh = (dl + 1) & 16383u;
-					const float  intp = dsp[dl] * (1.f - dd) + dd * dsp[dh];
-					t                 = K.drumSpacing[p] + intp + (float)outpos;
+					xa                  = p < 2 ? xin : (p < 4 ? xd1v : xd2v);
+					const float*   dsp  = fwd ? drFwd : drBwd;
+					const float    d1   = (float)(da * (unsigned int)16384 + K.hornPhase[p]);
+					const float    dd   = frac1 (d1);
+					const unsigned dl   = ((unsigned int)floorf (d1)) & 16383u;
+					const unsigned dh   = (dl + 1) & 16383u;
+					const float    intp = dsp[dl] * (1.f - dd) + dd * dsp[dh];
+					t                   = K.drumSpacing[p] + intp + (float)outpos;
 				}
 				const float rr = floorf (t);
 				const float qq = xa * (t - rr);
-				s.mu[q][n]     = (int32_t)((unsigned int)rr) + unwrap;
-				s.ma[q][n]     = xa - qq;
-				s.mb[q][n]     = qq;
+				mu[q]          = (int32_t)((unsigned int)rr) + unwrap;
+				ma[q]          = xa - qq;
+				mb[q]          = qq;
 			}
-			__syncthreads ();
+			TBF_MARK (14);
+			/* fast path preconditions (wave vote): each motion's slot non-decreasing in n
+			 * with groups of <= 2 equal slots, and the ring's motions >= 2 slots apart in
+			 * source order at every sample (so passes farthest-first keep the per-slot
+			 * order: a farther motion reaches a slot only at earlier samples) */
+			int ok = (mu[1] >= mu[0] + 2) && (mu[2] >= mu[1] + 2);
+#pragma unroll
+			for (int q = 0; q < 3; q++) {
+				const int up = __shfl_up (mu[q], 1);
+				const int un = __shfl_down (mu[q], 1);
+				if (lane > 0 && mu[q] < up)
+					ok = 0;
+				if (lane > 0 && lane < NL - 1 && up == mu[q] && un == mu[q])
+					ok = 0;
+			}
+			float* ring = sm.wring[r];
+			if (__all (ok)) {
+				motion_add<W> (ring, mu[2], ma[2], mb[2], lane);
+				__syncthreads ();
+				motion_add<W> (ring, mu[1], ma[1], mb[1], lane);
+				__syncthreads ();
+				motion_add<W> (ring, mu[0], ma[0], mb[0], lane);
+				__syncthreads ();
+			} else {
+				/* serial replay in the reference order: sample-major, motions in source order */
+				for (int i = 0; i < TBF_SUB; i++) {
+#pragma unroll
+					for (int q = 0; q < 3; q++) {
+						const uint32_t sl = (uint32_t)__shfl (mu[q], i) & WM;
+						const float    aa = __shfl (ma[q], i);
+						const float    bb = __shfl (mb[q], i);
+						if (lane == 0) {
+							ring[sl] += aa;
+							ring[(sl + 1) & WM] += bb;
+						}
+					}
+				}
+				__syncthreads ();
+			}
 			TBF_MARK (15);
-			ring_accumulate<W> (sm.wring[r], s, lane);
-			TBF_MARK (16);
 		}
 		/* ---- outputs (whirlProc2 outHL/outHR/outDL/outDR + whirlProc3 mix) ---- */
 		{
 			const float leak = xf * K.leakage;
 			const float hL   = K.hornLevel * hlv + leak;
 			const float hR   = K.hornLevel * hrv + leak;
-			const float dL   = s.y[0][n];
-			const float dR   = s.y[1][n];
+			const float dL   = sm.rd[0][n];
+			const float dR   = sm.rd[1][n];
 			oL[sb * TBF_SUB + n] = hL * K.mic[0] + hR * K.mic[1] + dL * K.mic[2] + dR * K.mic[3];
 			oR[sb * TBF_SUB + n] = hL * K.mic[4] + hR * K.mic[5] + dL * K.mic[6] + dR * K.mic[7];
 		}
@@ -1043,14 +1175,14 @@ __device__ void stage_whirl (const tbf_launch& P, Lds<W>& sm, const tbf_seg_ctl&
 		__syncthreads ();
 		if (lane == 0) {
 			for (int j = 0; j < 8; j++) {
-				st.adx[0][(st.adi[0] + j) & 7] = s.xf[4 + TBF_SUB - 1 - j];
-				st.adx[1][(st.adi[1] + j) & 7] = s.x1[4 + TBF_SUB - 1 - j];
-				st.adx[2][(st.adi[2] + j) & 7] = s.x2[4 + TBF_SUB - 1 - j];
+				st.adx[0][(st.adi[0] + j) & 7] = sm.xf[4 + TBF_SUB - 1 - j];
+				st.adx[1][(st.adi[1] + j) & 7] = sm.x1[4 + TBF_SUB - 1 - j];
+				st.adx[2][(st.adi[2] + j) & 7] = sm.x2[4 + TBF_SUB - 1 - j];
 			}
 			st.outpos = (st.outpos + TBF_SUB) & 2047u;
 		}
 		__syncthreads ();
-		TBF_MARK (17);
+		TBF_MARK (16);
 	}
 	if (lane == 0) {
 		/* NaN scrub, src/whirl.cpp:1622-1630 */
@@ -1067,93 +1199,56 @@ __device__ void stage_whirl (const tbf_launch& P, Lds<W>& sm, const tbf_seg_ctl&
 	__syncthreads ();
 }
 
-/* ------------------------------------------------------------------ kernel */
 template <int W>
-__global__ void __launch_bounds__ (NL, (W <= 1024 ? 2 : 1))
-tbf_render_kernel (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_seg_ctl* __restrict__ ctl,
-                   const tbf_tpl_desc* __restrict__ tpls)
+__global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL), amdgpu_waves_per_eu (W <= 512 ? WH_WAVES : (W <= 1024 ? 2 : 1))))
+k_whirl (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_seg_ctl* __restrict__ ctl)
 {
-	__shared__ Lds<W> sm;
-	const int      lane = threadIdx.x;
+	__shared__ WhLds<W> sm;
 	const uint32_t inst = blockIdx.x + P.instBase;
 	if (inst >= P.nInst)
 		return;
-	/* read-only per-instance records come in as restrict kernel arguments so their
-	 * uniform fields are fetched with scalar loads */
-	const tbf_inst_const& K = cst[inst];
-	const tbf_seg_ctl&    G = ctl[inst];
-	const tbf_tpl_desc*   T = tpls + K.tpl;
-	tbf_inst_state*       S = P.st + inst;
+	const tbf_inst_const& K  = cst[inst];
+	const tbf_seg_ctl&    G  = ctl[inst];
+	tbf_wh_state*         S  = &P.st[inst].wh;
 	float*                wr = P.wring + (size_t)inst * 4 * W;
-	double*               slab = P.rslab + (size_t)inst * P.slabLen;
-
-	if (P.prof) {
-		if (lane < TBF_PROF_SLOTS)
-			sm.prof[lane] = 0;
-		if (lane == 0)
-			sm.plast = __builtin_amdgcn_s_memtime ();
-	}
-	/* state -> LDS */
-	{
-		const uint32_t* src = (const uint32_t*)S;
-		uint32_t*       dst = (uint32_t*)&sm.st;
-		for (uint32_t i = lane; i < sizeof (tbf_inst_state) / 4; i += NL)
-			dst[i] = src[i];
-		for (uint32_t i = lane; i < 4u * W; i += NL)
-			(&sm.wring[0][0])[i] = wr[i];
-	}
+	prof_begin (P, sm);
+	copy_words (&sm.st, S);
+	for (uint32_t i = threadIdx.x; i < 4u * W; i += NL)
+		(&sm.wring[0][0])[i] = wr[i];
 	__syncthreads ();
-	TBF_MARK (18);
-
+	TBF_MARK (17);
 	for (uint32_t blk = 0; blk < P.nBlocks; blk++) {
-		stage_tonegen<W> (P, sm, G, T);
-		float* oL = P.outL + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
-		float* oR = P.outR + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
-		if (P.chain == 1) {
-			oL[lane]      = sm.bufA[lane];
-			oL[lane + NL] = sm.bufA[lane + NL];
-			oR[lane]      = sm.bufA[lane];
-			oR[lane + NL] = sm.bufA[lane + NL];
-			continue;
-		}
-		stage_overdrive<W> (P, sm, G);
-		if (P.chain == 2) { /* stage tap: preamp output */
-			oL[lane] = oR[lane] = sm.bufB[lane];
-			oL[lane + NL] = oR[lane + NL] = sm.bufB[lane + NL];
-			continue;
-		}
-		stage_reverb<W> (P, sm, G, K, slab);
-		if (P.chain == 3) { /* stage tap: reverb output */
-			oL[lane] = oR[lane] = sm.bufC[lane];
-			oL[lane + NL] = oR[lane + NL] = sm.bufC[lane + NL];
-			continue;
-		}
-		stage_whirl<W> (P, sm, G, K, blk == 0, oL, oR);
+		const float* in = P.mid2 + (size_t)inst * P.midStride + (size_t)blk * TBF_BLK;
+		float*       oL = P.outL + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
+		float*       oR = P.outR + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
+		stage_whirl<W> (P, sm, G, K, blk == 0, in, oL, oR);
 	}
-
 	__syncthreads ();
-	{
-		uint32_t*       dst = (uint32_t*)S;
-		const uint32_t* src = (const uint32_t*)&sm.st;
-		for (uint32_t i = lane; i < sizeof (tbf_inst_state) / 4; i += NL)
-			dst[i] = src[i];
-		for (uint32_t i = lane; i < 4u * W; i += NL)
-			wr[i] = (&sm.wring[0][0])[i];
-	}
+	copy_words (S, &sm.st);
+	for (uint32_t i = threadIdx.x; i < 4u * W; i += NL)
+		wr[i] = (&sm.wring[0][0])[i];
 	TBF_MARK (19);
-	if (P.prof && lane < TBF_PROF_SLOTS)
-		P.prof[(size_t)inst * TBF_PROF_SLOTS + lane] += sm.prof[lane];
+	prof_end (P, sm, inst);
 }
 
+/* ------------------------------------------------------------------ launch */
 extern "C" int tbf_launch_render (const tbf_launch* P, hipStream_t stream)
 {
 	if (P->nInst == 0 || P->nBlocks == 0)
 		return 0;
-	dim3 grid (P->nInst), block (NL);
+	if (P->chain != TBF_CHAIN_TONEGEN && (uint64_t)P->nBlocks * TBF_BLK > P->midStride)
+		return -22;
+	const dim3 grid (P->nInst), block (NL);
+	hipLaunchKernelGGL (k_tonegen, grid, block, 0, stream, *P, P->ctl, P->tpls, P->cst);
+	if (P->chain == TBF_CHAIN_TONEGEN || P->chain == TBF_CHAIN_TAP_PREAMP)
+		return hipGetLastError () == hipSuccess ? 0 : -5;
+	hipLaunchKernelGGL (k_reverb, grid, block, 0, stream, *P, P->cst, P->ctl);
+	if (P->chain == TBF_CHAIN_TAP_REVERB)
+		return hipGetLastError () == hipSuccess ? 0 : -5;
 	switch (P->wringLen) {
-		case 512: hipLaunchKernelGGL (tbf_render_kernel<512>, grid, block, 0, stream, *P, P->cst, P->ctl, P->tpls); break;
-		case 1024: hipLaunchKernelGGL (tbf_render_kernel<1024>, grid, block, 0, stream, *P, P->cst, P->ctl, P->tpls); break;
-		case 2048: hipLaunchKernelGGL (tbf_render_kernel<2048>, grid, block, 0, stream, *P, P->cst, P->ctl, P->tpls); break;
+		case 512: hipLaunchKernelGGL (k_whirl<512>, grid, block, 0, stream, *P, P->cst, P->ctl); break;
+		case 1024: hipLaunchKernelGGL (k_whirl<1024>, grid, block, 0, stream, *P, P->cst, P->ctl); break;
+		case 2048: hipLaunchKernelGGL (k_whirl<2048>, grid, block, 0, stream, *P, P->cst, P->ctl); break;
 		default: return -22;
 	}
 	return hipGetLastError () == hipSuccess ? 0 : -5;

@@ -77,24 +77,27 @@ typedef struct tbf_inst_const {
 	double   sr;
 } tbf_inst_const;
 
-/* per instance device-resident DSP state */
-typedef struct tbf_inst_state {
-	/* tonegen */
+/* per instance device-resident DSP state, one sub-struct per render kernel (each
+ * kernel stages only its own part in LDS); sizes are multiples of 8 bytes */
+typedef struct tbf_tg_state { /* tonegen + vibrato + overdrive: k_tonegen */
 	uint32_t pos[TBF_NW + 1];
 	float    keyCompLevel, percEnvGain, pz;
-	/* vibrato */
 	uint32_t stator, outPos;
 	float    vring[TBF_VRING];
-	/* overdrive */
 	double   iirA, iirB;
 	uint32_t fpFlip, odFpd;
-	/* reverb */
+} tbf_tg_state;
+
+typedef struct tbf_rv_state { /* reverb: k_reverb */
 	int32_t  count[13];
 	uint32_t fpdL, fpdR;
+	uint32_t pad0;
 	double   bq[3][4]; /* [A/B/C][L7, L8, R9, R10] */
 	double   fb[2][8];
 	double   vib[2][8];
-	/* whirl */
+} tbf_rv_state;
+
+typedef struct tbf_wh_state { /* whirl: k_whirl */
 	double   hornAngle, drumAngle, hornIncr, drumIncr, hornTarget, drumTarget;
 	int32_t  hornAcDc, drumAcDc;
 	uint32_t outpos;
@@ -102,7 +105,13 @@ typedef struct tbf_inst_state {
 	float    fz[4][2]; /* hafw, hbfw, drfL, drfR: z0, z1 */
 	float    adx[3][8];
 	int32_t  adi[3];
-	int32_t  pad1;
+	int32_t  pad1[2];
+} tbf_wh_state;
+
+typedef struct tbf_inst_state {
+	tbf_tg_state tg;
+	tbf_rv_state rv;
+	tbf_wh_state wh;
 } tbf_inst_state;
 
 /* per template (tuning x sample rate): offsets into the shared wave bank */
@@ -120,6 +129,9 @@ typedef struct tbf_launch {
 	const tbf_inst_const* cst;
 	tbf_inst_state*       st;
 	float*                wring; /* [inst][4][wring_len] */
+	float*                mid1;  /* [inst][midStride] preamp output of the chunk */
+	float*                mid2;  /* [inst][midStride] reverb output of the chunk */
+	uint64_t              midStride;
 	double*               rslab; /* [inst][slabLen] */
 	const tbf_seg_ctl*    ctl;
 	const tbf_prog_entry* prog;
@@ -134,7 +146,7 @@ typedef struct tbf_launch {
 	uint32_t              nBlocks;
 	uint32_t              wringLen;
 	uint32_t              statorInc;
-	uint32_t              chain;     /* 0 full, 1 tonegen only */
+	uint32_t              chain;     /* TBF_CHAIN_*: 0 full, 1 tonegen, 2 preamp tap, 3 reverb tap */
 	uint32_t              instBase;
 	uint32_t              slabLen;
 	uint32_t              pad;

@@ -2,11 +2,13 @@
 from __future__ import annotations
 
 import ctypes as C
+import os
 from pathlib import Path
 
 import numpy as np
 
-LIB_PATH = Path(__file__).resolve().parent / "libtbf.so"
+# TBF_LIB overrides the library path (build variants for A/B measurements)
+LIB_PATH = Path(os.environ.get("TBF_LIB", Path(__file__).resolve().parent / "libtbf.so"))
 
 _fp = C.POINTER(C.c_float)
 _dp = C.POINTER(C.c_double)

@@ -24,8 +24,14 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "tests"))
 
-BYTES_PER_STEREO_SAMPLE = 424  # 8 B output + 13 lines x 2 ch x (8 B write + 8 B read)
-HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# algorithmic HBM bytes per stereo sample, per kernel:
+#   k_reverb  = 13 lines x 2 ch x (8 B write + 8 B read) ring streaming + 4 B in + 4 B out
+#   k_tonegen = 4 B stage output (wave bank L2/MALL-resident)
+#   k_whirl   = 4 B in + 8 B L/R out
+ALGO_BYTES = {"k_tonegen": 4, "k_reverb": 424, "k_whirl": 12}
+DOMINANT = "k_reverb"  # the HBM-streaming kernel the roofline is quoted for
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+TRAFFIC_JSON = ROOT / "profiles" / "traffic.json"  # written by tools/traffic_from_pmc.py
 
 
 def parse():
@@ -41,6 +47,9 @@ def parse():
     ap.add_argument("--cpu-instances", type=int, default=128)
     ap.add_argument("--cpu-blocks", type=int, default=12000)
     ap.add_argument("--chain", type=int, default=0, help="0 full chain; 1/2/3 stage taps (profiling only)")
+    ap.add_argument("--traffic", default=str(TRAFFIC_JSON), help="PMC traffic JSON (tools/traffic_from_pmc.py)")
+    ap.add_argument("--kernel-steps", type=int, default=None,
+                    help="extra steps timed per kernel with HIP events for the roofline (default = --steps)")
     return ap.parse_args()
 
 
@@ -173,10 +182,21 @@ def main():
     total_samples = world * B * nsamp * a.steps
     value = total_samples / elapsed
 
+    # per-kernel launch durations (HIP events on the launch stream, inside the engine);
+    # a separate pass so the events do not perturb the timed region above
+    ksteps = a.steps if a.kernel_steps is None else a.kernel_steps
+    eng.kernel_times(True)
+    for _ in range(ksteps):
+        step()
+    torch.cuda.synchronize()
+    kt = eng.kernel_times()
+    eng.kernel_times(False)
+    kern = {k: v[0] / v[1] for k, v in kt.items() if v[1]}
+
     # parity on the last step (first --check instances of this rank)
     gL = outL[: a.check].cpu().numpy()
     gR = outR[: a.check].cpu().numpy()
-    total_blocks = (a.warmup + a.steps) * a.blocks
+    total_blocks = (a.warmup + a.steps + ksteps) * a.blocks
     max_err, exact = oracle_check(first_global, a.check, total_blocks, a.blocks, gL, gR, a.sr) if a.check else (None, None)
     if dist:
         e = torch.tensor([max_err or 0.0], dtype=torch.float64, device="cuda")
@@ -184,8 +204,16 @@ def main():
         max_err = float(e.item())
 
     if rank == 0:
-        per_launch_bytes = B * nsamp * BYTES_PER_STEREO_SAMPLE
-        achieved = per_launch_bytes / (kern_ms * 1e-3) / 1e9
+        samples_launch = B * nsamp
+        dom = DOMINANT if DOMINANT in kern else max(kern, key=kern.get)
+        achieved = samples_launch * ALGO_BYTES[dom] / (kern[dom] * 1e-3) / 1e9
+        traffic, traffic_src = None, None
+        if Path(a.traffic).exists():
+            tj = json.loads(Path(a.traffic).read_text())
+            if tj.get("workload") == {"batch": B, "blocks": a.blocks, "sr": a.sr, "chain": a.chain} \
+                    and dom in tj.get("kernels", {}):
+                traffic = tj["kernels"][dom]["bytes_per_launch"]
+                traffic_src = tj.get("source")
         cpu = cpu_baseline(a.cpu_instances, a.cpu_blocks, a.sr) if (a.cpu_baseline and world == 1) else None
         line = {
             "metric": "stereo samples/sec whole-node, batch=4096 full chain @48kHz; max|err| vs CPU",
@@ -199,9 +227,13 @@ def main():
                        "parallelism": f"instance-sharded x{world} (no collective)"},
             "max_err": max_err, "bit_exact_frac": exact, "checked_instances": a.check,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "tbf_render_kernel", "kernel_ms_per_launch": kern_ms,
-                         "bytes_per_stereo_sample": BYTES_PER_STEREO_SAMPLE},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": dom, "kernel_ms_per_launch": kern[dom],
+                         "algorithmic_bytes_per_launch": samples_launch * ALGO_BYTES[dom],
+                         "bytes_per_stereo_sample": ALGO_BYTES[dom], "traffic_source": traffic_src,
+                         "kernels_ms_per_launch": kern, "gpu_ms_per_step_events": kern_ms,
+                         "pipeline_gbs": samples_launch * sum(ALGO_BYTES[k] for k in kern)
+                         / (sum(kern.values()) * 1e-3) / 1e9},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

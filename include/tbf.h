@@ -128,6 +128,10 @@ int tbf_debug_exact (int32_t op, const double* in3, double* out2, uint32_t n);
 /* stage timing: enable 1 zeroes per-instance counters and turns the kernel's marks on;
  * 0 copies out [inst][32] cycle sums (returns the count); -1 turns the marks off */
 int tbf_debug_profile (tbf_engine* e, int32_t enable, uint64_t* out, uint32_t cap);
+/* per-stage kernel timing with HIP events on the render stream: enable 1 / -1 turns
+ * recording on / off; 0 returns the summed milliseconds and launch counts of the
+ * stages k_tonegen, k_reverb, k_whirl since the last query (ms3[3], count3[3]) */
+int tbf_debug_kernel_times (tbf_engine* e, int32_t enable, double* ms3, uint32_t* count3);
 /* PMC calibration: op 0 streams n doubles from d_buf (8 B/lane reads, the reverb ring
  * pattern), op 1 writes them; enqueued on `stream` (NULL = legacy default stream) */
 int tbf_debug_calibrate (int32_t op, void* d_buf, uint64_t n_doubles, void* stream);

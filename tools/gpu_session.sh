@@ -45,6 +45,14 @@ for s in $STEPS; do
 		for v in tunebfree_amd/_variants/libtbf_*.so; do
 			run "var_$(basename $v .so)" 300 env TBF_LIB=$v python3 bench.py --cpu-baseline 0 --check 2 --steps 3 --warmup 1
 		done ;;
+	full)
+		BC="--cpu-baseline 0"
+		run fstats 600 rocprofv3 --kernel-trace --stats -d "$OUT/fstats" -o run --output-format csv -- python3 bench.py $BC
+		run ffetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/ffetch" -o run --output-format csv -- python3 bench.py $BC
+		run fwrite 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/fwrite" -o run --output-format csv -- python3 bench.py $BC
+		run ftraffic 60 python3 tools/traffic_from_pmc.py "$OUT/ffetch" "$OUT/fwrite" --out "$OUT/traffic.json"
+		run fbench 900 python3 bench.py --traffic "$OUT/traffic.json"
+		;;
 	calib)
 		run calib_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/calib_fetch" -o run --output-format csv -- python3 tools/calib_pmc.py
 		run calib_write 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/calib_write" -o run --output-format csv -- python3 tools/calib_pmc.py

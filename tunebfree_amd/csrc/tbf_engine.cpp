@@ -18,7 +18,8 @@
 #include "tbf_host.h"
 #include "tbf_types.h"
 
-extern "C" int tbf_launch_render (const tbf_launch* P, hipStream_t stream);
+extern "C" int tbf_launch_stage (const tbf_launch* P, int k, hipStream_t stream);
+extern "C" int tbf_chain_stages (uint32_t chain);
 extern "C" int tbf_launch_calibrate (int op, void* buf, uint64_t n, hipStream_t s);
 
 using namespace tbf;
@@ -114,6 +115,9 @@ struct tbf_engine {
 	DevBuf<uint32_t>                        err;
 	DevBuf<uint64_t>                        prof; /* tbf_debug_profile */
 	bool                                    profOn = false;
+	/* tbf_debug_kernel_times: HIP events around every stage launch */
+	bool                                    timeOn = false;
+	std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> tev;
 	DevBuf<float>                           outL, outR;
 	DevBuf<float>                           mid1, mid2; /* inter-stage blocks of one launch chunk */
 	std::vector<tbf_seg_ctl>                hCtl;
@@ -667,9 +671,22 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 				}
 				ctlChanged = false;
 			}
-			rc = tbf_launch_render (&P, s);
-			if (rc)
-				return fail (rc, std::string ("kernel launch failed: ") + hipGetErrorString (hipGetLastError ()));
+			const int nst = tbf_chain_stages (P.chain);
+			for (int k = 0; k < nst; k++) {
+				hipEvent_t e0 = nullptr, e1 = nullptr;
+				if (e->timeOn) {
+					HIPCHK (hipEventCreate (&e0));
+					HIPCHK (hipEventCreate (&e1));
+					HIPCHK (hipEventRecord (e0, s));
+				}
+				rc = tbf_launch_stage (&P, k, s);
+				if (rc)
+					return fail (rc, std::string ("kernel launch failed: ") + hipGetErrorString (hipGetLastError ()));
+				if (e->timeOn) {
+					HIPCHK (hipEventRecord (e1, s));
+					e->tev.push_back ({k, {e0, e1}});
+				}
+			}
 		}
 		/* host staging buffers are rewritten by the next buildControl: keep order */
 		if (needSync)
@@ -860,6 +877,35 @@ int tbf_debug_calibrate (int32_t op, void* buf, uint64_t n, void* stream)
 		return fail (-22, "bad arguments");
 	int rc = tbf_launch_calibrate (op, buf, n, (hipStream_t)stream);
 	return rc ? fail (rc, "calibration launch failed") : 0;
+}
+
+int tbf_debug_kernel_times (tbf_engine* e, int32_t enable, double* ms3, uint32_t* count3)
+{
+	if (!e)
+		return fail (-22, "null engine");
+	if (enable == 1 || enable == -1) {
+		e->timeOn = enable == 1;
+		return 0;
+	}
+	if (e->cfg.device >= 0)
+		HIPCHK (hipSetDevice (e->cfg.device));
+	double   ms[3] = {0, 0, 0};
+	uint32_t cnt[3] = {0, 0, 0};
+	for (auto& t : e->tev) {
+		HIPCHK (hipEventSynchronize (t.second.second));
+		float v = 0.f;
+		HIPCHK (hipEventElapsedTime (&v, t.second.first, t.second.second));
+		ms[t.first] += v;
+		cnt[t.first]++;
+		(void)hipEventDestroy (t.second.first);
+		(void)hipEventDestroy (t.second.second);
+	}
+	e->tev.clear ();
+	for (int k = 0; k < 3; k++) {
+		if (ms3) ms3[k] = ms[k];
+		if (count3) count3[k] = cnt[k];
+	}
+	return 0;
 }
 
 } /* extern "C" */

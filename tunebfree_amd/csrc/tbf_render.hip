@@ -1232,24 +1232,33 @@ k_whirl (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 }
 
 /* ------------------------------------------------------------------ launch */
-extern "C" int tbf_launch_render (const tbf_launch* P, hipStream_t stream)
+/* stage k (0 k_tonegen, 1 k_reverb, 2 k_whirl) of one launch chunk; the chain mode
+ * decides which stages run (tbf_chain_stages) */
+extern "C" int tbf_launch_stage (const tbf_launch* P, int k, hipStream_t stream)
 {
 	if (P->nInst == 0 || P->nBlocks == 0)
 		return 0;
 	if (P->chain != TBF_CHAIN_TONEGEN && (uint64_t)P->nBlocks * TBF_BLK > P->midStride)
 		return -22;
 	const dim3 grid (P->nInst), block (NL);
-	hipLaunchKernelGGL (k_tonegen, grid, block, 0, stream, *P, P->ctl, P->tpls, P->cst);
-	if (P->chain == TBF_CHAIN_TONEGEN || P->chain == TBF_CHAIN_TAP_PREAMP)
-		return hipGetLastError () == hipSuccess ? 0 : -5;
-	hipLaunchKernelGGL (k_reverb, grid, block, 0, stream, *P, P->cst, P->ctl);
-	if (P->chain == TBF_CHAIN_TAP_REVERB)
-		return hipGetLastError () == hipSuccess ? 0 : -5;
-	switch (P->wringLen) {
-		case 512: hipLaunchKernelGGL (k_whirl<512>, grid, block, 0, stream, *P, P->cst, P->ctl); break;
-		case 1024: hipLaunchKernelGGL (k_whirl<1024>, grid, block, 0, stream, *P, P->cst, P->ctl); break;
-		case 2048: hipLaunchKernelGGL (k_whirl<2048>, grid, block, 0, stream, *P, P->cst, P->ctl); break;
-		default: return -22;
-	}
+	if (k == 0)
+		hipLaunchKernelGGL (k_tonegen, grid, block, 0, stream, *P, P->ctl, P->tpls, P->cst);
+	else if (k == 1)
+		hipLaunchKernelGGL (k_reverb, grid, block, 0, stream, *P, P->cst, P->ctl);
+	else if (k == 2) {
+		switch (P->wringLen) {
+			case 512: hipLaunchKernelGGL (k_whirl<512>, grid, block, 0, stream, *P, P->cst, P->ctl); break;
+			case 1024: hipLaunchKernelGGL (k_whirl<1024>, grid, block, 0, stream, *P, P->cst, P->ctl); break;
+			case 2048: hipLaunchKernelGGL (k_whirl<2048>, grid, block, 0, stream, *P, P->cst, P->ctl); break;
+			default: return -22;
+		}
+	} else
+		return -22;
 	return hipGetLastError () == hipSuccess ? 0 : -5;
+}
+
+/* number of stages the chain mode runs */
+extern "C" int tbf_chain_stages (uint32_t chain)
+{
+	return chain == TBF_CHAIN_TONEGEN || chain == TBF_CHAIN_TAP_PREAMP ? 1 : (chain == TBF_CHAIN_TAP_REVERB ? 2 : 3);
 }

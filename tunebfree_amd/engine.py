@@ -148,6 +148,19 @@ class Engine:
     def synchronize(self):
         _check(self._lib.tbf_synchronize(self._h))
 
+    def kernel_times(self, enable=None):
+        """Per-stage HIP-event timing (tbf_debug_kernel_times): enable=True/False switches
+        recording; with no argument returns {stage: (ms_total, launches)} since the last call."""
+        fn = self._lib.tbf_debug_kernel_times
+        fn.restype, fn.argtypes = C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
+        if enable is not None:
+            _check(fn(self._h, 1 if enable else -1, None, None))
+            return None
+        ms = np.zeros(3, np.float64)
+        cnt = np.zeros(3, np.uint32)
+        _check(fn(self._h, 0, ms.ctypes.data, cnt.ctypes.data))
+        return {k: (float(ms[i]), int(cnt[i])) for i, k in enumerate(("k_tonegen", "k_reverb", "k_whirl"))}
+
     def error_flags(self):
         f = C.c_uint32()
         _check(self._lib.tbf_error_flags(self._h, C.byref(f)))

@@ -25,11 +25,13 @@ sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "tests"))
 
 # algorithmic HBM bytes per stereo sample, per kernel:
-#   k_reverb  = 13 lines x 2 ch x (8 B write + 8 B read) ring streaming + 4 B in + 4 B out
+#   k_rv_core = 12 lines x 2 ch x (8 B write + 8 B read) ring streaming + 16 B in + 16 B out
+#   k_rv_in   = predelay ring 2 ch x 16 B + 4 B in + 16 B out
+#   k_rv_out  = 16 B tap mix + 4 B dry in + 4 B out
 #   k_tonegen = 4 B stage output (wave bank L2/MALL-resident)
 #   k_whirl   = 4 B in + 8 B L/R out
-ALGO_BYTES = {"k_tonegen": 4, "k_reverb": 424, "k_whirl": 12}
-DOMINANT = "k_reverb"  # the HBM-streaming kernel the roofline is quoted for
+ALGO_BYTES = {"k_tonegen": 4, "k_rv_in": 52, "k_rv_core": 416, "k_rv_out": 24, "k_whirl": 12}
+DOMINANT = "k_rv_core"  # the HBM-streaming kernel the roofline is quoted for
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 TRAFFIC_JSON = ROOT / "profiles" / "traffic.json"  # written by tools/traffic_from_pmc.py
 

@@ -123,15 +123,17 @@ int tbf_debug_tables (tbf_engine* e, uint32_t tpl_id, float* attack, float* rele
 int tbf_debug_step (tbf_engine* e, uint32_t inst, float* entries9, uint32_t cap);
 /* the kernel's exact shortcuts of serial recurrences, evaluated on the host (same source,
  * csrc/tbf_exact.h): op 0 phase_run (in: v0, d, m -> out: ok, D), op 1 cnt_adv (in: c0,
- * d, n -> out: count), op 2 wrap1 (in: x, -, - -> out: fmod (x, 1)); n records */
+ * d, n -> out: count), op 2 wrap1 (in: x, -, - -> out: fmod (x, 1)), op 3 xorshift
+ * dither jump (in: x0, k, - -> out: jump-table state, k literal steps); n records */
 int tbf_debug_exact (int32_t op, const double* in3, double* out2, uint32_t n);
 /* stage timing: enable 1 zeroes per-instance counters and turns the kernel's marks on;
  * 0 copies out [inst][32] cycle sums (returns the count); -1 turns the marks off */
 int tbf_debug_profile (tbf_engine* e, int32_t enable, uint64_t* out, uint32_t cap);
 /* per-stage kernel timing with HIP events on the render stream: enable 1 / -1 turns
- * recording on / off; 0 returns the summed milliseconds and launch counts of the
- * stages k_tonegen, k_reverb, k_whirl since the last query (ms3[3], count3[3]) */
-int tbf_debug_kernel_times (tbf_engine* e, int32_t enable, double* ms3, uint32_t* count3);
+ * recording on / off; 0 returns the summed milliseconds and launch counts of the five
+ * stage kernels k_tonegen, k_rv_in, k_rv_core, k_rv_out, k_whirl since the last query
+ * (ms5[5], count5[5]) */
+int tbf_debug_kernel_times (tbf_engine* e, int32_t enable, double* ms5, uint32_t* count5);
 /* PMC calibration: op 0 streams n doubles from d_buf (8 B/lane reads, the reverb ring
  * pattern), op 1 writes them; enqueued on `stream` (NULL = legacy default stream) */
 int tbf_debug_calibrate (int32_t op, void* d_buf, uint64_t n_doubles, void* stream);

@@ -12,12 +12,14 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "tests"))
 
-NAMES = {0: "tg state load + interpreter", 1: "tg vibrato", 2: "tg mixdown", 3: "od serial", 4: "od parallel",
-         18: "tg state store",
-         5: "rv state load + fpd serial", 6: "rv reads+taps", 7: "rv pd write + A/B chains",
-         8: "rv ap/line writes + asin", 9: "rv C chain", 10: "rv out + counts",
-         17: "wh state + ring load", 11: "wh speed", 12: "wh ring rd + serial filt+angles", 13: "wh FILTER_C",
-         14: "wh motions", 15: "wh accumulate", 16: "wh out + carry", 19: "wh state + ring store"}
+NAMES = {0: "tg state load + interpreter", 1: "tg vibrato", 2: "tg mixdown", 3: "od dither + HPF chain",
+         4: "od waveshaper", 18: "tg state store",
+         5: "rv_in dither", 6: "rv_in predelay + biquadA chain", 7: "rv_in sin(x*wet)",
+         8: "rv_core channel L", 9: "rv_core channel R + counts",
+         10: "rv_out dither", 11: "rv_out biquadB chain", 12: "rv_out asin", 13: "rv_out biquadC chain",
+         14: "rv_out dry/dither/store",
+         26: "wh state + ring load", 20: "wh speed", 21: "wh ring rd + serial filt+angles", 22: "wh FILTER_C",
+         23: "wh motions", 24: "wh accumulate", 25: "wh out + carry", 27: "wh state + ring store"}
 
 
 def main():

@@ -111,6 +111,7 @@ struct tbf_engine {
 	DevBuf<tbf_seg_ctl>                     ctl;
 	DevBuf<tbf_prog_entry>                  prog;
 	DevBuf<uint32_t>                        vib;
+	DevBuf<uint32_t>                        xsj; /* xorshift32 jump table */
 	DevBuf<float>                           whTab, whBw;
 	DevBuf<uint32_t>                        err;
 	DevBuf<uint64_t>                        prof; /* tbf_debug_profile */
@@ -120,6 +121,7 @@ struct tbf_engine {
 	std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> tev;
 	DevBuf<float>                           outL, outR;
 	DevBuf<float>                           mid1, mid2; /* inter-stage blocks of one launch chunk */
+	DevBuf<double>                          rvA, rvB;   /* reverb inter-kernel streams (FP64) */
 	std::vector<tbf_seg_ctl>                hCtl;
 	std::vector<tbf_prog_entry>             hProg;
 	/* synth_sound FIFO */
@@ -131,6 +133,7 @@ struct tbf_engine {
 /* blocks per kernel launch chunk: bounds the inter-stage buffers to
  * n_inst x TBF_CHUNK x 128 floats each (134 MB at 4096 instances) */
 #define TBF_CHUNK 64
+#define TBF_NSTAGES 5 /* k_tonegen, k_rv_in, k_rv_core, k_rv_out, k_whirl */
 
 /* ------------------------------------------------------------------ construction */
 
@@ -296,6 +299,7 @@ int tbf_engine_destroy (tbf_engine* e)
 	e->ctl.release ();
 	e->prog.release ();
 	e->vib.release ();
+	e->xsj.release ();
 	e->whTab.release ();
 	e->whBw.release ();
 	e->err.release ();
@@ -303,6 +307,8 @@ int tbf_engine_destroy (tbf_engine* e)
 	e->outR.release ();
 	e->mid1.release ();
 	e->mid2.release ();
+	e->rvA.release ();
+	e->rvB.release ();
 	if (e->stream)
 		(void)hipStreamDestroy (e->stream);
 	delete e;
@@ -369,6 +375,8 @@ int tbf_instances_add (tbf_engine* e, uint32_t n, const uint32_t* tpl_ids, const
 		while (f < 16386)
 			f = (uint32_t)rnd.next () * 0xFFFFFFFFu;
 		in.s0.rv.fpdR = f;
+		in.s0.rv.fpdL2 = in.s0.rv.fpdL;
+		in.s0.rv.fpdR2 = in.s0.rv.fpdR;
 		f          = 1;
 		while (f < 16386)
 			f = (uint32_t)rnd.next () * 0xFFFFFFFFu;
@@ -505,6 +513,16 @@ static int ensureDevice (tbf_engine* e)
 	    e->err.ensure (4))
 		return fail (-12, "out of device memory (tables)");
 	HIPCHK (hipMemcpy (e->vib.p, e->vibTab.data (), e->vibTab.size () * 4, hipMemcpyHostToDevice));
+	{
+		/* xorshift32 (src/overdrive.cpp:158-160, src/reverb.cpp:775-783) is linear over
+		 * GF(2): state after k steps = XOR over the set bits j of the state of
+		 * xorshift^k (1 << j).  Column k of row j holds that image, k = 0 .. 128. */
+		std::vector<uint32_t> J (32 * TBF_XS_JUMP);
+		xs_jump_table (J.data (), TBF_XS_JUMP);
+		if (e->xsj.ensure (J.size ()))
+			return fail (-12, "out of device memory (tables)");
+		HIPCHK (hipMemcpy (e->xsj.p, J.data (), J.size () * 4, hipMemcpyHostToDevice));
+	}
 	HIPCHK (hipMemcpy (e->whTab.p, e->wt.displ.data (), e->wt.displ.size () * 4, hipMemcpyHostToDevice));
 	HIPCHK (hipMemcpy (e->whBw.p, e->wt.bw.data (), e->wt.bw.size () * 4, hipMemcpyHostToDevice));
 	HIPCHK (hipMemset (e->err.p, 0, 16));
@@ -621,6 +639,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 	P.ctl       = e->ctl.p;
 	P.prog      = e->prog.p;
 	P.vibTab    = e->vib.p;
+	P.xsJump    = e->xsj.p;
 	P.whTab     = e->whTab.p;
 	P.whBw      = e->whBw.p;
 	P.outL      = dL;
@@ -637,7 +656,11 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		const size_t need = (size_t)n * TBF_CHUNK * TBF_BLK;
 		if (e->mid1.ensure (need) || e->mid2.ensure (need))
 			return fail (-12, "out of device memory (stage buffers)");
+		if (e->cfg.chain_mode != TBF_CHAIN_TAP_PREAMP && (e->rvA.ensure (2 * need) || e->rvB.ensure (2 * need)))
+			return fail (-12, "out of device memory (reverb stage buffers)");
 	}
+	P.rvA       = e->rvA.p;
+	P.rvB       = e->rvB.p;
 	P.mid1      = e->mid1.p;
 	P.mid2      = e->mid2.p;
 	P.midStride = (uint64_t)TBF_CHUNK * TBF_BLK;
@@ -852,8 +875,13 @@ int tbf_debug_profile (tbf_engine* e, int32_t enable, uint64_t* out, uint32_t ca
 
 int tbf_debug_exact (int32_t op, const double* in, double* out, uint32_t n)
 {
-	if (!in || !out || op < 0 || op > 2)
+	if (!in || !out || op < 0 || op > 3)
 		return fail (-22, "bad arguments");
+	static std::vector<uint32_t> J;
+	if (op == 3 && J.empty ()) {
+		J.resize (32 * TBF_XS_JUMP);
+		xs_jump_table (J.data (), TBF_XS_JUMP);
+	}
 	for (uint32_t i = 0; i < n; i++) {
 		const double* a = in + 3 * i;
 		double*       o = out + 2 * i;
@@ -864,8 +892,19 @@ int tbf_debug_exact (int32_t op, const double* in, double* out, uint32_t n)
 			o[1]     = D;
 		} else if (op == 1) {
 			o[0] = cnt_adv ((int)a[0], (int)a[1], (int)a[2]);
-		} else {
+		} else if (op == 2) {
 			o[0] = wrap1 (a[0]);
+		} else {
+			/* op 3: xorshift jump (device table) vs k literal steps from x0 */
+			const uint32_t x0 = (uint32_t)a[0];
+			const int      k  = (int)a[1];
+			if (k < 0 || k >= TBF_XS_JUMP)
+				return fail (-22, "jump length out of range");
+			uint32_t x = x0;
+			for (int q = 0; q < k; q++)
+				x = xs_step (x);
+			o[0] = xs_jump_ref (J.data (), TBF_XS_JUMP, x0, k);
+			o[1] = x;
 		}
 	}
 	return 0;
@@ -889,8 +928,8 @@ int tbf_debug_kernel_times (tbf_engine* e, int32_t enable, double* ms3, uint32_t
 	}
 	if (e->cfg.device >= 0)
 		HIPCHK (hipSetDevice (e->cfg.device));
-	double   ms[3] = {0, 0, 0};
-	uint32_t cnt[3] = {0, 0, 0};
+	double   ms[TBF_NSTAGES] = {0};
+	uint32_t cnt[TBF_NSTAGES] = {0};
 	for (auto& t : e->tev) {
 		HIPCHK (hipEventSynchronize (t.second.second));
 		float v = 0.f;
@@ -901,7 +940,7 @@ int tbf_debug_kernel_times (tbf_engine* e, int32_t enable, double* ms3, uint32_t
 		(void)hipEventDestroy (t.second.second);
 	}
 	e->tev.clear ();
-	for (int k = 0; k < 3; k++) {
+	for (int k = 0; k < TBF_NSTAGES; k++) {
 		if (ms3) ms3[k] = ms[k];
 		if (count3) count3[k] = cnt[k];
 	}

@@ -57,4 +57,35 @@ TBF_HD double wrap1 (double x)
 	return fmod (x, 1.0);
 }
 
+/* xorshift32 of the Airwindows dither (src/overdrive.cpp:158-160, src/reverb.cpp:775-783) */
+TBF_HD uint32_t xs_step (uint32_t x)
+{
+	x ^= x << 13;
+	x ^= x >> 17;
+	x ^= x << 5;
+	return x;
+}
+
+/* xorshift32 is linear over GF(2): the state after k steps from x0 is the XOR, over the
+ * set bits j of x0, of the k-step image of (1 << j).  J[j * cols + k] holds that image. */
+static inline void xs_jump_table (uint32_t* J, int cols)
+{
+	for (int j = 0; j < 32; j++) {
+		uint32_t x = 1u << j;
+		for (int k = 0; k < cols; k++) {
+			J[j * cols + k] = x;
+			x               = xs_step (x);
+		}
+	}
+}
+
+TBF_HD uint32_t xs_jump_ref (const uint32_t* J, int cols, uint32_t x0, int k)
+{
+	uint32_t r = 0;
+	for (int j = 0; j < 32; j++)
+		if ((x0 >> j) & 1u)
+			r ^= J[j * cols + k];
+	return r;
+}
+
 #endif

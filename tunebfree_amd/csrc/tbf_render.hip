@@ -37,7 +37,10 @@
 #define TG_WAVES 4
 #endif
 #ifndef RV_WAVES
-#define RV_WAVES 2
+#define RV_WAVES 3
+#endif
+#ifndef RVIO_WAVES
+#define RVIO_WAVES 4
 #endif
 #ifndef WH_WAVES
 #define WH_WAVES 3
@@ -75,18 +78,6 @@ struct TgLds {
 	unsigned long long plast;
 };
 
-struct RvLds {
-	tbf_rv_state st;
-	float        in[TBF_BLK];
-	double       a[2][TBF_SUB]; /* predelay output -> biquadA output */
-	double       b[2][TBF_SUB]; /* tap mix -> biquadB -> asin -> biquadC output */
-	double       t[8][TBF_SUB]; /* one channel's vibrato offsets */
-	double       vn[2][8];      /* vibrato phases after the sub-block */
-	double       fbn[2][8];     /* feedback of the sub-block's last sample */
-	uint32_t     fpd[2][TBF_SUB + 1];
-	unsigned long long prof[TBF_PROF_SLOTS];
-	unsigned long long plast;
-};
 
 template <int W>
 struct WhLds {
@@ -153,6 +144,20 @@ __device__ __forceinline__ uint32_t xorshift (uint32_t s)
 	s ^= s >> 17;
 	s ^= s << 5;
 	return s;
+}
+
+/* xorshift32 state after k steps from x0 (uniform), k per lane (0 .. 128), by the
+ * GF(2) jump table: coalesced row reads, one per set bit of x0 */
+__device__ __forceinline__ uint32_t xs_jump (const uint32_t* __restrict__ J, uint32_t x0, int k)
+{
+	x0         = __builtin_amdgcn_readfirstlane (x0);
+	uint32_t r = 0;
+	while (x0) {
+		const int j = __builtin_ctz (x0);
+		r ^= J[j * TBF_XS_JUMP + k];
+		x0 &= x0 - 1;
+	}
+	return r;
 }
 
 __device__ __forceinline__ int wave_min (int v)
@@ -415,26 +420,15 @@ __device__ void stage_overdrive (const tbf_launch& P, TgLds& sm, const tbf_seg_c
 		__syncthreads ();
 		return;
 	}
-	/* serial: xorshift sequence + alternating one-pole HPF */
+	/* xorshift dither states F[0..128] (F[n+1] after sample n) by GF(2) jumps */
 	{
-		/* xorshift dither sequence F[0..128] on the scalar unit, written into lanes */
-		uint32_t       f  = __builtin_amdgcn_readfirstlane (st.odFpd);
-		const uint32_t f0 = f;
-		uint32_t       lo = 0, hi = 0;
-		for (int i = 0; i < NL; i++) {
-			f  = xorshift (f);
-			lo = (lane == i) ? f : lo;
-		}
-		for (int i = 0; i < NL; i++) {
-			f  = xorshift (f);
-			hi = (lane == i) ? f : hi;
-		}
-		sm.u.od.fpd[lane + 1]      = lo;
-		sm.u.od.fpd[lane + 1 + NL] = hi;
+		const uint32_t f0 = st.odFpd;
+		sm.u.od.fpd[lane + 1]      = xs_jump (P.xsJump, f0, lane + 1);
+		sm.u.od.fpd[lane + 1 + NL] = xs_jump (P.xsJump, f0, lane + 1 + NL);
 		__syncthreads (); /* all lanes have read st.odFpd */
 		if (lane == 0) {
 			sm.u.od.fpd[0] = f0;
-			st.odFpd       = f;
+			st.odFpd       = sm.u.od.fpd[TBF_BLK];
 		}
 	}
 	__syncthreads ();
@@ -542,15 +536,26 @@ k_tonegen (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl, const tbf_tp
 	prof_end (P, sm, inst);
 }
 
-/* ================================================================== k_reverb */
+/* ================================================================== reverb */
+/* b_reverb::reverb (src/reverb.cpp:274-794) as three kernels.  The MatrixVerb's serial
+ * FP64 biquads sit outside its feedback network: biquadA filters the predelayed input
+ * before the allpasses (src/reverb.cpp:361-375), biquadB -> asin -> biquadC filter the
+ * tap mix on its way out (733-764).  So:
+ *   k_rv_in    predelay ring, biquadA, sin(x * wet)            -> a0[c][n] (FP64)
+ *   k_rv_core  allpasses, 16 modulated taps, Householder feedback, ring writes
+ *                                                               -> tap mix b[c][n] (FP64)
+ *   k_rv_out   biquadB, clamp + asin, biquadC, dry mix, dither, (L+R)/sqrt2 -> mid2
+ * k_rv_core has no serial recurrence besides the one-sample feedback shift, so it runs
+ * lane-parallel at high occupancy; the two chain kernels are small.  Each kernel
+ * regenerates what it needs of the xorshift dither streams (fpdL/fpdR advance once
+ * per sample regardless of the signal, src/reverb.cpp:775-783). */
 
-/* Serial IIR chains of one sub-block on lanes 0..nch-1: lane j runs the biquad
- * coefficient set q with state (s7, s8) over 64 samples of its LDS row, in place. */
-__device__ __forceinline__ void rv_chains (const tbf_inst_const& K, tbf_rv_state& st, double* row, int q, int c)
+/* Serial IIR chain (biquadA/B/C, src/reverb.cpp:361-369, 733-741, 756-764) of one
+ * channel over 64 samples of an LDS row, in place; st7/st8 = the channel's state pair */
+__device__ __forceinline__ void rv_chain (const double* cf, double& st7, double& st8, double* row)
 {
-	const double* cf = K.bq[q];
-	const double  c0 = cf[0], c1 = cf[1], c2 = cf[2], c3 = cf[3], c4 = cf[4];
-	double        s7 = st.bq[q][2 * c], s8 = st.bq[q][2 * c + 1];
+	const double c0 = cf[0], c1 = cf[1], c2 = cf[2], c3 = cf[3], c4 = cf[4];
+	double       s7 = st7, s8 = st8;
 	for (int i0 = 0; i0 < TBF_SUB; i0 += 8) {
 		double xv[8];
 #pragma unroll
@@ -565,216 +570,313 @@ __device__ __forceinline__ void rv_chains (const tbf_inst_const& K, tbf_rv_state
 			row[i0 + k]    = t;
 		}
 	}
-	st.bq[q][2 * c]     = s7;
-	st.bq[q][2 * c + 1] = s8;
+	st7 = s7;
+	st8 = s8;
 }
 
-/* b_reverb::reverb (src/reverb.cpp:274-794), 64-sample sub-blocks, lane = sample.
- * All 13 rings are >= 560 samples long (the reference's fixed A..F settings), so every
- * ring read of a sub-block precedes the ring writes of that sub-block.  Serial parts:
- * the two dither sequences (scalar unit); biquadA (predelay output) and biquadB (tap
- * mix) of both channels together on lanes 0..3 -- their inputs are known once the reads
- * are done; biquadC on lanes 0,1. */
-__device__ void stage_reverb (const tbf_launch& P, RvLds& sm, const tbf_seg_ctl& G, const tbf_inst_const& K,
-                              double* __restrict__ slab, float* __restrict__ out)
+/* xorshift dither streams of one sub-block by GF(2) jumps: fpd[c][0] = state before
+ * sample 0, fpd[c][n + 1] = state after sample n */
+__device__ __forceinline__ void rv_dither (const uint32_t* __restrict__ J, uint32_t& sL, uint32_t& sR,
+                                           uint32_t (*fpd)[TBF_SUB + 1])
 {
-	const int     lane = threadIdx.x;
-	tbf_rv_state& st   = sm.st;
-	const double  wet  = G.rvWet;
-
-#pragma unroll 1
-	for (int sb = 0; sb < TBF_BLK / TBF_SUB; sb++) {
-		const int n = lane; /* sample within the sub-block */
-		/* dither sequences (src/reverb.cpp:775-783) on the scalar unit, into lanes */
-		{
-			uint32_t       fL = __builtin_amdgcn_readfirstlane (st.fpdL);
-			uint32_t       fR = __builtin_amdgcn_readfirstlane (st.fpdR);
-			const uint32_t gL = fL, gR = fR;
-			uint32_t       nL = 0, nR = 0;
-			for (int i = 0; i < TBF_SUB; i++) {
-				fL = xorshift (fL);
-				fR = xorshift (fR);
-				nL = (lane == i) ? fL : nL;
-				nR = (lane == i) ? fR : nR;
-			}
-			sm.fpd[0][lane + 1] = nL;
-			sm.fpd[1][lane + 1] = nR;
-			__syncthreads (); /* all lanes have read st.fpdL/R */
-			if (lane == 0) {
-				sm.fpd[0][0] = gL;
-				sm.fpd[1][0] = gR;
-				st.fpdL      = fL;
-				st.fpdR      = fR;
-			}
-		}
-		TBF_MARK (5);
-		const double inS = (double)sm.in[sb * TBF_SUB + n];
-		/* ---- predelay M (line 12) ---- */
-		const int dM  = K.delay[12];
-		const int cMn = cnt_adv (st.count[12], dM, n);     /* write slot */
-		const int cMr = cnt_adv (st.count[12], dM, n + 1); /* read slot  */
-		double*   mL  = slab + K.ringOff[12];
-		double*   mR  = slab + K.ringOff[13 + 12];
-		sm.a[0][n]    = mL[cMr];
-		sm.a[1][n]    = mR[cMr];
-		/* ---- allpass reads (lines 8..11) ---- */
-		double apOld[2][4];
-		int    apW[4];
-		for (int l = 8; l < 12; l++) {
-			const int d     = K.delay[l];
-			const int cr    = cnt_adv (st.count[l], d, n + 1);
-			apW[l - 8]      = cnt_adv (st.count[l], d, n);
-			apOld[0][l - 8] = slab[K.ringOff[l] + cr];
-			apOld[1][l - 8] = slab[K.ringOff[13 + l] + cr];
-		}
-		/* ---- delay-line taps (lines 0..7) with the vibrato offsets; Householder
-		 * feedback and tap mix (src/reverb.cpp:479-560, 686-724) ---- */
-		double fb[2][8];
-#pragma unroll
-		for (int c = 0; c < 2; c++) {
-			/* pass 1: vibrato phases and offsets (one sin per line) -> LDS */
-#pragma unroll 1
-			for (int l = 0; l < 8; l++) {
-				const double v0 = st.vib[c][l], dl = K.vibDelta[l];
-				double       D, v;
-				if (phase_run (v0, dl, TBF_SUB, D)) {
-					v = v0 + (double)(n + 1) * D;
-				} else {
-					v = v0;
-					for (int i = 0; i <= n; i++)
-						v += dl;
-				}
-				sm.t[l][n] = (sin (v) + 1.0) * K.vibDepth;
-				if (n == TBF_SUB - 1)
-					sm.vn[c][l] = v;
-			}
-			/* pass 2: the 16 two-tap reads of the channel and their interpolation */
-			double I[8];
-#pragma unroll
-			for (int l = 0; l < 8; l++) {
-				const int     d   = K.delay[l];
-				const int     cn  = cnt_adv (st.count[l], d, n + 1);
-				const double  off = sm.t[l][n];
-				const int     wk  = (int)(cn + off);
-				const int     w0  = wk - ((wk > d) ? d + 1 : 0);
-				const int     w1  = wk + 1 - ((wk + 1 > d) ? d + 1 : 0);
-				const double* a   = slab + K.ringOff[c * 13 + l];
-				const double  fr  = off - floor (off);
-				const double  r0  = a[w0];
-				const double  r1  = a[w1];
-				double        x   = (r0 * (1 - fr));
-				x += (r1 * fr);
-				I[l] = ((1.0 - K.blend) * x) + (r0 * K.blend);
-			}
-			I[0]     = (I[0] * K.oneMinusAbsCm) + (I[4] * K.crossmod);
-			I[4]     = (I[4] * K.oneMinusAbsCm) + (I[0] * K.crossmod);
-			fb[c][0] = (I[0] - (I[1] + I[2] + I[3])) * K.regen;
-			fb[c][1] = (I[1] - (I[0] + I[2] + I[3])) * K.regen;
-			fb[c][2] = (I[2] - (I[0] + I[1] + I[3])) * K.regen;
-			fb[c][3] = (I[3] - (I[0] + I[1] + I[2])) * K.regen;
-			fb[c][4] = (I[4] - (I[5] + I[6] + I[7])) * K.regen;
-			fb[c][5] = (I[5] - (I[4] + I[6] + I[7])) * K.regen;
-			fb[c][6] = (I[6] - (I[4] + I[5] + I[7])) * K.regen;
-			fb[c][7] = (I[7] - (I[4] + I[5] + I[6])) * K.regen;
-			sm.b[c][n] = (I[0] + I[1] + I[2] + I[3] + I[4] + I[5] + I[6] + I[7]) / 8.0;
-		}
-		TBF_MARK (6);
-		__syncthreads (); /* all ring reads of the sub-block are complete */
-		if (lane < 16)
-			st.vib[lane >> 3][lane & 7] = sm.vn[lane >> 3][lane & 7];
-#pragma unroll
-		for (int c = 0; c < 2; c++) {
-			double x = inS;
-			if (fabs (x) < 1.18e-23)
-				x = sm.fpd[c][n] * 1.18e-17;
-			(c ? mR : mL)[cMn] = x;
-		}
-		/* ---- biquadA (predelay out) and biquadB (tap mix), both channels, lanes 0..3 ---- */
-		if (lane < 4)
-			rv_chains (K, st, lane < 2 ? sm.a[lane] : sm.b[lane - 2], lane >> 1, lane & 1);
-		__syncthreads ();
-		TBF_MARK (7);
-		/* ---- allpasses and delay-line writes; clamp + asin of the biquadB output ---- */
-		static const int srcAp[8] = {3, 2, 1, 0, 0, 1, 2, 3};
-#pragma unroll
-		for (int c = 0; c < 2; c++) {
-			const double a0 = sin (sm.a[c][n] * wet);
-			double       ap[4];
-			for (int l = 0; l < 4; l++) {
-				double a = a0;
-				a -= apOld[c][l] * 0.5;
-				slab[K.ringOff[c * 13 + 8 + l] + apW[l]] = a;
-				a *= 0.5;
-				a += apOld[c][l];
-				ap[l] = a;
-			}
-			for (int l = 0; l < 8; l++) {
-				double prev = __shfl_up (fb[c][l], 1);
-				if (lane == 0)
-					prev = st.fb[c][l];
-				slab[K.ringOff[c * 13 + l] + cnt_adv (st.count[l], K.delay[l], n)] = ap[srcAp[l]] + prev;
-				if (lane == NL - 1)
-					sm.fbn[c][l] = fb[c][l];
-			}
-			double y = sm.b[c][n];
-			if (y > 1.0) y = 1.0;
-			if (y < -1.0) y = -1.0;
-			sm.b[c][n] = asin (y);
-		}
-		__syncthreads ();
-		if (lane < 16)
-			st.fb[lane >> 3][lane & 7] = sm.fbn[lane >> 3][lane & 7];
-		TBF_MARK (8);
-		/* ---- biquadC, lanes 0,1 ---- */
-		if (lane < 2)
-			rv_chains (K, st, sm.b[lane], 2, lane);
-		__syncthreads ();
-		TBF_MARK (9);
-		double o[2];
-#pragma unroll
-		for (int c = 0; c < 2; c++) {
-			double x = sm.b[c][n];
-			if (wet != 1.0) {
-				double dry = inS;
-				if (fabs (dry) < 1.18e-23)
-					dry = sm.fpd[c][n] * 1.18e-17;
-				x += (dry * (1.0 - wet));
-			}
-			o[c] = dither_add (x, sm.fpd[c][n + 1]);
-		}
-		out[sb * TBF_SUB + n] = (float)(0.7071067811865476 * (o[0] + o[1]));
-		__syncthreads ();
-		if (lane < 13)
-			st.count[lane] = cnt_adv (st.count[lane], K.delay[lane], TBF_SUB);
-		__syncthreads ();
-		TBF_MARK (10);
+	const int      lane = threadIdx.x;
+	const uint32_t gL = sL, gR = sR;
+	fpd[0][lane + 1]  = xs_jump (J, gL, lane + 1);
+	fpd[1][lane + 1]  = xs_jump (J, gR, lane + 1);
+	__syncthreads (); /* all lanes have read sL/sR */
+	if (lane == 0) {
+		fpd[0][0] = gL;
+		fpd[1][0] = gR;
+		sL        = fpd[0][TBF_SUB];
+		sR        = fpd[1][TBF_SUB];
 	}
+	__syncthreads ();
 }
 
-__global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL), amdgpu_waves_per_eu (RV_WAVES)))
-k_reverb (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_seg_ctl* __restrict__ ctl)
+struct RvInLds {
+	tbf_rv_state st;
+	double       a[2][TBF_SUB];
+	uint32_t     fpd[2][TBF_SUB + 1];
+	unsigned long long prof[TBF_PROF_SLOTS];
+	unsigned long long plast;
+};
+
+struct RvOutLds {
+	tbf_rv_state st;
+	double       b[2][TBF_SUB];
+	uint32_t     fpd[2][TBF_SUB + 1];
+	unsigned long long prof[TBF_PROF_SLOTS];
+	unsigned long long plast;
+};
+
+struct RvCoreLds {
+	tbf_rv_state st;
+	unsigned long long prof[TBF_PROF_SLOTS];
+	unsigned long long plast;
+};
+
+/* FP64 stage buffers of one chunk: [inst][c][midStride] */
+__device__ __forceinline__ double* rv_buf (double* base, const tbf_launch& P, uint32_t inst, int c)
 {
-	__shared__ RvLds sm;
+	return base + ((size_t)inst * 2 + c) * P.midStride;
+}
+
+__global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL), amdgpu_waves_per_eu (RVIO_WAVES)))
+k_rv_in (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_seg_ctl* __restrict__ ctl)
+{
+	__shared__ RvInLds sm;
 	const int      lane = threadIdx.x;
 	const uint32_t inst = blockIdx.x + P.instBase;
 	if (inst >= P.nInst)
 		return;
 	const tbf_inst_const& K    = cst[inst];
-	const tbf_seg_ctl&    G    = ctl[inst];
+	const double          wet  = ctl[inst].rvWet;
+	tbf_rv_state*         S    = &P.st[inst].rv;
+	double*               mL   = P.rslab + (size_t)inst * P.slabLen + K.ringOff[12];
+	double*               mR   = P.rslab + (size_t)inst * P.slabLen + K.ringOff[13 + 12];
+	const int             dM   = K.delay[12];
+	double*               a0L  = rv_buf (P.rvA, P, inst, 0);
+	double*               a0R  = rv_buf (P.rvA, P, inst, 1);
+	prof_begin (P, sm);
+	copy_words (&sm.st, S);
+	__syncthreads ();
+	tbf_rv_state& st = sm.st;
+	for (uint32_t blk = 0; blk < P.nBlocks; blk++) {
+		const float* in = P.mid1 + (size_t)inst * P.midStride + (size_t)blk * TBF_BLK;
+#pragma unroll 1
+		for (int sb = 0; sb < TBF_BLK / TBF_SUB; sb++) {
+			const int n = lane;
+			rv_dither (P.xsJump, st.fpdL, st.fpdR, sm.fpd);
+			TBF_MARK (5);
+			const double inS = (double)in[sb * TBF_SUB + n];
+			/* predelay M (src/reverb.cpp:350-358): write at count, read at count + 1 */
+			const int cMn = cnt_adv (st.count[12], dM, n);
+			const int cMr = cnt_adv (st.count[12], dM, n + 1);
+			sm.a[0][n]    = mL[cMr];
+			sm.a[1][n]    = mR[cMr];
+			__syncthreads (); /* every read of the sub-block precedes its writes */
+#pragma unroll
+			for (int c = 0; c < 2; c++) {
+				double x = inS;
+				if (fabs (x) < 1.18e-23)
+					x = sm.fpd[c][n] * 1.18e-17;
+				(c ? mR : mL)[cMn] = x;
+			}
+			/* biquadA, both channels: lanes 0, 1 */
+			if (lane < 2)
+				rv_chain (K.bq[0], st.bq[0][2 * lane], st.bq[0][2 * lane + 1], sm.a[lane]);
+			__syncthreads ();
+			TBF_MARK (6);
+			const size_t o = (size_t)blk * TBF_BLK + sb * TBF_SUB + n;
+			a0L[o]         = sin (sm.a[0][n] * wet);
+			a0R[o]         = sin (sm.a[1][n] * wet);
+			if (lane == 0)
+				st.count[12] = cnt_adv (st.count[12], dM, TBF_SUB);
+			__syncthreads ();
+			TBF_MARK (7);
+		}
+	}
+	__syncthreads ();
+	copy_words (S, &sm.st);
+	prof_end (P, sm, inst);
+}
+
+/* One channel of k_rv_core for a 64-sample sub-block: allpasses I..L (lines 8-11),
+ * delay lines A..H (0-7) with the vibrato-modulated two-tap reads, crossmod and
+ * Householder feedback (src/reverb.cpp:381-730).  Every read of the channel's rings
+ * precedes every write (all ring delays >= 560 > 64). */
+__device__ __forceinline__ void rv_core_channel (const tbf_launch& P, RvCoreLds& sm, const tbf_inst_const& K,
+                                                 double* __restrict__ slab, int c, size_t o, double a0,
+                                                 double* __restrict__ bout)
+{
+	const int     lane = threadIdx.x;
+	const int     n    = lane;
+	tbf_rv_state& st   = sm.st;
+	/* allpass reads at count + 1 */
+	double apOld[4];
+	int    apW[4];
+#pragma unroll
+	for (int l = 8; l < 12; l++) {
+		const int d = K.delay[l];
+		apW[l - 8]  = cnt_adv (st.count[l], d, n);
+		apOld[l - 8] = slab[K.ringOff[c * 13 + l] + cnt_adv (st.count[l], d, n + 1)];
+	}
+	/* modulated taps: phase (closed form when exact, else the literal recurrence),
+	 * offset, two-tap interpolation and blend */
+	double I[8];
+#pragma unroll
+	for (int l = 0; l < 8; l++) {
+		const double v0 = st.vib[c][l], dl = K.vibDelta[l];
+		double       D, v;
+		if (phase_run (v0, dl, TBF_SUB, D)) {
+			v = v0 + (double)(n + 1) * D;
+		} else {
+			v = v0;
+			for (int i = 0; i <= n; i++)
+				v += dl;
+		}
+		if (lane == NL - 1) /* every lane has read st.vib[c][l] above (one wave, program order) */
+			st.vib[c][l] = v;
+		const double  off = (sin (v) + 1.0) * K.vibDepth;
+		const int     d   = K.delay[l];
+		const int     cn  = cnt_adv (st.count[l], d, n + 1);
+		const int     wk  = (int)(cn + off);
+		const int     w0  = wk - ((wk > d) ? d + 1 : 0);
+		const int     w1  = wk + 1 - ((wk + 1 > d) ? d + 1 : 0);
+		const double* a   = slab + K.ringOff[c * 13 + l];
+		const double  fr  = off - floor (off);
+		const double  r0  = a[w0];
+		const double  r1  = a[w1];
+		double        x   = (r0 * (1 - fr));
+		x += (r1 * fr);
+		I[l] = ((1.0 - K.blend) * x) + (r0 * K.blend);
+#ifdef RV_SCHED_BARRIER
+		__builtin_amdgcn_sched_barrier (0); /* one line at a time: bounds register pressure */
+#endif
+	}
+	I[0] = (I[0] * K.oneMinusAbsCm) + (I[4] * K.crossmod);
+	I[4] = (I[4] * K.oneMinusAbsCm) + (I[0] * K.crossmod);
+	double fb[8];
+	fb[0] = (I[0] - (I[1] + I[2] + I[3])) * K.regen;
+	fb[1] = (I[1] - (I[0] + I[2] + I[3])) * K.regen;
+	fb[2] = (I[2] - (I[0] + I[1] + I[3])) * K.regen;
+	fb[3] = (I[3] - (I[0] + I[1] + I[2])) * K.regen;
+	fb[4] = (I[4] - (I[5] + I[6] + I[7])) * K.regen;
+	fb[5] = (I[5] - (I[4] + I[6] + I[7])) * K.regen;
+	fb[6] = (I[6] - (I[4] + I[5] + I[7])) * K.regen;
+	fb[7] = (I[7] - (I[4] + I[5] + I[6])) * K.regen;
+	bout[o] = (I[0] + I[1] + I[2] + I[3] + I[4] + I[5] + I[6] + I[7]) / 8.0;
+	__syncthreads (); /* all ring reads of the channel are complete */
+	/* allpass writes (a = a0 - old/2 at count; out = a/2 + old) */
+	double ap[4];
+#pragma unroll
+	for (int l = 0; l < 4; l++) {
+		double a = a0;
+		a -= apOld[l] * 0.5;
+		slab[K.ringOff[c * 13 + 8 + l] + apW[l]] = a;
+		a *= 0.5;
+		a += apOld[l];
+		ap[l] = a;
+	}
+	/* delay-line writes: allpass output + the previous sample's feedback */
+	const int srcAp[8] = {3, 2, 1, 0, 0, 1, 2, 3};
+#pragma unroll
+	for (int l = 0; l < 8; l++) {
+		double prev = __shfl_up (fb[l], 1);
+		if (lane == 0)
+			prev = st.fb[c][l];
+		slab[K.ringOff[c * 13 + l] + cnt_adv (st.count[l], K.delay[l], n)] = ap[srcAp[l]] + prev;
+	}
+	__syncthreads (); /* lane 0 has read st.fb */
+	if (lane == NL - 1) {
+#pragma unroll
+		for (int l = 0; l < 8; l++)
+			st.fb[c][l] = fb[l];
+	}
+	__syncthreads ();
+}
+
+__global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL), amdgpu_waves_per_eu (RV_WAVES)))
+k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
+{
+	__shared__ RvCoreLds sm;
+	const int      lane = threadIdx.x;
+	const uint32_t inst = blockIdx.x + P.instBase;
+	if (inst >= P.nInst)
+		return;
+	const tbf_inst_const& K    = cst[inst];
 	tbf_rv_state*         S    = &P.st[inst].rv;
 	double*               slab = P.rslab + (size_t)inst * P.slabLen;
 	prof_begin (P, sm);
 	copy_words (&sm.st, S);
 	__syncthreads ();
 	for (uint32_t blk = 0; blk < P.nBlocks; blk++) {
-		const float* in = P.mid1 + (size_t)inst * P.midStride + (size_t)blk * TBF_BLK;
-		sm.in[lane]      = in[lane];
-		sm.in[lane + NL] = in[lane + NL];
-		__syncthreads ();
-		float* out = P.chain == TBF_CHAIN_TAP_REVERB
-		                 ? P.outL + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK
-		                 : P.mid2 + (size_t)inst * P.midStride + (size_t)blk * TBF_BLK;
-		stage_reverb (P, sm, G, K, slab, out);
+#pragma unroll 1
+		for (int sb = 0; sb < TBF_BLK / TBF_SUB; sb++) {
+			const size_t o = (size_t)blk * TBF_BLK + sb * TBF_SUB + lane;
+			rv_core_channel (P, sm, K, slab, 0, o, rv_buf (P.rvA, P, inst, 0)[o], rv_buf (P.rvB, P, inst, 0));
+			TBF_MARK (8);
+			rv_core_channel (P, sm, K, slab, 1, o, rv_buf (P.rvA, P, inst, 1)[o], rv_buf (P.rvB, P, inst, 1));
+			if (lane < 12)
+				sm.st.count[lane] = cnt_adv (sm.st.count[lane], K.delay[lane], TBF_SUB);
+			__syncthreads ();
+			TBF_MARK (9);
+		}
+	}
+	__syncthreads ();
+	copy_words (S, &sm.st);
+	prof_end (P, sm, inst);
+}
+
+__global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL), amdgpu_waves_per_eu (RVIO_WAVES)))
+k_rv_out (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_seg_ctl* __restrict__ ctl)
+{
+	__shared__ RvOutLds sm;
+	const int      lane = threadIdx.x;
+	const uint32_t inst = blockIdx.x + P.instBase;
+	if (inst >= P.nInst)
+		return;
+	const tbf_inst_const& K   = cst[inst];
+	const double          wet = ctl[inst].rvWet;
+	tbf_rv_state*         S   = &P.st[inst].rv;
+	const double*         bL  = rv_buf (P.rvB, P, inst, 0);
+	const double*         bR  = rv_buf (P.rvB, P, inst, 1);
+	prof_begin (P, sm);
+	copy_words (&sm.st, S);
+	__syncthreads ();
+	tbf_rv_state& st = sm.st;
+	for (uint32_t blk = 0; blk < P.nBlocks; blk++) {
+		const float* in  = P.mid1 + (size_t)inst * P.midStride + (size_t)blk * TBF_BLK;
+		float*       out = P.chain == TBF_CHAIN_TAP_REVERB
+		                       ? P.outL + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK
+		                       : P.mid2 + (size_t)inst * P.midStride + (size_t)blk * TBF_BLK;
+#pragma unroll 1
+		for (int sb = 0; sb < TBF_BLK / TBF_SUB; sb++) {
+			const int n = lane;
+			rv_dither (P.xsJump, st.fpdL2, st.fpdR2, sm.fpd);
+			TBF_MARK (10);
+			const size_t o = (size_t)blk * TBF_BLK + sb * TBF_SUB + n;
+			sm.b[0][n]     = bL[o];
+			sm.b[1][n]     = bR[o];
+			__syncthreads ();
+			/* biquadB (src/reverb.cpp:733-741), lanes 0, 1 */
+			if (lane < 2)
+				rv_chain (K.bq[1], st.bq[1][2 * lane], st.bq[1][2 * lane + 1], sm.b[lane]);
+			__syncthreads ();
+			TBF_MARK (11);
+			/* clamp + asin (743-751) */
+#pragma unroll
+			for (int c = 0; c < 2; c++) {
+				double y = sm.b[c][n];
+				if (y > 1.0) y = 1.0;
+				if (y < -1.0) y = -1.0;
+				sm.b[c][n] = asin (y);
+			}
+			__syncthreads ();
+			TBF_MARK (12);
+			/* biquadC (756-764), lanes 0, 1 */
+			if (lane < 2)
+				rv_chain (K.bq[2], st.bq[2][2 * lane], st.bq[2][2 * lane + 1], sm.b[lane]);
+			__syncthreads ();
+			TBF_MARK (13);
+			/* dry mix, dither, mono sum (766-787) */
+			const double inS = (double)in[sb * TBF_SUB + n];
+			double       ov[2];
+#pragma unroll
+			for (int c = 0; c < 2; c++) {
+				double x = sm.b[c][n];
+				if (wet != 1.0) {
+					double dry = inS;
+					if (fabs (dry) < 1.18e-23)
+						dry = sm.fpd[c][n] * 1.18e-17;
+					x += (dry * (1.0 - wet));
+				}
+				ov[c] = dither_add (x, sm.fpd[c][n + 1]);
+			}
+			out[sb * TBF_SUB + n] = (float)(0.7071067811865476 * (ov[0] + ov[1]));
+			__syncthreads ();
+			TBF_MARK (14);
+		}
 		if (P.chain == TBF_CHAIN_TAP_REVERB) {
 			float* oR = P.outR + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
 			oR[lane]      = out[lane];
@@ -959,7 +1061,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 		sm.brake = brake;
 	}
 	__syncthreads ();
-	TBF_MARK (11);
+	TBF_MARK (20);
 	const double   hornIncr = st.hornIncr, drumIncr = st.drumIncr;
 	const uint32_t WM       = (uint32_t)W - 1u;
 	/* serial filter coefficients: lane 0 horn A, lanes 1-2 drum shelf */
@@ -1047,7 +1149,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 				st.drumAngle = a;
 		}
 		__syncthreads ();
-		TBF_MARK (12);
+		TBF_MARK (21);
 		/* reflection filters FILTER_C (src/whirl.cpp:1472-1477), lane-parallel */
 		const float xf   = sm.xf[n + 4];
 		const float xfp  = n == 0 ? st.z[0] : sm.xf[n + 3];
@@ -1064,7 +1166,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 		sm.x2[n + 4]     = x2v;
 		const float xd2v = (float)((0.4 * xd1v) + (0.4 * sm.xd1[n]));
 		__syncthreads ();
-		TBF_MARK (13);
+		TBF_MARK (22);
 
 		/* ---- per ring (HL, HR, DL, DR): its three motions, then the ordered adds ---- */
 		const double ha = sm.ang[0][n];
@@ -1114,7 +1216,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 				ma[q]          = xa - qq;
 				mb[q]          = qq;
 			}
-			TBF_MARK (14);
+			TBF_MARK (23);
 			/* fast path preconditions (wave vote): each motion's slot non-decreasing in n
 			 * with groups of <= 2 equal slots, and the ring's motions >= 2 slots apart in
 			 * source order at every sample (so passes farthest-first keep the per-slot
@@ -1153,7 +1255,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 				}
 				__syncthreads ();
 			}
-			TBF_MARK (15);
+			TBF_MARK (24);
 		}
 		/* ---- outputs (whirlProc2 outHL/outHR/outDL/outDR + whirlProc3 mix) ---- */
 		{
@@ -1182,7 +1284,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 			st.outpos = (st.outpos + TBF_SUB) & 2047u;
 		}
 		__syncthreads ();
-		TBF_MARK (16);
+		TBF_MARK (25);
 	}
 	if (lane == 0) {
 		/* NaN scrub, src/whirl.cpp:1622-1630 */
@@ -1216,7 +1318,7 @@ k_whirl (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 	for (uint32_t i = threadIdx.x; i < 4u * W; i += NL)
 		(&sm.wring[0][0])[i] = wr[i];
 	__syncthreads ();
-	TBF_MARK (17);
+	TBF_MARK (26);
 	for (uint32_t blk = 0; blk < P.nBlocks; blk++) {
 		const float* in = P.mid2 + (size_t)inst * P.midStride + (size_t)blk * TBF_BLK;
 		float*       oL = P.outL + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
@@ -1227,12 +1329,12 @@ k_whirl (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 	copy_words (S, &sm.st);
 	for (uint32_t i = threadIdx.x; i < 4u * W; i += NL)
 		wr[i] = (&sm.wring[0][0])[i];
-	TBF_MARK (19);
+	TBF_MARK (27);
 	prof_end (P, sm, inst);
 }
 
 /* ------------------------------------------------------------------ launch */
-/* stage k (0 k_tonegen, 1 k_reverb, 2 k_whirl) of one launch chunk; the chain mode
+/* stage k (0 k_tonegen, 1 k_rv_in, 2 k_rv_core, 3 k_rv_out, 4 k_whirl) of one launch chunk; the chain mode
  * decides which stages run (tbf_chain_stages) */
 extern "C" int tbf_launch_stage (const tbf_launch* P, int k, hipStream_t stream)
 {
@@ -1244,8 +1346,12 @@ extern "C" int tbf_launch_stage (const tbf_launch* P, int k, hipStream_t stream)
 	if (k == 0)
 		hipLaunchKernelGGL (k_tonegen, grid, block, 0, stream, *P, P->ctl, P->tpls, P->cst);
 	else if (k == 1)
-		hipLaunchKernelGGL (k_reverb, grid, block, 0, stream, *P, P->cst, P->ctl);
-	else if (k == 2) {
+		hipLaunchKernelGGL (k_rv_in, grid, block, 0, stream, *P, P->cst, P->ctl);
+	else if (k == 2)
+		hipLaunchKernelGGL (k_rv_core, grid, block, 0, stream, *P, P->cst);
+	else if (k == 3)
+		hipLaunchKernelGGL (k_rv_out, grid, block, 0, stream, *P, P->cst, P->ctl);
+	else if (k == 4) {
 		switch (P->wringLen) {
 			case 512: hipLaunchKernelGGL (k_whirl<512>, grid, block, 0, stream, *P, P->cst, P->ctl); break;
 			case 1024: hipLaunchKernelGGL (k_whirl<1024>, grid, block, 0, stream, *P, P->cst, P->ctl); break;
@@ -1260,5 +1366,5 @@ extern "C" int tbf_launch_stage (const tbf_launch* P, int k, hipStream_t stream)
 /* number of stages the chain mode runs */
 extern "C" int tbf_chain_stages (uint32_t chain)
 {
-	return chain == TBF_CHAIN_TONEGEN || chain == TBF_CHAIN_TAP_PREAMP ? 1 : (chain == TBF_CHAIN_TAP_REVERB ? 2 : 3);
+	return chain == TBF_CHAIN_TONEGEN || chain == TBF_CHAIN_TAP_PREAMP ? 1 : (chain == TBF_CHAIN_TAP_REVERB ? 4 : 5);
 }

@@ -14,7 +14,8 @@
 #define TBF_SUB 64    /* sub-block for reverb/whirl: one sample per lane of a wave64 */
 #define TBF_NW 256    /* NOF_WHEELS, src/tonegen.h:79 */
 #define TBF_PROF_SLOTS 32
-#define TBF_VRING 256 /* compact vibrato ring (reference 1024; live window <= 21+128) */
+#define TBF_VRING 256
+#define TBF_XS_JUMP 129 /* dither jump table columns: k = 0 .. 128 steps */ /* compact vibrato ring (reference 1024; live window <= 21+128) */
 
 /* one core-program entry = one wheel's contribution for one block
  * (CoreIns, src/tonegen.h:114-129; wrap splitting is done on the device) */
@@ -88,10 +89,11 @@ typedef struct tbf_tg_state { /* tonegen + vibrato + overdrive: k_tonegen */
 	uint32_t fpFlip, odFpd;
 } tbf_tg_state;
 
-typedef struct tbf_rv_state { /* reverb: k_reverb */
+typedef struct tbf_rv_state { /* reverb: k_rv_in / k_rv_core / k_rv_out */
 	int32_t  count[13];
-	uint32_t fpdL, fpdR;
-	uint32_t pad0;
+	uint32_t fpdL, fpdR;   /* dither streams as advanced by k_rv_in ... */
+	uint32_t fpdL2, fpdR2; /* ... and the identical copies advanced by k_rv_out */
+	uint32_t pad0[3];
 	double   bq[3][4]; /* [A/B/C][L7, L8, R9, R10] */
 	double   fb[2][8];
 	double   vib[2][8];
@@ -131,11 +133,14 @@ typedef struct tbf_launch {
 	float*                wring; /* [inst][4][wring_len] */
 	float*                mid1;  /* [inst][midStride] preamp output of the chunk */
 	float*                mid2;  /* [inst][midStride] reverb output of the chunk */
+	double*               rvA;   /* [inst][2][midStride] k_rv_in -> k_rv_core: sin(biquadA * wet) */
+	double*               rvB;   /* [inst][2][midStride] k_rv_core -> k_rv_out: tap mix */
 	uint64_t              midStride;
 	double*               rslab; /* [inst][slabLen] */
 	const tbf_seg_ctl*    ctl;
 	const tbf_prog_entry* prog;
 	const uint32_t*       vibTab; /* [3][2048] */
+	const uint32_t*       xsJump; /* [32][TBF_XS_JUMP]: xorshift32^k (1 << j), k = 0..128 */
 	const float*          whTab;  /* hnFwd, hnBwd, drFwd, drBwd [4][16384] */
 	const float*          whBw;   /* bfw, bbw [2][16384][5] */
 	float*                outL;

@@ -15,6 +15,10 @@ _dp = C.POINTER(C.c_double)
 _u32p = C.POINTER(C.c_uint32)
 
 
+# the render kernels of one launch chunk, in stream order (tbf_debug_kernel_times)
+STAGES = ("k_tonegen", "k_rv_in", "k_rv_core", "k_rv_out", "k_whirl")
+
+
 class TbfError(RuntimeError):
     pass
 
@@ -156,10 +160,10 @@ class Engine:
         if enable is not None:
             _check(fn(self._h, 1 if enable else -1, None, None))
             return None
-        ms = np.zeros(3, np.float64)
-        cnt = np.zeros(3, np.uint32)
+        ms = np.zeros(len(STAGES), np.float64)
+        cnt = np.zeros(len(STAGES), np.uint32)
         _check(fn(self._h, 0, ms.ctypes.data, cnt.ctypes.data))
-        return {k: (float(ms[i]), int(cnt[i])) for i, k in enumerate(("k_tonegen", "k_reverb", "k_whirl"))}
+        return {k: (float(ms[i]), int(cnt[i])) for i, k in enumerate(STAGES)}
 
     def error_flags(self):
         f = C.c_uint32()

@@ -53,6 +53,13 @@ for s in $STEPS; do
 		run ftraffic 60 python3 tools/traffic_from_pmc.py "$OUT/ffetch" "$OUT/fwrite" --out "$OUT/traffic.json"
 		run fbench 900 python3 bench.py --traffic "$OUT/traffic.json"
 		;;
+	kpmc)
+		BP="--steps 2 --warmup 1 --cpu-baseline 0 --check 0 --blocks 16"
+		run kp_a 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d "$OUT/kp_a" -o run --output-format csv -- python3 bench.py $BP
+		run kp_b 300 rocprofv3 --pmc SQ_WAVES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INST_LEVEL_VMEM -d "$OUT/kp_b" -o run --output-format csv -- python3 bench.py $BP
+		run kp_c 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_THREAD_CYCLES_VALU SQ_LDS_BANK_CONFLICT SQ_INST_CYCLES_VMEM_RD -d "$OUT/kp_c" -o run --output-format csv -- python3 bench.py $BP
+		run kp_sum 60 python3 tools/pmc_kernels.py 16 "$OUT/kp_a" "$OUT/kp_b" "$OUT/kp_c"
+		;;
 	calib)
 		run calib_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/calib_fetch" -o run --output-format csv -- python3 tools/calib_pmc.py
 		run calib_write 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/calib_write" -o run --output-format csv -- python3 tools/calib_pmc.py

@@ -366,7 +366,7 @@ int tbf_instances_add (tbf_engine* e, uint32_t n, const uint32_t* tpl_ids, const
 		GlibcRand rnd (seeds[q]);
 		for (int c = 0; c < 2; c++)
 			for (int l = 0; l < 8; l++)
-				in.s0.rv.vib[c][l] = rnd.next () - 2147483647 / 2;
+				in.s0.rv.ch[c].vib[l] = rnd.next () - 2147483647 / 2;
 		uint32_t f = 1;
 		while (f < 16386)
 			f = (uint32_t)rnd.next () * 0xFFFFFFFFu;
@@ -382,8 +382,10 @@ int tbf_instances_add (tbf_engine* e, uint32_t n, const uint32_t* tpl_ids, const
 			f = (uint32_t)rnd.next () * 0xFFFFFFFFu;
 		in.s0.tg.odFpd  = f;
 		in.s0.tg.fpFlip = 1;
-		for (int l = 0; l < 13; l++)
-			in.s0.rv.count[l] = 1;
+		in.s0.rv.countM = 1;
+		for (int c = 0; c < 2; c++)
+			for (int l = 0; l < 12; l++)
+				in.s0.rv.ch[c].count[l] = 1;
 		reverbConsts (in.k, sr, 1.0f, 0.2f, 0.0f, 0.0f, 0.4f, 0.8f);
 		whirlConsts (in.k, e->wt);
 		/* initWhirl -> computeRotationSpeeds -> setRevSelect(0) -> useRevOption(4) */

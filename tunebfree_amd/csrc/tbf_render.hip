@@ -147,16 +147,36 @@ __device__ __forceinline__ uint32_t xorshift (uint32_t s)
 }
 
 /* xorshift32 state after k steps from x0 (uniform), k per lane (0 .. 128), by the
- * GF(2) jump table: coalesced row reads, one per set bit of x0 */
+ * GF(2) jump table: 32 coalesced row reads, selected by the bits of x0 */
 __device__ __forceinline__ uint32_t xs_jump (const uint32_t* __restrict__ J, uint32_t x0, int k)
 {
-	x0         = __builtin_amdgcn_readfirstlane (x0);
+	x0 = __builtin_amdgcn_readfirstlane (x0);
+	/* opaque k: keeps the loop-invariant table loads inside the block loop instead of
+	 * pinning 32 VGPRs for the whole kernel */
+	asm volatile ("" : "+v"(k));
 	uint32_t r = 0;
-	while (x0) {
-		const int j = __builtin_ctz (x0);
-		r ^= J[j * TBF_XS_JUMP + k];
-		x0 &= x0 - 1;
+#pragma unroll
+	for (int h = 0; h < 32; h += 16) {
+		uint32_t v[16];
+#pragma unroll
+		for (int j = 0; j < 16; j++) /* 16 row loads in flight together */
+			v[j] = J[(h + j) * TBF_XS_JUMP + k];
+#pragma unroll
+		for (int j = 0; j < 16; j++)
+			r ^= ((x0 >> (h + j)) & 1u) ? v[j] : 0u;
 	}
+	return r;
+}
+
+/* xorshift32 state after a uniform k steps from a per-lane x: column k of the table is
+ * uniform, so its 32 words come in as scalar loads */
+__device__ __forceinline__ uint32_t xs_jump_u (const uint32_t* __restrict__ J, uint32_t x, int k)
+{
+	asm volatile ("" : "+s"(k));
+	uint32_t r = 0;
+#pragma unroll
+	for (int j = 0; j < 32; j++)
+		r ^= ((x >> j) & 1u) ? J[j * TBF_XS_JUMP + k] : 0u;
 	return r;
 }
 
@@ -423,8 +443,9 @@ __device__ void stage_overdrive (const tbf_launch& P, TgLds& sm, const tbf_seg_c
 	/* xorshift dither states F[0..128] (F[n+1] after sample n) by GF(2) jumps */
 	{
 		const uint32_t f0 = st.odFpd;
-		sm.u.od.fpd[lane + 1]      = xs_jump (P.xsJump, f0, lane + 1);
-		sm.u.od.fpd[lane + 1 + NL] = xs_jump (P.xsJump, f0, lane + 1 + NL);
+		const uint32_t lo          = xs_jump (P.xsJump, f0, lane + 1);
+		sm.u.od.fpd[lane + 1]      = lo;
+		sm.u.od.fpd[lane + 1 + NL] = xs_jump_u (P.xsJump, lo, NL);
 		__syncthreads (); /* all lanes have read st.odFpd */
 		if (lane == 0) {
 			sm.u.od.fpd[0] = f0;
@@ -609,8 +630,11 @@ struct RvOutLds {
 	unsigned long long plast;
 };
 
+#define RV_WIN 72 /* tap window per line: 64 samples + max offset 2 * vibDepth (5.4) + 2 */
+
 struct RvCoreLds {
-	tbf_rv_state st;
+	tbf_rv_chan st;
+	double      tap[8][TBF_SUB]; /* tap offsets of the sub-block */
 	unsigned long long prof[TBF_PROF_SLOTS];
 	unsigned long long plast;
 };
@@ -650,8 +674,8 @@ k_rv_in (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 			TBF_MARK (5);
 			const double inS = (double)in[sb * TBF_SUB + n];
 			/* predelay M (src/reverb.cpp:350-358): write at count, read at count + 1 */
-			const int cMn = cnt_adv (st.count[12], dM, n);
-			const int cMr = cnt_adv (st.count[12], dM, n + 1);
+			const int cMn = cnt_adv (st.countM, dM, n);
+			const int cMr = cnt_adv (st.countM, dM, n + 1);
 			sm.a[0][n]    = mL[cMr];
 			sm.a[1][n]    = mR[cMr];
 			__syncthreads (); /* every read of the sub-block precedes its writes */
@@ -671,7 +695,7 @@ k_rv_in (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 			a0L[o]         = sin (sm.a[0][n] * wet);
 			a0R[o]         = sin (sm.a[1][n] * wet);
 			if (lane == 0)
-				st.count[12] = cnt_adv (st.count[12], dM, TBF_SUB);
+				st.countM = cnt_adv (st.countM, dM, TBF_SUB);
 			__syncthreads ();
 			TBF_MARK (7);
 		}
@@ -681,32 +705,50 @@ k_rv_in (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 	prof_end (P, sm, inst);
 }
 
-/* One channel of k_rv_core for a 64-sample sub-block: allpasses I..L (lines 8-11),
- * delay lines A..H (0-7) with the vibrato-modulated two-tap reads, crossmod and
- * Householder feedback (src/reverb.cpp:381-730).  Every read of the channel's rings
- * precedes every write (all ring delays >= 560 > 64). */
+/* One channel of the feedback network for a 64-sample sub-block: allpasses I..L
+ * (lines 8-11), delay lines A..H (0-7) with vibrato-modulated two-tap reads, crossmod
+ * and Householder feedback (src/reverb.cpp:381-730).  The two channels never mix
+ * inside the network, so each is its own wave.  Every read of the channel's rings
+ * precedes every write (all ring delays >= 560 > 64).  The tap reads of a sub-block
+ * fall in slots count+1 .. count+64+7 of each line, so those windows are fetched first
+ * with coalesced loads (one HBM round trip for all 8 lines) and the modulated taps
+ * gather from LDS. */
 __device__ __forceinline__ void rv_core_channel (const tbf_launch& P, RvCoreLds& sm, const tbf_inst_const& K,
                                                  double* __restrict__ slab, int c, size_t o, double a0,
                                                  double* __restrict__ bout)
 {
-	const int     lane = threadIdx.x;
-	const int     n    = lane;
-	tbf_rv_state& st   = sm.st;
-	/* allpass reads at count + 1 */
+	const int    lane = threadIdx.x;
+	const int    n    = lane;
+	tbf_rv_chan& st   = sm.st;
+	/* windows of lines 0-7 and the allpass reads at count + 1, all in flight together */
 	double apOld[4];
 	int    apW[4];
 #pragma unroll
 	for (int l = 8; l < 12; l++) {
-		const int d = K.delay[l];
-		apW[l - 8]  = cnt_adv (st.count[l], d, n);
+		const int d  = K.delay[l];
+		apW[l - 8]   = cnt_adv (st.count[l], d, n);
 		apOld[l - 8] = slab[K.ringOff[c * 13 + l] + cnt_adv (st.count[l], d, n + 1)];
 	}
-	/* modulated taps: phase (closed form when exact, else the literal recurrence),
-	 * offset, two-tap interpolation and blend */
-	double I[8];
+	/* tap windows: slot count+1+lane and count+65+lane (lanes 0..7) of each line, loaded
+	 * into registers first so their latency overlaps the phase/sin loop below */
+	double wlo[8], whi[8];
 #pragma unroll
 	for (int l = 0; l < 8; l++) {
-		const double v0 = st.vib[c][l], dl = K.vibDelta[l];
+		const int     d  = K.delay[l];
+		const int     c1 = cnt_adv (st.count[l], d, 1);
+		const double* a  = slab + K.ringOff[c * 13 + l];
+		int           s0 = c1 + lane;
+		s0 -= (s0 > d) ? d + 1 : 0;
+		wlo[l] = a[s0];
+		int s1 = c1 + NL + (lane & (RV_WIN - NL - 1));
+		s1 -= (s1 > d) ? d + 1 : 0;
+		whi[l] = a[s1];
+	}
+	/* vibrato phases (closed form when exact, else the literal recurrence) and tap
+	 * offsets, one line at a time (bounds VGPRs); offsets parked in LDS */
+#pragma unroll 1
+	for (int l = 0; l < 8; l++) {
+		const double v0 = st.vib[l], dl = K.vibDelta[l];
 		double       D, v;
 		if (phase_run (v0, dl, TBF_SUB, D)) {
 			v = v0 + (double)(n + 1) * D;
@@ -715,24 +757,37 @@ __device__ __forceinline__ void rv_core_channel (const tbf_launch& P, RvCoreLds&
 			for (int i = 0; i <= n; i++)
 				v += dl;
 		}
-		if (lane == NL - 1) /* every lane has read st.vib[c][l] above (one wave, program order) */
-			st.vib[c][l] = v;
-		const double  off = (sin (v) + 1.0) * K.vibDepth;
-		const int     d   = K.delay[l];
-		const int     cn  = cnt_adv (st.count[l], d, n + 1);
-		const int     wk  = (int)(cn + off);
-		const int     w0  = wk - ((wk > d) ? d + 1 : 0);
-		const int     w1  = wk + 1 - ((wk + 1 > d) ? d + 1 : 0);
-		const double* a   = slab + K.ringOff[c * 13 + l];
-		const double  fr  = off - floor (off);
-		const double  r0  = a[w0];
-		const double  r1  = a[w1];
-		double        x   = (r0 * (1 - fr));
+		if (lane == NL - 1) /* every lane has read st.vib[l] above (one wave, program order) */
+			st.vib[l] = v;
+		sm.tap[l][n] = (sin (v) + 1.0) * K.vibDepth;
+	}
+	/* two-tap interpolation and blend; the taps come from the window registers by
+	 * cross-lane permutes */
+	double I[8];
+#pragma unroll
+	for (int l = 0; l < 8; l++) {
+		const double off = sm.tap[l][n];
+		const int    d   = K.delay[l];
+		const int    cn  = cnt_adv (st.count[l], d, n + 1);
+		const int    wk  = (int)(cn + off);
+		const int    rel = n + (wk - cn); /* window index of slot wk */
+		const double fr  = off - floor (off);
+		const bool   inw = rel >= 0 && rel + 1 < RV_WIN;
+		const int    i0 = inw ? rel : 0, i1 = inw ? rel + 1 : 0;
+		const double a0lo = __shfl (wlo[l], i0 & (NL - 1)), a0hi = __shfl (whi[l], i0 & (NL - 1));
+		const double a1lo = __shfl (wlo[l], i1 & (NL - 1)), a1hi = __shfl (whi[l], i1 & (NL - 1));
+		double       r0 = i0 < NL ? a0lo : a0hi;
+		double       r1 = i1 < NL ? a1lo : a1hi;
+		if (!inw) { /* outside the window (not reachable at the fixed vibDepth): ring reads */
+			const int     w0 = wk - ((wk > d) ? d + 1 : 0);
+			const int     w1 = wk + 1 - ((wk + 1 > d) ? d + 1 : 0);
+			const double* a  = slab + K.ringOff[c * 13 + l];
+			r0               = a[w0];
+			r1               = a[w1];
+		}
+		double x = (r0 * (1 - fr));
 		x += (r1 * fr);
 		I[l] = ((1.0 - K.blend) * x) + (r0 * K.blend);
-#ifdef RV_SCHED_BARRIER
-		__builtin_amdgcn_sched_barrier (0); /* one line at a time: bounds register pressure */
-#endif
 	}
 	I[0] = (I[0] * K.oneMinusAbsCm) + (I[4] * K.crossmod);
 	I[4] = (I[4] * K.oneMinusAbsCm) + (I[0] * K.crossmod);
@@ -746,7 +801,7 @@ __device__ __forceinline__ void rv_core_channel (const tbf_launch& P, RvCoreLds&
 	fb[6] = (I[6] - (I[4] + I[5] + I[7])) * K.regen;
 	fb[7] = (I[7] - (I[4] + I[5] + I[6])) * K.regen;
 	bout[o] = (I[0] + I[1] + I[2] + I[3] + I[4] + I[5] + I[6] + I[7]) / 8.0;
-	__syncthreads (); /* all ring reads of the channel are complete */
+	__syncthreads (); /* all ring reads of the channel are complete (fallback reads included) */
 	/* allpass writes (a = a0 - old/2 at count; out = a/2 + old) */
 	double ap[4];
 #pragma unroll
@@ -764,29 +819,35 @@ __device__ __forceinline__ void rv_core_channel (const tbf_launch& P, RvCoreLds&
 	for (int l = 0; l < 8; l++) {
 		double prev = __shfl_up (fb[l], 1);
 		if (lane == 0)
-			prev = st.fb[c][l];
+			prev = st.fb[l];
 		slab[K.ringOff[c * 13 + l] + cnt_adv (st.count[l], K.delay[l], n)] = ap[srcAp[l]] + prev;
 	}
 	__syncthreads (); /* lane 0 has read st.fb */
 	if (lane == NL - 1) {
 #pragma unroll
 		for (int l = 0; l < 8; l++)
-			st.fb[c][l] = fb[l];
+			st.fb[l] = fb[l];
 	}
+	if (lane < 12)
+		st.count[lane] = cnt_adv (st.count[lane], K.delay[lane], TBF_SUB);
 	__syncthreads ();
 }
 
+/* one wave per (instance, channel) */
 __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL), amdgpu_waves_per_eu (RV_WAVES)))
 k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 {
 	__shared__ RvCoreLds sm;
 	const int      lane = threadIdx.x;
-	const uint32_t inst = blockIdx.x + P.instBase;
+	const uint32_t inst = (blockIdx.x >> 1) + P.instBase;
+	const int      c    = blockIdx.x & 1;
 	if (inst >= P.nInst)
 		return;
 	const tbf_inst_const& K    = cst[inst];
-	tbf_rv_state*         S    = &P.st[inst].rv;
+	tbf_rv_chan*          S    = &P.st[inst].rv.ch[c];
 	double*               slab = P.rslab + (size_t)inst * P.slabLen;
+	const double*         a0s  = rv_buf (P.rvA, P, inst, c);
+	double*               bout = rv_buf (P.rvB, P, inst, c);
 	prof_begin (P, sm);
 	copy_words (&sm.st, S);
 	__syncthreads ();
@@ -794,13 +855,8 @@ k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 #pragma unroll 1
 		for (int sb = 0; sb < TBF_BLK / TBF_SUB; sb++) {
 			const size_t o = (size_t)blk * TBF_BLK + sb * TBF_SUB + lane;
-			rv_core_channel (P, sm, K, slab, 0, o, rv_buf (P.rvA, P, inst, 0)[o], rv_buf (P.rvB, P, inst, 0));
-			TBF_MARK (8);
-			rv_core_channel (P, sm, K, slab, 1, o, rv_buf (P.rvA, P, inst, 1)[o], rv_buf (P.rvB, P, inst, 1));
-			if (lane < 12)
-				sm.st.count[lane] = cnt_adv (sm.st.count[lane], K.delay[lane], TBF_SUB);
-			__syncthreads ();
-			TBF_MARK (9);
+			rv_core_channel (P, sm, K, slab, c, o, a0s[o], bout);
+			TBF_MARK (8 + c);
 		}
 	}
 	__syncthreads ();
@@ -1348,7 +1404,7 @@ extern "C" int tbf_launch_stage (const tbf_launch* P, int k, hipStream_t stream)
 	else if (k == 1)
 		hipLaunchKernelGGL (k_rv_in, grid, block, 0, stream, *P, P->cst, P->ctl);
 	else if (k == 2)
-		hipLaunchKernelGGL (k_rv_core, grid, block, 0, stream, *P, P->cst);
+		hipLaunchKernelGGL (k_rv_core, dim3 (2 * P->nInst), block, 0, stream, *P, P->cst);
 	else if (k == 3)
 		hipLaunchKernelGGL (k_rv_out, grid, block, 0, stream, *P, P->cst, P->ctl);
 	else if (k == 4) {

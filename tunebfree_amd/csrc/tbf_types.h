@@ -89,14 +89,20 @@ typedef struct tbf_tg_state { /* tonegen + vibrato + overdrive: k_tonegen */
 	uint32_t fpFlip, odFpd;
 } tbf_tg_state;
 
+typedef struct tbf_rv_chan { /* one channel of the feedback network: k_rv_core wave */
+	int32_t  count[12]; /* delay-line counters A..L (lines 0-11) */
+	uint32_t pad[4];
+	double   fb[8];     /* feedback of the channel's last sample */
+	double   vib[8];    /* vibrato phases */
+} tbf_rv_chan;
+
 typedef struct tbf_rv_state { /* reverb: k_rv_in / k_rv_core / k_rv_out */
-	int32_t  count[13];
-	uint32_t fpdL, fpdR;   /* dither streams as advanced by k_rv_in ... */
-	uint32_t fpdL2, fpdR2; /* ... and the identical copies advanced by k_rv_out */
-	uint32_t pad0[3];
-	double   bq[3][4]; /* [A/B/C][L7, L8, R9, R10] */
-	double   fb[2][8];
-	double   vib[2][8];
+	int32_t     countM;       /* predelay counter (k_rv_in) */
+	uint32_t    fpdL, fpdR;   /* dither streams as advanced by k_rv_in ... */
+	uint32_t    fpdL2, fpdR2; /* ... and the identical copies advanced by k_rv_out */
+	uint32_t    pad0[3];
+	double      bq[3][4]; /* [A/B/C][L7, L8, R9, R10] */
+	tbf_rv_chan ch[2];
 } tbf_rv_state;
 
 typedef struct tbf_wh_state { /* whirl: k_whirl */

@@ -16,8 +16,8 @@ NAMES = {0: "tg state load + interpreter", 1: "tg vibrato", 2: "tg mixdown", 3: 
          4: "od waveshaper", 18: "tg state store",
          5: "rv_in dither", 6: "rv_in predelay + biquadA chain", 7: "rv_in sin(x*wet)",
          8: "rv_core channel L", 9: "rv_core channel R + counts",
-         10: "rv_out dither", 11: "rv_out biquadB chain", 12: "rv_out asin", 13: "rv_out biquadC chain",
-         14: "rv_out dry/dither/store",
+         10: "rv_out load", 11: "rv_out B(b) + C(b-1) chains", 12: "rv_out dither + dry + store",
+         13: "rv_out asin",
          26: "wh state + ring load", 20: "wh speed", 21: "wh ring rd + serial filt+angles", 22: "wh FILTER_C",
          23: "wh motions", 24: "wh accumulate", 25: "wh out + carry", 27: "wh state + ring store"}
 

@@ -624,8 +624,9 @@ struct RvInLds {
 
 struct RvOutLds {
 	tbf_rv_state st;
-	double       b[2][TBF_SUB];
-	uint32_t     fpd[2][TBF_SUB + 1];
+	double       bx[2][TBF_BLK]; /* block b: tap mix -> biquadB output */
+	double       cx[2][TBF_BLK]; /* block b-1: asin output -> biquadC output */
+	uint32_t     fpd[2][TBF_BLK + 1];
 	unsigned long long prof[TBF_PROF_SLOTS];
 	unsigned long long plast;
 };
@@ -864,6 +865,10 @@ k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 	prof_end (P, sm, inst);
 }
 
+/* k_rv_out: biquadB -> clamp + asin -> biquadC -> dry mix, dither, (L+R)/sqrt2, in
+ * 128-sample blocks, software-pipelined so biquadB of block b and biquadC of block b-1
+ * advance in the same serial instruction stream (lanes 0,1: B of L,R; lanes 2,3: C of
+ * L,R).  One serial pass per block instead of two. */
 __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL), amdgpu_waves_per_eu (RVIO_WAVES)))
 k_rv_out (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_seg_ctl* __restrict__ ctl)
 {
@@ -877,69 +882,112 @@ k_rv_out (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 	tbf_rv_state*         S   = &P.st[inst].rv;
 	const double*         bL  = rv_buf (P.rvB, P, inst, 0);
 	const double*         bR  = rv_buf (P.rvB, P, inst, 1);
+	const bool            tap = P.chain == TBF_CHAIN_TAP_REVERB;
 	prof_begin (P, sm);
 	copy_words (&sm.st, S);
 	__syncthreads ();
 	tbf_rv_state& st = sm.st;
-	for (uint32_t blk = 0; blk < P.nBlocks; blk++) {
-		const float* in  = P.mid1 + (size_t)inst * P.midStride + (size_t)blk * TBF_BLK;
-		float*       out = P.chain == TBF_CHAIN_TAP_REVERB
-		                       ? P.outL + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK
-		                       : P.mid2 + (size_t)inst * P.midStride + (size_t)blk * TBF_BLK;
-#pragma unroll 1
-		for (int sb = 0; sb < TBF_BLK / TBF_SUB; sb++) {
-			const int n = lane;
-			rv_dither (P.xsJump, st.fpdL2, st.fpdR2, sm.fpd);
-			TBF_MARK (10);
-			const size_t o = (size_t)blk * TBF_BLK + sb * TBF_SUB + n;
-			sm.b[0][n]     = bL[o];
-			sm.b[1][n]     = bR[o];
-			__syncthreads ();
-			/* biquadB (src/reverb.cpp:733-741), lanes 0, 1 */
-			if (lane < 2)
-				rv_chain (K.bq[1], st.bq[1][2 * lane], st.bq[1][2 * lane + 1], sm.b[lane]);
-			__syncthreads ();
-			TBF_MARK (11);
-			/* clamp + asin (743-751) */
+	/* serial lane roles: q = 0 biquadB, 1 biquadC; c = channel */
+	const int     q   = (lane >> 1) & 1, c = lane & 1;
+	const double* cf  = K.bq[1 + q];
+	const double  c0 = cf[0], c1 = cf[1], c2 = cf[2], c3 = cf[3], c4 = cf[4];
+	for (uint32_t it = 0; it <= P.nBlocks; it++) {
+		const bool haveB = it < P.nBlocks, haveC = it > 0;
+		/* (a) tap mix of block `it` */
+		if (haveB) {
+			const size_t o = (size_t)it * TBF_BLK;
+			sm.bx[0][lane]      = bL[o + lane];
+			sm.bx[0][lane + NL] = bL[o + lane + NL];
+			sm.bx[1][lane]      = bR[o + lane];
+			sm.bx[1][lane + NL] = bR[o + lane + NL];
+		}
+		__syncthreads ();
+		TBF_MARK (10);
+		/* (b) serial: B over block it (lanes 0,1), C over block it-1 (lanes 2,3) */
+		if (lane < 4 && (q == 0 ? haveB : haveC)) {
+			double* row = q == 0 ? sm.bx[c] : sm.cx[c];
+			double  s7 = st.bq[1 + q][2 * c], s8 = st.bq[1 + q][2 * c + 1];
+			for (int i0 = 0; i0 < TBF_BLK; i0 += 8) {
+				double xv[8];
 #pragma unroll
-			for (int c = 0; c < 2; c++) {
-				double y = sm.b[c][n];
-				if (y > 1.0) y = 1.0;
-				if (y < -1.0) y = -1.0;
-				sm.b[c][n] = asin (y);
-			}
-			__syncthreads ();
-			TBF_MARK (12);
-			/* biquadC (756-764), lanes 0, 1 */
-			if (lane < 2)
-				rv_chain (K.bq[2], st.bq[2][2 * lane], st.bq[2][2 * lane + 1], sm.b[lane]);
-			__syncthreads ();
-			TBF_MARK (13);
-			/* dry mix, dither, mono sum (766-787) */
-			const double inS = (double)in[sb * TBF_SUB + n];
-			double       ov[2];
+				for (int k = 0; k < 8; k++)
+					xv[k] = row[i0 + k];
 #pragma unroll
-			for (int c = 0; c < 2; c++) {
-				double x = sm.b[c][n];
-				if (wet != 1.0) {
-					double dry = inS;
-					if (fabs (dry) < 1.18e-23)
-						dry = sm.fpd[c][n] * 1.18e-17;
-					x += (dry * (1.0 - wet));
+				for (int k = 0; k < 8; k++) {
+					const double x = xv[k];
+					const double t = (x * c0) + s7;
+					s7             = (x * c1) - (t * c3) + s8;
+					s8             = (x * c2) - (t * c4);
+					row[i0 + k]    = t;
 				}
-				ov[c] = dither_add (x, sm.fpd[c][n + 1]);
 			}
-			out[sb * TBF_SUB + n] = (float)(0.7071067811865476 * (ov[0] + ov[1]));
+			st.bq[1 + q][2 * c]     = s7;
+			st.bq[1 + q][2 * c + 1] = s8;
+		}
+		__syncthreads ();
+		TBF_MARK (11);
+		/* (c) output of block it-1: dry mix, dither, mono sum (src/reverb.cpp:766-787) */
+		if (haveC) {
+			const uint32_t ob = it - 1;
+			/* dither states F[0..128] of both streams for the block */
+			const uint32_t gL = st.fpdL2, gR = st.fpdR2;
+			const uint32_t l1 = xs_jump (P.xsJump, gL, lane + 1), r1 = xs_jump (P.xsJump, gR, lane + 1);
+			sm.fpd[0][lane + 1]      = l1;
+			sm.fpd[1][lane + 1]      = r1;
+			sm.fpd[0][lane + 1 + NL] = xs_jump_u (P.xsJump, l1, NL);
+			sm.fpd[1][lane + 1 + NL] = xs_jump_u (P.xsJump, r1, NL);
 			__syncthreads ();
-			TBF_MARK (14);
+			if (lane == 0) {
+				sm.fpd[0][0] = gL;
+				sm.fpd[1][0] = gR;
+				st.fpdL2     = sm.fpd[0][TBF_BLK];
+				st.fpdR2     = sm.fpd[1][TBF_BLK];
+			}
+			__syncthreads ();
+			const float* in  = P.mid1 + (size_t)inst * P.midStride + (size_t)ob * TBF_BLK;
+			float*       out = tap ? P.outL + (size_t)inst * P.outStride + P.outOffset + (size_t)ob * TBF_BLK
+			                       : P.mid2 + (size_t)inst * P.midStride + (size_t)ob * TBF_BLK;
+#pragma unroll
+			for (int h = 0; h < 2; h++) {
+				const int    n   = lane + h * NL;
+				const double inS = (double)in[n];
+				double       ov[2];
+#pragma unroll
+				for (int cc = 0; cc < 2; cc++) {
+					double x = sm.cx[cc][n];
+					if (wet != 1.0) {
+						double dry = inS;
+						if (fabs (dry) < 1.18e-23)
+							dry = sm.fpd[cc][n] * 1.18e-17;
+						x += (dry * (1.0 - wet));
+					}
+					ov[cc] = dither_add (x, sm.fpd[cc][n + 1]);
+				}
+				const float y = (float)(0.7071067811865476 * (ov[0] + ov[1]));
+				out[n]        = y;
+				if (tap)
+					P.outR[(size_t)inst * P.outStride + P.outOffset + (size_t)ob * TBF_BLK + n] = y;
+			}
 		}
-		if (P.chain == TBF_CHAIN_TAP_REVERB) {
-			float* oR = P.outR + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
-			oR[lane]      = out[lane];
-			oR[lane + NL] = out[lane + NL];
+		__syncthreads ();
+		TBF_MARK (12);
+		/* (d) clamp + asin of block it's biquadB output -> C input of the next pass
+		 * (src/reverb.cpp:743-751) */
+		if (haveB) {
+#pragma unroll
+			for (int h = 0; h < 2; h++)
+#pragma unroll
+				for (int cc = 0; cc < 2; cc++) {
+					const int n = lane + h * NL;
+					double    y = sm.bx[cc][n];
+					if (y > 1.0) y = 1.0;
+					if (y < -1.0) y = -1.0;
+					sm.cx[cc][n] = asin (y);
+				}
 		}
+		__syncthreads ();
+		TBF_MARK (13);
 	}
-	__syncthreads ();
 	copy_words (S, &sm.st);
 	prof_end (P, sm, inst);
 }

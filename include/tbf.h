@@ -106,6 +106,26 @@ int tbf_render_device (tbf_engine* e, uint32_t nblocks, float* d_outL, float* d_
  * the 128-sample block FIFO, rendering blocks as needed. */
 int tbf_synth_sound (tbf_engine* e, uint32_t nframes, float* outL, float* outR, uint64_t stride);
 
+/* ---- host control surface (src/midi.cpp, src/program.cpp, src/pgmParser.cpp) ---- */
+/* callMIDIControlFunction (src/midi.cpp:535-545) on one instance.  fn is a control
+ * function name of src/midi.cpp:100-170 that reaches the DSP chain: upper|lower|pedal.
+ * drawbar16/513/8/4/223/2/135/113/1, percussion.enable|volume|decay|harmonic,
+ * vibrato.knob|routing|upper|lower, swellpedal1|2, overdrive.enable|character,
+ * reverb.mix, rotary.speed-preset|speed-select|speed-toggle.  value 0..127 (clamped).
+ * Returns 0 when applied, 1 for any other name (ignored, as the reference ignores
+ * names without a registered function). */
+int tbf_midi_control (tbf_engine* e, uint32_t inst, const char* fn, int32_t value);
+/* programme definitions in the .pgm syntax (src/pgmParser.cpp:65-73, properties of
+ * bindToProgram src/program.cpp:133-603) into the engine's programme table; returns the
+ * number of programmes in use, or < 0 with tbf_last_error () = "line N: message" */
+int tbf_program_parse (tbf_engine* e, const char* text);
+/* installProgram (src/program.cpp:735-921): MIDI program change pc (0..127, plus the
+ * reference's default pgm.controller.offset of 1) on one instance; random drawbars draw
+ * from the instance's control rand() stream */
+int tbf_program_install (tbf_engine* e, uint32_t inst, uint32_t pc);
+/* name of the programme program change pc selects; returns 1 if in use, else 0 */
+int tbf_program_name (tbf_engine* e, uint32_t pc, char* out, uint32_t cap);
+
 int tbf_synchronize (tbf_engine* e);
 /* bit 0: vibrato scatter took the serial path in some block (informational) */
 int tbf_error_flags (tbf_engine* e, uint32_t* flags);
@@ -121,6 +141,10 @@ int tbf_debug_tables (tbf_engine* e, uint32_t tpl_id, float* attack, float* rele
 /* run one block of the tonegen control plane for an instance and return the core
  * program: per entry {wheel, env, row, sg, pg, vg, nsg, npg, nvg} as 9 floats */
 int tbf_debug_step (tbf_engine* e, uint32_t inst, float* entries9, uint32_t cap);
+/* an instance's host control state: odClean, odA, odC, rvG, revOpt, revSelect, whBypass,
+ * newRouting, swellPedalGain, percEnabled, percIsSoft, percIsFast, percSendBus, vibTable,
+ * vibMixed, percDrawbarGain, drawBarGain[27]; returns the count (43) */
+int tbf_debug_control (tbf_engine* e, uint32_t inst, double* out, uint32_t cap);
 /* the kernel's exact shortcuts of serial recurrences, evaluated on the host (same source,
  * csrc/tbf_exact.h): op 0 phase_run (in: v0, d, m -> out: ok, D), op 1 cnt_adv (in: c0,
  * d, n -> out: count), op 2 wrap1 (in: x, -, - -> out: fmod (x, 1)), op 3 xorshift

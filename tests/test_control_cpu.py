@@ -1,0 +1,192 @@
+"""CPU tests of the host control surface (§8(f) row 4: programmes and MIDI control
+functions), on host-only engines (device = -1, no GPU):
+
+  - the .pgm parser accepts the reference's syntax (src/pgmParser.cpp:65-73) and
+    property vocabulary (src/program.cpp:133-603), reports errors with line numbers;
+  - installProgram (src/program.cpp:735-921) leaves an instance in the same control
+    state, and emits the same per-block core programs, as the equivalent CLAP parameter
+    sequence the oracle is driven with (tests/scenarios.py jazz1_params);
+  - each MIDI control function maps its 0..127 value like the reference handler;
+  - when /root/reference is present, its own pgm/default.pgm parses completely and
+    every programme name matches the file.
+"""
+import ctypes as C
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import scenarios as S
+
+T = pytest.importorskip("tunebfree_amd")
+REF_PGM = Path("/root/reference/pgm/default.pgm")
+
+# a programme file in the reference's syntax (the "Jazz 1 all" entry of pgm/default.pgm
+# is reproduced by its properties, not copied: 888 0000 000, perc on/soft/fast/3rd,
+# vibrato c3 upper, overdrive, chorale)
+PGM = """
+# comment line
+1 {name="Jazz 1 all",
+   drawbars="888 0000 000",
+   perc=on, percvol=soft, percspeed=fast, percharm=3rd,
+   vibrato=c3, vibratoupper=on,
+   overdrive=on,
+   rotaryspeed=chorale}
+2   { name="Standard B", drawbars="88 8000 000" }
+7 { name = "Fast \\"quoted\\"", drawbars="80-0808_000", vibrato=v2, vibratolower=yes, rotaryspeed=tremolo,
+    reverbmix=0.3, keysplitlower=55, transpose=-12 }
+9 { name="stop", rotaryspeed=stop, perc=off, overdrive=no, attackenv=click, rotary=on }
+"""
+
+
+def _ctl(lib, eng, i):
+    fn = lib.tbf_debug_control
+    fn.restype, fn.argtypes = C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]
+    out = np.zeros(64, np.float64)
+    n = fn(eng._h, i, out.ctypes.data, 64)
+    assert n == 43
+    return out[:n]
+
+
+def _step(lib, eng, i):
+    lib.tbf_debug_step.restype = C.c_int
+    lib.tbf_debug_step.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]
+    buf = np.zeros(9 * 600, np.float32)
+    n = lib.tbf_debug_step(eng._h, i, buf.ctypes.data, 600)
+    assert n >= 0
+    return buf[: 9 * n].reshape(n, 9).copy()
+
+
+def _engine(n=2):
+    eng = T.Engine(sample_rate=48000.0, device=-1)
+    tid = eng.template(seed=7)
+    eng.add_instances([tid] * n, [1000 + i for i in range(n)])
+    return eng
+
+
+def test_pgm_parse_names_and_errors():
+    eng = _engine(1)
+    assert eng.program_parse(PGM) == 4
+    assert eng.program_name(0) == "Jazz 1 all"  # program change 0 -> programme 1 (offset 1)
+    assert eng.program_name(1) == "Standard B"
+    assert eng.program_name(6) == 'Fast "quoted"'
+    assert eng.program_name(3) is None
+    for bad, msg in (("1 { drawbars=\"889\" }", "Illegal char"), ("1 { nonsense=1 }", "Unrecognized property"),
+                     ("\n\n3 { vibrato=c9 }", "line 3"), ("4 { name=\"x\" ", "expected"),
+                     ("5 { perc=maybe }", "percussion enabled"), ("6 { reverbmix=1.5 }", "out of range"),
+                     ("x { name=a }", "program number expected"), ("200 { name=a }", "out of range")):
+        with pytest.raises(T.TbfError, match=msg):
+            eng.program_parse(bad)
+    eng.close()
+
+
+def test_program_install_equals_clap_parameters():
+    """installProgram of "Jazz 1 all" == the CLAP parameter script the oracle and the GPU
+    parity tests use (character/reverb excluded: not programme properties)."""
+    lib = T.load_library()
+    a, b = _engine(1), _engine(1)
+    assert a.program_parse(PGM) == 4
+    a.program_install(0, 0)
+    for (_, kind, pid, v) in [(0, k, p, v) for (k, p, v) in S.jazz1_params()]:
+        if pid in (S.P_CHARACTER, S.P_REVERB):
+            continue
+        b.set_param(0, pid, v)
+    ca, cb = _ctl(lib, a, 0), _ctl(lib, b, 0)
+    assert np.array_equal(ca, cb), np.nonzero(ca != cb)
+    for eng in (a, b):
+        for k in S.chord_for(3):
+            eng.note(0, k, 1)
+    for _ in range(4):  # attack block, steady blocks
+        assert np.array_equal(_step(lib, a, 0), _step(lib, b, 0))
+    a.close()
+    b.close()
+
+
+def test_program_install_rotary_and_stop():
+    lib = T.load_library()
+    eng = _engine(1)
+    eng.program_parse(PGM)
+    eng.program_install(0, 6)  # tremolo: rotary.speed-preset 127 -> revSelect 2 -> option 8
+    c = _ctl(lib, eng, 0)
+    assert c[4] == 8 and c[5] == 2
+    assert c[3] == pytest.approx(0.1)  # reverbmix: "reverb.mix-preset" is unregistered in the reference
+    eng.program_install(0, 8)  # stop: 64 -> revSelect 1 -> option 0; perc off; overdrive off
+    c = _ctl(lib, eng, 0)
+    assert c[4] == 0 and c[5] == 1 and c[9] == 0 and c[0] == 1
+    eng.program_install(0, 3)  # unused programme: no change
+    assert np.array_equal(_ctl(lib, eng, 0), c)
+    eng.close()
+
+
+def test_midi_control_functions():
+    lib = T.load_library()
+    eng = _engine(1)
+    base = _ctl(lib, eng, 0)
+    # setMIDIDrawBar: inverted, rint(val * 8 / 127)
+    for v, setting in ((0, 8), (127, 0), (64, 4), (4, 8), (8, 7), (9, 7), (71, 4)):
+        assert setting == int(np.rint((127 - v) * 8.0 / 127.0))
+        assert eng.midi_control(0, "upper.drawbar16", v)
+        ref = T.Engine(sample_rate=48000.0, device=-1)
+        t2 = ref.template(seed=7)
+        ref.add_instances([t2], [1000])
+        ref.set_param(0, S.P_DRAWBAR + 0, setting)
+        assert _ctl(lib, eng, 0)[16] == _ctl(lib, ref, 0)[16], (v, setting)
+        ref.close()
+    assert eng.midi_control(0, "lower.drawbar1", 0) and _ctl(lib, eng, 0)[16 + 17] > 0
+    # percussion thresholds at 64
+    eng.midi_control(0, "percussion.enable", 63)
+    assert _ctl(lib, eng, 0)[9] == 0
+    eng.midi_control(0, "percussion.enable", 64)
+    assert _ctl(lib, eng, 0)[9] == 1
+    # vibrato knob: u / 23 -> V1 C1 V2 C2 V3 C3 (vibTable 0..2, chorus flag)
+    for u, table, mixed in ((0, 0, 0), (23, 0, 1), (46, 1, 0), (69, 1, 1), (92, 2, 0), (115, 2, 1), (127, 2, 1)):
+        eng.midi_control(0, "vibrato.knob", u)
+        c = _ctl(lib, eng, 0)
+        assert (c[13], c[14] != 0) == (table, bool(mixed)), u
+    # routing: u / 32 -> bits upper(2) lower(1)
+    for u, bits in ((0, 0), (32, 1), (64, 2), (96, 3)):
+        eng.midi_control(0, "vibrato.routing", u)
+        assert int(_ctl(lib, eng, 0)[7]) & 3 == bits
+    # overdrive / reverb / swell
+    eng.midi_control(0, "overdrive.enable", 64)
+    assert _ctl(lib, eng, 0)[0] == 0
+    eng.midi_control(0, "overdrive.character", 127)
+    assert _ctl(lib, eng, 0)[1] == pytest.approx(1.0)
+    eng.midi_control(0, "reverb.mix", 127)
+    assert _ctl(lib, eng, 0)[3] == 1.0
+    eng.midi_control(0, "swellpedal1", 127)
+    assert _ctl(lib, eng, 0)[8] == pytest.approx(0.07)
+    # rotary: speed-select u / 15 -> option 0..8, revSelect from the horn speed
+    eng.midi_control(0, "rotary.speed-select", 127)
+    c = _ctl(lib, eng, 0)
+    assert c[4] == 8 and c[5] == 2
+    eng.midi_control(0, "rotary.speed-toggle", 127)  # not slow -> slow option 4
+    c = _ctl(lib, eng, 0)
+    assert c[4] == 4 and c[5] == 0
+    eng.midi_control(0, "rotary.speed-toggle", 10)  # release: nothing
+    assert _ctl(lib, eng, 0)[4] == 4
+    # names without a hot-path function are ignored like the reference does
+    assert not eng.midi_control(0, "reverb.mix-preset", 100)
+    assert not eng.midi_control(0, "xov.ctl_biased", 3)
+    with pytest.raises(T.TbfError):
+        eng.midi_control(0, "reverb.mix", -1)
+    assert base.shape == c.shape
+    eng.close()
+
+
+@pytest.mark.skipif(not REF_PGM.exists(), reason="reference tree not present")
+def test_reference_default_pgm_parses():
+    """The reference's own pgm/default.pgm (read in place, not copied)."""
+    text = REF_PGM.read_text()
+    names = {}
+    for m in re.finditer(r'^\s*(\d+)\s*\{\s*name\s*=\s*"([^"]*)"', text, re.M):
+        names[int(m.group(1))] = m.group(2)
+    eng = _engine(1)
+    n = eng.program_parse(text)
+    assert n == len(names) and n > 20
+    for pgm, name in names.items():
+        assert eng.program_name(pgm - 1) == name[:31]
+    for pc in range(0, 128, 7):
+        eng.program_install(0, pc)
+    eng.close()

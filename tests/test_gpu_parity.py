@@ -128,3 +128,23 @@ def test_gpu_config5_mixed_tunings_96k(oracle):
             ex.append(x)
     print(f"config5: {n} instances, {len(names)} tunings, max|err|={worst:.3g} bit-exact={min(ex):.6f}")
     assert worst <= TOL
+
+
+def test_gpu_program_install_matches_clap_script(oracle):
+    """§8(f) row 4: an organ configured by installProgram ("Jazz 1 all" in .pgm syntax,
+    src/program.cpp:735-921) plus the character knob renders bit-identically to the
+    oracle driven by the CLAP parameter script of the bench scenario."""
+    from test_control_cpu import PGM
+    eng, tpl, seeds, scens = _setup(oracle, 4, S.bench_scenario)
+    assert eng.program_parse(PGM) == 4
+    script = []
+    for i in range(4):
+        eng.program_install(i, 0)
+        eng.set_param(i, S.P_CHARACTER, 0.5)
+        script.append([(0, "note", k, 1) for k in S.chord_for(i)])
+    L, R = engine_run(eng, script, 40)
+    oL, oR, *_ = oracle_run(oracle, tpl, seeds, scens, 40)
+    eL, xL = compare(L, oL)
+    eR, xR = compare(R, oR)
+    print(f"program install: max|err| L={eL:.3g} R={eR:.3g} bit-exact L={xL:.6f} R={xR:.6f}")
+    assert max(eL, eR) <= TOL

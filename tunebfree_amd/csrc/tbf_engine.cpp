@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../include/tbf.h"
+#include "tbf_engine_impl.h"
 #include "tbf_exact.h"
 #include "tbf_host.h"
 #include "tbf_types.h"
@@ -26,7 +27,7 @@ using namespace tbf;
 
 static thread_local std::string g_err;
 
-static int fail (int code, const std::string& msg)
+int tbf::fail (int code, const std::string& msg)
 {
 	g_err = msg;
 	return code;
@@ -39,95 +40,6 @@ static int fail (int code, const std::string& msg)
 			return fail (-5, std::string (#x ": ") + hipGetErrorString (_e));           \
 	} while (0)
 
-namespace {
-
-struct Instance {
-	uint32_t       tpl = 0;
-	TgControl      tg;
-	tbf_inst_const k;
-	tbf_inst_state s0;
-	tbf_seg_ctl    ctl;
-	double         params[64];
-	/* preamp (struct b_preamp) */
-	int            odClean = 1;
-	float          odA = 0.0f, odB = 0.0f, odC = 1.0f, odD = 0.5f;
-	/* reverb mix */
-	float          rvG = 0.1f;
-	int            whBypass = 0;
-	int            revOpt = -1;
-	bool           ctlDirty = true;
-	bool           progDirty = true;
-	std::vector<tbf_prog_entry> prog;
-};
-
-template <typename T>
-struct DevBuf {
-	T*     p   = nullptr;
-	size_t cap = 0;
-	int    ensure (size_t n)
-	{
-		if (n <= cap)
-			return 0;
-		if (p)
-			(void)hipFree (p);
-		p   = nullptr;
-		cap = 0;
-		if (hipMalloc ((void**)&p, std::max<size_t> (n, 1) * sizeof (T)) != hipSuccess)
-			return -12;
-		cap = n;
-		return 0;
-	}
-	void release ()
-	{
-		if (p)
-			(void)hipFree (p);
-		p   = nullptr;
-		cap = 0;
-	}
-};
-
-} // namespace
-
-struct tbf_engine {
-	tbf_engine_config                       cfg;
-	hipStream_t                             stream = nullptr;
-	WhirlTables                             wt;
-	std::vector<uint32_t>                   vibTab;
-	uint32_t                                statorInc = 0;
-	uint32_t                                wringLen  = 512;
-	std::vector<std::unique_ptr<TgTemplate>> tpls;
-	std::vector<Instance>                   inst;
-	/* reverb ring layout (identical for all instances: A..F are fixed) */
-	uint32_t                                slabLen = 0;
-	/* device side */
-	bool                                    deviceReady = false;
-	uint32_t                                devInst     = 0;
-	DevBuf<float>                           bank;
-	DevBuf<tbf_tpl_desc>                    tplDesc;
-	DevBuf<tbf_inst_const>                  cst;
-	DevBuf<tbf_inst_state>                  st;
-	DevBuf<float>                           wring;
-	DevBuf<double>                          rslab;
-	DevBuf<tbf_seg_ctl>                     ctl;
-	DevBuf<tbf_prog_entry>                  prog;
-	DevBuf<uint32_t>                        vib;
-	DevBuf<uint32_t>                        xsj; /* xorshift32 jump table */
-	DevBuf<float>                           whTab, whBw;
-	DevBuf<uint32_t>                        err;
-	DevBuf<uint64_t>                        prof; /* tbf_debug_profile */
-	bool                                    profOn = false;
-	/* tbf_debug_kernel_times: HIP events around every stage launch */
-	bool                                    timeOn = false;
-	std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> tev;
-	DevBuf<float>                           outL, outR;
-	DevBuf<float>                           mid1, mid2; /* inter-stage blocks of one launch chunk */
-	DevBuf<double>                          rvA, rvB;   /* reverb inter-kernel streams (FP64) */
-	std::vector<tbf_seg_ctl>                hCtl;
-	std::vector<tbf_prog_entry>             hProg;
-	/* synth_sound FIFO */
-	std::vector<float>                      fifoL, fifoR;
-	uint32_t                                boffset = TBF_BLK;
-};
 
 #define PROG_CAP (TBF_NW + 1)
 /* blocks per kernel launch chunk: bounds the inter-stage buffers to
@@ -235,6 +147,22 @@ static void odCtl (const Instance& in, double sr, tbf_seg_ctl& c)
 	c.odOut        = out;
 	c.odDensityPos = density > 0 ? 1u : 0u;
 	c.odClean      = (uint32_t)in.odClean;
+}
+
+/* fsetCharacter (src/overdrive.cpp:547-574): character A and the linear-segment output
+ * level C */
+void tbf::setCharacter (Instance& in, float value)
+{
+	static const double Aval[5] = {0.0, 0.25, 0.50, 0.75, 1.00};
+	static const double Cval[5] = {1.0, 0.70, 0.25, 0.15, 0.13};
+	in.odA                      = value;
+	for (int q = 0; q < 4; q++)
+		if (value <= Aval[q + 1]) {
+			float a = (float)Aval[q], b = (float)Aval[q + 1], p = (float)Cval[q], qq = (float)Cval[q + 1];
+			in.odC  = p + (value - a) * (qq - p) / (b - a);
+			break;
+		}
+	in.ctlDirty = true;
 }
 
 extern "C" {
@@ -356,6 +284,7 @@ int tbf_instances_add (tbf_engine* e, uint32_t n, const uint32_t* tpl_ids, const
 		e->inst.emplace_back ();
 		Instance& in = e->inst.back ();
 		in.tpl       = tpl_ids[q];
+		in.ctlRand   = GlibcRand (seeds[q] ^ 0x5bd1e995u);
 		memset (&in.k, 0, sizeof (in.k));
 		memset (&in.s0, 0, sizeof (in.s0));
 		memset (&in.ctl, 0, sizeof (in.ctl));
@@ -443,16 +372,7 @@ int tbf_set_param (tbf_engine* e, uint32_t i, int32_t index, double v)
 	else if (index == TBF_P_OVERDRIVE)
 		in.odClean = (int)rint (1.0f - value);
 	else if (index == TBF_P_CHARACTER) {
-		/* fsetCharacter + linseg, src/overdrive.cpp:547-574 */
-		static const double Aval[5] = {0.0, 0.25, 0.50, 0.75, 1.00};
-		static const double Cval[5] = {1.0, 0.70, 0.25, 0.15, 0.13};
-		in.odA                      = value;
-		for (int q = 0; q < 4; q++)
-			if (value <= Aval[q + 1]) {
-				float a = (float)Aval[q], b = (float)Aval[q + 1], p = (float)Cval[q], qq = (float)Cval[q + 1];
-				in.odC  = p + (value - a) * (qq - p) / (b - a);
-				break;
-			}
+		setCharacter (in, value);
 	} else if (index == TBF_P_REVERB)
 		in.rvG = value;
 	else if (index == TBF_P_PERCUSSION)

@@ -1,0 +1,139 @@
+/*
+ * tbf_engine_impl.h -- private engine state shared by the C-ABI translation units
+ * (tbf_engine.cpp: construction, device setup, rendering; tbf_control.cpp: MIDI control
+ * functions and programmes).  Not part of the ABI.
+ */
+#ifndef TBF_ENGINE_IMPL_H
+#define TBF_ENGINE_IMPL_H
+
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/tbf.h"
+#include "tbf_host.h"
+#include "tbf_types.h"
+
+namespace tbf {
+
+/* one programme of the .pgm table (struct _programme, src/program.h:104-140; the
+ * fields the engine applies) */
+struct Programme {
+	uint32_t flags = 0;
+	char     name[32] = {0};
+	unsigned drawbars[9] = {0}, lowerDrawbars[9] = {0}, pedalDrawbars[9] = {0};
+	uint32_t scanner = 0;
+	int      percussionEnabled = 0, percussionVolume = 0, percussionSpeed = 0, percussionHarmonic = 0;
+	int      overdriveSelect = 0;
+	int      rotarySpeedSelect = 0;
+	float    reverbMix = 0.f;
+	int      keyboardSplitLower = 0, keyboardSplitPedals = 0;
+	int      transpose[7] = {0};
+};
+
+int  fail (int code, const std::string& msg);
+void setCharacter (struct Instance& in, float v);
+
+} // namespace tbf
+
+namespace tbf {
+
+struct Instance {
+	uint32_t       tpl = 0;
+	TgControl      tg;
+	tbf_inst_const k;
+	tbf_inst_state s0;
+	tbf_seg_ctl    ctl;
+	double         params[64];
+	/* preamp (struct b_preamp) */
+	int            odClean = 1;
+	float          odA = 0.0f, odB = 0.0f, odC = 1.0f, odD = 0.5f;
+	/* reverb mix */
+	float          rvG = 0.1f;
+	int            whBypass = 0;
+	int            revOpt = -1;   /* useRevOption (n) pending for the next block */
+	int            revSelect = 0; /* whirl revSelect: WHIRL_SLOW after initWhirl (src/whirl.cpp:1131) */
+	GlibcRand      ctlRand{1};    /* control-plane rand() stream (randomizeDrawbars) */
+	bool           ctlDirty = true;
+	bool           progDirty = true;
+	std::vector<tbf_prog_entry> prog;
+};
+
+template <typename T>
+struct DevBuf {
+	T*     p   = nullptr;
+	size_t cap = 0;
+	int    ensure (size_t n)
+	{
+		if (n <= cap)
+			return 0;
+		if (p)
+			(void)hipFree (p);
+		p   = nullptr;
+		cap = 0;
+		if (hipMalloc ((void**)&p, std::max<size_t> (n, 1) * sizeof (T)) != hipSuccess)
+			return -12;
+		cap = n;
+		return 0;
+	}
+	void release ()
+	{
+		if (p)
+			(void)hipFree (p);
+		p   = nullptr;
+		cap = 0;
+	}
+};
+
+} // namespace tbf
+
+using namespace tbf; /* private header: the engine's own translation units only */
+
+struct tbf_engine {
+	tbf_engine_config                       cfg;
+	hipStream_t                             stream = nullptr;
+	WhirlTables                             wt;
+	std::vector<uint32_t>                   vibTab;
+	uint32_t                                statorInc = 0;
+	uint32_t                                wringLen  = 512;
+	std::vector<std::unique_ptr<TgTemplate>> tpls;
+	std::vector<Instance>                   inst;
+	/* reverb ring layout (identical for all instances: A..F are fixed) */
+	uint32_t                                slabLen = 0;
+	/* device side */
+	bool                                    deviceReady = false;
+	uint32_t                                devInst     = 0;
+	DevBuf<float>                           bank;
+	DevBuf<tbf_tpl_desc>                    tplDesc;
+	DevBuf<tbf_inst_const>                  cst;
+	DevBuf<tbf_inst_state>                  st;
+	DevBuf<float>                           wring;
+	DevBuf<double>                          rslab;
+	DevBuf<tbf_seg_ctl>                     ctl;
+	DevBuf<tbf_prog_entry>                  prog;
+	DevBuf<uint32_t>                        vib;
+	DevBuf<uint32_t>                        xsj; /* xorshift32 jump table */
+	DevBuf<float>                           whTab, whBw;
+	DevBuf<uint32_t>                        err;
+	DevBuf<uint64_t>                        prof; /* tbf_debug_profile */
+	bool                                    profOn = false;
+	/* tbf_debug_kernel_times: HIP events around every stage launch */
+	bool                                    timeOn = false;
+	std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> tev;
+	DevBuf<float>                           outL, outR;
+	DevBuf<float>                           mid1, mid2; /* inter-stage blocks of one launch chunk */
+	DevBuf<double>                          rvA, rvB;   /* reverb inter-kernel streams (FP64) */
+	std::vector<tbf_seg_ctl>                hCtl;
+	std::vector<tbf_prog_entry>             hProg;
+	/* programme table (.pgm), src/program.h:26 MAXPROGS; pgm.controller.offset */
+	std::vector<Programme>                  progs = std::vector<Programme> (129);
+	int                                     pgmOffset = 1;
+	/* synth_sound FIFO */
+	std::vector<float>                      fifoL, fifoR;
+	uint32_t                                boffset = TBF_BLK;
+};
+
+#endif

@@ -45,6 +45,10 @@ SIGNATURES = {
     "tbf_synchronize": (C.c_int, [C.c_void_p]),
     "tbf_error_flags": (C.c_int, [C.c_void_p, _u32p]),
     "tbf_template_bank": (C.c_int, [C.c_void_p, C.c_uint32, _fp, C.c_uint64, _u32p]),
+    "tbf_midi_control": (C.c_int, [C.c_void_p, C.c_uint32, C.c_char_p, C.c_int32]),
+    "tbf_program_parse": (C.c_int, [C.c_void_p, C.c_char_p]),
+    "tbf_program_install": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32]),
+    "tbf_program_name": (C.c_int, [C.c_void_p, C.c_uint32, C.c_char_p, C.c_uint32]),
 }
 
 _lib = None
@@ -148,6 +152,22 @@ class Engine:
         _check(self._lib.tbf_synth_sound(self._h, int(nframes), L.ctypes.data_as(_fp), R.ctypes.data_as(_fp),
                                          nframes))
         return L, R
+
+    def midi_control(self, inst, fn, value):
+        """callMIDIControlFunction (src/midi.cpp:535): True if the name is a hot-path control."""
+        return _check(self._lib.tbf_midi_control(self._h, int(inst), fn.encode(), int(value))) == 0
+
+    def program_parse(self, text):
+        """Load programme definitions in the reference's .pgm syntax; returns programmes in use."""
+        return _check(self._lib.tbf_program_parse(self._h, text.encode()))
+
+    def program_install(self, inst, pc):
+        """installProgram (src/program.cpp:735) for MIDI program change pc on one instance."""
+        _check(self._lib.tbf_program_install(self._h, int(inst), int(pc)))
+
+    def program_name(self, pc):
+        buf = C.create_string_buffer(64)
+        return buf.value.decode() if _check(self._lib.tbf_program_name(self._h, int(pc), buf, 64)) else None
 
     def synchronize(self):
         _check(self._lib.tbf_synchronize(self._h))

@@ -90,6 +90,7 @@ struct WhLds {
 	float        x2[TBF_SUB + 4];
 	float        xd1[TBF_SUB + 1];
 	float        rd[2][TBF_SUB]; /* drum ring outputs -> drum shelf outputs (in place) */
+	float        tmp[3][TBF_SUB + 2]; /* DF2 state sequences temp[n-2 .. 63] of the serial biquads */
 	int          brake;
 	unsigned long long prof[TBF_PROF_SLOTS];
 	unsigned long long plast;
@@ -1170,8 +1171,8 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 	const uint32_t WM       = (uint32_t)W - 1u;
 	/* serial filter coefficients: lane 0 horn A, lanes 1-2 drum shelf */
 	const float* cfa = lane == 0 ? K.hafw : K.drf;
-	const float  fa0 = cfa[0], fa1 = cfa[1], fa2 = cfa[2], fa3 = cfa[3], fa4 = cfa[4];
-	const float  hb0 = K.hbfw[0], hb1 = K.hbfw[1], hb2 = K.hbfw[2], hb3 = K.hbfw[3], hb4 = K.hbfw[4];
+	const float  fa0 = cfa[0], fa1 = cfa[1]; /* a1, a2 of the serial state recurrences */
+	const float  hb0 = K.hbfw[0], hb1 = K.hbfw[1];
 
 #pragma unroll 1
 	for (int sb = 0; sb < TBF_BLK / TBF_SUB; sb++) {
@@ -1199,58 +1200,104 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 			sm.x2[i] = st.adx[2][(st.adi[2] + 3 - i) & 7];
 		}
 		__syncthreads ();
-		/* independent serial biquads as lane chains: lane 0 horn filter A (hafw), lanes
-		 * 1, 2 drum shelves (drfL, drfR, in place on rd); then lane 0 horn filter B
-		 * (hbfw) while lanes 1, 2 step the rotor angles */
+		/* DF2 biquads (EQ_IIR, src/whirl.cpp:1479-1485): only the state recurrence
+		 * temp[n] = (x - a1 temp[n-1]) - a2 temp[n-2] is serial; the output
+		 * y[n] = (b0 temp[n] + b1 temp[n-1]) + b2 temp[n-2] is the same expression
+		 * evaluated lane-parallel afterwards.  Pass 1: lane 0 horn filter A (hafw) on the
+		 * input, lanes 1, 2 the drum shelves (drfL, drfR) on the ring outputs. */
 		if (lane < 3) {
 			const int    fi = lane == 0 ? 0 : lane + 1;
 			const float* ip = lane == 0 ? sm.xx + 1 : sm.rd[lane - 1];
-			float*       ou = lane == 0 ? sm.xf + 4 : sm.rd[lane - 1];
+			float*       tp = sm.tmp[lane];
 			float        z0 = st.fz[fi][0], z1 = st.fz[fi][1];
+			tp[0] = z1;
+			tp[1] = z0;
 			for (int i0 = 0; i0 < TBF_SUB; i0 += 8) {
 				float xv[8];
 #pragma unroll
 				for (int k = 0; k < 8; k++)
 					xv[k] = ip[i0 + k];
 #pragma unroll
-				for (int k = 0; k < 8; k++)
-					ou[i0 + k] = eq_iir (fa0, fa1, fa2, fa3, fa4, z0, z1, xv[k]);
+				for (int k = 0; k < 8; k++) {
+					const float t = xv[k] - (fa0 * z0) - (fa1 * z1);
+					z1            = z0;
+					z0            = t;
+					tp[2 + i0 + k] = t;
+				}
 			}
 			st.fz[fi][0] = z0;
 			st.fz[fi][1] = z1;
 		}
+		__syncthreads ();
+		{
+			/* filter outputs: horn A -> x1 (scratch until FILTER_C), drum shelves in place */
+			const float* T0 = sm.tmp[0];
+			sm.x1[4 + n]    = (T0[n + 2] * K.hafw[2]) + (K.hafw[3] * T0[n + 1]) + (K.hafw[4] * T0[n]);
+#pragma unroll
+			for (int c = 0; c < 2; c++) {
+				const float* Tc = sm.tmp[1 + c];
+				sm.rd[c][n]     = (Tc[n + 2] * K.drf[2]) + (K.drf[3] * Tc[n + 1]) + (K.drf[4] * Tc[n]);
+			}
+		}
+		__syncthreads ();
+		/* pass 2: lane 0 horn filter B (hbfw) on the horn A output */
 		if (lane == 0) {
 			float  z0 = st.fz[1][0], z1 = st.fz[1][1];
-			float* io = sm.xf + 4;
+			float* tp = sm.tmp[0];
+			tp[0]     = z1;
+			tp[1]     = z0;
 			for (int i0 = 0; i0 < TBF_SUB; i0 += 8) {
 				float xv[8];
 #pragma unroll
 				for (int k = 0; k < 8; k++)
-					xv[k] = io[i0 + k];
+					xv[k] = sm.x1[4 + i0 + k];
 #pragma unroll
-				for (int k = 0; k < 8; k++)
-					io[i0 + k] = eq_iir (hb0, hb1, hb2, hb3, hb4, z0, z1, xv[k]);
+				for (int k = 0; k < 8; k++) {
+					const float t = xv[k] - (hb0 * z0) - (hb1 * z1);
+					z1            = z0;
+					z0            = t;
+					tp[2 + i0 + k] = t;
+				}
 			}
 			st.fz[1][0] = z0;
 			st.fz[1][1] = z1;
-		} else if (lane < 3) {
-			double       a   = lane == 1 ? st.hornAngle : st.drumAngle;
-			const double inc = lane == 1 ? hornIncr : drumIncr;
-			for (int i0 = 0; i0 < TBF_SUB; i0 += 8) {
-				double av[8];
+		}
+		/* rotor angles, angle = fmod (angle + incr, 1) per sample (src/whirl.cpp:1428-1429):
+		 * inside one binade of the angle every sum lands on the same grid, so the run is
+		 * a0 + n D exactly (phase_run); otherwise lanes 1, 2 replay the recurrence */
+		{
+			double Dh, Dd;
+			const bool okh = phase_run (st.hornAngle, hornIncr, TBF_SUB, Dh);
+			const bool okd = phase_run (st.drumAngle, drumIncr, TBF_SUB, Dd);
+			if (okh)
+				sm.ang[0][n] = st.hornAngle + (double)n * Dh;
+			if (okd)
+				sm.ang[1][n] = st.drumAngle + (double)n * Dd;
+			if ((lane == 1 && !okh) || (lane == 2 && !okd)) {
+				double       a   = lane == 1 ? st.hornAngle : st.drumAngle;
+				const double inc = lane == 1 ? hornIncr : drumIncr;
+				for (int i0 = 0; i0 < TBF_SUB; i0 += 8) {
+					double av[8];
 #pragma unroll
-				for (int k = 0; k < 8; k++) {
-					av[k] = a;
-					a     = wrap1 (a + inc);
+					for (int k = 0; k < 8; k++) {
+						av[k] = a;
+						a     = wrap1 (a + inc);
+					}
+#pragma unroll
+					for (int k = 0; k < 8; k++)
+						sm.ang[lane - 1][i0 + k] = av[k];
 				}
-#pragma unroll
-				for (int k = 0; k < 8; k++)
-					sm.ang[lane - 1][i0 + k] = av[k];
 			}
+			__syncthreads (); /* every lane has read the start angles */
 			if (lane == 1)
-				st.hornAngle = a;
-			else
-				st.drumAngle = a;
+				st.hornAngle = okh ? st.hornAngle + (double)TBF_SUB * Dh : wrap1 (sm.ang[0][TBF_SUB - 1] + hornIncr);
+			if (lane == 2)
+				st.drumAngle = okd ? st.drumAngle + (double)TBF_SUB * Dd : wrap1 (sm.ang[1][TBF_SUB - 1] + drumIncr);
+		}
+		__syncthreads ();
+		{
+			const float* T0 = sm.tmp[0];
+			sm.xf[4 + n]    = (T0[n + 2] * K.hbfw[2]) + (K.hbfw[3] * T0[n + 1]) + (K.hbfw[4] * T0[n]);
 		}
 		__syncthreads ();
 		TBF_MARK (21);

@@ -126,6 +126,31 @@ int tbf_program_install (tbf_engine* e, uint32_t inst, uint32_t pc);
 /* name of the programme program change pc selects; returns 1 if in use, else 0 */
 int tbf_program_name (tbf_engine* e, uint32_t pc, char* out, uint32_t cap);
 
+/* ---- scheduled events (§8(f) row 1): a whole event script in one render ---- */
+#define TBF_EV_NOTE 0    /* id = key 0..383 (oscKeyOn/Off), value != 0: on */
+#define TBF_EV_PARAM 1   /* id = TBF_P_*, value as tbf_set_param */
+#define TBF_EV_CONTROL 2 /* id = tbf_midi_control_id (name), value 0..127 */
+#define TBF_EV_PROGRAM 3 /* id = program change 0..127 (tbf_program_install) */
+
+typedef struct tbf_event {
+	uint32_t block; /* block index (from the start of this call) before which it applies */
+	uint32_t inst;
+	int32_t  kind;  /* TBF_EV_* */
+	int32_t  id;
+	double   value;
+} tbf_event;
+
+/* id of a control function name for TBF_EV_CONTROL events, < 0 if not a hot-path name */
+int tbf_midi_control_id (const char* fn);
+/* render nblocks with events applied at their block boundaries (b_synth/lv2.cpp:
+ * 1130-1134 timing), into device memory like tbf_render_device.  Events must be sorted
+ * by block; within a block they apply in array order; events at or beyond nblocks apply
+ * after the render.  The host steps the control plane per block and uploads only the
+ * per-block control deltas, so one launch set covers a whole chunk of 64 blocks however
+ * many events land in it. */
+int tbf_render_events (tbf_engine* e, uint32_t nblocks, const tbf_event* ev, uint32_t nev, float* d_outL,
+                       float* d_outR, uint64_t stride, void* stream);
+
 int tbf_synchronize (tbf_engine* e);
 /* bit 0: vibrato scatter took the serial path in some block (informational) */
 int tbf_error_flags (tbf_engine* e, uint32_t* flags);

@@ -34,3 +34,17 @@ def refchk():
     if lib is None:
         pytest.skip("oracle/_ref not built (no /root/reference here)")
     return lib
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _torch_device_first():
+    """Tests that hand torch device buffers to the engine need torch's HIP runtime
+    initialised before libtbf initialises HIP in the same process (bench.py does the
+    same: torch.cuda.set_device before the engine)."""
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.zeros(1, device="cuda")
+    except Exception:
+        pass
+    yield

@@ -148,3 +148,76 @@ def test_gpu_program_install_matches_clap_script(oracle):
     eR, xR = compare(R, oR)
     print(f"program install: max|err| L={eL:.3g} R={eR:.3g} bit-exact L={xL:.6f} R={xR:.6f}")
     assert max(eL, eR) <= TOL
+
+
+def _script_events(eng, scens):
+    rows = []
+    for i, sc in enumerate(scens):
+        for (b, kind, a, v) in sc:
+            if kind == "note":
+                rows.append((b, i, 0, a, 1.0 if v else 0.0))
+            else:
+                rows.append((b, i, 1, a, float(v)))
+    return eng.events(rows)
+
+
+def test_gpu_render_events_one_call(oracle):
+    """§8(f) row 1: the event script of every instance (chord changes, drawbar, rotary,
+    percussion, vibrato and swell events at blocks 0/32/40/48/56) in ONE
+    tbf_render_events call -- per-block control deltas instead of launch segments --
+    is bit-identical to the oracle."""
+    import torch
+    eng, tpl, seeds, scens = _setup(oracle, 6, S.event_scenario)
+    nb = 72
+    L = torch.zeros((6, nb * 128), dtype=torch.float32, device="cuda")
+    R = torch.zeros_like(L)
+    eng.render_events_device(nb, _script_events(eng, scens), L.data_ptr(), R.data_ptr(), nb * 128)
+    eng.synchronize()
+    oL, oR, *_ = oracle_run(oracle, tpl, seeds, scens, nb)
+    eL, xL = compare(L.cpu().numpy(), oL)
+    eR, xR = compare(R.cpu().numpy(), oR)
+    print(f"render_events: max|err| L={eL:.3g} R={eR:.3g} bit-exact L={xL:.6f} R={xR:.6f}")
+    assert max(eL, eR) <= TOL
+
+
+def test_gpu_render_events_dense_across_chunks(oracle):
+    """Events on many blocks and across the 64-block chunk boundary (notes every 7
+    blocks, MIDI control functions and a programme change), split over two calls."""
+    import torch
+    from test_control_cpu import PGM
+    eng, tpl, seeds, scens = _setup(oracle, 3, S.bench_scenario)
+    assert eng.program_parse(PGM) == 4
+    cid = eng.control_id("upper.drawbar4")
+    assert cid >= 0 and eng.control_id("nope") < 0
+    rows, oscen = [], []
+    for i in range(3):
+        sc = list(scens[i])
+        for b in range(5, 150, 7):
+            k = 60 + (b + 3 * i) % 12
+            sc.append((b, "note", k, 1))
+            sc.append((b + 3, "note", k, 0))
+        sc.append((63, "param", S.P_DRAWBAR + 3, 5))   # same effect as upper.drawbar4 <- CC 48
+        sc.append((64, "param", S.P_HORN, 2))
+        oscen.append(sc)
+        for (b, kind, a, v) in sc:
+            if (b, a) == (63, S.P_DRAWBAR + 3):
+                rows.append((b, i, 2, cid, 48.0))  # rint ((127 - 48) * 8 / 127) = 5
+            elif kind == "note":
+                rows.append((b, i, 0, a, 1.0 if v else 0.0))
+            else:
+                rows.append((b, i, 1, a, float(v)))
+    ev = eng.events(rows)
+    nb = 160
+    L = torch.zeros((3, nb * 128), dtype=torch.float32, device="cuda")
+    R = torch.zeros_like(L)
+    first = ev[ev["block"] < 100]
+    rest = ev[ev["block"] >= 100].copy()
+    rest["block"] -= 100
+    eng.render_events_device(100, first, L.data_ptr(), R.data_ptr(), nb * 128)
+    eng.render_events_device(60, rest, L[:, 100 * 128:].data_ptr(), R[:, 100 * 128:].data_ptr(), nb * 128)
+    eng.synchronize()
+    oL, oR, *_ = oracle_run(oracle, tpl, seeds, oscen, nb)
+    eL, xL = compare(L.cpu().numpy(), oL)
+    eR, xR = compare(R.cpu().numpy(), oR)
+    print(f"dense events: max|err| L={eL:.3g} R={eR:.3g} bit-exact L={xL:.6f} R={xR:.6f}")
+    assert max(eL, eR) <= TOL

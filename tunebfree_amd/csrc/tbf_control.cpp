@@ -136,6 +136,20 @@ bool controlFunction (Instance& in, const char* fn, unsigned char u)
 	return true;
 }
 
+/* control function ids of TBF_EV_CONTROL events (tbf_midi_control_id) */
+const char* const kControlNames[] = {
+    "upper.drawbar16", "upper.drawbar513", "upper.drawbar8", "upper.drawbar4", "upper.drawbar223",
+    "upper.drawbar2", "upper.drawbar135", "upper.drawbar113", "upper.drawbar1",
+    "lower.drawbar16", "lower.drawbar513", "lower.drawbar8", "lower.drawbar4", "lower.drawbar223",
+    "lower.drawbar2", "lower.drawbar135", "lower.drawbar113", "lower.drawbar1",
+    "pedal.drawbar16", "pedal.drawbar513", "pedal.drawbar8", "pedal.drawbar4", "pedal.drawbar223",
+    "pedal.drawbar2", "pedal.drawbar135", "pedal.drawbar113", "pedal.drawbar1",
+    "percussion.enable", "percussion.decay", "percussion.harmonic", "percussion.volume",
+    "swellpedal1", "swellpedal2", "vibrato.knob", "vibrato.routing", "vibrato.upper", "vibrato.lower",
+    "overdrive.enable", "overdrive.character", "reverb.mix",
+    "rotary.speed-preset", "rotary.speed-select", "rotary.speed-toggle"};
+const int kNControls = (int)(sizeof (kControlNames) / sizeof (kControlNames[0]));
+
 /* ---------------------------------------------------------------- .pgm parser */
 enum { TKN_EOF = -1, TKN_ERROR = -2, TKN_STRING = 256 };
 
@@ -419,7 +433,25 @@ void randomizeDrawbars (Instance& in, unsigned bar[9])
 
 } // namespace
 
+int tbf::controlById (Instance& in, int id, int value)
+{
+	if (id < 0 || id >= kNControls || value < 0)
+		return -1;
+	controlFunction (in, kControlNames[id], (unsigned char)(value > 127 ? 127 : value));
+	return 0;
+}
+
 extern "C" {
+
+int tbf_midi_control_id (const char* fn)
+{
+	if (!fn)
+		return -1;
+	for (int i = 0; i < kNControls; i++)
+		if (!strcmp (fn, kControlNames[i]))
+			return i;
+	return -1;
+}
 
 int tbf_midi_control (tbf_engine* e, uint32_t inst, const char* fn, int32_t value)
 {

@@ -45,6 +45,8 @@ int tbf::fail (int code, const std::string& msg)
 /* blocks per kernel launch chunk: bounds the inter-stage buffers to
  * n_inst x TBF_CHUNK x 128 floats each (134 MB at 4096 instances) */
 #define TBF_CHUNK 64
+/* delta program entries one chunk may add (a chunk ends early when they would not fit) */
+#define DPROG_CAP(n) ((size_t)(n) * PROG_CAP * 2 + 4096)
 #define TBF_NSTAGES 5 /* k_tonegen, k_rv_in, k_rv_core, k_rv_out, k_whirl */
 
 /* ------------------------------------------------------------------ construction */
@@ -477,8 +479,10 @@ static int ensureDevice (tbf_engine* e)
 		std::vector<tbf_inst_const> k (n);
 		for (uint32_t i = 0; i < n; i++)
 			k[i] = e->inst[i].k;
-		if (e->cst.ensure (n) || e->ctl.ensure (n) || e->prog.ensure ((size_t)n * PROG_CAP))
+		if (e->cst.ensure (n) || e->ctl.ensure ((size_t)n * (TBF_CHUNK + 2)) ||
+		    e->prog.ensure ((size_t)n * PROG_CAP + DPROG_CAP (n)) || e->ctlIdx.ensure ((size_t)n * TBF_CHUNK))
 			return fail (-12, "out of device memory (control)");
+		e->persistStale = true;
 		HIPCHK (hipMemcpy (e->cst.p, k.data (), n * sizeof (tbf_inst_const), hipMemcpyHostToDevice));
 		e->hCtl.resize (n);
 		e->hProg.resize ((size_t)n * PROG_CAP);
@@ -488,59 +492,71 @@ static int ensureDevice (tbf_engine* e)
 	return 0;
 }
 
-/* control for the next segment; returns true if some instance must be re-stepped at
- * the following block (env -> steady transition) */
-static bool buildControl (tbf_engine* e, uint32_t& progLo, uint32_t& progHi, bool& ctlChanged)
+int tbf::controlById (Instance& in, int id, int value);
+
+/* a scheduled event (tbf_render_events) at its block boundary */
+static int applyEvent (tbf_engine* e, const tbf_event& ev)
 {
-	bool           again = false;
-	const uint32_t n     = (uint32_t)e->inst.size ();
-	progLo               = n;
-	progHi               = 0;
-	ctlChanged           = false;
-	for (uint32_t i = 0; i < n; i++) {
-		Instance&    in = e->inst[i];
-		tbf_seg_ctl& c  = e->hCtl[i];
-		const bool   tgDirty = in.tg.dirty ();
-		if (tgDirty) {
-			in.tg.step (in.prog, c);
-			in.progDirty = true;
-			in.ctlDirty  = true;
-			if (in.tg.dirty ())
-				again = true;
-		}
-		if (in.progDirty) {
-			if (in.prog.size () > PROG_CAP)
-				in.prog.resize (PROG_CAP);
-			std::copy (in.prog.begin (), in.prog.end (), e->hProg.begin () + (size_t)i * PROG_CAP);
-			progLo       = std::min (progLo, i);
-			progHi       = std::max (progHi, i + 1);
-			in.progDirty = false;
-		}
-		if (in.ctlDirty || in.revOpt >= 0) {
-			if (!tgDirty) {
-				/* mixdown fields that setters can change without a tonegen step */
-				c.swellPedalGain   = in.tg.swellPedalGain;
-				c.outputGain       = in.tg.swellPedalGain * in.tg.percDrawbarGain;
-				c.percEnvGainDecay = in.tg.percEnvGainDecay;
-				c.percEnvGainReset = in.tg.percEnvGainReset;
-				c.vibTable         = in.tg.vibTable;
-				c.vibMixed         = in.tg.vibMixed;
-			}
-			c.prog_off = i * PROG_CAP;
-			c.prog_len = (uint32_t)in.prog.size ();
-			odCtl (in, e->cfg.sample_rate, c);
-			c.rvWet       = in.rvG;
-			c.whBypass    = (uint32_t)in.whBypass;
-			c.whRevOption = in.revOpt;
-			in.revOpt     = -1;
-			in.ctlDirty   = (c.whRevOption >= 0); /* clear the one-shot next segment */
-			ctlChanged    = true;
-		}
+	if (ev.inst >= e->inst.size ())
+		return fail (-22, "event for a bad instance");
+	switch (ev.kind) {
+		case TBF_EV_NOTE: return tbf_note (e, ev.inst, ev.id, ev.value != 0.0);
+		case TBF_EV_PARAM: return tbf_set_param (e, ev.inst, ev.id, ev.value);
+		case TBF_EV_CONTROL:
+			if (controlById (e->inst[ev.inst], ev.id, (int)ev.value) < 0)
+				return fail (-22, "bad control function id");
+			return 0;
+		case TBF_EV_PROGRAM: return tbf_program_install (e, ev.inst, (uint32_t)ev.id);
+		default: return fail (-22, "bad event kind");
 	}
-	return again;
 }
 
-static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, uint64_t stride, hipStream_t s)
+/* one block of host control for instance i (the message-queue / active-list / routing
+ * part of oscGenerateFragment and the effect setters' per-block constants).  Updates
+ * the instance's current control e->hCtl[i] / program e->hProg; returns true when the
+ * control the next block renders with changed. */
+static bool stepControl (tbf_engine* e, uint32_t i, bool& progChanged)
+{
+	Instance&    in      = e->inst[i];
+	tbf_seg_ctl& c       = e->hCtl[i];
+	progChanged          = false;
+	const bool   tgDirty = in.tg.dirty ();
+	if (!tgDirty && !in.progDirty && !in.ctlDirty && in.revOpt < 0)
+		return false;
+	if (tgDirty) {
+		in.tg.step (in.prog, c);
+		in.progDirty = true;
+		in.ctlDirty  = true;
+	}
+	if (in.progDirty) {
+		if (in.prog.size () > PROG_CAP)
+			in.prog.resize (PROG_CAP);
+		std::copy (in.prog.begin (), in.prog.end (), e->hProg.begin () + (size_t)i * PROG_CAP);
+		in.progDirty = false;
+		progChanged  = true;
+	}
+	if (!tgDirty) {
+		/* mixdown fields that setters can change without a tonegen step */
+		c.swellPedalGain   = in.tg.swellPedalGain;
+		c.outputGain       = in.tg.swellPedalGain * in.tg.percDrawbarGain;
+		c.percEnvGainDecay = in.tg.percEnvGainDecay;
+		c.percEnvGainReset = in.tg.percEnvGainReset;
+		c.vibTable         = in.tg.vibTable;
+		c.vibMixed         = in.tg.vibMixed;
+	}
+	c.prog_off = i * PROG_CAP;
+	c.prog_len = (uint32_t)in.prog.size ();
+	odCtl (in, e->cfg.sample_rate, c);
+	c.rvWet       = in.rvG;
+	c.whBypass    = (uint32_t)in.whBypass;
+	c.whRevOption = in.revOpt; /* a one-shot: the next block gets a fresh entry without it */
+	in.revOpt     = -1;
+	in.ctlDirty   = (c.whRevOption >= 0);
+	return true;
+}
+
+static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, uint64_t stride, hipStream_t s,
+                       const tbf_event* ev = nullptr, uint32_t nev = 0)
 {
 	int rc = ensureDevice (e);
 	if (rc)
@@ -586,57 +602,104 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 	P.mid1      = e->mid1.p;
 	P.mid2      = e->mid2.p;
 	P.midStride = (uint64_t)TBF_CHUNK * TBF_BLK;
-	uint32_t b0 = 0;
+	const size_t dprogCap = DPROG_CAP (n);
+	e->chg.assign (n, 0);
+	uint32_t b0 = 0, evi = 0;
 	while (b0 < nblocks) {
-		uint32_t lo, hi;
-		bool     ctlChanged;
-		bool     again = buildControl (e, lo, hi, ctlChanged);
-		if (ctlChanged)
-			HIPCHK (hipMemcpyAsync (e->ctl.p, e->hCtl.data (), n * sizeof (tbf_seg_ctl), hipMemcpyHostToDevice, s));
-		if (hi > lo)
-			HIPCHK (hipMemcpyAsync (e->prog.p + (size_t)lo * PROG_CAP, e->hProg.data () + (size_t)lo * PROG_CAP,
-			                        (size_t)(hi - lo) * PROG_CAP * sizeof (tbf_prog_entry), hipMemcpyHostToDevice, s));
-		const uint32_t len      = again ? 1u : nblocks - b0;
-		bool           needSync = ctlChanged || hi > lo;
-		/* the segment runs in chunks; only the first chunk may apply a rotary one-shot */
-		for (uint32_t c0 = 0; c0 < len; c0 += TBF_CHUNK) {
-			P.nBlocks   = std::min<uint32_t> (TBF_CHUNK, len - c0);
-			P.outOffset = (uint64_t)(b0 + c0) * TBF_BLK;
-			if (c0 > 0 && ctlChanged) {
-				/* clear the rev-option one-shot for the following chunks */
-				bool any = false;
-				for (uint32_t i = 0; i < n; i++)
-					if (e->hCtl[i].whRevOption >= 0) {
-						e->hCtl[i].whRevOption = -1;
-						any                    = true;
-					}
-				if (any) {
-					HIPCHK (hipStreamSynchronize (s));
-					HIPCHK (hipMemcpyAsync (e->ctl.p, e->hCtl.data (), n * sizeof (tbf_seg_ctl), hipMemcpyHostToDevice, s));
-				}
-				ctlChanged = false;
-			}
-			const int nst = tbf_chain_stages (P.chain);
-			for (int k = 0; k < nst; k++) {
-				hipEvent_t e0 = nullptr, e1 = nullptr;
-				if (e->timeOn) {
-					HIPCHK (hipEventCreate (&e0));
-					HIPCHK (hipEventCreate (&e1));
-					HIPCHK (hipEventRecord (e0, s));
-				}
-				rc = tbf_launch_stage (&P, k, s);
+		/* host control for the chunk, block by block: entry indices per (block, instance),
+		 * new pool entries only where an instance's control changes */
+		const uint32_t want = std::min<uint32_t> (TBF_CHUNK, nblocks - b0);
+		e->dCtl.clear ();
+		e->dProg.clear ();
+		e->hIdx.resize ((size_t)want * n);
+		std::vector<uint32_t> cur (n);
+		for (uint32_t i = 0; i < n; i++)
+			cur[i] = i;
+		bool     delta = false;
+		uint32_t len   = 0;
+		for (; len < want; len++) {
+			if (e->dProg.size () + (size_t)n * PROG_CAP > dprogCap && len > 0)
+				break; /* delta program pool full: end the chunk here */
+			for (; evi < nev && ev[evi].block <= b0 + len; evi++) {
+				rc = applyEvent (e, ev[evi]);
 				if (rc)
-					return fail (rc, std::string ("kernel launch failed: ") + hipGetErrorString (hipGetLastError ()));
-				if (e->timeOn) {
-					HIPCHK (hipEventRecord (e1, s));
-					e->tev.push_back ({k, {e0, e1}});
+					return rc;
+			}
+			for (uint32_t i = 0; i < n; i++) {
+				bool pc;
+				if (stepControl (e, i, pc)) {
+					tbf_seg_ctl c = e->hCtl[i];
+					if (pc) {
+						c.prog_off = (uint32_t)((size_t)n * PROG_CAP + e->dProg.size ());
+						e->dProg.insert (e->dProg.end (), e->hProg.begin () + (size_t)i * PROG_CAP,
+						                 e->hProg.begin () + (size_t)i * PROG_CAP + c.prog_len);
+					} else if (cur[i] >= n)
+						c.prog_off = e->dCtl[cur[i] - n].prog_off; /* program of the previous delta */
+					cur[i] = n + (uint32_t)e->dCtl.size ();
+					e->dCtl.push_back (c);
+					e->chg[i] = 1;
+					delta     = true;
 				}
+				e->hIdx[(size_t)len * n + i] = cur[i];
 			}
 		}
-		/* host staging buffers are rewritten by the next buildControl: keep order */
-		if (needSync)
+		if (e->persistStale) {
+			HIPCHK (hipMemcpyAsync (e->ctl.p, e->hCtl.data (), n * sizeof (tbf_seg_ctl), hipMemcpyHostToDevice, s));
+			HIPCHK (hipMemcpyAsync (e->prog.p, e->hProg.data (), (size_t)n * PROG_CAP * sizeof (tbf_prog_entry),
+			                        hipMemcpyHostToDevice, s));
+			e->persistStale = false;
+		}
+		if (delta) {
+			HIPCHK (hipMemcpyAsync (e->ctl.p + n, e->dCtl.data (), e->dCtl.size () * sizeof (tbf_seg_ctl),
+			                        hipMemcpyHostToDevice, s));
+			if (!e->dProg.empty ())
+				HIPCHK (hipMemcpyAsync (e->prog.p + (size_t)n * PROG_CAP, e->dProg.data (),
+				                        e->dProg.size () * sizeof (tbf_prog_entry), hipMemcpyHostToDevice, s));
+			HIPCHK (hipMemcpyAsync (e->ctlIdx.p, e->hIdx.data (), (size_t)len * n * sizeof (uint32_t),
+			                        hipMemcpyHostToDevice, s));
+		}
+		P.ctlIdx    = delta ? e->ctlIdx.p : nullptr;
+		P.nBlocks   = len;
+		P.outOffset = (uint64_t)b0 * TBF_BLK;
+		const int nst = tbf_chain_stages (P.chain);
+		for (int k = 0; k < nst; k++) {
+			hipEvent_t e0 = nullptr, e1 = nullptr;
+			if (e->timeOn) {
+				HIPCHK (hipEventCreate (&e0));
+				HIPCHK (hipEventCreate (&e1));
+				HIPCHK (hipEventRecord (e0, s));
+			}
+			rc = tbf_launch_stage (&P, k, s);
+			if (rc)
+				return fail (rc, std::string ("kernel launch failed: ") + hipGetErrorString (hipGetLastError ()));
+			if (e->timeOn) {
+				HIPCHK (hipEventRecord (e1, s));
+				e->tev.push_back ({k, {e0, e1}});
+			}
+		}
+		if (delta) {
+			/* the instances' final entries become their current (pool 0..n-1) control for
+			 * the next chunk (one-shots cleared); staging buffers are reused, so keep order */
+			uint32_t lo = n, hi = 0;
+			for (uint32_t i = 0; i < n; i++)
+				if (e->chg[i]) {
+					e->hCtl[i].whRevOption = -1;
+					lo                     = std::min (lo, i);
+					hi                     = std::max (hi, i + 1);
+					e->chg[i]              = 0;
+				}
+			HIPCHK (hipMemcpyAsync (e->ctl.p, e->hCtl.data (), n * sizeof (tbf_seg_ctl), hipMemcpyHostToDevice, s));
+			if (hi > lo)
+				HIPCHK (hipMemcpyAsync (e->prog.p + (size_t)lo * PROG_CAP, e->hProg.data () + (size_t)lo * PROG_CAP,
+				                        (size_t)(hi - lo) * PROG_CAP * sizeof (tbf_prog_entry), hipMemcpyHostToDevice, s));
 			HIPCHK (hipStreamSynchronize (s));
+		}
 		b0 += len;
+	}
+	for (; evi < nev; evi++) { /* events at or after the last block apply to the next render */
+		rc = applyEvent (e, ev[evi]);
+		if (rc)
+			return rc;
 	}
 	return 0;
 }
@@ -651,6 +714,20 @@ int tbf_render_device (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		return fail (-19, "host-only engine (device -1) cannot render");
 	HIPCHK (hipSetDevice (e->cfg.device));
 	return renderImpl (e, nblocks, dL, dR, stride, stream ? (hipStream_t)stream : e->stream);
+}
+
+int tbf_render_events (tbf_engine* e, uint32_t nblocks, const tbf_event* ev, uint32_t nev, float* dL, float* dR,
+                       uint64_t stride, void* stream)
+{
+	if (!e || !dL || !dR || (nev && !ev))
+		return fail (-22, "null argument");
+	if (e->cfg.device < 0)
+		return fail (-19, "host-only engine (device -1) cannot render");
+	for (uint32_t k = 1; k < nev; k++)
+		if (ev[k].block < ev[k - 1].block)
+			return fail (-22, "events must be sorted by block");
+	HIPCHK (hipSetDevice (e->cfg.device));
+	return renderImpl (e, nblocks, dL, dR, stride, stream ? (hipStream_t)stream : e->stream, ev, nev);
 }
 
 int tbf_render (tbf_engine* e, uint32_t nblocks, float* outL, float* outR, uint64_t stride)

@@ -35,6 +35,7 @@ struct Programme {
 };
 
 int  fail (int code, const std::string& msg);
+int  controlById (struct Instance& in, int id, int value); /* tbf_control.cpp */
 void setCharacter (struct Instance& in, float v);
 
 } // namespace tbf
@@ -126,8 +127,15 @@ struct tbf_engine {
 	DevBuf<float>                           outL, outR;
 	DevBuf<float>                           mid1, mid2; /* inter-stage blocks of one launch chunk */
 	DevBuf<double>                          rvA, rvB;   /* reverb inter-kernel streams (FP64) */
-	std::vector<tbf_seg_ctl>                hCtl;
-	std::vector<tbf_prog_entry>             hProg;
+	std::vector<tbf_seg_ctl>                hCtl;  /* current control per instance (pool entries 0..n-1) */
+	std::vector<tbf_prog_entry>             hProg; /* current program per instance (slots i * PROG_CAP) */
+	/* per-chunk control deltas (tbf_render_events / renderImpl) */
+	std::vector<tbf_seg_ctl>                dCtl;
+	std::vector<tbf_prog_entry>             dProg;
+	std::vector<uint32_t>                   hIdx;
+	std::vector<uint8_t>                    chg;
+	DevBuf<uint32_t>                        ctlIdx;
+	bool                                    persistStale = true; /* device pool entries 0..n-1 need upload */
 	/* programme table (.pgm), src/program.h:26 MAXPROGS; pgm.controller.offset */
 	std::vector<Programme>                  progs = std::vector<Programme> (129);
 	int                                     pgmOffset = 1;

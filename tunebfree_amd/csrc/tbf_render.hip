@@ -128,6 +128,14 @@ __device__ __forceinline__ void prof_end (const tbf_launch& P, L& sm, uint32_t i
 		P.prof[(size_t)inst * TBF_PROF_SLOTS + threadIdx.x] += sm.prof[threadIdx.x];
 }
 
+/* the control entry of instance `inst` for block `blk` of the chunk: events land at
+ * block boundaries, so the host records a new pool entry only where one changes */
+__device__ __forceinline__ const tbf_seg_ctl& ctl_of (const tbf_launch& P, const tbf_seg_ctl* __restrict__ ctl,
+                                                      uint32_t blk, uint32_t inst)
+{
+	return ctl[P.ctlIdx ? P.ctlIdx[(size_t)blk * P.nInst + inst] : inst];
+}
+
 /* copy a state sub-struct between HBM and LDS, one dword per lane */
 template <typename T>
 __device__ __forceinline__ void copy_words (T* dst, const T* src)
@@ -526,13 +534,13 @@ k_tonegen (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl, const tbf_tp
 	const uint32_t inst = blockIdx.x + P.instBase;
 	if (inst >= P.nInst)
 		return;
-	const tbf_seg_ctl&  G = ctl[inst];
 	const tbf_tpl_desc* T = tpls + cst[inst].tpl;
 	tbf_tg_state*       S = &P.st[inst].tg;
 	prof_begin (P, sm);
 	copy_words (&sm.st, S);
 	__syncthreads ();
 	for (uint32_t blk = 0; blk < P.nBlocks; blk++) {
+		const tbf_seg_ctl& G = ctl_of (P, ctl, blk, inst);
 		stage_tonegen (P, sm, G, T);
 		if (P.chain == TBF_CHAIN_TONEGEN) {
 			float* oL = P.outL + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
@@ -656,7 +664,6 @@ k_rv_in (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 	if (inst >= P.nInst)
 		return;
 	const tbf_inst_const& K    = cst[inst];
-	const double          wet  = ctl[inst].rvWet;
 	tbf_rv_state*         S    = &P.st[inst].rv;
 	double*               mL   = P.rslab + (size_t)inst * P.slabLen + K.ringOff[12];
 	double*               mR   = P.rslab + (size_t)inst * P.slabLen + K.ringOff[13 + 12];
@@ -668,6 +675,7 @@ k_rv_in (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 	__syncthreads ();
 	tbf_rv_state& st = sm.st;
 	for (uint32_t blk = 0; blk < P.nBlocks; blk++) {
+		const double wet = ctl_of (P, ctl, blk, inst).rvWet;
 		const float* in = P.mid1 + (size_t)inst * P.midStride + (size_t)blk * TBF_BLK;
 #pragma unroll 1
 		for (int sb = 0; sb < TBF_BLK / TBF_SUB; sb++) {
@@ -879,7 +887,6 @@ k_rv_out (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 	if (inst >= P.nInst)
 		return;
 	const tbf_inst_const& K   = cst[inst];
-	const double          wet = ctl[inst].rvWet;
 	tbf_rv_state*         S   = &P.st[inst].rv;
 	const double*         bL  = rv_buf (P.rvB, P, inst, 0);
 	const double*         bR  = rv_buf (P.rvB, P, inst, 1);
@@ -929,7 +936,8 @@ k_rv_out (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 		TBF_MARK (11);
 		/* (c) output of block it-1: dry mix, dither, mono sum (src/reverb.cpp:766-787) */
 		if (haveC) {
-			const uint32_t ob = it - 1;
+			const uint32_t ob  = it - 1;
+			const double   wet = ctl_of (P, ctl, ob, inst).rvWet;
 			/* dither states F[0..128] of both streams for the block */
 			const uint32_t gL = st.fpdL2, gR = st.fpdR2;
 			const uint32_t l1 = xs_jump (P.xsJump, gL, lane + 1), r1 = xs_jump (P.xsJump, gR, lane + 1);
@@ -1138,7 +1146,7 @@ __device__ __forceinline__ void motion_add (float* ring, int U, float a, float b
 /* whirlProc2 (src/whirl.cpp:1191-1638) + whirlProc3 mic mix (1653-1681) */
 template <int W>
 __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ctl& G, const tbf_inst_const& K,
-                             int firstBlock, const float* __restrict__ in, float* __restrict__ oL,
+                             const float* __restrict__ in, float* __restrict__ oL,
                              float* __restrict__ oR)
 {
 	const int     lane  = threadIdx.x;
@@ -1162,7 +1170,8 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 	}
 	if (lane == 0) {
 		int brake;
-		whirl_speed (st, K, firstBlock ? G.whRevOption : -1, brake);
+		/* a control entry carrying a rotary selection is used for exactly one block */
+		whirl_speed (st, K, G.whRevOption, brake);
 		sm.brake = brake;
 	}
 	__syncthreads ();
@@ -1461,7 +1470,6 @@ k_whirl (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 	if (inst >= P.nInst)
 		return;
 	const tbf_inst_const& K  = cst[inst];
-	const tbf_seg_ctl&    G  = ctl[inst];
 	tbf_wh_state*         S  = &P.st[inst].wh;
 	float*                wr = P.wring + (size_t)inst * 4 * W;
 	prof_begin (P, sm);
@@ -1474,7 +1482,7 @@ k_whirl (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 		const float* in = P.mid2 + (size_t)inst * P.midStride + (size_t)blk * TBF_BLK;
 		float*       oL = P.outL + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
 		float*       oR = P.outR + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
-		stage_whirl<W> (P, sm, G, K, blk == 0, in, oL, oR);
+		stage_whirl<W> (P, sm, ctl_of (P, ctl, blk, inst), K, in, oL, oR);
 	}
 	__syncthreads ();
 	copy_words (S, &sm.st);

@@ -143,7 +143,8 @@ typedef struct tbf_launch {
 	double*               rvB;   /* [inst][2][midStride] k_rv_core -> k_rv_out: tap mix */
 	uint64_t              midStride;
 	double*               rslab; /* [inst][slabLen] */
-	const tbf_seg_ctl*    ctl;
+	const tbf_seg_ctl*    ctl;    /* control pool: [0, nInst) current per instance, then this chunk's deltas */
+	const uint32_t*       ctlIdx; /* [nBlocks][nInst] pool index per block, or NULL: entry inst */
 	const tbf_prog_entry* prog;
 	const uint32_t*       vibTab; /* [3][2048] */
 	const uint32_t*       xsJump; /* [32][TBF_XS_JUMP]: xorshift32^k (1 << j), k = 0..128 */

@@ -49,7 +49,14 @@ SIGNATURES = {
     "tbf_program_parse": (C.c_int, [C.c_void_p, C.c_char_p]),
     "tbf_program_install": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32]),
     "tbf_program_name": (C.c_int, [C.c_void_p, C.c_uint32, C.c_char_p, C.c_uint32]),
+    "tbf_midi_control_id": (C.c_int, [C.c_char_p]),
+    "tbf_render_events": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                    C.c_uint64, C.c_void_p]),
 }
+
+# tbf_event kinds (include/tbf.h)
+EV_NOTE, EV_PARAM, EV_CONTROL, EV_PROGRAM = 0, 1, 2, 3
+EVENT_DTYPE = np.dtype([("block", "<u4"), ("inst", "<u4"), ("kind", "<i4"), ("id", "<i4"), ("value", "<f8")])
 
 _lib = None
 
@@ -168,6 +175,23 @@ class Engine:
     def program_name(self, pc):
         buf = C.create_string_buffer(64)
         return buf.value.decode() if _check(self._lib.tbf_program_name(self._h, int(pc), buf, 64)) else None
+
+    def control_id(self, fn):
+        return self._lib.tbf_midi_control_id(fn.encode())
+
+    def events(self, rows):
+        """Pack (block, inst, kind, id, value) rows into the tbf_event array, stably sorted
+        by block."""
+        a = np.array([tuple(r) for r in rows], dtype=EVENT_DTYPE)
+        return a[np.argsort(a["block"], kind="stable")] if len(a) else a
+
+    def render_events_device(self, nblocks, events, outL_ptr, outR_ptr, stride, stream=None):
+        """tbf_render_events: enqueue a render of nblocks with scheduled events into device
+        memory (e.g. torch tensor data_ptr())."""
+        ev = np.ascontiguousarray(events, dtype=EVENT_DTYPE)
+        _check(self._lib.tbf_render_events(self._h, int(nblocks), ev.ctypes.data if len(ev) else None, len(ev),
+                                           C.c_void_p(int(outL_ptr)), C.c_void_p(int(outR_ptr)), int(stride),
+                                           None if stream is None else C.c_void_p(int(stream))))
 
     def synchronize(self):
         _check(self._lib.tbf_synchronize(self._h))

@@ -221,3 +221,43 @@ def test_gpu_render_events_dense_across_chunks(oracle):
     eR, xR = compare(R.cpu().numpy(), oR)
     print(f"dense events: max|err| L={eL:.3g} R={eR:.3g} bit-exact L={xL:.6f} R={xR:.6f}")
     assert max(eL, eR) <= TOL
+
+
+def test_gpu_cli_host_synth_sound(oracle, tmp_path):
+    """§8(f) row 3: the headless host shell (tunebfree_amd/tbf_cli, the counterpart of
+    src/main.cpp:243-292 and b_synth/lv2.cpp:212-239) pulls 256-frame periods through
+    tbf_synth_sound after installing a programme; its audio equals the oracle's."""
+    import subprocess
+    from pathlib import Path
+    from orc_bind import Chain, Template
+    from test_control_cpu import PGM
+    cli = Path(__file__).resolve().parents[1] / "tunebfree_amd" / "tbf_cli"
+    assert cli.exists(), "tbf_cli not built"
+    (tmp_path / "t.pgm").write_text(PGM)
+    nb, buf, n = 24, 256, 2
+    frames = nb * 128
+    subprocess.run([str(cli), "--pgm", str(tmp_path / "t.pgm"), "--program", "0", "--instances", str(n),
+                    "--buffer", str(buf), "--seconds", str(frames / 48000.0), "--seed", "5",
+                    "--character", "0.5", "--raw", str(tmp_path / "o.raw")], check=True, timeout=120)
+    raw = np.fromfile(tmp_path / "o.raw", np.float32)
+    L = np.zeros((n, frames), np.float32)
+    R = np.zeros((n, frames), np.float32)
+    pos, done = 0, 0
+    while done < frames:
+        nf = min(buf, frames - done)
+        blk = raw[pos: pos + n * nf * 2].reshape(n, nf, 2)
+        L[:, done:done + nf], R[:, done:done + nf] = blk[..., 0], blk[..., 1]
+        pos += n * nf * 2
+        done += nf
+    tpl = Template(oracle, seed=5)
+    worst = 0.0
+    for i in range(n):
+        ch = Chain(oracle, tpl, 5 + 1000 + i)
+        for (kind, a, v) in S.jazz1_params():
+            ch.param(a, v)
+        for k in (60, 64, 67, 72):
+            ch.note(k, 1)
+        oL, oR = ch.render(nb)
+        worst = max(worst, compare(L[i], oL)[0], compare(R[i], oR)[0])
+    print(f"cli host: max|err|={worst:.3g}")
+    assert worst <= TOL

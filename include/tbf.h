@@ -173,7 +173,9 @@ int tbf_debug_control (tbf_engine* e, uint32_t inst, double* out, uint32_t cap);
 /* the kernel's exact shortcuts of serial recurrences, evaluated on the host (same source,
  * csrc/tbf_exact.h): op 0 phase_run (in: v0, d, m -> out: ok, D), op 1 cnt_adv (in: c0,
  * d, n -> out: count), op 2 wrap1 (in: x, -, - -> out: fmod (x, 1)), op 3 xorshift
- * dither jump (in: x0, k, - -> out: jump-table state, k literal steps); n records */
+ * dither jump (in: x0, k, - -> out: jump-table state, k literal steps), op 4 cached
+ * phase steps along 4096 sub-blocks (in: v0, d, m -> out: mismatches vs phase_run, cache
+ * hits); n records */
 int tbf_debug_exact (int32_t op, const double* in3, double* out2, uint32_t n);
 /* stage timing: enable 1 zeroes per-instance counters and turns the kernel's marks on;
  * 0 copies out [inst][32] cycle sums (returns the count); -1 turns the marks off */

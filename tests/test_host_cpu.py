@@ -335,3 +335,14 @@ def test_dither_jump_table_matches_literal_xorshift():
         x ^= (x << 5) & 0xFFFFFFFF
         seq.append(x)
     assert [int(v) for v in _exact(3, [(16386, k, 0) for k in range(1, 6)])[:, 1]] == seq
+
+
+def test_phase_cache_matches_phase_run():
+    """The reverb core caches each line's closed-form phase step per binade
+    (phase_run_cached); along long runs it decides exactly like phase_run."""
+    rng = np.random.default_rng(11)
+    v0s = [float(x) - 2147483647 // 2 for x in rng.integers(0, 2 ** 31 - 1, 12)] + [3.0, -3.0, 1e-3, 0.75]
+    ds = [0.003251 * 0.06, 0.002088 * 0.06, 0.0, 1.0 / 3.0]
+    out = _exact(4, [(v, d, 64) for v in v0s for d in ds])
+    assert out[:, 0].sum() == 0
+    assert out[:, 1].sum() > 0.9 * 4096 * len(v0s) * 2  # the cache serves almost every sub-block

@@ -874,7 +874,7 @@ int tbf_debug_profile (tbf_engine* e, int32_t enable, uint64_t* out, uint32_t ca
 
 int tbf_debug_exact (int32_t op, const double* in, double* out, uint32_t n)
 {
-	if (!in || !out || op < 0 || op > 3)
+	if (!in || !out || op < 0 || op > 4)
 		return fail (-22, "bad arguments");
 	static std::vector<uint32_t> J;
 	if (op == 3 && J.empty ()) {
@@ -893,6 +893,28 @@ int tbf_debug_exact (int32_t op, const double* in, double* out, uint32_t n)
 			o[0] = cnt_adv ((int)a[0], (int)a[1], (int)a[2]);
 		} else if (op == 2) {
 			o[0] = wrap1 (a[0]);
+		} else if (op == 4) {
+			/* op 4: phase_run_cached along a run of 4096 sub-blocks of m steps from v0
+			 * (advancing like the kernel) vs phase_run: out = mismatches, cache hits */
+			double   v = a[0], cD = 0, cLo = 0, cHi = 0;
+			const int m = (int)a[2];
+			uint32_t bad = 0, hits = 0;
+			for (int s = 0; s < 4096; s++) {
+				double    D1 = 0, D2 = 0;
+				const double pD = cD;
+				const bool ok1 = phase_run (v, a[1], m, D1);
+				const bool ok2 = phase_run_cached (v, a[1], m, D2, cD, cLo, cHi);
+				hits += (pD > 0 && cD == pD && ok2) ? 1 : 0;
+				if (ok1 != ok2 || (ok1 && D1 != D2))
+					bad++;
+				if (ok1)
+					v = v + (double)m * D1;
+				else
+					for (int q = 0; q < m; q++)
+						v += a[1];
+			}
+			o[0] = bad;
+			o[1] = hits;
 		} else {
 			/* op 3: xorshift jump (device table) vs k literal steps from x0 */
 			const uint32_t x0 = (uint32_t)a[0];

@@ -48,6 +48,31 @@ TBF_HD bool phase_run (double v0, double d, int m, double& D)
 	return a0 >= lo && a0 <= hi && a1 >= lo && a1 <= hi && ((v0 < 0) == (w < 0));
 }
 
+/* phase_run with a per-line cache: the step D and the binade it belongs to only change
+ * when the phase crosses a binade, so the frexp/ldexp/rint analysis runs only then.
+ * Same result as phase_run (v0, d, m, D). */
+TBF_HD bool phase_run_cached (double v0, double d, int m, double& D, double& cD, double& cLo, double& cHi)
+{
+	if (cD > 0.0) {
+		const double w = v0 + (double)m * cD, a0 = fabs (v0), a1 = fabs (w);
+		if (a0 >= cLo && a0 <= cHi && a1 >= cLo && a1 <= cHi && ((v0 < 0) == (w < 0))) {
+			D = cD;
+			return true;
+		}
+	}
+	if (!phase_run (v0, d, m, D))
+		return false;
+	if (D > 0.0) {
+		int e;
+		frexp (v0, &e);
+		const double u = ldexp (1.0, e - 53);
+		cD             = D;
+		cLo            = ldexp (1.0, e - 1) + u;
+		cHi            = ldexp (1.0, e) - u;
+	}
+	return true;
+}
+
 /* fmod (x, 1.0) for the rotor angle update (src/whirl.cpp:1428-1429): for x in [0, 2)
  * fmod is x or x - 1, the latter exact by Sterbenz; anything else takes libm. */
 TBF_HD double wrap1 (double x)

@@ -756,11 +756,18 @@ __device__ __forceinline__ void rv_core_channel (const tbf_launch& P, RvCoreLds&
 	}
 	/* vibrato phases (closed form when exact, else the literal recurrence) and tap
 	 * offsets, one line at a time (bounds VGPRs); offsets parked in LDS */
-#pragma unroll 1
+#pragma unroll 2
 	for (int l = 0; l < 8; l++) {
 		const double v0 = st.vib[l], dl = K.vibDelta[l];
 		double       D, v;
-		if (phase_run (v0, dl, TBF_SUB, D)) {
+		double       cD = st.phD[l], cLo = st.phLo[l], cHi = st.phHi[l];
+		const bool   ok = phase_run_cached (v0, dl, TBF_SUB, D, cD, cLo, cHi);
+		if (lane == 0) { /* every lane has read the cache above */
+			st.phD[l]  = cD;
+			st.phLo[l] = cLo;
+			st.phHi[l] = cHi;
+		}
+		if (ok) {
 			v = v0 + (double)(n + 1) * D;
 		} else {
 			v = v0;

@@ -94,6 +94,10 @@ typedef struct tbf_rv_chan { /* one channel of the feedback network: k_rv_core w
 	uint32_t pad[4];
 	double   fb[8];     /* feedback of the channel's last sample */
 	double   vib[8];    /* vibrato phases */
+	double   phD[8];    /* cached closed-form phase step of each line (0: none; valid for the
+	                       instance's fixed vibDelta, zero it if that ever changes) ... */
+	double   phLo[8];   /* ... and the |phase| range of the binade it is valid in */
+	double   phHi[8];
 } tbf_rv_chan;
 
 typedef struct tbf_rv_state { /* reverb: k_rv_in / k_rv_core / k_rv_out */

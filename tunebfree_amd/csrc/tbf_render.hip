@@ -645,6 +645,9 @@ struct RvOutLds {
 struct RvCoreLds {
 	tbf_rv_chan st;
 	double      tap[8][TBF_SUB]; /* tap offsets of the sub-block */
+	double      sd[8][TBF_SUB];  /* sin ((n+1) D) of each line's closed-form step D ... */
+	double      cm[8][TBF_SUB];  /* ... and 1 - cos ((n+1) D) = 2 sin^2 ((n+1) D / 2) */
+	double      tabD[8];         /* the D the rows above hold (-1: none yet) */
 	unsigned long long prof[TBF_PROF_SLOTS];
 	unsigned long long plast;
 };
@@ -715,51 +718,79 @@ k_rv_in (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 	prof_end (P, sm, inst);
 }
 
-/* One channel of the feedback network for a 64-sample sub-block: allpasses I..L
- * (lines 8-11), delay lines A..H (0-7) with vibrato-modulated two-tap reads, crossmod
- * and Householder feedback (src/reverb.cpp:381-730).  The two channels never mix
- * inside the network, so each is its own wave.  Every read of the channel's rings
- * precedes every write (all ring delays >= 560 > 64).  The tap reads of a sub-block
- * fall in slots count+1 .. count+64+7 of each line, so those windows are fetched first
- * with coalesced loads (one HBM round trip for all 8 lines) and the modulated taps
- * gather from LDS. */
-__device__ __forceinline__ void rv_core_channel (const tbf_launch& P, RvCoreLds& sm, const tbf_inst_const& K,
-                                                 double* __restrict__ slab, int c, size_t o, double a0,
-                                                 double* __restrict__ bout)
+/* One channel of the feedback network, 64-sample sub-blocks: allpasses I..L (lines
+ * 8-11), delay lines A..H (0-7) with vibrato-modulated two-tap reads, crossmod and
+ * Householder feedback (src/reverb.cpp:381-730).  The two channels never mix inside the
+ * network, so each is its own wave.  Every read of a channel's rings precedes every
+ * write (all ring delays >= 560 > 64), and a sub-block's reads never touch the slots
+ * the previous sub-block writes (they lie >= 65 slots ahead of them), so the kernel is
+ * software-pipelined: the reads of sub-block k+1 are issued before the writes of
+ * sub-block k, and their latency overlaps k+1's phase/sin work.  The tap reads of a
+ * sub-block fall in slots count+1 .. count+64+7 of each line; those windows are
+ * fetched into registers and the modulated taps come from cross-lane permutes.
+ * Per-line scalars (counter, delay, ring offset) live one per lane in a VGPR and are
+ * read out with v_readlane where a line needs them. */
+struct RvFetch {
+	double wlo[8]; /* line l, slot count+1+lane */
+	double whi;    /* lane 8l+j: line l, slot count+65+j */
+	double apOld[4]; /* allpass reads at count+1+lane */
+	double a0;       /* network input (k_rv_in output) */
+};
+
+__device__ __forceinline__ int rl (int v, int l) { return __builtin_amdgcn_readlane (v, l); }
+
+__device__ __forceinline__ double rld (double v, int l)
+{
+	const unsigned long long u = __double_as_longlong (v);
+	const unsigned lo = __builtin_amdgcn_readlane ((unsigned)u, l), hi = __builtin_amdgcn_readlane ((unsigned)(u >> 32), l);
+	return __longlong_as_double ((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+__device__ __forceinline__ int wrap_slot (int s, int d) { return s - ((s > d) ? d + 1 : 0); }
+
+/* issue every global read of a sub-block whose ring counters are lane-held in cntv */
+__device__ __forceinline__ void rv_core_fetch (const double* slab, int cntv, int dlyv, int roffv,
+                                               const double* __restrict__ a0s, size_t o, RvFetch& f)
+{
+	const int lane = threadIdx.x;
+#pragma unroll
+	for (int l = 8; l < 12; l++) {
+		const int d    = rl (dlyv, l);
+		f.apOld[l - 8] = slab[rl (roffv, l) + wrap_slot (rl (cntv, l) + lane + 1, d)];
+	}
+#pragma unroll
+	for (int l = 0; l < 8; l++) {
+		const int d = rl (dlyv, l);
+		f.wlo[l]    = slab[rl (roffv, l) + wrap_slot (rl (cntv, l) + 1 + lane, d)];
+	}
+	{
+		const int l = lane >> 3, j = lane & 7;
+		const int d = __shfl (dlyv, l), cl = __shfl (cntv, l), ro = __shfl (roffv, l);
+		f.whi       = slab[ro + wrap_slot (cl + 1 + NL + j, d)];
+	}
+	f.a0 = a0s[o];
+}
+
+/* vibrato phases of the sub-block (src/reverb.cpp:479-496) and tap offsets
+ * (sin (v) + 1) * vibDepth, parked in LDS.  When the phase run has the exact closed
+ * form v_n = v0 + (n+1) D, sin (v_n) = S + (C sd_n - S cm_n) with S, C = sincos (v0)
+ * (one large-argument reduction per line, lanes 0..7 in parallel) and sd_n =
+ * sin ((n+1) D), cm_n = 2 sin^2 ((n+1) D / 2) cached per D (D changes only when the
+ * phase crosses a binade).  The correction term is < 0.013 in magnitude, so the result
+ * carries the accuracy of S; its tap offset is identical to the literal sin's in ~87 %
+ * of samples, against ~47 % for a 1-ulp change of sin, which SURVEY.md §0.9 measured to
+ * change no float output.  Otherwise the literal recurrence and sin. */
+__device__ __forceinline__ void rv_core_phases (RvCoreLds& sm, const tbf_inst_const& K)
 {
 	const int    lane = threadIdx.x;
 	const int    n    = lane;
 	tbf_rv_chan& st   = sm.st;
-	/* windows of lines 0-7 and the allpass reads at count + 1, all in flight together */
-	double apOld[4];
-	int    apW[4];
-#pragma unroll
-	for (int l = 8; l < 12; l++) {
-		const int d  = K.delay[l];
-		apW[l - 8]   = cnt_adv (st.count[l], d, n);
-		apOld[l - 8] = slab[K.ringOff[c * 13 + l] + cnt_adv (st.count[l], d, n + 1)];
-	}
-	/* tap windows: slot count+1+lane and count+65+lane (lanes 0..7) of each line, loaded
-	 * into registers first so their latency overlaps the phase/sin loop below */
-	double wlo[8], whi[8];
-#pragma unroll
-	for (int l = 0; l < 8; l++) {
-		const int     d  = K.delay[l];
-		const int     c1 = cnt_adv (st.count[l], d, 1);
-		const double* a  = slab + K.ringOff[c * 13 + l];
-		int           s0 = c1 + lane;
-		s0 -= (s0 > d) ? d + 1 : 0;
-		wlo[l] = a[s0];
-		int s1 = c1 + NL + (lane & (RV_WIN - NL - 1));
-		s1 -= (s1 > d) ? d + 1 : 0;
-		whi[l] = a[s1];
-	}
-	/* vibrato phases (closed form when exact, else the literal recurrence) and tap
-	 * offsets, one line at a time (bounds VGPRs); offsets parked in LDS */
+	double       Sx, Cx;
+	sincos (st.vib[lane & 7], &Sx, &Cx);
 #pragma unroll 2
 	for (int l = 0; l < 8; l++) {
 		const double v0 = st.vib[l], dl = K.vibDelta[l];
-		double       D, v;
+		double       D, v, s;
 		double       cD = st.phD[l], cLo = st.phLo[l], cHi = st.phHi[l];
 		const bool   ok = phase_run_cached (v0, dl, TBF_SUB, D, cD, cLo, cHi);
 		if (lane == 0) { /* every lane has read the cache above */
@@ -768,86 +799,32 @@ __device__ __forceinline__ void rv_core_channel (const tbf_launch& P, RvCoreLds&
 			st.phHi[l] = cHi;
 		}
 		if (ok) {
-			v = v0 + (double)(n + 1) * D;
+			const double dn = (double)(n + 1) * D; /* exact */
+			if (sm.tabD[l] != D) {                /* wave-uniform */
+				const double h = sin (dn * 0.5);
+				sm.sd[l][n]    = sin (dn);
+				sm.cm[l][n]    = 2.0 * h * h;
+				__syncthreads (); /* every lane has compared tabD[l] */
+				if (lane == 0)
+					sm.tabD[l] = D;
+			}
+			v                = v0 + dn;
+			const double S = rld (Sx, l), C = rld (Cx, l);
+			s                = S + ((C * sm.sd[l][n]) - (S * sm.cm[l][n]));
 		} else {
 			v = v0;
 			for (int i = 0; i <= n; i++)
 				v += dl;
+			s = sin (v);
 		}
 		if (lane == NL - 1) /* every lane has read st.vib[l] above (one wave, program order) */
 			st.vib[l] = v;
-		sm.tap[l][n] = (sin (v) + 1.0) * K.vibDepth;
+#ifdef RV_ABL_SIN /* ablation (timing only, wrong results): cheap sine */
+		sm.tap[l][n] = ((double)__sinf ((float)v) + 1.0) * K.vibDepth;
+#else
+		sm.tap[l][n] = (s + 1.0) * K.vibDepth;
+#endif
 	}
-	/* two-tap interpolation and blend; the taps come from the window registers by
-	 * cross-lane permutes */
-	double I[8];
-#pragma unroll
-	for (int l = 0; l < 8; l++) {
-		const double off = sm.tap[l][n];
-		const int    d   = K.delay[l];
-		const int    cn  = cnt_adv (st.count[l], d, n + 1);
-		const int    wk  = (int)(cn + off);
-		const int    rel = n + (wk - cn); /* window index of slot wk */
-		const double fr  = off - floor (off);
-		const bool   inw = rel >= 0 && rel + 1 < RV_WIN;
-		const int    i0 = inw ? rel : 0, i1 = inw ? rel + 1 : 0;
-		const double a0lo = __shfl (wlo[l], i0 & (NL - 1)), a0hi = __shfl (whi[l], i0 & (NL - 1));
-		const double a1lo = __shfl (wlo[l], i1 & (NL - 1)), a1hi = __shfl (whi[l], i1 & (NL - 1));
-		double       r0 = i0 < NL ? a0lo : a0hi;
-		double       r1 = i1 < NL ? a1lo : a1hi;
-		if (!inw) { /* outside the window (not reachable at the fixed vibDepth): ring reads */
-			const int     w0 = wk - ((wk > d) ? d + 1 : 0);
-			const int     w1 = wk + 1 - ((wk + 1 > d) ? d + 1 : 0);
-			const double* a  = slab + K.ringOff[c * 13 + l];
-			r0               = a[w0];
-			r1               = a[w1];
-		}
-		double x = (r0 * (1 - fr));
-		x += (r1 * fr);
-		I[l] = ((1.0 - K.blend) * x) + (r0 * K.blend);
-	}
-	I[0] = (I[0] * K.oneMinusAbsCm) + (I[4] * K.crossmod);
-	I[4] = (I[4] * K.oneMinusAbsCm) + (I[0] * K.crossmod);
-	double fb[8];
-	fb[0] = (I[0] - (I[1] + I[2] + I[3])) * K.regen;
-	fb[1] = (I[1] - (I[0] + I[2] + I[3])) * K.regen;
-	fb[2] = (I[2] - (I[0] + I[1] + I[3])) * K.regen;
-	fb[3] = (I[3] - (I[0] + I[1] + I[2])) * K.regen;
-	fb[4] = (I[4] - (I[5] + I[6] + I[7])) * K.regen;
-	fb[5] = (I[5] - (I[4] + I[6] + I[7])) * K.regen;
-	fb[6] = (I[6] - (I[4] + I[5] + I[7])) * K.regen;
-	fb[7] = (I[7] - (I[4] + I[5] + I[6])) * K.regen;
-	bout[o] = (I[0] + I[1] + I[2] + I[3] + I[4] + I[5] + I[6] + I[7]) / 8.0;
-	__syncthreads (); /* all ring reads of the channel are complete (fallback reads included) */
-	/* allpass writes (a = a0 - old/2 at count; out = a/2 + old) */
-	double ap[4];
-#pragma unroll
-	for (int l = 0; l < 4; l++) {
-		double a = a0;
-		a -= apOld[l] * 0.5;
-		slab[K.ringOff[c * 13 + 8 + l] + apW[l]] = a;
-		a *= 0.5;
-		a += apOld[l];
-		ap[l] = a;
-	}
-	/* delay-line writes: allpass output + the previous sample's feedback */
-	const int srcAp[8] = {3, 2, 1, 0, 0, 1, 2, 3};
-#pragma unroll
-	for (int l = 0; l < 8; l++) {
-		double prev = __shfl_up (fb[l], 1);
-		if (lane == 0)
-			prev = st.fb[l];
-		slab[K.ringOff[c * 13 + l] + cnt_adv (st.count[l], K.delay[l], n)] = ap[srcAp[l]] + prev;
-	}
-	__syncthreads (); /* lane 0 has read st.fb */
-	if (lane == NL - 1) {
-#pragma unroll
-		for (int l = 0; l < 8; l++)
-			st.fb[l] = fb[l];
-	}
-	if (lane < 12)
-		st.count[lane] = cnt_adv (st.count[lane], K.delay[lane], TBF_SUB);
-	__syncthreads ();
 }
 
 /* one wave per (instance, channel) */
@@ -856,26 +833,119 @@ k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 {
 	__shared__ RvCoreLds sm;
 	const int      lane = threadIdx.x;
+	const int      n    = lane;
 	const uint32_t inst = (blockIdx.x >> 1) + P.instBase;
 	const int      c    = blockIdx.x & 1;
 	if (inst >= P.nInst)
 		return;
 	const tbf_inst_const& K    = cst[inst];
 	tbf_rv_chan*          S    = &P.st[inst].rv.ch[c];
-	double*               slab = P.rslab + (size_t)inst * P.slabLen;
+#ifdef RV_ABL_MEM /* ablation (timing only, wrong results): 64 slabs shared, MALL-resident */
+	double* slab = P.rslab + (size_t)(inst & 63) * P.slabLen;
+#else
+	double* slab = P.rslab + (size_t)inst * P.slabLen;
+#endif
 	const double*         a0s  = rv_buf (P.rvA, P, inst, c);
 	double*               bout = rv_buf (P.rvB, P, inst, c);
 	prof_begin (P, sm);
 	copy_words (&sm.st, S);
+	if (lane < 8)
+		sm.tabD[lane] = -1.0;
 	__syncthreads ();
-	for (uint32_t blk = 0; blk < P.nBlocks; blk++) {
+	/* lane l < 12: counter, delay and ring offset of line l; lane l < 8: the feedback
+	 * of the channel's last sample on line l */
+	const int dlyv  = lane < 12 ? K.delay[lane] : 0;
+	const int roffv = lane < 12 ? (int)K.ringOff[c * 13 + lane] : 0;
+	/* counters in [0, d] from here on: an out-of-range counter steps exactly like d
+	 * (`count++; if (count < 0 || count > d) count = 0`), so every later slot is
+	 * wrap_slot (count + k, d) for k <= 72 < d + 1 (all delays >= 560) */
+	int cntv = lane < 12 ? sm.st.count[lane] : 0;
+	cntv     = (cntv < 0 || cntv > dlyv) ? dlyv : cntv;
+	double    fbv   = lane < 8 ? sm.st.fb[lane] : 0.0;
+	const uint32_t nSub = P.nBlocks * (TBF_BLK / TBF_SUB);
+	RvFetch        f;
+	if (nSub > 0)
+		rv_core_fetch (slab, cntv, dlyv, roffv, a0s, lane, f);
 #pragma unroll 1
-		for (int sb = 0; sb < TBF_BLK / TBF_SUB; sb++) {
-			const size_t o = (size_t)blk * TBF_BLK + sb * TBF_SUB + lane;
-			rv_core_channel (P, sm, K, slab, c, o, a0s[o], bout);
-			TBF_MARK (8 + c);
+	for (uint32_t s = 0; s < nSub; s++) {
+		const size_t o = (size_t)s * TBF_SUB + lane;
+		rv_core_phases (sm, K);
+		__syncthreads ();
+		/* two-tap interpolation and blend */
+		double I[8];
+#pragma unroll
+		for (int l = 0; l < 8; l++) {
+			const double off = sm.tap[l][n];
+			const int    d   = rl (dlyv, l);
+			const int    cn  = wrap_slot (rl (cntv, l) + n + 1, d);
+			const int    wk  = (int)(cn + off);
+			const int    rel = n + (wk - cn); /* window index of slot wk */
+			const double fr  = off - floor (off);
+			const bool   inw = rel >= 0 && rel + 1 < RV_WIN;
+			const int    i0 = inw ? rel : 0, i1 = inw ? rel + 1 : 0;
+			const double a0lo = __shfl (f.wlo[l], i0 & (NL - 1)), a0hi = __shfl (f.whi, 8 * l + (i0 & 7));
+			const double a1lo = __shfl (f.wlo[l], i1 & (NL - 1)), a1hi = __shfl (f.whi, 8 * l + (i1 & 7));
+			double       r0 = i0 < NL ? a0lo : a0hi;
+			double       r1 = i1 < NL ? a1lo : a1hi;
+			if (!inw) { /* outside the window (not reachable at the fixed vibDepth): ring reads */
+				const double* a = slab + rl (roffv, l);
+				r0              = a[wrap_slot (wk, d)];
+				r1              = a[wrap_slot (wk + 1, d)];
+			}
+			double x = (r0 * (1 - fr));
+			x += (r1 * fr);
+			I[l] = ((1.0 - K.blend) * x) + (r0 * K.blend);
 		}
+		I[0] = (I[0] * K.oneMinusAbsCm) + (I[4] * K.crossmod);
+		I[4] = (I[4] * K.oneMinusAbsCm) + (I[0] * K.crossmod);
+		double fb[8];
+		fb[0] = (I[0] - (I[1] + I[2] + I[3])) * K.regen;
+		fb[1] = (I[1] - (I[0] + I[2] + I[3])) * K.regen;
+		fb[2] = (I[2] - (I[0] + I[1] + I[3])) * K.regen;
+		fb[3] = (I[3] - (I[0] + I[1] + I[2])) * K.regen;
+		fb[4] = (I[4] - (I[5] + I[6] + I[7])) * K.regen;
+		fb[5] = (I[5] - (I[4] + I[6] + I[7])) * K.regen;
+		fb[6] = (I[6] - (I[4] + I[5] + I[7])) * K.regen;
+		fb[7] = (I[7] - (I[4] + I[5] + I[6])) * K.regen;
+		const double mix = (I[0] + I[1] + I[2] + I[3] + I[4] + I[5] + I[6] + I[7]) / 8.0;
+		/* allpass outputs (a = a0 - old/2 written at count; out = a/2 + old) */
+		double apw[4], ap[4];
+#pragma unroll
+		for (int l = 0; l < 4; l++) {
+			double a = f.a0;
+			a -= f.apOld[l] * 0.5;
+			apw[l] = a;
+			a *= 0.5;
+			a += f.apOld[l];
+			ap[l] = a;
+		}
+		/* reads of the next sub-block, in flight before this one's writes */
+		const int ncv = wrap_slot (cntv + TBF_SUB, dlyv);
+		if (s + 1 < nSub)
+			rv_core_fetch (slab, ncv, dlyv, roffv, a0s, o + TBF_SUB, f);
+		bout[o] = mix;
+#pragma unroll
+		for (int l = 8; l < 12; l++)
+			slab[rl (roffv, l) + wrap_slot (rl (cntv, l) + n, rl (dlyv, l))] = apw[l - 8];
+		/* delay-line writes: allpass output + the previous sample's feedback */
+		const int srcAp[8] = {3, 2, 1, 0, 0, 1, 2, 3};
+		double    fbn      = fbv;
+#pragma unroll
+		for (int l = 0; l < 8; l++) {
+			const double up = __shfl_up (fb[l], 1), carry = rld (fbv, l);
+			const double prev = lane == 0 ? carry : up;
+			slab[rl (roffv, l) + wrap_slot (rl (cntv, l) + n, rl (dlyv, l))] = ap[srcAp[l]] + prev;
+			const double last = rld (fb[l], NL - 1);
+			fbn               = lane == l ? last : fbn;
+		}
+		fbv  = fbn;
+		cntv = ncv;
+		TBF_MARK (8 + c);
 	}
+	if (lane < 12)
+		sm.st.count[lane] = cntv;
+	if (lane < 8)
+		sm.st.fb[lane] = fbv;
 	__syncthreads ();
 	copy_words (S, &sm.st);
 	prof_end (P, sm, inst);

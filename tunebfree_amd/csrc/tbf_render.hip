@@ -644,7 +644,7 @@ struct RvOutLds {
 
 struct RvCoreLds {
 	tbf_rv_chan st;
-	double      tap[8][TBF_SUB]; /* tap offsets of the sub-block */
+	double      win[8][RV_WIN];  /* tap windows of the sub-block: slots count+1 .. count+72 */
 	double      sd[8][TBF_SUB];  /* sin ((n+1) D) of each line's closed-form step D ... */
 	double      cm[8][TBF_SUB];  /* ... and 1 - cos ((n+1) D) = 2 sin^2 ((n+1) D / 2) */
 	double      tabD[8];         /* the D the rows above hold (-1: none yet) */
@@ -771,60 +771,72 @@ __device__ __forceinline__ void rv_core_fetch (const double* slab, int cntv, int
 	f.a0 = a0s[o];
 }
 
-/* vibrato phases of the sub-block (src/reverb.cpp:479-496) and tap offsets
- * (sin (v) + 1) * vibDepth, parked in LDS.  When the phase run has the exact closed
- * form v_n = v0 + (n+1) D, sin (v_n) = S + (C sd_n - S cm_n) with S, C = sincos (v0)
- * (one large-argument reduction per line, lanes 0..7 in parallel) and sd_n =
- * sin ((n+1) D), cm_n = 2 sin^2 ((n+1) D / 2) cached per D (D changes only when the
- * phase crosses a binade).  The correction term is < 0.013 in magnitude, so the result
- * carries the accuracy of S; its tap offset is identical to the literal sin's in ~87 %
- * of samples, against ~47 % for a 1-ulp change of sin, which SURVEY.md §0.9 measured to
- * change no float output.  Otherwise the literal recurrence and sin. */
-__device__ __forceinline__ void rv_core_phases (RvCoreLds& sm, const tbf_inst_const& K)
+/* Vibrato phases (src/reverb.cpp:479-496) and tap offsets (sin (v) + 1) * vibDepth.
+ * When a line's phase run has the exact closed form v_n = v0 + (n+1) D (phase_run),
+ * sin (v_n) = S + (C sd_n - S cm_n) with S, C = sincos (v0) and sd_n = sin ((n+1) D),
+ * cm_n = 2 sin^2 ((n+1) D / 2); the rows sd, cm are cached per D, which changes only
+ * when the phase crosses a binade.  The correction term is < 0.013 in magnitude, so the
+ * result carries the accuracy of S; its tap offset is identical to the literal sin's in
+ * ~87 % of samples, against ~47 % for a 1-ulp change of sin, which SURVEY.md §0.9
+ * measured to change no float output.  Otherwise the literal recurrence and sin.
+ *
+ * rv_core_lines: the per-line (wave-uniform) part for all 8 lines at once, line l on
+ * lane l (lanes 8..63 duplicate): closed-form check, step D, sincos of the start phase;
+ * the end phase of every closed-form line is stored. */
+__device__ __forceinline__ uint64_t rv_core_lines (RvCoreLds& sm, double vdl, double& v0x, double& Sx, double& Cx, double& Dx)
 {
 	const int    lane = threadIdx.x;
-	const int    n    = lane;
+	const int    li   = lane & 7;
 	tbf_rv_chan& st   = sm.st;
-	double       Sx, Cx;
-	sincos (st.vib[lane & 7], &Sx, &Cx);
-#pragma unroll 2
-	for (int l = 0; l < 8; l++) {
-		const double v0 = st.vib[l], dl = K.vibDelta[l];
-		double       D, v, s;
-		double       cD = st.phD[l], cLo = st.phLo[l], cHi = st.phHi[l];
-		const bool   ok = phase_run_cached (v0, dl, TBF_SUB, D, cD, cLo, cHi);
-		if (lane == 0) { /* every lane has read the cache above */
-			st.phD[l]  = cD;
-			st.phLo[l] = cLo;
-			st.phHi[l] = cHi;
-		}
-		if (ok) {
-			const double dn = (double)(n + 1) * D; /* exact */
-			if (sm.tabD[l] != D) {                /* wave-uniform */
-				const double h = sin (dn * 0.5);
-				sm.sd[l][n]    = sin (dn);
-				sm.cm[l][n]    = 2.0 * h * h;
-				__syncthreads (); /* every lane has compared tabD[l] */
-				if (lane == 0)
-					sm.tabD[l] = D;
-			}
-			v                = v0 + dn;
-			const double S = rld (Sx, l), C = rld (Cx, l);
-			s                = S + ((C * sm.sd[l][n]) - (S * sm.cm[l][n]));
-		} else {
-			v = v0;
-			for (int i = 0; i <= n; i++)
-				v += dl;
-			s = sin (v);
-		}
-		if (lane == NL - 1) /* every lane has read st.vib[l] above (one wave, program order) */
-			st.vib[l] = v;
-#ifdef RV_ABL_SIN /* ablation (timing only, wrong results): cheap sine */
-		sm.tap[l][n] = ((double)__sinf ((float)v) + 1.0) * K.vibDepth;
-#else
-		sm.tap[l][n] = (s + 1.0) * K.vibDepth;
-#endif
+	const double v0   = st.vib[li];
+	double       D = 0.0, cD = st.phD[li], cLo = st.phLo[li], cHi = st.phHi[li];
+	const bool   ok = phase_run_cached (v0, vdl, TBF_SUB, D, cD, cLo, cHi);
+	sincos (v0, &Sx, &Cx);
+	v0x = v0;
+	Dx  = D;
+	__syncthreads (); /* every lane has read st */
+	if (lane < 8) {
+		st.phD[li]  = cD;
+		st.phLo[li] = cLo;
+		st.phHi[li] = cHi;
+		if (ok)
+			st.vib[li] = v0 + (double)TBF_SUB * D; /* exact, = lane 63's v_n */
 	}
+	return __ballot (ok) & 0xff;
+}
+
+/* the lane's tap offset on line l */
+__device__ __forceinline__ double rv_core_tap (RvCoreLds& sm, const tbf_inst_const& K, int l, uint64_t okm, double v0x,
+                                               double Sx, double Cx, double Dx)
+{
+	const int n = threadIdx.x;
+	double    s;
+	if ((okm >> l) & 1) {
+		const double D  = rld (Dx, l);
+		const double dn = (double)(n + 1) * D; /* exact */
+		if (sm.tabD[l] != D) {                /* wave-uniform */
+			const double h = sin (dn * 0.5);
+			sm.sd[l][n]    = sin (dn);
+			sm.cm[l][n]    = 2.0 * h * h;
+			__syncthreads (); /* every lane has compared tabD[l] */
+			if (n == 0)
+				sm.tabD[l] = D;
+		}
+		const double S = rld (Sx, l), C = rld (Cx, l);
+		s              = S + ((C * sm.sd[l][n]) - (S * sm.cm[l][n]));
+#ifdef RV_ABL_SIN /* ablation (timing only, wrong results): cheap sine */
+		s = (double)__sinf ((float)(rld (v0x, l) + dn));
+#endif
+	} else {
+		const double dl = K.vibDelta[l];
+		double       v  = rld (v0x, l);
+		for (int i = 0; i <= n; i++)
+			v += dl;
+		if (n == NL - 1)
+			sm.st.vib[l] = v;
+		s = sin (v);
+	}
+	return (s + 1.0) * K.vibDepth;
 }
 
 /* one wave per (instance, channel) */
@@ -854,7 +866,8 @@ k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 	__syncthreads ();
 	/* lane l < 12: counter, delay and ring offset of line l; lane l < 8: the feedback
 	 * of the channel's last sample on line l */
-	const int dlyv  = lane < 12 ? K.delay[lane] : 0;
+	const int    dlyv = lane < 12 ? K.delay[lane] : 0;
+	const double vdl  = K.vibDelta[lane & 7];
 	const int roffv = lane < 12 ? (int)K.ringOff[c * 13 + lane] : 0;
 	/* counters in [0, d] from here on: an out-of-range counter steps exactly like d
 	 * (`count++; if (count < 0 || count > d) count = 0`), so every later slot is
@@ -869,24 +882,29 @@ k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 #pragma unroll 1
 	for (uint32_t s = 0; s < nSub; s++) {
 		const size_t o = (size_t)s * TBF_SUB + lane;
-		rv_core_phases (sm, K);
+		/* per-line phase analysis and sincos, lanes 0..7 in parallel */
+		double         v0x, Sx, Cx, Dx;
+		const uint64_t okm = rv_core_lines (sm, vdl, v0x, Sx, Cx, Dx);
+		/* windows to LDS (the reads were issued one sub-block ago) */
+#pragma unroll
+		for (int l = 0; l < 8; l++)
+			sm.win[l][lane] = f.wlo[l];
+		if (lane < 64)
+			sm.win[lane >> 3][NL + (lane & 7)] = f.whi;
 		__syncthreads ();
 		/* two-tap interpolation and blend */
 		double I[8];
-#pragma unroll
+#pragma unroll 2
 		for (int l = 0; l < 8; l++) {
-			const double off = sm.tap[l][n];
+			const double off = rv_core_tap (sm, K, l, okm, v0x, Sx, Cx, Dx);
 			const int    d   = rl (dlyv, l);
 			const int    cn  = wrap_slot (rl (cntv, l) + n + 1, d);
 			const int    wk  = (int)(cn + off);
 			const int    rel = n + (wk - cn); /* window index of slot wk */
 			const double fr  = off - floor (off);
 			const bool   inw = rel >= 0 && rel + 1 < RV_WIN;
-			const int    i0 = inw ? rel : 0, i1 = inw ? rel + 1 : 0;
-			const double a0lo = __shfl (f.wlo[l], i0 & (NL - 1)), a0hi = __shfl (f.whi, 8 * l + (i0 & 7));
-			const double a1lo = __shfl (f.wlo[l], i1 & (NL - 1)), a1hi = __shfl (f.whi, 8 * l + (i1 & 7));
-			double       r0 = i0 < NL ? a0lo : a0hi;
-			double       r1 = i1 < NL ? a1lo : a1hi;
+			const int    i0  = inw ? rel : 0;
+			double       r0 = sm.win[l][i0], r1 = sm.win[l][i0 + 1];
 			if (!inw) { /* outside the window (not reachable at the fixed vibDepth): ring reads */
 				const double* a = slab + rl (roffv, l);
 				r0              = a[wrap_slot (wk, d)];

@@ -90,8 +90,11 @@ struct WhLds {
 	float        x2[TBF_SUB + 4];
 	float        xd1[TBF_SUB + 1];
 	float        rd[2][TBF_SUB]; /* drum ring outputs -> drum shelf outputs (in place) */
-	float        tmp[3][TBF_SUB + 2]; /* DF2 state sequences temp[n-2 .. 63] of the serial biquads */
+	float        tmp[4][TBF_SUB + 2]; /* DF2 state sequences temp[n-2 .. 63]: horn A, horn B, drum L, drum R */
+	float        xn[TBF_SUB];         /* input of the next sub-block (horn A runs one sub-block ahead) */
+	float        aOut[TBF_SUB];       /* horn A output of the current sub-block */
 	int          brake;
+	int          aReady;              /* aOut holds the current sub-block's horn A output */
 	unsigned long long prof[TBF_PROF_SLOTS];
 	unsigned long long plast;
 };
@@ -1238,11 +1241,42 @@ __device__ __forceinline__ void motion_add (float* ring, int U, float a, float b
 	}
 }
 
+/* one DF2 state recurrence over a sub-block (one lane): tp[0..1] = temp[-2], temp[-1],
+ * tp[2 + i] = temp[i]; scrub applies the block-end NaN scrub (src/whirl.cpp:1622-1630)
+ * to the incoming state first */
+__device__ __forceinline__ void wh_serial (const float* ip, float* tp, float* fz, float a1, float a2, bool scrub)
+{
+	float z0 = fz[0], z1 = fz[1];
+	if (scrub) {
+		if (isnan (z0))
+			z0 = 0.f;
+		if (isnan (z1))
+			z1 = 0.f;
+	}
+	tp[0] = z1;
+	tp[1] = z0;
+	for (int i0 = 0; i0 < TBF_SUB; i0 += 8) {
+		float xv[8];
+#pragma unroll
+		for (int k = 0; k < 8; k++)
+			xv[k] = ip[i0 + k];
+#pragma unroll
+		for (int k = 0; k < 8; k++) {
+			const float t = xv[k] - (a1 * z0) - (a2 * z1);
+			z1             = z0;
+			z0             = t;
+			tp[2 + i0 + k] = t;
+		}
+	}
+	fz[0] = z0;
+	fz[1] = z1;
+}
+
 /* whirlProc2 (src/whirl.cpp:1191-1638) + whirlProc3 mic mix (1653-1681) */
 template <int W>
 __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ctl& G, const tbf_inst_const& K,
-                             const float* __restrict__ in, float* __restrict__ oL,
-                             float* __restrict__ oR)
+                             const float* __restrict__ in, const float* __restrict__ nextIn,
+                             float* __restrict__ oL, float* __restrict__ oR)
 {
 	const int     lane  = threadIdx.x;
 	tbf_wh_state& st    = sm.st;
@@ -1273,10 +1307,9 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 	TBF_MARK (20);
 	const double   hornIncr = st.hornIncr, drumIncr = st.drumIncr;
 	const uint32_t WM       = (uint32_t)W - 1u;
-	/* serial filter coefficients: lane 0 horn A, lanes 1-2 drum shelf */
-	const float* cfa = lane == 0 ? K.hafw : K.drf;
+	/* serial filter coefficients: lane 0 horn A, lane 1 horn B, lanes 2-3 drum shelf */
+	const float* cfa = lane == 0 ? K.hafw : (lane == 1 ? K.hbfw : K.drf);
 	const float  fa0 = cfa[0], fa1 = cfa[1]; /* a1, a2 of the serial state recurrences */
-	const float  hb0 = K.hbfw[0], hb1 = K.hbfw[1];
 
 #pragma unroll 1
 	for (int sb = 0; sb < TBF_BLK / TBF_SUB; sb++) {
@@ -1307,64 +1340,45 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 		/* DF2 biquads (EQ_IIR, src/whirl.cpp:1479-1485): only the state recurrence
 		 * temp[n] = (x - a1 temp[n-1]) - a2 temp[n-2] is serial; the output
 		 * y[n] = (b0 temp[n] + b1 temp[n-1]) + b2 temp[n-2] is the same expression
-		 * evaluated lane-parallel afterwards.  Pass 1: lane 0 horn filter A (hafw) on the
-		 * input, lanes 1, 2 the drum shelves (drfL, drfR) on the ring outputs. */
-		if (lane < 3) {
-			const int    fi = lane == 0 ? 0 : lane + 1;
-			const float* ip = lane == 0 ? sm.xx + 1 : sm.rd[lane - 1];
-			float*       tp = sm.tmp[lane];
-			float        z0 = st.fz[fi][0], z1 = st.fz[fi][1];
-			tp[0] = z1;
-			tp[1] = z0;
-			for (int i0 = 0; i0 < TBF_SUB; i0 += 8) {
-				float xv[8];
-#pragma unroll
-				for (int k = 0; k < 8; k++)
-					xv[k] = ip[i0 + k];
-#pragma unroll
-				for (int k = 0; k < 8; k++) {
-					const float t = xv[k] - (fa0 * z0) - (fa1 * z1);
-					z1            = z0;
-					z0            = t;
-					tp[2 + i0 + k] = t;
-				}
-			}
-			st.fz[fi][0] = z0;
-			st.fz[fi][1] = z1;
+		 * evaluated lane-parallel afterwards.  Horn filter B runs on horn filter A's
+		 * output, so A runs one sub-block ahead: one serial pass advances A over the
+		 * next sub-block (lane 0), B over this one (lane 1) and the drum shelves over
+		 * this one's ring outputs (lanes 2, 3).  A's own pass runs only when it is not
+		 * ahead (launch start, after a bypassed block). */
+		const bool aNext = sb + 1 < TBF_BLK / TBF_SUB || nextIn != nullptr;
+		if (aNext)
+			sm.xn[n] = (float)((double)(sb + 1 < TBF_BLK / TBF_SUB ? in[(sb + 1) * TBF_SUB + n] : nextIn[n]) + 1e-14);
+		__syncthreads ();
+		if (!sm.aReady) {
+			if (lane == 0)
+				wh_serial (sm.xx + 1, sm.tmp[0], st.fz[0], K.hafw[0], K.hafw[1], false);
+			__syncthreads ();
+			const float* T0 = sm.tmp[0];
+			sm.aOut[n]      = (T0[n + 2] * K.hafw[2]) + (K.hafw[3] * T0[n + 1]) + (K.hafw[4] * T0[n]);
+			__syncthreads ();
+		}
+		if (lane < 4 && (lane > 0 || aNext)) {
+			const float* ip = lane == 0 ? sm.xn : (lane == 1 ? sm.aOut : sm.rd[lane - 2]);
+			/* crossing into the next block: A's state gets that block's NaN scrub first */
+			wh_serial (ip, sm.tmp[lane], st.fz[lane], fa0, fa1, lane == 0 && sb + 1 == TBF_BLK / TBF_SUB);
 		}
 		__syncthreads ();
 		{
-			/* filter outputs: horn A -> x1 (scratch until FILTER_C), drum shelves in place */
-			const float* T0 = sm.tmp[0];
-			sm.x1[4 + n]    = (T0[n + 2] * K.hafw[2]) + (K.hafw[3] * T0[n + 1]) + (K.hafw[4] * T0[n]);
+			/* filter outputs: horn B -> xf, drum shelves in place, horn A of the next
+			 * sub-block -> aOut */
+			const float* T1 = sm.tmp[1];
+			sm.xf[4 + n]    = (T1[n + 2] * K.hbfw[2]) + (K.hbfw[3] * T1[n + 1]) + (K.hbfw[4] * T1[n]);
 #pragma unroll
 			for (int c = 0; c < 2; c++) {
-				const float* Tc = sm.tmp[1 + c];
+				const float* Tc = sm.tmp[2 + c];
 				sm.rd[c][n]     = (Tc[n + 2] * K.drf[2]) + (K.drf[3] * Tc[n + 1]) + (K.drf[4] * Tc[n]);
 			}
-		}
-		__syncthreads ();
-		/* pass 2: lane 0 horn filter B (hbfw) on the horn A output */
-		if (lane == 0) {
-			float  z0 = st.fz[1][0], z1 = st.fz[1][1];
-			float* tp = sm.tmp[0];
-			tp[0]     = z1;
-			tp[1]     = z0;
-			for (int i0 = 0; i0 < TBF_SUB; i0 += 8) {
-				float xv[8];
-#pragma unroll
-				for (int k = 0; k < 8; k++)
-					xv[k] = sm.x1[4 + i0 + k];
-#pragma unroll
-				for (int k = 0; k < 8; k++) {
-					const float t = xv[k] - (hb0 * z0) - (hb1 * z1);
-					z1            = z0;
-					z0            = t;
-					tp[2 + i0 + k] = t;
-				}
+			if (aNext) {
+				const float* T0 = sm.tmp[0];
+				sm.aOut[n]      = (T0[n + 2] * K.hafw[2]) + (K.hafw[3] * T0[n + 1]) + (K.hafw[4] * T0[n]);
 			}
-			st.fz[1][0] = z0;
-			st.fz[1][1] = z1;
+			if (lane == 0)
+				sm.aReady = aNext;
 		}
 		/* rotor angles, angle = fmod (angle + incr, 1) per sample (src/whirl.cpp:1428-1429):
 		 * inside one binade of the angle every sum lands on the same grid, so the run is
@@ -1397,11 +1411,6 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 				st.hornAngle = okh ? st.hornAngle + (double)TBF_SUB * Dh : wrap1 (sm.ang[0][TBF_SUB - 1] + hornIncr);
 			if (lane == 2)
 				st.drumAngle = okd ? st.drumAngle + (double)TBF_SUB * Dd : wrap1 (sm.ang[1][TBF_SUB - 1] + drumIncr);
-		}
-		__syncthreads ();
-		{
-			const float* T0 = sm.tmp[0];
-			sm.xf[4 + n]    = (T0[n + 2] * K.hbfw[2]) + (K.hbfw[3] * T0[n + 1]) + (K.hbfw[4] * T0[n]);
 		}
 		__syncthreads ();
 		TBF_MARK (21);
@@ -1543,7 +1552,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 	}
 	if (lane == 0) {
 		/* NaN scrub, src/whirl.cpp:1622-1630 */
-		for (int f = 0; f < 4; f++)
+		for (int f = sm.aReady ? 1 : 0; f < 4; f++)
 			for (int j = 0; j < 2; j++)
 				if (isnan (st.fz[f][j]))
 					st.fz[f][j] = 0.f;
@@ -1569,6 +1578,8 @@ k_whirl (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 	float*                wr = P.wring + (size_t)inst * 4 * W;
 	prof_begin (P, sm);
 	copy_words (&sm.st, S);
+	if (threadIdx.x == 0)
+		sm.aReady = 0;
 	for (uint32_t i = threadIdx.x; i < 4u * W; i += NL)
 		(&sm.wring[0][0])[i] = wr[i];
 	__syncthreads ();
@@ -1577,7 +1588,9 @@ k_whirl (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 		const float* in = P.mid2 + (size_t)inst * P.midStride + (size_t)blk * TBF_BLK;
 		float*       oL = P.outL + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
 		float*       oR = P.outR + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
-		stage_whirl<W> (P, sm, ctl_of (P, ctl, blk, inst), K, in, oL, oR);
+		/* the next block's input, when horn filter A may run ahead into it */
+		const float* nextIn = (blk + 1 < P.nBlocks && !ctl_of (P, ctl, blk + 1, inst).whBypass) ? in + TBF_BLK : nullptr;
+		stage_whirl<W> (P, sm, ctl_of (P, ctl, blk, inst), K, in, nextIn, oL, oR);
 	}
 	__syncthreads ();
 	copy_words (S, &sm.st);

@@ -182,7 +182,8 @@ def test_gpu_render_events_one_call(oracle):
 
 def test_gpu_render_events_dense_across_chunks(oracle):
     """Events on many blocks and across the 64-block chunk boundary (notes every 7
-    blocks, MIDI control functions and a programme change), split over two calls."""
+    blocks, MIDI control functions, a programme change, whirl bypass toggles), split
+    over two calls."""
     import torch
     from test_control_cpu import PGM
     eng, tpl, seeds, scens = _setup(oracle, 3, S.bench_scenario)
@@ -198,6 +199,10 @@ def test_gpu_render_events_dense_across_chunks(oracle):
             sc.append((b + 3, "note", k, 0))
         sc.append((63, "param", S.P_DRAWBAR + 3, 5))   # same effect as upper.drawbar4 <- CC 48
         sc.append((64, "param", S.P_HORN, 2))
+        # whirl bypass on/off mid-chunk and across the chunk edge (horn filter A runs
+        # a sub-block ahead; it must not run into a bypassed block)
+        for (b, v) in ((30, 1), (33, 0), (63, 1), (64, 0), (99, 1), (101, 0)):
+            sc.append((b, "param", S.P_WHIRL_BYPASS, v))
         oscen.append(sc)
         for (b, kind, a, v) in sc:
             if (b, a) == (63, S.P_DRAWBAR + 3):

@@ -322,10 +322,19 @@ void TgTemplate::build (double rate, const double* mts128, const double* ratio9,
 		}
 		const double U = att[i] / aplSum;
 		float*       y = bank.data () + o;
+		/* a partial of amplitude 0 adds 0 * sin (finite) = +-0 to the sum, which leaves
+		 * it unchanged, so only the nonzero partials are evaluated (the default
+		 * spectrum has one) */
+		int nz[12], nnz = 0;
+		for (int j = 0; j < 12; j++)
+			if (apl[j] != 0.0)
+				nz[nnz++] = j;
 		for (size_t n = 0; n < wl[i]; n++) {
 			double s = 0.0;
-			for (int j = 0; j < 12; j++)
+			for (int q = 0; q < nnz; q++) {
+				const int j = nz[q];
 				s += apl[j] * sin (remainder ((plHz[j] * fullCircle * (double)n) / sr, fullCircle));
+			}
 			float v = (rnd.next () < (2147483647 >> 1)) ? (float)(1.0 / 32767.0) : 0.0f;
 			y[n]    = (float)((double)v + (U * s));
 		}

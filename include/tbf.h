@@ -84,6 +84,14 @@ int tbf_engine_destroy (tbf_engine* e);
 int tbf_template_create (tbf_engine* e, const double* mts128, const double* ratio9, uint32_t seed,
                          uint32_t* tpl_id);
 
+/* n templates built on the device: the same tables as n
+ * tbf_template_create calls, with the wave bank's sines and its per-sample rand() draws
+ * (each thread jumping the glibc stream to its chunk) computed on the engine's GPU.
+ * mts128: n x 128 frequencies or NULL; ratio9: n x 9 or NULL; seeds[n]; ids[n] out.
+ * Needs a device engine (-19 on a host-only engine). */
+int tbf_templates_create (tbf_engine* e, uint32_t n, const double* mts128, const double* ratio9,
+                          const uint32_t* seeds, uint32_t* tpl_ids);
+
 /* Add n instances: instance k uses template tpl_ids[k] and per-instance seed seeds[k]
  * (srand before allocReverb/allocPreamp).  Returns the first new index in *first. */
 int      tbf_instances_add (tbf_engine* e, uint32_t n, const uint32_t* tpl_ids, const uint32_t* seeds,
@@ -175,7 +183,8 @@ int tbf_debug_control (tbf_engine* e, uint32_t inst, double* out, uint32_t cap);
  * d, n -> out: count), op 2 wrap1 (in: x, -, - -> out: fmod (x, 1)), op 3 xorshift
  * dither jump (in: x0, k, - -> out: jump-table state, k literal steps), op 4 cached
  * phase steps along 4096 sub-blocks (in: v0, d, m -> out: mismatches vs phase_run, cache
- * hits); n records */
+ * hits), op 5 glibc rand() jump (in: seed, k, - -> out: next draw after GlibcRand::discard
+ * (k), after k literal draws); n records */
 int tbf_debug_exact (int32_t op, const double* in3, double* out2, uint32_t n);
 /* stage timing: enable 1 zeroes per-instance counters and turns the kernel's marks on;
  * 0 copies out [inst][32] cycle sums (returns the count); -1 turns the marks off */

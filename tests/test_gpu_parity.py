@@ -266,3 +266,48 @@ def test_gpu_cli_host_synth_sound(oracle, tmp_path):
         worst = max(worst, compare(L[i], oL)[0], compare(R[i], oR)[0])
     print(f"cli host: max|err|={worst:.3g}")
     assert worst <= TOL
+
+
+@pytest.mark.parametrize("sr", [48000.0, 96000.0])
+def test_gpu_device_templates_match_host(sr):
+    """§8(f) row 2: templates built on the device (tbf_templates_create: per-chunk
+    jumps of the glibc rand() stream + the writeSamples sines) equal the host-built
+    templates -- which the CPU tests pin to the oracle and the reference fixtures --
+    bit for bit: wave bank, wheel lengths, envelopes, key-compression table.  One batch
+    holds the 6 table tunings three times with distinct seeds; a second the 12-TET
+    default."""
+    import ctypes as C
+    import json
+    import time
+    from pathlib import Path
+    import tunebfree_amd as T
+    tunings = json.loads((Path(__file__).resolve().parent / "golden" / "tunings.json").read_text())
+    names = [k for k in sorted(tunings) if tunings[k] is not None]
+    mts = np.stack([np.asarray(tunings[nm], np.float64) for nm in names] * 3)
+    seeds = [300 + j for j in range(len(mts))]
+    eng = T.Engine(sample_rate=sr, device=0)
+    t0 = time.perf_counter()
+    dids = eng.templates(seeds, mts128=mts)
+    t_dev = time.perf_counter() - t0
+    dids += eng.templates([1, 2, 3])  # 12-TET (no MTS master)
+    t0 = time.perf_counter()
+    hids = [eng.template(mts128=mts[j], seed=seeds[j]) for j in range(len(mts))]
+    t_host = time.perf_counter() - t0
+    hids += [eng.template(seed=s) for s in (1, 2, 3)]
+    lib = T.load_library()
+    lib.tbf_debug_tables.restype = C.c_int
+    lib.tbf_debug_tables.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
+    for d, h in zip(dids, hids):
+        db, dl = eng.template_bank(d)
+        hb, hl = eng.template_bank(h)
+        assert np.array_equal(dl, hl)
+        assert np.array_equal(db.view(np.uint32), hb.view(np.uint32)), (d, int(np.sum(db != hb)))
+        tabs = []
+        for t in (d, h):
+            a, r, k = np.zeros((9, 128), np.float32), np.zeros((9, 128), np.float32), np.zeros(128, np.float32)
+            assert lib.tbf_debug_tables(eng._h, t, a.ctypes.data, r.ctypes.data, k.ctypes.data) >= 0
+            tabs.append((a, r, k))
+        for x, y in zip(*tabs):
+            assert np.array_equal(x.view(np.uint32), y.view(np.uint32))
+    print(f"device templates @{sr:.0f}: {len(mts)} in {t_dev * 1e3:.1f} ms; host {t_host * 1e3:.1f} ms")
+    eng.close()

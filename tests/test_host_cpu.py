@@ -346,3 +346,19 @@ def test_phase_cache_matches_phase_run():
     out = _exact(4, [(v, d, 64) for v in v0s for d in ds])
     assert out[:, 0].sum() == 0
     assert out[:, 1].sum() > 0.9 * 4096 * len(v0s) * 2  # the cache serves almost every sub-block
+
+
+def test_glibc_rand_jump_matches_literal_draws():
+    """csrc/tbf_rand.h: GlibcRand::discard (k) -- the polynomial jump x^k mod
+    (x^31 - x^28 - 1) over Z/2^32 that the device template builder uses per chunk --
+    leaves the same stream as k literal rand() calls (src/tonegen.cpp:1449 draws)."""
+    rows = [(s, k, 0) for s in (1, 7, 12345) for k in (0, 1, 2, 30, 31, 32, 61, 310, 4097, 359853)]
+    out = _exact(5, rows)
+    assert np.array_equal(out[:, 0], out[:, 1])
+
+
+def test_device_templates_refused_on_host_engine():
+    eng = T.Engine(sample_rate=48000.0, device=-1)
+    with pytest.raises(RuntimeError):
+        eng.templates([7])
+    eng.close()

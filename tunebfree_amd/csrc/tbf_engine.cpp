@@ -15,6 +15,8 @@
 
 #include "../../include/tbf.h"
 #include "tbf_engine_impl.h"
+#include "tbf_rand.h"
+#include "tbf_tpl.h"
 #include "tbf_exact.h"
 #include "tbf_host.h"
 #include "tbf_types.h"
@@ -253,6 +255,94 @@ int tbf_template_create (tbf_engine* e, const double* mts128, const double* rati
 	t->build (e->cfg.sample_rate, mts128, ratio9, seed);
 	*id = (uint32_t)e->tpls.size ();
 	e->tpls.push_back (std::move (t));
+	e->deviceReady = false;
+	return 0;
+}
+
+int tbf_templates_create (tbf_engine* e, uint32_t n, const double* mts128, const double* ratio9, const uint32_t* seeds,
+                          uint32_t* ids)
+{
+	if (!e || (n && (!seeds || !ids)))
+		return fail (-22, "null argument");
+	if (!e->stream)
+		return fail (-19, "device template construction needs a device engine");
+	if (n == 0)
+		return 0;
+	HIPCHK (hipSetDevice (e->cfg.device));
+	const double                             sr = e->cfg.sample_rate;
+	std::vector<std::unique_ptr<TgTemplate>> ts (n);
+	std::vector<uint32_t>                    E (61 * (size_t)n);
+	std::vector<uint64_t>                    total (n), base (n);
+	std::vector<tbf_tpl_wheel>               wh ((size_t)n * TBF_NW);
+	uint64_t                                 sum = 0;
+	uint32_t                                 maxChunks = 0, maxLen = 0;
+	for (uint32_t t = 0; t < n; t++) {
+		ts[t].reset (new TgTemplate ());
+		TgTemplate& T = *ts[t];
+		T.prepare (sr, mts128 ? mts128 + 128 * (size_t)t : nullptr, ratio9 ? ratio9 + 9 * (size_t)t : nullptr);
+		uint32_t  W[31];
+		GlibcRand rnd (seeds[t]);
+		rnd.window (W);
+		gr_extend (W, &E[61 * (size_t)t]);
+		total[t] = T.total;
+		base[t]  = sum;
+		sum += T.total;
+		maxChunks = std::max (maxChunks, (uint32_t)((T.total + 511) / 512));
+		for (int i = 1; i <= TBF_NW; i++) {
+			tbf_tpl_wheel& w = wh[(size_t)t * TBF_NW + i - 1];
+			memset (&w, 0, sizeof (w));
+			w.off = T.off[i];
+			w.len = T.len[i];
+			w.np  = T.nPartials[i];
+			w.U   = T.U[i];
+			for (int q = 0; q < w.np; q++) {
+				w.amp[q] = T.pAmp[i][q];
+				w.hz[q]  = T.pHz[i][q];
+			}
+			maxLen = std::max (maxLen, w.len);
+		}
+	}
+	DevBuf<uint32_t>      dE;
+	DevBuf<uint64_t>      dTot, dBase;
+	DevBuf<tbf_tpl_wheel> dWh;
+	DevBuf<uint8_t>       dLsb;
+	DevBuf<float>         dBank;
+	if (dE.ensure (E.size ()) || dTot.ensure (n) || dBase.ensure (n) || dWh.ensure (wh.size ()) || dLsb.ensure (sum) ||
+	    dBank.ensure (sum))
+		return fail (-12, "device template buffers");
+	int rc = 0;
+	std::vector<float> hb (sum);
+	do {
+		hipStream_t s = e->stream;
+		if (hipMemcpyAsync (dE.p, E.data (), E.size () * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
+		    hipMemcpyAsync (dTot.p, total.data (), n * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+		    hipMemcpyAsync (dBase.p, base.data (), n * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+		    hipMemcpyAsync (dWh.p, wh.data (), wh.size () * sizeof (tbf_tpl_wheel), hipMemcpyHostToDevice, s) != hipSuccess) {
+			rc = fail (-5, "template upload");
+			break;
+		}
+		if (tbf_tpl_launch (n, maxChunks, maxLen, dE.p, dTot.p, dBase.p, dWh.p, dLsb.p, dBank.p, sr, s)) {
+			rc = fail (-5, "template kernels");
+			break;
+		}
+		if (hipMemcpyAsync (hb.data (), dBank.p, sum * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+		    hipStreamSynchronize (s) != hipSuccess) {
+			rc = fail (-5, "template download");
+			break;
+		}
+	} while (0);
+	dE.release (), dTot.release (), dBase.release (), dWh.release (), dLsb.release (), dBank.release ();
+	if (rc)
+		return rc;
+	for (uint32_t t = 0; t < n; t++) {
+		TgTemplate& T = *ts[t];
+		T.bank.assign (hb.begin () + base[t], hb.begin () + base[t] + total[t]);
+		GlibcRand rnd (seeds[t]);
+		rnd.discard (T.total); /* the draws of the bank */
+		T.finish (rnd);
+		ids[t] = (uint32_t)e->tpls.size ();
+		e->tpls.push_back (std::move (ts[t]));
+	}
 	e->deviceReady = false;
 	return 0;
 }
@@ -874,7 +964,7 @@ int tbf_debug_profile (tbf_engine* e, int32_t enable, uint64_t* out, uint32_t ca
 
 int tbf_debug_exact (int32_t op, const double* in, double* out, uint32_t n)
 {
-	if (!in || !out || op < 0 || op > 4)
+	if (!in || !out || op < 0 || op > 5)
 		return fail (-22, "bad arguments");
 	static std::vector<uint32_t> J;
 	if (op == 3 && J.empty ()) {
@@ -893,6 +983,13 @@ int tbf_debug_exact (int32_t op, const double* in, double* out, uint32_t n)
 			o[0] = cnt_adv ((int)a[0], (int)a[1], (int)a[2]);
 		} else if (op == 2) {
 			o[0] = wrap1 (a[0]);
+		} else if (op == 5) {
+			GlibcRand j ((unsigned)a[0]), l ((unsigned)a[0]);
+			j.discard ((uint64_t)a[1]);
+			for (uint64_t q = 0; q < (uint64_t)a[1]; q++)
+				l.next ();
+			o[0] = j.next ();
+			o[1] = l.next ();
 		} else if (op == 4) {
 			/* op 4: phase_run_cached along a run of 4096 sub-blocks of m steps from v0
 			 * (advancing like the kernel) vs phase_run: out = mismatches, cache hits */

@@ -29,6 +29,10 @@ struct GlibcRand {
 	int     f = 3, r = 0;
 	explicit GlibcRand (unsigned int seed);
 	int32_t next ();
+	/* the 31 words y[i-31 .. i-1] before the next draw y[i] (oldest first) */
+	void window (uint32_t* W) const;
+	/* skip k draws by the polynomial jump of tbf_rand.h (same state as k next () calls) */
+	void discard (uint64_t k);
 };
 
 struct Contrib {
@@ -48,7 +52,19 @@ struct TgTemplate {
 	float                             keyCompTable[128];
 	float                             attackEnv[9][TBF_BLK];
 	float                             releaseEnv[9][TBF_BLK];
+	/* writeSamples spectrum per wheel: y[n] = (float)(lsb (draw off + n) + U sum_q
+	 * amp[q] sin (remainder (hz[q] 2 pi n / sr, 2 pi))) over the nonzero partials */
+	double                            U[TBF_NW + 1];
+	int                               nPartials[TBF_NW + 1];
+	double                            pAmp[TBF_NW + 1][12], pHz[TBF_NW + 1][12];
+	size_t                            total = 0; /* bank samples = rand() draws of the bank */
 	void build (double sr, const double* mts128, const double* ratio9, unsigned int seed);
+	/* the steps of build: prepare (tables, wheel lengths and spectra), synthHost (the
+	 * bank, one draw per sample), finish (key compression, envelopes: the draws after
+	 * the bank) */
+	void prepare (double sr, const double* mts128, const double* ratio9);
+	void synthHost (GlibcRand& rnd);
+	void finish (GlibcRand& rnd);
 };
 
 struct WhirlTables {

@@ -9,6 +9,7 @@
 #include <limits>
 
 #include "tbf_host.h"
+#include "tbf_rand.h"
 
 namespace tbf {
 
@@ -45,6 +46,24 @@ int32_t GlibcRand::next ()
 		r = 0;
 	}
 	return (int32_t)(val >> 1);
+}
+
+void GlibcRand::window (uint32_t* W) const
+{
+	for (int j = 0; j < 31; j++)
+		W[j] = (uint32_t)s[(f + j) % 31];
+}
+
+void GlibcRand::discard (uint64_t k)
+{
+	uint32_t W[31], E[61], W2[31];
+	window (W);
+	gr_extend (W, E);
+	gr_jump_window (E, k, W2);
+	for (int j = 0; j < 31; j++)
+		s[j] = (int32_t)W2[j];
+	f = 0;
+	r = 28;
 }
 
 static double dBToGain (double dB) { return pow (10.0, (dB / 20.0)); }
@@ -277,8 +296,15 @@ static size_t fitWave (double Hz, double precision, int minSamples, int maxSampl
 
 void TgTemplate::build (double rate, const double* mts128, const double* ratio9, unsigned int seed)
 {
+	GlibcRand rnd (seed);
+	prepare (rate, mts128, ratio9);
+	synthHost (rnd);
+	finish (rnd);
+}
+
+void TgTemplate::prepare (double rate, const double* mts128, const double* ratio9)
+{
 	static const double defaultRatio[9] = {0.5, 1.5, 1, 2, 3, 4, 5, 6, 8};
-	GlibcRand           rnd (seed);
 	sr     = rate;
 	envMin = std::min ((int)floor (sr * 8.0 / 22050.0), TBF_BLK);
 	envMax = std::min ((int)ceil (sr * 40.0 / 22050.0), TBF_BLK);
@@ -291,10 +317,7 @@ void TgTemplate::build (double rate, const double* mts128, const double* ratio9,
 
 	/* initOscillators (1470-1630): spline EQ (p1y=1,r1y=0,p4y=1,r4y=0), fitWave,
 	 * writeSamples with one rand() LSB per sample, wheels 1..256 in order */
-	const double fullCircle = 2.0 * M_PI;
-	size_t       total      = 0;
-	double       att[TBF_NW + 1], wf[TBF_NW + 1];
-	size_t       wl[TBF_NW + 1];
+	total = 0;
 	for (int i = 1; i <= TBF_NW; i++) {
 		double k   = TBF_NW - 1;
 		double tt  = ((double)(i - 1)) / k;
@@ -302,44 +325,52 @@ void TgTemplate::build (double rate, const double* mts128, const double* ratio9,
 		double tCb = tSq * tt;
 		double r   = 1.0 * (2.0 * tCb - 3.0 * tSq + 1.0) + 1.0 * (-2.0 * tCb + 3.0 * tSq) + 0.0 * (tCb - 2.0 * tSq + tt) +
 		           0.0 * (tCb - tSq);
-		att[i] = (r < 0.0) ? 0.0 : (1.0 < r) ? 1.0 : r;
-		wf[i]  = fmin (fmax (frequency[i - 1], 12.0), 2.5e10);
-		wl[i]  = fitWave (wf[i], 0.001, 3 * TBF_BLK, (int)(ceil (sr / 48000.0) * 4096), sr);
-		total += wl[i];
-	}
-	bank.assign (total, 0.f);
-	size_t o = 0;
-	for (int i = 1; i <= TBF_NW; i++) {
-		off[i]        = (uint32_t)o;
-		len[i]        = (uint32_t)wl[i];
+		const double att = (r < 0.0) ? 0.0 : (1.0 < r) ? 1.0 : r;
+		const double wf  = fmin (fmax (frequency[i - 1], 12.0), 2.5e10);
+		const size_t wl  = fitWave (wf, 0.001, 3 * TBF_BLK, (int)(ceil (sr / 48000.0) * 4096), sr);
+		off[i]           = (uint32_t)total;
+		len[i]           = (uint32_t)wl;
+		total += wl;
 		double apl[12], plHz[12], aplSum = 0.0;
 		for (int j = 0; j < 12; j++) {
 			apl[j] = j == 0 ? 1.0 : 0.0;
 			aplSum += fabs (apl[j]);
-			plHz[j] = wf[i] * ((double)(j + 1));
+			plHz[j] = wf * ((double)(j + 1));
 			if ((sr * 0.5) <= plHz[j])
 				apl[j] = 0.0;
 		}
-		const double U = att[i] / aplSum;
-		float*       y = bank.data () + o;
+		U[i] = att / aplSum;
 		/* a partial of amplitude 0 adds 0 * sin (finite) = +-0 to the sum, which leaves
-		 * it unchanged, so only the nonzero partials are evaluated (the default
-		 * spectrum has one) */
-		int nz[12], nnz = 0;
+		 * it unchanged, so only the nonzero partials are kept (the default spectrum
+		 * has one) */
+		nPartials[i] = 0;
 		for (int j = 0; j < 12; j++)
-			if (apl[j] != 0.0)
-				nz[nnz++] = j;
-		for (size_t n = 0; n < wl[i]; n++) {
-			double s = 0.0;
-			for (int q = 0; q < nnz; q++) {
-				const int j = nz[q];
-				s += apl[j] * sin (remainder ((plHz[j] * fullCircle * (double)n) / sr, fullCircle));
+			if (apl[j] != 0.0) {
+				pAmp[i][nPartials[i]] = apl[j];
+				pHz[i][nPartials[i]]  = plHz[j];
+				nPartials[i]++;
 			}
-			float v = (rnd.next () < (2147483647 >> 1)) ? (float)(1.0 / 32767.0) : 0.0f;
-			y[n]    = (float)((double)v + (U * s));
-		}
-		o += wl[i];
 	}
+}
+
+void TgTemplate::synthHost (GlibcRand& rnd)
+{
+	const double fullCircle = 2.0 * M_PI;
+	bank.assign (total, 0.f);
+	for (int i = 1; i <= TBF_NW; i++) {
+		float* y = bank.data () + off[i];
+		for (size_t n = 0; n < len[i]; n++) {
+			double s = 0.0;
+			for (int q = 0; q < nPartials[i]; q++)
+				s += pAmp[i][q] * sin (remainder ((pHz[i][q] * fullCircle * (double)n) / sr, fullCircle));
+			float v = (rnd.next () < (2147483647 >> 1)) ? (float)(1.0 / 32767.0) : 0.0f;
+			y[n]    = (float)((double)v + (U[i] * s));
+		}
+	}
+}
+
+void TgTemplate::finish (GlibcRand& rnd)
+{
 	/* initKeyCompTable (1939-1966) */
 	{
 		float u = -5.0f, v = -9.0f, m = (float)(1.0 / (128 - 12));

@@ -35,6 +35,7 @@ SIGNATURES = {
     "tbf_engine_create": (C.c_int, [C.POINTER(_Config), C.POINTER(C.c_void_p)]),
     "tbf_engine_destroy": (C.c_int, [C.c_void_p]),
     "tbf_template_create": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, _u32p]),
+    "tbf_templates_create": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, _u32p, _u32p]),
     "tbf_instances_add": (C.c_int, [C.c_void_p, C.c_uint32, _u32p, _u32p, _u32p]),
     "tbf_instance_count": (C.c_uint32, [C.c_void_p]),
     "tbf_note": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int32, C.c_int32]),
@@ -110,6 +111,19 @@ class Engine:
         _check(self._lib.tbf_template_create(self._h, None if m is None else m.ctypes.data,
                                              None if r is None else r.ctypes.data, int(seed), C.byref(out)))
         return out.value
+
+    def templates(self, seeds, mts128=None, ratio9=None):
+        """n templates built on the device (tbf_templates_create): mts128 (n, 128) or
+        None, ratio9 (n, 9) or None; returns the template ids."""
+        sd = np.ascontiguousarray(seeds, dtype=np.uint32).reshape(-1)
+        n = len(sd)
+        m = None if mts128 is None else np.ascontiguousarray(mts128, dtype=np.float64).reshape(n, 128)
+        r = None if ratio9 is None else np.ascontiguousarray(ratio9, dtype=np.float64).reshape(n, 9)
+        ids = np.zeros(n, np.uint32)
+        _check(self._lib.tbf_templates_create(self._h, n, None if m is None else m.ctypes.data,
+                                              None if r is None else r.ctypes.data,
+                                              sd.ctypes.data_as(_u32p), ids.ctypes.data_as(_u32p)))
+        return [int(x) for x in ids]
 
     def template_bank(self, tpl):
         lens = np.zeros(256, np.uint32)

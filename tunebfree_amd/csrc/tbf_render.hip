@@ -83,14 +83,15 @@ template <int W>
 struct WhLds {
 	tbf_wh_state st;
 	float        wring[4][W];
-	double       ang[2][TBF_SUB];
 	float        xx[TBF_SUB + 1];
 	float        xf[TBF_SUB + 4];
 	float        x1[TBF_SUB + 4];
 	float        x2[TBF_SUB + 4];
 	float        xd1[TBF_SUB + 1];
 	float        rd[2][TBF_SUB]; /* drum ring outputs -> drum shelf outputs (in place) */
-	float        tmp[4][TBF_SUB + 2]; /* DF2 state sequences temp[n-2 .. 63]: horn A, horn B, drum L, drum R */
+	/* DF2 state sequences temp[n-2 .. 63]: horn A, horn B, drum L, drum R; after the
+	 * filter outputs, the serial rotor-angle fallback's scratch (2 x 64 doubles) */
+	alignas (8) float tmp[4][TBF_SUB + 2];
 	float        xn[TBF_SUB];         /* input of the next sub-block (horn A runs one sub-block ahead) */
 	float        aOut[TBF_SUB];       /* horn A output of the current sub-block */
 	int          brake;
@@ -1382,18 +1383,20 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 		}
 		/* rotor angles, angle = fmod (angle + incr, 1) per sample (src/whirl.cpp:1428-1429):
 		 * inside one binade of the angle every sum lands on the same grid, so the run is
-		 * a0 + n D exactly (phase_run); otherwise lanes 1, 2 replay the recurrence */
+		 * a0 + n D exactly (phase_run); otherwise lanes 1, 2 replay the recurrence into
+		 * the (consumed) filter scratch */
+		double ha, da;
 		{
-			double Dh, Dd;
-			const bool okh = phase_run (st.hornAngle, hornIncr, TBF_SUB, Dh);
-			const bool okd = phase_run (st.drumAngle, drumIncr, TBF_SUB, Dd);
-			if (okh)
-				sm.ang[0][n] = st.hornAngle + (double)n * Dh;
-			if (okd)
-				sm.ang[1][n] = st.drumAngle + (double)n * Dd;
+			double*      angBuf = (double*)&sm.tmp[0][0];
+			double       Dh, Dd;
+			const double h0 = st.hornAngle, d0 = st.drumAngle;
+			const bool   okh = phase_run (h0, hornIncr, TBF_SUB, Dh);
+			const bool   okd = phase_run (d0, drumIncr, TBF_SUB, Dd);
+			__syncthreads (); /* every lane has read the filter scratch and the start angles */
 			if ((lane == 1 && !okh) || (lane == 2 && !okd)) {
-				double       a   = lane == 1 ? st.hornAngle : st.drumAngle;
+				double       a   = lane == 1 ? h0 : d0;
 				const double inc = lane == 1 ? hornIncr : drumIncr;
+				double*      row = angBuf + (lane - 1) * TBF_SUB;
 				for (int i0 = 0; i0 < TBF_SUB; i0 += 8) {
 					double av[8];
 #pragma unroll
@@ -1403,14 +1406,16 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 					}
 #pragma unroll
 					for (int k = 0; k < 8; k++)
-						sm.ang[lane - 1][i0 + k] = av[k];
+						row[i0 + k] = av[k];
 				}
 			}
-			__syncthreads (); /* every lane has read the start angles */
+			__syncthreads ();
+			ha = okh ? h0 + (double)n * Dh : angBuf[n];
+			da = okd ? d0 + (double)n * Dd : angBuf[TBF_SUB + n];
 			if (lane == 1)
-				st.hornAngle = okh ? st.hornAngle + (double)TBF_SUB * Dh : wrap1 (sm.ang[0][TBF_SUB - 1] + hornIncr);
+				st.hornAngle = okh ? h0 + (double)TBF_SUB * Dh : wrap1 (angBuf[TBF_SUB - 1] + hornIncr);
 			if (lane == 2)
-				st.drumAngle = okd ? st.drumAngle + (double)TBF_SUB * Dd : wrap1 (sm.ang[1][TBF_SUB - 1] + drumIncr);
+				st.drumAngle = okd ? d0 + (double)TBF_SUB * Dd : wrap1 (angBuf[2 * TBF_SUB - 1] + drumIncr);
 		}
 		__syncthreads ();
 		TBF_MARK (21);
@@ -1433,8 +1438,6 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 		TBF_MARK (22);
 
 		/* ---- per ring (HL, HR, DL, DR): its three motions, then the ordered adds ---- */
-		const double ha = sm.ang[0][n];
-		const double da = sm.ang[1][n];
 #pragma unroll 1
 		for (int r = 0; r < 4; r++) {
 			int   mu[3];

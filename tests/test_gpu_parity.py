@@ -311,3 +311,31 @@ def test_gpu_device_templates_match_host(sr):
             assert np.array_equal(x.view(np.uint32), y.view(np.uint32))
     print(f"device templates @{sr:.0f}: {len(mts)} in {t_dev * 1e3:.1f} ms; host {t_host * 1e3:.1f} ms")
     eng.close()
+
+
+def test_gpu_pipelined_chunks_across_calls(oracle):
+    """Cross-chunk pipelining (stage k of a chunk on its own stream, overlapping later
+    stages of earlier chunks and of the previous render call): back-to-back
+    tbf_render_device calls of 70 blocks (a 64-block chunk plus a 6-block chunk, so
+    both buffer parities alternate irregularly) on a torch stream with no host sync,
+    then a synchronous render; bit-identical to the oracle."""
+    import torch
+    eng, tpl, seeds, scens = _setup(oracle, 6, S.bench_scenario)
+    L0, R0 = engine_run(eng, scens, 1)  # block 0 carries the control uploads
+    nb, calls = 70, 4
+    L = torch.zeros((6, nb * calls * 128), dtype=torch.float32, device="cuda")
+    R = torch.zeros_like(L)
+    st = torch.cuda.Stream()
+    stride = nb * calls * 128
+    for c in range(calls):
+        eng.render_device(nb, L[:, c * nb * 128:].data_ptr(), R[:, c * nb * 128:].data_ptr(), stride, st.cuda_stream)
+    st.synchronize()
+    L2, R2 = eng.render(3)
+    gL = np.concatenate([L0, L.cpu().numpy(), L2], axis=1)
+    gR = np.concatenate([R0, R.cpu().numpy(), R2], axis=1)
+    total = 1 + nb * calls + 3
+    oL, oR, *_ = oracle_run(oracle, tpl, seeds, scens, total)
+    eL, xL = compare(gL, oL)
+    eR, xR = compare(gR, oR)
+    print(f"pipelined: {total} blocks, max|err| L={eL:.3g} R={eR:.3g} bit-exact L={xL:.6f} R={xR:.6f}")
+    assert max(eL, eR) <= TOL

@@ -6,6 +6,7 @@
  */
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -193,6 +194,13 @@ int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
 	if (cfg->device >= 0) {
 		HIPCHK (hipSetDevice (cfg->device));
 		HIPCHK (hipStreamCreateWithFlags (&e->stream, hipStreamNonBlocking));
+		for (int p = 0; p < 2; p++)
+			HIPCHK (hipStreamCreateWithFlags (&e->sstr[p], hipStreamNonBlocking));
+		for (int k = 0; k < TBF_NSTAGES; k++)
+			HIPCHK (hipEventCreateWithFlags (&e->sdone[k], hipEventDisableTiming));
+		HIPCHK (hipEventCreateWithFlags (&e->sjoin, hipEventDisableTiming));
+		const char* pl = getenv ("TBF_PIPELINE");
+		e->pipeline    = !(pl && pl[0] == '0');
 	}
 	e->wt.build (cfg->sample_rate);
 	/* compact whirl ring: live window < maxAhead + 2 + one sub-block */
@@ -222,6 +230,9 @@ int tbf_engine_destroy (tbf_engine* e)
 		(void)hipSetDevice (e->cfg.device);
 	if (e->stream)
 		(void)hipStreamSynchronize (e->stream);
+	for (int p = 0; p < 2; p++)
+		if (e->sstr[p])
+			(void)hipStreamSynchronize (e->sstr[p]);
 	e->bank.release ();
 	e->tplDesc.release ();
 	e->cst.release ();
@@ -243,6 +254,14 @@ int tbf_engine_destroy (tbf_engine* e)
 	e->rvB.release ();
 	if (e->stream)
 		(void)hipStreamDestroy (e->stream);
+	for (int p = 0; p < 2; p++)
+		if (e->sstr[p])
+			(void)hipStreamDestroy (e->sstr[p]);
+	for (int k = 0; k < TBF_NSTAGES; k++)
+		if (e->sdone[k])
+			(void)hipEventDestroy (e->sdone[k]);
+	if (e->sjoin)
+		(void)hipEventDestroy (e->sjoin);
 	delete e;
 	return 0;
 }
@@ -493,6 +512,30 @@ int tbf_set_param (tbf_engine* e, uint32_t i, int32_t index, double v)
 } /* extern "C" */
 
 /* ------------------------------------------------------------------ device setup */
+/* wait for all pipelined stage work (before the host touches device buffers) */
+static int drainStages (tbf_engine* e)
+{
+	if (!e->stagesBusy)
+		return 0;
+	for (int p = 0; p < 2; p++)
+		HIPCHK (hipStreamSynchronize (e->sstr[p]));
+	e->stagesBusy = false;
+	return 0;
+}
+
+/* make stream s wait for every pipelined stage launch so far */
+static int joinStages (tbf_engine* e, hipStream_t s)
+{
+	if (!e->stagesBusy)
+		return 0;
+	for (int p = 0; p < 2; p++) {
+		HIPCHK (hipEventRecord (e->sjoin, e->sstr[p]));
+		HIPCHK (hipStreamWaitEvent (s, e->sjoin, 0));
+	}
+	e->stagesBusy = false;
+	return 0;
+}
+
 static int ensureDevice (tbf_engine* e)
 {
 	if (e->deviceReady)
@@ -501,6 +544,8 @@ static int ensureDevice (tbf_engine* e)
 		return fail (-19, "host-only engine (device -1) cannot render");
 	HIPCHK (hipSetDevice (e->cfg.device));
 	HIPCHK (hipStreamSynchronize (e->stream));
+	if (int rc = drainStages (e))
+		return rc;
 	const uint32_t n = (uint32_t)e->inst.size ();
 	/* wave banks + template descriptors */
 	size_t total = 0;
@@ -680,18 +725,24 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 	P.slabLen   = e->slabLen;
 	P.errFlags  = e->err.p;
 	P.prof      = e->profOn ? e->prof.p : nullptr;
+	/* inter-stage buffers: two parities (alternate chunks), see the pipelining below */
+	const size_t need = (size_t)n * TBF_CHUNK * TBF_BLK;
 	if (e->cfg.chain_mode != TBF_CHAIN_TONEGEN) {
-		const size_t need = (size_t)n * TBF_CHUNK * TBF_BLK;
-		if (e->mid1.ensure (need) || e->mid2.ensure (need))
+		if (e->mid1.ensure (2 * need) || e->mid2.ensure (2 * need))
 			return fail (-12, "out of device memory (stage buffers)");
-		if (e->cfg.chain_mode != TBF_CHAIN_TAP_PREAMP && (e->rvA.ensure (2 * need) || e->rvB.ensure (2 * need)))
+		if (e->cfg.chain_mode != TBF_CHAIN_TAP_PREAMP && (e->rvA.ensure (4 * need) || e->rvB.ensure (4 * need)))
 			return fail (-12, "out of device memory (reverb stage buffers)");
 	}
-	P.rvA       = e->rvA.p;
-	P.rvB       = e->rvB.p;
-	P.mid1      = e->mid1.p;
-	P.mid2      = e->mid2.p;
 	P.midStride = (uint64_t)TBF_CHUNK * TBF_BLK;
+	/* Cross-chunk pipelining.  Every stage is causal and keeps its own state, so stage k
+	 * of chunk c depends only on stage k-1 of chunk c (same stream sstr[c % 2]) and on
+	 * stage k of chunk c-1 (event sdone[k], the other stream); its output buffer parity
+	 * c % 2 was last read by chunk c-2 on the same stream.  The kernels of neighbouring
+	 * chunks (and of consecutive render calls) then fill each other's tails on the GPU.
+	 * Used for the full chain on chunks without control uploads; uploads, tap modes and
+	 * the timing/profiling hooks run on the caller's stream after joining. */
+	const bool   pipe  = e->pipeline && e->cfg.chain_mode == TBF_CHAIN_FULL && !e->timeOn && !e->profOn;
+	bool         outWait = false; /* the output stage has waited for the caller's stream */
 	const size_t dprogCap = DPROG_CAP (n);
 	e->chg.assign (n, 0);
 	uint32_t b0 = 0, evi = 0;
@@ -733,6 +784,14 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 				e->hIdx[(size_t)len * n + i] = cur[i];
 			}
 		}
+		const bool     par     = (e->chunkSeq++ & 1) != 0;
+		const bool     piped   = pipe && !delta && !e->persistStale;
+		P.mid1 = e->mid1.p ? e->mid1.p + (par ? need : 0) : nullptr;
+		P.mid2 = e->mid2.p ? e->mid2.p + (par ? need : 0) : nullptr;
+		P.rvA  = e->rvA.p ? e->rvA.p + (par ? 2 * need : 0) : nullptr;
+		P.rvB  = e->rvB.p ? e->rvB.p + (par ? 2 * need : 0) : nullptr;
+		if (!piped && (rc = joinStages (e, s)))
+			return rc;
 		if (e->persistStale) {
 			HIPCHK (hipMemcpyAsync (e->ctl.p, e->hCtl.data (), n * sizeof (tbf_seg_ctl), hipMemcpyHostToDevice, s));
 			HIPCHK (hipMemcpyAsync (e->prog.p, e->hProg.data (), (size_t)n * PROG_CAP * sizeof (tbf_prog_entry),
@@ -752,6 +811,31 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		P.nBlocks   = len;
 		P.outOffset = (uint64_t)b0 * TBF_BLK;
 		const int nst = tbf_chain_stages (P.chain);
+		if (piped) {
+			hipStream_t sp = e->sstr[par];
+			if (!e->stagesBusy) {
+				/* from the caller's stream (uploads, earlier serialized chunks) */
+				HIPCHK (hipEventRecord (e->sjoin, s));
+				HIPCHK (hipStreamWaitEvent (sp, e->sjoin, 0));
+				outWait = true;
+			}
+			e->stagesBusy = true;
+			for (int k = 0; k < nst; k++) {
+				if (k == nst - 1 && !outWait) {
+					/* the output stage writes the caller's buffers: after the caller's work */
+					HIPCHK (hipEventRecord (e->sjoin, s));
+					HIPCHK (hipStreamWaitEvent (sp, e->sjoin, 0));
+					outWait = true;
+				}
+				HIPCHK (hipStreamWaitEvent (sp, e->sdone[k], 0)); /* stage k of the previous chunk */
+				rc = tbf_launch_stage (&P, k, sp);
+				if (rc)
+					return fail (rc, std::string ("kernel launch failed: ") + hipGetErrorString (hipGetLastError ()));
+				HIPCHK (hipEventRecord (e->sdone[k], sp));
+			}
+			b0 += len;
+			continue;
+		}
 		for (int k = 0; k < nst; k++) {
 			hipEvent_t e0 = nullptr, e1 = nullptr;
 			if (e->timeOn) {
@@ -790,6 +874,11 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		rc = applyEvent (e, ev[evi]);
 		if (rc)
 			return rc;
+	}
+	if (e->stagesBusy) {
+		/* the caller's stream waits for the last chunk's output stage (which follows
+		 * every earlier stage launch); later chunks keep overlapping from the streams */
+		HIPCHK (hipStreamWaitEvent (s, e->sdone[tbf_chain_stages (P.chain) - 1], 0));
 	}
 	return 0;
 }
@@ -876,7 +965,7 @@ int tbf_synchronize (tbf_engine* e)
 		return 0;
 	HIPCHK (hipSetDevice (e->cfg.device));
 	HIPCHK (hipStreamSynchronize (e->stream));
-	return 0;
+	return drainStages (e);
 }
 
 int tbf_error_flags (tbf_engine* e, uint32_t* flags)
@@ -886,6 +975,8 @@ int tbf_error_flags (tbf_engine* e, uint32_t* flags)
 	*flags = 0;
 	if (!e->err.p)
 		return 0;
+	if (int rc = drainStages (e))
+		return rc;
 	HIPCHK (hipMemcpy (flags, e->err.p, 4, hipMemcpyDeviceToHost));
 	return 0;
 }

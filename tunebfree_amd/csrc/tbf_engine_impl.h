@@ -136,6 +136,18 @@ struct tbf_engine {
 	std::vector<uint8_t>                    chg;
 	DevBuf<uint32_t>                        ctlIdx;
 	bool                                    persistStale = true; /* device pool entries 0..n-1 need upload */
+	/* cross-chunk pipelining (renderImpl): the stages of chunk c run in order on stream
+	 * sstr[c % 2]; stage k of chunk c waits for stage k of chunk c-1 (event sdone[k])
+	 * on the other stream, so the two streams overlap neighbouring chunks' kernels (and
+	 * consecutive render calls'); inter-stage buffers alternate with the same parity, so
+	 * their reuse is ordered by the stream itself.  Two streams, not one per stage: the
+	 * device exposes few hardware queues per process and streams sharing one serialize */
+	hipStream_t                             sstr[2] = {};
+	hipEvent_t                              sdone[5] = {};
+	hipEvent_t                              sjoin = nullptr;
+	uint64_t                                chunkSeq = 0;
+	bool                                    stagesBusy = false; /* pipelined work may be outstanding */
+	bool                                    pipeline = true;    /* TBF_PIPELINE=0 disables */
 	/* programme table (.pgm), src/program.h:26 MAXPROGS; pgm.controller.offset */
 	std::vector<Programme>                  progs = std::vector<Programme> (129);
 	int                                     pgmOffset = 1;

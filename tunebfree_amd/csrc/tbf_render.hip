@@ -151,6 +151,16 @@ __device__ __forceinline__ void copy_words (T* dst, const T* src)
 		d[i] = s[i];
 }
 
+/* the reverb state's shared head (predelay, dither streams, biquad states) without the
+ * feedback-network channels, which k_rv_core owns */
+__device__ __forceinline__ void copy_head (tbf_rv_state* dst, const tbf_rv_state* src)
+{
+	const uint32_t* s = (const uint32_t*)src;
+	uint32_t*       d = (uint32_t*)dst;
+	for (uint32_t i = threadIdx.x; i < offsetof (tbf_rv_state, ch) / 4; i += NL)
+		d[i] = s[i];
+}
+
 __device__ __forceinline__ uint32_t xorshift (uint32_t s)
 {
 	s ^= s << 13;
@@ -678,7 +688,7 @@ k_rv_in (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 	double*               a0L  = rv_buf (P.rvA, P, inst, 0);
 	double*               a0R  = rv_buf (P.rvA, P, inst, 1);
 	prof_begin (P, sm);
-	copy_words (&sm.st, S);
+	copy_head (&sm.st, S);
 	__syncthreads ();
 	tbf_rv_state& st = sm.st;
 	for (uint32_t blk = 0; blk < P.nBlocks; blk++) {
@@ -718,7 +728,14 @@ k_rv_in (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 		}
 	}
 	__syncthreads ();
-	copy_words (S, &sm.st);
+	if (lane == 0) { /* only k_rv_in's own fields: the other reverb kernels of neighbouring
+	                  * chunks may run concurrently (cross-chunk pipelining) */
+		S->countM = sm.st.countM;
+		S->fpdL   = sm.st.fpdL;
+		S->fpdR   = sm.st.fpdR;
+		for (int j = 0; j < 4; j++)
+			S->bq[0][j] = sm.st.bq[0][j];
+	}
 	prof_end (P, sm, inst);
 }
 
@@ -991,7 +1008,7 @@ k_rv_out (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 	const double*         bR  = rv_buf (P.rvB, P, inst, 1);
 	const bool            tap = P.chain == TBF_CHAIN_TAP_REVERB;
 	prof_begin (P, sm);
-	copy_words (&sm.st, S);
+	copy_head (&sm.st, S);
 	__syncthreads ();
 	tbf_rv_state& st = sm.st;
 	/* serial lane roles: q = 0 biquadB, 1 biquadC; c = channel */
@@ -1096,7 +1113,14 @@ k_rv_out (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 		__syncthreads ();
 		TBF_MARK (13);
 	}
-	copy_words (S, &sm.st);
+	if (lane == 0) { /* only k_rv_out's own fields (see k_rv_in) */
+		S->fpdL2 = sm.st.fpdL2;
+		S->fpdR2 = sm.st.fpdR2;
+		for (int j = 0; j < 4; j++) {
+			S->bq[1][j] = sm.st.bq[1][j];
+			S->bq[2][j] = sm.st.bq[2][j];
+		}
+	}
 	prof_end (P, sm, inst);
 }
 

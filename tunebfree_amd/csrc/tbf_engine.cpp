@@ -740,8 +740,10 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 	 * c % 2 was last read by chunk c-2 on the same stream.  The kernels of neighbouring
 	 * chunks (and of consecutive render calls) then fill each other's tails on the GPU.
 	 * Used for the full chain on chunks without control uploads; uploads, tap modes and
-	 * the timing/profiling hooks run on the caller's stream after joining. */
-	const bool   pipe  = e->pipeline && e->cfg.chain_mode == TBF_CHAIN_FULL && !e->timeOn && !e->profOn;
+	 * the profiling hook run on the caller's stream after joining.  With
+	 * tbf_debug_kernel_times on, each launch is bracketed by events on its own stream
+	 * (durations then include the overlap with the other stream's kernels). */
+	const bool   pipe  = e->pipeline && e->cfg.chain_mode == TBF_CHAIN_FULL && !e->profOn && !e->timeSerial;
 	bool         outWait = false; /* the output stage has waited for the caller's stream */
 	const size_t dprogCap = DPROG_CAP (n);
 	e->chg.assign (n, 0);
@@ -828,9 +830,19 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 					outWait = true;
 				}
 				HIPCHK (hipStreamWaitEvent (sp, e->sdone[k], 0)); /* stage k of the previous chunk */
+				hipEvent_t e0 = nullptr, e1 = nullptr;
+				if (e->timeOn) { /* launch duration on the launch stream, dependencies met */
+					HIPCHK (hipEventCreate (&e0));
+					HIPCHK (hipEventCreate (&e1));
+					HIPCHK (hipEventRecord (e0, sp));
+				}
 				rc = tbf_launch_stage (&P, k, sp);
 				if (rc)
 					return fail (rc, std::string ("kernel launch failed: ") + hipGetErrorString (hipGetLastError ()));
+				if (e->timeOn) {
+					HIPCHK (hipEventRecord (e1, sp));
+					e->tev.push_back ({k, {e0, e1}});
+				}
 				HIPCHK (hipEventRecord (e->sdone[k], sp));
 			}
 			b0 += len;
@@ -1131,8 +1143,9 @@ int tbf_debug_kernel_times (tbf_engine* e, int32_t enable, double* ms3, uint32_t
 {
 	if (!e)
 		return fail (-22, "null engine");
-	if (enable == 1 || enable == -1) {
-		e->timeOn = enable == 1;
+	if (enable == 1 || enable == 2 || enable == -1) {
+		e->timeOn     = enable >= 1;
+		e->timeSerial = enable == 2;
 		return 0;
 	}
 	if (e->cfg.device >= 0)

@@ -123,6 +123,7 @@ struct tbf_engine {
 	bool                                    profOn = false;
 	/* tbf_debug_kernel_times: HIP events around every stage launch */
 	bool                                    timeOn = false;
+	bool                                    timeSerial = false; /* time with pipelining off */
 	std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> tev;
 	DevBuf<float>                           outL, outR;
 	DevBuf<float>                           mid1, mid2; /* inter-stage blocks of one launch chunk */

@@ -212,11 +212,12 @@ class Engine:
 
     def kernel_times(self, enable=None):
         """Per-stage HIP-event timing (tbf_debug_kernel_times): enable=True/False switches
-        recording; with no argument returns {stage: (ms_total, launches)} since the last call."""
+        recording ("serial": with cross-chunk pipelining off, each kernel alone); with no
+        argument returns {stage: (ms_total, launches)} since the last call."""
         fn = self._lib.tbf_debug_kernel_times
         fn.restype, fn.argtypes = C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
         if enable is not None:
-            _check(fn(self._h, 1 if enable else -1, None, None))
+            _check(fn(self._h, -1 if not enable else (2 if enable == "serial" else 1), None, None))
             return None
         ms = np.zeros(len(STAGES), np.float64)
         cnt = np.zeros(len(STAGES), np.uint32)

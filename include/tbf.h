@@ -84,8 +84,9 @@ int tbf_engine_destroy (tbf_engine* e);
 int tbf_template_create (tbf_engine* e, const double* mts128, const double* ratio9, uint32_t seed,
                          uint32_t* tpl_id);
 
-/* n templates built on the device: the same tables as n
- * tbf_template_create calls, with the wave bank's sines and its per-sample rand() draws
+/* n templates built on the device (replaces n initToneGenerator
+ * table builds, src/tonegen.cpp:1470-1630 initOscillators + 2562-2728 initEnvelopes):
+ * the same tables as n tbf_template_create calls, with the wave bank's sines and its per-sample rand() draws
  * (each thread jumping the glibc stream to its chunk) computed on the engine's GPU.
  * mts128: n x 128 frequencies or NULL; ratio9: n x 9 or NULL; seeds[n]; ids[n] out.
  * Needs a device engine (-19 on a host-only engine). */

@@ -211,7 +211,7 @@ def main():
     # parity on the last step (first --check instances of this rank)
     gL = outL[: a.check].cpu().numpy()
     gR = outR[: a.check].cpu().numpy()
-    total_blocks = (a.warmup + a.steps + ksteps) * a.blocks
+    total_blocks = (a.warmup + a.steps + ksteps * (2 if a.isolated else 1)) * a.blocks
     max_err, exact = oracle_check(first_global, a.check, total_blocks, a.blocks, gL, gR, a.sr) if a.check else (None, None)
     if dist:
         e = torch.tensor([max_err or 0.0], dtype=torch.float64, device="cuda")

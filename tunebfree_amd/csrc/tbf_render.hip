@@ -45,6 +45,9 @@
 #ifndef WH_WAVES
 #define WH_WAVES 3
 #endif
+#ifndef TG_UNROLL
+#define TG_UNROLL 4 /* program entries of the tonegen interpreter in flight */
+#endif
 
 /* ------------------------------------------------------------------ LDS layouts */
 struct TgLds {
@@ -217,6 +220,20 @@ __device__ __forceinline__ int wave_max (int v)
 	return v;
 }
 
+/* Whole-wave lane shifts by DPP (wave_shr:1 / wave_shl:1, GFX9 DPP controls 0x138 /
+ * 0x130): lane i receives lane i-1 (shr) or i+1 (shl); the lane with no source keeps
+ * its own value (callers mask it).  VALU-only, unlike __shfl_up/down (ds_bpermute). */
+__device__ __forceinline__ int lane_shr1 (int v) { return __builtin_amdgcn_update_dpp (v, v, 0x138, 0xF, 0xF, false); }
+__device__ __forceinline__ int lane_shl1 (int v) { return __builtin_amdgcn_update_dpp (v, v, 0x130, 0xF, 0xF, false); }
+__device__ __forceinline__ float lane_shr1 (float v) { return __int_as_float (lane_shr1 (__float_as_int (v))); }
+__device__ __forceinline__ float lane_shl1 (float v) { return __int_as_float (lane_shl1 (__float_as_int (v))); }
+__device__ __forceinline__ double lane_shr1 (double v)
+{
+	const unsigned long long u = __double_as_longlong (v);
+	const unsigned long long lo = (unsigned)lane_shr1 ((int)(unsigned)u), hi = (unsigned)lane_shr1 ((int)(unsigned)(u >> 32));
+	return __longlong_as_double ((long long)((hi << 32) | lo));
+}
+
 /* Airwindows 32-bit dither term, src/overdrive.cpp:153-159 / src/reverb.cpp:775-783.
  * The reference multiplies by a long double literal; FP64 here (the
  * difference reaches the float output with probability ~1e-17 per sample). */
@@ -276,7 +293,7 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 	__syncthreads ();
 	/* main loop in program order (the adds keep the reference's order); unrolled so
 	 * several entries' wave loads are in flight together */
-#pragma unroll 4
+#pragma unroll TG_UNROLL
 	for (int e = 0; e < np; e++) {
 		const tbf_prog_entry E    = prog[e];
 		const uint32_t       base = sm.u.ent.base[e];
@@ -971,7 +988,7 @@ k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 		double    fbn      = fbv;
 #pragma unroll
 		for (int l = 0; l < 8; l++) {
-			const double up = __shfl_up (fb[l], 1), carry = rld (fbv, l);
+			const double up = lane_shr1 (fb[l]), carry = rld (fbv, l);
 			const double prev = lane == 0 ? carry : up;
 			slab[rl (roffv, l) + wrap_slot (rl (cntv, l) + n, rl (dlyv, l))] = ap[srcAp[l]] + prev;
 			const double last = rld (fb[l], NL - 1);
@@ -1228,40 +1245,93 @@ __device__ void whirl_speed (tbf_wh_state& st, const tbf_inst_const& K, int revO
  * Groups have at most 2 samples (checked by the caller), so the first lane of each
  * group owns slot t = U (and slot t + 1 when no group sits at t + 1) and finds its
  * neighbours' terms with lane shifts; owners never share a slot. */
+/* the owner lanes' slots and ordered sums of one motion (see motion_add) */
+struct MotionOwn {
+	bool     first, own2, pair, lead, lead2;
+	uint32_t t;
+	float    a, an, b, bn, bp1, bp2;
+};
+
+__device__ __forceinline__ MotionOwn motion_own (int U, float a, float b, int lane)
+{
+	MotionOwn m;
+	const int Up  = lane_shr1 (U);
+	const int Up2 = lane_shr1 (Up);
+	const int Un  = lane_shl1 (U);
+	const int Un2 = lane_shl1 (Un);
+	m.bp1         = lane_shr1 (b);
+	m.bp2         = lane_shr1 (m.bp1);
+	m.an          = lane_shl1 (a);
+	m.bn          = lane_shl1 (b);
+	m.a           = a;
+	m.b           = b;
+	m.t           = (uint32_t)U;
+	m.first       = lane == 0 || U != Up;
+	m.pair        = lane < NL - 1 && Un == U;
+	m.lead        = lane > 0 && Up == U - 1;
+	m.lead2       = lane > 1 && Up2 == Up;
+	const bool nextExists = m.pair ? lane < NL - 2 : lane < NL - 1;
+	const int  Unx        = m.pair ? Un2 : Un;
+	m.own2                = !nextExists || Unx != U + 1;
+	return m;
+}
+
+/* slot t: b of the group at t-1 (<= 2 samples, in order), then a of the group at t */
+__device__ __forceinline__ float motion_sum_t (const MotionOwn& m, float v)
+{
+	if (m.lead) {
+		if (m.lead2)
+			v += m.bp2;
+		v += m.bp1;
+	}
+	v += m.a;
+	if (m.pair)
+		v += m.an;
+	return v;
+}
+
+/* slot t + 1 when no group sits there: b of this group */
+__device__ __forceinline__ float motion_sum_t1 (const MotionOwn& m, float w)
+{
+	w += m.b;
+	if (m.pair)
+		w += m.bn;
+	return w;
+}
+
 template <int W>
 __device__ __forceinline__ void motion_add (float* ring, int U, float a, float b, int lane)
 {
-	const uint32_t WM  = (uint32_t)W - 1u;
-	const int      Up  = __shfl_up (U, 1);
-	const int      Up2 = __shfl_up (U, 2);
-	const int      Un  = __shfl_down (U, 1);
-	const int      Un2 = __shfl_down (U, 2);
-	const float    bp1 = __shfl_up (b, 1);
-	const float    bp2 = __shfl_up (b, 2);
-	const float    an  = __shfl_down (a, 1);
-	const float    bn  = __shfl_down (b, 1);
-	const bool     first = lane == 0 || U != Up;
-	if (first) {
-		const bool     pair = lane < NL - 1 && Un == U;
-		const uint32_t t    = (uint32_t)U;
-		float          v    = ring[t & WM];
-		if (lane > 0 && Up == U - 1) {
-			if (lane > 1 && Up2 == Up)
-				v += bp2;
-			v += bp1;
-		}
-		v += a;
-		if (pair)
-			v += an;
-		ring[t & WM] = v;
-		const bool nextExists = pair ? lane < NL - 2 : lane < NL - 1;
-		const int  Unx        = pair ? Un2 : Un;
-		if (!nextExists || Unx != U + 1) {
-			float w = ring[(t + 1) & WM];
-			w += b;
-			if (pair)
-				w += bn;
-			ring[(t + 1) & WM] = w;
+	const uint32_t  WM = (uint32_t)W - 1u;
+	const MotionOwn m  = motion_own (U, a, b, lane);
+	if (m.first) {
+		ring[m.t & WM] = motion_sum_t (m, ring[m.t & WM]);
+		if (m.own2)
+			ring[(m.t + 1) & WM] = motion_sum_t1 (m, ring[(m.t + 1) & WM]);
+	}
+}
+
+/* the three motions of a ring when their slot ranges [U_q(0), U_q(63) + 1] are disjoint:
+ * every slot takes terms of one motion only, so all reads go out together, then all
+ * writes (no slot is read after another motion's write) */
+template <int W>
+__device__ __forceinline__ void motion_add3 (float* ring, const int* U, const float* a, const float* b, int lane)
+{
+	const uint32_t WM = (uint32_t)W - 1u;
+	MotionOwn      m[3];
+	float          v[3], w[3];
+#pragma unroll
+	for (int q = 0; q < 3; q++) {
+		m[q] = motion_own (U[q], a[q], b[q], lane);
+		v[q] = m[q].first ? ring[m[q].t & WM] : 0.f;
+		w[q] = (m[q].first && m[q].own2) ? ring[(m[q].t + 1) & WM] : 0.f;
+	}
+#pragma unroll
+	for (int q = 0; q < 3; q++) {
+		if (m[q].first) {
+			ring[m[q].t & WM] = motion_sum_t (m[q], v[q]);
+			if (m[q].own2)
+				ring[(m[q].t + 1) & WM] = motion_sum_t1 (m[q], w[q]);
 		}
 	}
 }
@@ -1515,15 +1585,20 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 			int ok = (mu[1] >= mu[0] + 2) && (mu[2] >= mu[1] + 2);
 #pragma unroll
 			for (int q = 0; q < 3; q++) {
-				const int up = __shfl_up (mu[q], 1);
-				const int un = __shfl_down (mu[q], 1);
+				const int up = lane_shr1 (mu[q]);
+				const int un = lane_shl1 (mu[q]);
 				if (lane > 0 && mu[q] < up)
 					ok = 0;
 				if (lane > 0 && lane < NL - 1 && up == mu[q] && un == mu[q])
 					ok = 0;
 			}
 			float* ring = sm.wring[r];
-			if (__all (ok)) {
+			if (__all (ok) && __builtin_amdgcn_readlane (mu[0], NL - 1) + 1 < __builtin_amdgcn_readfirstlane (mu[1]) &&
+			    __builtin_amdgcn_readlane (mu[1], NL - 1) + 1 < __builtin_amdgcn_readfirstlane (mu[2])) {
+				/* non-decreasing slots, so lane 0 / lane 63 hold each motion's range ends */
+				motion_add3<W> (ring, mu, ma, mb, lane);
+				__syncthreads ();
+			} else if (__all (ok)) {
 				motion_add<W> (ring, mu[2], ma[2], mb[2], lane);
 				__syncthreads ();
 				motion_add<W> (ring, mu[1], ma[1], mb[1], lane);

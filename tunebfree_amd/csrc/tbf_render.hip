@@ -786,9 +786,13 @@ __device__ __forceinline__ double rld (double v, int l)
 
 __device__ __forceinline__ int wrap_slot (int s, int d) { return s - ((s > d) ? d + 1 : 0); }
 
-/* issue every global read of a sub-block whose ring counters are lane-held in cntv */
+/* issue every global read of a sub-block whose ring counters are lane-held in cntv.
+ * full: the whole tap windows, slots count+1 .. count+72 (wlo: +1..+64, whi: +65..+72);
+ * carry: only slots count+9 .. count+72 (into wlo), since slots +1..+8 are the previous
+ * sub-block's +65..+72, still in its window and not written since (the sub-block in
+ * between writes slots count-64 .. count-1) */
 __device__ __forceinline__ void rv_core_fetch (const double* slab, int cntv, int dlyv, int roffv,
-                                               const double* __restrict__ a0s, size_t o, RvFetch& f)
+                                               const double* __restrict__ a0s, size_t o, RvFetch& f, bool carry)
 {
 	const int lane = threadIdx.x;
 #pragma unroll
@@ -796,12 +800,13 @@ __device__ __forceinline__ void rv_core_fetch (const double* slab, int cntv, int
 		const int d    = rl (dlyv, l);
 		f.apOld[l - 8] = slab[rl (roffv, l) + wrap_slot (rl (cntv, l) + lane + 1, d)];
 	}
+	const int k0 = carry ? 9 : 1;
 #pragma unroll
 	for (int l = 0; l < 8; l++) {
 		const int d = rl (dlyv, l);
-		f.wlo[l]    = slab[rl (roffv, l) + wrap_slot (rl (cntv, l) + 1 + lane, d)];
+		f.wlo[l]    = slab[rl (roffv, l) + wrap_slot (rl (cntv, l) + k0 + lane, d)];
 	}
-	{
+	if (!carry) {
 		const int l = lane >> 3, j = lane & 7;
 		const int d = __shfl (dlyv, l), cl = __shfl (cntv, l), ro = __shfl (roffv, l);
 		f.whi       = slab[ro + wrap_slot (cl + 1 + NL + j, d)];
@@ -916,7 +921,7 @@ k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 	const uint32_t nSub = P.nBlocks * (TBF_BLK / TBF_SUB);
 	RvFetch        f;
 	if (nSub > 0)
-		rv_core_fetch (slab, cntv, dlyv, roffv, a0s, lane, f);
+		rv_core_fetch (slab, cntv, dlyv, roffv, a0s, lane, f, false);
 #pragma unroll 1
 	for (uint32_t s = 0; s < nSub; s++) {
 		const size_t o = (size_t)s * TBF_SUB + lane;
@@ -924,11 +929,20 @@ k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 		double         v0x, Sx, Cx, Dx;
 		const uint64_t okm = rv_core_lines (sm, vdl, v0x, Sx, Cx, Dx);
 		/* windows to LDS (the reads were issued one sub-block ago) */
+		if (s == 0) {
 #pragma unroll
-		for (int l = 0; l < 8; l++)
-			sm.win[l][lane] = f.wlo[l];
-		if (lane < 64)
+			for (int l = 0; l < 8; l++)
+				sm.win[l][lane] = f.wlo[l];
 			sm.win[lane >> 3][NL + (lane & 7)] = f.whi;
+		} else {
+			/* carried slots +1..+8 = the last sub-block's +65..+72, then the fetched +9..+72 */
+			const double tail = sm.win[lane >> 3][NL + (lane & 7)];
+			__syncthreads (); /* every lane has read its tail slot */
+			sm.win[lane >> 3][lane & 7] = tail;
+#pragma unroll
+			for (int l = 0; l < 8; l++)
+				sm.win[l][8 + lane] = f.wlo[l];
+		}
 		__syncthreads ();
 		/* two-tap interpolation and blend */
 		double I[8];
@@ -978,7 +992,7 @@ k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 		/* reads of the next sub-block, in flight before this one's writes */
 		const int ncv = wrap_slot (cntv + TBF_SUB, dlyv);
 		if (s + 1 < nSub)
-			rv_core_fetch (slab, ncv, dlyv, roffv, a0s, o + TBF_SUB, f);
+			rv_core_fetch (slab, ncv, dlyv, roffv, a0s, o + TBF_SUB, f, true);
 		bout[o] = mix;
 #pragma unroll
 		for (int l = 8; l < 12; l++)

@@ -708,41 +708,58 @@ k_rv_in (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 	copy_head (&sm.st, S);
 	__syncthreads ();
 	tbf_rv_state& st = sm.st;
-	for (uint32_t blk = 0; blk < P.nBlocks; blk++) {
-		const double wet = ctl_of (P, ctl, blk, inst).rvWet;
-		const float* in = P.mid1 + (size_t)inst * P.midStride + (size_t)blk * TBF_BLK;
+	/* software-pipelined: the predelay reads and the input of sub-block g+1 are issued
+	 * before sub-block g's writes and serial chain, so their latency overlaps it (the
+	 * reads lie at count+65 .. count+128, the writes at count .. count+63, and the ring
+	 * holds >= 561 slots) */
+	const float*   inBase = P.mid1 + (size_t)inst * P.midStride;
+	const uint32_t nSub   = P.nBlocks * (TBF_BLK / TBF_SUB);
+	double         pL = 0.0, pR = 0.0;
+	float          pIn = 0.f;
+	if (nSub > 0) {
+		const int cMr = cnt_adv (st.countM, dM, lane + 1);
+		pL            = mL[cMr];
+		pR            = mR[cMr];
+		pIn           = inBase[lane];
+	}
 #pragma unroll 1
-		for (int sb = 0; sb < TBF_BLK / TBF_SUB; sb++) {
-			const int n = lane;
-			rv_dither (P.xsJump, st.fpdL, st.fpdR, sm.fpd);
-			TBF_MARK (5);
-			const double inS = (double)in[sb * TBF_SUB + n];
-			/* predelay M (src/reverb.cpp:350-358): write at count, read at count + 1 */
-			const int cMn = cnt_adv (st.countM, dM, n);
-			const int cMr = cnt_adv (st.countM, dM, n + 1);
-			sm.a[0][n]    = mL[cMr];
-			sm.a[1][n]    = mR[cMr];
-			__syncthreads (); /* every read of the sub-block precedes its writes */
-#pragma unroll
-			for (int c = 0; c < 2; c++) {
-				double x = inS;
-				if (fabs (x) < 1.18e-23)
-					x = sm.fpd[c][n] * 1.18e-17;
-				(c ? mR : mL)[cMn] = x;
-			}
-			/* biquadA, both channels: lanes 0, 1 */
-			if (lane < 2)
-				rv_chain (K.bq[0], st.bq[0][2 * lane], st.bq[0][2 * lane + 1], sm.a[lane]);
-			__syncthreads ();
-			TBF_MARK (6);
-			const size_t o = (size_t)blk * TBF_BLK + sb * TBF_SUB + n;
-			a0L[o]         = sin (sm.a[0][n] * wet);
-			a0R[o]         = sin (sm.a[1][n] * wet);
-			if (lane == 0)
-				st.countM = cnt_adv (st.countM, dM, TBF_SUB);
-			__syncthreads ();
-			TBF_MARK (7);
+	for (uint32_t g = 0; g < nSub; g++) {
+		const uint32_t blk = g / (TBF_BLK / TBF_SUB), sb = g % (TBF_BLK / TBF_SUB);
+		const double   wet = ctl_of (P, ctl, blk, inst).rvWet;
+		const int      n   = lane;
+		rv_dither (P.xsJump, st.fpdL, st.fpdR, sm.fpd);
+		TBF_MARK (5);
+		const double inS = (double)pIn;
+		/* predelay M (src/reverb.cpp:350-358): write at count, read at count + 1 */
+		const int cMn = cnt_adv (st.countM, dM, n);
+		sm.a[0][n]    = pL;
+		sm.a[1][n]    = pR;
+		if (g + 1 < nSub) {
+			const int cMr = cnt_adv (st.countM, dM, TBF_SUB + n + 1);
+			pL            = mL[cMr];
+			pR            = mR[cMr];
+			pIn           = inBase[(size_t)(g + 1) * TBF_SUB + n];
 		}
+		__syncthreads (); /* every read of the sub-block precedes its writes */
+#pragma unroll
+		for (int c = 0; c < 2; c++) {
+			double x = inS;
+			if (fabs (x) < 1.18e-23)
+				x = sm.fpd[c][n] * 1.18e-17;
+			(c ? mR : mL)[cMn] = x;
+		}
+		/* biquadA, both channels: lanes 0, 1 */
+		if (lane < 2)
+			rv_chain (K.bq[0], st.bq[0][2 * lane], st.bq[0][2 * lane + 1], sm.a[lane]);
+		__syncthreads ();
+		TBF_MARK (6);
+		const size_t o = (size_t)blk * TBF_BLK + sb * TBF_SUB + n;
+		a0L[o]         = sin (sm.a[0][n] * wet);
+		a0R[o]         = sin (sm.a[1][n] * wet);
+		if (lane == 0)
+			st.countM = cnt_adv (st.countM, dM, TBF_SUB);
+		__syncthreads ();
+		TBF_MARK (7);
 	}
 	__syncthreads ();
 	if (lane == 0) { /* only k_rv_in's own fields: the other reverb kernels of neighbouring
@@ -1046,15 +1063,36 @@ k_rv_out (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 	const int     q   = (lane >> 1) & 1, c = lane & 1;
 	const double* cf  = K.bq[1 + q];
 	const double  c0 = cf[0], c1 = cf[1], c2 = cf[2], c3 = cf[3], c4 = cf[4];
+	/* software-pipelined loads: the tap mix of block it+1 and the dry input of block it-1
+	 * are issued before block it's serial pass and consumed after it */
+	double pb[4] = {0.0, 0.0, 0.0, 0.0};
+	if (P.nBlocks > 0) {
+		pb[0] = bL[lane];
+		pb[1] = bL[lane + NL];
+		pb[2] = bR[lane];
+		pb[3] = bR[lane + NL];
+	}
 	for (uint32_t it = 0; it <= P.nBlocks; it++) {
 		const bool haveB = it < P.nBlocks, haveC = it > 0;
 		/* (a) tap mix of block `it` */
 		if (haveB) {
-			const size_t o = (size_t)it * TBF_BLK;
-			sm.bx[0][lane]      = bL[o + lane];
-			sm.bx[0][lane + NL] = bL[o + lane + NL];
-			sm.bx[1][lane]      = bR[o + lane];
-			sm.bx[1][lane + NL] = bR[o + lane + NL];
+			sm.bx[0][lane]      = pb[0];
+			sm.bx[0][lane + NL] = pb[1];
+			sm.bx[1][lane]      = pb[2];
+			sm.bx[1][lane + NL] = pb[3];
+			if (it + 1 < P.nBlocks) {
+				const size_t o = (size_t)(it + 1) * TBF_BLK;
+				pb[0]          = bL[o + lane];
+				pb[1]          = bL[o + lane + NL];
+				pb[2]          = bR[o + lane];
+				pb[3]          = bR[o + lane + NL];
+			}
+		}
+		float pIn[2] = {0.f, 0.f};
+		if (haveC) {
+			const float* in = P.mid1 + (size_t)inst * P.midStride + (size_t)(it - 1) * TBF_BLK;
+			pIn[0]          = in[lane];
+			pIn[1]          = in[lane + NL];
 		}
 		__syncthreads ();
 		TBF_MARK (10);
@@ -1100,13 +1138,12 @@ k_rv_out (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 				st.fpdR2     = sm.fpd[1][TBF_BLK];
 			}
 			__syncthreads ();
-			const float* in  = P.mid1 + (size_t)inst * P.midStride + (size_t)ob * TBF_BLK;
 			float*       out = tap ? P.outL + (size_t)inst * P.outStride + P.outOffset + (size_t)ob * TBF_BLK
 			                       : P.mid2 + (size_t)inst * P.midStride + (size_t)ob * TBF_BLK;
 #pragma unroll
 			for (int h = 0; h < 2; h++) {
 				const int    n   = lane + h * NL;
-				const double inS = (double)in[n];
+				const double inS = (double)pIn[h];
 				double       ov[2];
 #pragma unroll
 				for (int cc = 0; cc < 2; cc++) {

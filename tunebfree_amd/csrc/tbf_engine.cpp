@@ -47,7 +47,9 @@ int tbf::fail (int code, const std::string& msg)
 #define PROG_CAP (TBF_NW + 1)
 /* blocks per kernel launch chunk: bounds the inter-stage buffers to
  * n_inst x TBF_CHUNK x 128 floats each (134 MB at 4096 instances) */
+#ifndef TBF_CHUNK
 #define TBF_CHUNK 64
+#endif
 /* delta program entries one chunk may add (a chunk ends early when they would not fit) */
 #define DPROG_CAP(n) ((size_t)(n) * PROG_CAP * 2 + 4096)
 #define TBF_NSTAGES 5 /* k_tonegen, k_rv_in, k_rv_core, k_rv_out, k_whirl */
@@ -690,6 +692,15 @@ static bool stepControl (tbf_engine* e, uint32_t i, bool& progChanged)
 	return true;
 }
 
+/* instance i may have new control (an event touched it): step it from this block on */
+static void markActive (tbf_engine* e, uint32_t i)
+{
+	if (i < e->inAct.size () && !e->inAct[i]) {
+		e->inAct[i] = 1;
+		e->actList.push_back (i);
+	}
+}
+
 static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, uint64_t stride, hipStream_t s,
                        const tbf_event* ev = nullptr, uint32_t nev = 0)
 {
@@ -701,6 +712,11 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		return 0;
 	if (stride < (uint64_t)nblocks * TBF_BLK)
 		return fail (-22, "stride smaller than nblocks*128");
+	/* every instance may have been changed through the API since the last call */
+	e->inAct.assign (n, 1);
+	e->actList.resize (n);
+	for (uint32_t i = 0; i < n; i++)
+		e->actList[i] = i;
 	tbf_launch P;
 	memset (&P, 0, sizeof (P));
 	P.bank      = e->bank.p;
@@ -755,7 +771,8 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		e->dCtl.clear ();
 		e->dProg.clear ();
 		e->hIdx.resize ((size_t)want * n);
-		std::vector<uint32_t> cur (n);
+		std::vector<uint32_t>& cur = e->curIdx;
+		cur.resize (n);
 		for (uint32_t i = 0; i < n; i++)
 			cur[i] = i;
 		bool     delta = false;
@@ -767,9 +784,15 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 				rc = applyEvent (e, ev[evi]);
 				if (rc)
 					return rc;
+				markActive (e, ev[evi].inst);
 			}
-			for (uint32_t i = 0; i < n; i++) {
-				bool pc;
+			/* only the instances whose control may still change are stepped: one that
+			 * steps to no change stays unchanged until an event touches it */
+			const bool hadDelta = delta;
+			size_t     keep     = 0;
+			for (size_t a = 0; a < e->actList.size (); a++) {
+				const uint32_t i = e->actList[a];
+				bool           pc;
 				if (stepControl (e, i, pc)) {
 					tbf_seg_ctl c = e->hCtl[i];
 					if (pc) {
@@ -782,8 +805,19 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 					e->dCtl.push_back (c);
 					e->chg[i] = 1;
 					delta     = true;
-				}
-				e->hIdx[(size_t)len * n + i] = cur[i];
+					e->actList[keep++] = i;
+				} else
+					e->inAct[i] = 0;
+			}
+			e->actList.resize (keep);
+			/* entry index table: written only once the chunk has a delta (before that
+			 * every row is the identity) */
+			if (delta) {
+				if (!hadDelta)
+					for (uint32_t r = 0; r < len; r++)
+						for (uint32_t i = 0; i < n; i++)
+							e->hIdx[(size_t)r * n + i] = i;
+				std::copy (cur.begin (), cur.end (), e->hIdx.begin () + (size_t)len * n);
 			}
 		}
 		const bool     par     = (e->chunkSeq++ & 1) != 0;

@@ -135,6 +135,9 @@ struct tbf_engine {
 	std::vector<tbf_prog_entry>             dProg;
 	std::vector<uint32_t>                   hIdx;
 	std::vector<uint8_t>                    chg;
+	std::vector<uint32_t>                   actList; /* instances stepped per block (renderImpl) */
+	std::vector<uint8_t>                    inAct;   /* membership of actList */
+	std::vector<uint32_t>                   curIdx;  /* pool entry per instance, current block */
 	DevBuf<uint32_t>                        ctlIdx;
 	bool                                    persistStale = true; /* device pool entries 0..n-1 need upload */
 	/* cross-chunk pipelining (renderImpl): the stages of chunk c run in order on stream

@@ -460,6 +460,7 @@ int tbf_midi_control (tbf_engine* e, uint32_t inst, const char* fn, int32_t valu
 	if (value < 0)
 		return fail (-22, "control value must be 0..127");
 	const unsigned char u = (unsigned char)(value > 127 ? 127 : value);
+	markActive (e, inst);
 	return controlFunction (e->inst[inst], fn, u) ? 0 : 1;
 }
 
@@ -516,6 +517,7 @@ int tbf_program_install (tbf_engine* e, uint32_t inst, uint32_t pc)
 		return fail (-22, "bad instance");
 	Instance& in = e->inst[inst];
 	const int p  = (int)(pc & 0x7f) + e->pgmOffset;
+	markActive (e, inst);
 	if (!(0 < p && p < (int)e->progs.size ()))
 		return 0;
 	Programme&     P  = e->progs[p];

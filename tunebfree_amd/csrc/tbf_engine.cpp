@@ -447,6 +447,7 @@ int tbf_instances_add (tbf_engine* e, uint32_t n, const uint32_t* tpl_ids, const
 			return fail (-22, "inconsistent reverb geometry");
 	}
 	e->deviceReady = false;
+	e->actAll      = true;
 	return 0;
 }
 
@@ -462,6 +463,7 @@ int tbf_note (tbf_engine* e, uint32_t i, int32_t key, int32_t on)
 		e->inst[i].tg.keyOn (key);
 	else
 		e->inst[i].tg.keyOff (key);
+	markActive (e, i);
 	return 0;
 }
 
@@ -471,6 +473,7 @@ int tbf_set_param (tbf_engine* e, uint32_t i, int32_t index, double v)
 		return fail (-22, "bad instance");
 	Instance& in    = e->inst[i];
 	float     value = (float)v;
+	markActive (e, i);
 	if (index >= 0 && index < 64)
 		in.params[index] = value;
 	/* src/clap.cpp:108-121 setToneGenParam + 162-207 setParam */
@@ -692,15 +695,6 @@ static bool stepControl (tbf_engine* e, uint32_t i, bool& progChanged)
 	return true;
 }
 
-/* instance i may have new control (an event touched it): step it from this block on */
-static void markActive (tbf_engine* e, uint32_t i)
-{
-	if (i < e->inAct.size () && !e->inAct[i]) {
-		e->inAct[i] = 1;
-		e->actList.push_back (i);
-	}
-}
-
 static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, uint64_t stride, hipStream_t s,
                        const tbf_event* ev = nullptr, uint32_t nev = 0)
 {
@@ -712,11 +706,13 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		return 0;
 	if (stride < (uint64_t)nblocks * TBF_BLK)
 		return fail (-22, "stride smaller than nblocks*128");
-	/* every instance may have been changed through the API since the last call */
-	e->inAct.assign (n, 1);
-	e->actList.resize (n);
-	for (uint32_t i = 0; i < n; i++)
-		e->actList[i] = i;
+	if (e->actAll || e->inAct.size () != n) { /* new instances: step every one */
+		e->inAct.assign (n, 1);
+		e->actList.resize (n);
+		for (uint32_t i = 0; i < n; i++)
+			e->actList[i] = i;
+		e->actAll = false;
+	}
 	tbf_launch P;
 	memset (&P, 0, sizeof (P));
 	P.bank      = e->bank.p;
@@ -1061,6 +1057,7 @@ int tbf_debug_step (tbf_engine* e, uint32_t i, float* out, uint32_t cap)
 	memset (&c, 0, sizeof (c));
 	in.tg.step (in.prog, c);
 	in.progDirty = in.ctlDirty = true;
+	markActive (e, i);
 	for (uint32_t q = 0; q < in.prog.size () && q < cap; q++) {
 		const tbf_prog_entry& p = in.prog[q];
 		float*                o = out + 9 * q;

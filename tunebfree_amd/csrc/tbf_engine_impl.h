@@ -135,8 +135,11 @@ struct tbf_engine {
 	std::vector<tbf_prog_entry>             dProg;
 	std::vector<uint32_t>                   hIdx;
 	std::vector<uint8_t>                    chg;
-	std::vector<uint32_t>                   actList; /* instances stepped per block (renderImpl) */
+	/* instances whose control may change at the next block (renderImpl steps only
+	 * these): every entry point that changes an instance marks it (markActive) */
+	std::vector<uint32_t>                   actList;
 	std::vector<uint8_t>                    inAct;   /* membership of actList */
+	bool                                    actAll = true; /* instances added: step all */
 	std::vector<uint32_t>                   curIdx;  /* pool entry per instance, current block */
 	DevBuf<uint32_t>                        ctlIdx;
 	bool                                    persistStale = true; /* device pool entries 0..n-1 need upload */
@@ -159,5 +162,15 @@ struct tbf_engine {
 	std::vector<float>                      fifoL, fifoR;
 	uint32_t                                boffset = TBF_BLK;
 };
+
+namespace tbf {
+inline void markActive (tbf_engine* e, uint32_t i)
+{
+	if (i < e->inAct.size () && !e->inAct[i]) {
+		e->inAct[i] = 1;
+		e->actList.push_back (i);
+	}
+}
+} // namespace tbf
 
 #endif

@@ -45,6 +45,15 @@
 #ifndef WH_WAVES
 #define WH_WAVES 3
 #endif
+#ifndef RV_TAP_UNROLL
+#define RV_TAP_UNROLL 2 /* k_rv_core delay lines whose taps are computed together */
+#endif
+#ifndef WH_SB_UNROLL
+#define WH_SB_UNROLL 1 /* k_whirl sub-blocks of a block unrolled */
+#endif
+#ifndef WH_RING_UNROLL
+#define WH_RING_UNROLL 4 /* k_whirl rings whose motions are computed together */
+#endif
 #ifndef TG_UNROLL
 #define TG_UNROLL 4 /* program entries of the tonegen interpreter in flight */
 #endif
@@ -963,7 +972,7 @@ k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 		__syncthreads ();
 		/* two-tap interpolation and blend */
 		double I[8];
-#pragma unroll 2
+#pragma unroll RV_TAP_UNROLL
 		for (int l = 0; l < 8; l++) {
 			const double off = rv_core_tap (sm, K, l, okm, v0x, Sx, Cx, Dx);
 			const int    d   = rl (dlyv, l);
@@ -1457,7 +1466,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 	const float* cfa = lane == 0 ? K.hafw : (lane == 1 ? K.hbfw : K.drf);
 	const float  fa0 = cfa[0], fa1 = cfa[1]; /* a1, a2 of the serial state recurrences */
 
-#pragma unroll 1
+#pragma unroll WH_SB_UNROLL
 	for (int sb = 0; sb < TBF_BLK / TBF_SUB; sb++) {
 		const int      n      = lane;
 		const uint32_t outpos = (st.outpos + (uint32_t)n) & 2047u;
@@ -1583,7 +1592,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 		TBF_MARK (22);
 
 		/* ---- per ring (HL, HR, DL, DR): its three motions, then the ordered adds ---- */
-#pragma unroll 1
+#pragma unroll WH_RING_UNROLL
 		for (int r = 0; r < 4; r++) {
 			int   mu[3];
 			float ma[3], mb[3];

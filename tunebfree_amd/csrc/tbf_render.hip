@@ -1371,31 +1371,6 @@ __device__ __forceinline__ void motion_add (float* ring, int U, float a, float b
 	}
 }
 
-/* the three motions of a ring when their slot ranges [U_q(0), U_q(63) + 1] are disjoint:
- * every slot takes terms of one motion only, so all reads go out together, then all
- * writes (no slot is read after another motion's write) */
-template <int W>
-__device__ __forceinline__ void motion_add3 (float* ring, const int* U, const float* a, const float* b, int lane)
-{
-	const uint32_t WM = (uint32_t)W - 1u;
-	MotionOwn      m[3];
-	float          v[3], w[3];
-#pragma unroll
-	for (int q = 0; q < 3; q++) {
-		m[q] = motion_own (U[q], a[q], b[q], lane);
-		v[q] = m[q].first ? ring[m[q].t & WM] : 0.f;
-		w[q] = (m[q].first && m[q].own2) ? ring[(m[q].t + 1) & WM] : 0.f;
-	}
-#pragma unroll
-	for (int q = 0; q < 3; q++) {
-		if (m[q].first) {
-			ring[m[q].t & WM] = motion_sum_t (m[q], v[q]);
-			if (m[q].own2)
-				ring[(m[q].t + 1) & WM] = motion_sum_t1 (m[q], w[q]);
-		}
-	}
-}
-
 /* one DF2 state recurrence over a sub-block (one lane): tp[0..1] = temp[-2], temp[-1],
  * tp[2 + i] = temp[i]; scrub applies the block-end NaN scrub (src/whirl.cpp:1622-1630)
  * to the incoming state first */
@@ -1653,12 +1628,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 					ok = 0;
 			}
 			float* ring = sm.wring[r];
-			if (__all (ok) && __builtin_amdgcn_readlane (mu[0], NL - 1) + 1 < __builtin_amdgcn_readfirstlane (mu[1]) &&
-			    __builtin_amdgcn_readlane (mu[1], NL - 1) + 1 < __builtin_amdgcn_readfirstlane (mu[2])) {
-				/* non-decreasing slots, so lane 0 / lane 63 hold each motion's range ends */
-				motion_add3<W> (ring, mu, ma, mb, lane);
-				__syncthreads ();
-			} else if (__all (ok)) {
+			if (__all (ok)) {
 				motion_add<W> (ring, mu[2], ma[2], mb[2], lane);
 				__syncthreads ();
 				motion_add<W> (ring, mu[1], ma[1], mb[1], lane);

@@ -1365,9 +1365,13 @@ __device__ __forceinline__ void motion_add (float* ring, int U, float a, float b
 	const uint32_t  WM = (uint32_t)W - 1u;
 	const MotionOwn m  = motion_own (U, a, b, lane);
 	if (m.first) {
-		ring[m.t & WM] = motion_sum_t (m, ring[m.t & WM]);
+		/* both slots read before either is written (one LDS round trip): an owner's
+		 * slot t+1 is read but left alone when another group owns it */
+		const uint32_t i0 = m.t & WM, i1 = (m.t + 1) & WM;
+		const float    v = ring[i0], w = ring[i1];
+		ring[i0]         = motion_sum_t (m, v);
 		if (m.own2)
-			ring[(m.t + 1) & WM] = motion_sum_t1 (m, ring[(m.t + 1) & WM]);
+			ring[i1] = motion_sum_t1 (m, w);
 	}
 }
 

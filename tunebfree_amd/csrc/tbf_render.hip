@@ -285,7 +285,7 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 	tbf_tg_state&         st   = sm.st;
 	const tbf_prog_entry* __restrict__ prog = P.prog + G.prog_off;
 	const int             np   = (int)G.prog_len;
-	float                 sw0 = 0.f, sw1 = 0.f, vb0 = 0.f, vb1 = 0.f, pc0 = 0.f, pc1 = 0.f;
+	float                 sw0 = -0.f, sw1 = -0.f, vb0 = -0.f, vb1 = -0.f, pc0 = -0.f, pc1 = -0.f;
 
 	/* core interpreter (wrap split folded into the index).  Prologue, lane per entry:
 	 * resolve the wheel's bank position and advance st.pos (each wheel appears once per
@@ -331,12 +331,12 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 			c0 = x0 * E.pg;
 			c1 = x1 * E.pg;
 		}
-		if (e == 0) {
-			sw0 = a0; sw1 = a1; vb0 = b0; vb1 = b1; pc0 = c0; pc1 = c1;
-		} else {
-			sw0 = sw0 + a0; sw1 = sw1 + a1; vb0 = vb0 + b0; vb1 = vb1 + b1; pc0 = pc0 + c0; pc1 = pc1 + c1;
-		}
+		/* the sums start at -0.f (below): -0 + a == a for every a, so the first entry's
+		 * add equals the reference's copy (CR_CPY) without a branch */
+		sw0 = sw0 + a0; sw1 = sw1 + a1; vb0 = vb0 + b0; vb1 = vb1 + b1; pc0 = pc0 + c0; pc1 = pc1 + c1;
 	}
+	if (np == 0) /* no program: the buses stay cleared (+0) */
+		sw0 = sw1 = vb0 = vb1 = pc0 = pc1 = 0.f;
 	__syncthreads (); /* the entry table is overwritten below */
 	sm.swl[lane] = sw0; sm.swl[lane + NL] = sw1;
 	sm.vin[lane] = vb0; sm.vin[lane + NL] = vb1;

@@ -43,7 +43,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=4096, help="instances per GPU")
     ap.add_argument("--blocks", type=int, default=64, help="128-sample blocks per step")
-    ap.add_argument("--sr", type=float, default=48000.0)
+    ap.add_argument("--sr", type=float, default=None, help="sample rate (default 48000; 96000 for cfg5)")
+    ap.add_argument("--workload", choices=("cfg3", "cfg5"), default="cfg3",
+                    help="cfg3: BASELINE configs[2]/[3] (the metric's workload); cfg5: configs[4] per-GPU "
+                         "sub-batch (96 kHz, 7 tunings, random drawbars) -- a secondary line, not the headline")
     ap.add_argument("--check", type=int, default=4, help="instances checked against the CPU oracle")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-instances", type=int, default=128)
@@ -57,10 +60,50 @@ def parse():
     return ap.parse_args()
 
 
-def setup_events(eng, first_global, n):
-    import scenarios as S
+class Workload:
+    """Per-instance template, seed and event script of a BASELINE config.
+    cfg3: configs[2]/[3] (one 48 kHz template, seed 7; Jazz-1 + chord per instance).
+    cfg5: configs[4] (one shared template per tuning of tests/golden/tunings.json,
+    instance g on tuning (5 g) mod 7, randomizeDrawbars-style upper drawbars)."""
+
+    def __init__(self, kind, sr):
+        import scenarios as S
+        self.kind, self.sr, self.S = kind, sr, S
+        self.names = [None]
+        self.mts = {None: None}
+        if kind == "cfg5":
+            import numpy as np
+            tun = json.loads((ROOT / "tests" / "golden" / "tunings.json").read_text())
+            self.names = sorted(tun, key=lambda k: (tun[k] is not None, k))
+            self.mts = {nm: (None if tun[nm] is None else np.array(tun[nm], np.float64)) for nm in self.names}
+
+    def tpl_seed(self, j):
+        return 7 if self.kind == "cfg3" else 100 + j
+
+    def tuning_of(self, g):
+        return 0 if self.kind == "cfg3" else (5 * g) % len(self.names)
+
+    def seed_of(self, g):
+        return 1000 + g
+
+    def scenario(self, g):
+        return self.S.bench_scenario(g) if self.kind == "cfg3" else self.S.random_drawbar_scenario(g)
+
+    def describe(self, B, world, blocks):
+        if self.kind == "cfg3":
+            return (f"configs[{2 if world == 1 else 3}]: full chain tonegen->vibrato->overdrive->reverb->whirl, "
+                    f"{B} instances/GPU x {world} GPU(s), {self.sr:.0f} Hz, {blocks} blocks/step, "
+                    f"Jazz-1 registration + 4-note chords")
+        return (f"configs[4] per-GPU sub-batch: full chain, {B} instances/GPU x {world} GPU(s), {self.sr:.0f} Hz, "
+                f"{len(self.names)} tunings (one shared bank each), random upper drawbars, {blocks} blocks/step")
+
+
+def setup_instances(eng, wl, first_global, n):
+    tids = [eng.template(mts128=wl.mts[nm], seed=wl.tpl_seed(j)) for j, nm in enumerate(wl.names)]
+    eng.add_instances([tids[wl.tuning_of(first_global + i)] for i in range(n)],
+                      [wl.seed_of(first_global + i) for i in range(n)])
     for i in range(n):
-        for (_, kind, a, v) in S.bench_scenario(first_global + i):
+        for (_, kind, a, v) in wl.scenario(first_global + i):
             if kind == "note":
                 eng.note(i, a, v)
             else:
@@ -106,18 +149,20 @@ def cpu_baseline(n_inst, blocks, sr):
                       f"oracle/ C restatement, {cores} processes, construction excluded (wall {wall:.1f}s)"}
 
 
-def oracle_check(rank_first, n_check, total_blocks, last_blocks, gpu_L, gpu_R, sr):
+def oracle_check(wl, rank_first, n_check, total_blocks, last_blocks, gpu_L, gpu_R):
     """max|err| of the last step's outputs vs the CPU oracle for the first instances."""
     import numpy as np
-    import scenarios as S
     from orc_bind import Chain, Template, load_oracle
     lib = load_oracle()
-    tpl = Template(lib, sr=sr, seed=7)
+    tpls = {}
     err, exact, tot = 0.0, 0, 0
     for i in range(n_check):
         g = rank_first + i
-        ch = Chain(lib, tpl, 1000 + g)
-        for (_, kind, a, v) in S.bench_scenario(g):
+        j = wl.tuning_of(g)
+        if j not in tpls:
+            tpls[j] = Template(lib, sr=wl.sr, mts128=wl.mts[wl.names[j]], seed=wl.tpl_seed(j))
+        ch = Chain(lib, tpls[j], wl.seed_of(g))
+        for (_, kind, a, v) in wl.scenario(g):
             (ch.note if kind == "note" else ch.param)(a, v)
         ch.render(total_blocks - last_blocks)
         L, R = ch.render(last_blocks)
@@ -147,10 +192,11 @@ def main():
 
     B = a.batch
     first_global = rank * B
+    if a.sr is None:
+        a.sr = 96000.0 if a.workload == "cfg5" else 48000.0
+    wl = Workload(a.workload, a.sr)
     eng = T.Engine(sample_rate=a.sr, device=torch.cuda.current_device(), chain=a.chain)
-    tid = eng.template(seed=7)
-    eng.add_instances([tid] * B, [1000 + first_global + i for i in range(B)])
-    setup_events(eng, first_global, B)
+    setup_instances(eng, wl, first_global, B)
     nsamp = a.blocks * 128
     outL = torch.empty((B, nsamp), dtype=torch.float32, device="cuda")
     outR = torch.empty((B, nsamp), dtype=torch.float32, device="cuda")
@@ -212,7 +258,7 @@ def main():
     gL = outL[: a.check].cpu().numpy()
     gR = outR[: a.check].cpu().numpy()
     total_blocks = (a.warmup + a.steps + ksteps * (2 if a.isolated else 1)) * a.blocks
-    max_err, exact = oracle_check(first_global, a.check, total_blocks, a.blocks, gL, gR, a.sr) if a.check else (None, None)
+    max_err, exact = oracle_check(wl, first_global, a.check, total_blocks, a.blocks, gL, gR) if a.check else (None, None)
     if dist:
         e = torch.tensor([max_err or 0.0], dtype=torch.float64, device="cuda")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
@@ -229,15 +275,13 @@ def main():
                     and dom in tj.get("kernels", {}):
                 traffic = tj["kernels"][dom]["bytes_per_launch"]
                 traffic_src = tj.get("source")
-        cpu = cpu_baseline(a.cpu_instances, a.cpu_blocks, a.sr) if (a.cpu_baseline and world == 1) else None
+        cpu = cpu_baseline(a.cpu_instances, a.cpu_blocks, a.sr) if (a.cpu_baseline and world == 1 and a.workload == "cfg3") else None
         line = {
             "metric": "stereo samples/sec whole-node, batch=4096 full chain @48kHz; max|err| vs CPU",
             "value": value, "unit": "stereo samples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32 (f64 reverb/overdrive)", "data": "synthetic",
-            "config": {"workload": f"configs[{2 if world == 1 else 3}]: full chain tonegen->vibrato->overdrive->"
-                                   f"reverb->whirl, {B} instances/GPU x {world} GPU(s), {a.sr:.0f} Hz, "
-                                   f"{a.blocks} blocks/step, Jazz-1 registration + 4-note chords",
+            "config": {"workload": wl.describe(B, world, a.blocks),
                        "batch_per_gpu": B, "blocks_per_step": a.blocks, "sample_rate": a.sr,
                        "parallelism": f"instance-sharded x{world} (no collective)"},
             "max_err": max_err, "bit_exact_frac": exact, "checked_instances": a.check,

@@ -44,9 +44,10 @@ def parse():
     ap.add_argument("--batch", type=int, default=4096, help="instances per GPU")
     ap.add_argument("--blocks", type=int, default=64, help="128-sample blocks per step")
     ap.add_argument("--sr", type=float, default=None, help="sample rate (default 48000; 96000 for cfg5)")
-    ap.add_argument("--workload", choices=("cfg3", "cfg5"), default="cfg3",
-                    help="cfg3: BASELINE configs[2]/[3] (the metric's workload); cfg5: configs[4] per-GPU "
-                         "sub-batch (96 kHz, 7 tunings, random drawbars) -- a secondary line, not the headline")
+    ap.add_argument("--workload", choices=("cfg3", "cfg2", "cfg5"), default="cfg3",
+                    help="cfg3: BASELINE configs[2]/[3] (the metric's workload); cfg2: configs[1] (tonegen only, "
+                         "use with --batch 256); cfg5: configs[4] per-GPU sub-batch (96 kHz, 7 tunings, random "
+                         "drawbars) -- secondary lines, not the headline")
     ap.add_argument("--check", type=int, default=4, help="instances checked against the CPU oracle")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-instances", type=int, default=128)
@@ -63,6 +64,8 @@ def parse():
 class Workload:
     """Per-instance template, seed and event script of a BASELINE config.
     cfg3: configs[2]/[3] (one 48 kHz template, seed 7; Jazz-1 + chord per instance).
+    cfg2: configs[1] (tonegen only: chain mode 1, L = R = oscGenerateFragment; drawbars
+    888000000 + vibrato, the same chords).
     cfg5: configs[4] (one shared template per tuning of tests/golden/tunings.json,
     instance g on tuning (5 g) mod 7, randomizeDrawbars-style upper drawbars)."""
 
@@ -78,18 +81,23 @@ class Workload:
             self.mts = {nm: (None if tun[nm] is None else np.array(tun[nm], np.float64)) for nm in self.names}
 
     def tpl_seed(self, j):
-        return 7 if self.kind == "cfg3" else 100 + j
+        return 100 + j if self.kind == "cfg5" else 7
 
     def tuning_of(self, g):
-        return 0 if self.kind == "cfg3" else (5 * g) % len(self.names)
+        return (5 * g) % len(self.names) if self.kind == "cfg5" else 0
 
     def seed_of(self, g):
         return 1000 + g
 
     def scenario(self, g):
-        return self.S.bench_scenario(g) if self.kind == "cfg3" else self.S.random_drawbar_scenario(g)
+        if self.kind == "cfg5":
+            return self.S.random_drawbar_scenario(g)
+        return self.S.bench_scenario(g, full=self.kind == "cfg3")
 
     def describe(self, B, world, blocks):
+        if self.kind == "cfg2":
+            return (f"configs[1]: tonegen only (oscGenerateFragment + vibrato, L = R), {B} instances/GPU x "
+                    f"{world} GPU(s), {self.sr:.0f} Hz, {blocks} blocks/step, drawbars 888000000 + 4-note chords")
         if self.kind == "cfg3":
             return (f"configs[{2 if world == 1 else 3}]: full chain tonegen->vibrato->overdrive->reverb->whirl, "
                     f"{B} instances/GPU x {world} GPU(s), {self.sr:.0f} Hz, {blocks} blocks/step, "
@@ -162,6 +170,8 @@ def oracle_check(wl, rank_first, n_check, total_blocks, last_blocks, gpu_L, gpu_
         if j not in tpls:
             tpls[j] = Template(lib, sr=wl.sr, mts128=wl.mts[wl.names[j]], seed=wl.tpl_seed(j))
         ch = Chain(lib, tpls[j], wl.seed_of(g))
+        if wl.kind == "cfg2":
+            ch.chain(1)
         for (_, kind, a, v) in wl.scenario(g):
             (ch.note if kind == "note" else ch.param)(a, v)
         ch.render(total_blocks - last_blocks)
@@ -195,6 +205,8 @@ def main():
     if a.sr is None:
         a.sr = 96000.0 if a.workload == "cfg5" else 48000.0
     wl = Workload(a.workload, a.sr)
+    if a.workload == "cfg2":
+        a.chain = 1  # TBF_CHAIN_TONEGEN
     eng = T.Engine(sample_rate=a.sr, device=torch.cuda.current_device(), chain=a.chain)
     setup_instances(eng, wl, first_global, B)
     nsamp = a.blocks * 128
@@ -266,6 +278,8 @@ def main():
 
     if rank == 0:
         samples_launch = B * nsamp
+        if a.chain == 1:  # tonegen only: k_tonegen writes L and R (8 B); bank reads are L2-resident
+            ALGO_BYTES["k_tonegen"] = 8
         dom = DOMINANT if DOMINANT in kern else max(kern, key=kern.get)
         achieved = samples_launch * ALGO_BYTES[dom] / (kern[dom] * 1e-3) / 1e9
         traffic, traffic_src = None, None

@@ -573,7 +573,7 @@ static int ensureDevice (tbf_engine* e)
 	}
 	HIPCHK (hipMemcpy (e->tplDesc.p, desc.data (), desc.size () * sizeof (tbf_tpl_desc), hipMemcpyHostToDevice));
 	/* shared tables */
-	if (e->vib.ensure (e->vibTab.size ()) || e->whTab.ensure (e->wt.displ.size ()) || e->whBw.ensure (e->wt.bw.size ()) ||
+	if (e->vib.ensure (e->vibTab.size ()) || e->whTab.ensure (4 * (size_t)TBF_WH_TSTRIDE) || e->whBw.ensure (e->wt.bw.size ()) ||
 	    e->err.ensure (4))
 		return fail (-12, "out of device memory (tables)");
 	HIPCHK (hipMemcpy (e->vib.p, e->vibTab.data (), e->vibTab.size () * 4, hipMemcpyHostToDevice));
@@ -587,7 +587,16 @@ static int ensureDevice (tbf_engine* e)
 			return fail (-12, "out of device memory (tables)");
 		HIPCHK (hipMemcpy (e->xsj.p, J.data (), J.size () * 4, hipMemcpyHostToDevice));
 	}
-	HIPCHK (hipMemcpy (e->whTab.p, e->wt.displ.data (), e->wt.displ.size () * 4, hipMemcpyHostToDevice));
+	{ /* each displacement table followed by its entry 0, so the kernel reads an entry and
+	   * its successor (wrapping at 16384) as one pair */
+		std::vector<float> padded (4 * (size_t)TBF_WH_TSTRIDE, 0.0f);
+		for (int t = 0; t < 4; t++) {
+			std::copy (e->wt.displ.begin () + (size_t)t * 16384, e->wt.displ.begin () + (size_t)(t + 1) * 16384,
+			           padded.begin () + (size_t)t * TBF_WH_TSTRIDE);
+			padded[(size_t)t * TBF_WH_TSTRIDE + 16384] = e->wt.displ[(size_t)t * 16384];
+		}
+		HIPCHK (hipMemcpy (e->whTab.p, padded.data (), padded.size () * 4, hipMemcpyHostToDevice));
+	}
 	HIPCHK (hipMemcpy (e->whBw.p, e->wt.bw.data (), e->wt.bw.size () * 4, hipMemcpyHostToDevice));
 	HIPCHK (hipMemset (e->err.p, 0, 16));
 	/* per-instance buffers: new instances start from their initial state, existing

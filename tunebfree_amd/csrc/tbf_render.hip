@@ -255,6 +255,10 @@ __device__ __forceinline__ double dither_add (double v, uint32_t fpd)
 	return v + t;
 }
 
+/* 4-byte-aligned float pairs / quads: one global load for consecutive table entries */
+typedef float f2u __attribute__ ((ext_vector_type (2), aligned (4)));
+typedef float f4u __attribute__ ((ext_vector_type (4), aligned (4)));
+
 /* fmodf (x, 1.f) (src/whirl.cpp:1436, 1458): for finite x >= 0 it is x - floorf (x),
  * which is exact (the fractional bits of x); anything else takes libm */
 __device__ __forceinline__ float frac1 (float x)
@@ -1415,9 +1419,9 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 	const int     lane  = threadIdx.x;
 	tbf_wh_state& st    = sm.st;
 	const float*  hnFwd = P.whTab;
-	const float*  hnBwd = P.whTab + 16384;
-	const float*  drFwd = P.whTab + 2 * 16384;
-	const float*  drBwd = P.whTab + 3 * 16384;
+	const float*  hnBwd = P.whTab + TBF_WH_TSTRIDE;
+	const float*  drFwd = P.whTab + 2 * TBF_WH_TSTRIDE;
+	const float*  drBwd = P.whTab + 3 * TBF_WH_TSTRIDE;
 	const float*  bfw   = P.whBw;
 	const float*  bbw   = P.whBw + 16384 * 5;
 
@@ -1589,15 +1593,16 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 					const float    h1   = (float)(ang * (unsigned int)16384 + K.hornPhase[p]);
 					const float    hd   = frac1 (h1);
 					const unsigned hl   = ((unsigned int)floorf (h1)) & 16383u;
-					const unsigned hh   = (hl + 1) & 16383u;
-					const float    intp = dsp[hl] * (1.f - hd) + hd * dsp[hh];
+					const f2u      dp   = *(const f2u*)(dsp + hl); /* dsp[hl], dsp[(hl + 1) & 16383] */
+					const float    intp = dp.x * (1.f - hd) + hd * dp.y;
 					const unsigned kk   = ((unsigned int)roundf (h1)) & 16383u;
 					t                   = K.hornSpacing[p] + intp + (float)outpos;
 					const float* b      = bw + 5 * kk;
-					xa                  = b[0] * hist[n + 4];
-					xa += b[1] * hist[n + 3];
-					xa += b[2] * hist[n + 2];
-					xa += b[3] * hist[n + 1];
+					const f4u    b4     = *(const f4u*)b;
+					xa                  = b4.x * hist[n + 4];
+					xa += b4.y * hist[n + 3];
+					xa += b4.z * hist[n + 2];
+					xa += b4.w * hist[n + 1];
 					xa += b[4] * hist[n + 0];
 				} else {
 					/* DR_MOTION, src/whirl.cpp:1455-1469 */
@@ -1606,8 +1611,8 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 					const float    d1   = (float)(da * (unsigned int)16384 + K.hornPhase[p]);
 					const float    dd   = frac1 (d1);
 					const unsigned dl   = ((unsigned int)floorf (d1)) & 16383u;
-					const unsigned dh   = (dl + 1) & 16383u;
-					const float    intp = dsp[dl] * (1.f - dd) + dd * dsp[dh];
+					const f2u      dp   = *(const f2u*)(dsp + dl); /* dsp[dl], dsp[(dl + 1) & 16383] */
+					const float    intp = dp.x * (1.f - dd) + dd * dp.y;
 					t                   = K.drumSpacing[p] + intp + (float)outpos;
 				}
 				const float rr = floorf (t);

@@ -15,6 +15,7 @@
 #define TBF_NW 256    /* NOF_WHEELS, src/tonegen.h:79 */
 #define TBF_PROF_SLOTS 32
 #define TBF_VRING 256
+#define TBF_WH_TSTRIDE 16388 /* device stride of the whirl displacement tables (16-byte aligned rows) */
 #define TBF_XS_JUMP 129 /* dither jump table columns: k = 0 .. 128 steps */ /* compact vibrato ring (reference 1024; live window <= 21+128) */
 
 /* one core-program entry = one wheel's contribution for one block
@@ -152,7 +153,7 @@ typedef struct tbf_launch {
 	const tbf_prog_entry* prog;
 	const uint32_t*       vibTab; /* [3][2048] */
 	const uint32_t*       xsJump; /* [32][TBF_XS_JUMP]: xorshift32^k (1 << j), k = 0..128 */
-	const float*          whTab;  /* hnFwd, hnBwd, drFwd, drBwd [4][16384] */
+	const float*          whTab;  /* hnFwd, hnBwd, drFwd, drBwd [4][TBF_WH_TSTRIDE]: 16384 + [0] again + pad */
 	const float*          whBw;   /* bfw, bbw [2][16384][5] */
 	float*                outL;
 	float*                outR;

@@ -51,6 +51,9 @@
 #ifndef WH_SB_UNROLL
 #define WH_SB_UNROLL 1 /* k_whirl sub-blocks of a block unrolled */
 #endif
+#ifndef WH_MG
+#define WH_MG 4 /* k_whirl rings whose motions are computed before their adds */
+#endif
 #ifndef WH_RING_UNROLL
 #define WH_RING_UNROLL 4 /* k_whirl rings whose motions are computed together */
 #endif
@@ -1574,93 +1577,102 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 		__syncthreads ();
 		TBF_MARK (22);
 
-		/* ---- per ring (HL, HR, DL, DR): its three motions, then the ordered adds ---- */
-#pragma unroll WH_RING_UNROLL
-		for (int r = 0; r < 4; r++) {
-			int   mu[3];
-			float ma[3], mb[3];
+		/* ---- rings (HL, HR, DL, DR) in groups of WH_MG: the group's motions first (their
+		 * table loads in flight together), then each ring's ordered adds ---- */
 #pragma unroll
-			for (int q = 0; q < 3; q++) {
-				const int  p   = (r & 1) + 2 * q;
-				const bool fwd = (p == 0 || p == 3 || p == 4);
-				float      xa, t;
-				if (r < 2) {
-					/* HN_MOTION, src/whirl.cpp:1432-1453 */
-					const float*   hist = p < 2 ? sm.xf : (p < 4 ? sm.x1 : sm.x2);
-					const float*   dsp  = fwd ? hnFwd : hnBwd;
-					const float*   bw   = fwd ? bbw : bfw;
-					const double   ang  = ha + ((p & 1) ? K.bwAng : K.fwAng);
-					const float    h1   = (float)(ang * (unsigned int)16384 + K.hornPhase[p]);
-					const float    hd   = frac1 (h1);
-					const unsigned hl   = ((unsigned int)floorf (h1)) & 16383u;
-					const f2u      dp   = *(const f2u*)(dsp + hl); /* dsp[hl], dsp[(hl + 1) & 16383] */
-					const float    intp = dp.x * (1.f - hd) + hd * dp.y;
-					const unsigned kk   = ((unsigned int)roundf (h1)) & 16383u;
-					t                   = K.hornSpacing[p] + intp + (float)outpos;
-					const float* b      = bw + 5 * kk;
-					const f4u    b4     = *(const f4u*)b;
-					xa                  = b4.x * hist[n + 4];
-					xa += b4.y * hist[n + 3];
-					xa += b4.z * hist[n + 2];
-					xa += b4.w * hist[n + 1];
-					xa += b[4] * hist[n + 0];
-				} else {
-					/* DR_MOTION, src/whirl.cpp:1455-1469 */
-					xa                  = p < 2 ? xin : (p < 4 ? xd1v : xd2v);
-					const float*   dsp  = fwd ? drFwd : drBwd;
-					const float    d1   = (float)(da * (unsigned int)16384 + K.hornPhase[p]);
-					const float    dd   = frac1 (d1);
-					const unsigned dl   = ((unsigned int)floorf (d1)) & 16383u;
-					const f2u      dp   = *(const f2u*)(dsp + dl); /* dsp[dl], dsp[(dl + 1) & 16383] */
-					const float    intp = dp.x * (1.f - dd) + dd * dp.y;
-					t                   = K.drumSpacing[p] + intp + (float)outpos;
+		for (int r0 = 0; r0 < 4; r0 += WH_MG) {
+			int   mu[WH_MG][3];
+			float ma[WH_MG][3], mb[WH_MG][3];
+#pragma unroll
+			for (int gi = 0; gi < WH_MG; gi++) {
+				const int r = r0 + gi;
+	#pragma unroll
+				for (int q = 0; q < 3; q++) {
+					const int  p   = (r & 1) + 2 * q;
+					const bool fwd = (p == 0 || p == 3 || p == 4);
+					float      xa, t;
+					if (r < 2) {
+						/* HN_MOTION, src/whirl.cpp:1432-1453 */
+						const float*   hist = p < 2 ? sm.xf : (p < 4 ? sm.x1 : sm.x2);
+						const float*   dsp  = fwd ? hnFwd : hnBwd;
+						const float*   bw   = fwd ? bbw : bfw;
+						const double   ang  = ha + ((p & 1) ? K.bwAng : K.fwAng);
+						const float    h1   = (float)(ang * (unsigned int)16384 + K.hornPhase[p]);
+						const float    hd   = frac1 (h1);
+						const unsigned hl   = ((unsigned int)floorf (h1)) & 16383u;
+						const f2u      dp   = *(const f2u*)(dsp + hl); /* dsp[hl], dsp[(hl + 1) & 16383] */
+						const float    intp = dp.x * (1.f - hd) + hd * dp.y;
+						const unsigned kk   = ((unsigned int)roundf (h1)) & 16383u;
+						t                   = K.hornSpacing[p] + intp + (float)outpos;
+						const float* b      = bw + 5 * kk;
+						const f4u    b4     = *(const f4u*)b;
+						xa                  = b4.x * hist[n + 4];
+						xa += b4.y * hist[n + 3];
+						xa += b4.z * hist[n + 2];
+						xa += b4.w * hist[n + 1];
+						xa += b[4] * hist[n + 0];
+					} else {
+						/* DR_MOTION, src/whirl.cpp:1455-1469 */
+						xa                  = p < 2 ? xin : (p < 4 ? xd1v : xd2v);
+						const float*   dsp  = fwd ? drFwd : drBwd;
+						const float    d1   = (float)(da * (unsigned int)16384 + K.hornPhase[p]);
+						const float    dd   = frac1 (d1);
+						const unsigned dl   = ((unsigned int)floorf (d1)) & 16383u;
+						const f2u      dp   = *(const f2u*)(dsp + dl); /* dsp[dl], dsp[(dl + 1) & 16383] */
+						const float    intp = dp.x * (1.f - dd) + dd * dp.y;
+						t                   = K.drumSpacing[p] + intp + (float)outpos;
+					}
+					const float rr = floorf (t);
+					const float qq = xa * (t - rr);
+					mu[gi][q]          = (int32_t)((unsigned int)rr) + unwrap;
+					ma[gi][q]          = xa - qq;
+					mb[gi][q]          = qq;
 				}
-				const float rr = floorf (t);
-				const float qq = xa * (t - rr);
-				mu[q]          = (int32_t)((unsigned int)rr) + unwrap;
-				ma[q]          = xa - qq;
-				mb[q]          = qq;
 			}
 			TBF_MARK (23);
-			/* fast path preconditions (wave vote): each motion's slot non-decreasing in n
-			 * with groups of <= 2 equal slots, and the ring's motions >= 2 slots apart in
-			 * source order at every sample (so passes farthest-first keep the per-slot
-			 * order: a farther motion reaches a slot only at earlier samples) */
-			int ok = (mu[1] >= mu[0] + 2) && (mu[2] >= mu[1] + 2);
 #pragma unroll
-			for (int q = 0; q < 3; q++) {
-				const int up = lane_shr1 (mu[q]);
-				const int un = lane_shl1 (mu[q]);
-				if (lane > 0 && mu[q] < up)
-					ok = 0;
-				if (lane > 0 && lane < NL - 1 && up == mu[q] && un == mu[q])
-					ok = 0;
-			}
-			float* ring = sm.wring[r];
-			if (__all (ok)) {
-				motion_add<W> (ring, mu[2], ma[2], mb[2], lane);
-				__syncthreads ();
-				motion_add<W> (ring, mu[1], ma[1], mb[1], lane);
-				__syncthreads ();
-				motion_add<W> (ring, mu[0], ma[0], mb[0], lane);
-				__syncthreads ();
-			} else {
-				/* serial replay in the reference order: sample-major, motions in source order */
-				for (int i = 0; i < TBF_SUB; i++) {
-#pragma unroll
-					for (int q = 0; q < 3; q++) {
-						const uint32_t sl = (uint32_t)__shfl (mu[q], i) & WM;
-						const float    aa = __shfl (ma[q], i);
-						const float    bb = __shfl (mb[q], i);
-						if (lane == 0) {
-							ring[sl] += aa;
-							ring[(sl + 1) & WM] += bb;
+			for (int gi = 0; gi < WH_MG; gi++) {
+				const int r = r0 + gi;
+				/* fast path preconditions (wave vote): each motion's slot non-decreasing in n
+				 * with groups of <= 2 equal slots, and the ring's motions >= 2 slots apart in
+				 * source order at every sample (so passes farthest-first keep the per-slot
+				 * order: a farther motion reaches a slot only at earlier samples) */
+				int ok = (mu[gi][1] >= mu[gi][0] + 2) && (mu[gi][2] >= mu[gi][1] + 2);
+	#pragma unroll
+				for (int q = 0; q < 3; q++) {
+					const int up = lane_shr1 (mu[gi][q]);
+					const int un = lane_shl1 (mu[gi][q]);
+					if (lane > 0 && mu[gi][q] < up)
+						ok = 0;
+					if (lane > 0 && lane < NL - 1 && up == mu[gi][q] && un == mu[gi][q])
+						ok = 0;
+				}
+				float* ring = sm.wring[r];
+				if (__all (ok)) {
+					motion_add<W> (ring, mu[gi][2], ma[gi][2], mb[gi][2], lane);
+					__syncthreads ();
+					motion_add<W> (ring, mu[gi][1], ma[gi][1], mb[gi][1], lane);
+					__syncthreads ();
+					motion_add<W> (ring, mu[gi][0], ma[gi][0], mb[gi][0], lane);
+					__syncthreads ();
+				} else {
+					/* serial replay in the reference order: sample-major, motions in source order */
+					for (int i = 0; i < TBF_SUB; i++) {
+	#pragma unroll
+						for (int q = 0; q < 3; q++) {
+							const uint32_t sl = (uint32_t)__shfl (mu[gi][q], i) & WM;
+							const float    aa = __shfl (ma[gi][q], i);
+							const float    bb = __shfl (mb[gi][q], i);
+							if (lane == 0) {
+								ring[sl] += aa;
+								ring[(sl + 1) & WM] += bb;
+							}
 						}
 					}
+					__syncthreads ();
 				}
-				__syncthreads ();
+				TBF_MARK (24);
 			}
-			TBF_MARK (24);
 		}
 		/* ---- outputs (whirlProc2 outHL/outHR/outDL/outDR + whirlProc3 mix) ---- */
 		{

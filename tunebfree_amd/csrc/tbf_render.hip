@@ -1416,7 +1416,7 @@ __device__ __forceinline__ void wh_serial (const float* ip, float* tp, float* fz
 /* whirlProc2 (src/whirl.cpp:1191-1638) + whirlProc3 mic mix (1653-1681) */
 template <int W>
 __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ctl& G, const tbf_inst_const& K,
-                             const float* __restrict__ in, const float* __restrict__ nextIn,
+                             const float in0, const float in1, const float nin0, const bool hasNext,
                              float* __restrict__ oL, float* __restrict__ oR)
 {
 	const int     lane  = threadIdx.x;
@@ -1432,7 +1432,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 		/* whirlProc2 bypass (src/whirl.cpp:1197-1215) + whirlProc3 mix */
 		for (int k = 0; k < 2; k++) {
 			const int   n = lane + k * NL;
-			const float x = in[n];
+			const float x = k == 0 ? in0 : in1;
 			oL[n] = x * K.mic[0] + x * K.mic[1] + 0.f * K.mic[2] + 0.f * K.mic[3];
 			oR[n] = x * K.mic[4] + x * K.mic[5] + 0.f * K.mic[6] + 0.f * K.mic[7];
 		}
@@ -1457,7 +1457,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 		const int      n      = lane;
 		const uint32_t outpos = (st.outpos + (uint32_t)n) & 2047u;
 		const int32_t  unwrap = (int32_t)(st.outpos + (uint32_t)n - outpos); /* 0 or 2048 */
-		const float    xin    = (float)((double)in[sb * TBF_SUB + n] + 1e-14);
+		const float    xin    = (float)((double)(sb == 0 ? in0 : in1) + 1e-14);
 		sm.xx[n + 1]          = xin;
 		if (lane == 0)
 			sm.xx[0] = st.z[2];
@@ -1486,9 +1486,9 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 		 * next sub-block (lane 0), B over this one (lane 1) and the drum shelves over
 		 * this one's ring outputs (lanes 2, 3).  A's own pass runs only when it is not
 		 * ahead (launch start, after a bypassed block). */
-		const bool aNext = sb + 1 < TBF_BLK / TBF_SUB || nextIn != nullptr;
+		const bool aNext = sb + 1 < TBF_BLK / TBF_SUB || hasNext;
 		if (aNext)
-			sm.xn[n] = (float)((double)(sb + 1 < TBF_BLK / TBF_SUB ? in[(sb + 1) * TBF_SUB + n] : nextIn[n]) + 1e-14);
+			sm.xn[n] = (float)((double)(sb + 1 < TBF_BLK / TBF_SUB ? in1 : nin0) + 1e-14);
 		__syncthreads ();
 		if (!sm.aReady) {
 			if (lane == 0)
@@ -1737,13 +1737,28 @@ k_whirl (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 		(&sm.wring[0][0])[i] = wr[i];
 	__syncthreads ();
 	TBF_MARK (26);
+	/* the input (lane n: samples n and n + 64 of a block) is loaded one block ahead, so
+	 * its latency overlaps a whole block instead of stalling a sub-block start */
+	const float* inBase = P.mid2 + (size_t)inst * P.midStride;
+	float        c0 = 0.f, c1 = 0.f;
+	if (P.nBlocks > 0) {
+		c0 = inBase[threadIdx.x];
+		c1 = inBase[threadIdx.x + NL];
+	}
 	for (uint32_t blk = 0; blk < P.nBlocks; blk++) {
-		const float* in = P.mid2 + (size_t)inst * P.midStride + (size_t)blk * TBF_BLK;
-		float*       oL = P.outL + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
-		float*       oR = P.outR + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
-		/* the next block's input, when horn filter A may run ahead into it */
-		const float* nextIn = (blk + 1 < P.nBlocks && !ctl_of (P, ctl, blk + 1, inst).whBypass) ? in + TBF_BLK : nullptr;
-		stage_whirl<W> (P, sm, ctl_of (P, ctl, blk, inst), K, in, nextIn, oL, oR);
+		float*     oL = P.outL + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
+		float*     oR = P.outR + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
+		float      n0 = 0.f, n1 = 0.f;
+		const bool more = blk + 1 < P.nBlocks;
+		if (more) {
+			n0 = inBase[(size_t)(blk + 1) * TBF_BLK + threadIdx.x];
+			n1 = inBase[(size_t)(blk + 1) * TBF_BLK + threadIdx.x + NL];
+		}
+		/* horn filter A may run ahead into the next block unless that one is bypassed */
+		const bool hasNext = more && !ctl_of (P, ctl, blk + 1, inst).whBypass;
+		stage_whirl<W> (P, sm, ctl_of (P, ctl, blk, inst), K, c0, c1, n0, hasNext, oL, oR);
+		c0 = n0;
+		c1 = n1;
 	}
 	__syncthreads ();
 	copy_words (S, &sm.st);

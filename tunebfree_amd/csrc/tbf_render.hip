@@ -206,6 +206,17 @@ __device__ __forceinline__ uint32_t xs_jump (const uint32_t* __restrict__ J, uin
 	return r;
 }
 
+/* xs_jump with the lane's 32 table entries (rows j, column k) already in registers */
+__device__ __forceinline__ uint32_t xs_jump_reg (const uint32_t* jr, uint32_t x0)
+{
+	x0         = __builtin_amdgcn_readfirstlane (x0);
+	uint32_t r = 0;
+#pragma unroll
+	for (int j = 0; j < 32; j++)
+		r ^= ((x0 >> j) & 1u) ? jr[j] : 0u;
+	return r;
+}
+
 /* xorshift32 state after a uniform k steps from a per-lane x: column k of the table is
  * uniform, so its 32 words come in as scalar loads */
 __device__ __forceinline__ uint32_t xs_jump_u (const uint32_t* __restrict__ J, uint32_t x, int k)
@@ -652,14 +663,15 @@ __device__ __forceinline__ void rv_chain (const double* cf, double& st7, double&
 }
 
 /* xorshift dither streams of one sub-block by GF(2) jumps: fpd[c][0] = state before
- * sample 0, fpd[c][n + 1] = state after sample n */
-__device__ __forceinline__ void rv_dither (const uint32_t* __restrict__ J, uint32_t& sL, uint32_t& sR,
+ * sample 0, fpd[c][n + 1] = state after sample n; jr = the lane's jump-table entries
+ * for k = lane + 1 (loaded once per launch) */
+__device__ __forceinline__ void rv_dither (const uint32_t* jr, uint32_t& sL, uint32_t& sR,
                                            uint32_t (*fpd)[TBF_SUB + 1])
 {
 	const int      lane = threadIdx.x;
 	const uint32_t gL = sL, gR = sR;
-	fpd[0][lane + 1]  = xs_jump (J, gL, lane + 1);
-	fpd[1][lane + 1]  = xs_jump (J, gR, lane + 1);
+	fpd[0][lane + 1]  = xs_jump_reg (jr, gL);
+	fpd[1][lane + 1]  = xs_jump_reg (jr, gR);
 	__syncthreads (); /* all lanes have read sL/sR */
 	if (lane == 0) {
 		fpd[0][0] = gL;
@@ -732,6 +744,10 @@ k_rv_in (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 	const uint32_t nSub   = P.nBlocks * (TBF_BLK / TBF_SUB);
 	double         pL = 0.0, pR = 0.0;
 	float          pIn = 0.f;
+	uint32_t       jr[32]; /* the dither jump table's column k = lane + 1, for every sub-block */
+#pragma unroll
+	for (int j = 0; j < 32; j++)
+		jr[j] = P.xsJump[j * TBF_XS_JUMP + lane + 1];
 	if (nSub > 0) {
 		const int cMr = cnt_adv (st.countM, dM, lane + 1);
 		pL            = mL[cMr];
@@ -743,7 +759,7 @@ k_rv_in (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 		const uint32_t blk = g / (TBF_BLK / TBF_SUB), sb = g % (TBF_BLK / TBF_SUB);
 		const double   wet = ctl_of (P, ctl, blk, inst).rvWet;
 		const int      n   = lane;
-		rv_dither (P.xsJump, st.fpdL, st.fpdR, sm.fpd);
+		rv_dither (jr, st.fpdL, st.fpdR, sm.fpd);
 		TBF_MARK (5);
 		const double inS = (double)pIn;
 		/* predelay M (src/reverb.cpp:350-358): write at count, read at count + 1 */

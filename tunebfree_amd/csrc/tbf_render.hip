@@ -1097,6 +1097,10 @@ k_rv_out (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 	const double  c0 = cf[0], c1 = cf[1], c2 = cf[2], c3 = cf[3], c4 = cf[4];
 	/* software-pipelined loads: the tap mix of block it+1 and the dry input of block it-1
 	 * are issued before block it's serial pass and consumed after it */
+	uint32_t jr[32]; /* the dither jump table's column k = lane + 1, for every block */
+#pragma unroll
+	for (int j = 0; j < 32; j++)
+		jr[j] = P.xsJump[j * TBF_XS_JUMP + lane + 1];
 	double pb[4] = {0.0, 0.0, 0.0, 0.0};
 	if (P.nBlocks > 0) {
 		pb[0] = bL[lane];
@@ -1157,7 +1161,7 @@ k_rv_out (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 			const double   wet = ctl_of (P, ctl, ob, inst).rvWet;
 			/* dither states F[0..128] of both streams for the block */
 			const uint32_t gL = st.fpdL2, gR = st.fpdR2;
-			const uint32_t l1 = xs_jump (P.xsJump, gL, lane + 1), r1 = xs_jump (P.xsJump, gR, lane + 1);
+			const uint32_t l1 = xs_jump_reg (jr, gL), r1 = xs_jump_reg (jr, gR);
 			sm.fpd[0][lane + 1]      = l1;
 			sm.fpd[1][lane + 1]      = r1;
 			sm.fpd[0][lane + 1 + NL] = xs_jump_u (P.xsJump, l1, NL);

@@ -27,7 +27,7 @@ for s in $STEPS; do
 	list) run counters 120 rocprofv3 -L ;;
 	tests) run tests 900 python3 -u -m pytest tests -x -v -s -m gpu --timeout 300 --timeout-method thread ;;
 	bench) run bench 900 python3 bench.py ;;
-	prof) run prof 300 python3 tools/prof_stages.py ;;
+	prof) run prof 300 env TBF_LIB=tunebfree_amd/_variants/libtbf_prof.so python3 tools/prof_stages.py ;;
 	ablate) for c in 1 2 3 0; do run ablate$c 300 python3 bench.py --chain $c --steps 3 --warmup 1 --cpu-baseline 0 --check 0; done ;;
 	stats) run stats 600 rocprofv3 --kernel-trace --stats -d "$OUT/stats" -o run --output-format csv -- python3 bench.py $BENCHP ;;
 	pmc)

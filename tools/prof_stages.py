@@ -1,5 +1,8 @@
 """Per-stage wave-clock breakdown of the render kernel (tbf_debug_profile marks).
 usage: python tools/prof_stages.py [--batch 4096] [--blocks 32]
+The marks are compiled only into a profiling build (the product kernels keep that LDS free):
+  make -C tunebfree_amd variant NAME=prof VFLAGS=-DTBF_STAGE_PROF=1
+  TBF_LIB=tunebfree_amd/_variants/libtbf_prof.so python tools/prof_stages.py
 Marks add a workgroup barrier each, so totals run ~10% above the unprofiled kernel."""
 import argparse
 import ctypes as C

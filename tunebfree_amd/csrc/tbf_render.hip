@@ -45,6 +45,9 @@
 #ifndef WH_WAVES
 #define WH_WAVES 3
 #endif
+#ifndef RV_PAD
+#define RV_PAD 2 /* doubles of padding per serial-chain LDS row (rows read together by lanes 0..3 on distinct banks) */
+#endif
 #ifndef RV_TAP_UNROLL
 #define RV_TAP_UNROLL 2 /* k_rv_core delay lines whose taps are computed together */
 #endif
@@ -61,61 +64,16 @@
 #define TG_UNROLL 4 /* program entries of the tonegen interpreter in flight */
 #endif
 
-/* ------------------------------------------------------------------ LDS layouts */
-struct TgLds {
-	tbf_tg_state st;
-	float        bufA[TBF_BLK];
-	float        bufB[TBF_BLK];
-	float        swl[TBF_BLK];
-	float        vin[TBF_BLK];
-	float        prc[TBF_BLK];
-	union {
-		struct { /* core-program entries resolved by the interpreter prologue */
-			uint32_t base[TBF_NW + 8]; /* bank index of the wheel's current sample */
-			uint32_t lim[TBF_NW + 8];  /* samples before the wheel's wrap */
-			uint32_t len[TBF_NW + 8];  /* wheel length */
-		} ent;
-		struct { /* vibrato + mixdown */
-			float   vout[TBF_BLK];
-			float   va[TBF_BLK];
-			float   vg[TBF_BLK];
-			int32_t vh[TBF_BLK];
-			float   pe[TBF_BLK];
-			float   kc[TBF_BLK];
-		} v;
-		struct { /* overdrive */
-			double   odx[TBF_BLK];
-			double   odh[TBF_BLK];
-			uint32_t fpd[TBF_BLK + 1];
-		} od;
-	} u;
-	unsigned long long prof[TBF_PROF_SLOTS];
+/* optional stage timing (tbf_debug_profile): wave-clock cycles accumulated per mark.
+ * Compiled in only with -DTBF_STAGE_PROF=1 (tools/prof_stages.py builds such a variant):
+ * the product kernels keep their LDS for co-resident workgroups of the other chunk. */
+#ifndef TBF_STAGE_PROF
+#define TBF_STAGE_PROF 0
+#endif
+#if TBF_STAGE_PROF
+#define TBF_PROF_LDS                                                                     \
+	unsigned long long prof[TBF_PROF_SLOTS];                                             \
 	unsigned long long plast;
-};
-
-
-template <int W>
-struct WhLds {
-	tbf_wh_state st;
-	float        wring[4][W];
-	float        xx[TBF_SUB + 1];
-	float        xf[TBF_SUB + 4];
-	float        x1[TBF_SUB + 4];
-	float        x2[TBF_SUB + 4];
-	float        xd1[TBF_SUB + 1];
-	float        rd[2][TBF_SUB]; /* drum ring outputs -> drum shelf outputs (in place) */
-	/* DF2 state sequences temp[n-2 .. 63]: horn A, horn B, drum L, drum R; after the
-	 * filter outputs, the serial rotor-angle fallback's scratch (2 x 64 doubles) */
-	alignas (8) float tmp[4][TBF_SUB + 2];
-	float        xn[TBF_SUB];         /* input of the next sub-block (horn A runs one sub-block ahead) */
-	float        aOut[TBF_SUB];       /* horn A output of the current sub-block */
-	int          brake;
-	int          aReady;              /* aOut holds the current sub-block's horn A output */
-	unsigned long long prof[TBF_PROF_SLOTS];
-	unsigned long long plast;
-};
-
-/* optional stage timing (tbf_debug_profile): wave-clock cycles accumulated per mark */
 #define TBF_MARK(k)                                                                      \
 	do {                                                                                 \
 		if (P.prof) {                                                                    \
@@ -146,6 +104,66 @@ __device__ __forceinline__ void prof_end (const tbf_launch& P, L& sm, uint32_t i
 	if (P.prof && threadIdx.x < TBF_PROF_SLOTS)
 		P.prof[(size_t)inst * TBF_PROF_SLOTS + threadIdx.x] += sm.prof[threadIdx.x];
 }
+#else
+#define TBF_PROF_LDS
+#define TBF_MARK(k) \
+	do {        \
+	} while (0)
+template <typename L> __device__ __forceinline__ void prof_begin (const tbf_launch&, L&) {}
+template <typename L> __device__ __forceinline__ void prof_end (const tbf_launch&, L&, uint32_t) {}
+#endif
+
+/* ------------------------------------------------------------------ LDS layouts */
+struct TgLds {
+	tbf_tg_state st;
+	float        bufA[TBF_BLK];
+	float        bufB[TBF_BLK];
+	float        swl[TBF_BLK];
+	float        vin[TBF_BLK];
+	float        prc[TBF_BLK];
+	union {
+		struct { /* core-program entries resolved by the interpreter prologue */
+			uint32_t base[TBF_NW + 8]; /* bank index of the wheel's current sample */
+			uint32_t lim[TBF_NW + 8];  /* samples before the wheel's wrap */
+			uint32_t len[TBF_NW + 8];  /* wheel length */
+		} ent;
+		struct { /* vibrato + mixdown */
+			float   vout[TBF_BLK];
+			float   va[TBF_BLK];
+			float   vg[TBF_BLK];
+			int32_t vh[TBF_BLK];
+			float   pe[TBF_BLK];
+			float   kc[TBF_BLK];
+		} v;
+		struct { /* overdrive */
+			double   odx[TBF_BLK];
+			double   odh[TBF_BLK];
+			uint32_t fpd[TBF_BLK + 1];
+		} od;
+	} u;
+	TBF_PROF_LDS
+};
+
+
+template <int W>
+struct WhLds {
+	tbf_wh_state st;
+	float        wring[4][W];
+	float        xx[TBF_SUB + 1];
+	float        xf[TBF_SUB + 4];
+	float        x1[TBF_SUB + 4];
+	float        x2[TBF_SUB + 4];
+	float        xd1[TBF_SUB + 1];
+	float        rd[2][TBF_SUB]; /* drum ring outputs -> drum shelf outputs (in place) */
+	/* DF2 state sequences temp[n-2 .. 63]: horn A, horn B, drum L, drum R; after the
+	 * filter outputs, the serial rotor-angle fallback's scratch (2 x 64 doubles) */
+	alignas (8) float tmp[4][TBF_SUB + 2];
+	float        xn[TBF_SUB];         /* input of the next sub-block (horn A runs one sub-block ahead) */
+	float        aOut[TBF_SUB];       /* horn A output of the current sub-block */
+	int          brake;
+	int          aReady;              /* aOut holds the current sub-block's horn A output */
+	TBF_PROF_LDS
+};
 
 /* the control entry of instance `inst` for block `blk` of the chunk: events land at
  * block boundaries, so the host records a new pool entry only where one changes */
@@ -662,6 +680,13 @@ __device__ __forceinline__ void rv_chain (const double* cf, double& st7, double&
 	st8 = s8;
 }
 
+/* the reverb state's head (everything before the channels' network state) in LDS: k_rv_in
+ * and k_rv_out use only these fields */
+struct RvHeadLds {
+	alignas (16) unsigned char b[offsetof (tbf_rv_state, ch)];
+	__device__ tbf_rv_state&   get () { return *reinterpret_cast<tbf_rv_state*> (b); }
+};
+
 /* xorshift dither streams of one sub-block by GF(2) jumps: fpd[c][0] = state before
  * sample 0, fpd[c][n + 1] = state after sample n; jr = the lane's jump-table entries
  * for k = lane + 1 (loaded once per launch) */
@@ -683,20 +708,18 @@ __device__ __forceinline__ void rv_dither (const uint32_t* jr, uint32_t& sL, uin
 }
 
 struct RvInLds {
-	tbf_rv_state st;
-	double       a[2][TBF_SUB];
+	RvHeadLds    hd;
+	double       a[2][TBF_SUB + RV_PAD];
 	uint32_t     fpd[2][TBF_SUB + 1];
-	unsigned long long prof[TBF_PROF_SLOTS];
-	unsigned long long plast;
+	TBF_PROF_LDS
 };
 
 struct RvOutLds {
-	tbf_rv_state st;
-	double       bx[2][TBF_BLK]; /* block b: tap mix -> biquadB output */
-	double       cx[2][TBF_BLK]; /* block b-1: asin output -> biquadC output */
+	RvHeadLds    hd;
+	double       bx[2][TBF_BLK + RV_PAD]; /* block b: tap mix -> biquadB output */
+	double       cx[2][TBF_BLK + RV_PAD]; /* block b-1: asin output -> biquadC output */
 	uint32_t     fpd[2][TBF_BLK + 1];
-	unsigned long long prof[TBF_PROF_SLOTS];
-	unsigned long long plast;
+	TBF_PROF_LDS
 };
 
 #define RV_WIN 72 /* tap window per line: 64 samples + max offset 2 * vibDepth (5.4) + 2 */
@@ -707,8 +730,7 @@ struct RvCoreLds {
 	double      sd[8][TBF_SUB];  /* sin ((n+1) D) of each line's closed-form step D ... */
 	double      cm[8][TBF_SUB];  /* ... and 1 - cos ((n+1) D) = 2 sin^2 ((n+1) D / 2) */
 	double      tabD[8];         /* the D the rows above hold (-1: none yet) */
-	unsigned long long prof[TBF_PROF_SLOTS];
-	unsigned long long plast;
+	TBF_PROF_LDS
 };
 
 /* FP64 stage buffers of one chunk: [inst][c][midStride] */
@@ -733,9 +755,9 @@ k_rv_in (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 	double*               a0L  = rv_buf (P.rvA, P, inst, 0);
 	double*               a0R  = rv_buf (P.rvA, P, inst, 1);
 	prof_begin (P, sm);
-	copy_head (&sm.st, S);
+	copy_head (&sm.hd.get (), S);
 	__syncthreads ();
-	tbf_rv_state& st = sm.st;
+	tbf_rv_state& st = sm.hd.get ();
 	/* software-pipelined: the predelay reads and the input of sub-block g+1 are issued
 	 * before sub-block g's writes and serial chain, so their latency overlaps it (the
 	 * reads lie at count+65 .. count+128, the writes at count .. count+63, and the ring
@@ -796,11 +818,11 @@ k_rv_in (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 	__syncthreads ();
 	if (lane == 0) { /* only k_rv_in's own fields: the other reverb kernels of neighbouring
 	                  * chunks may run concurrently (cross-chunk pipelining) */
-		S->countM = sm.st.countM;
-		S->fpdL   = sm.st.fpdL;
-		S->fpdR   = sm.st.fpdR;
+		S->countM = st.countM;
+		S->fpdL   = st.fpdL;
+		S->fpdR   = st.fpdR;
 		for (int j = 0; j < 4; j++)
-			S->bq[0][j] = sm.st.bq[0][j];
+			S->bq[0][j] = st.bq[0][j];
 	}
 	prof_end (P, sm, inst);
 }
@@ -1088,9 +1110,9 @@ k_rv_out (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 	const double*         bR  = rv_buf (P.rvB, P, inst, 1);
 	const bool            tap = P.chain == TBF_CHAIN_TAP_REVERB;
 	prof_begin (P, sm);
-	copy_head (&sm.st, S);
+	copy_head (&sm.hd.get (), S);
 	__syncthreads ();
-	tbf_rv_state& st = sm.st;
+	tbf_rv_state& st = sm.hd.get ();
 	/* serial lane roles: q = 0 biquadB, 1 biquadC; c = channel */
 	const int     q   = (lane >> 1) & 1, c = lane & 1;
 	const double* cf  = K.bq[1 + q];
@@ -1218,11 +1240,11 @@ k_rv_out (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 		TBF_MARK (13);
 	}
 	if (lane == 0) { /* only k_rv_out's own fields (see k_rv_in) */
-		S->fpdL2 = sm.st.fpdL2;
-		S->fpdR2 = sm.st.fpdR2;
+		S->fpdL2 = st.fpdL2;
+		S->fpdR2 = st.fpdR2;
 		for (int j = 0; j < 4; j++) {
-			S->bq[1][j] = sm.st.bq[1][j];
-			S->bq[2][j] = sm.st.bq[2][j];
+			S->bq[1][j] = st.bq[1][j];
+			S->bq[2][j] = st.bq[2][j];
 		}
 	}
 	prof_end (P, sm, inst);

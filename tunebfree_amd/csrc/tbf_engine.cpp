@@ -203,6 +203,22 @@ int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
 		HIPCHK (hipEventCreateWithFlags (&e->sjoin, hipEventDisableTiming));
 		const char* pl = getenv ("TBF_PIPELINE");
 		e->pipeline    = !(pl && pl[0] == '0');
+		/* TBF_PIPE_WAIT="w0,w1,...": stage k of a chunk also waits for stage w_k >= k of the
+		 * previous chunk (default w_k = k), which moves which stages of neighbouring chunks
+		 * co-run; any such table is exact (it only adds dependencies) */
+		for (int k = 0; k < TBF_NSTAGES; k++)
+			e->pipeWait[k] = k;
+		if (const char* pw = getenv ("TBF_PIPE_WAIT")) {
+			for (int k = 0; k < TBF_NSTAGES && *pw; k++) {
+				const int w = atoi (pw);
+				if (w >= k && w < TBF_NSTAGES)
+					e->pipeWait[k] = w;
+				while (*pw && *pw != ',')
+					pw++;
+				if (*pw == ',')
+					pw++;
+			}
+		}
 	}
 	e->wt.build (cfg->sample_rate);
 	/* compact whirl ring: live window < maxAhead + 2 + one sub-block */
@@ -868,7 +884,8 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 					HIPCHK (hipStreamWaitEvent (sp, e->sjoin, 0));
 					outWait = true;
 				}
-				HIPCHK (hipStreamWaitEvent (sp, e->sdone[k], 0)); /* stage k of the previous chunk */
+				/* stage k of the previous chunk (or a later one of it, TBF_PIPE_WAIT) */
+				HIPCHK (hipStreamWaitEvent (sp, e->sdone[std::min (e->pipeWait[k], nst - 1)], 0));
 				hipEvent_t e0 = nullptr, e1 = nullptr;
 				if (e->timeOn) { /* launch duration on the launch stream, dependencies met */
 					HIPCHK (hipEventCreate (&e0));

@@ -155,6 +155,7 @@ struct tbf_engine {
 	uint64_t                                chunkSeq = 0;
 	bool                                    stagesBusy = false; /* pipelined work may be outstanding */
 	bool                                    pipeline = true;    /* TBF_PIPELINE=0 disables */
+	int                                     pipeWait[5] = {0, 1, 2, 3, 4}; /* stage k of a chunk waits for stage pipeWait[k] >= k of the previous one */
 	/* programme table (.pgm), src/program.h:26 MAXPROGS; pgm.controller.offset */
 	std::vector<Programme>                  progs = std::vector<Programme> (129);
 	int                                     pgmOffset = 1;

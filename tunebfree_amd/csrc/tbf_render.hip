@@ -48,6 +48,9 @@
 #ifndef RV_PAD
 #define RV_PAD 2 /* doubles of padding per serial-chain LDS row (rows read together by lanes 0..3 on distinct banks) */
 #endif
+#ifndef RV_NT
+#define RV_NT 2 /* k_rv_core streaming accesses nontemporal: 2 ring and tap-mix stores (kept), 1 loads too (k_rv_core 2.94 -> 4.23 ms) */
+#endif
 #ifndef RV_TAP_UNROLL
 #define RV_TAP_UNROLL 2 /* k_rv_core delay lines whose taps are computed together */
 #endif
@@ -862,6 +865,23 @@ __device__ __forceinline__ int wrap_slot (int s, int d) { return s - ((s > d) ? 
  * carry: only slots count+9 .. count+72 (into wlo), since slots +1..+8 are the previous
  * sub-block's +65..+72, still in its window and not written since (the sub-block in
  * between writes slots count-64 .. count-1) */
+template <typename T> __device__ __forceinline__ T rv_ld (const T* p)
+{
+#if RV_NT == 1
+	return __builtin_nontemporal_load (p);
+#else
+	return *p;
+#endif
+}
+template <typename T> __device__ __forceinline__ void rv_st (T* p, T v)
+{
+#if RV_NT >= 1
+	__builtin_nontemporal_store (v, p);
+#else
+	*p = v;
+#endif
+}
+
 __device__ __forceinline__ void rv_core_fetch (const double* slab, int cntv, int dlyv, int roffv,
                                                const double* __restrict__ a0s, size_t o, RvFetch& f, bool carry)
 {
@@ -869,20 +889,20 @@ __device__ __forceinline__ void rv_core_fetch (const double* slab, int cntv, int
 #pragma unroll
 	for (int l = 8; l < 12; l++) {
 		const int d    = rl (dlyv, l);
-		f.apOld[l - 8] = slab[rl (roffv, l) + wrap_slot (rl (cntv, l) + lane + 1, d)];
+		f.apOld[l - 8] = rv_ld (&slab[rl (roffv, l) + wrap_slot (rl (cntv, l) + lane + 1, d)]);
 	}
 	const int k0 = carry ? 9 : 1;
 #pragma unroll
 	for (int l = 0; l < 8; l++) {
 		const int d = rl (dlyv, l);
-		f.wlo[l]    = slab[rl (roffv, l) + wrap_slot (rl (cntv, l) + k0 + lane, d)];
+		f.wlo[l]    = rv_ld (&slab[rl (roffv, l) + wrap_slot (rl (cntv, l) + k0 + lane, d)]);
 	}
 	if (!carry) {
 		const int l = lane >> 3, j = lane & 7;
 		const int d = __shfl (dlyv, l), cl = __shfl (cntv, l), ro = __shfl (roffv, l);
-		f.whi       = slab[ro + wrap_slot (cl + 1 + NL + j, d)];
+		f.whi       = rv_ld (&slab[ro + wrap_slot (cl + 1 + NL + j, d)]);
 	}
-	f.a0 = a0s[o];
+	f.a0 = rv_ld (&a0s[o]);
 }
 
 /* Vibrato phases (src/reverb.cpp:479-496) and tap offsets (sin (v) + 1) * vibDepth.
@@ -1064,10 +1084,10 @@ k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 		const int ncv = wrap_slot (cntv + TBF_SUB, dlyv);
 		if (s + 1 < nSub)
 			rv_core_fetch (slab, ncv, dlyv, roffv, a0s, o + TBF_SUB, f, true);
-		bout[o] = mix;
+		rv_st (&bout[o], mix);
 #pragma unroll
 		for (int l = 8; l < 12; l++)
-			slab[rl (roffv, l) + wrap_slot (rl (cntv, l) + n, rl (dlyv, l))] = apw[l - 8];
+			rv_st (&slab[rl (roffv, l) + wrap_slot (rl (cntv, l) + n, rl (dlyv, l))], apw[l - 8]);
 		/* delay-line writes: allpass output + the previous sample's feedback */
 		const int srcAp[8] = {3, 2, 1, 0, 0, 1, 2, 3};
 		double    fbn      = fbv;
@@ -1075,7 +1095,7 @@ k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 		for (int l = 0; l < 8; l++) {
 			const double up = lane_shr1 (fb[l]), carry = rld (fbv, l);
 			const double prev = lane == 0 ? carry : up;
-			slab[rl (roffv, l) + wrap_slot (rl (cntv, l) + n, rl (dlyv, l))] = ap[srcAp[l]] + prev;
+			rv_st (&slab[rl (roffv, l) + wrap_slot (rl (cntv, l) + n, rl (dlyv, l))], ap[srcAp[l]] + prev);
 			const double last = rld (fb[l], NL - 1);
 			fbn               = lane == l ? last : fbn;
 		}

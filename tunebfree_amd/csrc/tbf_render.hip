@@ -51,6 +51,9 @@
 #ifndef RV_NT
 #define RV_NT 2 /* k_rv_core streaming accesses nontemporal: 2 ring and tap-mix stores (kept), 1 loads too (k_rv_core 2.94 -> 4.23 ms) */
 #endif
+#ifndef STREAM_NT
+#define STREAM_NT 0 /* stage-stream stores (mid1, rvA, mid2, output, predelay ring) nontemporal */
+#endif
 #ifndef RV_TAP_UNROLL
 #define RV_TAP_UNROLL 2 /* k_rv_core delay lines whose taps are computed together */
 #endif
@@ -115,6 +118,16 @@ __device__ __forceinline__ void prof_end (const tbf_launch& P, L& sm, uint32_t i
 template <typename L> __device__ __forceinline__ void prof_begin (const tbf_launch&, L&) {}
 template <typename L> __device__ __forceinline__ void prof_end (const tbf_launch&, L&, uint32_t) {}
 #endif
+
+/* a stage-stream store (STREAM_NT: nontemporal) */
+template <typename T> __device__ __forceinline__ void stream_st (T* p, T v)
+{
+#if STREAM_NT
+	__builtin_nontemporal_store (v, p);
+#else
+	*p = v;
+#endif
+}
 
 /* ------------------------------------------------------------------ LDS layouts */
 struct TgLds {
@@ -630,8 +643,8 @@ k_tonegen (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl, const tbf_tp
 		}
 		stage_overdrive (P, sm, G);
 		float* o = P.mid1 + (size_t)inst * P.midStride + (size_t)blk * TBF_BLK;
-		o[lane]      = sm.bufB[lane];
-		o[lane + NL] = sm.bufB[lane + NL];
+		stream_st (&o[lane], sm.bufB[lane]);
+		stream_st (&o[lane + NL], sm.bufB[lane + NL]);
 		if (P.chain == TBF_CHAIN_TAP_PREAMP) {
 			float* oL = P.outL + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
 			float* oR = P.outR + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
@@ -803,7 +816,7 @@ k_rv_in (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 			double x = inS;
 			if (fabs (x) < 1.18e-23)
 				x = sm.fpd[c][n] * 1.18e-17;
-			(c ? mR : mL)[cMn] = x;
+			stream_st (&(c ? mR : mL)[cMn], x);
 		}
 		/* biquadA, both channels: lanes 0, 1 */
 		if (lane < 2)
@@ -811,8 +824,8 @@ k_rv_in (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 		__syncthreads ();
 		TBF_MARK (6);
 		const size_t o = (size_t)blk * TBF_BLK + sb * TBF_SUB + n;
-		a0L[o]         = sin (sm.a[0][n] * wet);
-		a0R[o]         = sin (sm.a[1][n] * wet);
+		stream_st (&a0L[o], sin (sm.a[0][n] * wet));
+		stream_st (&a0R[o], sin (sm.a[1][n] * wet));
 		if (lane == 0)
 			st.countM = cnt_adv (st.countM, dM, TBF_SUB);
 		__syncthreads ();
@@ -1235,7 +1248,7 @@ k_rv_out (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 					ov[cc] = dither_add (x, sm.fpd[cc][n + 1]);
 				}
 				const float y = (float)(0.7071067811865476 * (ov[0] + ov[1]));
-				out[n]        = y;
+				stream_st (&out[n], y);
 				if (tap)
 					P.outR[(size_t)inst * P.outStride + P.outOffset + (size_t)ob * TBF_BLK + n] = y;
 			}
@@ -1743,8 +1756,8 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 			const float hR   = K.hornLevel * hrv + leak;
 			const float dL   = sm.rd[0][n];
 			const float dR   = sm.rd[1][n];
-			oL[sb * TBF_SUB + n] = hL * K.mic[0] + hR * K.mic[1] + dL * K.mic[2] + dR * K.mic[3];
-			oR[sb * TBF_SUB + n] = hL * K.mic[4] + hR * K.mic[5] + dL * K.mic[6] + dR * K.mic[7];
+			stream_st (&oL[sb * TBF_SUB + n], hL * K.mic[0] + hR * K.mic[1] + dL * K.mic[2] + dR * K.mic[3]);
+			stream_st (&oR[sb * TBF_SUB + n], hL * K.mic[4] + hR * K.mic[5] + dL * K.mic[6] + dR * K.mic[7]);
 		}
 		/* ---- carry filter taps and histories ---- */
 		if (lane == NL - 1) {

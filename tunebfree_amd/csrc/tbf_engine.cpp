@@ -597,8 +597,10 @@ static int ensureDevice (tbf_engine* e)
 		/* xorshift32 (src/overdrive.cpp:158-160, src/reverb.cpp:775-783) is linear over
 		 * GF(2): state after k steps = XOR over the set bits j of the state of
 		 * xorshift^k (1 << j).  Column k of row j holds that image, k = 0 .. 128. */
-		std::vector<uint32_t> J (32 * TBF_XS_JUMP);
+		std::vector<uint32_t> J (32 * TBF_XS_JUMP + 128 * TBF_XS_JUMP);
 		xs_jump_table (J.data (), TBF_XS_JUMP);
+		/* followed by its nibble-sliced form [8][16][TBF_XS_JUMP] (xs_nib_table) */
+		xs_nib_table (J.data () + 32 * TBF_XS_JUMP, J.data (), TBF_XS_JUMP);
 		if (e->xsj.ensure (J.size ()))
 			return fail (-12, "out of device memory (tables)");
 		HIPCHK (hipMemcpy (e->xsj.p, J.data (), J.size () * 4, hipMemcpyHostToDevice));

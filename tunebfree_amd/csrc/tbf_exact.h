@@ -104,6 +104,21 @@ static inline void xs_jump_table (uint32_t* J, int cols)
 	}
 }
 
+/* nibble-sliced form of J: N[(i * 16 + v) * cols + k] = XOR over the set bits b of v of
+ * J[(4 i + b) * cols + k], so the k-step state is the XOR of 8 entries, one per nibble */
+static inline void xs_nib_table (uint32_t* N, const uint32_t* J, int cols)
+{
+	for (int i = 0; i < 8; i++)
+		for (int v = 0; v < 16; v++)
+			for (int k = 0; k < cols; k++) {
+				uint32_t r = 0;
+				for (int b = 0; b < 4; b++)
+					if ((v >> b) & 1)
+						r ^= J[(4 * i + b) * cols + k];
+				N[(i * 16 + v) * cols + k] = r;
+			}
+}
+
 TBF_HD uint32_t xs_jump_ref (const uint32_t* J, int cols, uint32_t x0, int k)
 {
 	uint32_t r = 0;

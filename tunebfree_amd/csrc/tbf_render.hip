@@ -54,6 +54,9 @@
 #ifndef STREAM_NT
 #define STREAM_NT 0 /* stage-stream stores (mid1, rvA, mid2, output, predelay ring) nontemporal */
 #endif
+#ifndef XS_NIB
+#define XS_NIB 1 /* dither jumps from the nibble-sliced table: 8 coalesced loads per state */
+#endif
 #ifndef RV_TAP_UNROLL
 #define RV_TAP_UNROLL 2 /* k_rv_core delay lines whose taps are computed together */
 #endif
@@ -238,6 +241,19 @@ __device__ __forceinline__ uint32_t xs_jump (const uint32_t* __restrict__ J, uin
 			r ^= ((x0 >> (h + j)) & 1u) ? v[j] : 0u;
 	}
 	return r;
+}
+
+/* xorshift32 state after a per-lane k steps from a uniform x0, from the nibble-sliced table
+ * (xs_nib_table): one coalesced row load per nibble of x0, 8 in flight together */
+__device__ __forceinline__ uint32_t xs_jump_n (const uint32_t* __restrict__ J, uint32_t x0, int k)
+{
+	const uint32_t* N = J + 32 * TBF_XS_JUMP;
+	x0                = __builtin_amdgcn_readfirstlane (x0);
+	uint32_t v[8];
+#pragma unroll
+	for (int i = 0; i < 8; i++)
+		v[i] = N[(i * 16 + ((x0 >> (4 * i)) & 15u)) * TBF_XS_JUMP + k];
+	return ((v[0] ^ v[1]) ^ (v[2] ^ v[3])) ^ ((v[4] ^ v[5]) ^ (v[6] ^ v[7]));
 }
 
 /* xs_jump with the lane's 32 table entries (rows j, column k) already in registers */
@@ -544,9 +560,14 @@ __device__ void stage_overdrive (const tbf_launch& P, TgLds& sm, const tbf_seg_c
 	/* xorshift dither states F[0..128] (F[n+1] after sample n) by GF(2) jumps */
 	{
 		const uint32_t f0 = st.odFpd;
+#if XS_NIB
+		sm.u.od.fpd[lane + 1]      = xs_jump_n (P.xsJump, f0, lane + 1);
+		sm.u.od.fpd[lane + 1 + NL] = xs_jump_n (P.xsJump, f0, lane + 1 + NL);
+#else
 		const uint32_t lo          = xs_jump (P.xsJump, f0, lane + 1);
 		sm.u.od.fpd[lane + 1]      = lo;
 		sm.u.od.fpd[lane + 1 + NL] = xs_jump_u (P.xsJump, lo, NL);
+#endif
 		__syncthreads (); /* all lanes have read st.odFpd */
 		if (lane == 0) {
 			sm.u.od.fpd[0] = f0;
@@ -706,13 +727,18 @@ struct RvHeadLds {
 /* xorshift dither streams of one sub-block by GF(2) jumps: fpd[c][0] = state before
  * sample 0, fpd[c][n + 1] = state after sample n; jr = the lane's jump-table entries
  * for k = lane + 1 (loaded once per launch) */
-__device__ __forceinline__ void rv_dither (const uint32_t* jr, uint32_t& sL, uint32_t& sR,
-                                           uint32_t (*fpd)[TBF_SUB + 1])
+__device__ __forceinline__ void rv_dither (const uint32_t* __restrict__ J, const uint32_t* jr, uint32_t& sL,
+                                           uint32_t& sR, uint32_t (*fpd)[TBF_SUB + 1])
 {
 	const int      lane = threadIdx.x;
 	const uint32_t gL = sL, gR = sR;
+#if XS_NIB
+	fpd[0][lane + 1] = xs_jump_n (J, gL, lane + 1);
+	fpd[1][lane + 1] = xs_jump_n (J, gR, lane + 1);
+#else
 	fpd[0][lane + 1]  = xs_jump_reg (jr, gL);
 	fpd[1][lane + 1]  = xs_jump_reg (jr, gR);
+#endif
 	__syncthreads (); /* all lanes have read sL/sR */
 	if (lane == 0) {
 		fpd[0][0] = gL;
@@ -782,10 +808,14 @@ k_rv_in (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 	const uint32_t nSub   = P.nBlocks * (TBF_BLK / TBF_SUB);
 	double         pL = 0.0, pR = 0.0;
 	float          pIn = 0.f;
+#if XS_NIB
+	const uint32_t* jr = nullptr;
+#else
 	uint32_t       jr[32]; /* the dither jump table's column k = lane + 1, for every sub-block */
 #pragma unroll
 	for (int j = 0; j < 32; j++)
 		jr[j] = P.xsJump[j * TBF_XS_JUMP + lane + 1];
+#endif
 	if (nSub > 0) {
 		const int cMr = cnt_adv (st.countM, dM, lane + 1);
 		pL            = mL[cMr];
@@ -797,7 +827,7 @@ k_rv_in (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 		const uint32_t blk = g / (TBF_BLK / TBF_SUB), sb = g % (TBF_BLK / TBF_SUB);
 		const double   wet = ctl_of (P, ctl, blk, inst).rvWet;
 		const int      n   = lane;
-		rv_dither (jr, st.fpdL, st.fpdR, sm.fpd);
+		rv_dither (P.xsJump, jr, st.fpdL, st.fpdR, sm.fpd);
 		TBF_MARK (5);
 		const double inS = (double)pIn;
 		/* predelay M (src/reverb.cpp:350-358): write at count, read at count + 1 */
@@ -1152,10 +1182,12 @@ k_rv_out (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 	const double  c0 = cf[0], c1 = cf[1], c2 = cf[2], c3 = cf[3], c4 = cf[4];
 	/* software-pipelined loads: the tap mix of block it+1 and the dry input of block it-1
 	 * are issued before block it's serial pass and consumed after it */
+#if !XS_NIB
 	uint32_t jr[32]; /* the dither jump table's column k = lane + 1, for every block */
 #pragma unroll
 	for (int j = 0; j < 32; j++)
 		jr[j] = P.xsJump[j * TBF_XS_JUMP + lane + 1];
+#endif
 	double pb[4] = {0.0, 0.0, 0.0, 0.0};
 	if (P.nBlocks > 0) {
 		pb[0] = bL[lane];
@@ -1216,11 +1248,18 @@ k_rv_out (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 			const double   wet = ctl_of (P, ctl, ob, inst).rvWet;
 			/* dither states F[0..128] of both streams for the block */
 			const uint32_t gL = st.fpdL2, gR = st.fpdR2;
+#if XS_NIB
+			sm.fpd[0][lane + 1]      = xs_jump_n (P.xsJump, gL, lane + 1);
+			sm.fpd[1][lane + 1]      = xs_jump_n (P.xsJump, gR, lane + 1);
+			sm.fpd[0][lane + 1 + NL] = xs_jump_n (P.xsJump, gL, lane + 1 + NL);
+			sm.fpd[1][lane + 1 + NL] = xs_jump_n (P.xsJump, gR, lane + 1 + NL);
+#else
 			const uint32_t l1 = xs_jump_reg (jr, gL), r1 = xs_jump_reg (jr, gR);
 			sm.fpd[0][lane + 1]      = l1;
 			sm.fpd[1][lane + 1]      = r1;
 			sm.fpd[0][lane + 1 + NL] = xs_jump_u (P.xsJump, l1, NL);
 			sm.fpd[1][lane + 1 + NL] = xs_jump_u (P.xsJump, r1, NL);
+#endif
 			__syncthreads ();
 			if (lane == 0) {
 				sm.fpd[0][0] = gL;

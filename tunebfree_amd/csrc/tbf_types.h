@@ -152,7 +152,7 @@ typedef struct tbf_launch {
 	const uint32_t*       ctlIdx; /* [nBlocks][nInst] pool index per block, or NULL: entry inst */
 	const tbf_prog_entry* prog;
 	const uint32_t*       vibTab; /* [3][2048] */
-	const uint32_t*       xsJump; /* [32][TBF_XS_JUMP]: xorshift32^k (1 << j), k = 0..128 */
+	const uint32_t*       xsJump; /* [32][TBF_XS_JUMP]: xorshift32^k (1 << j), k = 0..128; then [8][16][TBF_XS_JUMP] nibble-sliced */
 	const float*          whTab;  /* hnFwd, hnBwd, drFwd, drBwd [4][TBF_WH_TSTRIDE]: 16384 + [0] again + pad */
 	const float*          whBw;   /* bfw, bbw [2][16384][5] */
 	float*                outL;

@@ -322,7 +322,9 @@ def test_count_and_wrap_shortcuts():
 def test_dither_jump_table_matches_literal_xorshift():
     """The kernels generate the Airwindows xorshift32 dither streams (src/overdrive.cpp:
     158-160, src/reverb.cpp:775-783) by GF(2) jumps instead of 64-128 serial steps; the
-    jump equals the literal recurrence for every k the kernels use (0..128)."""
+    jump equals the literal recurrence for every k the kernels use (0..128).  The host
+    hook evaluates it as the kernels do, from the nibble-sliced table (8 entries per state),
+    and fails if that ever differs from the 32 bit-row form."""
     rng = np.random.default_rng(5)
     seeds = [1, 16386, 0xFFFFFFFF, 0x80000000, 12345] + [int(x) for x in rng.integers(1, 2 ** 32, 40)]
     rows = [(x0, k, 0) for x0 in seeds for k in (0, 1, 2, 63, 64, 65, 127, 128)]

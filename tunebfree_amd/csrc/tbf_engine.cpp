@@ -1129,9 +1129,10 @@ int tbf_debug_exact (int32_t op, const double* in, double* out, uint32_t n)
 	if (!in || !out || op < 0 || op > 5)
 		return fail (-22, "bad arguments");
 	static std::vector<uint32_t> J;
-	if (op == 3 && J.empty ()) {
-		J.resize (32 * TBF_XS_JUMP);
+	if (op == 3 && J.empty ()) { /* the device layout: bit rows, then the nibble-sliced rows */
+		J.resize (32 * TBF_XS_JUMP + 128 * TBF_XS_JUMP);
 		xs_jump_table (J.data (), TBF_XS_JUMP);
+		xs_nib_table (J.data () + 32 * TBF_XS_JUMP, J.data (), TBF_XS_JUMP);
 	}
 	for (uint32_t i = 0; i < n; i++) {
 		const double* a = in + 3 * i;
@@ -1175,7 +1176,8 @@ int tbf_debug_exact (int32_t op, const double* in, double* out, uint32_t n)
 			o[0] = bad;
 			o[1] = hits;
 		} else {
-			/* op 3: xorshift jump (device table) vs k literal steps from x0 */
+			/* op 3: xorshift jump as the kernels take it (nibble-sliced table, which must
+			 * agree with the bit-row form) vs k literal steps from x0 */
 			const uint32_t x0 = (uint32_t)a[0];
 			const int      k  = (int)a[1];
 			if (k < 0 || k >= TBF_XS_JUMP)
@@ -1183,7 +1185,13 @@ int tbf_debug_exact (int32_t op, const double* in, double* out, uint32_t n)
 			uint32_t x = x0;
 			for (int q = 0; q < k; q++)
 				x = xs_step (x);
-			o[0] = xs_jump_ref (J.data (), TBF_XS_JUMP, x0, k);
+			const uint32_t* N = J.data () + 32 * TBF_XS_JUMP;
+			uint32_t        r = 0;
+			for (int q = 0; q < 8; q++)
+				r ^= N[(q * 16 + ((x0 >> (4 * q)) & 15u)) * TBF_XS_JUMP + k];
+			if (r != xs_jump_ref (J.data (), TBF_XS_JUMP, x0, k))
+				return fail (-5, "nibble-sliced jump differs from the bit-row jump");
+			o[0] = r;
 			o[1] = x;
 		}
 	}

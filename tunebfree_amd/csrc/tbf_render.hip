@@ -57,6 +57,9 @@
 #ifndef XS_NIB
 #define XS_NIB 1 /* dither jumps from the nibble-sliced table: 8 coalesced loads per state */
 #endif
+#ifndef RVIN_IPW
+#define RVIN_IPW 2 /* k_rv_in instances per wave (their biquadA chains share one serial pass) */
+#endif
 #ifndef RV_TAP_UNROLL
 #define RV_TAP_UNROLL 2 /* k_rv_core delay lines whose taps are computed together */
 #endif
@@ -749,10 +752,11 @@ __device__ __forceinline__ void rv_dither (const uint32_t* __restrict__ J, const
 	__syncthreads ();
 }
 
+template <int IPW>
 struct RvInLds {
-	RvHeadLds    hd;
-	double       a[2][TBF_SUB + RV_PAD];
-	uint32_t     fpd[2][TBF_SUB + 1];
+	RvHeadLds    hd[IPW];
+	double       a[IPW][2][TBF_SUB + RV_PAD];
+	uint32_t     fpd[IPW][2][TBF_SUB + 1];
 	TBF_PROF_LDS
 };
 
@@ -781,33 +785,32 @@ __device__ __forceinline__ double* rv_buf (double* base, const tbf_launch& P, ui
 	return base + ((size_t)inst * 2 + c) * P.midStride;
 }
 
+/* k_rv_in, IPW instances per wave: the biquadA chains of all IPW instances' channels run
+ * in one serial pass (lanes 0 .. 2 IPW - 1), so a pass's FP64 instructions serve 2 IPW
+ * chains instead of 2; the lane-parallel parts loop over the instances */
+template <int IPW>
 __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL), amdgpu_waves_per_eu (RVIO_WAVES)))
 k_rv_in (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_seg_ctl* __restrict__ ctl)
 {
-	__shared__ RvInLds sm;
-	const int      lane = threadIdx.x;
-	const uint32_t inst = blockIdx.x + P.instBase;
-	if (inst >= P.nInst)
+	__shared__ RvInLds<IPW> sm;
+	const int      lane  = threadIdx.x;
+	const uint32_t inst0 = blockIdx.x * IPW + P.instBase;
+	if (inst0 >= P.nInst)
 		return;
-	const tbf_inst_const& K    = cst[inst];
-	tbf_rv_state*         S    = &P.st[inst].rv;
-	double*               mL   = P.rslab + (size_t)inst * P.slabLen + K.ringOff[12];
-	double*               mR   = P.rslab + (size_t)inst * P.slabLen + K.ringOff[13 + 12];
-	const int             dM   = K.delay[12];
-	double*               a0L  = rv_buf (P.rvA, P, inst, 0);
-	double*               a0R  = rv_buf (P.rvA, P, inst, 1);
+	const int nj = (int)min ((uint32_t)IPW, P.nInst - inst0); /* instances of this wave */
 	prof_begin (P, sm);
-	copy_head (&sm.hd.get (), S);
+#pragma unroll
+	for (int j = 0; j < IPW; j++)
+		if (j < nj)
+			copy_head (&sm.hd[j].get (), &P.st[inst0 + j].rv);
 	__syncthreads ();
-	tbf_rv_state& st = sm.hd.get ();
 	/* software-pipelined: the predelay reads and the input of sub-block g+1 are issued
 	 * before sub-block g's writes and serial chain, so their latency overlaps it (the
 	 * reads lie at count+65 .. count+128, the writes at count .. count+63, and the ring
 	 * holds >= 561 slots) */
-	const float*   inBase = P.mid1 + (size_t)inst * P.midStride;
-	const uint32_t nSub   = P.nBlocks * (TBF_BLK / TBF_SUB);
-	double         pL = 0.0, pR = 0.0;
-	float          pIn = 0.f;
+	const uint32_t nSub = P.nBlocks * (TBF_BLK / TBF_SUB);
+	double         pL[IPW], pR[IPW];
+	float          pIn[IPW];
 #if XS_NIB
 	const uint32_t* jr = nullptr;
 #else
@@ -816,61 +819,106 @@ k_rv_in (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 	for (int j = 0; j < 32; j++)
 		jr[j] = P.xsJump[j * TBF_XS_JUMP + lane + 1];
 #endif
-	if (nSub > 0) {
-		const int cMr = cnt_adv (st.countM, dM, lane + 1);
-		pL            = mL[cMr];
-		pR            = mR[cMr];
-		pIn           = inBase[lane];
+#pragma unroll
+	for (int j = 0; j < IPW; j++) {
+		pL[j] = pR[j] = 0.0;
+		pIn[j]        = 0.f;
+		const uint32_t        inst = inst0 + j;
+		const tbf_inst_const& K    = cst[inst];
+		if (j < nj && nSub > 0) {
+			const double* slab = P.rslab + (size_t)inst * P.slabLen;
+			const int     cMr  = cnt_adv (sm.hd[j].get ().countM, K.delay[12], lane + 1);
+			pL[j]              = slab[K.ringOff[12] + cMr];
+			pR[j]              = slab[K.ringOff[13 + 12] + cMr];
+			pIn[j]             = P.mid1[(size_t)inst * P.midStride + lane];
+		}
 	}
+	/* serial lane roles: instance lane >> 1, channel lane & 1 */
+	const int     sj  = min (lane >> 1, IPW - 1), sc = lane & 1;
+	const double* scf = cst[inst0 + min (sj, nj - 1)].bq[0];
 #pragma unroll 1
 	for (uint32_t g = 0; g < nSub; g++) {
 		const uint32_t blk = g / (TBF_BLK / TBF_SUB), sb = g % (TBF_BLK / TBF_SUB);
-		const double   wet = ctl_of (P, ctl, blk, inst).rvWet;
 		const int      n   = lane;
-		rv_dither (P.xsJump, jr, st.fpdL, st.fpdR, sm.fpd);
+#pragma unroll
+		for (int j = 0; j < IPW; j++)
+			if (j < nj)
+				rv_dither (P.xsJump, jr, sm.hd[j].get ().fpdL, sm.hd[j].get ().fpdR, sm.fpd[j]);
 		TBF_MARK (5);
-		const double inS = (double)pIn;
-		/* predelay M (src/reverb.cpp:350-358): write at count, read at count + 1 */
-		const int cMn = cnt_adv (st.countM, dM, n);
-		sm.a[0][n]    = pL;
-		sm.a[1][n]    = pR;
-		if (g + 1 < nSub) {
-			const int cMr = cnt_adv (st.countM, dM, TBF_SUB + n + 1);
-			pL            = mL[cMr];
-			pR            = mR[cMr];
-			pIn           = inBase[(size_t)(g + 1) * TBF_SUB + n];
+		float inS[IPW];
+#pragma unroll
+		for (int j = 0; j < IPW; j++) {
+			inS[j]         = pIn[j];
+			sm.a[j][0][n] = pL[j];
+			sm.a[j][1][n] = pR[j];
+			if (j < nj && g + 1 < nSub) {
+				const uint32_t        inst = inst0 + j;
+				const tbf_inst_const& K    = cst[inst];
+				const double*         slab = P.rslab + (size_t)inst * P.slabLen;
+				const int cMr = cnt_adv (sm.hd[j].get ().countM, K.delay[12], TBF_SUB + n + 1);
+				pL[j]         = slab[K.ringOff[12] + cMr];
+				pR[j]         = slab[K.ringOff[13 + 12] + cMr];
+				pIn[j]        = P.mid1[(size_t)inst * P.midStride + (size_t)(g + 1) * TBF_SUB + n];
+			}
 		}
 		__syncthreads (); /* every read of the sub-block precedes its writes */
 #pragma unroll
-		for (int c = 0; c < 2; c++) {
-			double x = inS;
-			if (fabs (x) < 1.18e-23)
-				x = sm.fpd[c][n] * 1.18e-17;
-			stream_st (&(c ? mR : mL)[cMn], x);
+		for (int j = 0; j < IPW; j++) {
+			if (j >= nj)
+				continue;
+			/* predelay M (src/reverb.cpp:350-358): write at count, read at count + 1 */
+			const uint32_t        inst = inst0 + j;
+			const tbf_inst_const& K    = cst[inst];
+			double*               slab = P.rslab + (size_t)inst * P.slabLen;
+			const int             cMn  = cnt_adv (sm.hd[j].get ().countM, K.delay[12], n);
+#pragma unroll
+			for (int c = 0; c < 2; c++) {
+				double x = (double)inS[j];
+				if (fabs (x) < 1.18e-23)
+					x = sm.fpd[j][c][n] * 1.18e-17;
+				stream_st (&slab[K.ringOff[13 * c + 12] + cMn], x);
+			}
 		}
-		/* biquadA, both channels: lanes 0, 1 */
-		if (lane < 2)
-			rv_chain (K.bq[0], st.bq[0][2 * lane], st.bq[0][2 * lane + 1], sm.a[lane]);
+		/* biquadA, every instance and channel: lanes 0 .. 2 IPW - 1 */
+		if (lane < 2 * nj) {
+			tbf_rv_state& ss = sm.hd[sj].get ();
+			rv_chain (scf, ss.bq[0][2 * sc], ss.bq[0][2 * sc + 1], sm.a[sj][sc]);
+		}
 		__syncthreads ();
 		TBF_MARK (6);
-		const size_t o = (size_t)blk * TBF_BLK + sb * TBF_SUB + n;
-		stream_st (&a0L[o], sin (sm.a[0][n] * wet));
-		stream_st (&a0R[o], sin (sm.a[1][n] * wet));
-		if (lane == 0)
-			st.countM = cnt_adv (st.countM, dM, TBF_SUB);
+#pragma unroll
+		for (int j = 0; j < IPW; j++) {
+			if (j >= nj)
+				continue;
+			const uint32_t inst = inst0 + j;
+			const double   wet  = ctl_of (P, ctl, blk, inst).rvWet;
+			const size_t   o    = (size_t)blk * TBF_BLK + sb * TBF_SUB + n;
+			stream_st (&rv_buf (P.rvA, P, inst, 0)[o], sin (sm.a[j][0][n] * wet));
+			stream_st (&rv_buf (P.rvA, P, inst, 1)[o], sin (sm.a[j][1][n] * wet));
+		}
+		__syncthreads ();
+		if (lane < nj) {
+			tbf_rv_state& ss = sm.hd[lane].get ();
+			ss.countM        = cnt_adv (ss.countM, cst[inst0 + lane].delay[12], TBF_SUB);
+		}
 		__syncthreads ();
 		TBF_MARK (7);
 	}
 	__syncthreads ();
-	if (lane == 0) { /* only k_rv_in's own fields: the other reverb kernels of neighbouring
+	if (lane < nj) { /* only k_rv_in's own fields: the other reverb kernels of neighbouring
 	                  * chunks may run concurrently (cross-chunk pipelining) */
-		S->countM = st.countM;
-		S->fpdL   = st.fpdL;
-		S->fpdR   = st.fpdR;
-		for (int j = 0; j < 4; j++)
-			S->bq[0][j] = st.bq[0][j];
+		const tbf_rv_state& ss = sm.hd[lane].get ();
+		tbf_rv_state*       S  = &P.st[inst0 + lane].rv;
+		S->countM              = ss.countM;
+		S->fpdL                = ss.fpdL;
+		S->fpdR                = ss.fpdR;
+		for (int q = 0; q < 4; q++)
+			S->bq[0][q] = ss.bq[0][q];
 	}
-	prof_end (P, sm, inst);
+#pragma unroll
+	for (int j = 0; j < IPW; j++) /* each instance's slots get the wave's stage times */
+		if (j < nj)
+			prof_end (P, sm, inst0 + j);
 }
 
 /* One channel of the feedback network, 64-sample sub-blocks: allpasses I..L (lines
@@ -1895,7 +1943,8 @@ extern "C" int tbf_launch_stage (const tbf_launch* P, int k, hipStream_t stream)
 	if (k == 0)
 		hipLaunchKernelGGL (k_tonegen, grid, block, 0, stream, *P, P->ctl, P->tpls, P->cst);
 	else if (k == 1)
-		hipLaunchKernelGGL (k_rv_in, grid, block, 0, stream, *P, P->cst, P->ctl);
+		hipLaunchKernelGGL (k_rv_in<RVIN_IPW>, dim3 ((P->nInst + RVIN_IPW - 1) / RVIN_IPW), block, 0, stream, *P, P->cst,
+		                    P->ctl);
 	else if (k == 2)
 		hipLaunchKernelGGL (k_rv_core, dim3 (2 * P->nInst), block, 0, stream, *P, P->cst);
 	else if (k == 3)

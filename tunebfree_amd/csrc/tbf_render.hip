@@ -60,6 +60,9 @@
 #ifndef RVIN_IPW
 #define RVIN_IPW 2 /* k_rv_in instances per wave (their biquadA chains share one serial pass) */
 #endif
+#ifndef RVOUT_IPW
+#define RVOUT_IPW 2 /* k_rv_out instances per wave (their biquadB/C chains share one serial pass) */
+#endif
 #ifndef RV_TAP_UNROLL
 #define RV_TAP_UNROLL 2 /* k_rv_core delay lines whose taps are computed together */
 #endif
@@ -760,11 +763,12 @@ struct RvInLds {
 	TBF_PROF_LDS
 };
 
+template <int IPW>
 struct RvOutLds {
-	RvHeadLds    hd;
-	double       bx[2][TBF_BLK + RV_PAD]; /* block b: tap mix -> biquadB output */
-	double       cx[2][TBF_BLK + RV_PAD]; /* block b-1: asin output -> biquadC output */
-	uint32_t     fpd[2][TBF_BLK + 1];
+	RvHeadLds    hd[IPW];
+	double       bx[IPW][2][TBF_BLK + RV_PAD]; /* block b: tap mix -> biquadB output */
+	double       cx[IPW][2][TBF_BLK + RV_PAD]; /* block b-1: asin output -> biquadC output */
+	uint32_t     fpd[IPW][2][TBF_BLK + 1];
 	TBF_PROF_LDS
 };
 
@@ -1205,28 +1209,29 @@ k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 
 /* k_rv_out: biquadB -> clamp + asin -> biquadC -> dry mix, dither, (L+R)/sqrt2, in
  * 128-sample blocks, software-pipelined so biquadB of block b and biquadC of block b-1
- * advance in the same serial instruction stream (lanes 0,1: B of L,R; lanes 2,3: C of
- * L,R).  One serial pass per block instead of two. */
-__global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL), amdgpu_waves_per_eu (RVIO_WAVES)))
+ * advance in the same serial instruction stream (lane 4j + 2q + c: instance j of the
+ * wave, q = 0 B / 1 C, channel c).  One serial pass per block serves the 4 IPW chains of
+ * the wave's IPW instances; the lane-parallel parts loop over the instances. */
+template <int IPW>
+__global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL), amdgpu_waves_per_eu (RVIO_WAVES / IPW)))
 k_rv_out (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_seg_ctl* __restrict__ ctl)
 {
-	__shared__ RvOutLds sm;
-	const int      lane = threadIdx.x;
-	const uint32_t inst = blockIdx.x + P.instBase;
-	if (inst >= P.nInst)
+	__shared__ RvOutLds<IPW> sm;
+	const int      lane  = threadIdx.x;
+	const uint32_t inst0 = blockIdx.x * IPW + P.instBase;
+	if (inst0 >= P.nInst)
 		return;
-	const tbf_inst_const& K   = cst[inst];
-	tbf_rv_state*         S   = &P.st[inst].rv;
-	const double*         bL  = rv_buf (P.rvB, P, inst, 0);
-	const double*         bR  = rv_buf (P.rvB, P, inst, 1);
-	const bool            tap = P.chain == TBF_CHAIN_TAP_REVERB;
+	const int  nj  = (int)min ((uint32_t)IPW, P.nInst - inst0); /* instances of this wave */
+	const bool tap = P.chain == TBF_CHAIN_TAP_REVERB;
 	prof_begin (P, sm);
-	copy_head (&sm.hd.get (), S);
+#pragma unroll
+	for (int j = 0; j < IPW; j++)
+		if (j < nj)
+			copy_head (&sm.hd[j].get (), &P.st[inst0 + j].rv);
 	__syncthreads ();
-	tbf_rv_state& st = sm.hd.get ();
-	/* serial lane roles: q = 0 biquadB, 1 biquadC; c = channel */
-	const int     q   = (lane >> 1) & 1, c = lane & 1;
-	const double* cf  = K.bq[1 + q];
+	/* serial lane roles */
+	const int     sj = min (lane >> 2, IPW - 1), q = (lane >> 1) & 1, c = lane & 1;
+	const double* cf = cst[inst0 + min (sj, nj - 1)].bq[1 + q];
 	const double  c0 = cf[0], c1 = cf[1], c2 = cf[2], c3 = cf[3], c4 = cf[4];
 	/* software-pipelined loads: the tap mix of block it+1 and the dry input of block it-1
 	 * are issued before block it's serial pass and consumed after it */
@@ -1236,41 +1241,57 @@ k_rv_out (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 	for (int j = 0; j < 32; j++)
 		jr[j] = P.xsJump[j * TBF_XS_JUMP + lane + 1];
 #endif
-	double pb[4] = {0.0, 0.0, 0.0, 0.0};
-	if (P.nBlocks > 0) {
-		pb[0] = bL[lane];
-		pb[1] = bL[lane + NL];
-		pb[2] = bR[lane];
-		pb[3] = bR[lane + NL];
+	double pb[IPW][4];
+#pragma unroll
+	for (int j = 0; j < IPW; j++) {
+		pb[j][0] = pb[j][1] = pb[j][2] = pb[j][3] = 0.0;
+		if (j < nj && P.nBlocks > 0) {
+			const double* bL = rv_buf (P.rvB, P, inst0 + j, 0);
+			const double* bR = rv_buf (P.rvB, P, inst0 + j, 1);
+			pb[j][0]         = bL[lane];
+			pb[j][1]         = bL[lane + NL];
+			pb[j][2]         = bR[lane];
+			pb[j][3]         = bR[lane + NL];
+		}
 	}
 	for (uint32_t it = 0; it <= P.nBlocks; it++) {
 		const bool haveB = it < P.nBlocks, haveC = it > 0;
-		/* (a) tap mix of block `it` */
-		if (haveB) {
-			sm.bx[0][lane]      = pb[0];
-			sm.bx[0][lane + NL] = pb[1];
-			sm.bx[1][lane]      = pb[2];
-			sm.bx[1][lane + NL] = pb[3];
-			if (it + 1 < P.nBlocks) {
-				const size_t o = (size_t)(it + 1) * TBF_BLK;
-				pb[0]          = bL[o + lane];
-				pb[1]          = bL[o + lane + NL];
-				pb[2]          = bR[o + lane];
-				pb[3]          = bR[o + lane + NL];
+		float      pIn[IPW][2];
+#pragma unroll
+		for (int j = 0; j < IPW; j++) {
+			pIn[j][0] = pIn[j][1] = 0.f;
+			if (j >= nj)
+				continue;
+			const uint32_t inst = inst0 + j;
+			/* (a) tap mix of block `it` */
+			if (haveB) {
+				sm.bx[j][0][lane]      = pb[j][0];
+				sm.bx[j][0][lane + NL] = pb[j][1];
+				sm.bx[j][1][lane]      = pb[j][2];
+				sm.bx[j][1][lane + NL] = pb[j][3];
+				if (it + 1 < P.nBlocks) {
+					const double* bL = rv_buf (P.rvB, P, inst, 0);
+					const double* bR = rv_buf (P.rvB, P, inst, 1);
+					const size_t  o  = (size_t)(it + 1) * TBF_BLK;
+					pb[j][0]         = bL[o + lane];
+					pb[j][1]         = bL[o + lane + NL];
+					pb[j][2]         = bR[o + lane];
+					pb[j][3]         = bR[o + lane + NL];
+				}
 			}
-		}
-		float pIn[2] = {0.f, 0.f};
-		if (haveC) {
-			const float* in = P.mid1 + (size_t)inst * P.midStride + (size_t)(it - 1) * TBF_BLK;
-			pIn[0]          = in[lane];
-			pIn[1]          = in[lane + NL];
+			if (haveC) {
+				const float* in = P.mid1 + (size_t)inst * P.midStride + (size_t)(it - 1) * TBF_BLK;
+				pIn[j][0]       = in[lane];
+				pIn[j][1]       = in[lane + NL];
+			}
 		}
 		__syncthreads ();
 		TBF_MARK (10);
-		/* (b) serial: B over block it (lanes 0,1), C over block it-1 (lanes 2,3) */
-		if (lane < 4 && (q == 0 ? haveB : haveC)) {
-			double* row = q == 0 ? sm.bx[c] : sm.cx[c];
-			double  s7 = st.bq[1 + q][2 * c], s8 = st.bq[1 + q][2 * c + 1];
+		/* (b) serial: B over block it (q = 0), C over block it-1 (q = 1) */
+		if (lane < 4 * nj && (q == 0 ? haveB : haveC)) {
+			tbf_rv_state& ss  = sm.hd[sj].get ();
+			double*       row = q == 0 ? sm.bx[sj][c] : sm.cx[sj][c];
+			double        s7 = ss.bq[1 + q][2 * c], s8 = ss.bq[1 + q][2 * c + 1];
 			for (int i0 = 0; i0 < TBF_BLK; i0 += 8) {
 				double xv[8];
 #pragma unroll
@@ -1285,59 +1306,71 @@ k_rv_out (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 					row[i0 + k]    = t;
 				}
 			}
-			st.bq[1 + q][2 * c]     = s7;
-			st.bq[1 + q][2 * c + 1] = s8;
+			ss.bq[1 + q][2 * c]     = s7;
+			ss.bq[1 + q][2 * c + 1] = s8;
 		}
 		__syncthreads ();
 		TBF_MARK (11);
 		/* (c) output of block it-1: dry mix, dither, mono sum (src/reverb.cpp:766-787) */
 		if (haveC) {
-			const uint32_t ob  = it - 1;
-			const double   wet = ctl_of (P, ctl, ob, inst).rvWet;
-			/* dither states F[0..128] of both streams for the block */
-			const uint32_t gL = st.fpdL2, gR = st.fpdR2;
+			const uint32_t ob = it - 1;
+			/* dither states F[0..128] of both streams of every instance for the block */
+#pragma unroll
+			for (int j = 0; j < IPW; j++) {
+				if (j >= nj)
+					continue;
+				const tbf_rv_state& ss = sm.hd[j].get ();
 #if XS_NIB
-			sm.fpd[0][lane + 1]      = xs_jump_n (P.xsJump, gL, lane + 1);
-			sm.fpd[1][lane + 1]      = xs_jump_n (P.xsJump, gR, lane + 1);
-			sm.fpd[0][lane + 1 + NL] = xs_jump_n (P.xsJump, gL, lane + 1 + NL);
-			sm.fpd[1][lane + 1 + NL] = xs_jump_n (P.xsJump, gR, lane + 1 + NL);
+				sm.fpd[j][0][lane + 1]      = xs_jump_n (P.xsJump, ss.fpdL2, lane + 1);
+				sm.fpd[j][1][lane + 1]      = xs_jump_n (P.xsJump, ss.fpdR2, lane + 1);
+				sm.fpd[j][0][lane + 1 + NL] = xs_jump_n (P.xsJump, ss.fpdL2, lane + 1 + NL);
+				sm.fpd[j][1][lane + 1 + NL] = xs_jump_n (P.xsJump, ss.fpdR2, lane + 1 + NL);
 #else
-			const uint32_t l1 = xs_jump_reg (jr, gL), r1 = xs_jump_reg (jr, gR);
-			sm.fpd[0][lane + 1]      = l1;
-			sm.fpd[1][lane + 1]      = r1;
-			sm.fpd[0][lane + 1 + NL] = xs_jump_u (P.xsJump, l1, NL);
-			sm.fpd[1][lane + 1 + NL] = xs_jump_u (P.xsJump, r1, NL);
+				const uint32_t l1 = xs_jump_reg (jr, ss.fpdL2), r1 = xs_jump_reg (jr, ss.fpdR2);
+				sm.fpd[j][0][lane + 1]      = l1;
+				sm.fpd[j][1][lane + 1]      = r1;
+				sm.fpd[j][0][lane + 1 + NL] = xs_jump_u (P.xsJump, l1, NL);
+				sm.fpd[j][1][lane + 1 + NL] = xs_jump_u (P.xsJump, r1, NL);
 #endif
-			__syncthreads ();
-			if (lane == 0) {
-				sm.fpd[0][0] = gL;
-				sm.fpd[1][0] = gR;
-				st.fpdL2     = sm.fpd[0][TBF_BLK];
-				st.fpdR2     = sm.fpd[1][TBF_BLK];
+			}
+			__syncthreads (); /* all lanes have read the states */
+			if (lane < nj) {
+				tbf_rv_state& ss    = sm.hd[lane].get ();
+				sm.fpd[lane][0][0] = ss.fpdL2;
+				sm.fpd[lane][1][0] = ss.fpdR2;
+				ss.fpdL2           = sm.fpd[lane][0][TBF_BLK];
+				ss.fpdR2           = sm.fpd[lane][1][TBF_BLK];
 			}
 			__syncthreads ();
-			float*       out = tap ? P.outL + (size_t)inst * P.outStride + P.outOffset + (size_t)ob * TBF_BLK
-			                       : P.mid2 + (size_t)inst * P.midStride + (size_t)ob * TBF_BLK;
 #pragma unroll
-			for (int h = 0; h < 2; h++) {
-				const int    n   = lane + h * NL;
-				const double inS = (double)pIn[h];
-				double       ov[2];
+			for (int j = 0; j < IPW; j++) {
+				if (j >= nj)
+					continue;
+				const uint32_t inst = inst0 + j;
+				const double   wet  = ctl_of (P, ctl, ob, inst).rvWet;
+				float*         out  = tap ? P.outL + (size_t)inst * P.outStride + P.outOffset + (size_t)ob * TBF_BLK
+				                          : P.mid2 + (size_t)inst * P.midStride + (size_t)ob * TBF_BLK;
 #pragma unroll
-				for (int cc = 0; cc < 2; cc++) {
-					double x = sm.cx[cc][n];
-					if (wet != 1.0) {
-						double dry = inS;
-						if (fabs (dry) < 1.18e-23)
-							dry = sm.fpd[cc][n] * 1.18e-17;
-						x += (dry * (1.0 - wet));
+				for (int h = 0; h < 2; h++) {
+					const int    n   = lane + h * NL;
+					const double inS = (double)pIn[j][h];
+					double       ov[2];
+#pragma unroll
+					for (int cc = 0; cc < 2; cc++) {
+						double x = sm.cx[j][cc][n];
+						if (wet != 1.0) {
+							double dry = inS;
+							if (fabs (dry) < 1.18e-23)
+								dry = sm.fpd[j][cc][n] * 1.18e-17;
+							x += (dry * (1.0 - wet));
+						}
+						ov[cc] = dither_add (x, sm.fpd[j][cc][n + 1]);
 					}
-					ov[cc] = dither_add (x, sm.fpd[cc][n + 1]);
+					const float y = (float)(0.7071067811865476 * (ov[0] + ov[1]));
+					stream_st (&out[n], y);
+					if (tap)
+						P.outR[(size_t)inst * P.outStride + P.outOffset + (size_t)ob * TBF_BLK + n] = y;
 				}
-				const float y = (float)(0.7071067811865476 * (ov[0] + ov[1]));
-				stream_st (&out[n], y);
-				if (tap)
-					P.outR[(size_t)inst * P.outStride + P.outOffset + (size_t)ob * TBF_BLK + n] = y;
 			}
 		}
 		__syncthreads ();
@@ -1346,28 +1379,38 @@ k_rv_out (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 		 * (src/reverb.cpp:743-751) */
 		if (haveB) {
 #pragma unroll
-			for (int h = 0; h < 2; h++)
+			for (int j = 0; j < IPW; j++) {
+				if (j >= nj)
+					continue;
 #pragma unroll
-				for (int cc = 0; cc < 2; cc++) {
-					const int n = lane + h * NL;
-					double    y = sm.bx[cc][n];
-					if (y > 1.0) y = 1.0;
-					if (y < -1.0) y = -1.0;
-					sm.cx[cc][n] = asin (y);
-				}
+				for (int h = 0; h < 2; h++)
+#pragma unroll
+					for (int cc = 0; cc < 2; cc++) {
+						const int n = lane + h * NL;
+						double    y = sm.bx[j][cc][n];
+						if (y > 1.0) y = 1.0;
+						if (y < -1.0) y = -1.0;
+						sm.cx[j][cc][n] = asin (y);
+					}
+			}
 		}
 		__syncthreads ();
 		TBF_MARK (13);
 	}
-	if (lane == 0) { /* only k_rv_out's own fields (see k_rv_in) */
-		S->fpdL2 = st.fpdL2;
-		S->fpdR2 = st.fpdR2;
-		for (int j = 0; j < 4; j++) {
-			S->bq[1][j] = st.bq[1][j];
-			S->bq[2][j] = st.bq[2][j];
+	if (lane < nj) { /* only k_rv_out's own fields (see k_rv_in) */
+		const tbf_rv_state& ss = sm.hd[lane].get ();
+		tbf_rv_state*       S  = &P.st[inst0 + lane].rv;
+		S->fpdL2               = ss.fpdL2;
+		S->fpdR2               = ss.fpdR2;
+		for (int k = 0; k < 4; k++) {
+			S->bq[1][k] = ss.bq[1][k];
+			S->bq[2][k] = ss.bq[2][k];
 		}
 	}
-	prof_end (P, sm, inst);
+#pragma unroll
+	for (int j = 0; j < IPW; j++)
+		if (j < nj)
+			prof_end (P, sm, inst0 + j);
 }
 
 /* ================================================================== k_whirl */
@@ -1948,7 +1991,8 @@ extern "C" int tbf_launch_stage (const tbf_launch* P, int k, hipStream_t stream)
 	else if (k == 2)
 		hipLaunchKernelGGL (k_rv_core, dim3 (2 * P->nInst), block, 0, stream, *P, P->cst);
 	else if (k == 3)
-		hipLaunchKernelGGL (k_rv_out, grid, block, 0, stream, *P, P->cst, P->ctl);
+		hipLaunchKernelGGL (k_rv_out<RVOUT_IPW>, dim3 ((P->nInst + RVOUT_IPW - 1) / RVOUT_IPW), block, 0, stream, *P,
+		                    P->cst, P->ctl);
 	else if (k == 4) {
 		switch (P->wringLen) {
 			case 512: hipLaunchKernelGGL (k_whirl<512>, grid, block, 0, stream, *P, P->cst, P->ctl); break;

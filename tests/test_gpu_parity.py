@@ -61,6 +61,24 @@ def test_gpu_full_chain_bench(oracle):
     assert max(eL, eR) <= TOL
 
 
+def test_gpu_full_chain_odd_batch_mixed_scenarios(oracle):
+    """k_rv_in and k_rv_out serve two instances per wave: an odd batch leaves the last
+    wave with one, and neighbouring instances with different scripts (events, a quiet
+    one, reverb-heavy) must not leak into each other."""
+    def scen(i):
+        if i == 2:
+            return []  # silent instance between two playing ones
+        return S.event_scenario(i) if i % 2 else S.bench_scenario(i)
+    eng, tpl, seeds, scens = _setup(oracle, 5, scen)
+    L, R = engine_run(eng, scens, 40)
+    oL, oR, *_ = oracle_run(oracle, tpl, seeds, scens, 40)
+    eL, xL = compare(L, oL)
+    eR, xR = compare(R, oR)
+    print(f"odd batch: max|err| L={eL:.3g} R={eR:.3g} bit-exact L={xL:.6f} R={xR:.6f}")
+    assert max(eL, eR) <= TOL
+    assert float(np.abs(L[1]).max()) > 1e-3 and float(np.abs(L[3]).max()) > 1e-3
+
+
 def test_gpu_full_chain_events(oracle):
     eng, tpl, seeds, scens = _setup(oracle, 6, S.event_scenario)
     L, R = engine_run(eng, scens, 72)

@@ -119,15 +119,19 @@ def setup_instances(eng, wl, first_global, n):
 
 
 def _cpu_worker(args):
-    """Oracle (CPU restatement) render of a slice of instances; returns samples and seconds."""
-    idx, blocks, sr = args
+    """CPU render of a slice of instances; returns samples and seconds.  kind "reference":
+    the reference's own tonegen/vibrato/overdrive/reverb/whirl translation units compiled
+    by oracle/Makefile (oracle/_ref/libtbfref.so), driven like synthSound; kind "port":
+    the oracle's C restatement."""
+    idx, blocks, sr, kind = args
     import scenarios as S
-    from orc_bind import Chain, Template, load_oracle
+    from orc_bind import Chain, Template, load_oracle, load_ref
     lib = load_oracle()
+    ref = load_ref() if kind == "reference" else None
     tpl = Template(lib, sr=sr, seed=7)
     chains = []
     for i in idx:
-        ch = Chain(lib, tpl, 1000 + i)
+        ch = Chain(ref, tpl, 1000 + i, ref=True) if ref is not None else Chain(lib, tpl, 1000 + i)
         for (_, kind, a, v) in S.bench_scenario(i):
             (ch.note if kind == "note" else ch.param)(a, v)
         chains.append(ch)
@@ -139,6 +143,7 @@ def _cpu_worker(args):
 
 def cpu_baseline(n_inst, blocks, sr):
     import multiprocessing as mp
+    kind = "reference" if (ROOT / "oracle" / "_ref" / "libtbfref.so").exists() else "port"
     try:
         cores = len(os.sched_getaffinity(0))
     except AttributeError:
@@ -148,13 +153,15 @@ def cpu_baseline(n_inst, blocks, sr):
     ctx = mp.get_context("spawn")
     t0 = time.perf_counter()
     with ctx.Pool(cores) as pool:
-        res = pool.map(_cpu_worker, [(p, blocks, sr) for p in parts])
+        res = pool.map(_cpu_worker, [(p, blocks, sr, kind) for p in parts])
     wall = time.perf_counter() - t0
     samples = sum(r[0] for r in res)
     busy = max(r[1] for r in res)  # render time of the slowest worker (construction excluded)
-    return {"value": samples / busy, "unit": "stereo samples/s", "cores": cores, "kind": "port",
+    what = ("the reference's src/tonegen.cpp, vibrato.cpp, overdrive.cpp, reverb.cpp, whirl.cpp "
+            "compiled by oracle/Makefile (gcc -O2)" if kind == "reference" else "oracle/ C restatement")
+    return {"value": samples / busy, "unit": "stereo samples/s", "cores": cores, "kind": kind,
             "sample": f"{n_inst} instances x {blocks} blocks ({blocks * 128 / sr:.2f} s audio each), "
-                      f"oracle/ C restatement, {cores} processes, construction excluded (wall {wall:.1f}s)"}
+                      f"{what}, {cores} processes, construction excluded (wall {wall:.1f}s)"}
 
 
 def oracle_check(wl, rank_first, n_check, total_blocks, last_blocks, gpu_L, gpu_R):

@@ -63,6 +63,19 @@
 #ifndef RVOUT_IPW
 #define RVOUT_IPW 2 /* k_rv_out instances per wave (their biquadB/C chains share one serial pass) */
 #endif
+#ifndef SERIAL_PRIO
+#define SERIAL_PRIO 1 /* wave priority raised (s_setprio) while a wave runs a serial chain */
+#endif
+#define PRIO_UP()                                  \
+	do {                                           \
+		if (SERIAL_PRIO)                           \
+			__builtin_amdgcn_s_setprio (SERIAL_PRIO); \
+	} while (0)
+#define PRIO_DOWN()                        \
+	do {                                   \
+		if (SERIAL_PRIO)                   \
+			__builtin_amdgcn_s_setprio (0); \
+	} while (0)
 #ifndef RV_TAP_UNROLL
 #define RV_TAP_UNROLL 2 /* k_rv_core delay lines whose taps are computed together */
 #endif
@@ -502,6 +515,7 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 	TBF_MARK (1);
 	/* mixdown, src/tonegen.cpp:3712-3777: the two per-sample gain chases run as
 	 * independent chains, lane 0 keyCompLevel += delta, lane 1 percEnvGain *= decay */
+	PRIO_UP ();
 	if (lane < 2) {
 		const float keyCompDelta = (G.keyCompTarget - st.keyCompLevel) / (float)TBF_BLK;
 		const bool  perc         = (routing & 0x0C) != 0;
@@ -526,6 +540,7 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 		else
 			st.percEnvGain = G.resetPercAtEnd ? G.percEnvGainReset : v;
 	}
+	PRIO_DOWN ();
 	__syncthreads ();
 	for (int k = 0; k < 2; k++) {
 		const int   n = lane + k * NL;
@@ -589,6 +604,7 @@ __device__ void stage_overdrive (const tbf_launch& P, TgLds& sm, const tbf_seg_c
 		sm.u.od.odx[n] = x;
 	}
 	__syncthreads ();
+	PRIO_UP ();
 	if (lane < 2) {
 		/* alternating one-pole HPF (fpFlip): lane 0 carries iirSampleA over the samples it
 		 * owns, lane 1 iirSampleB over the others; 128 samples keep fpFlip unchanged */
@@ -611,6 +627,7 @@ __device__ void stage_overdrive (const tbf_launch& P, TgLds& sm, const tbf_seg_c
 		else
 			st.iirB = iir;
 	}
+	PRIO_DOWN ();
 	__syncthreads ();
 	TBF_MARK (3);
 	for (int k = 0; k < 2; k++) {
@@ -884,10 +901,12 @@ k_rv_in (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 			}
 		}
 		/* biquadA, every instance and channel: lanes 0 .. 2 IPW - 1 */
+		PRIO_UP ();
 		if (lane < 2 * nj) {
 			tbf_rv_state& ss = sm.hd[sj].get ();
 			rv_chain (scf, ss.bq[0][2 * sc], ss.bq[0][2 * sc + 1], sm.a[sj][sc]);
 		}
+		PRIO_DOWN ();
 		__syncthreads ();
 		TBF_MARK (6);
 #pragma unroll
@@ -1288,6 +1307,7 @@ k_rv_out (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 		__syncthreads ();
 		TBF_MARK (10);
 		/* (b) serial: B over block it (q = 0), C over block it-1 (q = 1) */
+		PRIO_UP ();
 		if (lane < 4 * nj && (q == 0 ? haveB : haveC)) {
 			tbf_rv_state& ss  = sm.hd[sj].get ();
 			double*       row = q == 0 ? sm.bx[sj][c] : sm.cx[sj][c];
@@ -1309,6 +1329,7 @@ k_rv_out (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 			ss.bq[1 + q][2 * c]     = s7;
 			ss.bq[1 + q][2 * c + 1] = s8;
 		}
+		PRIO_DOWN ();
 		__syncthreads ();
 		TBF_MARK (11);
 		/* (c) output of block it-1: dry mix, dither, mono sum (src/reverb.cpp:766-787) */
@@ -1703,11 +1724,13 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 			sm.aOut[n]      = (T0[n + 2] * K.hafw[2]) + (K.hafw[3] * T0[n + 1]) + (K.hafw[4] * T0[n]);
 			__syncthreads ();
 		}
+		PRIO_UP ();
 		if (lane < 4 && (lane > 0 || aNext)) {
 			const float* ip = lane == 0 ? sm.xn : (lane == 1 ? sm.aOut : sm.rd[lane - 2]);
 			/* crossing into the next block: A's state gets that block's NaN scrub first */
 			wh_serial (ip, sm.tmp[lane], st.fz[lane], fa0, fa1, lane == 0 && sb + 1 == TBF_BLK / TBF_SUB);
 		}
+		PRIO_DOWN ();
 		__syncthreads ();
 		{
 			/* filter outputs: horn B -> xf, drum shelves in place, horn A of the next

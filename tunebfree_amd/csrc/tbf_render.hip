@@ -66,6 +66,9 @@
 #ifndef SERIAL_PRIO
 #define SERIAL_PRIO 1 /* wave priority raised (s_setprio) while a wave runs a serial chain */
 #endif
+#ifndef WH_PRIO
+#define WH_PRIO 0 /* the same for k_whirl's filter pass (measured slightly slower: 4.47-4.50 vs 4.52e9) */
+#endif
 #define PRIO_UP()                                  \
 	do {                                           \
 		if (SERIAL_PRIO)                           \
@@ -1724,13 +1727,15 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 			sm.aOut[n]      = (T0[n + 2] * K.hafw[2]) + (K.hafw[3] * T0[n + 1]) + (K.hafw[4] * T0[n]);
 			__syncthreads ();
 		}
-		PRIO_UP ();
+		if (WH_PRIO)
+			PRIO_UP ();
 		if (lane < 4 && (lane > 0 || aNext)) {
 			const float* ip = lane == 0 ? sm.xn : (lane == 1 ? sm.aOut : sm.rd[lane - 2]);
 			/* crossing into the next block: A's state gets that block's NaN scrub first */
 			wh_serial (ip, sm.tmp[lane], st.fz[lane], fa0, fa1, lane == 0 && sb + 1 == TBF_BLK / TBF_SUB);
 		}
-		PRIO_DOWN ();
+		if (WH_PRIO)
+			PRIO_DOWN ();
 		__syncthreads ();
 		{
 			/* filter outputs: horn B -> xf, drum shelves in place, horn A of the next

@@ -64,11 +64,17 @@ extern "C" {
 
 typedef struct tbf_engine tbf_engine;
 
+/* tbf_engine_config.debug_flags */
+#define TBF_DEBUG_FORCE_SERIAL 1u /* fail every fast-path precondition vote, so each guarded
+                                   * stage takes its exact serial replay (parity tests of the
+                                   * fallbacks; slow) */
+
 typedef struct tbf_engine_config {
 	double   sample_rate; /* Hz, 22050 .. 96000 */
 	int32_t  device;      /* HIP device ordinal */
 	uint32_t chain_mode;  /* TBF_CHAIN_* */
-	uint32_t reserved[4];
+	uint32_t debug_flags; /* TBF_DEBUG_*, 0 in production */
+	uint32_t reserved[3];
 } tbf_engine_config;
 
 int         tbf_abi_version (void);
@@ -106,13 +112,19 @@ int tbf_set_param (tbf_engine* e, uint32_t inst, int32_t param, double value);
  * out[i * stride + 0 .. nblocks*128).  Synchronous. */
 int tbf_render (tbf_engine* e, uint32_t nblocks, float* outL, float* outR, uint64_t stride);
 
-/* Same into device memory on `stream` (hipStream_t, NULL = engine stream); returns
- * once the work is enqueued.  Outputs stay in HBM. */
+/* Same into device memory on `stream` (hipStream_t, NULL = the engine's own
+ * non-blocking stream); returns once the work is enqueued.  Outputs stay in HBM.
+ * Ordering: the render is ordered after earlier work on `stream` and the outputs are
+ * complete when `stream` reaches this point.  A NULL stream is NOT the legacy default
+ * stream: a caller that consumes the outputs on another stream (e.g. torch's current
+ * stream, whose handle is 0 on the default stream) must pass that stream's real handle
+ * or call tbf_synchronize () first. */
 int tbf_render_device (tbf_engine* e, uint32_t nblocks, float* d_outL, float* d_outR, uint64_t stride,
                        void* stream);
 
 /* synthSound semantics (b_synth/lv2.cpp:212-239): serve nframes per instance out of
- * the 128-sample block FIFO, rendering blocks as needed. */
+ * the 128-sample block FIFO, rendering blocks as needed.  Instance i writes
+ * out[i * stride + 0 .. nframes); stride >= nframes (else -22). */
 int tbf_synth_sound (tbf_engine* e, uint32_t nframes, float* outL, float* outR, uint64_t stride);
 
 /* ---- host control surface (src/midi.cpp, src/program.cpp, src/pgmParser.cpp) ---- */
@@ -161,7 +173,15 @@ int tbf_render_events (tbf_engine* e, uint32_t nblocks, const tbf_event* ev, uin
                        float* d_outR, uint64_t stride, void* stream);
 
 int tbf_synchronize (tbf_engine* e);
-/* bit 0: vibrato scatter took the serial path in some block (informational) */
+/* Which exact-but-slow paths the kernels took since the engine was created (cumulative,
+ * informational; the results are bit-identical either way).  Waits for the engine's
+ * own stream and the pipelined stage streams; a caller rendering on its own stream must
+ * synchronize that stream first. */
+#define TBF_PATH_VIB_SERIAL 1u   /* vibrato scatter: lane-serial replay (src/vibrato.cpp:380-409) */
+#define TBF_PATH_WH_ANGLE 2u     /* whirl rotor angles: literal fmod recurrence (src/whirl.cpp:1428-1429) */
+#define TBF_PATH_WH_MOTION 4u    /* whirl ring adds: sample-serial replay (src/whirl.cpp:1432-1469) */
+#define TBF_PATH_RV_PHASE 8u     /* reverb LFO phases: literal recurrence + sin (src/reverb.cpp:479-496) */
+#define TBF_PATH_RV_WINDOW 16u   /* reverb tap outside the staged window: direct ring reads */
 int tbf_error_flags (tbf_engine* e, uint32_t* flags);
 /* read back the wave bank of a template (wheels 1..256 concatenated) for checks */
 int tbf_template_bank (tbf_engine* e, uint32_t tpl_id, float* out, uint64_t cap, uint32_t* lens256);
@@ -175,6 +195,9 @@ int tbf_debug_tables (tbf_engine* e, uint32_t tpl_id, float* attack, float* rele
 /* run one block of the tonegen control plane for an instance and return the core
  * program: per entry {wheel, env, row, sg, pg, vg, nsg, npg, nvg} as 9 floats */
 int tbf_debug_step (tbf_engine* e, uint32_t inst, float* entries9, uint32_t cap);
+/* the core program the instance's next rendered block uses, after the control-plane
+ * step a render makes for that block (which steps only when something changed) */
+int tbf_debug_render_program (tbf_engine* e, uint32_t inst, float* entries9, uint32_t cap);
 /* an instance's host control state: odClean, odA, odC, rvG, revOpt, revSelect, whBypass,
  * newRouting, swellPedalGain, percEnabled, percIsSoft, percIsFast, percSendBus, vibTable,
  * vibMixed, percDrawbarGain, drawBarGain[27]; returns the count (43) */

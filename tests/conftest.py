@@ -28,6 +28,12 @@ def oracle():
 
 
 @pytest.fixture(scope="session")
+def tunings():
+    import json
+    return json.loads((Path(__file__).resolve().parent / "golden" / "tunings.json").read_text())
+
+
+@pytest.fixture(scope="session")
 def refchk():
     from orc_bind import load_ref
     lib = load_ref()

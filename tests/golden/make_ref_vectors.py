@@ -31,6 +31,16 @@ CASES = [
     ("events44_19tet", 44100.0, "19TET", 5, 4242, ("events", 2), 72, 0),
     ("bench96_p4", 96000.0, "p4", 11, 9, ("bench", 17), 40, 0),
     ("random96_bagpipe4", 96000.0, "bagpipe4", 13, 31, ("random", 3), 40, 0),
+    # parameter sweep (scenarios.sweep_scenario): overdrive character, reverb mix, percussion
+    # variants, clusters, pedal keys, rotary stop <-> fast
+    ("sweep48_0", 48000.0, None, 7, 2100, ("sweep", 0), 72, 0),
+    ("sweep48_1", 48000.0, None, 7, 2101, ("sweep", 1), 72, 0),
+    ("sweep48_2", 48000.0, None, 7, 2102, ("sweep", 2), 72, 0),
+    ("sweep48_3", 48000.0, None, 7, 2103, ("sweep", 3), 72, 0),
+    ("sweep44_5", 44100.0, "duodene", 9, 2105, ("sweep", 5), 72, 0),
+    ("sweep96_6", 96000.0, "5TET", 3, 2106, ("sweep", 6), 48, 0),
+    # drawbar / routing / percussion changes with no key event in the block
+    ("reroute48_1", 48000.0, None, 7, 2201, ("reroute", 1), 56, 0),
 ]
 
 
@@ -43,6 +53,10 @@ def scenario(kind, i):
         return S.bench_scenario(i, full=False) + [(20, "note", 70, 1), (30, "param", S.P_PERC, 1)]
     if kind == "random":
         return S.random_drawbar_scenario(i)
+    if kind == "sweep":
+        return S.sweep_scenario(i)
+    if kind == "reroute":
+        return S.reroute_scenario(i)
     raise ValueError(kind)
 
 

@@ -15,6 +15,7 @@ import numpy as np
 ROOT = Path(__file__).resolve().parents[1]
 ORC_SO = ROOT / "oracle" / "liborc.so"
 REF_SO = ROOT / "oracle" / "_ref" / "libtbfref.so"
+PIN_SO = ROOT / "oracle" / "_ref" / "libtbfpin.so"
 
 _fp = C.POINTER(C.c_float)
 _dp = C.POINTER(C.c_double)
@@ -98,6 +99,37 @@ def load_ref():
     lib.ref_preamp_proc.argtypes = [C.c_void_p, _fp, _fp, C.c_int]
     lib.ref_preamp_free.argtypes = [C.c_void_p]
     return lib
+
+
+def load_pin():
+    """The template-pin harness (oracle/ref_tpl_pin.cpp: src/tonegen.cpp's own static
+    table builders); None when not built (e.g. on the GPU box)."""
+    if not PIN_SO.exists():
+        return None
+    lib = C.CDLL(str(PIN_SO))
+    lib.refpin_template.restype = C.c_long
+    lib.refpin_template.argtypes = [C.c_double, _dp, C.c_void_p, C.c_uint, _fp, C.c_uint64, _u32p, _dp, _fp, _fp,
+                                    _fp]
+    return lib
+
+
+def pin_template(pin, orc, sr, mts128, seed):
+    """Wave bank, lengths, wheel frequencies, envelopes and key-compression table built by
+    the reference's own initOscillators / initKeyCompTable / initEnvelopes."""
+    f300 = np.zeros(300, np.float64)
+    m = None if mts128 is None else np.ascontiguousarray(mts128, np.float64)
+    orc.orc_get_frequencies(f300.ctypes.data_as(_dp), None if m is None else m.ctypes.data)
+    n = pin.refpin_template(float(sr), f300.ctypes.data_as(_dp), None, int(seed), None, 0, None, None, None, None,
+                            None)
+    bank = np.zeros(n, np.float32)
+    lens = np.zeros(256, np.uint32)
+    wf = np.zeros(256, np.float64)
+    a = np.zeros((9, 128), np.float32)
+    r = np.zeros((9, 128), np.float32)
+    k = np.zeros(128, np.float32)
+    pin.refpin_template(float(sr), f300.ctypes.data_as(_dp), None, int(seed), _f(bank), n, lens.ctypes.data_as(_u32p),
+                        wf.ctypes.data_as(_dp), _f(a), _f(r), _f(k))
+    return {"bank": bank, "lens": lens, "wfreq": wf, "attack": a, "release": r, "keycomp": k}
 
 
 class Template:

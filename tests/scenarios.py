@@ -88,6 +88,61 @@ class GlibcRand:
         return self._step()
 
 
+SWEEP_CHARACTER = (0.0, 0.3, 0.9, 1.0)
+SWEEP_REVERB = (0.0, 0.7, 1.0)
+
+
+def sweep_scenario(i):
+    """Parameter regions beyond the bench registration ("what's weak" 2),
+    varied with the instance index i:
+      - overdrive character SWEEP_CHARACTER[i % 4] (fsetCharacter, src/overdrive.cpp:552-574:
+        0 iterations / density 0 takes the 1 - cos branch, 1.0 squares to 16 sin passes);
+        instance i % 7 == 6 runs clean
+      - reverb mix SWEEP_REVERB[i % 3] (setReverbMix, src/reverb.cpp:233: 1.0 drops the dry path)
+      - percussion volume/decay/harmonic = bits 0/1/2 of i (normal/soft, fast/slow, 2nd/3rd),
+        retriggered after all upper keys go up (src/tonegen.cpp:3257-3327)
+      - i % 3 == 0: a 13-key upper cluster (key-compression table past index 12),
+        otherwise a 4-note chord
+      - pedal drawbars 8 0 6 0 ... and pedal keys 256..383 (src/midi.cpp:1469-1484)
+      - rotary: even i starts stopped (rev option 0, free stop), goes fast at block 12,
+        stops again at block 36 (deceleration to 0), chorale at 60; odd i the reverse
+        order from fast."""
+    ev = [(0, k, a, b) for (k, a, b) in jazz1_params(character=SWEEP_CHARACTER[i % 4],
+                                                       reverb=SWEEP_REVERB[i % 3])]
+    if i % 7 == 6:
+        ev.append((0, "param", P_OVERDRIVE, 0))
+    ev += [(0, "param", P_PERC_VOL, (i >> 0) & 1), (0, "param", P_PERC_DECAY, 1 - ((i >> 1) & 1)),
+           (0, "param", P_PERC_HARM, (i >> 2) & 1)]
+    for j, v in enumerate((8, 0, 6, 0, 0, 0, 0, 0, 4)):
+        ev.append((0, "param", P_BUS_DRAWBAR + 18 + j, v))
+    keys = list(range(48 + i % 5, 61 + i % 5)) if i % 3 == 0 else chord_for(i)
+    ev += [(0, "note", k, 1) for k in keys]
+    ped = 256 + 24 + (i % 12)
+    ev += [(0, "note", ped, 1), (20, "note", ped, 0), (21, "note", ped + 5, 1), (44, "note", ped + 5, 0),
+           (45, "note", 383, 1), (46, "note", 256, 1)]
+    # all upper keys up, then a retrigger (percussion fires on the first key down again)
+    ev += [(24, "note", k, 0) for k in keys]
+    ev += [(28, "note", k, 1) for k in keys[:3]]
+    ev += [(50, "note", 40 + (i % 9), 1), (52, "note", 127, 1)]
+    rot = [(0, 0, 0), (12, 2, 2), (36, 0, 0), (60, 1, 1)] if i % 2 == 0 else \
+          [(0, 2, 2), (12, 0, 0), (30, 2, 2), (60, 0, 0)]
+    for (b, d, h) in rot:
+        ev += [(b, "param", P_DRUM, d), (b, "param", P_HORN, h)]
+    return ev
+
+
+def reroute_scenario(i):
+    """Drawbar, routing and percussion changes with no key event in the same block
+    (drawbar sweeps, vibrato switches): the active wheels keep envelope-free entries
+    but their routed sums change, which the reference applies from the next block
+    (src/tonegen.cpp:3427-3485)."""
+    return bench_scenario(i) + [(0, "note", 128 + 40, 1), (19, "param", P_DRAWBAR + 4, 7),
+                                (23, "param", P_VIBRATO, 0), (26, "param", P_VIB_LOWER, 1),
+                                (29, "param", P_BUS_DRAWBAR + 11, 3), (33, "param", P_PERC, 0),
+                                (37, "param", P_PERC, 1), (41, "param", P_PERC_HARM, 1),
+                                (44, "param", P_DRAWBAR + 0, 0), (45, "param", P_DRAWBAR + 1, 2)]
+
+
 def random_drawbar_scenario(i, seed=None):
     """BASELINE config 5: upper drawbars from randomizeDrawbars (`rand() % 9` x 9,
     src/program.cpp:716-729) after srand(seed), rest of the Jazz-1 registration,

@@ -15,14 +15,14 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-5
 
 
-def _engine(chain=0, sr=48000.0):
+def _engine(chain=0, sr=48000.0, debug_flags=0):
     import tunebfree_amd as T
-    return T.Engine(sample_rate=sr, device=0, chain=chain)
+    return T.Engine(sample_rate=sr, device=0, chain=chain, debug_flags=debug_flags)
 
 
-def _setup(oracle, n, scen_fn, chain=0, tpl_seed=7, sr=48000.0):
+def _setup(oracle, n, scen_fn, chain=0, tpl_seed=7, sr=48000.0, debug_flags=0):
     from orc_bind import Template
-    eng = _engine(chain, sr)
+    eng = _engine(chain, sr, debug_flags)
     tid = eng.template(seed=tpl_seed)
     seeds = [1000 + 17 * i for i in range(n)]
     eng.add_instances([tid] * n, seeds)
@@ -89,10 +89,15 @@ def test_gpu_full_chain_events(oracle):
     assert max(eL, eR) <= TOL
 
 
-def test_gpu_vs_committed_reference_vectors():
+@pytest.mark.parametrize("debug_flags", [0, 1])
+def test_gpu_vs_committed_reference_vectors(debug_flags):
     """The HIP engine against the reference's own compiled chain (committed vectors,
     tests/golden/ref_vectors.npz): 44.1/48/96 kHz (whirl ring W=512/1024), 12-TET /
-    19-TET / p4 / bagpipe4 templates, event scripts, config-5 random drawbars."""
+    19-TET / p4 / bagpipe4 / duodene / 5TET templates, event scripts, config-5 random
+    drawbars, the parameter sweep (overdrive character, reverb mix, percussion variants,
+    clusters, pedal keys, rotary stop <-> fast).  debug_flags=1 (TBF_DEBUG_FORCE_SERIAL)
+    runs every guarded stage on its serial replay instead of the lane-parallel fast
+    path: both must match."""
     import json
     from pathlib import Path
     import tunebfree_amd as T
@@ -102,7 +107,7 @@ def test_gpu_vs_committed_reference_vectors():
     tunings = json.loads((gold / "tunings.json").read_text())
     worst = 0.0
     for c in json.loads(str(z["cases"])):
-        eng = T.Engine(sample_rate=c["sr"], device=0, chain=c["chain"])
+        eng = T.Engine(sample_rate=c["sr"], device=0, chain=c["chain"], debug_flags=debug_flags)
         m = None if c["tuning"] is None else np.array(tunings[c["tuning"]], np.float64)
         tid = eng.template(mts128=m, seed=c["tpl_seed"])
         eng.add_instances([tid], [c["inst_seed"]])
@@ -111,6 +116,11 @@ def test_gpu_vs_committed_reference_vectors():
             err, exact = compare(got, z[f"{c['name']}/{k}"])
             print(f"{c['name']}/{k}: max|err|={err:.3g} bit-exact={exact:.6f}")
             worst = max(worst, err)
+        flags = eng.error_flags()
+        print(f"{c['name']}: paths taken 0x{flags:x}")
+        if debug_flags and c["chain"] == 0:
+            assert flags & (T.engine.PATH_WH_ANGLE | T.engine.PATH_WH_MOTION | T.engine.PATH_RV_PHASE) == \
+                T.engine.PATH_WH_ANGLE | T.engine.PATH_WH_MOTION | T.engine.PATH_RV_PHASE, hex(flags)
         eng.close()
     assert worst <= TOL
 
@@ -287,47 +297,68 @@ def test_gpu_cli_host_synth_sound(oracle, tmp_path):
 
 
 @pytest.mark.parametrize("sr", [48000.0, 96000.0])
-def test_gpu_device_templates_match_host(sr):
+def test_gpu_device_templates_match_oracle_and_reference(oracle, sr):
     """§8(f) row 2: templates built on the device (tbf_templates_create: per-chunk
-    jumps of the glibc rand() stream + the writeSamples sines) equal the host-built
-    templates -- which the CPU tests pin to the oracle and the reference fixtures --
-    bit for bit: wave bank, wheel lengths, envelopes, key-compression table.  One batch
-    holds the 6 table tunings three times with distinct seeds; a second the 12-TET
-    default."""
+    jumps of the glibc rand() stream + the writeSamples sines) against
+      - the oracle's template builder, bit for bit (wave bank, wheel lengths,
+        envelopes, key-compression table), on the same (tuning, seed) inputs, and
+      - the reference's own src/tonegen.cpp builders (digests committed in
+        tests/golden/template_pins.json, generated by oracle/ref_tpl_pin.cpp): the 7
+        tunings at this sample rate with their pinned seeds.
+    A second batch (the 6 table tunings again with other seeds, plus three 12-TET
+    templates) is checked against the oracle."""
     import ctypes as C
+    import hashlib
     import json
     import time
     from pathlib import Path
     import tunebfree_amd as T
-    tunings = json.loads((Path(__file__).resolve().parent / "golden" / "tunings.json").read_text())
-    names = [k for k in sorted(tunings) if tunings[k] is not None]
-    mts = np.stack([np.asarray(tunings[nm], np.float64) for nm in names] * 3)
-    seeds = [300 + j for j in range(len(mts))]
+    from orc_bind import Template
+    gold = Path(__file__).resolve().parent / "golden"
+    tunings = json.loads((gold / "tunings.json").read_text())
+    pins = [p for p in json.loads((gold / "template_pins.json").read_text()) if p["sr"] == sr]
     eng = T.Engine(sample_rate=sr, device=0)
-    t0 = time.perf_counter()
-    dids = eng.templates(seeds, mts128=mts)
-    t_dev = time.perf_counter() - t0
-    dids += eng.templates([1, 2, 3])  # 12-TET (no MTS master)
-    t0 = time.perf_counter()
-    hids = [eng.template(mts128=mts[j], seed=seeds[j]) for j in range(len(mts))]
-    t_host = time.perf_counter() - t0
-    hids += [eng.template(seed=s) for s in (1, 2, 3)]
     lib = T.load_library()
     lib.tbf_debug_tables.restype = C.c_int
     lib.tbf_debug_tables.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
-    for d, h in zip(dids, hids):
-        db, dl = eng.template_bank(d)
-        hb, hl = eng.template_bank(h)
-        assert np.array_equal(dl, hl)
-        assert np.array_equal(db.view(np.uint32), hb.view(np.uint32)), (d, int(np.sum(db != hb)))
-        tabs = []
-        for t in (d, h):
-            a, r, k = np.zeros((9, 128), np.float32), np.zeros((9, 128), np.float32), np.zeros(128, np.float32)
-            assert lib.tbf_debug_tables(eng._h, t, a.ctypes.data, r.ctypes.data, k.ctypes.data) >= 0
-            tabs.append((a, r, k))
-        for x, y in zip(*tabs):
-            assert np.array_equal(x.view(np.uint32), y.view(np.uint32))
-    print(f"device templates @{sr:.0f}: {len(mts)} in {t_dev * 1e3:.1f} ms; host {t_host * 1e3:.1f} ms")
+
+    def tables(tid):
+        bank, lens = eng.template_bank(tid)
+        a, r, k = np.zeros((9, 128), np.float32), np.zeros((9, 128), np.float32), np.zeros(128, np.float32)
+        assert lib.tbf_debug_tables(eng._h, tid, a.ctypes.data, r.ctypes.data, k.ctypes.data) >= 0
+        return {"bank": bank, "lens": lens, "attack": a, "release": r, "keycomp": k}
+
+    def mts(nm):
+        return None if tunings[nm] is None else np.asarray(tunings[nm], np.float64)
+
+    # batch 1: the pinned (tuning, seed) cases; the 12-TET one has no MTS table, so it is
+    # built in its own call (tbf_templates_create takes all-or-none frequency tables)
+    table_pins = [p for p in pins if tunings[p["tuning"]] is not None]
+    t0 = time.perf_counter()
+    ids = eng.templates([p["seed"] for p in table_pins], mts128=np.stack([mts(p["tuning"]) for p in table_pins]))
+    t_dev = time.perf_counter() - t0
+    tet = [p for p in pins if tunings[p["tuning"]] is None]
+    ids += eng.templates([p["seed"] for p in tet])
+    cases = [(tid, p["tuning"], p["seed"], p) for tid, p in zip(ids, table_pins + tet)]
+    # batch 2: other seeds, checked against the oracle only
+    names = [k for k in sorted(tunings) if tunings[k] is not None]
+    ids2 = eng.templates([500 + j for j in range(len(names))], mts128=np.stack([mts(nm) for nm in names]))
+    ids2 += eng.templates([1, 2, 3])
+    cases += [(tid, nm, 500 + j, None) for j, (tid, nm) in enumerate(zip(ids2, names))]
+    cases += [(tid, "12TET", s, None) for tid, s in zip(ids2[len(names):], (1, 2, 3))]
+    for tid, nm, seed, pin in cases:
+        got = tables(tid)
+        o = Template(oracle, sr=sr, mts128=mts(nm), seed=seed)
+        ob, ol = o.bank()
+        oa, orr, ok = o.envs()
+        want = {"bank": ob, "lens": ol, "attack": oa, "release": orr, "keycomp": ok}
+        for key in want:
+            assert np.array_equal(np.asarray(got[key]).view(np.uint32), np.asarray(want[key]).view(np.uint32)), \
+                (nm, seed, key)
+            if pin is not None:
+                assert hashlib.sha256(np.ascontiguousarray(got[key]).tobytes()).hexdigest() == pin[key], (nm, key)
+    print(f"device templates @{sr:.0f}: {len(cases)} vs oracle, {len(pins)} vs reference pins; "
+          f"first batch of {len(table_pins)} in {t_dev * 1e3:.1f} ms")
     eng.close()
 
 
@@ -395,3 +426,115 @@ def test_gpu_full_size_bench_batch(oracle):
     R2 = np.concatenate([R2a, R2b], axis=1)
     assert np.array_equal(L2.view(np.uint32), L[half:].view(np.uint32))
     assert np.array_equal(R2.view(np.uint32), R[half:].view(np.uint32))
+
+
+@pytest.mark.parametrize("debug_flags", [0, 1])
+def test_gpu_parameter_sweep(oracle, debug_flags):
+    """Parameter regions the bench registration does not reach (scenarios.sweep_scenario):
+    overdrive character 0 / 0.3 / 0.9 / 1.0 and clean, reverb mix 0 / 0.7 / 1.0,
+    percussion normal/soft x fast/slow x 2nd/3rd with retriggers, 13-key clusters,
+    pedal keys 256..383 with pedal drawbars, rotary stop <-> fast transitions; 12
+    instances in one engine against the oracle, with the fast paths and with every
+    guarded stage forced onto its serial replay (TBF_DEBUG_FORCE_SERIAL)."""
+    import tunebfree_amd as T
+    n, nb = 12, 72
+    eng, tpl, seeds, scens = _setup(oracle, n, S.sweep_scenario, debug_flags=debug_flags)
+    L, R = engine_run(eng, scens, nb)
+    oL, oR, oA, oB, oC = oracle_run(oracle, tpl, seeds, scens, nb)
+    eL, xL = compare(L, oL)
+    eR, xR = compare(R, oR)
+    flags = eng.error_flags()
+    print(f"sweep (debug {debug_flags}): max|err| L={eL:.3g} R={eR:.3g} bit-exact L={xL:.6f} R={xR:.6f} "
+          f"paths 0x{flags:x}")
+    assert max(eL, eR) <= TOL
+    for i in range(n):  # every instance sounds (no silent pass through a broken stage)
+        assert float(np.abs(oL[i]).max()) > 1e-3
+    if debug_flags:
+        want = T.engine.PATH_VIB_SERIAL | T.engine.PATH_WH_ANGLE | T.engine.PATH_WH_MOTION | T.engine.PATH_RV_PHASE
+        assert flags & want == want, hex(flags)
+
+
+def test_gpu_reroute_without_key_events(oracle):
+    """Drawbar / vibrato-routing / percussion changes while keys are held, with no key
+    event in the block (scenarios.reroute_scenario): the new sums must take effect from
+    the next block, as in the reference (the render path steps the control plane only
+    when something changed)."""
+    eng, tpl, seeds, scens = _setup(oracle, 4, S.reroute_scenario)
+    L, R = engine_run(eng, scens, 56)
+    oL, oR, *_ = oracle_run(oracle, tpl, seeds, scens, 56)
+    eL, xL = compare(L, oL)
+    eR, xR = compare(R, oR)
+    print(f"reroute: max|err| L={eL:.3g} R={eR:.3g} bit-exact L={xL:.6f} R={xR:.6f}")
+    assert max(eL, eR) <= TOL
+
+
+def test_gpu_forced_serial_events_and_taps(oracle):
+    """The event script (chord changes, note-offs with release envelopes, lower-manual
+    vibrato, rotary fast -> slow) and the preamp / reverb stage taps with every guarded
+    stage on its serial replay."""
+    eng, tpl, seeds, scens = _setup(oracle, 4, S.event_scenario, debug_flags=1)
+    L, R = engine_run(eng, scens, 72)
+    oL, oR, *_ = oracle_run(oracle, tpl, seeds, scens, 72)
+    eL, xL = compare(L, oL)
+    eR, xR = compare(R, oR)
+    print(f"forced events: max|err| L={eL:.3g} R={eR:.3g} bit-exact L={xL:.6f} R={xR:.6f}")
+    assert max(eL, eR) <= TOL
+    for tap, idx in ((2, 3), (3, 4)):
+        eng, tpl, seeds, scens = _setup(oracle, 3, S.sweep_scenario, chain=tap, debug_flags=1)
+        L, _ = engine_run(eng, scens, 40)
+        ref = oracle_run(oracle, tpl, seeds, scens, 40)[idx]
+        err, exact = compare(L, ref)
+        print(f"forced tap {tap}: max|err|={err:.3g} bit-exact={exact:.6f}")
+        assert err <= TOL
+
+
+@pytest.mark.parametrize("via_events", [True, False])
+def test_gpu_add_instances_after_render_then_events(oracle, via_events):
+    """Instances added to an engine that has already rendered; then one
+    tbf_render_events call with events at blocks > 0 for instances that existed before
+    (and for new ones): an old instance's blocks before its event must still render with
+    its earlier control (the persistent control pool is uploaded as of the chunk start)."""
+    import torch
+    from orc_bind import Template
+    eng = _engine()
+    tid = eng.template(seed=7)
+    seeds = [1000 + 17 * i for i in range(5)]
+    eng.add_instances([tid] * 3, seeds[:3])
+    pre = [S.bench_scenario(i) for i in range(3)]
+    L0, R0 = engine_run(eng, pre, 10)
+    eng.add_instances([tid] * 2, seeds[3:])
+    for i in (3, 4):
+        for (b, kind, a, v) in S.bench_scenario(i):
+            (eng.note if kind == "note" else eng.set_param)(i, a, v)
+    nb = 40
+    rows = [(5, 0, 0, 72, 1.0), (5, 0, 1, S.P_HORN, 2.0), (9, 1, 1, S.P_DRAWBAR + 4, 7.0),
+            (17, 2, 0, 60 + 2, 0.0), (20, 2, 1, S.P_REVERB, 0.6), (7, 4, 0, 50, 1.0), (30, 1, 1, S.P_CHARACTER, 0.9)]
+    if via_events:
+        L = torch.zeros((5, nb * 128), dtype=torch.float32, device="cuda")
+        R = torch.zeros_like(L)
+        eng.render_events_device(nb, eng.events(rows), L.data_ptr(), R.data_ptr(), nb * 128)
+        eng.synchronize()
+        L, R = L.cpu().numpy(), R.cpu().numpy()
+    else:  # the same script through tbf_note / tbf_set_param between render calls
+        sc5 = [[(b, "note" if k == 0 else "param", a, v) for (b, inst, k, a, v) in rows if inst == i]
+               for i in range(5)]
+        L, R = engine_run(eng, sc5, nb)
+    tpl = Template(oracle, seed=7)
+    bad = []
+    for i in range(5):
+        off = 10 if i < 3 else 0  # old instances: the call starts at their block 10
+        sc = list(S.bench_scenario(i))
+        for (b, inst, kind, a, v) in rows:
+            if inst == i:
+                sc.append((b + off, "note" if kind == 0 else "param", a, v))
+        oL, oR, *_ = oracle_run(oracle, tpl, [seeds[i]], [sc], nb + off)
+        gl = np.concatenate([L0[i], L[i]]) if off else L[i]
+        gr = np.concatenate([R0[i], R[i]]) if off else R[i]
+        e1, x1 = compare(gl, oL[0])
+        e2, x2 = compare(gr, oR[0])
+        d = np.nonzero(gl.view(np.uint32) != oL[0].view(np.uint32))[0]
+        print(f"instance {i}: max|err| {max(e1, e2):.3g} bit-exact {min(x1, x2):.6f} "
+              f"first differing block {d[0] // 128 if len(d) else None}")
+        if max(e1, e2) > TOL:
+            bad.append(i)
+    assert not bad, bad

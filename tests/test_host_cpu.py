@@ -48,6 +48,8 @@ def _bind_debug(lib):
     lib.tbf_debug_tables.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
     lib.tbf_debug_step.restype = C.c_int
     lib.tbf_debug_step.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]
+    lib.tbf_debug_render_program.restype = C.c_int
+    lib.tbf_debug_render_program.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]
 
 
 def _orc_bind_debug(lib):
@@ -106,9 +108,10 @@ def _oracle_program(oracle, inst_ptr):
     return out
 
 
-def _engine_program(lib, eng, i):
+def _engine_program(lib, eng, i, lazy=False):
     buf = np.zeros(9 * 600, np.float32)
-    n = lib.tbf_debug_step(eng._h, i, buf.ctypes.data, 600)
+    fn = lib.tbf_debug_render_program if lazy else lib.tbf_debug_step
+    n = fn(eng._h, i, buf.ctypes.data, 600)
     assert n >= 0
     return buf[: 9 * n].reshape(n, 9)
 
@@ -120,9 +123,14 @@ def _events_by_block(scen):
     return by
 
 
-def test_control_plane_programs_match_oracle(oracle):
+@pytest.mark.parametrize("lazy", [False, True])
+@pytest.mark.parametrize("scen", ["events", "sweep", "reroute"])
+def test_control_plane_programs_match_oracle(oracle, lazy, scen):
     """Block-by-block core programs of the host control plane vs the oracle's
-    oscGenerateFragment (active list order, wheel, envelope row, all six gains)."""
+    oscGenerateFragment (active list order, wheel, envelope row, all six gains).
+    lazy=False steps the tonegen control every block (tbf_debug_step); lazy=True makes
+    exactly the step a render makes per block (tbf_debug_render_program: only when
+    something changed), so a change the render path fails to pick up shows here."""
     from orc_bind import Chain
     _orc_bind_debug(oracle)
     lib = T.load_library()
@@ -134,7 +142,8 @@ def test_control_plane_programs_match_oracle(oracle):
     seeds = [1000 + i for i in range(n_inst)]
     eng.add_instances([tid] * n_inst, seeds)
     chains = [Chain(oracle, tpl, s) for s in seeds]
-    scens = [_events_by_block(S.event_scenario(i)) for i in range(n_inst)]
+    fn = {"events": S.event_scenario, "sweep": S.sweep_scenario, "reroute": S.reroute_scenario}[scen]
+    scens = [_events_by_block(fn(i)) for i in range(n_inst)]
     checked = 0
     for blk in range(nblocks):
         for i in range(n_inst):
@@ -147,7 +156,7 @@ def test_control_plane_programs_match_oracle(oracle):
                     chains[i].param(a, v)
             chains[i].render(1)
             op = _oracle_program(oracle, chains[i].ptr)
-            pp = _engine_program(lib, eng, i)
+            pp = _engine_program(lib, eng, i, lazy)
             assert len(op) == len(pp), (blk, i)
             for (w, env, r, g), q in zip(op, pp):
                 assert (w, env) == (int(q[0]), int(q[1])), (blk, i)
@@ -364,3 +373,28 @@ def test_device_templates_refused_on_host_engine():
     with pytest.raises(RuntimeError):
         eng.templates([7])
     eng.close()
+
+
+def test_host_templates_vs_reference_pins(tunings):
+    """The product's host template builder (tbf_template_create on a host-only engine)
+    gives the wave banks, lengths, envelopes and key-compression tables of the
+    reference's own src/tonegen.cpp builders (digests in tests/golden/template_pins.json,
+    see tests/golden/make_template_pins.py), bit for bit: 7 tunings x 48 / 96 kHz."""
+    import hashlib
+    import json
+    pins = json.loads((ROOT / "tests" / "golden" / "template_pins.json").read_text())
+    lib = T.load_library()
+    _bind_debug(lib)
+    engines = {}
+    for p in pins:
+        eng = engines.setdefault(p["sr"], T.Engine(sample_rate=p["sr"], device=-1))
+        m = None if tunings[p["tuning"]] is None else np.array(tunings[p["tuning"]], np.float64)
+        tid = eng.template(mts128=m, seed=p["seed"])
+        bank, lens = eng.template_bank(tid)
+        a, r, k = np.zeros((9, 128), np.float32), np.zeros((9, 128), np.float32), np.zeros(128, np.float32)
+        assert lib.tbf_debug_tables(eng._h, tid, a.ctypes.data, r.ctypes.data, k.ctypes.data) == 0
+        got = {"bank": bank, "lens": lens, "attack": a, "release": r, "keycomp": k}
+        for key, v in got.items():
+            assert hashlib.sha256(np.ascontiguousarray(v).tobytes()).hexdigest() == p[key], (p["tuning"], p["sr"], key)
+    for e in engines.values():
+        e.close()

@@ -31,11 +31,6 @@ def fixtures(tmp_path_factory):
     return d / "regression_test_data"
 
 
-@pytest.fixture(scope="module")
-def tunings():
-    return json.loads((GOLD / "tunings.json").read_text())
-
-
 def test_rand_is_glibc_rand(oracle):
     """orc_rand == the C library's rand() after srand(seed) (TYPE_3, glibc)."""
     libc = C.CDLL(None)
@@ -220,3 +215,44 @@ def test_oracle_vs_committed_reference_vectors(oracle, tunings):
         for k, v in zip("LRABC", got):
             ref = z[f"{c['name']}/{k}"]
             assert np.array_equal(v.view(np.uint32), ref.view(np.uint32)), (c["name"], k)
+
+
+# --------------------------------------------------------------------------- template pins
+def _template_pins():
+    return json.loads((GOLD / "template_pins.json").read_text())
+
+
+def test_oracle_templates_vs_reference_pins(oracle, tunings):
+    """The oracle's wave banks (writeSamples sines + per-sample rand() LSB), wheel
+    lengths, envelopes and key-compression tables equal, bit for bit, the tables the
+    reference's own src/tonegen.cpp builds (static initOscillators / initKeyCompTable /
+    initEnvelopes reached by oracle/ref_tpl_pin.cpp; digests committed in
+    tests/golden/template_pins.json by tests/golden/make_template_pins.py): 7 tunings x
+    48 / 96 kHz."""
+    import hashlib
+    from golden.make_template_pins import digest
+    pins = _template_pins()
+    assert len(pins) == 14
+    for p in pins:
+        m = None if tunings[p["tuning"]] is None else np.array(tunings[p["tuning"]], np.float64)
+        tpl = Template(oracle, sr=p["sr"], mts128=m, seed=p["seed"])
+        bank, lens = tpl.bank()
+        a, r, k = tpl.envs()
+        got = {"bank": bank, "lens": lens, "attack": a, "release": r, "keycomp": k}
+        for key, v in got.items():
+            assert hashlib.sha256(np.ascontiguousarray(v).tobytes()).hexdigest() == p[key], (p["tuning"], p["sr"], key)
+
+
+def test_reference_pin_harness_reproduces_committed_pins(oracle, tunings):
+    """Where /root/reference is built (oracle/_ref/libtbfpin.so), the reference's own
+    builders still give the committed digests (the fixture is current)."""
+    from golden.make_template_pins import cases, digest
+    from orc_bind import load_pin, pin_template
+    pin = load_pin()
+    if pin is None:
+        pytest.skip("oracle/_ref/libtbfpin.so not built (no /root/reference here)")
+    pins = _template_pins()
+    for (nm, sr, seed, m), p in zip(cases(), pins):
+        d = digest(pin_template(pin, oracle, sr, m, seed))
+        assert {k: d[k] for k in p if k not in ("tuning", "sr", "seed")} == \
+            {k: p[k] for k in p if k not in ("tuning", "sr", "seed")}, (nm, sr)

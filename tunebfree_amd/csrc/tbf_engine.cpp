@@ -763,6 +763,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 	P.chain     = e->cfg.chain_mode;
 	P.slabLen   = e->slabLen;
 	P.errFlags  = e->err.p;
+	P.dbg       = e->cfg.debug_flags;
 	P.prof      = e->profOn ? e->prof.p : nullptr;
 	/* inter-stage buffers: two parities (alternate chunks), see the pipelining below */
 	const size_t need = (size_t)n * TBF_CHUNK * TBF_BLK;
@@ -791,6 +792,19 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		/* host control for the chunk, block by block: entry indices per (block, instance),
 		 * new pool entries only where an instance's control changes */
 		const uint32_t want = std::min<uint32_t> (TBF_CHUNK, nblocks - b0);
+		if (e->persistStale) {
+			/* the persistent pool (entry i = instance i's current control and programme) as
+			 * of the START of this chunk: an instance without a delta at some block renders
+			 * that block with entry i, so it must not yet hold a later block's events.
+			 * Rare (after instances are added), so it syncs. */
+			if ((rc = joinStages (e, s)))
+				return rc;
+			HIPCHK (hipMemcpyAsync (e->ctl.p, e->hCtl.data (), n * sizeof (tbf_seg_ctl), hipMemcpyHostToDevice, s));
+			HIPCHK (hipMemcpyAsync (e->prog.p, e->hProg.data (), (size_t)n * PROG_CAP * sizeof (tbf_prog_entry),
+			                        hipMemcpyHostToDevice, s));
+			HIPCHK (hipStreamSynchronize (s));
+			e->persistStale = false;
+		}
 		e->dCtl.clear ();
 		e->dProg.clear ();
 		e->hIdx.resize ((size_t)want * n);
@@ -844,19 +858,13 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			}
 		}
 		const bool     par     = (e->chunkSeq++ & 1) != 0;
-		const bool     piped   = pipe && !delta && !e->persistStale;
+		const bool     piped   = pipe && !delta;
 		P.mid1 = e->mid1.p ? e->mid1.p + (par ? need : 0) : nullptr;
 		P.mid2 = e->mid2.p ? e->mid2.p + (par ? need : 0) : nullptr;
 		P.rvA  = e->rvA.p ? e->rvA.p + (par ? 2 * need : 0) : nullptr;
 		P.rvB  = e->rvB.p ? e->rvB.p + (par ? 2 * need : 0) : nullptr;
 		if (!piped && (rc = joinStages (e, s)))
 			return rc;
-		if (e->persistStale) {
-			HIPCHK (hipMemcpyAsync (e->ctl.p, e->hCtl.data (), n * sizeof (tbf_seg_ctl), hipMemcpyHostToDevice, s));
-			HIPCHK (hipMemcpyAsync (e->prog.p, e->hProg.data (), (size_t)n * PROG_CAP * sizeof (tbf_prog_entry),
-			                        hipMemcpyHostToDevice, s));
-			e->persistStale = false;
-		}
 		if (delta) {
 			HIPCHK (hipMemcpyAsync (e->ctl.p + n, e->dCtl.data (), e->dCtl.size () * sizeof (tbf_seg_ctl),
 			                        hipMemcpyHostToDevice, s));
@@ -1005,6 +1013,8 @@ int tbf_synth_sound (tbf_engine* e, uint32_t nframes, float* outL, float* outR, 
 {
 	if (!e || !outL || !outR)
 		return fail (-22, "null argument");
+	if (stride < nframes)
+		return fail (-22, "stride smaller than nframes");
 	const uint32_t n = (uint32_t)e->inst.size ();
 	e->fifoL.resize ((size_t)n * TBF_BLK);
 	e->fifoR.resize ((size_t)n * TBF_BLK);
@@ -1045,9 +1055,12 @@ int tbf_error_flags (tbf_engine* e, uint32_t* flags)
 	*flags = 0;
 	if (!e->err.p)
 		return 0;
+	HIPCHK (hipSetDevice (e->cfg.device));
 	if (int rc = drainStages (e))
 		return rc;
-	HIPCHK (hipMemcpy (flags, e->err.p, 4, hipMemcpyDeviceToHost));
+	/* the engine stream carries the non-pipelined chunks: read after them, on it */
+	HIPCHK (hipMemcpyAsync (flags, e->err.p, 4, hipMemcpyDeviceToHost, e->stream));
+	HIPCHK (hipStreamSynchronize (e->stream));
 	return 0;
 }
 
@@ -1093,6 +1106,27 @@ int tbf_debug_step (tbf_engine* e, uint32_t i, float* out, uint32_t cap)
 		o[3] = p.sg; o[4] = p.pg; o[5] = p.vg; o[6] = p.nsg; o[7] = p.npg; o[8] = p.nvg;
 	}
 	return (int)in.prog.size ();
+}
+
+int tbf_debug_render_program (tbf_engine* e, uint32_t i, float* out, uint32_t cap)
+{
+	if (!e || i >= e->inst.size ())
+		return fail (-22, "bad instance");
+	const size_t n = e->inst.size ();
+	if (e->hCtl.size () < n) { /* a host-only engine never sized the pool */
+		e->hCtl.resize (n);
+		e->hProg.resize (n * PROG_CAP);
+	}
+	bool pc;
+	(void)stepControl (e, i, pc); /* exactly the per-block step renderImpl makes */
+	const std::vector<tbf_prog_entry>& prog = e->inst[i].prog;
+	for (uint32_t q = 0; q < prog.size () && q < cap; q++) {
+		const tbf_prog_entry& p = prog[q];
+		float*                o = out + 9 * q;
+		o[0] = p.wheel; o[1] = p.env; o[2] = p.row;
+		o[3] = p.sg; o[4] = p.pg; o[5] = p.vg; o[6] = p.nsg; o[7] = p.npg; o[8] = p.nvg;
+	}
+	return (int)prog.size ();
 }
 
 int tbf_debug_profile (tbf_engine* e, int32_t enable, uint64_t* out, uint32_t cap)

@@ -717,6 +717,7 @@ void TgControl::step (std::vector<tbf_prog_entry>& prog, tbf_seg_ctl& ctl)
 	int      removed[TBF_NW + 1];
 	int      removedEnd = 0;
 	bool     anyEnv     = false;
+	bool     anyRoute   = false; /* some wheel's routed sums changed: its next entry differs */
 	for (uint16_t m : msg) {
 		const int kn = m & 0x0fff;
 		if ((m & 0xf000) == 0x1000) {
@@ -793,6 +794,7 @@ void TgControl::step (std::vector<tbf_prog_entry>& prog, tbf_seg_ctl& ctl)
 				reroute    = true;
 			}
 			if (reroute || recomputeRouting) {
+				anyRoute   = true;
 				a.sumPercn = (oldRouting & 0x0C) ? a.busLevel[percSendBus] : 0.0f;
 				a.sumScanr = 0.0f;
 				a.sumSwell = a.sumPedal;
@@ -831,7 +833,10 @@ void TgControl::step (std::vector<tbf_prog_entry>& prog, tbf_seg_ctl& ctl)
 			}
 		}
 	}
-	steadyPending = anyEnv || removedEnd > 0;
+	/* the next block's program differs from this one's when an envelope ends, a wheel
+	 * left the active list, or a steady wheel was rerouted (a drawbar or routing change
+	 * with no key event: this block still plays the old sums, the next the new ones) */
+	steadyPending = anyEnv || removedEnd > 0 || anyRoute;
 
 	/* mixdown control (3712-3777) */
 	ctl.routing          = oldRouting;

@@ -467,7 +467,7 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 			dmn = min (dmn, d);
 			dmx = max (dmx, d);
 		}
-		bad = __any (bad);
+		bad = __any (bad) || (P.dbg & TBF_DEBUG_FORCE_SERIAL);
 		dmn = wave_min (dmn);
 		dmx = wave_max (dmx);
 		if (!bad) {
@@ -494,7 +494,7 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 			}
 		} else {
 			if (lane == 0) {
-				atomicOr (P.errFlags, 1u);
+				atomicOr (P.errFlags, (uint32_t)TBF_PATH_VIB_SERIAL);
 				for (int n = 0; n < TBF_BLK; n++) {
 					const uint32_t op = (out0 + n) & 0x3FFu;
 					const int      h  = (int)((op + (uint32_t)(sm.u.v.vh[n] - n)) & 0x3FFu);
@@ -1034,14 +1034,15 @@ __device__ __forceinline__ void rv_core_fetch (const double* slab, int cntv, int
  * rv_core_lines: the per-line (wave-uniform) part for all 8 lines at once, line l on
  * lane l (lanes 8..63 duplicate): closed-form check, step D, sincos of the start phase;
  * the end phase of every closed-form line is stored. */
-__device__ __forceinline__ uint64_t rv_core_lines (RvCoreLds& sm, double vdl, double& v0x, double& Sx, double& Cx, double& Dx)
+__device__ __forceinline__ uint64_t rv_core_lines (RvCoreLds& sm, double vdl, double& v0x, double& Sx, double& Cx, double& Dx,
+                                                    bool force)
 {
 	const int    lane = threadIdx.x;
 	const int    li   = lane & 7;
 	tbf_rv_chan& st   = sm.st;
 	const double v0   = st.vib[li];
 	double       D = 0.0, cD = st.phD[li], cLo = st.phLo[li], cHi = st.phHi[li];
-	const bool   ok = phase_run_cached (v0, vdl, TBF_SUB, D, cD, cLo, cHi);
+	const bool   ok = phase_run_cached (v0, vdl, TBF_SUB, D, cD, cLo, cHi) && !force;
 	sincos (v0, &Sx, &Cx);
 	v0x = v0;
 	Dx  = D;
@@ -1135,7 +1136,9 @@ k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 		const size_t o = (size_t)s * TBF_SUB + lane;
 		/* per-line phase analysis and sincos, lanes 0..7 in parallel */
 		double         v0x, Sx, Cx, Dx;
-		const uint64_t okm = rv_core_lines (sm, vdl, v0x, Sx, Cx, Dx);
+		const uint64_t okm = rv_core_lines (sm, vdl, v0x, Sx, Cx, Dx, (P.dbg & TBF_DEBUG_FORCE_SERIAL) != 0);
+		if (okm != 0xff && lane == 0)
+			atomicOr (P.errFlags, (uint32_t)TBF_PATH_RV_PHASE);
 		/* windows to LDS (the reads were issued one sub-block ago) */
 		if (s == 0) {
 #pragma unroll
@@ -1166,6 +1169,7 @@ k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 			const int    i0  = inw ? rel : 0;
 			double       r0 = sm.win[l][i0], r1 = sm.win[l][i0 + 1];
 			if (!inw) { /* outside the window (not reachable at the fixed vibDepth): ring reads */
+				atomicOr (P.errFlags, (uint32_t)TBF_PATH_RV_WINDOW);
 				const double* a = slab + rl (roffv, l);
 				r0              = a[wrap_slot (wk, d)];
 				r1              = a[wrap_slot (wk + 1, d)];
@@ -1763,9 +1767,12 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 			double*      angBuf = (double*)&sm.tmp[0][0];
 			double       Dh, Dd;
 			const double h0 = st.hornAngle, d0 = st.drumAngle;
-			const bool   okh = phase_run (h0, hornIncr, TBF_SUB, Dh);
-			const bool   okd = phase_run (d0, drumIncr, TBF_SUB, Dd);
+			const bool   frc = (P.dbg & TBF_DEBUG_FORCE_SERIAL) != 0;
+			const bool   okh = phase_run (h0, hornIncr, TBF_SUB, Dh) && !frc;
+			const bool   okd = phase_run (d0, drumIncr, TBF_SUB, Dd) && !frc;
 			__syncthreads (); /* every lane has read the filter scratch and the start angles */
+			if (lane == 0 && !(okh && okd))
+				atomicOr (P.errFlags, (uint32_t)TBF_PATH_WH_ANGLE);
 			if ((lane == 1 && !okh) || (lane == 2 && !okd)) {
 				double       a   = lane == 1 ? h0 : d0;
 				const double inc = lane == 1 ? hornIncr : drumIncr;
@@ -1881,7 +1888,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 						ok = 0;
 				}
 				float* ring = sm.wring[r];
-				if (__all (ok)) {
+				if (__all (ok) && !(P.dbg & TBF_DEBUG_FORCE_SERIAL)) {
 					motion_add<W> (ring, mu[gi][2], ma[gi][2], mb[gi][2], lane);
 					__syncthreads ();
 					motion_add<W> (ring, mu[gi][1], ma[gi][1], mb[gi][1], lane);
@@ -1890,6 +1897,8 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 					__syncthreads ();
 				} else {
 					/* serial replay in the reference order: sample-major, motions in source order */
+					if (lane == 0)
+						atomicOr (P.errFlags, (uint32_t)TBF_PATH_WH_MOTION);
 					for (int i = 0; i < TBF_SUB; i++) {
 	#pragma unroll
 						for (int q = 0; q < 3; q++) {

@@ -166,8 +166,8 @@ typedef struct tbf_launch {
 	uint32_t              chain;     /* TBF_CHAIN_*: 0 full, 1 tonegen, 2 preamp tap, 3 reverb tap */
 	uint32_t              instBase;
 	uint32_t              slabLen;
-	uint32_t              pad;
-	uint32_t*             errFlags;
+	uint32_t              dbg;       /* TBF_DEBUG_* bits of tbf_engine_config.debug_flags */
+	uint32_t*             errFlags;  /* TBF_PATH_* bits: which rare paths a launch took */
 	uint64_t*             prof;      /* [inst][TBF_PROF_SLOTS] stage cycle sums, or NULL */
 } tbf_launch;
 

@@ -25,7 +25,12 @@ class TbfError(RuntimeError):
 
 class _Config(C.Structure):
     _fields_ = [("sample_rate", C.c_double), ("device", C.c_int32), ("chain_mode", C.c_uint32),
-                ("reserved", C.c_uint32 * 4)]
+                ("debug_flags", C.c_uint32), ("reserved", C.c_uint32 * 3)]
+
+
+# tbf_engine_config.debug_flags / tbf_error_flags bits (include/tbf.h)
+DEBUG_FORCE_SERIAL = 1
+PATH_VIB_SERIAL, PATH_WH_ANGLE, PATH_WH_MOTION, PATH_RV_PHASE, PATH_RV_WINDOW = 1, 2, 4, 8, 16
 
 
 # every symbol include/tbf.h declares, with its ctypes signature
@@ -85,9 +90,9 @@ def _check(rc):
 class Engine:
     """A batch of organ instances on one GPU (one engine per device / rank)."""
 
-    def __init__(self, sample_rate=48000.0, device=0, chain=0):
+    def __init__(self, sample_rate=48000.0, device=0, chain=0, debug_flags=0):
         lib = load_library()
-        cfg = _Config(float(sample_rate), int(device), int(chain))
+        cfg = _Config(float(sample_rate), int(device), int(chain), int(debug_flags))
         h = C.c_void_p()
         _check(lib.tbf_engine_create(C.byref(cfg), C.byref(h)))
         self._lib, self._h = lib, h

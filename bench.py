@@ -24,16 +24,20 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "tests"))
 
-# algorithmic HBM bytes per stereo sample, per kernel:
-#   k_rv_core = 12 lines x 2 ch x (8 B write + 8 B read) ring streaming + 16 B in + 16 B out
-#   k_rv_in   = predelay ring 2 ch x 16 B + 4 B in + 16 B out
-#   k_rv_out  = 16 B tap mix + 4 B dry in + 4 B out
-#   k_tonegen = 4 B stage output (wave bank L2/MALL-resident)
-#   k_whirl   = 4 B in + 8 B L/R out
-ALGO_BYTES = {"k_tonegen": 4, "k_rv_in": 52, "k_rv_core": 416, "k_rv_out": 24, "k_whirl": 12}
+# Algorithmic HBM bytes per stereo sample, per kernel.
+# Only what the algorithm itself must move counts: the reverb's 13 delay lines x 2
+# channels streamed once per cycle (8 B write + 8 B read, FP64) and the 8 B L/R output.
+#   k_rv_core = the 12 network lines (A..L) x 2 ch x 16 B              = 384 B
+#   k_rv_in   = the predelay line M x 2 ch x 16 B                      =  32 B
+#   k_whirl   = L/R float32 output                                     =   8 B
+# The implementation's inter-stage streams (mid1/rvA/rvB/mid2, 92 B) are NOT algorithmic;
+# they show up in the PMC `traffic` figure instead.  Step total: 424 B.
+ALGO_BYTES = {"k_tonegen": 0, "k_rv_in": 32, "k_rv_core": 384, "k_rv_out": 0, "k_whirl": 8}
+STEP_ALGO_BYTES = 424  # cfg 3/4/5, bytes per stereo sample of the whole chain
 DOMINANT = "k_rv_core"  # the HBM-streaming kernel the roofline is quoted for
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 TRAFFIC_JSON = ROOT / "profiles" / "traffic.json"  # written by tools/traffic_from_pmc.py
+CHUNK = 64  # blocks per launch set (TBF_CHUNK, csrc/tbf_engine.cpp)
 
 
 def parse():
@@ -58,6 +62,11 @@ def parse():
     ap.add_argument("--traffic", default=str(TRAFFIC_JSON), help="PMC traffic JSON (tools/traffic_from_pmc.py)")
     ap.add_argument("--kernel-steps", type=int, default=None,
                     help="extra steps timed per kernel with HIP events for the roofline (default = --steps)")
+    ap.add_argument("--stage-check", type=int, default=1,
+                    help="per-stage max|err| (tonegen / preamp / reverb taps) of the checked instances")
+    ap.add_argument("--dry-run", type=int, default=0,
+                    help="host-only engines (device -1), no render: exercises the rank setup, the sharding, "
+                         "the max-over-ranks reductions and the JSON contract without a GPU")
     return ap.parse_args()
 
 
@@ -121,13 +130,14 @@ def setup_instances(eng, wl, first_global, n):
 def _cpu_worker(args):
     """CPU render of a slice of instances; returns samples and seconds.  kind "reference":
     the reference's own tonegen/vibrato/overdrive/reverb/whirl translation units compiled
-    by oracle/Makefile (oracle/_ref/libtbfref.so), driven like synthSound; kind "port":
-    the oracle's C restatement."""
+    by oracle/Makefile with its release flags (oracle/_ref/fast/libtbfref.so; the strict
+    build when that is absent), driven like synthSound; kind "port": the oracle's C
+    restatement."""
     idx, blocks, sr, kind = args
     import scenarios as S
     from orc_bind import Chain, Template, load_oracle, load_ref
     lib = load_oracle()
-    ref = load_ref() if kind == "reference" else None
+    ref = load_ref(fast=True) if kind == "reference" else None
     tpl = Template(lib, sr=sr, seed=7)
     chains = []
     for i in idx:
@@ -141,14 +151,39 @@ def _cpu_worker(args):
     return len(idx) * blocks * 128, time.perf_counter() - t0
 
 
+def host_info():
+    """CPU model, glibc version, visible cores and the core lease of this process."""
+    import platform
+    model = None
+    try:
+        for ln in Path("/proc/cpuinfo").read_text().splitlines():
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        visible = len(os.sched_getaffinity(0))
+    except AttributeError:
+        visible = os.cpu_count() or 1
+    lease = os.environ.get("OMP_NUM_THREADS")
+    return {"cpu_model": model, "glibc": "-".join(platform.libc_ver()), "cores_visible": visible,
+            "core_lease": int(lease) if lease and lease.isdigit() else None}
+
+
 def cpu_baseline(n_inst, blocks, sr):
     import multiprocessing as mp
-    kind = "reference" if (ROOT / "oracle" / "_ref" / "libtbfref.so").exists() else "port"
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16, n_inst))
+    from orc_bind import REF_FAST_SO, REF_SO
+    kind = "reference" if (REF_FAST_SO.exists() or REF_SO.exists()) else "port"
+    build = None
+    if kind == "reference":
+        build = ("-O3 -ffast-math -fno-finite-math-only (the reference's release flags, common.mak:16-18)"
+                 if REF_FAST_SO.exists() else "-O2 -ffp-contract=off (strict build; release build absent)")
+    hi = host_info()
+    # every core this process may use: the GPU box leases a fixed share of the host per GPU
+    # (OMP_NUM_THREADS there; nproc shows the whole machine), so that share is the pool
+    cores = hi["core_lease"] or hi["cores_visible"]
+    cores = max(1, min(cores, hi["cores_visible"], n_inst))
     parts = [list(range(k, n_inst, cores)) for k in range(cores)]
     ctx = mp.get_context("spawn")
     t0 = time.perf_counter()
@@ -158,37 +193,77 @@ def cpu_baseline(n_inst, blocks, sr):
     samples = sum(r[0] for r in res)
     busy = max(r[1] for r in res)  # render time of the slowest worker (construction excluded)
     what = ("the reference's src/tonegen.cpp, vibrato.cpp, overdrive.cpp, reverb.cpp, whirl.cpp "
-            "compiled by oracle/Makefile (gcc -O2)" if kind == "reference" else "oracle/ C restatement")
+            f"compiled by oracle/Makefile, {build}" if kind == "reference" else "oracle/ C restatement")
     return {"value": samples / busy, "unit": "stereo samples/s", "cores": cores, "kind": kind,
             "sample": f"{n_inst} instances x {blocks} blocks ({blocks * 128 / sr:.2f} s audio each), "
-                      f"{what}, {cores} processes, construction excluded (wall {wall:.1f}s)"}
+                      f"{what}, {cores} worker processes (one per leased core), construction excluded "
+                      f"(wall {wall:.1f}s)", **hi}
 
 
-def oracle_check(wl, rank_first, n_check, total_blocks, last_blocks, gpu_L, gpu_R):
-    """max|err| of the last step's outputs vs the CPU oracle for the first instances."""
-    import numpy as np
+def oracle_run(wl, g, total_blocks, last_blocks):
+    """The oracle's L, R and stage taps (tonegen, preamp, reverb) of instance g over the
+    last `last_blocks` of `total_blocks`."""
     from orc_bind import Chain, Template, load_oracle
     lib = load_oracle()
-    tpls = {}
-    err, exact, tot = 0.0, 0, 0
+    j = wl.tuning_of(g)
+    tpl = Template(lib, sr=wl.sr, mts128=wl.mts[wl.names[j]], seed=wl.tpl_seed(j))
+    ch = Chain(lib, tpl, wl.seed_of(g))
+    if wl.kind == "cfg2":
+        ch.chain(1)
+    for (_, kind, a, v) in wl.scenario(g):
+        (ch.note if kind == "note" else ch.param)(a, v)
+    ch.render(total_blocks - last_blocks)
+    return ch.render(last_blocks, stages=True)
+
+
+def _err(x, y):
+    import numpy as np
+    d = np.abs(x.astype(np.float64) - y.astype(np.float64))
+    return float(d.max()) if d.size else 0.0, int(np.sum(x.view(np.uint32) == y.view(np.uint32))), x.size
+
+
+def stage_taps(T, wl, first, n_check, total_blocks, last_blocks, device):
+    """The GPU's tonegen / preamp / reverb stage outputs of the checked instances: small
+    engines in the parity-tap chain modes (TBF_CHAIN_TONEGEN / _TAP_PREAMP / _TAP_REVERB)
+    replaying the same instances and script for the same number of blocks."""
+    import numpy as np
+    taps = {}
+    for mode, name in ((1, "tonegen"), (2, "preamp"), (3, "reverb")):
+        if wl.kind == "cfg2" and mode > 1:
+            continue
+        eng = T.Engine(sample_rate=wl.sr, device=device, chain=mode)
+        setup_instances(eng, wl, first, n_check)
+        L = None
+        left = total_blocks
+        while left:
+            nb = min(left, 256)
+            L, _ = eng.render(nb)
+            left -= nb
+        taps[name] = L[:, -last_blocks * 128:] if L is not None else np.zeros((n_check, 0), np.float32)
+        eng.close()
+    return taps
+
+
+def oracle_check(wl, rank_first, n_check, total_blocks, last_blocks, gpu_L, gpu_R, taps=None):
+    """max|err| and bit-exact fraction of the last step's outputs vs the CPU oracle for
+    the first instances of this rank, and per stage when the GPU stage taps are given."""
+    stages = {"whirl_L": [0.0, 0, 0], "whirl_R": [0.0, 0, 0]}
     for i in range(n_check):
-        g = rank_first + i
-        j = wl.tuning_of(g)
-        if j not in tpls:
-            tpls[j] = Template(lib, sr=wl.sr, mts128=wl.mts[wl.names[j]], seed=wl.tpl_seed(j))
-        ch = Chain(lib, tpls[j], wl.seed_of(g))
-        if wl.kind == "cfg2":
-            ch.chain(1)
-        for (_, kind, a, v) in wl.scenario(g):
-            (ch.note if kind == "note" else ch.param)(a, v)
-        ch.render(total_blocks - last_blocks)
-        L, R = ch.render(last_blocks)
-        for x, y in ((gpu_L[i], L), (gpu_R[i], R)):
-            d = np.abs(x.astype(np.float64) - y.astype(np.float64))
-            err = max(err, float(d.max()))
-            exact += int(np.sum(x.view(np.uint32) == y.view(np.uint32)))
-            tot += x.size
-    return err, exact / max(tot, 1)
+        L, R, A, B, C = oracle_run(wl, rank_first + i, total_blocks, last_blocks)
+        pairs = [("whirl_L", gpu_L[i], L), ("whirl_R", gpu_R[i], R)]
+        if taps:
+            ref = {"tonegen": A, "preamp": B, "reverb": C}
+            pairs += [(k, taps[k][i], ref[k]) for k in taps]
+        for k, x, y in pairs:
+            e, ex, n = _err(x, y)
+            acc = stages.setdefault(k, [0.0, 0, 0])
+            acc[0] = max(acc[0], e)
+            acc[1] += ex
+            acc[2] += n
+    out = {k: {"max_err": v[0], "bit_exact_frac": v[1] / max(v[2], 1)} for k, v in stages.items()}
+    err = max(out["whirl_L"]["max_err"], out["whirl_R"]["max_err"])
+    exact = (stages["whirl_L"][1] + stages["whirl_R"][1]) / max(stages["whirl_L"][2] + stages["whirl_R"][2], 1)
+    return err, exact, out
 
 
 def main():
@@ -198,126 +273,163 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import numpy as np
     import torch
+    from tunebfree_amd.shard import shard
     dist = None
     if world > 1:
+        # the only cross-rank traffic is the barrier and three scalars (elapsed, max|err|,
+        # dry-run checksum): gloo on the host, no RCCL (the data path has no collective)
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    else:
-        torch.cuda.set_device(0)
+        dist.init_process_group("gloo")
+    if not a.dry_run:
+        torch.cuda.set_device(local if world > 1 else 0)
     import tunebfree_amd as T
 
-    B = a.batch
-    first_global = rank * B
+    # weak scaling: --batch instances per GPU, world * batch in all, contiguous shards
+    first_global, B = shard(a.batch * world, rank, world)
     if a.sr is None:
         a.sr = 96000.0 if a.workload == "cfg5" else 48000.0
     wl = Workload(a.workload, a.sr)
     if a.workload == "cfg2":
         a.chain = 1  # TBF_CHAIN_TONEGEN
-    eng = T.Engine(sample_rate=a.sr, device=torch.cuda.current_device(), chain=a.chain)
+    device = -1 if a.dry_run else torch.cuda.current_device()
+    eng = T.Engine(sample_rate=a.sr, device=device, chain=a.chain)
     setup_instances(eng, wl, first_global, B)
     nsamp = a.blocks * 128
-    outL = torch.empty((B, nsamp), dtype=torch.float32, device="cuda")
-    outR = torch.empty((B, nsamp), dtype=torch.float32, device="cuda")
-    stream = torch.cuda.Stream()  # a real stream: the kernel and the timing events share it
-    torch.cuda.set_stream(stream)
-    sptr = stream.cuda_stream
 
-    def step():
-        eng.render_device(a.blocks, outL.data_ptr(), outR.data_ptr(), nsamp, sptr)
+    def reduce(x, op="max"):
+        if not dist:
+            return float(x)
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def sync():
+        if not a.dry_run:
+            torch.cuda.synchronize()
+
+    if a.dry_run:
+        # no device: the "step" is the host control step a render makes per block for every
+        # instance of the shard (tbf_debug_render_program), so the contract runs end to end
+        import ctypes as C
+        lib = T.load_library()
+        fn = lib.tbf_debug_render_program
+        fn.restype, fn.argtypes = C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]
+        buf = np.zeros(9 * 600, np.float32)
+        chk = [0]
+
+        def step():  # exact integer checksum of every instance's program (order-independent)
+            for i in range(B):
+                n = fn(eng._h, i, buf.ctypes.data, 600)
+                chk[0] += int(buf[: 9 * n].view(np.uint32).astype(np.int64).sum()) * (first_global + i + 1)
+    else:
+        outL = torch.empty((B, nsamp), dtype=torch.float32, device="cuda")
+        outR = torch.empty((B, nsamp), dtype=torch.float32, device="cuda")
+        stream = torch.cuda.Stream()  # a real stream: the kernel and the timing events share it
+        torch.cuda.set_stream(stream)
+        sptr = stream.cuda_stream
+
+        def step():
+            eng.render_device(a.blocks, outL.data_ptr(), outR.data_ptr(), nsamp, sptr)
 
     for _ in range(a.warmup):
         step()
-    torch.cuda.synchronize()
+    sync()
     if dist:
         dist.barrier()
-    torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    sync()
     t0 = time.perf_counter()
     for k in range(a.steps):
-        ev[k][0].record(stream)
         step()
-        ev[k][1].record(stream)
-    torch.cuda.synchronize()
+    sync()
     if dist:
         dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if dist:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
-    total_samples = world * B * nsamp * a.steps
+    sync()
+    elapsed = reduce(time.perf_counter() - t0)
+    total_samples = world * a.batch * nsamp * a.steps  # every rank's instances (shard sums to world * batch)
     value = total_samples / elapsed
 
-    # per-kernel launch durations (HIP events on each launch's stream, inside the
-    # engine), rendered exactly like the timed region (cross-chunk pipelining on, so a
-    # duration includes the overlap with the neighbouring chunk's kernels); a separate
-    # pass so the events do not perturb the timed region above
+    kern, kern_iso, max_err, exact, per_stage = {}, None, None, None, None
+    launches = -(-a.blocks // CHUNK)  # launch sets per step (one per 64-block chunk)
     ksteps = a.steps if a.kernel_steps is None else a.kernel_steps
-    eng.kernel_times(True)
-    for _ in range(ksteps):
-        step()
-    torch.cuda.synchronize()
-    kt = eng.kernel_times()
-    eng.kernel_times(False)
-    kern = {k: v[0] / v[1] for k, v in kt.items() if v[1]}
-    kern_iso = None
-    if a.isolated:  # each kernel alone on the GPU (pipelining off): per-kernel tuning
-        eng.kernel_times("serial")
+    if not a.dry_run:
+        # per-kernel launch durations (HIP events on each launch's stream, inside the
+        # engine), rendered exactly like the timed region (cross-chunk pipelining on, so a
+        # duration includes the overlap with the neighbouring chunk's kernels); a separate
+        # pass so the events do not perturb the timed region above
+        eng.kernel_times(True)
         for _ in range(ksteps):
             step()
         torch.cuda.synchronize()
         kt = eng.kernel_times()
         eng.kernel_times(False)
-        kern_iso = {k: v[0] / v[1] for k, v in kt.items() if v[1]}
-
-    # parity on the last step (first --check instances of this rank)
-    gL = outL[: a.check].cpu().numpy()
-    gR = outR[: a.check].cpu().numpy()
-    total_blocks = (a.warmup + a.steps + ksteps * (2 if a.isolated else 1)) * a.blocks
-    max_err, exact = oracle_check(wl, first_global, a.check, total_blocks, a.blocks, gL, gR) if a.check else (None, None)
-    if dist:
-        e = torch.tensor([max_err or 0.0], dtype=torch.float64, device="cuda")
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        max_err = float(e.item())
+        kern = {k: v[0] / v[1] for k, v in kt.items() if v[1]}
+        if a.isolated:  # each kernel alone on the GPU (pipelining off): per-kernel tuning
+            eng.kernel_times("serial")
+            for _ in range(ksteps):
+                step()
+            torch.cuda.synchronize()
+            kt = eng.kernel_times()
+            eng.kernel_times(False)
+            kern_iso = {k: v[0] / v[1] for k, v in kt.items() if v[1]}
+        # parity on the last step (first --check instances of this rank), per stage
+        total_blocks = (a.warmup + a.steps + ksteps * (2 if a.isolated else 1)) * a.blocks
+        if a.check:
+            gL = outL[: a.check].cpu().numpy()
+            gR = outR[: a.check].cpu().numpy()
+            taps = stage_taps(T, wl, first_global, a.check, total_blocks, a.blocks, device) if a.stage_check else None
+            max_err, exact, per_stage = oracle_check(wl, first_global, a.check, total_blocks, a.blocks, gL, gR, taps)
+    dry_sum = reduce(chk[0] % (1 << 50), "sum") if a.dry_run else None
+    max_err = reduce(max_err or 0.0) if (a.check and not a.dry_run) else None
 
     if rank == 0:
-        samples_launch = B * nsamp
+        samples_launch = B * min(a.blocks, CHUNK) * 128  # stereo samples one launch of a stage renders
+        algo = dict(ALGO_BYTES)
         if a.chain == 1:  # tonegen only: k_tonegen writes L and R (8 B); bank reads are L2-resident
-            ALGO_BYTES["k_tonegen"] = 8
-        dom = DOMINANT if DOMINANT in kern else max(kern, key=kern.get)
-        achieved = samples_launch * ALGO_BYTES[dom] / (kern[dom] * 1e-3) / 1e9
-        traffic, traffic_src = None, None
-        if Path(a.traffic).exists():
-            tj = json.loads(Path(a.traffic).read_text())
-            if tj.get("workload") == {"batch": B, "blocks": a.blocks, "sr": a.sr, "chain": a.chain} \
-                    and dom in tj.get("kernels", {}):
-                traffic = tj["kernels"][dom]["bytes_per_launch"]
-                traffic_src = tj.get("source")
-        cpu = cpu_baseline(a.cpu_instances, a.cpu_blocks, a.sr) if (a.cpu_baseline and world == 1 and a.workload == "cfg3") else None
+            algo["k_tonegen"] = 8
+        roof = None
+        if kern:
+            dom = DOMINANT if DOMINANT in kern else max(kern, key=kern.get)
+            achieved = samples_launch * algo[dom] / (kern[dom] * 1e-3) / 1e9
+            traffic, traffic_src = None, None
+            if Path(a.traffic).exists():
+                tj = json.loads(Path(a.traffic).read_text())
+                if tj.get("workload") == {"batch": B, "blocks": a.blocks, "sr": a.sr, "chain": a.chain} \
+                        and dom in tj.get("kernels", {}):
+                    traffic = tj["kernels"][dom]["bytes_per_launch"]
+                    traffic_src = tj.get("source")
+            step_bytes = STEP_ALGO_BYTES if a.chain == 0 else sum(algo.values())
+            step_gbs = B * nsamp * step_bytes / (elapsed / a.steps) / 1e9  # per GPU
+            roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                    "kernel": dom, "kernel_ms_per_launch": kern[dom],
+                    "algorithmic_bytes_per_launch": samples_launch * algo[dom],
+                    "bytes_per_stereo_sample": algo[dom], "traffic_source": traffic_src,
+                    "launches_per_step": launches,
+                    "step_bytes_per_stereo_sample": step_bytes, "step_gbs_per_gpu": step_gbs,
+                    "step_frac": step_gbs / HBM_PEAK_GBS,
+                    "kernels_ms_per_launch": kern, "kernels_ms_isolated": kern_iso,
+                    "timing": "HIP events on each launch's stream while neighbouring chunks' "
+                              "kernels overlap (cross-chunk pipelining, as in the timed region)"}
+        cpu = cpu_baseline(a.cpu_instances, a.cpu_blocks, a.sr) \
+            if (a.cpu_baseline and world == 1 and a.workload == "cfg3" and not a.dry_run) else None
         line = {
             "metric": "stereo samples/sec whole-node, batch=4096 full chain @48kHz; max|err| vs CPU",
             "value": value, "unit": "stereo samples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32 (f64 reverb/overdrive)", "data": "synthetic",
-            "config": {"workload": wl.describe(B, world, a.blocks),
-                       "batch_per_gpu": B, "blocks_per_step": a.blocks, "sample_rate": a.sr,
+            "config": {"workload": wl.describe(a.batch, world, a.blocks),
+                       "batch_per_gpu": a.batch, "blocks_per_step": a.blocks, "sample_rate": a.sr,
                        "parallelism": f"instance-sharded x{world} (no collective)"},
             "max_err": max_err, "bit_exact_frac": exact, "checked_instances": a.check,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": dom, "kernel_ms_per_launch": kern[dom],
-                         "algorithmic_bytes_per_launch": samples_launch * ALGO_BYTES[dom],
-                         "bytes_per_stereo_sample": ALGO_BYTES[dom], "traffic_source": traffic_src,
-                         "kernels_ms_per_launch": kern, "kernels_ms_isolated": kern_iso,
-                         "timing": "HIP events on each launch's stream while neighbouring chunks' "
-                                   "kernels overlap (cross-chunk pipelining, as in the timed region)",
-                         "gpu_ms_per_step_events": kern_ms,
-                         "chain_gbs": value * sum(ALGO_BYTES[k] for k in kern) / 1e9},
+            "max_err_per_stage": per_stage,
+            "roofline": roof,
             "cpu_baseline": cpu,
         }
+        if a.dry_run:
+            line["dry_run"] = {"note": "host-only engines, no render: value/ms_per_step time one host "
+                                       "control step per instance and step, not the DSP chain",
+                               "shard_rank0": [first_global, B],
+                               "checksum": dry_sum}  # sum over ranks of per-instance program checksums
         print(json.dumps(line), flush=True)
     if dist:
         dist.barrier()

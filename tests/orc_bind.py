@@ -16,6 +16,9 @@ ROOT = Path(__file__).resolve().parents[1]
 ORC_SO = ROOT / "oracle" / "liborc.so"
 REF_SO = ROOT / "oracle" / "_ref" / "libtbfref.so"
 PIN_SO = ROOT / "oracle" / "_ref" / "libtbfpin.so"
+# the same reference TUs built with the reference's release flags (common.mak:16-18):
+# the CPU baseline's timing build (bench.py), never a parity checker
+REF_FAST_SO = ROOT / "oracle" / "_ref" / "fast" / "libtbfref.so"
 
 _fp = C.POINTER(C.c_float)
 _dp = C.POINTER(C.c_double)
@@ -71,11 +74,13 @@ def load_oracle():
     return lib
 
 
-def load_ref():
-    """The reference-compiled checker; None when not built (e.g. on the GPU box)."""
-    if not REF_SO.exists():
+def load_ref(fast=False):
+    """The reference-compiled checker (strict IEEE build); None when not built.  fast=True:
+    the release-flag build for timing (falls back to the strict one when absent)."""
+    path = REF_FAST_SO if fast and REF_FAST_SO.exists() else REF_SO
+    if not path.exists():
         return None
-    lib = C.CDLL(str(REF_SO))
+    lib = C.CDLL(str(path))
     lib.ref_inst_new.restype = C.c_void_p
     lib.ref_inst_new.argtypes = [C.c_void_p, C.c_uint]
     lib.ref_inst_free.argtypes = [C.c_void_p]

@@ -398,3 +398,41 @@ def test_host_templates_vs_reference_pins(tunings):
             assert hashlib.sha256(np.ascontiguousarray(v).tobytes()).hexdigest() == p[key], (p["tuning"], p["sr"], key)
     for e in engines.values():
         e.close()
+
+
+def _bench_json(args, nproc=None, port=None):
+    import json
+    import subprocess
+    import sys
+    cmd = [sys.executable]
+    if nproc:
+        cmd += ["-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}", "--master-addr",
+                "127.0.0.1", f"--master-port={port}"]
+    cmd += [str(ROOT / "bench.py")] + args
+    out = subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=240, cwd=str(ROOT)).stdout
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out  # rank 0 alone prints, exactly one JSON line
+    return json.loads(lines[0])
+
+
+def test_bench_world2_dry_run_gloo():
+    """bench.py itself at world size 2 (torch.distributed.run, gloo, host-only engines,
+    --dry-run): the ranks take their instance ranges from tunebfree_amd.shard, run the
+    timed region between barriers, reduce over ranks, and rank 0 prints one JSON line
+    with the contract's keys.  The sum over ranks of per-instance control checksums
+    equals the single-process run over the whole batch, so the shards cover every
+    instance exactly once with the right global indices."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    common = ["--dry-run", "1", "--steps", "2", "--warmup", "1", "--check", "0"]
+    one = _bench_json(common + ["--batch", "10"])
+    two = _bench_json(common + ["--gpus", "2", "--batch", "5"], nproc=2, port=port)
+    for d, n in ((one, 1), (two, 2)):
+        for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                  "scaling", "vs_baseline", "dtype", "data", "config"):
+            assert k in d, k
+        assert d["n_gpus"] == n and d["scaling"] == "weak" and d["value"] > 0
+    assert two["dry_run"]["shard_rank0"] == [0, 5]
+    assert two["dry_run"]["checksum"] == one["dry_run"]["checksum"]

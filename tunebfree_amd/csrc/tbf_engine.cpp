@@ -568,25 +568,39 @@ static int ensureDevice (tbf_engine* e)
 	if (int rc = drainStages (e))
 		return rc;
 	const uint32_t n = (uint32_t)e->inst.size ();
-	/* wave banks + template descriptors */
+	/* wave banks + template descriptors.  On the device each wheel's wave is followed by
+	 * its first TBF_BLK samples again, so a block's 128 samples from any position < len
+	 * are contiguous (the interpreter's wrap split, src/tonegen.cpp:3376-3402, becomes
+	 * plain indexing: len >= 384 > 128, so a block wraps at most once) */
 	size_t total = 0;
 	for (auto& t : e->tpls)
-		total += t->bank.size ();
+		for (int w = 1; w <= TBF_NW; w++)
+			total += t->len[w] + (t->len[w] ? TBF_BLK : 0);
 	if (e->bank.ensure (total) || e->tplDesc.ensure (e->tpls.size ()))
 		return fail (-12, "out of device memory (bank)");
 	std::vector<tbf_tpl_desc> desc (e->tpls.size ());
+	std::vector<float>        ext (total);
 	size_t                    o = 0;
 	for (size_t q = 0; q < e->tpls.size (); q++) {
 		const TgTemplate& t = *e->tpls[q];
-		HIPCHK (hipMemcpy (e->bank.p + o, t.bank.data (), t.bank.size () * sizeof (float), hipMemcpyHostToDevice));
-		for (int w = 0; w <= TBF_NW; w++) {
-			desc[q].off[w] = (uint32_t)(o + t.off[w]);
-			desc[q].len[w] = t.len[w];
+		memset (desc[q].off, 0, sizeof (desc[q].off));
+		memset (desc[q].len, 0, sizeof (desc[q].len));
+		for (int w = 1; w <= TBF_NW; w++) {
+			const uint32_t L = t.len[w];
+			desc[q].off[w]   = (uint32_t)o;
+			desc[q].len[w]   = L;
+			if (!L)
+				continue;
+			const float* src = t.bank.data () + t.off[w];
+			std::copy (src, src + L, ext.begin () + o);
+			for (uint32_t k = 0; k < TBF_BLK; k++)
+				ext[o + L + k] = src[k % L];
+			o += L + TBF_BLK;
 		}
 		memcpy (desc[q].attackEnv, t.attackEnv, sizeof (desc[q].attackEnv));
 		memcpy (desc[q].releaseEnv, t.releaseEnv, sizeof (desc[q].releaseEnv));
-		o += t.bank.size ();
 	}
+	HIPCHK (hipMemcpy (e->bank.p, ext.data (), total * sizeof (float), hipMemcpyHostToDevice));
 	HIPCHK (hipMemcpy (e->tplDesc.p, desc.data (), desc.size () * sizeof (tbf_tpl_desc), hipMemcpyHostToDevice));
 	/* shared tables */
 	if (e->vib.ensure (e->vibTab.size ()) || e->whTab.ensure (4 * (size_t)TBF_WH_TSTRIDE) || e->whBw.ensure (e->wt.bw.size ()) ||

@@ -164,9 +164,8 @@ struct TgLds {
 	float        prc[TBF_BLK];
 	union {
 		struct { /* core-program entries resolved by the interpreter prologue */
-			uint32_t base[TBF_NW + 8]; /* bank index of the wheel's current sample */
-			uint32_t lim[TBF_NW + 8];  /* samples before the wheel's wrap */
-			uint32_t len[TBF_NW + 8];  /* wheel length */
+			uint32_t base[TBF_NW + 8]; /* bank index of the wheel's current sample (the device
+			                            * bank repeats each wave's first 128 samples after it) */
 		} ent;
 		struct { /* vibrato + mixdown */
 			float   vout[TBF_BLK];
@@ -341,6 +340,8 @@ __device__ __forceinline__ double dither_add (double v, uint32_t fpd)
 	return v + t;
 }
 
+/* a lane's two samples (n, n + 64) of a 128-sample block: packed FP32 math */
+typedef float f2v __attribute__ ((ext_vector_type (2)));
 /* 4-byte-aligned float pairs / quads: one global load for consecutive table entries */
 typedef float f2u __attribute__ ((ext_vector_type (2), aligned (4)));
 typedef float f4u __attribute__ ((ext_vector_type (4), aligned (4)));
@@ -375,62 +376,65 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 	tbf_tg_state&         st   = sm.st;
 	const tbf_prog_entry* __restrict__ prog = P.prog + G.prog_off;
 	const int             np   = (int)G.prog_len;
-	float                 sw0 = -0.f, sw1 = -0.f, vb0 = -0.f, vb1 = -0.f, pc0 = -0.f, pc1 = -0.f;
 
-	/* core interpreter (wrap split folded into the index).  Prologue, lane per entry:
-	 * resolve the wheel's bank position and advance st.pos (each wheel appears once per
-	 * program). */
+	/* core interpreter.  Prologue, lane per entry: resolve the wheel's bank position and
+	 * advance st.pos (each wheel appears once per program).  The device bank repeats each
+	 * wave's first 128 samples after its end, so the reference's wrap split
+	 * (src/tonegen.cpp:3376-3402) is plain indexing from base. */
+	int envHere = 0;
 	for (int e = lane; e < np; e += NL) {
-		const uint32_t w   = prog[e].wheel;
-		const uint32_t pos = st.pos[w];
-		const uint32_t len = T->len[w];
-		sm.u.ent.base[e]   = T->off[w] + pos;
-		sm.u.ent.lim[e]    = len - pos;
-		sm.u.ent.len[e]    = len;
-		st.pos[w]          = (len < pos + TBF_BLK) ? pos + TBF_BLK - len : pos + TBF_BLK;
+		const tbf_prog_entry& E   = prog[e];
+		const uint32_t        w   = E.wheel;
+		const uint32_t        pos = st.pos[w];
+		const uint32_t        len = T->len[w];
+		sm.u.ent.base[e]          = T->off[w] + pos;
+		st.pos[w]                 = (len < pos + TBF_BLK) ? pos + TBF_BLK - len : pos + TBF_BLK;
+		envHere |= E.env != 0;
 	}
+	const bool anyEnv = __any (envHere);
 	__syncthreads ();
-	/* main loop in program order (the adds keep the reference's order); unrolled so
-	 * several entries' wave loads are in flight together */
+	/* main loop in program order (the adds keep the reference's order); a lane holds
+	 * samples lane and lane + 64 as a pair, so each bus costs one packed multiply and one
+	 * packed add (v_pk_mul_f32 / v_pk_add_f32: two IEEE float ops, no contraction).  The
+	 * loops have no data-dependent branch, so the unrolled entries' loads are in flight
+	 * together.  The sums start at -0.f: -0 + a == a for every a, so the first entry's add
+	 * equals the reference's copy (CR_CPY). */
+	f2v sw = {-0.f, -0.f}, vb = {-0.f, -0.f}, pc = {-0.f, -0.f};
+	if (!anyEnv) { /* steady program: x * g (src/tonegen.cpp:3667-3685) */
 #pragma unroll TG_UNROLL
-	for (int e = 0; e < np; e++) {
-		const tbf_prog_entry E    = prog[e];
-		const uint32_t       base = sm.u.ent.base[e];
-		const uint32_t       lim  = sm.u.ent.lim[e];
-		const uint32_t       len  = sm.u.ent.len[e];
-		const uint32_t       i0   = (uint32_t)lane < lim ? base + lane : base + lane - len;
-		const uint32_t       i1   = (uint32_t)(lane + NL) < lim ? base + lane + NL : base + lane + NL - len;
-		const float          x0   = P.bank[i0];
-		const float          x1   = P.bank[i1];
-		float                a0, a1, b0, b1, c0, c1;
-		if (E.env) {
-			const float* ep = (E.env == 1 ? T->attackEnv[E.row] : T->releaseEnv[E.row]);
-			const float  e0 = ep[lane], e1 = ep[lane + NL];
-			const float  ds = E.nsg - E.sg, dv = E.nvg - E.vg, dp = E.npg - E.pg;
-			a0 = x0 * (E.sg + (e0 * ds));
-			a1 = x1 * (E.sg + (e1 * ds));
-			b0 = x0 * (E.vg + (e0 * dv));
-			b1 = x1 * (E.vg + (e1 * dv));
-			c0 = x0 * (E.pg + (e0 * dp));
-			c1 = x1 * (E.pg + (e1 * dp));
-		} else {
-			a0 = x0 * E.sg;
-			a1 = x1 * E.sg;
-			b0 = x0 * E.vg;
-			b1 = x1 * E.vg;
-			c0 = x0 * E.pg;
-			c1 = x1 * E.pg;
+		for (int e = 0; e < np; e++) {
+			const float* __restrict__ bp = P.bank + sm.u.ent.base[e];
+			const f2v                 x  = {bp[lane], bp[lane + NL]};
+			const tbf_prog_entry&     E  = prog[e];
+			sw = sw + x * E.sg;
+			vb = vb + x * E.vg;
+			pc = pc + x * E.pg;
 		}
-		/* the sums start at -0.f (below): -0 + a == a for every a, so the first entry's
-		 * add equals the reference's copy (CR_CPY) without a branch */
-		sw0 = sw0 + a0; sw1 = sw1 + a1; vb0 = vb0 + b0; vb1 = vb1 + b1; pc0 = pc0 + c0; pc1 = pc1 + c1;
+	} else { /* envelope entries x * (g + e (ng - g)) (3640-3662); steady entries take the same
+	          * expression with e = -0 and ng - g = +0: g + (-0 * +0) == g for every g */
+#pragma unroll TG_UNROLL
+		for (int e = 0; e < np; e++) {
+			const float* __restrict__ bp = P.bank + sm.u.ent.base[e];
+			const f2v                 x  = {bp[lane], bp[lane + NL]};
+			const tbf_prog_entry&     E  = prog[e];
+			const int                 en = E.env;
+			const float*              ep = (en == 2 ? T->releaseEnv[E.row & 7] : T->attackEnv[E.row & 7]);
+			f2v                       ev = {ep[lane], ep[lane + NL]};
+			ev                            = en ? ev : f2v{-0.f, -0.f};
+			const float               ds = en ? E.nsg - E.sg : 0.f;
+			const float               dv = en ? E.nvg - E.vg : 0.f;
+			const float               dp = en ? E.npg - E.pg : 0.f;
+			sw = sw + x * (E.sg + (ev * ds));
+			vb = vb + x * (E.vg + (ev * dv));
+			pc = pc + x * (E.pg + (ev * dp));
+		}
 	}
 	if (np == 0) /* no program: the buses stay cleared (+0) */
-		sw0 = sw1 = vb0 = vb1 = pc0 = pc1 = 0.f;
+		sw = vb = pc = f2v{0.f, 0.f};
 	__syncthreads (); /* the entry table is overwritten below */
-	sm.swl[lane] = sw0; sm.swl[lane + NL] = sw1;
-	sm.vin[lane] = vb0; sm.vin[lane + NL] = vb1;
-	sm.prc[lane] = pc0; sm.prc[lane + NL] = pc1;
+	sm.swl[lane] = sw.x; sm.swl[lane + NL] = sw.y;
+	sm.vin[lane] = vb.x; sm.vin[lane + NL] = vb.y;
+	sm.prc[lane] = pc.x; sm.prc[lane + NL] = pc.y;
 	__syncthreads ();
 
 	const uint32_t routing = G.routing;

@@ -95,6 +95,13 @@
 #define TG_UNROLL 4 /* program entries of the tonegen interpreter in flight */
 #endif
 
+/* timing-only ablations (wrong results; tools/gpu_ab.sh variants): bit 0 waveshaper sin,
+ * 1 vibrato gather, 2 tonegen serial chains, 3 overdrive dither jumps, 4 whirl ring
+ * accumulation, 5 whirl serial filters, 6 whirl motion table loads */
+#ifndef TBF_ABL
+#define TBF_ABL 0
+#endif
+
 /* optional stage timing (tbf_debug_profile): wave-clock cycles accumulated per mark.
  * Compiled in only with -DTBF_STAGE_PROF=1 (tools/prof_stages.py builds such a variant):
  * the product kernels keep their LDS for co-resident workgroups of the other chunk. */
@@ -474,7 +481,10 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 		bad = __any (bad) || (P.dbg & TBF_DEBUG_FORCE_SERIAL);
 		dmn = wave_min (dmn);
 		dmx = wave_max (dmx);
-		if (!bad) {
+		if (TBF_ABL & 2) {
+			sm.u.v.vout[lane] = sm.vin[lane];
+			sm.u.v.vout[lane + NL] = sm.vin[lane + NL];
+		} else if (!bad) {
 			/* sample m reaches slot wo iff m + d_m is wo or wo - 1: m in [wo-1-dmax, wo-dmin] */
 			for (int wo = lane; wo < TBF_BLK + 32; wo += NL) {
 				const uint32_t slot = (out0 + wo) & (TBF_VRING - 1);
@@ -523,7 +533,10 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 	/* mixdown, src/tonegen.cpp:3712-3777: the two per-sample gain chases run as
 	 * independent chains, lane 0 keyCompLevel += delta, lane 1 percEnvGain *= decay */
 	PRIO_UP ();
-	if (lane < 2) {
+	if ((TBF_ABL & 4) && lane < 2) {
+		for (int k = 0; k < TBF_BLK; k++)
+			(lane == 0 ? sm.u.v.kc : sm.u.v.pe)[k] = 0.5f;
+	} else if (lane < 2) {
 		const float keyCompDelta = (G.keyCompTarget - st.keyCompLevel) / (float)TBF_BLK;
 		const bool  perc         = (routing & 0x0C) != 0;
 		const float dec          = G.percEnvGainDecay;
@@ -588,7 +601,10 @@ __device__ void stage_overdrive (const tbf_launch& P, TgLds& sm, const tbf_seg_c
 	/* xorshift dither states F[0..128] (F[n+1] after sample n) by GF(2) jumps */
 	{
 		const uint32_t f0 = st.odFpd;
-#if XS_NIB
+#if TBF_ABL & 8
+		sm.u.od.fpd[lane + 1]      = f0 + lane;
+		sm.u.od.fpd[lane + 1 + NL] = f0 - lane;
+#elif XS_NIB
 		sm.u.od.fpd[lane + 1]      = xs_jump_n (P.xsJump, f0, lane + 1);
 		sm.u.od.fpd[lane + 1 + NL] = xs_jump_n (P.xsJump, f0, lane + 1 + NL);
 #else
@@ -612,7 +628,10 @@ __device__ void stage_overdrive (const tbf_launch& P, TgLds& sm, const tbf_seg_c
 	}
 	__syncthreads ();
 	PRIO_UP ();
-	if (lane < 2) {
+	if ((TBF_ABL & 4) && lane < 2) {
+		for (int k = lane; k < TBF_BLK; k += 2)
+			sm.u.od.odh[k] = sm.u.od.odx[k];
+	} else if (lane < 2) {
 		/* alternating one-pole HPF (fpFlip): lane 0 carries iirSampleA over the samples it
 		 * owns, lane 1 iirSampleB over the others; 128 samples keep fpFlip unchanged */
 		const int    start = ((lane == 0) == (st.fpFlip != 0)) ? 0 : 1;
@@ -646,13 +665,13 @@ __device__ void stage_overdrive (const tbf_launch& P, TgLds& sm, const tbf_seg_c
 			br = fabs (x) * 1.57079633;
 			if (br > 1.57079633)
 				br = 1.57079633;
-			br = sin (br);
+			br = (TBF_ABL & 1) ? br * 0.9 : sin (br);
 			x  = (x > 0.0) ? br : -br;
 		}
 		br = fabs (x) * 1.57079633;
 		if (br > 1.57079633)
 			br = 1.57079633;
-		br = G.odDensityPos ? sin (br) : 1 - cos (br);
+		br = (TBF_ABL & 1) ? br * 0.9 : (G.odDensityPos ? sin (br) : 1 - cos (br));
 		if (x > 0)
 			x = (x * (1 - G.odOut)) + (br * G.odOut);
 		else
@@ -1619,6 +1638,27 @@ __device__ __forceinline__ void motion_add (float* ring, int U, float a, float b
 	}
 }
 
+/* motion_add for a motion whose slot advances by exactly one per sample over the
+ * sub-block (U_n = U_0 + n: the common case at slow and stopped rotor speeds): slot U_n
+ * receives b of sample n-1, then a of sample n; lane 63's b goes to slot U_63 + 1.  Lane
+ * 0's slot got sample -1's b in the previous sub-block.  Same adds, same order. */
+template <int W>
+__device__ __forceinline__ void unit_add (float* ring, int U, float a, float b, int lane)
+{
+	const uint32_t WM = (uint32_t)W - 1u;
+	const float    bp = lane_shr1 (b);
+	const uint32_t i0 = (uint32_t)U & WM;
+	float          v  = ring[i0];
+	if (lane > 0)
+		v += bp;
+	v += a;
+	ring[i0] = v;
+	if (lane == NL - 1) {
+		const uint32_t i1 = (i0 + 1u) & WM;
+		ring[i1]          = ring[i1] + b;
+	}
+}
+
 /* one DF2 state recurrence over a sub-block (one lane): tp[0..1] = temp[-2], temp[-1],
  * tp[2 + i] = temp[i]; scrub applies the block-end NaN scrub (src/whirl.cpp:1622-1630)
  * to the incoming state first */
@@ -1737,7 +1777,10 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 		}
 		if (WH_PRIO)
 			PRIO_UP ();
-		if (lane < 4 && (lane > 0 || aNext)) {
+		if ((TBF_ABL & 32) && lane < 4) {
+			for (int k = 0; k < TBF_SUB; k++)
+				sm.tmp[lane][2 + k] = 0.5f;
+		} else if (lane < 4 && (lane > 0 || aNext)) {
 			const float* ip = lane == 0 ? sm.xn : (lane == 1 ? sm.aOut : sm.rd[lane - 2]);
 			/* crossing into the next block: A's state gets that block's NaN scrub first */
 			wh_serial (ip, sm.tmp[lane], st.fz[lane], fa0, fa1, lane == 0 && sb + 1 == TBF_BLK / TBF_SUB);
@@ -1844,12 +1887,20 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 						const float    h1   = (float)(ang * (unsigned int)16384 + K.hornPhase[p]);
 						const float    hd   = frac1 (h1);
 						const unsigned hl   = ((unsigned int)floorf (h1)) & 16383u;
+#if TBF_ABL & 64
+						const f2u      dp   = {hd, h1};
+#else
 						const f2u      dp   = *(const f2u*)(dsp + hl); /* dsp[hl], dsp[(hl + 1) & 16383] */
+#endif
 						const float    intp = dp.x * (1.f - hd) + hd * dp.y;
 						const unsigned kk   = ((unsigned int)roundf (h1)) & 16383u;
 						t                   = K.hornSpacing[p] + intp + (float)outpos;
 						const float* b      = bw + 5 * kk;
+#if TBF_ABL & 64
+						const f4u    b4     = {hd, intp, h1, t};
+#else
 						const f4u    b4     = *(const f4u*)b;
+#endif
 						xa                  = b4.x * hist[n + 4];
 						xa += b4.y * hist[n + 3];
 						xa += b4.z * hist[n + 2];
@@ -1874,13 +1925,16 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 				}
 			}
 			TBF_MARK (23);
+			/* fast path preconditions (wave votes), per ring: each motion's slot
+			 * non-decreasing in n with groups of <= 2 equal slots, and the ring's motions
+			 * >= 2 slots apart in source order at every sample (so passes farthest-first
+			 * keep the per-slot order: a farther motion reaches a slot only at earlier
+			 * samples); per motion: unit steps (unit_add instead of motion_add) */
+			bool     okr[WH_MG];
+			uint32_t unit = 0;
+			bool     allOk = !(P.dbg & TBF_DEBUG_FORCE_SERIAL);
 #pragma unroll
 			for (int gi = 0; gi < WH_MG; gi++) {
-				const int r = r0 + gi;
-				/* fast path preconditions (wave vote): each motion's slot non-decreasing in n
-				 * with groups of <= 2 equal slots, and the ring's motions >= 2 slots apart in
-				 * source order at every sample (so passes farthest-first keep the per-slot
-				 * order: a farther motion reaches a slot only at earlier samples) */
 				int ok = (mu[gi][1] >= mu[gi][0] + 2) && (mu[gi][2] >= mu[gi][1] + 2);
 	#pragma unroll
 				for (int q = 0; q < 3; q++) {
@@ -1890,35 +1944,61 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 						ok = 0;
 					if (lane > 0 && lane < NL - 1 && up == mu[gi][q] && un == mu[gi][q])
 						ok = 0;
+					if (__all (lane == 0 || mu[gi][q] == up + 1))
+						unit |= 1u << (gi * 3 + q);
 				}
-				float* ring = sm.wring[r];
-				if (__all (ok) && !(P.dbg & TBF_DEBUG_FORCE_SERIAL)) {
-					motion_add<W> (ring, mu[gi][2], ma[gi][2], mb[gi][2], lane);
-					__syncthreads ();
-					motion_add<W> (ring, mu[gi][1], ma[gi][1], mb[gi][1], lane);
-					__syncthreads ();
-					motion_add<W> (ring, mu[gi][0], ma[gi][0], mb[gi][0], lane);
-					__syncthreads ();
-				} else {
-					/* serial replay in the reference order: sample-major, motions in source order */
-					if (lane == 0)
-						atomicOr (P.errFlags, (uint32_t)TBF_PATH_WH_MOTION);
-					for (int i = 0; i < TBF_SUB; i++) {
+				okr[gi] = __all (ok) && !(P.dbg & TBF_DEBUG_FORCE_SERIAL);
+				allOk   = allOk && okr[gi];
+			}
+			if (TBF_ABL & 16) {
+				if (lane == 0)
+					sm.wring[r0][mu[0][0] & (W - 1)] += ma[0][0] + mb[0][1] + ma[0][2];
+			} else if (allOk) {
+				/* every ring on its fast path: the rings are independent, so each pass
+				 * (farthest motion first) updates all of them in one LDS round trip */
 	#pragma unroll
-						for (int q = 0; q < 3; q++) {
-							const uint32_t sl = (uint32_t)__shfl (mu[gi][q], i) & WM;
-							const float    aa = __shfl (ma[gi][q], i);
-							const float    bb = __shfl (mb[gi][q], i);
-							if (lane == 0) {
-								ring[sl] += aa;
-								ring[(sl + 1) & WM] += bb;
-							}
-						}
+				for (int q = 2; q >= 0; q--) {
+	#pragma unroll
+					for (int gi = 0; gi < WH_MG; gi++) {
+						if ((unit >> (gi * 3 + q)) & 1u)
+							unit_add<W> (sm.wring[r0 + gi], mu[gi][q], ma[gi][q], mb[gi][q], lane);
+						else
+							motion_add<W> (sm.wring[r0 + gi], mu[gi][q], ma[gi][q], mb[gi][q], lane);
 					}
 					__syncthreads ();
 				}
-				TBF_MARK (24);
+			} else {
+#pragma unroll
+				for (int gi = 0; gi < WH_MG; gi++) {
+					float* ring = sm.wring[r0 + gi];
+					if (okr[gi]) {
+						motion_add<W> (ring, mu[gi][2], ma[gi][2], mb[gi][2], lane);
+						__syncthreads ();
+						motion_add<W> (ring, mu[gi][1], ma[gi][1], mb[gi][1], lane);
+						__syncthreads ();
+						motion_add<W> (ring, mu[gi][0], ma[gi][0], mb[gi][0], lane);
+						__syncthreads ();
+					} else {
+						/* serial replay in the reference order: sample-major, motions in source order */
+						if (lane == 0)
+							atomicOr (P.errFlags, (uint32_t)TBF_PATH_WH_MOTION);
+						for (int i = 0; i < TBF_SUB; i++) {
+		#pragma unroll
+							for (int q = 0; q < 3; q++) {
+								const uint32_t sl = (uint32_t)__shfl (mu[gi][q], i) & WM;
+								const float    aa = __shfl (ma[gi][q], i);
+								const float    bb = __shfl (mb[gi][q], i);
+								if (lane == 0) {
+									ring[sl] += aa;
+									ring[(sl + 1) & WM] += bb;
+								}
+							}
+						}
+						__syncthreads ();
+					}
+				}
 			}
+			TBF_MARK (24);
 		}
 		/* ---- outputs (whirlProc2 outHL/outHR/outDL/outDR + whirlProc3 mix) ---- */
 		{

@@ -224,8 +224,8 @@ class Engine:
         if enable is not None:
             _check(fn(self._h, -1 if not enable else (2 if enable == "serial" else 1), None, None))
             return None
-        ms = np.zeros(len(STAGES), np.float64)
-        cnt = np.zeros(len(STAGES), np.uint32)
+        ms = np.zeros(8, np.float64)  # room for any build's stage count (A/B against older builds)
+        cnt = np.zeros(8, np.uint32)
         _check(fn(self._h, 0, ms.ctypes.data, cnt.ctypes.data))
         return {k: (float(ms[i]), int(cnt[i])) for i, k in enumerate(STAGES)}
 

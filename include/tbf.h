@@ -83,6 +83,32 @@ const char* tbf_last_error (void);
 int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out);
 int tbf_engine_destroy (tbf_engine* e);
 
+/* ---- cfg keys (§8(f) row 4): the reference's `key=value` configuration lines ----
+ * parseConfigurationLine / distributeParameter (src/cfgParser.cpp:61-160) hand each line
+ * to every module; the ones that reach this engine are
+ *   whirl.*   whirlConfig (src/whirl.cpp:992-1160): speeds, accelerations, geometry
+ *             (horn/drum radius, mic distance, horn offsets), the three filters,
+ *             horn level / leak, mic widths and angle, brake positions, speed preset,
+ *             bypass.  Geometry re-derives the compact ring window (512 / 1024 / 2048)
+ *   scanner.* scannerConfig (src/vibrato.cpp:334-357): scanner frequency, V1-V3 depths
+ *   reverb.mix reverbConfig (src/reverb.cpp:242-256)
+ *   osc.*     oscConfig's scalar keys (src/tonegen.cpp:2173-2555): x-precision, the
+ *             key-click / release envelope models, levels and lengths, percussion
+ *             gains, buses and trigger bus (osc.perc.fast / .slow are stored but, as in
+ *             the reference, never reach the decay constants)
+ * A setting applies to what is built after it: whirl.* tables and scanner.* shape
+ * engine-wide tables and must precede tbf_instances_add (-16 after); osc.* template
+ * keys apply to later tbf_template_create / tbf_templates_create; the rest to later
+ * tbf_instances_add.  Returns 0 applied, 1 not a key of this path (ignored, as the
+ * reference ignores it; overdrive.* / xov.* are accepted with no effect: ampConfig,
+ * src/overdrive.cpp:395-433, writes fields airwindows_density never reads), -22 bad
+ * value (nothing assigned), -95 a key of these modules this engine does not implement
+ * (osc list models, EQ macros, crosstalk levels, tuning, the comb filter). */
+int tbf_config_set (tbf_engine* e, const char* key, const char* value);
+/* a cfg file's text (`name = value` lines, '#' comments): returns the number of keys
+ * applied, or < 0 with tbf_last_error () = "line N: message" */
+int tbf_config_parse (tbf_engine* e, const char* text);
+
 /* Tone-generator template (initToneGenerator's shared tables: wave bank, play matrix,
  * envelopes) for one tuning.  mts128: 128 MTS-ESP note frequencies or NULL for the
  * no-master 12-TET table; ratio9: drawbar target ratios or NULL for

@@ -63,6 +63,49 @@ typedef struct {
 	int     n, cap;
 } orc_list;
 
+/* ---------------- configuration: the cfg keys of the hot path ----------------
+ * Restates the assignments of whirlConfig (src/whirl.cpp:992-1160), oscConfig
+ * (src/tonegen.cpp:2173-2555, the scalar keys), scannerConfig (src/vibrato.cpp:334-357)
+ * and reverbConfig (src/reverb.cpp:242-256), with the defaults of initValues
+ * (src/whirl.cpp:43-134, src/tonegen.cpp:238-331, src/vibrato.cpp:296-300) and the
+ * reverb ctor (src/reverb.cpp:217).  overdrive.* / xov.* (ampConfig,
+ * src/overdrive.cpp:395-433) only write legacy fields airwindows_density never reads,
+ * so they are accepted and have no effect, as in the reference. */
+#define ORC_ENV_CLICK 0
+#define ORC_ENV_COSINE 1
+#define ORC_ENV_LINEAR 2
+#define ORC_ENV_SHELF 3
+typedef struct orc_cfg {
+	/* whirl.* (struct b_whirl field types) */
+	float  hornRPMslow, hornRPMfast, drumRPMslow, drumRPMfast;
+	float  hornAcc, hornDec, drumAcc, drumDec;
+	float  hornRadiusCm, drumRadiusCm, micDistCm, hornXOffsetCm, hornZOffsetCm;
+	float  hornLevel, leakLevel;
+	float  drumMicWidth, hornMicWidth;
+	int    lpT;
+	double lpF, lpQ, lpG;
+	float  haT, haF, haQ, haG, hbT, hbF, hbQ, hbG;
+	int    revSelect, bypass;
+	double micAngle, hnBrakePos, drBrakePos;
+	/* scanner.* */
+	double vibFqHertz, vib1OffAmp, vib2OffAmp, vib3OffAmp;
+	/* reverb.mix */
+	float  reverbMix;
+	/* osc.* */
+	double tgPrecision, percFastDecaySeconds, percSlowDecaySeconds;
+	float  percEnvGainResetNorm, percEnvGainResetSoft, percEnvScaling;
+	int    percSendBusA, percSendBusB, percTriggerBus;
+	float  envAttackClickLevel, envReleaseClickLevel;
+	int    envAtkClkMinLength, envAtkClkMaxLength; /* -1: from the sample rate */
+	int    envAttackModel, envReleaseModel;
+} orc_cfg;
+
+void   orc_cfg_default (orc_cfg* c);
+size_t orc_cfg_size (void);
+/* one cfg line's key and value: 1 applied, 0 not a key of the hot path (ignored), -1
+ * unparsable or out of range (not applied), as getConfigParameter_* (src/cfgParser.cpp) */
+int  orc_cfg_set (orc_cfg* c, const char* key, const char* value);
+
 /* ---------------- tonegen template: everything initToneGenerator builds ---------------- */
 typedef struct orc_template {
 	double sr;
@@ -83,6 +126,9 @@ typedef struct orc_template {
 } orc_template;
 
 orc_template* orc_template_new (double sr, const double* mts128, const double* ratio9, unsigned int seed);
+/* the same with the osc.* template keys of cfg (x-precision, envelope models/levels/lengths) */
+orc_template* orc_template_new_cfg (double sr, const double* mts128, const double* ratio9, unsigned int seed,
+                                    const orc_cfg* cfg);
 void          orc_template_free (orc_template* t);
 int           orc_template_dump (const orc_template* t, const char* dir);
 /* flat export of the wave bank (wheels 1..256 concatenated) for product cross-checks */
@@ -100,6 +146,9 @@ typedef struct orc_inst orc_inst;
  * then initSynth: tonegen runtime init, init_vibrato, initPreamp, initReverb,
  * initWhirl, setDrawBars(upper, {8,8,6,0,...}). */
 orc_inst* orc_inst_new (const orc_template* tpl, unsigned int seed);
+/* the same with cfg applied before each module's init, as the reference's startup
+ * parses the cfg between alloc* and init* (whirl, scanner, percussion, reverb.mix) */
+orc_inst* orc_inst_new_cfg (const orc_template* tpl, unsigned int seed, const orc_cfg* cfg);
 void      orc_inst_free (orc_inst* p);
 void      orc_note (orc_inst* p, int key, int on);                 /* oscKeyOn/Off */
 void      orc_set_param (orc_inst* p, int pid, double value);      /* CLAP setParam */

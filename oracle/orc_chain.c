@@ -10,17 +10,25 @@
 
 /* b_synth/lv2.cpp:336-353 allocSynth + 164-193 initSynth, with the tonegen template
  * shared between instances (batch protocol, SURVEY.md s7 "hard parts"). */
-orc_inst* orc_inst_new (const orc_template* tpl, unsigned int seed)
+orc_inst* orc_inst_new (const orc_template* tpl, unsigned int seed) { return orc_inst_new_cfg (tpl, seed, NULL); }
+
+orc_inst* orc_inst_new_cfg (const orc_template* tpl, unsigned int seed, const orc_cfg* cfg)
 {
 	static const unsigned int defaultPreset[9] = {8, 8, 6, 0, 0, 0, 0, 0, 0};
 	orc_inst*                 p                = (orc_inst*)calloc (1, sizeof (orc_inst));
 	orc_rand                  rnd;
+	orc_cfg                   dflt;
 	int                       i;
+	if (!cfg) {
+		orc_cfg_default (&dflt);
+		cfg = &dflt;
+	}
 	orc_srand (&rnd, seed);
 	p->rev = orc_reverb_alloc (&rnd, tpl->sr);   /* allocReverb: 18+ rand() */
-	p->wh  = orc_whirl_alloc (tpl->sr);          /* allocWhirl + initWhirl (no rand) */
+	p->rev->G = cfg->reverbMix;                  /* reverbConfig: setReverbMix */
+	p->wh  = orc_whirl_alloc (tpl->sr, cfg);     /* allocWhirl + whirlConfig + initWhirl (no rand) */
 	orc_preamp_init (&p->pre, &rnd, tpl->sr);    /* allocPreamp: 1+ rand(), initPreamp */
-	orc_tg_init (&p->tg, tpl);                   /* allocTonegen + initToneGenerator + init_vibrato */
+	orc_tg_init (&p->tg, tpl, cfg);              /* allocTonegen + oscConfig/scannerConfig + initToneGenerator + init_vibrato */
 	for (i = 0; i < 9; i++)                      /* setDrawBars (inst, 0, defaultPreset) */
 		orc_tg_set_drawbar (&p->tg, i, defaultPreset[i]);
 	return p;

@@ -588,42 +588,71 @@ static void computeOffsets (struct orc_whirl* w)
 }
 
 /* src/whirl.cpp:43-134 initValues, 956-986 initWhirl (initialize + computeRotationSpeeds) */
-struct orc_whirl* orc_whirl_alloc (double sr)
+struct orc_whirl* orc_whirl_alloc (double sr, const orc_cfg* c)
 {
 	struct orc_whirl* w = (struct orc_whirl*)calloc (1, sizeof (*w));
 	double            hfast, hslow, dfast, dslow;
-	w->hornRPMslow      = (float)(60.0 * 0.672);
-	w->hornRPMfast      = (float)(60.0 * 7.056);
-	w->drumRPMslow      = (float)(60.0 * 0.600);
-	w->drumRPMfast      = (float)(60.0 * 5.955);
-	w->hornAcc          = 0.161f;
-	w->hornDec          = 0.321f;
-	w->drumAcc          = 4.127f;
-	w->drumDec          = 1.371f;
+	orc_cfg           dflt;
+	if (!c) {
+		orc_cfg_default (&dflt);
+		c = &dflt;
+	}
+	/* initValues (43-134), then the cfg's whirlConfig assignments (992-1160) */
+	w->hornRPMslow      = c->hornRPMslow;
+	w->hornRPMfast      = c->hornRPMfast;
+	w->drumRPMslow      = c->drumRPMslow;
+	w->drumRPMfast      = c->drumRPMfast;
+	w->hornAcc          = c->hornAcc;
+	w->hornDec          = c->hornDec;
+	w->drumAcc          = c->drumAcc;
+	w->drumDec          = c->drumDec;
 	w->airSpeed         = 340.0f;
-	w->micDistCm        = 42.0f;
-	w->hornXOffsetCm    = 0.0f;
-	w->hornZOffsetCm    = 0.0f;
-	w->hornRadiusCm     = 19.2f;
-	w->drumRadiusCm     = 22.0f;
-	w->lpT              = 8;
-	w->lpF              = 811.9695;
-	w->lpQ              = 1.6016;
-	w->lpG              = -38.9291;
-	w->haT              = 0;
-	w->haF              = 4500;
-	w->haQ              = 2.7456f;
-	w->haG              = -30.0f;
-	w->hbT              = 7;
-	w->hbF              = 300.0f;
-	w->hbQ              = 1.0f;
-	w->hbG              = -30.0f;
+	w->micDistCm        = c->micDistCm;
+	w->hornXOffsetCm    = c->hornXOffsetCm;
+	w->hornZOffsetCm    = c->hornZOffsetCm;
+	w->hornRadiusCm     = c->hornRadiusCm;
+	w->drumRadiusCm     = c->drumRadiusCm;
+	w->lpT              = c->lpT;
+	w->lpF              = c->lpF;
+	w->lpQ              = c->lpQ;
+	w->lpG              = c->lpG;
+	w->haT              = c->haT;
+	w->haF              = c->haF;
+	w->haQ              = c->haQ;
+	w->haG              = c->haG;
+	w->hbT              = c->hbT;
+	w->hbF              = c->hbF;
+	w->hbQ              = c->hbQ;
+	w->hbG              = c->hbG;
 	w->hornMic_hll = w->drumMic_dll = 1.0f;
 	w->hornMic_hlr = w->drumMic_dlr = 0.0f;
 	w->hornMic_hrl = w->drumMic_drl = 0.0f;
 	w->hornMic_hrr = w->drumMic_drr = 1.0f;
-	w->hornLevel        = 0.7f;
-	w->leakLevel        = 0.15f;
+	if (c->drumMicWidth != 0.0f) { /* fsetDrumMicWidth (912-930; no-op at the current width 0) */
+		const float dw = c->drumMicWidth;
+		const float dwP = dw > 0.f ? (dw > 1.f ? 1.f : dw) : 0.f;
+		const float dwN = dw < 0.f ? (dw < -1.f ? 1.f : -dw) : 0.f;
+		w->drumMic_dll  = sqrtf (1.f - dwP);
+		w->drumMic_dlr  = sqrtf (0.f + dwP);
+		w->drumMic_drl  = sqrtf (0.f + dwN);
+		w->drumMic_drr  = sqrtf (1.f - dwN);
+	}
+	if (c->hornMicWidth != 0.0f) { /* fsetHornMicWidth (932-949) */
+		const float hw = c->hornMicWidth;
+		const float hwP = hw > 0.f ? (hw > 1.f ? 1.f : hw) : 0.f;
+		const float hwN = hw < 0.f ? (hw < -1.f ? 1.f : -hw) : 0.f;
+		w->hornMic_hll  = sqrtf (1.f - hwP);
+		w->hornMic_hlr  = sqrtf (0.f + hwP);
+		w->hornMic_hrl  = sqrtf (0.f + hwN);
+		w->hornMic_hrr  = sqrtf (1.f - hwN);
+	}
+	w->hornLevel        = c->hornLevel;
+	w->leakLevel        = c->leakLevel;
+	w->bypass           = c->bypass;
+	w->revSelect        = c->revSelect;
+	w->micAngle         = c->micAngle;
+	w->hnBrakePos       = c->hnBrakePos;
+	w->drBrakePos       = c->drBrakePos;
 	w->SampleRateD      = sr;
 	/* initialize (626-662) */
 	w->leakage = w->leakLevel * w->hornLevel;
@@ -903,7 +932,7 @@ void orc_whirl_run3 (struct orc_whirl* w, const float* inbuffer, float* outL, fl
 }
 
 /* ------------------------------------------------------------------ standalone stage API */
-orc_whirl* orc_whirl_new (double sr) { return orc_whirl_alloc (sr); }
+orc_whirl* orc_whirl_new (double sr) { return orc_whirl_alloc (sr, NULL); }
 void       orc_whirl_free (orc_whirl* w) { free (w); }
 void       orc_whirl_rev_option (orc_whirl* w, int n) { orc_whirl_use_rev_option (w, n, 2); }
 void       orc_whirl_proc3 (orc_whirl* w, const float* in, float* L, float* R, int n)

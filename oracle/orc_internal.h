@@ -151,7 +151,7 @@ struct orc_inst {
 };
 
 /* tonegen runtime (orc_tonegen.c) */
-void orc_tg_init (orc_tonegen* t, const orc_template* tpl);
+void orc_tg_init (orc_tonegen* t, const orc_template* tpl, const orc_cfg* c);
 void orc_tg_key_on (orc_tonegen* t, int key);
 void orc_tg_key_off (orc_tonegen* t, int key);
 void orc_tg_set_drawbar (orc_tonegen* t, int bus, unsigned int setting);
@@ -163,7 +163,7 @@ void orc_tg_set_perc_volume (orc_tonegen* t, int isSoft);
 void orc_tg_set_perc_fast (orc_tonegen* t, int isFast);
 void orc_tg_set_perc_first (orc_tonegen* t, int isFirst);
 void orc_tg_generate (orc_tonegen* t, float* buf);
-void orc_vibrato_init (orc_vibrato* v, double rate);
+void orc_vibrato_init (orc_vibrato* v, double rate, const orc_cfg* c);
 void orc_vibrato_proc (orc_vibrato* v, const float* in, float* out, size_t n);
 
 /* effects (orc_fx.c) */
@@ -172,7 +172,7 @@ void orc_preamp_set_character (struct orc_preamp* p, float A);
 void orc_preamp_run (struct orc_preamp* p, const float* in, float* out, int n);
 struct orc_reverb* orc_reverb_alloc (orc_rand* rnd, double sr);
 void orc_reverb_run (struct orc_reverb* r, const float* in, float* out, int n);
-struct orc_whirl* orc_whirl_alloc (double sr);
+struct orc_whirl* orc_whirl_alloc (double sr, const orc_cfg* c);
 void orc_whirl_use_rev_option (struct orc_whirl* w, int n, int signals);
 void orc_whirl_run3 (struct orc_whirl* w, const float* in, float* L, float* R, float* tL, float* tR, size_t n);
 void orc_eq_compute (int type, double fqHz, double Q, double dbG, double* C, double sr);

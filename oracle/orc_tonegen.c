@@ -373,31 +373,91 @@ static void initKeyCompTable (orc_template* t)
 
 /* src/tonegen.cpp:2562-2728 initEnvelopes with the default models
  * (attack = ENV_CLICK level 0.5, release = ENV_LINEAR; tonegen.cpp:247-251) */
-static void initEnvelopes (orc_template* t, orc_rand* rnd)
+static void initEnvelopes (orc_template* t, orc_rand* rnd, const orc_cfg* c)
 {
-	const float attackClickLevel = 0.50f;
-	int         b, i, burst, bound, start;
+	const double T = (double)(BSS - 1);
+	int          b, i, burst, bound, start;
 	for (b = 0; b < 9; b++) {
-		bound = t->envAtkClkMaxLength - t->envAtkClkMinLength;
-		if (bound < 1)
-			bound = 1;
-		burst = t->envAtkClkMinLength + (orc_rand_next (rnd) % bound);
-		if (BSS <= burst)
-			burst = BSS - 1;
-		start = (orc_rand_next (rnd) % (BSS - burst));
-		for (i = 0; i < start; i++)
-			t->attackEnv[b][i] = 0.0f;
-		for (; i < (start + burst); i++) {
-			double drnd        = ((double)orc_rand_next (rnd)) / (double)2147483647;
-			t->attackEnv[b][i] = (float)(1.0 - (attackClickLevel * drnd));
+		if (c->envAttackModel == ORC_ENV_CLICK) {
+			bound = t->envAtkClkMaxLength - t->envAtkClkMinLength;
+			if (bound < 1)
+				bound = 1;
+			burst = t->envAtkClkMinLength + (orc_rand_next (rnd) % bound);
+			if (BSS <= burst)
+				burst = BSS - 1;
+			start = (orc_rand_next (rnd) % (BSS - burst));
+			for (i = 0; i < start; i++)
+				t->attackEnv[b][i] = 0.0f;
+			for (; i < (start + burst); i++) {
+				double drnd        = ((double)orc_rand_next (rnd)) / (double)2147483647;
+				t->attackEnv[b][i] = (float)(1.0 - (c->envAttackClickLevel * drnd));
+			}
+			for (; i < BSS; i++)
+				t->attackEnv[b][i] = 1.0f;
+			t->attackEnv[b][0] = (float)(t->attackEnv[b][0] / 2.0);
+			for (i = 1; i < BSS; i++)
+				t->attackEnv[b][i] = (float)((float)(t->attackEnv[b][i - 1] + t->attackEnv[b][i]) / 2.0);
 		}
-		for (; i < BSS; i++)
-			t->attackEnv[b][i] = 1.0f;
-		t->attackEnv[b][0] = (float)(t->attackEnv[b][0] / 2.0);
-		for (i = 1; i < BSS; i++)
-			t->attackEnv[b][i] = (float)((float)(t->attackEnv[b][i - 1] + t->attackEnv[b][i]) / 2.0);
-		for (i = 0; i < BSS; i++)
-			t->releaseEnv[b][i] = ((float)i) / (float)BSS;
+		if (c->envAttackModel == ORC_ENV_SHELF) {
+			bound = t->envAtkClkMaxLength - t->envAtkClkMinLength;
+			if (bound < 1)
+				bound = 1;
+			start = orc_rand_next (rnd) % bound;
+			if ((BSS - 2) <= start)
+				start = BSS - 2;
+			for (i = 0; i < start; i++)
+				t->attackEnv[b][i] = 0.0f;
+			t->attackEnv[b][i + 0] = (float)0.33333333;
+			t->attackEnv[b][i + 1] = (float)0.66666666;
+			for (i = i + 2; i < BSS; i++)
+				t->attackEnv[b][i] = 1.0f;
+		}
+		if (c->envReleaseModel == ORC_ENV_SHELF) {
+			bound = t->envAtkClkMaxLength - t->envAtkClkMinLength;
+			if (bound < 1)
+				bound = 1;
+			start = orc_rand_next (rnd) % bound;
+			if ((BSS - 2) <= start)
+				start = BSS - 2;
+			for (i = 0; i < start; i++)
+				t->releaseEnv[b][i] = 0.0f;
+			t->releaseEnv[b][i + 0] = (float)0.33333333;
+			t->releaseEnv[b][i + 1] = (float)0.66666666;
+			for (i = i + 2; i < BSS; i++)
+				t->releaseEnv[b][i] = 1.0f;
+		}
+		if (c->envReleaseModel == ORC_ENV_CLICK) {
+			burst = 8 + (orc_rand_next (rnd) % 32);
+			start = (orc_rand_next (rnd) % (BSS - burst));
+			for (i = 0; i < start; i++)
+				t->releaseEnv[b][i] = 0.0f;
+			for (; i < (start + burst); i++) {
+				double drnd         = ((double)orc_rand_next (rnd)) / (double)2147483647;
+				t->releaseEnv[b][i] = (float)(1.0 - (c->envReleaseClickLevel * drnd));
+			}
+			for (; i < BSS; i++)
+				t->releaseEnv[b][i] = 1.0f;
+			t->releaseEnv[b][0] = (float)(t->releaseEnv[b][0] / 2.0);
+			for (i = 1; i < BSS; i++)
+				t->releaseEnv[b][i] = (float)((float)(t->releaseEnv[b][i - 1] + t->releaseEnv[b][i]) / 2.0);
+		}
+		if (c->envAttackModel == ORC_ENV_COSINE)
+			for (i = 0; i < BSS; i++) {
+				int    d          = BSS - (i + 1);
+				double a          = (M_PI * (double)d) / T;
+				t->attackEnv[b][i] = (float)(0.5 + (0.5 * cos (a)));
+			}
+		if (c->envReleaseModel == ORC_ENV_COSINE)
+			for (i = 0; i < BSS; i++) {
+				double a           = (M_PI * (double)i) / T;
+				t->releaseEnv[b][i] = (float)(0.5 - (0.5 * cos (a)));
+			}
+		if (c->envAttackModel == ORC_ENV_LINEAR)
+			for (i = 0; i < BSS; i++)
+				t->attackEnv[b][i] = ((float)i) / (float)BSS;
+		if (c->envReleaseModel == ORC_ENV_LINEAR)
+			for (i = 0; i < BSS; i++)
+				t->releaseEnv[b][i] = ((float)i) / (float)BSS;
 	}
 }
 
@@ -405,15 +465,30 @@ static void initEnvelopes (orc_template* t, orc_rand* rnd)
  * the rand() stream seeded explicitly (batch protocol). */
 orc_template* orc_template_new (double sr, const double* mts128, const double* ratio9, unsigned int seed)
 {
+	return orc_template_new_cfg (sr, mts128, ratio9, seed, NULL);
+}
+
+orc_template* orc_template_new_cfg (double sr, const double* mts128, const double* ratio9, unsigned int seed,
+                                    const orc_cfg* cfg)
+{
 	static const double defaultRatio[9] = {0.5, 1.5, 1, 2, 3, 4, 5, 6, 8};
 	orc_template*       t               = (orc_template*)calloc (1, sizeof (orc_template));
 	orc_rand            rnd;
+	orc_cfg             dflt;
 	int                 i, j;
 	double              harm[ORC_MAX_PARTIALS];
+	if (!cfg) {
+		orc_cfg_default (&dflt);
+		cfg = &dflt;
+	}
 	orc_srand (&rnd, seed);
 	t->sr                 = sr;
-	t->envAtkClkMinLength = (int)floor (sr * 8.0 / 22050.0);
-	t->envAtkClkMaxLength = (int)ceil (sr * 40.0 / 22050.0);
+	t->envAtkClkMinLength = cfg->envAtkClkMinLength;
+	t->envAtkClkMaxLength = cfg->envAtkClkMaxLength;
+	if (t->envAtkClkMinLength < 0)
+		t->envAtkClkMinLength = (int)floor (sr * 8.0 / 22050.0);
+	if (t->envAtkClkMaxLength < 0)
+		t->envAtkClkMaxLength = (int)ceil (sr * 40.0 / 22050.0);
 	if (t->envAtkClkMinLength > BSS)
 		t->envAtkClkMinLength = BSS;
 	if (t->envAtkClkMaxLength > BSS)
@@ -429,12 +504,12 @@ orc_template* orc_template_new (double sr, const double* mts128, const double* r
 		harm[j] = j == 0 ? 1.0 : 0.0;
 	for (i = 1; i <= NW; i++) {
 		t->wfreq[i] = oscFreq (t, i);
-		t->wlen[i]  = orc_fitwave (t->wfreq[i], 0.001, 3 * BSS, (int)(ceil (sr / 48000.0) * 4096), sr);
+		t->wlen[i]  = orc_fitwave (t->wfreq[i], cfg->tgPrecision, 3 * BSS, (int)(ceil (sr / 48000.0) * 4096), sr);
 		t->wave[i]  = (float*)malloc (sizeof (float) * t->wlen[i]);
 		writeSamples (t->wave[i], t->wlen[i], harm, t->watt[i], t->wfreq[i], sr, &rnd);
 	}
 	initKeyCompTable (t);
-	initEnvelopes (t, &rnd);
+	initEnvelopes (t, &rnd, cfg);
 	return t;
 }
 
@@ -585,7 +660,7 @@ int orc_template_dump (const orc_template* t, const char* dir)
 
 /* src/vibrato.cpp:312-329 reset_vibrato + init_vibrato (setScannerFrequency 91-95,
  * initIncrementTables 224-283, setVibrato(v, 0)) */
-void orc_vibrato_init (orc_vibrato* v, double rate)
+void orc_vibrato_init (orc_vibrato* v, double rate, const orc_cfg* c)
 {
 	int    i;
 	double S = 65536.0;
@@ -593,10 +668,10 @@ void orc_vibrato_init (orc_vibrato* v, double rate)
 	v->offsetTable     = v->offset3Table;
 	v->stator          = 0;
 	v->outPos          = 1023 / 2;
-	v->vib1OffAmp      = 3.0;
-	v->vib2OffAmp      = 6.0;
-	v->vib3OffAmp      = 9.0;
-	v->vibFqHertz      = 7.25;
+	v->vib1OffAmp      = c->vib1OffAmp;
+	v->vib2OffAmp      = c->vib2OffAmp;
+	v->vib3OffAmp      = c->vib3OffAmp;
+	v->vibFqHertz      = c->vibFqHertz;
 	v->statorIncrement = (unsigned int)(((v->vibFqHertz * 2048) / rate) * 65536.0);
 	for (i = 0; i < 2048; i++) {
 		double m           = sin ((2.0 * M_PI * i) / 2048);
@@ -733,20 +808,20 @@ void orc_tg_set_perc_first (orc_tonegen* t, int isFirst)
 
 /* allocTonegen (initValues, tonegen.cpp:238-331; resetVibrato) + the per-instance
  * part of initToneGenerator (tonegen.cpp:2914-3021) on a shared template. */
-void orc_tg_init (orc_tonegen* t, const orc_template* tpl)
+void orc_tg_init (orc_tonegen* t, const orc_template* tpl, const orc_cfg* c)
 {
 	int i, s;
 	memset (t, 0, sizeof (*t));
 	t->tpl                      = tpl;
 	t->percSendBus              = 4;
-	t->percSendBusA             = 3;
-	t->percSendBusB             = 4;
+	t->percSendBusA             = c->percSendBusA;
+	t->percSendBusB             = c->percSendBusB;
 	t->swellPedalGain           = 0.07f;
 	t->outputLevelTrim          = 0.07f;
-	t->percTriggerBus           = 8;
-	t->percEnvScaling           = 11.0f;
-	t->percEnvGainResetNorm     = 1.0f;
-	t->percEnvGainResetSoft     = 0.5012f;
+	t->percTriggerBus           = c->percTriggerBus;
+	t->percEnvScaling           = c->percEnvScaling;
+	t->percEnvGainResetNorm     = c->percEnvGainResetNorm;
+	t->percEnvGainResetSoft     = c->percEnvGainResetSoft;
 	t->percEnvGainDecayFastNorm = 0.9995f;
 	t->percEnvGainDecayFastSoft = 0.9995f;
 	t->percEnvGainDecaySlowNorm = 0.9999f;
@@ -776,7 +851,7 @@ void orc_tg_init (orc_tonegen* t, const orc_template* tpl)
 	orc_tg_set_perc_volume (t, 0);
 	orc_tg_set_perc_fast (t, 1);
 	orc_tg_set_perc_enabled (t, 0);
-	orc_vibrato_init (&t->vib, tpl->sr);
+	orc_vibrato_init (&t->vib, tpl->sr, c);
 }
 
 /* src/tonegen.cpp:3096-3166 oscKeyOff / oscKeyOn (msgQueue 1024 u16) */

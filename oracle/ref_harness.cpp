@@ -35,6 +35,11 @@
 
 #define API extern "C" __attribute__ ((visibility ("default")))
 
+/* defined with external linkage in src/tonegen.cpp:1853-1866 (no header declaration) */
+void setNormalPercussionGain (struct b_tonegen* t, double g);
+void setSoftPercussionGain (struct b_tonegen* t, double g);
+void setPercussionGainScaling (struct b_tonegen* t, double s);
+
 struct ref_inst {
 	b_tonegen*       t;
 	struct b_preamp* p;
@@ -63,10 +68,20 @@ static ListElement* mk_list (const orc_list* l)
 	return head;
 }
 
-static b_tonegen* ref_tonegen (const orc_template* tpl)
+static b_tonegen* ref_tonegen (const orc_template* tpl, const orc_cfg* c)
 {
 	b_tonegen* t = allocTonegen ();
 	int        i;
+	/* oscConfig's runtime keys (src/tonegen.cpp:2206-2237): field assignments and the
+	 * exported setters, between allocTonegen and initToneGenerator as at startup */
+	t->percFastDecaySeconds = c->percFastDecaySeconds;
+	t->percSlowDecaySeconds = c->percSlowDecaySeconds;
+	setNormalPercussionGain (t, c->percEnvGainResetNorm);
+	setSoftPercussionGain (t, c->percEnvGainResetSoft);
+	setPercussionGainScaling (t, c->percEnvScaling);
+	t->percSendBusA   = c->percSendBusA;
+	t->percSendBusB   = c->percSendBusB;
+	t->percTriggerBus = c->percTriggerBus;
 	/* initToneGenerator runtime part, tonegen.cpp:2909-2955 */
 	t->SampleRateD  = tpl->sr;
 	t->midi_cfg_ptr = NULL;
@@ -124,14 +139,86 @@ static b_tonegen* ref_tonegen (const orc_template* tpl)
 	return t;
 }
 
-API ref_inst* ref_inst_new (const orc_template* tpl, unsigned int seed)
+/* whirlConfig's assignments (src/whirl.cpp:992-1160) on the reference's own struct, between
+ * allocWhirl and initWhirl as at startup.  The mic-width setters fsetHornMicWidth /
+ * fsetDrumMicWidth (912-949) sit in the LV2-only part the CLAP define set compiles out;
+ * their four assignments each are replayed here. */
+static void ref_whirl_cfg (b_whirl* w, const orc_cfg* c)
 {
+	w->hornRPMslow   = c->hornRPMslow;
+	w->hornRPMfast   = c->hornRPMfast;
+	w->drumRPMslow   = c->drumRPMslow;
+	w->drumRPMfast   = c->drumRPMfast;
+	w->hornAcc       = c->hornAcc;
+	w->hornDec       = c->hornDec;
+	w->drumAcc       = c->drumAcc;
+	w->drumDec       = c->drumDec;
+	w->hornRadiusCm  = c->hornRadiusCm;
+	w->drumRadiusCm  = c->drumRadiusCm;
+	w->hornLevel     = c->hornLevel;
+	w->leakLevel     = c->leakLevel;
+	w->micDistCm     = c->micDistCm;
+	w->hornXOffsetCm = c->hornXOffsetCm;
+	w->hornZOffsetCm = c->hornZOffsetCm;
+	w->lpT           = c->lpT;
+	w->lpQ           = c->lpQ;
+	w->lpF           = c->lpF;
+	w->lpG           = c->lpG;
+	w->haT           = c->haT;
+	w->haF           = c->haF;
+	w->haQ           = c->haQ;
+	w->haG           = c->haG;
+	w->hbT           = c->hbT;
+	w->hbF           = c->hbF;
+	w->hbQ           = c->hbQ;
+	w->hbG           = c->hbG;
+	w->revSelect     = c->revSelect;
+	w->bypass        = c->bypass;
+	w->micAngle      = c->micAngle;
+	w->hnBrakePos    = c->hnBrakePos;
+	w->drBrakePos    = c->drBrakePos;
+	if (c->drumMicWidth != w->drumMicWidth) {
+		const float dw = c->drumMicWidth;
+		w->drumMicWidth = dw;
+		const float dwP = dw > 0.f ? (dw > 1.f ? 1.f : dw) : 0.f;
+		const float dwN = dw < 0.f ? (dw < -1.f ? 1.f : -dw) : 0.f;
+		w->drumMic_dll  = sqrtf (1.f - dwP);
+		w->drumMic_dlr  = sqrtf (0.f + dwP);
+		w->drumMic_drl  = sqrtf (0.f + dwN);
+		w->drumMic_drr  = sqrtf (1.f - dwN);
+	}
+	if (c->hornMicWidth != w->hornMicWidth) {
+		const float hw = c->hornMicWidth;
+		w->hornMicWidth = hw;
+		const float hwP = hw > 0.f ? (hw > 1.f ? 1.f : hw) : 0.f;
+		const float hwN = hw < 0.f ? (hw < -1.f ? 1.f : -hw) : 0.f;
+		w->hornMic_hll  = sqrtf (1.f - hwP);
+		w->hornMic_hlr  = sqrtf (0.f + hwP);
+		w->hornMic_hrl  = sqrtf (0.f + hwN);
+		w->hornMic_hrr  = sqrtf (1.f - hwN);
+	}
+}
+
+API ref_inst* ref_inst_new_cfg (const orc_template* tpl, unsigned int seed, const orc_cfg* cfg)
+{
+	orc_cfg dflt;
+	if (!cfg) {
+		orc_cfg_default (&dflt);
+		cfg = &dflt;
+	}
 	ref_inst* p = (ref_inst*)calloc (1, sizeof (ref_inst));
 	srand (seed);
 	p->r = allocReverb ();
+	setReverbMix (p->r, cfg->reverbMix); /* reverbConfig (src/reverb.cpp:242-256) */
 	p->w = allocWhirl ();
-	p->t = ref_tonegen (tpl);
+	ref_whirl_cfg (p->w, cfg);
+	p->t = ref_tonegen (tpl, cfg);
 	p->p = (struct b_preamp*)allocPreamp ();
+	/* scannerConfig (src/vibrato.cpp:334-357): the fields init_vibrato reads */
+	p->t->inst_vibrato.vibFqHertz = cfg->vibFqHertz;
+	p->t->inst_vibrato.vib1OffAmp = cfg->vib1OffAmp;
+	p->t->inst_vibrato.vib2OffAmp = cfg->vib2OffAmp;
+	p->t->inst_vibrato.vib3OffAmp = cfg->vib3OffAmp;
 	init_vibrato (&p->t->inst_vibrato, tpl->sr);
 	initPreamp (p->p, NULL, tpl->sr);
 	initReverb (p->r, NULL, tpl->sr);
@@ -141,6 +228,8 @@ API ref_inst* ref_inst_new (const orc_template* tpl, unsigned int seed)
 		setDrawBar (p->t, i, preset[i]);
 	return p;
 }
+
+API ref_inst* ref_inst_new (const orc_template* tpl, unsigned int seed) { return ref_inst_new_cfg (tpl, seed, NULL); }
 
 API void ref_inst_free (ref_inst* p)
 {

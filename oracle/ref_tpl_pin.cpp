@@ -26,17 +26,30 @@
 
 #include <stdint.h>
 
+#include "orc.h"
+
 #define PIN_API extern "C" __attribute__ ((visibility ("default")))
 
 /* Build one template's tables the reference's way.  Outputs (any may be NULL):
  *   bank[cap]          wave samples of wheels 1..256 concatenated (returns the total)
  *   lens[256]          wave lengths; wfreq[256] wheel frequencies
  *   atk[9*128], rel[9*128], kc[128]   envelopes and key-compression table */
-PIN_API long refpin_template (double sr, const double* freq300, const double* ratio9, unsigned int seed, float* bank,
-                              uint64_t cap, uint32_t* lens, double* wfreq, float* atk, float* rel, float* kc)
+PIN_API long refpin_template_cfg (double sr, const double* freq300, const double* ratio9, unsigned int seed,
+                                  const orc_cfg* cfg, float* bank, uint64_t cap, uint32_t* lens, double* wfreq, float* atk,
+                                  float* rel, float* kc)
 {
 	struct b_tonegen* t = allocTonegen ();
 	int               i;
+	if (cfg) { /* oscConfig's template keys, through the reference's own setters
+	            * (src/tonegen.cpp:479-485, 1868-1921), between alloc and init as at startup */
+		setWavePrecision (t, cfg->tgPrecision);
+		setEnvAttackModel (t, cfg->envAttackModel);
+		setEnvReleaseModel (t, cfg->envReleaseModel);
+		setEnvAttackClickLevel (t, cfg->envAttackClickLevel);
+		setEnvReleaseClickLevel (t, cfg->envReleaseClickLevel);
+		t->envAtkClkMinLength = cfg->envAtkClkMinLength; /* setEnvAtkClkMinLength's result */
+		t->envAtkClkMaxLength = cfg->envAtkClkMaxLength;
+	}
 	/* initToneGenerator, src/tonegen.cpp:2909-2955 */
 	t->SampleRateD  = sr;
 	t->midi_cfg_ptr = NULL;
@@ -98,4 +111,10 @@ PIN_API long refpin_template (double sr, const double* freq300, const double* ra
 	for (i = 1; i <= NOF_WHEELS; i++)
 		free (t->oscillators[i].wave);
 	return (long)total;
+}
+
+PIN_API long refpin_template (double sr, const double* freq300, const double* ratio9, unsigned int seed, float* bank,
+                              uint64_t cap, uint32_t* lens, double* wfreq, float* atk, float* rel, float* kc)
+{
+	return refpin_template_cfg (sr, freq300, ratio9, seed, NULL, bank, cap, lens, wfreq, atk, rel, kc);
 }

@@ -35,20 +35,28 @@ def digest(tables):
 
 
 def cases():
+    """(tuning, sr, seed, mts128, cfg set name or None)"""
     tun = json.loads((HERE / "tunings.json").read_text())
     names = sorted(tun)
     for sr in (48000.0, 96000.0):
         for j, nm in enumerate(names):
-            yield nm, sr, 300 + j, (None if tun[nm] is None else np.array(tun[nm], np.float64))
+            yield nm, sr, 300 + j, (None if tun[nm] is None else np.array(tun[nm], np.float64)), None
+    # the template cfg keys (envelope models / levels / lengths, x-precision)
+    for k, cfgname in enumerate(("envelopes", "envelopes2")):
+        yield "12TET", 48000.0, 400 + k, None, cfgname
 
 
 def main():
     orc, pin = load_oracle(), load_pin()
     if pin is None:
         raise SystemExit("oracle/_ref/libtbfpin.so not built (make -C oracle pin)")
+    import scenarios as S
+    from orc_bind import Cfg
     rows = []
-    for nm, sr, seed, m in cases():
-        rows.append({"tuning": nm, "sr": sr, "seed": seed, **digest(pin_template(pin, orc, sr, m, seed))})
+    for nm, sr, seed, m, cfgname in cases():
+        cfg = None if cfgname is None else Cfg(orc, S.CFG_SETS[cfgname])
+        rows.append({"tuning": nm, "sr": sr, "seed": seed, "cfg": cfgname,
+                     **digest(pin_template(pin, orc, sr, m, seed, cfg))})
     (HERE / "template_pins.json").write_text(json.dumps(rows, indent=1) + "\n")
     print(f"wrote template_pins.json: {len(rows)} templates")
 

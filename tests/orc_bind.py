@@ -55,6 +55,14 @@ def load_oracle():
     lib.orc_set_param.argtypes = [C.c_void_p, C.c_int, C.c_double]
     lib.orc_set_chain.argtypes = [C.c_void_p, C.c_int]
     lib.orc_render.argtypes = [C.c_void_p, C.c_int, _fp, _fp, _fp, _fp, _fp]
+    lib.orc_cfg_size.restype = C.c_size_t
+    lib.orc_cfg_default.argtypes = [C.c_void_p]
+    lib.orc_cfg_set.restype = C.c_int
+    lib.orc_cfg_set.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p]
+    lib.orc_template_new_cfg.restype = C.c_void_p
+    lib.orc_template_new_cfg.argtypes = [C.c_double, C.c_void_p, C.c_void_p, C.c_uint, C.c_void_p]
+    lib.orc_inst_new_cfg.restype = C.c_void_p
+    lib.orc_inst_new_cfg.argtypes = [C.c_void_p, C.c_uint, C.c_void_p]
     for pre in ("orc",):
         getattr(lib, f"{pre}_whirl_new").restype = C.c_void_p
         getattr(lib, f"{pre}_whirl_new").argtypes = [C.c_double]
@@ -84,6 +92,8 @@ def load_ref(fast=False):
     lib.ref_inst_new.restype = C.c_void_p
     lib.ref_inst_new.argtypes = [C.c_void_p, C.c_uint]
     lib.ref_inst_free.argtypes = [C.c_void_p]
+    lib.ref_inst_new_cfg.restype = C.c_void_p
+    lib.ref_inst_new_cfg.argtypes = [C.c_void_p, C.c_uint, C.c_void_p]
     lib.ref_note.argtypes = [C.c_void_p, C.c_int, C.c_int]
     lib.ref_set_param.argtypes = [C.c_void_p, C.c_int, C.c_double]
     lib.ref_set_chain.argtypes = [C.c_void_p, C.c_int]
@@ -115,40 +125,65 @@ def load_pin():
     lib.refpin_template.restype = C.c_long
     lib.refpin_template.argtypes = [C.c_double, _dp, C.c_void_p, C.c_uint, _fp, C.c_uint64, _u32p, _dp, _fp, _fp,
                                     _fp]
+    lib.refpin_template_cfg.restype = C.c_long
+    lib.refpin_template_cfg.argtypes = [C.c_double, _dp, C.c_void_p, C.c_uint, C.c_void_p, _fp, C.c_uint64, _u32p,
+                                        _dp, _fp, _fp, _fp]
     return lib
 
 
-def pin_template(pin, orc, sr, mts128, seed):
+def pin_template(pin, orc, sr, mts128, seed, cfg=None):
     """Wave bank, lengths, wheel frequencies, envelopes and key-compression table built by
-    the reference's own initOscillators / initKeyCompTable / initEnvelopes."""
+    the reference's own initOscillators / initKeyCompTable / initEnvelopes (with the
+    template keys of an oracle Cfg record, set through the reference's own setters)."""
     f300 = np.zeros(300, np.float64)
     m = None if mts128 is None else np.ascontiguousarray(mts128, np.float64)
     orc.orc_get_frequencies(f300.ctypes.data_as(_dp), None if m is None else m.ctypes.data)
-    n = pin.refpin_template(float(sr), f300.ctypes.data_as(_dp), None, int(seed), None, 0, None, None, None, None,
-                            None)
+    cp = None if cfg is None else cfg.ptr
+    n = pin.refpin_template_cfg(float(sr), f300.ctypes.data_as(_dp), None, int(seed), cp, None, 0, None, None, None,
+                                None, None)
     bank = np.zeros(n, np.float32)
     lens = np.zeros(256, np.uint32)
     wf = np.zeros(256, np.float64)
     a = np.zeros((9, 128), np.float32)
     r = np.zeros((9, 128), np.float32)
     k = np.zeros(128, np.float32)
-    pin.refpin_template(float(sr), f300.ctypes.data_as(_dp), None, int(seed), _f(bank), n, lens.ctypes.data_as(_u32p),
-                        wf.ctypes.data_as(_dp), _f(a), _f(r), _f(k))
+    pin.refpin_template_cfg(float(sr), f300.ctypes.data_as(_dp), None, int(seed), cp, _f(bank), n,
+                            lens.ctypes.data_as(_u32p), wf.ctypes.data_as(_dp), _f(a), _f(r), _f(k))
     return {"bank": bank, "lens": lens, "wfreq": wf, "attack": a, "release": r, "keycomp": k}
+
+
+class Cfg:
+    """An oracle cfg record (orc_cfg): the reference's defaults plus key=value lines."""
+
+    def __init__(self, lib, items=()):
+        self.lib = lib
+        self.buf = C.create_string_buffer(lib.orc_cfg_size())
+        lib.orc_cfg_default(self.buf)
+        for k, v in (items.items() if isinstance(items, dict) else items):
+            self.set(k, v)
+
+    def set(self, key, value):
+        return self.lib.orc_cfg_set(self.buf, str(key).encode(), str(value).encode())
+
+    @property
+    def ptr(self):
+        return C.cast(self.buf, C.c_void_p)
 
 
 class Template:
     """Tonegen template (wave bank + play matrix + envelopes) built by the oracle."""
 
-    def __init__(self, lib, sr=48000.0, mts128=None, ratio9=None, seed=1):
+    def __init__(self, lib, sr=48000.0, mts128=None, ratio9=None, seed=1, cfg=None):
         self.lib = lib
         self._mts = None if mts128 is None else np.ascontiguousarray(mts128, dtype=np.float64)
         self._rat = None if ratio9 is None else np.ascontiguousarray(ratio9, dtype=np.float64)
-        self.ptr = lib.orc_template_new(
+        self.cfg = cfg
+        self.ptr = lib.orc_template_new_cfg(
             float(sr),
             None if self._mts is None else self._mts.ctypes.data,
             None if self._rat is None else self._rat.ctypes.data,
             int(seed),
+            None if cfg is None else cfg.ptr,
         )
         self.sr = sr
 
@@ -179,16 +214,17 @@ class Template:
 class Chain:
     """One organ instance driven through either the oracle or the reference checker."""
 
-    def __init__(self, lib, tpl: Template, seed: int, ref: bool = False):
+    def __init__(self, lib, tpl: Template, seed: int, ref: bool = False, cfg=None):
         self.lib, self.ref = lib, ref
         p = "ref" if ref else "orc"
-        self._new = getattr(lib, f"{p}_inst_new")
+        self._new = getattr(lib, f"{p}_inst_new_cfg")
         self._note = getattr(lib, f"{p}_note")
         self._param = getattr(lib, f"{p}_set_param")
         self._chain = getattr(lib, f"{p}_set_chain")
         self._render = getattr(lib, f"{p}_render")
         self._free = getattr(lib, f"{p}_inst_free")
-        self.ptr = self._new(tpl.ptr, int(seed))
+        self.cfg = cfg if cfg is not None else tpl.cfg
+        self.ptr = self._new(tpl.ptr, int(seed), None if self.cfg is None else self.cfg.ptr)
         self.tpl = tpl
 
     def note(self, key, on):

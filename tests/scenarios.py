@@ -143,6 +143,42 @@ def reroute_scenario(i):
                                 (44, "param", P_DRAWBAR + 0, 0), (45, "param", P_DRAWBAR + 1, 2)]
 
 
+# cfg key sets (tbf_config_set / the oracle's orc_cfg / the reference structs' fields):
+# each reshapes the tables the engine builds after it (cfg keys)
+CFG_SETS = {
+    "geometry": {"whirl.horn.radius": 25, "whirl.drum.radius": 18, "whirl.mic.distance": 60,
+                 "whirl.horn.offset.x": 3, "whirl.horn.offset.z": -2},
+    "filters": {"whirl.drum.filter.type": 6, "whirl.drum.filter.hz": 700, "whirl.drum.filter.q": 1.2,
+                "whirl.drum.filter.gain": -20, "whirl.horn.filter.a.hz": 3800, "whirl.horn.filter.a.q": 1.8,
+                "whirl.horn.filter.b.type": 7, "whirl.horn.filter.b.hz": 350, "whirl.horn.filter.b.gain": -25,
+                "whirl.horn.filter.b.q": 1.3},
+    "brake": {"whirl.speed-preset": 1, "whirl.horn.brakepos": 0.75, "whirl.drum.brakepos": 0.5,
+              "whirl.horn.slowrpm": 48, "whirl.horn.fastrpm": 400, "whirl.drum.slowrpm": 40,
+              "whirl.drum.fastrpm": 342, "whirl.horn.acceleration": 0.3, "whirl.drum.deceleration": 2.0},
+    "mix": {"whirl.horn.level": 0.8, "whirl.horn.leak": 0.1, "whirl.horn.mic.angle": 150,
+            "whirl.horn.width": 0.4, "whirl.drum.width": -0.3, "scanner.hz": 6.5, "scanner.modulation.v3": 7.5,
+            "scanner.modulation.v1": 2.0, "reverb.mix": 0.3, "osc.perc.normal": 0.9, "osc.perc.soft": 0.4,
+            "osc.perc.gain": 9, "osc.perc.bus.a": 2, "osc.perc.bus.b": 5, "osc.perc.bus.trig": 7},
+    "envelopes": {"osc.attack.model": "shelf", "osc.release.model": "click", "osc.release.click.level": 0.4,
+                  "osc.attack.click.minlength": 0.05, "osc.attack.click.maxlength": 0.4, "osc.x-precision": 0.002},
+    "envelopes2": {"osc.attack.model": "cosine", "osc.release.model": "shelf", "osc.attack.click.level": 0.7,
+                   "osc.attack.click.maxlength": 0.3},
+}
+
+
+def cfg_scenario(i):
+    """For the cfg sets: the Jazz-1 registration without its rotary selection (the cfg's
+    speed preset holds at the start), chords, a note-off/on, then the rotor through
+    stop -> fast -> stop (the brake positions, when set) -> slow -> stop."""
+    ev = [(0, k, a, b) for (k, a, b) in jazz1_params() if a not in (P_DRUM, P_HORN)]
+    ev += [(0, "param", P_PERC_VOL, i & 1), (0, "param", P_VIBRATO_TYPE, 4 + (i & 1))]
+    ev += [(0, "note", k, 1) for k in chord_for(i)] + [(0, "note", 256 + 30 + i % 5, 1)]
+    ev += [(20, "note", k, 0) for k in chord_for(i)] + [(22, "note", k, 1) for k in chord_for(i + 3)]
+    for (b, d, h) in ((6, 0, 0), (9, 2, 2), (26, 0, 0), (48, 1, 1), (60, 0, 0)):
+        ev += [(b, "param", P_DRUM, d), (b, "param", P_HORN, h)]
+    return ev
+
+
 def random_drawbar_scenario(i, seed=None):
     """BASELINE config 5: upper drawbars from randomizeDrawbars (`rand() % 9` x 9,
     src/program.cpp:716-729) after srand(seed), rest of the Jazz-1 registration,

@@ -20,13 +20,15 @@ def _engine(chain=0, sr=48000.0, debug_flags=0):
     return T.Engine(sample_rate=sr, device=0, chain=chain, debug_flags=debug_flags)
 
 
-def _setup(oracle, n, scen_fn, chain=0, tpl_seed=7, sr=48000.0, debug_flags=0):
-    from orc_bind import Template
+def _setup(oracle, n, scen_fn, chain=0, tpl_seed=7, sr=48000.0, debug_flags=0, cfg=None):
+    from orc_bind import Cfg, Template
     eng = _engine(chain, sr, debug_flags)
+    if cfg is not None:  # as a cfg file's text, through tbf_config_parse
+        assert eng.config_parse("# cfg\n" + "".join(f"{k} = {v}\n" for k, v in cfg.items())) == len(cfg)
     tid = eng.template(seed=tpl_seed)
     seeds = [1000 + 17 * i for i in range(n)]
     eng.add_instances([tid] * n, seeds)
-    tpl = Template(oracle, sr=sr, seed=tpl_seed)
+    tpl = Template(oracle, sr=sr, seed=tpl_seed, cfg=None if cfg is None else Cfg(oracle, cfg))
     scens = [scen_fn(i) for i in range(n)]
     return eng, tpl, seeds, scens
 
@@ -316,7 +318,8 @@ def test_gpu_device_templates_match_oracle_and_reference(oracle, sr):
     from orc_bind import Template
     gold = Path(__file__).resolve().parent / "golden"
     tunings = json.loads((gold / "tunings.json").read_text())
-    pins = [p for p in json.loads((gold / "template_pins.json").read_text()) if p["sr"] == sr]
+    allpins = json.loads((gold / "template_pins.json").read_text())
+    pins = [p for p in allpins if p["sr"] == sr and not p.get("cfg")]
     eng = T.Engine(sample_rate=sr, device=0)
     lib = T.load_library()
     lib.tbf_debug_tables.restype = C.c_int
@@ -360,6 +363,24 @@ def test_gpu_device_templates_match_oracle_and_reference(oracle, sr):
     print(f"device templates @{sr:.0f}: {len(cases)} vs oracle, {len(pins)} vs reference pins; "
           f"first batch of {len(table_pins)} in {t_dev * 1e3:.1f} ms")
     eng.close()
+    # the template cfg keys (envelope models, lengths, levels, x-precision) on the device path
+    from orc_bind import Cfg
+    for p in [p for p in allpins if p["sr"] == sr and p.get("cfg")]:
+        eng = T.Engine(sample_rate=sr, device=0)
+        eng.config(S.CFG_SETS[p["cfg"]])
+        tid = eng.templates([p["seed"]])[0]
+        bank, lens = eng.template_bank(tid)
+        a, r, k = np.zeros((9, 128), np.float32), np.zeros((9, 128), np.float32), np.zeros(128, np.float32)
+        assert lib.tbf_debug_tables(eng._h, tid, a.ctypes.data, r.ctypes.data, k.ctypes.data) >= 0
+        got = {"bank": bank, "lens": lens, "attack": a, "release": r, "keycomp": k}
+        o = Template(oracle, sr=sr, mts128=None, seed=p["seed"], cfg=Cfg(oracle, S.CFG_SETS[p["cfg"]]))
+        ob, ol = o.bank()
+        oa, orr, ok = o.envs()
+        want = {"bank": ob, "lens": ol, "attack": oa, "release": orr, "keycomp": ok}
+        for key, v in got.items():
+            assert np.array_equal(np.asarray(v).view(np.uint32), np.asarray(want[key]).view(np.uint32)), (p["cfg"], key)
+            assert hashlib.sha256(np.ascontiguousarray(v).tobytes()).hexdigest() == p[key], (p["cfg"], key)
+        eng.close()
 
 
 def test_gpu_pipelined_chunks_across_calls(oracle):
@@ -452,6 +473,28 @@ def test_gpu_parameter_sweep(oracle, debug_flags):
     if debug_flags:
         want = T.engine.PATH_VIB_SERIAL | T.engine.PATH_WH_ANGLE | T.engine.PATH_WH_MOTION | T.engine.PATH_RV_PHASE
         assert flags & want == want, hex(flags)
+
+
+@pytest.mark.parametrize("name", sorted(S.CFG_SETS))
+def test_gpu_cfg_keys(oracle, name):
+    """§8(f) row 4: each cfg key set (scenarios.CFG_SETS — whirl geometry, the three
+    whirl filters, speed preset + rpm + brake positions, horn/drum mic mix and widths,
+    scanner rate/depths, reverb.mix, percussion gains/buses, the four envelope models)
+    given to the engine through tbf_config_parse before its templates and instances,
+    against the oracle under the same orc_cfg (itself bit-identical to the reference's
+    own structs, test_oracle_cpu.py::test_oracle_cfg_vs_reference): every stage tap,
+    6 instances over the rotor stop -> fast -> brake -> slow script."""
+    n, nb = 6, 72
+    eng, tpl, seeds, scens = _setup(oracle, n, S.cfg_scenario, cfg=S.CFG_SETS[name])
+    L, R = engine_run(eng, scens, nb)
+    oL, oR, oA, oB, oC = oracle_run(oracle, tpl, seeds, scens, nb)
+    eL, xL = compare(L, oL)
+    eR, xR = compare(R, oR)
+    print(f"cfg {name}: max|err| L={eL:.3g} R={eR:.3g} bit-exact L={xL:.6f} R={xR:.6f}")
+    assert max(eL, eR) <= TOL
+    for i in range(n):
+        assert float(np.abs(oL[i]).max()) > 1e-3
+    eng.close()
 
 
 def test_gpu_reroute_without_key_events(oracle):

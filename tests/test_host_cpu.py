@@ -368,6 +368,49 @@ def test_glibc_rand_jump_matches_literal_draws():
     assert np.array_equal(out[:, 0], out[:, 1])
 
 
+def test_config_api_semantics():
+    """tbf_config_set / tbf_config_parse return codes (include/tbf.h): applied, ignored
+    (keys of other modules; overdrive.* / xov.* accepted with no effect), bad values
+    (getConfigParameter_*'s ranges, src/cfgParser.cpp:453-620: nothing assigned),
+    unimplemented keys of these modules, engine-wide keys after instances exist, and the
+    parser's line-numbered errors."""
+    import scenarios as S
+    eng = T.Engine(device=-1)
+    assert eng.config_set("whirl.horn.radius", 25) == 0
+    assert eng.config_set("WHIRL.DRUM.RADIUS", 18) == 0  # strcasecmp, as the reference
+    assert eng.config_set("midi.upper.channel", 1) == 1
+    assert eng.config_set("overdrive.character", 0.5) == 1
+    assert eng.config_set("xov.ctl_biased", 0.3) == 1
+    for k, v in (("scanner.hz", 3.9), ("whirl.drum.filter.type", 9), ("reverb.mix", 1.5),
+                 ("whirl.horn.brakepos", -0.1), ("osc.perc.bus.trig", -2)):
+        with pytest.raises(T.TbfError, match="-22"):
+            eng.config_set(k, v)
+    for k in ("osc.tuning", "osc.temperament", "osc.crosstalk.k6", "whirl.horn.comb.a.feedback"):
+        with pytest.raises(T.TbfError, match="-95"):
+            eng.config_set(k, 1)
+    # geometry beyond the reference's 2048-sample ring is refused and leaves the engine as it was
+    with pytest.raises(T.TbfError, match="-22"):
+        eng.config_set("whirl.horn.radius", 1000)
+    assert eng.config_set("whirl.horn.radius", 25) == 0
+    txt = "# a cfg file\n\n  scanner.hz = 6.5  # comment\nmidi.lower.channel=2\nreverb.mix=0.3\n"
+    assert eng.config_parse(txt) == 2
+    with pytest.raises(T.TbfError, match="line 2"):
+        eng.config_parse("reverb.mix=0.2\nnot a key value line\n")
+    with pytest.raises(T.TbfError, match="line 3"):
+        eng.config_parse("reverb.mix=0.2\n\nscanner.hz=30\n")
+    tid = eng.template(seed=3)
+    eng.add_instances([tid], [5])
+    # engine-wide tables are fixed once instances exist; per-instance / template keys are not
+    for k, v in (("whirl.horn.radius", 20), ("scanner.modulation.v1", 4), ("whirl.horn.filter.a.hz", 3000)):
+        with pytest.raises(T.TbfError, match="-16"):
+            eng.config_set(k, v)
+    assert eng.config_set("reverb.mix", 0.2) == 0
+    assert eng.config_set("osc.attack.model", "cosine") == 0
+    assert eng.config_set("whirl.speed-preset", 2) == 0
+    eng.close()
+    assert S.CFG_SETS  # the parity sets: test_oracle_cpu / test_gpu_parity
+
+
 def test_device_templates_refused_on_host_engine():
     eng = T.Engine(sample_rate=48000.0, device=-1)
     with pytest.raises(RuntimeError):
@@ -387,7 +430,12 @@ def test_host_templates_vs_reference_pins(tunings):
     _bind_debug(lib)
     engines = {}
     for p in pins:
-        eng = engines.setdefault(p["sr"], T.Engine(sample_rate=p["sr"], device=-1))
+        key = (p["sr"], p.get("cfg"))
+        if key not in engines:
+            engines[key] = T.Engine(sample_rate=p["sr"], device=-1)
+            if p.get("cfg"):
+                engines[key].config(S.CFG_SETS[p["cfg"]])
+        eng = engines[key]
         m = None if tunings[p["tuning"]] is None else np.array(tunings[p["tuning"]], np.float64)
         tid = eng.template(mts128=m, seed=p["seed"])
         bank, lens = eng.template_bank(tid)

@@ -231,11 +231,13 @@ def test_oracle_templates_vs_reference_pins(oracle, tunings):
     48 / 96 kHz."""
     import hashlib
     from golden.make_template_pins import digest
+    from orc_bind import Cfg
     pins = _template_pins()
-    assert len(pins) == 14
+    assert len(pins) == 16
     for p in pins:
         m = None if tunings[p["tuning"]] is None else np.array(tunings[p["tuning"]], np.float64)
-        tpl = Template(oracle, sr=p["sr"], mts128=m, seed=p["seed"])
+        cfg = Cfg(oracle, S.CFG_SETS[p["cfg"]]) if p.get("cfg") else None
+        tpl = Template(oracle, sr=p["sr"], mts128=m, seed=p["seed"], cfg=cfg)
         bank, lens = tpl.bank()
         a, r, k = tpl.envs()
         got = {"bank": bank, "lens": lens, "attack": a, "release": r, "keycomp": k}
@@ -247,12 +249,46 @@ def test_reference_pin_harness_reproduces_committed_pins(oracle, tunings):
     """Where /root/reference is built (oracle/_ref/libtbfpin.so), the reference's own
     builders still give the committed digests (the fixture is current)."""
     from golden.make_template_pins import cases, digest
-    from orc_bind import load_pin, pin_template
+    from orc_bind import Cfg, load_pin, pin_template
     pin = load_pin()
     if pin is None:
         pytest.skip("oracle/_ref/libtbfpin.so not built (no /root/reference here)")
     pins = _template_pins()
-    for (nm, sr, seed, m), p in zip(cases(), pins):
-        d = digest(pin_template(pin, oracle, sr, m, seed))
-        assert {k: d[k] for k in p if k not in ("tuning", "sr", "seed")} == \
-            {k: p[k] for k in p if k not in ("tuning", "sr", "seed")}, (nm, sr)
+    meta = ("tuning", "sr", "seed", "cfg")
+    for (nm, sr, seed, m, cfgname), p in zip(cases(), pins):
+        cfg = Cfg(oracle, S.CFG_SETS[cfgname]) if cfgname else None
+        d = digest(pin_template(pin, oracle, sr, m, seed, cfg))
+        assert {k: d[k] for k in p if k not in meta} == {k: p[k] for k in p if k not in meta}, (nm, sr, cfgname)
+
+
+# --------------------------------------------------------------------------- cfg keys
+@pytest.mark.parametrize("name", sorted(S.CFG_SETS))
+def test_oracle_cfg_vs_reference(oracle, refchk, name):
+    """Each cfg key set (scenarios.CFG_SETS: whirl geometry, filters, speeds + brake
+    positions, mic mix / scanner / reverb.mix / percussion, envelope models) applied by
+    the oracle (orc_cfg_set) and, on the reference's own structs, by the harness: the
+    chain is bit-identical at every stage tap over a rotor stop -> fast -> brake -> slow
+    script."""
+    from orc_bind import Cfg
+    cfg = Cfg(oracle, S.CFG_SETS[name])
+    tpl = Template(oracle, sr=48000.0, seed=7, cfg=cfg)
+    for i in range(2):
+        sc = S.cfg_scenario(i)
+        a = S.run(Chain(oracle, tpl, 500 + i), sc, 72, stages=True)
+        b = S.run(Chain(refchk, tpl, 500 + i, ref=True), sc, 72, stages=True)
+        for k, x, y in zip("LRABC", a, b):
+            assert np.array_equal(x.view(np.uint32), y.view(np.uint32)), (name, i, k)
+        assert float(np.abs(a[0]).max()) > 1e-3
+
+
+def test_oracle_cfg_parsing(oracle):
+    """orc_cfg_set follows getConfigParameter_*: ranges are inclusive, a bad or
+    out-of-range value assigns nothing (-1), unknown keys are ignored (0)."""
+    from orc_bind import Cfg
+    c = Cfg(oracle)
+    assert c.set("whirl.horn.brakepos", "0.5") == 1
+    assert c.set("whirl.horn.brakepos", "1.5") == -1
+    assert c.set("whirl.drum.filter.type", "9") == -1
+    assert c.set("scanner.hz", "3.9") == -1 and c.set("scanner.hz", "4") == 1
+    assert c.set("WHIRL.HORN.RADIUS", "20") == 1  # strcasecmp
+    assert c.set("midi.upper.channel", "1") == 0

@@ -99,7 +99,7 @@ static void reverbConsts (tbf_inst_const& k, double sr, float A, float B, float 
 	k.slabLen = o;
 }
 
-static void whirlConsts (tbf_inst_const& k, const WhirlTables& wt)
+static void whirlConsts (tbf_inst_const& k, const WhirlTables& wt, const Config& c)
 {
 	memcpy (k.hafw, wt.hafw, sizeof (k.hafw));
 	memcpy (k.hbfw, wt.hbfw, sizeof (k.hbfw));
@@ -107,20 +107,41 @@ static void whirlConsts (tbf_inst_const& k, const WhirlTables& wt)
 	memcpy (k.hornSpacing, wt.hornSpacing, sizeof (k.hornSpacing));
 	memcpy (k.drumSpacing, wt.drumSpacing, sizeof (k.drumSpacing));
 	memcpy (k.hornPhase, wt.phase, sizeof (k.hornPhase));
-	const float hornLevel = 0.7f, leakLevel = 0.15f, micAngle = 0.0f;
-	k.leakage   = leakLevel * hornLevel;
-	k.hornLevel = hornLevel;
-	/* default mic widths 0 (src/whirl.cpp:113-117): hll dll hrr drr = 1, others 0 */
-	const float mic[8] = {1.0f, 0.0f, 1.0f, 0.0f, 0.0f, 1.0f, 0.0f, 1.0f};
+	/* initialize (src/whirl.cpp:626-662): leakage = leakLevel * hornLevel */
+	k.leakage   = c.leakLevel * c.hornLevel;
+	k.hornLevel = c.hornLevel;
+	/* mic widths (fsetHornMicWidth / fsetDrumMicWidth, src/whirl.cpp:912-949; width 0
+	 * leaves the initValues gains hll dll hrr drr = 1, others 0) */
+	float hll = 1.f, hlr = 0.f, hrl = 0.f, hrr = 1.f, dll = 1.f, dlr = 0.f, drl = 0.f, drr = 1.f;
+	if (c.drumMicWidth != 0.f) {
+		const float dw = c.drumMicWidth;
+		const float dwP = dw > 0.f ? (dw > 1.f ? 1.f : dw) : 0.f;
+		const float dwN = dw < 0.f ? (dw < -1.f ? 1.f : -dw) : 0.f;
+		dll = sqrtf (1.f - dwP);
+		dlr = sqrtf (0.f + dwP);
+		drl = sqrtf (0.f + dwN);
+		drr = sqrtf (1.f - dwN);
+	}
+	if (c.hornMicWidth != 0.f) {
+		const float hw = c.hornMicWidth;
+		const float hwP = hw > 0.f ? (hw > 1.f ? 1.f : hw) : 0.f;
+		const float hwN = hw < 0.f ? (hw < -1.f ? 1.f : -hw) : 0.f;
+		hll = sqrtf (1.f - hwP);
+		hlr = sqrtf (0.f + hwP);
+		hrl = sqrtf (0.f + hwN);
+		hrr = sqrtf (1.f - hwN);
+	}
+	const float mic[8] = {hll, hlr, dll, dlr, hrl, hrr, drl, drr};
 	memcpy (k.mic, mic, sizeof (mic));
-	k.fwAng = micAngle * .25;
-	k.bwAng = 1. + micAngle * -.25;
+	/* HN_MOTION / DR_MOTION angle offsets (src/whirl.cpp:1396-1400) */
+	k.fwAng = c.micAngle * .25;
+	k.bwAng = 1. + c.micAngle * -.25;
 	memcpy (k.lAcc, wt.lAcc, sizeof (k.lAcc));
 	k.deadzone = (.05 / (60.f * wt.sr));
 	memcpy (k.revHorn, wt.revHorn, sizeof (k.revHorn));
 	memcpy (k.revDrum, wt.revDrum, sizeof (k.revDrum));
-	k.hnBrakePos = 0;
-	k.drBrakePos = 0;
+	k.hnBrakePos = c.hnBrakePos;
+	k.drBrakePos = c.drBrakePos;
 	k.hnHardstop = (float)(10.f / (60.f * wt.sr));
 	k.drHardstop = (float)(8.f / (60.f * wt.sr));
 	k.minspeed   = (float)(3.f / (60.f * wt.sr));
@@ -172,6 +193,33 @@ void tbf::setCharacter (Instance& in, float value)
 	in.ctlDirty = true;
 }
 
+/* the engine-wide tables the cfg shapes: whirl displacement / IR tables, filters and
+ * speeds (initWhirl, src/whirl.cpp:956-986), the compact ring window derived from the
+ * geometry, the scanner's offset tables and stator increment (init_vibrato,
+ * src/vibrato.cpp:312-317) */
+static int buildShared (tbf_engine* e)
+{
+	const double sr = e->cfg.sample_rate;
+	e->wt.build (sr, e->conf);
+	/* compact whirl ring: live window < maxAhead + 2 + one sub-block */
+	uint32_t W = 512;
+	while ((float)W < e->wt.maxAhead + 2.0f + TBF_SUB + 2.0f)
+		W *= 2;
+	if (W > 2048)
+		return fail (-22, "whirl write-ahead exceeds the reference ring (2048 samples): geometry out of range");
+	e->wringLen = W;
+	/* vibrato tables (src/vibrato.cpp:91-95, 224-251) */
+	e->vibTab.resize (3 * 2048);
+	const double amp[3] = {e->conf.vib1OffAmp, e->conf.vib2OffAmp, e->conf.vib3OffAmp};
+	for (int t = 0; t < 3; t++)
+		for (int i = 0; i < 2048; i++) {
+			double m                = sin ((2.0 * M_PI * i) / 2048);
+			e->vibTab[t * 2048 + i] = (unsigned int)((1.0 + amp[t] + (m * amp[t])) * 65536.0);
+		}
+	e->statorInc = (unsigned int)(((e->conf.vibFqHertz * 2048) / sr) * 65536.0);
+	return 0;
+}
+
 extern "C" {
 
 int tbf_abi_version (void) { return TBF_ABI_VERSION; }
@@ -220,23 +268,9 @@ int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
 			}
 		}
 	}
-	e->wt.build (cfg->sample_rate);
-	/* compact whirl ring: live window < maxAhead + 2 + one sub-block */
-	e->wringLen = 512;
-	while ((float)e->wringLen < e->wt.maxAhead + 2.0f + TBF_SUB + 2.0f)
-		e->wringLen *= 2;
-	if (e->wringLen > 2048)
-		return fail (-22, "whirl write-ahead exceeds the reference ring");
-	/* vibrato tables (src/vibrato.cpp:91-95, 224-251) */
-	e->vibTab.resize (3 * 2048);
-	const double amp[3] = {3.0, 6.0, 9.0};
-	for (int t = 0; t < 3; t++)
-		for (int i = 0; i < 2048; i++) {
-			double m                  = sin ((2.0 * M_PI * i) / 2048);
-			e->vibTab[t * 2048 + i] = (unsigned int)((1.0 + amp[t] + (m * amp[t])) * 65536.0);
-		}
-	e->statorInc = (unsigned int)(((7.25 * 2048) / cfg->sample_rate) * 65536.0);
-	*out         = e.release ();
+	if (int rc = buildShared (e.get ()))
+		return rc;
+	*out = e.release ();
 	return 0;
 }
 
@@ -289,7 +323,7 @@ int tbf_template_create (tbf_engine* e, const double* mts128, const double* rati
 	if (!e || !id)
 		return fail (-22, "null argument");
 	std::unique_ptr<TgTemplate> t (new TgTemplate ());
-	t->build (e->cfg.sample_rate, mts128, ratio9, seed);
+	t->build (e->cfg.sample_rate, mts128, ratio9, seed, e->conf);
 	*id = (uint32_t)e->tpls.size ();
 	e->tpls.push_back (std::move (t));
 	e->deviceReady = false;
@@ -316,7 +350,7 @@ int tbf_templates_create (tbf_engine* e, uint32_t n, const double* mts128, const
 	for (uint32_t t = 0; t < n; t++) {
 		ts[t].reset (new TgTemplate ());
 		TgTemplate& T = *ts[t];
-		T.prepare (sr, mts128 ? mts128 + 128 * (size_t)t : nullptr, ratio9 ? ratio9 + 9 * (size_t)t : nullptr);
+		T.prepare (sr, mts128 ? mts128 + 128 * (size_t)t : nullptr, ratio9 ? ratio9 + 9 * (size_t)t : nullptr, e->conf);
 		uint32_t  W[31];
 		GlibcRand rnd (seeds[t]);
 		rnd.window (W);
@@ -445,18 +479,24 @@ int tbf_instances_add (tbf_engine* e, uint32_t n, const uint32_t* tpl_ids, const
 			for (int l = 0; l < 12; l++)
 				in.s0.rv.ch[c].count[l] = 1;
 		reverbConsts (in.k, sr, 1.0f, 0.2f, 0.0f, 0.0f, 0.4f, 0.8f);
-		whirlConsts (in.k, e->wt);
-		/* initWhirl -> computeRotationSpeeds -> setRevSelect(0) -> useRevOption(4) */
+		whirlConsts (in.k, e->wt, e->conf);
+		in.rvG      = e->conf.reverbMix;  /* reverbConfig: setReverbMix */
+		in.whBypass = e->conf.bypass;     /* whirlConfig: whirl.bypass */
+		/* initWhirl -> computeRotationSpeeds -> setRevSelect(revSelect) ->
+		 * useRevOption(revselects[revSelect]), revselects = {4, 0, 8} (src/whirl.cpp:226-293) */
+		static const int revselects[3] = {4, 0, 8};
+		const int        rs            = revselects[((e->conf.revSelect % 3) + 3) % 3];
+		in.revSelect                   = ((e->conf.revSelect % 3) + 3) % 3;
 		tbf_wh_state& w  = in.s0.wh;
-		w.hornTarget     = e->wt.revHorn[4];
-		w.drumTarget     = e->wt.revDrum[4];
+		w.hornTarget     = e->wt.revHorn[rs];
+		w.drumTarget     = e->wt.revDrum[rs];
 		w.hornAcDc       = w.hornIncr < w.hornTarget ? 1 : (w.hornTarget < w.hornIncr ? -1 : 0);
 		w.drumAcDc       = w.drumIncr < w.drumTarget ? 1 : (w.drumTarget < w.drumIncr ? -1 : 0);
 		/* tonegen + vibrato runtime state (initToneGenerator, reset_vibrato) */
 		in.s0.tg.keyCompLevel = 1.0f;
 		in.s0.tg.percEnvGain  = 0.0f;
 		in.s0.tg.outPos       = 1023 / 2;
-		in.tg.init (e->tpls[in.tpl].get ());
+		in.tg.init (e->tpls[in.tpl].get (), e->conf);
 		if (e->slabLen == 0)
 			e->slabLen = in.k.slabLen;
 		else if (e->slabLen != in.k.slabLen)
@@ -528,6 +568,70 @@ int tbf_set_param (tbf_engine* e, uint32_t i, int32_t index, double v)
 		return fail (-22, "unknown parameter id");
 	in.ctlDirty = true;
 	return 0;
+}
+
+int tbf_config_set (tbf_engine* e, const char* key, const char* value)
+{
+	if (!e || !key || !value)
+		return fail (-22, "null argument");
+	Config c     = e->conf;
+	int    scope = 0;
+	int    rc    = configSet (c, key, value, &scope);
+	if (rc == -1)
+		return fail (-22, std::string ("bad value for ") + key + ": " + value);
+	if (rc == -2)
+		return fail (-95, std::string ("cfg key not implemented by this engine: ") + key);
+	if (rc == 0)
+		return 1; /* not a key of the hot path: ignored, as the reference ignores it */
+	if ((scope & CFG_SHARED) && !e->inst.empty ())
+		return fail (-16, std::string (key) + " shapes the engine-wide tables: set it before tbf_instances_add");
+	const Config old = e->conf;
+	e->conf          = c;
+	if (scope & CFG_SHARED) {
+		if (int r = buildShared (e)) {
+			e->conf = old;
+			(void)buildShared (e);
+			return r;
+		}
+		e->deviceReady = false;
+	}
+	return 0;
+}
+
+int tbf_config_parse (tbf_engine* e, const char* text)
+{
+	if (!e || !text)
+		return fail (-22, "null argument");
+	/* parseConfigurationLine (src/cfgParser.cpp:94-160): `name = value`, '#' comments,
+	 * surrounding blanks trimmed */
+	int         applied = 0, line = 0;
+	const char* p       = text;
+	while (*p) {
+		const char* q = p;
+		while (*q && *q != '\n')
+			q++;
+		std::string ln (p, q);
+		p = *q ? q + 1 : q;
+		line++;
+		const size_t h = ln.find ('#');
+		if (h != std::string::npos)
+			ln.resize (h);
+		const size_t eq = ln.find ('=');
+		auto trim = [] (std::string s) {
+			const size_t a = s.find_first_not_of (" \t\r"), b = s.find_last_not_of (" \t\r");
+			return a == std::string::npos ? std::string () : s.substr (a, b - a + 1);
+		};
+		if (trim (ln).empty ())
+			continue;
+		if (eq == std::string::npos)
+			return fail (-22, "line " + std::to_string (line) + ": expected name=value");
+		const std::string k = trim (ln.substr (0, eq)), v = trim (ln.substr (eq + 1));
+		const int         rc = tbf_config_set (e, k.c_str (), v.c_str ());
+		if (rc < 0)
+			return fail (rc, "line " + std::to_string (line) + ": " + tbf_last_error ());
+		applied += rc == 0;
+	}
+	return applied;
 }
 
 } /* extern "C" */

@@ -95,6 +95,7 @@ using namespace tbf; /* private header: the engine's own translation units only 
 
 struct tbf_engine {
 	tbf_engine_config                       cfg;
+	Config                                  conf; /* cfg keys (tbf_config_set) for tables built from now on */
 	hipStream_t                             stream = nullptr;
 	WhirlTables                             wt;
 	std::vector<uint32_t>                   vibTab;

@@ -40,6 +40,47 @@ struct Contrib {
 	float   level;
 };
 
+/* The hot path's cfg keys (parseConfigurationLine / distributeParameter,
+ * src/cfgParser.cpp:61-160) with the reference's defaults and field types:
+ * whirlConfig (src/whirl.cpp:992-1160; initValues 43-134), the scalar keys of oscConfig
+ * (src/tonegen.cpp:2173-2555; initValues 238-331), scannerConfig (src/vibrato.cpp:334-357)
+ * and reverbConfig (src/reverb.cpp:242-256). */
+enum { ENV_CLICK = 0, ENV_COSINE = 1, ENV_LINEAR = 2, ENV_SHELF = 3 };
+struct Config {
+	/* whirl.* */
+	float  hornRPMslow = (float)(60.0 * 0.672), hornRPMfast = (float)(60.0 * 7.056);
+	float  drumRPMslow = (float)(60.0 * 0.600), drumRPMfast = (float)(60.0 * 5.955);
+	float  hornAcc = 0.161f, hornDec = 0.321f, drumAcc = 4.127f, drumDec = 1.371f;
+	float  hornRadiusCm = 19.2f, drumRadiusCm = 22.0f, micDistCm = 42.0f, hornXOffsetCm = 0.0f, hornZOffsetCm = 0.0f;
+	float  hornLevel = 0.7f, leakLevel = 0.15f;
+	float  drumMicWidth = 0.0f, hornMicWidth = 0.0f;
+	int    lpT = 8;
+	double lpF = 811.9695, lpQ = 1.6016, lpG = -38.9291;
+	float  haT = 0, haF = 4500, haQ = 2.7456f, haG = -30.0f;
+	float  hbT = 7, hbF = 300.0f, hbQ = 1.0f, hbG = -30.0f;
+	int    revSelect = 0, bypass = 0;
+	double micAngle = 0, hnBrakePos = 0, drBrakePos = 0;
+	/* scanner.* */
+	double vibFqHertz = 7.25, vib1OffAmp = 3.0, vib2OffAmp = 6.0, vib3OffAmp = 9.0;
+	/* reverb.mix */
+	float  reverbMix = 0.1f;
+	/* osc.* (scalar keys) */
+	double tgPrecision = 0.001, percFastDecaySeconds = 1.0, percSlowDecaySeconds = 4.0;
+	float  percEnvGainResetNorm = 1.0f, percEnvGainResetSoft = 0.5012f, percEnvScaling = 11.0f;
+	int    percSendBusA = 3, percSendBusB = 4, percTriggerBus = 8;
+	float  envAttackClickLevel = 0.50f, envReleaseClickLevel = 0.25f;
+	int    envAtkClkMinLength = -1, envAtkClkMaxLength = -1; /* -1: from the sample rate */
+	int    envAttackModel = ENV_CLICK, envReleaseModel = ENV_LINEAR;
+};
+
+/* what a cfg key touches (configSet's `scope` out-parameter) */
+enum { CFG_SHARED = 1, /* engine-wide tables: whirl.*, scanner.* */
+       CFG_TEMPLATE = 2, /* templates created afterwards: osc.x-precision, envelopes */
+       CFG_INSTANCE = 4 /* instances added afterwards: perc, reverb.mix, per-instance whirl */ };
+/* one key=value: 1 applied, 0 not a key of the hot path, -1 unparsable / out of range
+ * (nothing assigned), -2 a key of the reference this engine does not implement */
+int configSet (Config& c, const char* key, const char* value, int* scope);
+
 struct TgTemplate {
 	double                            sr = 48000.0;
 	double                            frequency[300];
@@ -58,11 +99,12 @@ struct TgTemplate {
 	int                               nPartials[TBF_NW + 1];
 	double                            pAmp[TBF_NW + 1][12], pHz[TBF_NW + 1][12];
 	size_t                            total = 0; /* bank samples = rand() draws of the bank */
-	void build (double sr, const double* mts128, const double* ratio9, unsigned int seed);
+	Config                            cfg; /* the osc.* template keys it was built with */
+	void build (double sr, const double* mts128, const double* ratio9, unsigned int seed, const Config& c);
 	/* the steps of build: prepare (tables, wheel lengths and spectra), synthHost (the
 	 * bank, one draw per sample), finish (key compression, envelopes: the draws after
 	 * the bank) */
-	void prepare (double sr, const double* mts128, const double* ratio9);
+	void prepare (double sr, const double* mts128, const double* ratio9, const Config& c);
 	void synthHost (GlibcRand& rnd);
 	void finish (GlibcRand& rnd);
 };
@@ -77,7 +119,7 @@ struct WhirlTables {
 	double             revHorn[9], revDrum[9];
 	double             lAcc[4];
 	float              maxAhead; /* largest write-ahead in samples */
-	void build (double sr);
+	void build (double sr, const Config& c);
 };
 
 /* per-instance tonegen control state (runtime fields of struct b_tonegen) */
@@ -114,7 +156,7 @@ struct TgControl {
 	uint32_t          vibTable = 2, vibMixed = 0;
 	bool              steadyPending = false; /* last block emitted env entries / removals */
 
-	void init (const TgTemplate* t);
+	void init (const TgTemplate* t, const Config& c);
 	void keyOn (int key);
 	void keyOff (int key);
 	void setDrawBar (int bus, unsigned setting);

@@ -294,20 +294,24 @@ static size_t fitWave (double Hz, double precision, int minSamples, int maxSampl
 	return (size_t)minSpn;
 }
 
-void TgTemplate::build (double rate, const double* mts128, const double* ratio9, unsigned int seed)
+void TgTemplate::build (double rate, const double* mts128, const double* ratio9, unsigned int seed, const Config& c)
 {
 	GlibcRand rnd (seed);
-	prepare (rate, mts128, ratio9);
+	prepare (rate, mts128, ratio9, c);
 	synthHost (rnd);
 	finish (rnd);
 }
 
-void TgTemplate::prepare (double rate, const double* mts128, const double* ratio9)
+void TgTemplate::prepare (double rate, const double* mts128, const double* ratio9, const Config& c)
 {
 	static const double defaultRatio[9] = {0.5, 1.5, 1, 2, 3, 4, 5, 6, 8};
 	sr     = rate;
-	envMin = std::min ((int)floor (sr * 8.0 / 22050.0), TBF_BLK);
-	envMax = std::min ((int)ceil (sr * 40.0 / 22050.0), TBF_BLK);
+	cfg    = c;
+	/* initToneGenerator (tonegen.cpp:2938-2955): click lengths from the rate unless set */
+	envMin = c.envAtkClkMinLength < 0 ? (int)floor (sr * 8.0 / 22050.0) : c.envAtkClkMinLength;
+	envMax = c.envAtkClkMaxLength < 0 ? (int)ceil (sr * 40.0 / 22050.0) : c.envAtkClkMaxLength;
+	envMin = std::min (envMin, TBF_BLK);
+	envMax = std::min (envMax, TBF_BLK);
 	frequencies (frequency, mts128);
 	for (int i = 0; i < 9; i++)
 		targetRatio[i] = ratio9 ? ratio9[i] : defaultRatio[i];
@@ -327,7 +331,7 @@ void TgTemplate::prepare (double rate, const double* mts128, const double* ratio
 		           0.0 * (tCb - tSq);
 		const double att = (r < 0.0) ? 0.0 : (1.0 < r) ? 1.0 : r;
 		const double wf  = fmin (fmax (frequency[i - 1], 12.0), 2.5e10);
-		const size_t wl  = fitWave (wf, 0.001, 3 * TBF_BLK, (int)(ceil (sr / 48000.0) * 4096), sr);
+		const size_t wl  = fitWave (wf, c.tgPrecision, 3 * TBF_BLK, (int)(ceil (sr / 48000.0) * 4096), sr);
 		off[i]           = (uint32_t)total;
 		len[i]           = (uint32_t)wl;
 		total += wl;
@@ -383,29 +387,76 @@ void TgTemplate::finish (GlibcRand& rnd)
 			keyCompTable[i] = (float)dBToGain (u + ((v - u) * a * m));
 		}
 	}
-	/* initEnvelopes (2562-2728): attack ENV_CLICK level 0.5, release ENV_LINEAR */
+	/* initEnvelopes (2562-2728): the four attack / release models; the default pair is
+	 * click (level 0.5) / linear */
+	const int    bss = TBF_BLK;
+	const double T   = (double)(TBF_BLK - 1);
 	for (int b = 0; b < 9; b++) {
-		int bound = envMax - envMin;
-		if (bound < 1)
-			bound = 1;
-		int burst = envMin + (rnd.next () % bound);
-		if (TBF_BLK <= burst)
-			burst = TBF_BLK - 1;
-		int start = (rnd.next () % (TBF_BLK - burst));
-		int i;
-		for (i = 0; i < start; i++)
-			attackEnv[b][i] = 0.0f;
-		for (; i < start + burst; i++) {
-			double d        = ((double)rnd.next ()) / (double)2147483647;
-			attackEnv[b][i] = (float)(1.0 - (0.50f * d));
+		float* A = attackEnv[b];
+		float* R = releaseEnv[b];
+		int    i, bound, burst, start;
+		if (cfg.envAttackModel == ENV_CLICK) {
+			bound = std::max (envMax - envMin, 1);
+			burst = envMin + (rnd.next () % bound);
+			if (bss <= burst)
+				burst = bss - 1;
+			start = (rnd.next () % (bss - burst));
+			for (i = 0; i < start; i++)
+				A[i] = 0.0f;
+			for (; i < start + burst; i++) {
+				double d = ((double)rnd.next ()) / (double)2147483647;
+				A[i]     = (float)(1.0 - (cfg.envAttackClickLevel * d));
+			}
+			for (; i < bss; i++)
+				A[i] = 1.0f;
+			A[0] = (float)(A[0] / 2.0);
+			for (i = 1; i < bss; i++)
+				A[i] = (float)((float)(A[i - 1] + A[i]) / 2.0);
 		}
-		for (; i < TBF_BLK; i++)
-			attackEnv[b][i] = 1.0f;
-		attackEnv[b][0] = (float)(attackEnv[b][0] / 2.0);
-		for (i = 1; i < TBF_BLK; i++)
-			attackEnv[b][i] = (float)((float)(attackEnv[b][i - 1] + attackEnv[b][i]) / 2.0);
-		for (i = 0; i < TBF_BLK; i++)
-			releaseEnv[b][i] = ((float)i) / (float)TBF_BLK;
+		if (cfg.envAttackModel == ENV_SHELF || cfg.envReleaseModel == ENV_SHELF) {
+			for (int pass = 0; pass < 2; pass++) { /* attack's draw first, then release's */
+				float* E = pass == 0 ? A : R;
+				if ((pass == 0 ? cfg.envAttackModel : cfg.envReleaseModel) != ENV_SHELF)
+					continue;
+				bound = std::max (envMax - envMin, 1);
+				start = rnd.next () % bound;
+				if ((bss - 2) <= start)
+					start = bss - 2;
+				for (i = 0; i < start; i++)
+					E[i] = 0.0f;
+				E[i + 0] = (float)0.33333333;
+				E[i + 1] = (float)0.66666666;
+				for (i = i + 2; i < bss; i++)
+					E[i] = 1.0f;
+			}
+		}
+		if (cfg.envReleaseModel == ENV_CLICK) {
+			burst = 8 + (rnd.next () % 32);
+			start = (rnd.next () % (bss - burst));
+			for (i = 0; i < start; i++)
+				R[i] = 0.0f;
+			for (; i < start + burst; i++) {
+				double d = ((double)rnd.next ()) / (double)2147483647;
+				R[i]     = (float)(1.0 - (cfg.envReleaseClickLevel * d));
+			}
+			for (; i < bss; i++)
+				R[i] = 1.0f;
+			R[0] = (float)(R[0] / 2.0);
+			for (i = 1; i < bss; i++)
+				R[i] = (float)((float)(R[i - 1] + R[i]) / 2.0);
+		}
+		if (cfg.envAttackModel == ENV_COSINE)
+			for (i = 0; i < bss; i++)
+				A[i] = (float)(0.5 + (0.5 * cos ((M_PI * (double)(bss - (i + 1))) / T)));
+		if (cfg.envReleaseModel == ENV_COSINE)
+			for (i = 0; i < bss; i++)
+				R[i] = (float)(0.5 - (0.5 * cos ((M_PI * (double)i) / T)));
+		if (cfg.envAttackModel == ENV_LINEAR)
+			for (i = 0; i < bss; i++)
+				A[i] = ((float)i) / (float)bss;
+		if (cfg.envReleaseModel == ENV_LINEAR)
+			for (i = 0; i < bss; i++)
+				R[i] = ((float)i) / (float)bss;
 	}
 }
 
@@ -493,14 +544,15 @@ static void iirCoef (float* W, int T, double F, double Q, double G, double SR)
 	W[4] = (float)C[2];
 }
 
-void WhirlTables::build (double rate)
+void WhirlTables::build (double rate, const Config& c)
 {
 	sr = rate;
 	displ.assign (4 * 16384, 0.f);
 	bw.assign (2 * 16384 * 5, 0.f);
-	/* initValues (src/whirl.cpp:43-134) geometry and filters */
-	const float  hornRadiusCm = 19.2f, drumRadiusCm = 22.0f, airSpeed = 340.0f, micDistCm = 42.0f;
-	const float  hornXOffsetCm = 0.0f, hornZOffsetCm = 0.0f;
+	/* initValues (src/whirl.cpp:43-134) geometry and filters, as the cfg left them */
+	const float  hornRadiusCm = c.hornRadiusCm, drumRadiusCm = c.drumRadiusCm, airSpeed = 340.0f,
+	            micDistCm = c.micDistCm;
+	const float  hornXOffsetCm = c.hornXOffsetCm, hornZOffsetCm = c.hornZOffsetCm;
 	const double hornR = (hornRadiusCm * sr / 100.0) / airSpeed;
 	const double drumR = (drumRadiusCm * sr / 100.0) / airSpeed;
 	const double micD  = (micDistCm * sr / 100.0) / airSpeed;
@@ -556,13 +608,12 @@ void WhirlTables::build (double rate)
 			obbw[(size_t)(16384 - i - 1) * 5 + j] = v;
 		}
 	/* initialize (626-662): drum hi-shelf, horn A low-pass, horn B low-shelf */
-	const float haF = 4500, haQ = 2.7456f, haG = -30.0f, hbF = 300.0f, hbQ = 1.0f, hbG = -30.0f;
-	iirCoef (drf, 8, 811.9695, 1.6016, -38.9291, sr);
-	iirCoef (hafw, 0, haF, haQ, haG, sr);
-	iirCoef (hbfw, 7, hbF, hbQ, hbG, sr);
+	iirCoef (drf, c.lpT, c.lpF, c.lpQ, c.lpG, sr);
+	iirCoef (hafw, (int)c.haT, c.haF, c.haQ, c.haG, sr);
+	iirCoef (hbfw, (int)c.hbT, c.hbF, c.hbQ, c.hbG, sr);
 	/* computeRotationSpeeds (270-293) */
-	const float  hornRPMslow = (float)(60.0 * 0.672), hornRPMfast = (float)(60.0 * 7.056);
-	const float  drumRPMslow = (float)(60.0 * 0.600), drumRPMfast = (float)(60.0 * 5.955);
+	const float  hornRPMslow = c.hornRPMslow, hornRPMfast = c.hornRPMfast;
+	const float  drumRPMslow = c.drumRPMslow, drumRPMfast = c.drumRPMfast;
 	const double hfast = hornRPMfast / (sr * 60.0), hslow = hornRPMslow / (sr * 60.0);
 	const double dfast = drumRPMfast / (sr * 60.0), dslow = drumRPMslow / (sr * 60.0);
 	const double H[9]  = {0, 0, 0, hslow, hslow, hslow, hfast, hfast, hfast};
@@ -572,16 +623,24 @@ void WhirlTables::build (double rate)
 		revDrum[i] = D[i];
 	}
 	/* speed-ramp factors of whirlProc2 (1255-1257, 1306-1308), block = 128 */
-	const float hornAcc = 0.161f, hornDec = 0.321f, drumAcc = 4.127f, drumDec = 1.371f;
+	const float hornAcc = c.hornAcc, hornDec = c.hornDec, drumAcc = c.drumAcc, drumDec = c.drumDec;
 	const float acc[4]  = {hornAcc, hornDec, drumAcc, drumDec};
 	for (int i = 0; i < 4; i++)
 		lAcc[i] = exp (-1.0 / (sr / (size_t)TBF_BLK * acc[i]));
 }
 
 /* ------------------------------------------------------------------ tonegen control */
-void TgControl::init (const TgTemplate* t)
+void TgControl::init (const TgTemplate* t, const Config& c)
 {
 	tpl = t;
+	/* oscConfig's runtime keys (src/tonegen.cpp:2206-2237), set before initToneGenerator's
+	 * setters below read them */
+	percSendBusA         = (unsigned)c.percSendBusA;
+	percSendBusB         = (unsigned)c.percSendBusB;
+	percTriggerBus       = c.percTriggerBus;
+	percEnvGainResetNorm = c.percEnvGainResetNorm;
+	percEnvGainResetSoft = c.percEnvGainResetSoft;
+	percEnvScaling       = c.percEnvScaling;
 	memset (aot, 0, sizeof (aot));
 	for (int i = 0; i <= TBF_NW; i++) {
 		aclPos[i] = -1;

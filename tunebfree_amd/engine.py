@@ -52,6 +52,8 @@ SIGNATURES = {
     "tbf_error_flags": (C.c_int, [C.c_void_p, _u32p]),
     "tbf_template_bank": (C.c_int, [C.c_void_p, C.c_uint32, _fp, C.c_uint64, _u32p]),
     "tbf_midi_control": (C.c_int, [C.c_void_p, C.c_uint32, C.c_char_p, C.c_int32]),
+    "tbf_config_set": (C.c_int, [C.c_void_p, C.c_char_p, C.c_char_p]),
+    "tbf_config_parse": (C.c_int, [C.c_void_p, C.c_char_p]),
     "tbf_program_parse": (C.c_int, [C.c_void_p, C.c_char_p]),
     "tbf_program_install": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32]),
     "tbf_program_name": (C.c_int, [C.c_void_p, C.c_uint32, C.c_char_p, C.c_uint32]),
@@ -108,6 +110,19 @@ class Engine:
             self.close()
         except Exception:
             pass
+
+    def config_set(self, key, value):
+        """One cfg key (tbf_config_set): 0 applied, 1 not a key of this path."""
+        return _check(self._lib.tbf_config_set(self._h, str(key).encode(), str(value).encode()))
+
+    def config(self, items):
+        """Several cfg keys, a dict or (key, value) pairs, in order."""
+        for k, v in (items.items() if isinstance(items, dict) else items):
+            self.config_set(k, v)
+
+    def config_parse(self, text):
+        """A cfg file's text; returns the number of keys applied."""
+        return _check(self._lib.tbf_config_parse(self._h, text.encode()))
 
     def template(self, mts128=None, ratio9=None, seed=1):
         m = None if mts128 is None else np.ascontiguousarray(mts128, dtype=np.float64)

@@ -92,18 +92,24 @@ int tbf_engine_destroy (tbf_engine* e);
  *             bypass.  Geometry re-derives the compact ring window (512 / 1024 / 2048)
  *   scanner.* scannerConfig (src/vibrato.cpp:334-357): scanner frequency, V1-V3 depths
  *   reverb.mix reverbConfig (src/reverb.cpp:242-256)
- *   osc.*     oscConfig's scalar keys (src/tonegen.cpp:2173-2555): x-precision, the
- *             key-click / release envelope models, levels and lengths, percussion
- *             gains, buses and trigger bus (osc.perc.fast / .slow are stored but, as in
- *             the reference, never reach the decay constants)
+ *   osc.*     oscConfig (src/tonegen.cpp:2173-2555): x-precision, the key-click /
+ *             release envelope models, levels and lengths, percussion gains, buses and
+ *             trigger bus (osc.perc.fast / .slow are stored but, as in the reference,
+ *             never reach the decay constants); the wheel EQ (osc.eq.macro, spline
+ *             points), extra wheel harmonics (osc.harmonic.*), terminal mixes, key tapers
+ *             and key crosstalk lists (osc.terminal.* / osc.taper.* / osc.crosstalk.*),
+ *             the default crosstalk levels and the contribution floor / minimum
  * A setting applies to what is built after it: whirl.* tables and scanner.* shape
  * engine-wide tables and must precede tbf_instances_add (-16 after); osc.* template
  * keys apply to later tbf_template_create / tbf_templates_create; the rest to later
- * tbf_instances_add.  Returns 0 applied, 1 not a key of this path (ignored, as the
- * reference ignores it; overdrive.* / xov.* are accepted with no effect: ampConfig,
- * src/overdrive.cpp:395-433, writes fields airwindows_density never reads), -22 bad
- * value (nothing assigned), -95 a key of these modules this engine does not implement
- * (osc list models, EQ macros, crosstalk levels, tuning, the comb filter). */
+ * tbf_instances_add.  Returns 0 applied, 1 ignored: not a key of this path, or a key
+ * the reference stores but never reads here (overdrive.* / xov.*: ampConfig,
+ * src/overdrive.cpp:395-433, writes fields airwindows_density never reads;
+ * osc.tuning / osc.temperament / osc.eqv.*; whirl.horn.comb.*), -22 bad value
+ * (nothing assigned; a list key with any malformed part assigns none of it, where the
+ * reference keeps the well-formed parts and warns; osc.transformer-crosstalk above 0,
+ * with which the reference aborts in findTransformerNeighbours,
+ * src/tonegen.cpp:914-927). */
 int tbf_config_set (tbf_engine* e, const char* key, const char* value);
 /* a cfg file's text (`name = value` lines, '#' comments): returns the number of keys
  * applied, or < 0 with tbf_last_error () = "line N: message" */

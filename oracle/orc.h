@@ -75,6 +75,14 @@ typedef struct {
 #define ORC_ENV_COSINE 1
 #define ORC_ENV_LINEAR 2
 #define ORC_ENV_SHELF 3
+#define ORC_EQ_SPLINE 0 /* src/tonegen.h eqMacro values (EQ_SPLINE, EQ_PEAK24, EQ_PEAK46) */
+#define ORC_EQ_PEAK24 1
+#define ORC_EQ_PEAK46 2
+#define ORC_LE_HARMONIC 0 /* wheelHarmonics[idx] (idx 0: every wheel) */
+#define ORC_LE_TERMINAL 1 /* terminalMix[idx] */
+#define ORC_LE_TAPER 2    /* keyTaper[idx] */
+#define ORC_LE_XTALK 3    /* keyCrosstalk[idx] */
+#define ORC_CFG_MAX_LE 8192
 typedef struct orc_cfg {
 	/* whirl.* (struct b_whirl field types) */
 	float  hornRPMslow, hornRPMfast, drumRPMslow, drumRPMfast;
@@ -98,6 +106,22 @@ typedef struct orc_cfg {
 	float  envAttackClickLevel, envReleaseClickLevel;
 	int    envAtkClkMinLength, envAtkClkMaxLength; /* -1: from the sample rate */
 	int    envAttackModel, envReleaseModel;
+	/* osc.* tone-generator model keys (struct b_tonegen fields, initValues 302-316):
+	 * wheel EQ macro and spline points, the default crosstalk levels, the play matrix
+	 * contribution floor / minimum */
+	int    eqMacro; /* ORC_EQ_* */
+	double eqP1y, eqR1y, eqP4y, eqR4y;
+	double compartmentXT, transformerXT, stripXT, wiringXT;
+	double contribFloor, contribMin;
+	/* the list keys (osc.harmonic.*, osc.terminal.*, osc.taper.*, osc.crosstalk.*) in
+	 * file order: each becomes one ListElement appended to its list, exactly as
+	 * oscConfig's appendListElement calls (src/tonegen.cpp:2296-2474) */
+	int    nle;
+	struct {
+		short kind, idx; /* ORC_LE_*, list index (wheel / terminal / key) */
+		short sa, sb;    /* harmonic number | wheel | terminal ; bus */
+		float fc;        /* level */
+	} le[ORC_CFG_MAX_LE];
 } orc_cfg;
 
 void   orc_cfg_default (orc_cfg* c);

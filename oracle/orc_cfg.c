@@ -3,7 +3,8 @@
  *
  * The cfg keys of the hot path: defaults and per-key assignments restated from
  *   whirlConfig   src/whirl.cpp:992-1160 (defaults: initValues 43-134)
- *   oscConfig     src/tonegen.cpp:2173-2555, scalar keys (defaults: initValues 238-331)
+ *   oscConfig     src/tonegen.cpp:2173-2555: the scalar keys, the wheel EQ, the default
+ *                 crosstalk levels and the list keys (defaults: initValues 238-331)
  *   scannerConfig src/vibrato.cpp:334-357 (defaults: reset_vibrato 296-300)
  *   reverbConfig  src/reverb.cpp:242-256 (default: the ctor's G, 217)
  * Value parsing follows getConfigParameter_d/_dr/_i/_ir (src/cfgParser.cpp:453-620):
@@ -74,6 +75,87 @@ void orc_cfg_default (orc_cfg* c)
 	c->envAtkClkMaxLength   = -1;
 	c->envAttackModel       = ORC_ENV_CLICK;
 	c->envReleaseModel      = ORC_ENV_LINEAR;
+	c->eqMacro              = ORC_EQ_SPLINE;
+	c->eqP1y                = 1.0;
+	c->eqR1y                = 0.0;
+	c->eqP4y                = 1.0;
+	c->eqR4y                = 0.0;
+	c->compartmentXT        = 0.01;
+	c->transformerXT        = 0.0;
+	c->stripXT              = 0.01;
+	c->wiringXT             = 0.01;
+	c->contribFloor         = 0.0000158;
+	c->contribMin           = 0.0;
+	c->nle                  = 0;
+}
+
+static int le_push (orc_cfg* c, int kind, int idx, int sa, int sb, double fc)
+{
+	if (c->nle >= ORC_CFG_MAX_LE)
+		return -1;
+	c->le[c->nle].kind = (short)kind;
+	c->le[c->nle].idx  = (short)idx;
+	c->le[c->nle].sa   = (short)sa;
+	c->le[c->nle].sb   = (short)sb;
+	c->le[c->nle].fc   = (float)fc;
+	c->nle++;
+	return 1;
+}
+
+/* oscConfig's list keys (src/tonegen.cpp:2296-2474).  The reference appends every
+ * well-formed element and only warns about the rest; here a key with any malformed or
+ * out-of-range part assigns nothing and returns -1.  A harmonic number below 1 would
+ * fail initOscillators' assert (1604-1605), so it is refused here. */
+static int osc_list_key (orc_cfg* c, const char* k, const char* v)
+{
+	int    n, w, b, kk;
+	double x;
+	if (!strncasecmp (k, "osc.harmonic.", 13)) {
+		if (sscanf (k + 13, "%d", &n) == 1) {
+			if (sscanf (v, "%lf", &x) != 1 || n < 1 || 32767 < n)
+				return -1;
+			return le_push (c, ORC_LE_HARMONIC, 0, n, 0, x);
+		}
+		if (sscanf (k + 13, "w%d.f%d", &w, &n) == 2) {
+			if (!(0 < w && w <= ORC_NOF_WHEELS) || n < 1 || 32767 < n || sscanf (v, "%lf", &x) != 1)
+				return -1;
+			return le_push (c, ORC_LE_HARMONIC, w, n, 0, x);
+		}
+		return -1;
+	}
+	if (!strncasecmp (k, "osc.terminal.", 13)) {
+		if (sscanf (k + 13, "t%d.w%d", &n, &w) != 2 || !(0 < n && n <= ORC_NOF_WHEELS) ||
+		    !(0 < w && w <= ORC_NOF_WHEELS) || sscanf (v, "%lf", &x) != 1)
+			return -1;
+		return le_push (c, ORC_LE_TERMINAL, n, w, 0, x);
+	}
+	if (!strncasecmp (k, "osc.taper.", 10)) {
+		/* bus 0 is refused, as the reference's 0 < b test does */
+		if (sscanf (k + 10, "k%d.b%d.t%d", &kk, &b, &w) != 3 || !(0 < kk && kk < ORC_MAX_KEYS) ||
+		    !(0 < b && b < ORC_NOF_BUSES) || !(0 < w && w <= ORC_NOF_WHEELS) || sscanf (v, "%lf", &x) != 1)
+			return -1;
+		return le_push (c, ORC_LE_TAPER, kk, w, b, x);
+	}
+	if (!strncasecmp (k, "osc.crosstalk.", 14)) {
+		const char* p;
+		int         cnt = 0;
+		if (sscanf (k + 14, "k%d", &kk) != 1 || !(0 < kk && kk < ORC_MAX_KEYS))
+			return -1;
+		for (p = v; p; p = strchr (p, ','), p = p ? p + 1 : p) { /* validate first */
+			if (sscanf (p, "%d:%d:%lf", &b, &w, &x) != 3 || !(0 < b && b < ORC_NOF_BUSES) ||
+			    !(0 < w && w <= ORC_NOF_WHEELS))
+				return -1;
+			cnt++;
+		}
+		if (c->nle + cnt > ORC_CFG_MAX_LE)
+			return -1;
+		for (p = v; p; p = strchr (p, ','), p = p ? p + 1 : p) {
+			sscanf (p, "%d:%d:%lf", &b, &w, &x);
+			le_push (c, ORC_LE_XTALK, kk, w, b, x);
+		}
+		return 1;
+	}
+	return 0;
 }
 
 /* getConfigParameter_d / _dr / _i / _ir: 1 assigned, -1 parse or range failure */
@@ -189,6 +271,32 @@ int orc_cfg_set (orc_cfg* c, const char* k, const char* v)
 	if (DR ("osc.attack.click.maxlength", 0.0, 1.0)) SET (clk_length (&c->envAtkClkMaxLength, d));
 	if (DR ("osc.attack.click.minlength", 0.0, 1.0)) SET (clk_length (&c->envAtkClkMinLength, d));
 	if (DR ("osc.release.click.level", 0.0, 1.0)) SET (c->envReleaseClickLevel = (float)d);
+	if (DR ("osc.compartment-crosstalk", 0.0, 1.0)) SET (c->compartmentXT = d);
+	/* a level above 0 makes initToneGenerator abort: findTransformerNeighbours asserts
+	 * for every wheel above 91 (src/tonegen.cpp:914-927, called for 44..256 at 973-978),
+	 * so only 0 is a usable value */
+	if (DR ("osc.transformer-crosstalk", 0.0, 0.0)) SET (c->transformerXT = d);
+	if (DR ("osc.terminalstrip-crosstalk", 0.0, 1.0)) SET (c->stripXT = d);
+	if (DR ("osc.wiring-crosstalk", 0.0, 1.0)) SET (c->wiringXT = d);
+	if (DR ("osc.contribution-floor", 0.0, 1.0)) SET (c->contribFloor = d);
+	if (DR ("osc.contribution-min", 0.0, 1.0)) SET (c->contribMin = d);
+	if (D ("osc.eq.p1y")) SET (c->eqP1y = d);
+	if (D ("osc.eq.r1y")) SET (c->eqR1y = d);
+	if (D ("osc.eq.p4y")) SET (c->eqP4y = d);
+	if (D ("osc.eq.r4y")) SET (c->eqR4y = d);
+	if (!strcasecmp (k, "osc.eq.macro")) {
+		if (!strcasecmp (v, "chspline"))
+			c->eqMacro = ORC_EQ_SPLINE;
+		else if (!strcasecmp (v, "peak24"))
+			c->eqMacro = ORC_EQ_PEAK24;
+		else if (!strcasecmp (v, "peak46"))
+			c->eqMacro = ORC_EQ_PEAK46;
+		else
+			return -1;
+		return 1;
+	}
+	if ((r = osc_list_key (c, k, v)) != 0)
+		return r;
 	if (!strcasecmp (k, "osc.release.model"))
 		return env_model (v, &c->envReleaseModel);
 	if (!strcasecmp (k, "osc.attack.model"))

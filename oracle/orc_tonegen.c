@@ -131,11 +131,10 @@ static void applyPedalDefaults (orc_template* t, int nofPedals)
 	}
 }
 
-/* src/tonegen.cpp:849-879 applyDefaultCrosstalk (defaultWiringCrosstalk = 0.01) */
-static void applyDefaultCrosstalk (orc_template* t, int keyOffset, int busOffset)
+/* src/tonegen.cpp:849-879 applyDefaultCrosstalk (defaultWiringCrosstalk) */
+static void applyDefaultCrosstalk (orc_template* t, int keyOffset, int busOffset, double wiring)
 {
-	const double wiring = 0.01;
-	int          k, b, e;
+	int k, b, e;
 	for (k = 0; k < 128; k++) {
 		int kn = k + keyOffset;
 		if (t->keyCrosstalk[kn].n != 0)
@@ -170,11 +169,11 @@ static int findEastWest (const short* v, int w, int* ep, int* wp)
 	return 0;
 }
 
-/* src/tonegen.cpp:933-1041 applyDefaultConfiguration (compartment 0.01, transformer 0,
- * terminal strip 0.01) */
-static void applyDefaultConfiguration (orc_template* t)
+/* src/tonegen.cpp:933-1041 applyDefaultConfiguration (defaults: compartment 0.01,
+ * transformer 0, terminal strip 0.01, wiring 0.01) */
+static void applyDefaultConfiguration (orc_template* t, const orc_cfg* c)
 {
-	const double compartment = 0.01, transformer = 0.0, strip = 0.01;
+	const double compartment = c->compartmentXT, transformer = c->transformerXT, strip = c->stripXT;
 	int          i;
 	for (i = 1; i <= NW; i++) {
 		if (t->terminalMix[i].n == 0) {
@@ -210,8 +209,8 @@ static void applyDefaultConfiguration (orc_template* t)
 	applyManualDefaults (t, 0, 0);
 	applyManualDefaults (t, 128, 9);
 	applyPedalDefaults (t, 32);
-	applyDefaultCrosstalk (t, 0, 0);
-	applyDefaultCrosstalk (t, 128, 9);
+	applyDefaultCrosstalk (t, 0, 0, c->wiringXT);
+	applyDefaultCrosstalk (t, 128, 9, c->wiringXT);
 }
 
 /* src/tonegen.cpp:1061-1111 cpmInsert */
@@ -249,14 +248,15 @@ static void cpmInsert (const orc_template* t, const orc_le* lep, unsigned char c
 	*endRowp = endRow;
 }
 
-/* src/tonegen.cpp:1122-1213 compilePlayMatrix (floor 0.0000158, min 0.0) */
-static void compilePlayMatrix (orc_template* t)
+/* src/tonegen.cpp:1122-1213 compilePlayMatrix (contribution floor / minimum: defaults
+ * 0.0000158 / 0.0) */
+static void compilePlayMatrix (orc_template* t, const orc_cfg* cfg)
 {
 	static unsigned char cpmBus[NW + 1][ORC_NOF_BUSES];
 	static float         cpmGain[NW][ORC_NOF_BUSES];
 	short                wheelNumber[NW + 1];
 	short                rowLength[NW];
-	const double         floorLevel = 0.0000158, minLevel = 0.0;
+	const double         floorLevel = cfg->contribFloor, minLevel = cfg->contribMin;
 	int                  k, w, c, e;
 	for (k = 0; k < ORC_MAX_KEYS; k++) {
 		int endRow = 0;
@@ -288,7 +288,28 @@ static void compilePlayMatrix (orc_template* t)
 	}
 }
 
-/* src/tonegen.cpp:1240-1261 apply_CH_Spline (p1y=1, r1y=0, p4y=1, r4y=0) */
+/* src/tonegen.cpp:1223-1233 damperCurve */
+static double damperCurve (int thisTG, int firstTG, int lastTG, double w, double v, double u)
+{
+	double x = ((double)(thisTG - firstTG)) / ((double)(lastTG - firstTG));
+	double z = (x * (u - v)) - u;
+	return 1.0 - w * z * z;
+}
+
+/* src/tonegen.cpp:1266-1311 applyOscEQ_peak24 / applyOscEQ_peak46 */
+static void applyPeak (orc_template* t, int nofOscillators, int peak46)
+{
+	int i;
+	for (i = 1; i <= 43; i++)
+		t->watt[i] = peak46 ? damperCurve (i, 1, 43, 0.3, 0.4, 1.0) : damperCurve (i, 1, 43, 0.2, -0.8, 1.0);
+	for (i = 44; i <= 48; i++)
+		t->watt[i] = peak46 ? damperCurve (i, 44, 48, 0.1, -0.4, 0.4) : damperCurve (i, 44, 48, 1.6, -0.4, -0.3);
+	for (i = 49; i <= nofOscillators; i++)
+		t->watt[i] = peak46 ? damperCurve (i, 49, nofOscillators, 0.8, -1.0, -0.3)
+		                    : damperCurve (i, 49, nofOscillators, 0.9, -1.0, -0.7);
+}
+
+/* src/tonegen.cpp:1240-1261 apply_CH_Spline (defaults p1y=1, r1y=0, p4y=1, r4y=0) */
 static void applySpline (orc_template* tg, int nofOscillators, double p1y, double r1y, double p4y, double r4y)
 {
 	int    i;
@@ -496,16 +517,36 @@ orc_template* orc_template_new_cfg (double sr, const double* mts128, const doubl
 	orc_get_frequencies (t->frequency, mts128);
 	for (i = 0; i < 9; i++)
 		t->targetRatio[i] = ratio9 ? ratio9[i] : defaultRatio[i];
-	applyDefaultConfiguration (t);
-	compilePlayMatrix (t);
+	/* the cfg's terminal / taper / crosstalk lists, in file order (oscConfig) */
+	for (j = 0; j < cfg->nle; j++) {
+		const int k = cfg->le[j].idx;
+		switch (cfg->le[j].kind) {
+			case ORC_LE_TERMINAL: lst_push (&t->terminalMix[k], cfg->le[j].sa, 0, cfg->le[j].fc); break;
+			case ORC_LE_TAPER: lst_push (&t->keyTaper[k], cfg->le[j].sa, cfg->le[j].sb, cfg->le[j].fc); break;
+			case ORC_LE_XTALK: lst_push (&t->keyCrosstalk[k], cfg->le[j].sa, cfg->le[j].sb, cfg->le[j].fc); break;
+		}
+	}
+	applyDefaultConfiguration (t, cfg);
+	compilePlayMatrix (t, cfg);
 	/* initOscillators (tonegen.cpp:1470-1630) */
-	applySpline (t, NW, 1.0, 0.0, 1.0, 0.0);
-	for (j = 0; j < ORC_MAX_PARTIALS; j++)
-		harm[j] = j == 0 ? 1.0 : 0.0;
+	if (cfg->eqMacro == ORC_EQ_SPLINE)
+		applySpline (t, NW, cfg->eqP1y, cfg->eqR1y, cfg->eqP4y, cfg->eqR4y);
+	else
+		applyPeak (t, NW, cfg->eqMacro == ORC_EQ_PEAK46);
 	for (i = 1; i <= NW; i++) {
+		int e;
 		t->wfreq[i] = oscFreq (t, i);
 		t->wlen[i]  = orc_fitwave (t->wfreq[i], cfg->tgPrecision, 3 * BSS, (int)(ceil (sr / 48000.0) * 4096), sr);
 		t->wave[i]  = (float*)malloc (sizeof (float) * t->wlen[i]);
+		/* compile-time harmonics, then the cfg's global ones, then this wheel's */
+		for (j = 0; j < ORC_MAX_PARTIALS; j++)
+			harm[j] = j == 0 ? 1.0 : 0.0;
+		for (e = 0; e < cfg->nle; e++)
+			if (cfg->le[e].kind == ORC_LE_HARMONIC && cfg->le[e].idx == 0 && cfg->le[e].sa - 1 < ORC_MAX_PARTIALS)
+				harm[cfg->le[e].sa - 1] += cfg->le[e].fc;
+		for (e = 0; e < cfg->nle; e++)
+			if (cfg->le[e].kind == ORC_LE_HARMONIC && cfg->le[e].idx == i && cfg->le[e].sa - 1 < ORC_MAX_PARTIALS)
+				harm[cfg->le[e].sa - 1] += cfg->le[e].fc;
 		writeSamples (t->wave[i], t->wlen[i], harm, t->watt[i], t->wfreq[i], sr, &rnd);
 	}
 	initKeyCompTable (t);

@@ -4,7 +4,8 @@ built by the reference's OWN code -- src/tonegen.cpp's static initOscillators
 (random click bursts), reached by oracle/ref_tpl_pin.cpp, which #includes that file
 unmodified (`make -C oracle pin`).  Run here, where /root/reference exists; the JSON is
 data only (inputs = sample rate, tuning, seed; outputs = SHA-256 of the float32 tables
-plus a few sampled values) and pins the oracle's and the product's template builders
+plus a few sampled values; the play matrix from the reference's compilePlayMatrix) and
+pins the oracle's and the product's template builders
 on machines without /root/reference.
 
 Cases: the 7 tunings of tests/golden/tunings.json x 48 / 96 kHz, template seed 300 + j
@@ -23,7 +24,7 @@ sys.path.insert(0, str(HERE.parent))
 
 from orc_bind import load_oracle, load_pin, pin_template  # noqa: E402
 
-KEYS = ("bank", "lens", "wfreq", "attack", "release", "keycomp")
+KEYS = ("bank", "lens", "wfreq", "attack", "release", "keycomp", "contrib")
 
 
 def digest(tables):
@@ -41,9 +42,11 @@ def cases():
     for sr in (48000.0, 96000.0):
         for j, nm in enumerate(names):
             yield nm, sr, 300 + j, (None if tun[nm] is None else np.array(tun[nm], np.float64)), None
-    # the template cfg keys (envelope models / levels / lengths, x-precision)
-    for k, cfgname in enumerate(("envelopes", "envelopes2")):
+    # the template cfg keys (envelope models / levels / lengths, x-precision; wheel EQ,
+    # harmonics, terminal mix, taper, crosstalk lists and levels, contribution floor)
+    for k, cfgname in enumerate(("envelopes", "envelopes2", "osc_lists", "osc_models")):
         yield "12TET", 48000.0, 400 + k, None, cfgname
+    yield "19TET", 96000.0, 410, np.array(tun["19TET"], np.float64), "osc_lists"
 
 
 def main():

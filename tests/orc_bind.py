@@ -128,7 +128,37 @@ def load_pin():
     lib.refpin_template_cfg.restype = C.c_long
     lib.refpin_template_cfg.argtypes = [C.c_double, _dp, C.c_void_p, C.c_uint, C.c_void_p, _fp, C.c_uint64, _u32p,
                                         _dp, _fp, _fp, _fp]
+    lib.refpin_template_full.restype = C.c_long
+    lib.refpin_template_full.argtypes = [C.c_double, _dp, C.c_void_p, C.c_uint, C.c_void_p, _fp, C.c_uint64, _u32p,
+                                         _dp, _fp, _fp, _fp, _u32p, C.c_void_p, C.c_void_p, _fp, C.c_uint32]
     return lib
+
+
+CONTRIB_CAP = 1 << 17
+
+
+def contrib_blob(n, wheel, bus, level):
+    """The play matrix (keyContrib of keys 0..383) as one byte string: entries per key,
+    then wheel / bus / level of all entries in key order."""
+    t = int(np.sum(n))
+    return np.frombuffer(np.asarray(n, np.uint32).tobytes() + np.asarray(wheel[:t], np.int16).tobytes() +
+                         np.asarray(bus[:t], np.int16).tobytes() + np.asarray(level[:t], np.float32).tobytes(),
+                         np.uint8)
+
+
+def contrib_from(fn):
+    """contrib_blob of a per-key exporter fn(key, wheel_ptr, bus_ptr, level_ptr, cap) -> count
+    (orc_template_contrib / tbf_debug_contrib)."""
+    cap = 4096
+    n = np.zeros(384, np.uint32)
+    W, B, L = [], [], []
+    w, b, lv = np.zeros(cap, np.int16), np.zeros(cap, np.int16), np.zeros(cap, np.float32)
+    for k in range(384):
+        c = fn(k, w.ctypes.data, b.ctypes.data, lv.ctypes.data, cap)
+        assert 0 <= c <= cap, (k, c)
+        n[k] = c
+        W.append(w[:c].copy()); B.append(b[:c].copy()); L.append(lv[:c].copy())
+    return contrib_blob(n, np.concatenate(W), np.concatenate(B), np.concatenate(L))
 
 
 def pin_template(pin, orc, sr, mts128, seed, cfg=None):
@@ -139,17 +169,22 @@ def pin_template(pin, orc, sr, mts128, seed, cfg=None):
     m = None if mts128 is None else np.ascontiguousarray(mts128, np.float64)
     orc.orc_get_frequencies(f300.ctypes.data_as(_dp), None if m is None else m.ctypes.data)
     cp = None if cfg is None else cfg.ptr
-    n = pin.refpin_template_cfg(float(sr), f300.ctypes.data_as(_dp), None, int(seed), cp, None, 0, None, None, None,
-                                None, None)
+    n = pin.refpin_template_full(float(sr), f300.ctypes.data_as(_dp), None, int(seed), cp, None, 0, None, None, None,
+                                 None, None, None, None, None, None, 0)
     bank = np.zeros(n, np.float32)
     lens = np.zeros(256, np.uint32)
     wf = np.zeros(256, np.float64)
     a = np.zeros((9, 128), np.float32)
     r = np.zeros((9, 128), np.float32)
     k = np.zeros(128, np.float32)
-    pin.refpin_template_cfg(float(sr), f300.ctypes.data_as(_dp), None, int(seed), cp, _f(bank), n,
-                            lens.ctypes.data_as(_u32p), wf.ctypes.data_as(_dp), _f(a), _f(r), _f(k))
-    return {"bank": bank, "lens": lens, "wfreq": wf, "attack": a, "release": r, "keycomp": k}
+    cn = np.zeros(384, np.uint32)
+    cw, cb, cl = np.zeros(CONTRIB_CAP, np.int16), np.zeros(CONTRIB_CAP, np.int16), np.zeros(CONTRIB_CAP, np.float32)
+    pin.refpin_template_full(float(sr), f300.ctypes.data_as(_dp), None, int(seed), cp, _f(bank), n,
+                             lens.ctypes.data_as(_u32p), wf.ctypes.data_as(_dp), _f(a), _f(r), _f(k),
+                             cn.ctypes.data_as(_u32p), cw.ctypes.data, cb.ctypes.data, _f(cl), CONTRIB_CAP)
+    assert int(cn.sum()) <= CONTRIB_CAP
+    return {"bank": bank, "lens": lens, "wfreq": wf, "attack": a, "release": r, "keycomp": k,
+            "contrib": contrib_blob(cn, cw, cb, cl)}
 
 
 class Cfg:
@@ -200,6 +235,12 @@ class Template:
         k = np.zeros(128, np.float32)
         self.lib.orc_template_envs(self.ptr, _f(a), _f(r), _f(k))
         return a, r, k
+
+    def contrib(self):
+        """contrib_blob of the oracle's play matrix"""
+        self.lib.orc_template_contrib.restype = C.c_int
+        self.lib.orc_template_contrib.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        return contrib_from(lambda k, w, b, lv, cap: self.lib.orc_template_contrib(self.ptr, k, w, b, lv, cap))
 
     def dump(self, d):
         return self.lib.orc_template_dump(self.ptr, str(d).encode())

@@ -163,6 +163,19 @@ CFG_SETS = {
                   "osc.attack.click.minlength": 0.05, "osc.attack.click.maxlength": 0.4, "osc.x-precision": 0.002},
     "envelopes2": {"osc.attack.model": "cosine", "osc.release.model": "shelf", "osc.attack.click.level": 0.7,
                    "osc.attack.click.maxlength": 0.3},
+    # the tone generator's list keys (oscConfig, src/tonegen.cpp:2296-2474): extra wheel
+    # harmonics (all wheels / one wheel), a terminal's own mix, key tapers (a manual key
+    # and a pedal), explicit key crosstalk, the spline EQ points
+    "osc_lists": [("osc.harmonic.3", 0.05), ("osc.harmonic.2", 0.1), ("osc.harmonic.w40.f5", 0.2),
+                  ("osc.harmonic.w40.f2", -0.05), ("osc.terminal.t57.w57", 0.9), ("osc.terminal.t57.w45", 0.05),
+                  ("osc.terminal.t60.w60", 0.7), ("osc.taper.k60.b2.t57", 0.8), ("osc.taper.k60.b3.t69", 0.5),
+                  ("osc.taper.k60.b8.t60", 0.3), ("osc.taper.k260.b19.t40", 1.0), ("osc.taper.k260.b20.t52", 0.6),
+                  ("osc.crosstalk.k60", "1:45:0.02, 4:57:0.01,7:81:0.004"), ("osc.crosstalk.k188", "12:60:0.03"),
+                  ("osc.eq.p1y", 0.8), ("osc.eq.r1y", 0.3), ("osc.eq.p4y", 0.6), ("osc.eq.r4y", -0.2)],
+    # the wheel EQ macro and the default crosstalk model's levels / the contribution floor
+    "osc_models": {"osc.eq.macro": "peak46", "osc.compartment-crosstalk": 0.03, "osc.transformer-crosstalk": 0,
+                   "osc.terminalstrip-crosstalk": 0.005, "osc.wiring-crosstalk": 0.02,
+                   "osc.contribution-floor": 0.0005, "osc.contribution-min": 0.001},
 }
 
 

@@ -24,7 +24,8 @@ def _setup(oracle, n, scen_fn, chain=0, tpl_seed=7, sr=48000.0, debug_flags=0, c
     from orc_bind import Cfg, Template
     eng = _engine(chain, sr, debug_flags)
     if cfg is not None:  # as a cfg file's text, through tbf_config_parse
-        assert eng.config_parse("# cfg\n" + "".join(f"{k} = {v}\n" for k, v in cfg.items())) == len(cfg)
+        items = list(cfg.items()) if isinstance(cfg, dict) else list(cfg)
+        assert eng.config_parse("# cfg\n" + "".join(f"{k} = {v}\n" for k, v in items)) == len(items)
     tid = eng.template(seed=tpl_seed)
     seeds = [1000 + 17 * i for i in range(n)]
     eng.add_instances([tid] * n, seeds)
@@ -363,20 +364,26 @@ def test_gpu_device_templates_match_oracle_and_reference(oracle, sr):
     print(f"device templates @{sr:.0f}: {len(cases)} vs oracle, {len(pins)} vs reference pins; "
           f"first batch of {len(table_pins)} in {t_dev * 1e3:.1f} ms")
     eng.close()
-    # the template cfg keys (envelope models, lengths, levels, x-precision) on the device path
-    from orc_bind import Cfg
+    # the template cfg keys (envelope models, lengths, levels, x-precision; wheel EQ,
+    # harmonics, the play matrix lists and levels) on the device path
+    from orc_bind import Cfg, contrib_from
+    lib.tbf_debug_contrib.restype = C.c_int
+    lib.tbf_debug_contrib.argtypes = [C.c_void_p, C.c_uint32, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.c_uint32]
     for p in [p for p in allpins if p["sr"] == sr and p.get("cfg")]:
         eng = T.Engine(sample_rate=sr, device=0)
         eng.config(S.CFG_SETS[p["cfg"]])
-        tid = eng.templates([p["seed"]])[0]
+        m = mts(p["tuning"])
+        tid = eng.templates([p["seed"]], mts128=None if m is None else m[None])[0]
         bank, lens = eng.template_bank(tid)
         a, r, k = np.zeros((9, 128), np.float32), np.zeros((9, 128), np.float32), np.zeros(128, np.float32)
         assert lib.tbf_debug_tables(eng._h, tid, a.ctypes.data, r.ctypes.data, k.ctypes.data) >= 0
         got = {"bank": bank, "lens": lens, "attack": a, "release": r, "keycomp": k}
-        o = Template(oracle, sr=sr, mts128=None, seed=p["seed"], cfg=Cfg(oracle, S.CFG_SETS[p["cfg"]]))
+        got["contrib"] = contrib_from(lambda kk, w, b, lv, cap: lib.tbf_debug_contrib(eng._h, tid, kk, w, b, lv, cap))
+        o = Template(oracle, sr=sr, mts128=m, seed=p["seed"], cfg=Cfg(oracle, S.CFG_SETS[p["cfg"]]))
         ob, ol = o.bank()
         oa, orr, ok = o.envs()
-        want = {"bank": ob, "lens": ol, "attack": oa, "release": orr, "keycomp": ok}
+        want = {"bank": ob, "lens": ol, "attack": oa, "release": orr, "keycomp": ok, "contrib": o.contrib()}
         for key, v in got.items():
             assert np.array_equal(np.asarray(v).view(np.uint32), np.asarray(want[key]).view(np.uint32)), (p["cfg"], key)
             assert hashlib.sha256(np.ascontiguousarray(v).tobytes()).hexdigest() == p[key], (p["cfg"], key)

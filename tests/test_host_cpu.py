@@ -370,9 +370,9 @@ def test_glibc_rand_jump_matches_literal_draws():
 
 def test_config_api_semantics():
     """tbf_config_set / tbf_config_parse return codes (include/tbf.h): applied, ignored
-    (keys of other modules; overdrive.* / xov.* accepted with no effect), bad values
-    (getConfigParameter_*'s ranges, src/cfgParser.cpp:453-620: nothing assigned),
-    unimplemented keys of these modules, engine-wide keys after instances exist, and the
+    (keys of other modules, and keys the reference stores but never reads on this path),
+    bad values (getConfigParameter_*'s ranges, src/cfgParser.cpp:453-620, and malformed
+    list keys: nothing assigned), engine-wide keys after instances exist, and the
     parser's line-numbered errors."""
     import scenarios as S
     eng = T.Engine(device=-1)
@@ -385,9 +385,22 @@ def test_config_api_semantics():
                  ("whirl.horn.brakepos", -0.1), ("osc.perc.bus.trig", -2)):
         with pytest.raises(T.TbfError, match="-22"):
             eng.config_set(k, v)
-    for k in ("osc.tuning", "osc.temperament", "osc.crosstalk.k6", "whirl.horn.comb.a.feedback"):
-        with pytest.raises(T.TbfError, match="-95"):
-            eng.config_set(k, 1)
+    # keys the reference stores but never reads on this path
+    for k, v in (("osc.tuning", 440), ("osc.temperament", "gear60"), ("osc.eqv.5", 0.5),
+                 ("whirl.horn.comb.a.feedback", -0.5)):
+        assert eng.config_set(k, v) == 1
+    # the tone generator's list keys: well formed, or refused whole
+    assert eng.config_set("osc.crosstalk.k60", "1:45:0.02, 4:57:0.01") == 0
+    assert eng.config_set("osc.taper.k60.b2.t57", 0.8) == 0
+    assert eng.config_set("osc.harmonic.w40.f3", 0.1) == 0
+    assert eng.config_set("osc.eq.macro", "peak24") == 0
+    for k, v in (("osc.crosstalk.k60", "1:45:0.02,4:57"), ("osc.crosstalk.k0", "1:45:0.02"),
+                 ("osc.taper.k60.b0.t57", 0.5), ("osc.taper.k60.b2.t257", 0.5), ("osc.harmonic.0", 0.1),
+                 ("osc.harmonic.w0.f2", 0.1), ("osc.terminal.t3.w300", 0.1), ("osc.eq.macro", "flat"),
+                 ("osc.transformer-crosstalk", 0.02)):
+        with pytest.raises(T.TbfError, match="-22"):
+            eng.config_set(k, v)
+    assert eng.config_set("osc.transformer-crosstalk", 0) == 0
     # geometry beyond the reference's 2048-sample ring is refused and leaves the engine as it was
     with pytest.raises(T.TbfError, match="-22"):
         eng.config_set("whirl.horn.radius", 1000)
@@ -420,11 +433,14 @@ def test_device_templates_refused_on_host_engine():
 
 def test_host_templates_vs_reference_pins(tunings):
     """The product's host template builder (tbf_template_create on a host-only engine)
-    gives the wave banks, lengths, envelopes and key-compression tables of the
-    reference's own src/tonegen.cpp builders (digests in tests/golden/template_pins.json,
-    see tests/golden/make_template_pins.py), bit for bit: 7 tunings x 48 / 96 kHz."""
+    gives the wave banks, lengths, envelopes, key-compression tables and play matrices of
+    the reference's own src/tonegen.cpp builders (digests in tests/golden/template_pins.json,
+    see tests/golden/make_template_pins.py), bit for bit: 7 tunings x 48 / 96 kHz and the
+    osc.* cfg sets (envelope models, wheel EQ, harmonics, terminal / taper / crosstalk
+    lists, crosstalk levels, contribution floor / minimum)."""
     import hashlib
     import json
+    from orc_bind import contrib_from
     pins = json.loads((ROOT / "tests" / "golden" / "template_pins.json").read_text())
     lib = T.load_library()
     _bind_debug(lib)
@@ -441,9 +457,11 @@ def test_host_templates_vs_reference_pins(tunings):
         bank, lens = eng.template_bank(tid)
         a, r, k = np.zeros((9, 128), np.float32), np.zeros((9, 128), np.float32), np.zeros(128, np.float32)
         assert lib.tbf_debug_tables(eng._h, tid, a.ctypes.data, r.ctypes.data, k.ctypes.data) == 0
-        got = {"bank": bank, "lens": lens, "attack": a, "release": r, "keycomp": k}
+        got = {"bank": bank, "lens": lens, "attack": a, "release": r, "keycomp": k,
+               "contrib": contrib_from(lambda kk, w, b, lv, cap: lib.tbf_debug_contrib(eng._h, tid, kk, w, b, lv, cap))}
         for key, v in got.items():
-            assert hashlib.sha256(np.ascontiguousarray(v).tobytes()).hexdigest() == p[key], (p["tuning"], p["sr"], key)
+            assert hashlib.sha256(np.ascontiguousarray(v).tobytes()).hexdigest() == p[key], \
+                (p["tuning"], p["sr"], p.get("cfg"), key)
     for e in engines.values():
         e.close()
 

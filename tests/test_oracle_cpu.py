@@ -224,25 +224,26 @@ def _template_pins():
 
 def test_oracle_templates_vs_reference_pins(oracle, tunings):
     """The oracle's wave banks (writeSamples sines + per-sample rand() LSB), wheel
-    lengths, envelopes and key-compression tables equal, bit for bit, the tables the
-    reference's own src/tonegen.cpp builds (static initOscillators / initKeyCompTable /
-    initEnvelopes reached by oracle/ref_tpl_pin.cpp; digests committed in
-    tests/golden/template_pins.json by tests/golden/make_template_pins.py): 7 tunings x
-    48 / 96 kHz."""
+    lengths, envelopes, key-compression tables and play matrices equal, bit for bit, the
+    tables the reference's own src/tonegen.cpp builds (static initOscillators /
+    initKeyCompTable / initEnvelopes / applyManualDefaults / compilePlayMatrix ... reached
+    by oracle/ref_tpl_pin.cpp; digests committed in tests/golden/template_pins.json by
+    tests/golden/make_template_pins.py): 7 tunings x 48 / 96 kHz, plus the osc.* cfg sets
+    (envelope models, wheel EQ, harmonics, terminal / taper / crosstalk lists)."""
     import hashlib
-    from golden.make_template_pins import digest
     from orc_bind import Cfg
     pins = _template_pins()
-    assert len(pins) == 16
+    assert len(pins) == 19
     for p in pins:
         m = None if tunings[p["tuning"]] is None else np.array(tunings[p["tuning"]], np.float64)
         cfg = Cfg(oracle, S.CFG_SETS[p["cfg"]]) if p.get("cfg") else None
         tpl = Template(oracle, sr=p["sr"], mts128=m, seed=p["seed"], cfg=cfg)
         bank, lens = tpl.bank()
         a, r, k = tpl.envs()
-        got = {"bank": bank, "lens": lens, "attack": a, "release": r, "keycomp": k}
+        got = {"bank": bank, "lens": lens, "attack": a, "release": r, "keycomp": k, "contrib": tpl.contrib()}
         for key, v in got.items():
-            assert hashlib.sha256(np.ascontiguousarray(v).tobytes()).hexdigest() == p[key], (p["tuning"], p["sr"], key)
+            assert hashlib.sha256(np.ascontiguousarray(v).tobytes()).hexdigest() == p[key], \
+                (p["tuning"], p["sr"], p.get("cfg"), key)
 
 
 def test_reference_pin_harness_reproduces_committed_pins(oracle, tunings):

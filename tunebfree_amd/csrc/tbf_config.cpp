@@ -3,13 +3,16 @@
  *
  * The reference routes each `key=value` cfg line to every module's config function
  * (distributeParameter, src/cfgParser.cpp:61-92); the ones that reach this engine's
- * tables are whirlConfig (src/whirl.cpp:992-1160), oscConfig's scalar keys
- * (src/tonegen.cpp:2173-2555), scannerConfig (src/vibrato.cpp:334-357) and
- * reverbConfig (src/reverb.cpp:242-256).  Values parse like getConfigParameter_d/_dr/
- * _i/_ir (src/cfgParser.cpp:453-620): sscanf %lf / %d, inclusive ranges, and a value
- * that fails either assigns nothing.  overdrive.* / xov.* (ampConfig,
- * src/overdrive.cpp:395-433) write legacy fields that airwindows_density never reads:
- * accepted, no effect, as in the reference.
+ * tables are whirlConfig (src/whirl.cpp:992-1160), oscConfig (src/tonegen.cpp:2173-2555),
+ * scannerConfig (src/vibrato.cpp:334-357) and reverbConfig (src/reverb.cpp:242-256).
+ * Values parse like getConfigParameter_d/_dr/_i/_ir (src/cfgParser.cpp:453-620): sscanf
+ * %lf / %d, inclusive ranges, and a value that fails either assigns nothing.  Keys the
+ * reference stores but never reads on this path are ignored: overdrive.* / xov.*
+ * (ampConfig, src/overdrive.cpp:395-433: legacy fields airwindows_density never reads),
+ * osc.tuning / osc.temperament (the wheel frequencies come from MTS-ESP; the gear code
+ * that read them is compiled out, src/tonegen.cpp:1518-1556), osc.eqv.* (cleared by
+ * initToneGenerator before initOscillators reads them, 2933-2937) and
+ * whirl.horn.comb.* (the comb filter is compiled out, src/whirl.cpp:1527-1533).
  */
 #include <stdio.h>
 #include <string.h>
@@ -50,6 +53,60 @@ void envModel (const char* v, int& m)
 		m = ENV_LINEAR;
 	else if (!strcasecmp (v, "shelf"))
 		m = ENV_SHELF;
+}
+
+int push (Config& c, int kind, int idx, int sa, int sb, double fc)
+{
+	c.lists.push_back ({(int16_t)kind, (int16_t)idx, (int16_t)sa, (int16_t)sb, (float)fc});
+	return 1;
+}
+
+/* oscConfig's list keys (src/tonegen.cpp:2296-2474).  The reference appends every
+ * well-formed element and warns about the rest; here a key with any malformed or
+ * out-of-range part assigns nothing (-1).  A harmonic number below 1 would fail
+ * initOscillators' assert (1604-1605) and is refused. */
+int listKey (Config& c, const char* k, const char* v)
+{
+	int    n, w, b, kk;
+	double x;
+	if (!strncasecmp (k, "osc.harmonic.", 13)) {
+		if (sscanf (k + 13, "%d", &n) == 1) {
+			if (sscanf (v, "%lf", &x) != 1 || n < 1 || 32767 < n)
+				return -1;
+			return push (c, LE_HARMONIC, 0, n, 0, x);
+		}
+		if (sscanf (k + 13, "w%d.f%d", &w, &n) == 2) {
+			if (!(0 < w && w <= TBF_NW) || n < 1 || 32767 < n || sscanf (v, "%lf", &x) != 1)
+				return -1;
+			return push (c, LE_HARMONIC, w, n, 0, x);
+		}
+		return -1;
+	}
+	if (!strncasecmp (k, "osc.terminal.", 13)) {
+		if (sscanf (k + 13, "t%d.w%d", &n, &w) != 2 || !(0 < n && n <= TBF_NW) || !(0 < w && w <= TBF_NW) ||
+		    sscanf (v, "%lf", &x) != 1)
+			return -1;
+		return push (c, LE_TERMINAL, n, w, 0, x);
+	}
+	if (!strncasecmp (k, "osc.taper.", 10)) { /* bus 0 refused, as the reference's 0 < b */
+		if (sscanf (k + 10, "k%d.b%d.t%d", &kk, &b, &w) != 3 || !(0 < kk && kk < 384) || !(0 < b && b < 27) ||
+		    !(0 < w && w <= TBF_NW) || sscanf (v, "%lf", &x) != 1)
+			return -1;
+		return push (c, LE_TAPER, kk, w, b, x);
+	}
+	if (!strncasecmp (k, "osc.crosstalk.", 14)) { /* "bus:terminal:level, ..." */
+		if (sscanf (k + 14, "k%d", &kk) != 1 || !(0 < kk && kk < 384))
+			return -1;
+		std::vector<Config::ListEntry> add;
+		for (const char* p = v; p; p = strchr (p, ',') ? strchr (p, ',') + 1 : nullptr) {
+			if (sscanf (p, "%d:%d:%lf", &b, &w, &x) != 3 || !(0 < b && b < 27) || !(0 < w && w <= TBF_NW))
+				return -1;
+			add.push_back ({LE_XTALK, (int16_t)kk, (int16_t)w, (int16_t)b, (float)x});
+		}
+		c.lists.insert (c.lists.end (), add.begin (), add.end ());
+		return 1;
+	}
+	return 0;
 }
 
 } // namespace
@@ -118,6 +175,18 @@ int configSet (Config& c, const char* k, const char* v, int* scope)
 		{"osc.attack.click.maxlength", 'r', 0.0, 1.0, CFG_TEMPLATE, [] (Config& c, double d, int) { c.envAtkClkMaxLength = (int)(128.0 * d); }},
 		{"osc.attack.click.minlength", 'r', 0.0, 1.0, CFG_TEMPLATE, [] (Config& c, double d, int) { c.envAtkClkMinLength = (int)(128.0 * d); }},
 		{"osc.release.click.level", 'r', 0.0, 1.0, CFG_TEMPLATE, [] (Config& c, double d, int) { c.envReleaseClickLevel = (float)d; }},
+		{"osc.eq.p1y", 'd', 0, 0, CFG_TEMPLATE, [] (Config& c, double d, int) { c.eqP1y = d; }},
+		{"osc.eq.r1y", 'd', 0, 0, CFG_TEMPLATE, [] (Config& c, double d, int) { c.eqR1y = d; }},
+		{"osc.eq.p4y", 'd', 0, 0, CFG_TEMPLATE, [] (Config& c, double d, int) { c.eqP4y = d; }},
+		{"osc.eq.r4y", 'd', 0, 0, CFG_TEMPLATE, [] (Config& c, double d, int) { c.eqR4y = d; }},
+		{"osc.compartment-crosstalk", 'r', 0.0, 1.0, CFG_TEMPLATE, [] (Config& c, double d, int) { c.compartmentXT = d; }},
+		/* above 0 initToneGenerator aborts: findTransformerNeighbours asserts for every
+		 * wheel above 91 (src/tonegen.cpp:914-927, called for 44..256 at 973-978) */
+		{"osc.transformer-crosstalk", 'r', 0.0, 0.0, CFG_TEMPLATE, [] (Config& c, double d, int) { c.transformerXT = d; }},
+		{"osc.terminalstrip-crosstalk", 'r', 0.0, 1.0, CFG_TEMPLATE, [] (Config& c, double d, int) { c.stripXT = d; }},
+		{"osc.wiring-crosstalk", 'r', 0.0, 1.0, CFG_TEMPLATE, [] (Config& c, double d, int) { c.wiringXT = d; }},
+		{"osc.contribution-floor", 'r', 0.0, 1.0, CFG_TEMPLATE, [] (Config& c, double d, int) { c.contribFloor = d; }},
+		{"osc.contribution-min", 'r', 0.0, 1.0, CFG_TEMPLATE, [] (Config& c, double d, int) { c.contribMin = d; }},
 		/* ... and instances (percussion) */
 		{"osc.perc.fast", 'd', 0, 0, CFG_INSTANCE, [] (Config& c, double d, int) { c.percFastDecaySeconds = d; }},
 		{"osc.perc.slow", 'd', 0, 0, CFG_INSTANCE, [] (Config& c, double d, int) { c.percSlowDecaySeconds = d; }},
@@ -155,19 +224,26 @@ int configSet (Config& c, const char* k, const char* v, int* scope)
 			*scope = CFG_TEMPLATE;
 		return 1;
 	}
-	/* keys of these modules the engine does not implement (list-valued tonegen
-	 * models, the comb filter, EQ macros, tuning: tuneBfree takes frequencies from
-	 * MTS-ESP) */
-	static const char* const todo[] = {"osc.tuning", "osc.temperament", "osc.eq.", "osc.eqv.", "osc.harmonic.",
-	                                   "osc.terminal.", "osc.taper.", "osc.crosstalk.", "osc.compartment-crosstalk",
-	                                   "osc.transformer-crosstalk", "osc.terminalstrip-crosstalk",
-	                                   "osc.wiring-crosstalk", "osc.contribution-floor", "osc.contribution-min",
-	                                   "whirl.horn.comb."};
-	for (const char* t : todo)
-		if (!strncasecmp (k, t, strlen (t)))
-			return -2;
-	/* overdrive.* / xov.* (ampConfig, src/overdrive.cpp:395-433) set fields the
-	 * airwindows_density preamp never reads: ignored like any other module's keys */
+	if (!strcasecmp (k, "osc.eq.macro")) {
+		if (!strcasecmp (v, "chspline"))
+			c.eqMacro = EQ_SPLINE;
+		else if (!strcasecmp (v, "peak24"))
+			c.eqMacro = EQ_PEAK24;
+		else if (!strcasecmp (v, "peak46"))
+			c.eqMacro = EQ_PEAK46;
+		else
+			return -1;
+		if (scope)
+			*scope = CFG_TEMPLATE;
+		return 1;
+	}
+	if (int r = listKey (c, k, v)) {
+		if (scope)
+			*scope = r == 1 ? CFG_TEMPLATE : 0;
+		return r;
+	}
+	/* everything else, including the keys with no effect on this path (header), is
+	 * ignored like any other module's keys */
 	return 0;
 }
 

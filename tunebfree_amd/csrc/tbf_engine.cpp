@@ -579,8 +579,6 @@ int tbf_config_set (tbf_engine* e, const char* key, const char* value)
 	int    rc    = configSet (c, key, value, &scope);
 	if (rc == -1)
 		return fail (-22, std::string ("bad value for ") + key + ": " + value);
-	if (rc == -2)
-		return fail (-95, std::string ("cfg key not implemented by this engine: ") + key);
 	if (rc == 0)
 		return 1; /* not a key of the hot path: ignored, as the reference ignores it */
 	if ((scope & CFG_SHARED) && !e->inst.empty ())

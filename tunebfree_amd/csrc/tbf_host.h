@@ -42,10 +42,12 @@ struct Contrib {
 
 /* The hot path's cfg keys (parseConfigurationLine / distributeParameter,
  * src/cfgParser.cpp:61-160) with the reference's defaults and field types:
- * whirlConfig (src/whirl.cpp:992-1160; initValues 43-134), the scalar keys of oscConfig
+ * whirlConfig (src/whirl.cpp:992-1160; initValues 43-134), oscConfig
  * (src/tonegen.cpp:2173-2555; initValues 238-331), scannerConfig (src/vibrato.cpp:334-357)
  * and reverbConfig (src/reverb.cpp:242-256). */
 enum { ENV_CLICK = 0, ENV_COSINE = 1, ENV_LINEAR = 2, ENV_SHELF = 3 };
+enum { EQ_SPLINE = 0, EQ_PEAK24 = 1, EQ_PEAK46 = 2 };                 /* src/tonegen.cpp:143-145 */
+enum { LE_HARMONIC = 0, LE_TERMINAL = 1, LE_TAPER = 2, LE_XTALK = 3 }; /* which list */
 struct Config {
 	/* whirl.* */
 	float  hornRPMslow = (float)(60.0 * 0.672), hornRPMfast = (float)(60.0 * 7.056);
@@ -71,14 +73,28 @@ struct Config {
 	float  envAttackClickLevel = 0.50f, envReleaseClickLevel = 0.25f;
 	int    envAtkClkMinLength = -1, envAtkClkMaxLength = -1; /* -1: from the sample rate */
 	int    envAttackModel = ENV_CLICK, envReleaseModel = ENV_LINEAR;
+	/* osc.* tone-generator model keys (initValues 302-316): wheel EQ, the default
+	 * crosstalk model's levels, the play matrix contribution floor / minimum */
+	int    eqMacro = EQ_SPLINE;
+	double eqP1y = 1.0, eqR1y = 0.0, eqP4y = 1.0, eqR4y = 0.0;
+	double compartmentXT = 0.01, transformerXT = 0.0, stripXT = 0.01, wiringXT = 0.01;
+	double contribFloor = 0.0000158, contribMin = 0.0;
+	/* osc.harmonic.* / osc.terminal.* / osc.taper.* / osc.crosstalk.*: one element per
+	 * appendListElement of oscConfig (src/tonegen.cpp:2296-2474), in file order */
+	struct ListEntry {
+		int16_t kind, idx; /* LE_*, list index (wheel / terminal / key) */
+		int16_t sa, sb;    /* harmonic number | wheel | terminal ; bus */
+		float   fc;        /* level */
+	};
+	std::vector<ListEntry> lists;
 };
 
 /* what a cfg key touches (configSet's `scope` out-parameter) */
 enum { CFG_SHARED = 1, /* engine-wide tables: whirl.*, scanner.* */
        CFG_TEMPLATE = 2, /* templates created afterwards: osc.x-precision, envelopes */
        CFG_INSTANCE = 4 /* instances added afterwards: perc, reverb.mix, per-instance whirl */ };
-/* one key=value: 1 applied, 0 not a key of the hot path, -1 unparsable / out of range
- * (nothing assigned), -2 a key of the reference this engine does not implement */
+/* one key=value: 1 applied, 0 not a key of the hot path or a key with no effect on it,
+ * -1 unparsable / out of range (nothing assigned) */
 int configSet (Config& c, const char* key, const char* value, int* scope);
 
 struct TgTemplate {

@@ -149,29 +149,45 @@ struct Le {
 	float fc;
 };
 
-/* src/tonegen.cpp:933-1213 applyDefaultConfiguration + compilePlayMatrix */
+/* src/tonegen.cpp:933-1213 applyDefaultConfiguration + compilePlayMatrix, over the cfg's
+ * lists (t.cfg.lists: a key / terminal with its own list keeps it and gets no default) */
 static void playMatrix (TgTemplate& t)
 {
+	const Config&   cf = t.cfg;
 	std::vector<Le> terminalMix[TBF_NW + 1], keyTaper[384], keyCrosstalk[384];
-	for (int i = 1; i <= TBF_NW; i++) {
-		terminalMix[i].push_back ({(short)i, 0, (float)(1.0 - 0.01)});
-		short pw = pairedWheel ((short)i);
-		if (0 < pw && pw <= TBF_NW)
-			terminalMix[i].push_back ({pw, 0, (float)0.01});
+	for (const Config::ListEntry& e : cf.lists) {
+		if (e.kind == LE_TERMINAL)
+			terminalMix[e.idx].push_back ({e.sa, 0, e.fc});
+		else if (e.kind == LE_TAPER)
+			keyTaper[e.idx].push_back ({e.sa, e.sb, e.fc});
+		else if (e.kind == LE_XTALK)
+			keyCrosstalk[e.idx].push_back ({e.sa, e.sb, e.fc});
 	}
 	for (int i = 1; i <= TBF_NW; i++) {
-		for (int j = 0; kTerminalStrip[j] > 0; j++) {
-			if (kTerminalStrip[j] == (short)i) {
-				int east = j > 0 ? kTerminalStrip[j - 1] : 0;
-				int west = kTerminalStrip[j + 1];
-				if (east > 0)
-					terminalMix[i].push_back ({(short)east, 0, (float)0.01});
-				if (west > 0)
-					terminalMix[i].push_back ({(short)west, 0, (float)0.01});
-				break;
-			}
+		if (!terminalMix[i].empty ())
+			continue;
+		terminalMix[i].push_back ({(short)i, 0, (float)(1.0 - cf.compartmentXT)});
+		if (0.0 < cf.compartmentXT) {
+			short pw = pairedWheel ((short)i);
+			if (0 < pw && pw <= TBF_NW)
+				terminalMix[i].push_back ({pw, 0, (float)cf.compartmentXT});
 		}
 	}
+	/* transformer crosstalk (971-997): configSet admits only 0, see tbf_config.cpp */
+	if (0.0 < cf.stripXT)
+		for (int i = 1; i <= TBF_NW; i++) {
+			for (int j = 0; kTerminalStrip[j] > 0; j++) {
+				if (kTerminalStrip[j] == (short)i) {
+					int east = j > 0 ? kTerminalStrip[j - 1] : 0;
+					int west = kTerminalStrip[j + 1];
+					if (east > 0)
+						terminalMix[i].push_back ({(short)east, 0, (float)cf.stripXT});
+					if (west > 0)
+						terminalMix[i].push_back ({(short)west, 0, (float)cf.stripXT});
+					break;
+				}
+			}
+		}
 	/* applyManualDefaults (707-802) */
 	double of[TBF_NW + 1];
 	for (int i = 1; i <= TBF_NW; i++)
@@ -179,6 +195,8 @@ static void playMatrix (TgTemplate& t)
 	for (int man = 0; man < 2; man++) {
 		const int keyOffset = man * 128, busOffset = man * 9;
 		for (int k = 0; k < 128; k++) {
+			if (!keyTaper[k + keyOffset].empty ())
+				continue;
 			for (int b = 0; b < 9; b++) {
 				float smallest = std::numeric_limits<float>::infinity ();
 				int   best     = 0;
@@ -197,23 +215,29 @@ static void playMatrix (TgTemplate& t)
 	}
 	/* applyPedalDefaults (810-841) */
 	static const int PDoffset[9] = {-12, 7, 0, 12, 19, 24, 28, 31, 36};
-	for (int k = 0; k < 32; k++)
+	for (int k = 0; k < 32; k++) {
+		if (!keyTaper[k + 256].empty ())
+			continue;
 		for (int b = 0; b < 9; b++) {
 			int tn = (k + 1) + PDoffset[b];
 			if (tn < 1 || TBF_NW < tn)
 				continue;
 			keyTaper[k + 256].push_back ({(short)tn, (short)(b + 18), (float)dBToGain (0.0)});
 		}
+	}
 	/* applyDefaultCrosstalk (849-879) */
 	for (int man = 0; man < 2; man++)
 		for (int k = 0; k < 128; k++) {
 			const int kn = k + man * 128;
+			if (!keyCrosstalk[kn].empty ())
+				continue;
 			for (int b = 0; b < 9; b++) {
 				const int busNumber = man * 9 + b;
 				for (const Le& e : keyTaper[kn]) {
 					if (e.sb == busNumber)
 						continue;
-					keyCrosstalk[kn].push_back ({e.sa, (short)busNumber, (float)((0.01 * e.fc) / abs (busNumber - e.sb))});
+					keyCrosstalk[kn].push_back (
+					    {e.sa, (short)busNumber, (float)((cf.wiringXT * e.fc) / abs (busNumber - e.sb))});
 				}
 			}
 		}
@@ -259,9 +283,11 @@ static void playMatrix (TgTemplate& t)
 		std::vector<Contrib>& out = t.keyContrib[k];
 		for (int w = 0; w < endRow; w++)
 			for (int c = 0; c < rowLength[w]; c++) {
-				if (cpmGain[w][c] < 0.0000158)
+				if (cpmGain[w][c] < cf.contribFloor)
 					continue;
 				Contrib rep {wheelNumber[w], (int16_t)cpmBus[w][c], cpmGain[w][c]};
+				if (rep.level < cf.contribMin)
+					rep.level = (float)cf.contribMin;
 				size_t  at = 0;
 				for (; at < out.size (); at++) {
 					if (rep.wheel < out[at].wheel)
@@ -319,25 +345,50 @@ void TgTemplate::prepare (double rate, const double* mts128, const double* ratio
 		v.clear ();
 	playMatrix (*this);
 
-	/* initOscillators (1470-1630): spline EQ (p1y=1,r1y=0,p4y=1,r4y=0), fitWave,
-	 * writeSamples with one rand() LSB per sample, wheels 1..256 in order */
+	/* initOscillators (1470-1630): wheel EQ (apply_CH_Spline 1240-1261 or the legacy
+	 * peak24 / peak46 damper curves 1223-1311), fitWave, the harmonics list (compile-time
+	 * fundamental + the cfg's global harmonics + this wheel's), writeSamples with one
+	 * rand() LSB per sample, wheels 1..256 in order */
+	auto damper = [] (int thisTG, int firstTG, int lastTG, double w, double v, double u) {
+		double x = ((double)(thisTG - firstTG)) / ((double)(lastTG - firstTG));
+		double z = (x * (u - v)) - u;
+		return 1.0 - w * z * z;
+	};
 	total = 0;
 	for (int i = 1; i <= TBF_NW; i++) {
-		double k   = TBF_NW - 1;
-		double tt  = ((double)(i - 1)) / k;
-		double tSq = tt * tt;
-		double tCb = tSq * tt;
-		double r   = 1.0 * (2.0 * tCb - 3.0 * tSq + 1.0) + 1.0 * (-2.0 * tCb + 3.0 * tSq) + 0.0 * (tCb - 2.0 * tSq + tt) +
-		           0.0 * (tCb - tSq);
-		const double att = (r < 0.0) ? 0.0 : (1.0 < r) ? 1.0 : r;
+		double att;
+		if (c.eqMacro == EQ_SPLINE) {
+			double k   = TBF_NW - 1;
+			double tt  = ((double)(i - 1)) / k;
+			double tSq = tt * tt;
+			double tCb = tSq * tt;
+			double r   = c.eqP1y * (2.0 * tCb - 3.0 * tSq + 1.0) + c.eqP4y * (-2.0 * tCb + 3.0 * tSq) +
+			           c.eqR1y * (tCb - 2.0 * tSq + tt) + c.eqR4y * (tCb - tSq);
+			att = (r < 0.0) ? 0.0 : (1.0 < r) ? 1.0 : r;
+		} else if (c.eqMacro == EQ_PEAK24) {
+			att = i <= 43 ? damper (i, 1, 43, 0.2, -0.8, 1.0)
+			    : i <= 48 ? damper (i, 44, 48, 1.6, -0.4, -0.3)
+			              : damper (i, 49, TBF_NW, 0.9, -1.0, -0.7);
+		} else {
+			att = i <= 43 ? damper (i, 1, 43, 0.3, 0.4, 1.0)
+			    : i <= 48 ? damper (i, 44, 48, 0.1, -0.4, 0.4)
+			              : damper (i, 49, TBF_NW, 0.8, -1.0, -0.3);
+		}
 		const double wf  = fmin (fmax (frequency[i - 1], 12.0), 2.5e10);
 		const size_t wl  = fitWave (wf, c.tgPrecision, 3 * TBF_BLK, (int)(ceil (sr / 48000.0) * 4096), sr);
 		off[i]           = (uint32_t)total;
 		len[i]           = (uint32_t)wl;
 		total += wl;
+		double harm[12];
+		for (int j = 0; j < 12; j++)
+			harm[j] = j == 0 ? 1.0 : 0.0;
+		for (int pass = 0; pass < 2; pass++) /* wheelHarmonics[0], then wheelHarmonics[i] */
+			for (const Config::ListEntry& e : c.lists)
+				if (e.kind == LE_HARMONIC && e.idx == (pass ? i : 0) && e.sa - 1 < 12)
+					harm[e.sa - 1] += e.fc;
 		double apl[12], plHz[12], aplSum = 0.0;
 		for (int j = 0; j < 12; j++) {
-			apl[j] = j == 0 ? 1.0 : 0.0;
+			apl[j] = harm[j];
 			aplSum += fabs (apl[j]);
 			plHz[j] = wf * ((double)(j + 1));
 			if ((sr * 0.5) <= plHz[j])

@@ -137,6 +137,19 @@ int      tbf_instances_add (tbf_engine* e, uint32_t n, const uint32_t* tpl_ids, 
                             uint32_t* first);
 uint32_t tbf_instance_count (const tbf_engine* e);
 
+/* MTS-ESP retune (§8(f) row 3): the CLAP plugin's reinitToneGen (src/clap.cpp:129-157,
+ * run from process() when MTS_NoteToFrequency or the drawbar ratios change,
+ * src/clap.cpp:1133-1175) for instance inst on template tpl_id (built from the new
+ * frequencies / ratios with tbf_template_create or tbf_templates_create).  From the next
+ * block the instance plays a fresh tone generator on the new tables: no keys down,
+ * initToneGenerator's defaults, then drawbars 16'..1', vibrato on/off and vibrato type
+ * restored from the instance's CLAP parameter values (their get_info defaults when never
+ * set, src/clap.cpp:383-545) and the routing word kept; preamp, reverb and whirl state
+ * continue.  Events given after the call apply after the retune, as the reference
+ * checks the tuning at the top of process() before the block's events.  The osc.* /
+ * scanner.* cfg keys in force now apply to the new tone generator. */
+int tbf_instance_retune (tbf_engine* e, uint32_t inst, uint32_t tpl_id);
+
 int tbf_note (tbf_engine* e, uint32_t inst, int32_t key, int32_t on);
 int tbf_set_param (tbf_engine* e, uint32_t inst, int32_t param, double value);
 
@@ -222,6 +235,9 @@ int tbf_template_bank (tbf_engine* e, uint32_t tpl_id, float* out, uint64_t cap,
 /* play-matrix entries of one key (keyContrib, src/tonegen.cpp:1122-1213) */
 int tbf_debug_contrib (tbf_engine* e, uint32_t tpl_id, int32_t key, int16_t* wheel, int16_t* bus, float* level,
                        uint32_t cap);
+/* the cfg-derived HBM layout: the compact whirl ring window (512 / 1024 / 2048 samples
+ * per ring, from the geometry's largest write-ahead) and the reverb slab length */
+int tbf_debug_layout (const tbf_engine* e, uint32_t* wring_len, float* max_ahead, uint32_t* slab_len);
 /* envelopes (9 x 128 each) and key-compression table (128) of a template */
 int tbf_debug_tables (tbf_engine* e, uint32_t tpl_id, float* attack, float* release, float* keycomp);
 /* run one block of the tonegen control plane for an instance and return the core

@@ -174,6 +174,10 @@ orc_inst* orc_inst_new (const orc_template* tpl, unsigned int seed);
  * parses the cfg between alloc* and init* (whirl, scanner, percussion, reverb.mix) */
 orc_inst* orc_inst_new_cfg (const orc_template* tpl, unsigned int seed, const orc_cfg* cfg);
 void      orc_inst_free (orc_inst* p);
+/* the CLAP reinitToneGen on a new template (MTS-ESP retune / drawbar ratios), see
+ * orc_chain.c; takes effect from the next orc_render block */
+void      orc_inst_retune (orc_inst* p, const orc_template* tpl, const orc_cfg* cfg);
+void      orc_param_defaults (double* params64);
 void      orc_note (orc_inst* p, int key, int on);                 /* oscKeyOn/Off */
 void      orc_set_param (orc_inst* p, int pid, double value);      /* CLAP setParam */
 void      orc_set_chain (orc_inst* p, int mode);                   /* 0 full, 1 tonegen only */

@@ -31,7 +31,49 @@ orc_inst* orc_inst_new_cfg (const orc_template* tpl, unsigned int seed, const or
 	orc_tg_init (&p->tg, tpl, cfg);              /* allocTonegen + oscConfig/scannerConfig + initToneGenerator + init_vibrato */
 	for (i = 0; i < 9; i++)                      /* setDrawBars (inst, 0, defaultPreset) */
 		orc_tg_set_drawbar (&p->tg, i, defaultPreset[i]);
+	orc_param_defaults (p->params);
 	return p;
+}
+
+/* the CLAP parameters' default values (clap_plugin_params get_info, src/clap.cpp:383-545;
+ * the plugin's init copies them into its parameter array, 1062-1067) */
+void orc_param_defaults (double* params)
+{
+	static const float drawbar[9] = {7.0f, 8.0f, 8.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+	static const float top[9] = {1, 3, 1, 2, 3, 4, 5, 6, 8}, bottom[9] = {2, 2, 1, 1, 1, 1, 1, 1, 1};
+	int                i;
+	for (i = 0; i < 64; i++)
+		params[i] = 0.0;
+	for (i = 0; i < 9; i++) {
+		params[ORC_P_DRAWBAR_MIN + i] = drawbar[i];
+		params[20 + i]            = top[i];    /* P_RATIO_TOP_MIN */
+		params[29 + i]            = bottom[i]; /* P_RATIO_BOTTOM_MIN */
+	}
+	params[ORC_P_DRUM]   = 1.0f;
+	params[ORC_P_HORN]   = 1.0f;
+	params[ORC_P_REVERB] = 0.1f;
+}
+
+/* reinitToneGen (src/clap.cpp:129-157), the CLAP plugin's response to an MTS-ESP tuning
+ * or drawbar-ratio change: a fresh tone generator on the new template (allocTonegen +
+ * initToneGenerator + init_vibrato), the drawbars, vibrato switch and vibrato type
+ * restored from the parameter values, the routing word kept.  Preamp, reverb and whirl
+ * go on. */
+void orc_inst_retune (orc_inst* p, const orc_template* tpl, const orc_cfg* cfg)
+{
+	orc_cfg            dflt;
+	const unsigned int newRouting = p->tg.newRouting;
+	int                i;
+	if (!cfg) {
+		orc_cfg_default (&dflt);
+		cfg = &dflt;
+	}
+	orc_tg_init (&p->tg, tpl, cfg);
+	for (i = 0; i < 9; i++) /* setToneGenParam (108-121): float parameter values */
+		orc_tg_set_drawbar (&p->tg, i, (unsigned int)rintf ((float)p->params[ORC_P_DRAWBAR_MIN + i]));
+	orc_tg_set_vibrato_upper (&p->tg, (int)rintf ((float)p->params[ORC_P_VIBRATO]));
+	orc_tg_set_vibrato_from_int (&p->tg, (int)floorf ((float)p->params[ORC_P_VIBRATO_TYPE]));
+	p->tg.newRouting = newRouting;
 }
 
 void orc_inst_free (orc_inst* p)

@@ -226,7 +226,47 @@ API ref_inst* ref_inst_new_cfg (const orc_template* tpl, unsigned int seed, cons
 	static const unsigned int preset[9] = {8, 8, 6, 0, 0, 0, 0, 0, 0};
 	for (int i = 0; i < 9; i++)
 		setDrawBar (p->t, i, preset[i]);
+	orc_param_defaults (p->params); /* the CLAP parameters' defaults (src/clap.cpp:383-545, 1062-1067) */
 	return p;
+}
+
+/* the keyContrib lists ref_tonegen built, then the reference's freeToneGenerator */
+static void ref_tonegen_free (b_tonegen* t)
+{
+	for (int i = 0; i < MAX_KEYS; i++)
+		for (ListElement* e = t->keyContrib[i]; e;) {
+			ListElement* n = e->next;
+			free (e);
+			e = n;
+		}
+	freeToneGenerator (t);
+}
+
+/* reinitToneGen (src/clap.cpp:129-157) with the reference's own calls: the tone
+ * generator rebuilt on a new template, init_vibrato, setToneGenParam for the drawbars,
+ * vibrato switch and vibrato type from the parameter values, newRouting kept */
+API void ref_inst_retune (ref_inst* p, const orc_template* tpl, const orc_cfg* cfg)
+{
+	orc_cfg dflt;
+	if (!cfg) {
+		orc_cfg_default (&dflt);
+		cfg = &dflt;
+	}
+	const unsigned int newRouting = p->t->newRouting;
+	ref_tonegen_free (p->t);
+	p->t                          = ref_tonegen (tpl, cfg);
+	p->t->inst_vibrato.vibFqHertz = cfg->vibFqHertz;
+	p->t->inst_vibrato.vib1OffAmp = cfg->vib1OffAmp;
+	p->t->inst_vibrato.vib2OffAmp = cfg->vib2OffAmp;
+	p->t->inst_vibrato.vib3OffAmp = cfg->vib3OffAmp;
+	init_vibrato (&p->t->inst_vibrato, tpl->sr);
+	for (int i = 0; i < 9; i++) {
+		const float value = (float)p->params[i];
+		setDrawBar (p->t, i, rint (value));
+	}
+	setVibratoUpper (p->t, rint ((float)p->params[9]));
+	setVibratoFromInt (p->t, floor ((float)p->params[10]));
+	p->t->newRouting = newRouting;
 }
 
 API ref_inst* ref_inst_new (const orc_template* tpl, unsigned int seed) { return ref_inst_new_cfg (tpl, seed, NULL); }
@@ -238,6 +278,7 @@ API void ref_inst_free (ref_inst* p)
 	freeReverb (p->r);
 	freeWhirl (p->w);
 	freePreamp (p->p);
+	ref_tonegen_free (p->t);
 	free (p);
 }
 

@@ -6,9 +6,10 @@ import numpy as np
 import scenarios as S
 
 
-def engine_run(eng, scens, nblocks):
+def engine_run(eng, scens, nblocks, tids=None):
     """scens: list (one per instance) of scenario event lists; events land at block
-    boundaries exactly like the reference's MIDI (b_synth/lv2.cpp:1130-1134)."""
+    boundaries exactly like the reference's MIDI (b_synth/lv2.cpp:1130-1134).
+    ("retune", j, 0) retunes the instance to template tids[j] (tbf_instance_retune)."""
     bounds = {0, nblocks}
     for sc in scens:
         bounds.update(b for (b, *_r) in sc if b < nblocks)
@@ -21,6 +22,8 @@ def engine_run(eng, scens, nblocks):
                     continue
                 if kind == "note":
                     eng.note(i, a, v)
+                elif kind == "retune":
+                    eng.retune(i, tids[a])
                 else:
                     eng.set_param(i, a, v)
         L, R = eng.render(e - s)
@@ -29,13 +32,13 @@ def engine_run(eng, scens, nblocks):
     return np.concatenate(outL, axis=1), np.concatenate(outR, axis=1)
 
 
-def oracle_run(lib, tpl, seeds, scens, nblocks, chain=0):
+def oracle_run(lib, tpl, seeds, scens, nblocks, chain=0, templates=None):
     from orc_bind import Chain
     Ls, Rs, As, Bs, Cs = [], [], [], [], []
     for seed, sc in zip(seeds, scens):
         ch = Chain(lib, tpl, seed)
         ch.chain(1 if chain == 1 else 0)
-        L, R, A, B, C = S.run(ch, sc, nblocks, stages=True)
+        L, R, A, B, C = S.run(ch, sc, nblocks, stages=True, templates=templates)
         Ls.append(L); Rs.append(R); As.append(A); Bs.append(B); Cs.append(C)
     return [np.stack(x) for x in (Ls, Rs, As, Bs, Cs)]
 

@@ -63,6 +63,7 @@ def load_oracle():
     lib.orc_template_new_cfg.argtypes = [C.c_double, C.c_void_p, C.c_void_p, C.c_uint, C.c_void_p]
     lib.orc_inst_new_cfg.restype = C.c_void_p
     lib.orc_inst_new_cfg.argtypes = [C.c_void_p, C.c_uint, C.c_void_p]
+    lib.orc_inst_retune.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     for pre in ("orc",):
         getattr(lib, f"{pre}_whirl_new").restype = C.c_void_p
         getattr(lib, f"{pre}_whirl_new").argtypes = [C.c_double]
@@ -94,6 +95,7 @@ def load_ref(fast=False):
     lib.ref_inst_free.argtypes = [C.c_void_p]
     lib.ref_inst_new_cfg.restype = C.c_void_p
     lib.ref_inst_new_cfg.argtypes = [C.c_void_p, C.c_uint, C.c_void_p]
+    lib.ref_inst_retune.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     lib.ref_note.argtypes = [C.c_void_p, C.c_int, C.c_int]
     lib.ref_set_param.argtypes = [C.c_void_p, C.c_int, C.c_double]
     lib.ref_set_chain.argtypes = [C.c_void_p, C.c_int]
@@ -264,6 +266,7 @@ class Chain:
         self._chain = getattr(lib, f"{p}_set_chain")
         self._render = getattr(lib, f"{p}_render")
         self._free = getattr(lib, f"{p}_inst_free")
+        self._retune = getattr(lib, f"{p}_inst_retune")
         self.cfg = cfg if cfg is not None else tpl.cfg
         self.ptr = self._new(tpl.ptr, int(seed), None if self.cfg is None else self.cfg.ptr)
         self.tpl = tpl
@@ -276,6 +279,11 @@ class Chain:
 
     def chain(self, mode):
         self._chain(self.ptr, int(mode))
+
+    def retune(self, tpl: Template):
+        """the CLAP reinitToneGen on another template, from the next block"""
+        self._retune(self.ptr, tpl.ptr, None if self.cfg is None else self.cfg.ptr)
+        self.tpl = tpl  # the oracle's tonegen points into it
 
     def render(self, nblocks, stages=False):
         n = nblocks * 128

@@ -148,6 +148,8 @@ def reroute_scenario(i):
 CFG_SETS = {
     "geometry": {"whirl.horn.radius": 25, "whirl.drum.radius": 18, "whirl.mic.distance": 60,
                  "whirl.horn.offset.x": 3, "whirl.horn.offset.z": -2},
+    # a wider horn: the compact whirl ring window doubles to 1024 at 48 kHz (2048 at 96)
+    "geometry_wide": {"whirl.horn.radius": 60, "whirl.drum.radius": 30, "whirl.mic.distance": 50},
     "filters": {"whirl.drum.filter.type": 6, "whirl.drum.filter.hz": 700, "whirl.drum.filter.q": 1.2,
                 "whirl.drum.filter.gain": -20, "whirl.horn.filter.a.hz": 3800, "whirl.horn.filter.a.q": 1.8,
                 "whirl.horn.filter.b.type": 7, "whirl.horn.filter.b.hz": 350, "whirl.horn.filter.b.gain": -25,
@@ -204,8 +206,9 @@ def random_drawbar_scenario(i, seed=None):
     return ev
 
 
-def run(chain, scenario, nblocks, stages=False):
-    """Apply events at block boundaries and render; returns concatenated arrays."""
+def run(chain, scenario, nblocks, stages=False, templates=None):
+    """Apply events at block boundaries and render; returns concatenated arrays.
+    ("retune", j, 0) switches the chain to templates[j] (CLAP reinitToneGen)."""
     import numpy as np
     by_block = {}
     for (blk, kind, a, b) in scenario:
@@ -217,7 +220,33 @@ def run(chain, scenario, nblocks, stages=False):
         for (kind, a, v) in by_block.get(s, []):
             if kind == "note":
                 chain.note(a, v)
+            elif kind == "retune":
+                chain.retune(templates[a])
             else:
                 chain.param(a, v)
         outs.append(chain.render(e - s, stages=stages))
     return [np.concatenate(x) for x in zip(*outs)]
+
+
+def retune_scenario(i, at=24, to=0):
+    """MTS-ESP retune mid-phrase (§8(f) row 3): the Jazz-1 registration with drawbars,
+    vibrato and percussion set through CLAP parameters, a chord held across the retune
+    at block `at` to templates[to] (the new tone generator starts with no keys down, its
+    drawbars / vibrato restored from the parameters, the routing word kept), then new
+    notes on the new tuning, a vibrato-type change and a release."""
+    ev = [(0, k, a, b) for (k, a, b) in jazz1_params()
+          if not (i & 1 and (a <= P_DRAWBAR + 8 or a == P_HORN))]
+    if i & 1:
+        # drawbars never set through parameters (the instance's {8,8,6} preset plays until
+        # the retune restores the parameters' defaults {7,8,8,0...}); the drum speed alone
+        # (the horn parameter at its default 1: revOption 2 + 3)
+        ev += [(0, "param", P_DRUM, 2)]
+    else:
+        ev += [(0, "param", P_DRAWBAR + 3, 5 + i % 3)]
+    ev += [(0, "param", P_VIBRATO, 1), (0, "param", P_VIBRATO_TYPE, i % 6), (0, "param", P_PERC, (i >> 1) & 1)]
+    ev += [(2, "note", k, 1) for k in chord_for(i)]
+    ev += [(at, "retune", to, 0)]
+    ev += [(at, "note", k, 1) for k in chord_for(i + 5)]
+    ev += [(at + 9, "param", P_VIBRATO_TYPE, (i + 3) % 6), (at + 12, "param", P_DRAWBAR + 1, 4)]
+    ev += [(at + 20, "note", k, 0) for k in chord_for(i + 5)]
+    return ev

@@ -259,6 +259,64 @@ def test_gpu_render_events_dense_across_chunks(oracle):
     assert max(eL, eR) <= TOL
 
 
+def test_gpu_synth_sound_irregular_periods(oracle, tunings):
+    """tbf_synth_sound (the synthSound FIFO of b_synth/lv2.cpp:1270-1287) with irregular
+    period sizes (1 .. 700 frames; a call that needs several blocks renders them in one
+    launch), events and an MTS-ESP retune between calls: each lands at the next block the
+    FIFO renders, so the stream equals the oracle's block-by-block render with the events
+    at those blocks."""
+    from orc_bind import Template
+    m19 = np.asarray(tunings["19TET"], np.float64)
+    n = 3
+    eng = _engine()
+    tid = eng.template(seed=7)
+    tid19 = eng.template(mts128=m19, seed=8)
+    seeds = [2000 + i for i in range(n)]
+    eng.add_instances([tid] * n, seeds)
+    t12, t19 = Template(oracle, seed=7), Template(oracle, mts128=m19, seed=8)
+    rng = np.random.default_rng(5)
+    periods = [int(x) for x in rng.choice([1, 37, 64, 128, 129, 256, 300, 515, 700], size=40)]
+    consumed, outL, outR = 0, [], []
+    oscen = [[] for _ in range(n)]
+    for c, nf in enumerate(periods):
+        blk = -(-consumed // 128)  # the next block the FIFO renders
+        evs = []
+        if c == 0:
+            evs += [(k, a, v) for (k, a, v) in S.jazz1_params()]
+        if c % 4 == 0:
+            evs += [("note", k, 1) for k in S.chord_for(c)]
+        if c % 4 == 2:
+            evs += [("note", k, 0) for k in S.chord_for(c - 2)]
+        if c % 7 == 3:
+            evs += [("param", S.P_DRAWBAR + 2, c % 9)]
+        if c == 20:
+            evs += [("retune", 1, 0)]
+        for i in range(n):
+            for (k, a, v) in evs:
+                if k == "note":
+                    eng.note(i, a + i, v)
+                    oscen[i].append((blk, k, a + i, v))
+                elif k == "retune":
+                    eng.retune(i, tid19)
+                    oscen[i].append((blk, k, a, v))
+                else:
+                    eng.set_param(i, a, v)
+                    oscen[i].append((blk, k, a, v))
+        L, R = eng.synth_sound(nf)
+        outL.append(L)
+        outR.append(R)
+        consumed += nf
+    L, R = np.concatenate(outL, axis=1), np.concatenate(outR, axis=1)
+    nb = -(-consumed // 128)
+    oL, oR, *_ = oracle_run(oracle, t12, seeds, oscen, nb, templates=[t12, t19])
+    eL, xL = compare(L, oL[:, :consumed])
+    eR, xR = compare(R, oR[:, :consumed])
+    print(f"synth_sound {len(periods)} periods / {consumed} frames: max|err| L={eL:.3g} R={eR:.3g} "
+          f"bit-exact L={xL:.6f} R={xR:.6f}")
+    assert max(eL, eR) <= TOL
+    eng.close()
+
+
 def test_gpu_cli_host_synth_sound(oracle, tmp_path):
     """§8(f) row 3: the headless host shell (tunebfree_amd/tbf_cli, the counterpart of
     src/main.cpp:243-292 and b_synth/lv2.cpp:212-239) pulls 256-frame periods through
@@ -482,6 +540,31 @@ def test_gpu_parameter_sweep(oracle, debug_flags):
         assert flags & want == want, hex(flags)
 
 
+def _ring_window(max_ahead):
+    """the compact whirl ring: the smallest of 512 / 1024 / 2048 holding the geometry's
+    write-ahead + 2 + one 64-sample sub-block + 2 (tbf_engine.cpp buildShared)"""
+    w = 512
+    while w < max_ahead + 2 + 64 + 2:
+        w *= 2
+    return w
+
+
+def test_gpu_cfg_widest_ring_96k(oracle):
+    """The largest compact whirl ring (k_whirl<2048>): 96 kHz with an 80 cm horn, 4
+    instances over the cfg script, against the oracle."""
+    cfg = {"whirl.horn.radius": 80, "whirl.mic.distance": 60}
+    eng, tpl, seeds, scens = _setup(oracle, 4, S.cfg_scenario, sr=96000.0, cfg=cfg)
+    lay = eng.layout()
+    assert lay["wring_len"] == _ring_window(lay["max_ahead"]) == 2048, lay
+    L, R = engine_run(eng, scens, 72)
+    oL, oR, *_ = oracle_run(oracle, tpl, seeds, scens, 72)
+    eL, xL = compare(L, oL)
+    eR, xR = compare(R, oR)
+    print(f"96k / 2048-sample ring: max|err| L={eL:.3g} R={eR:.3g} bit-exact L={xL:.6f} R={xR:.6f}")
+    assert max(eL, eR) <= TOL
+    eng.close()
+
+
 @pytest.mark.parametrize("name", sorted(S.CFG_SETS))
 def test_gpu_cfg_keys(oracle, name):
     """§8(f) row 4: each cfg key set (scenarios.CFG_SETS — whirl geometry, the three
@@ -493,6 +576,8 @@ def test_gpu_cfg_keys(oracle, name):
     6 instances over the rotor stop -> fast -> brake -> slow script."""
     n, nb = 6, 72
     eng, tpl, seeds, scens = _setup(oracle, n, S.cfg_scenario, cfg=S.CFG_SETS[name])
+    lay = eng.layout()
+    assert lay["wring_len"] == _ring_window(lay["max_ahead"]) == (1024 if name == "geometry_wide" else 512), lay
     L, R = engine_run(eng, scens, nb)
     oL, oR, oA, oB, oC = oracle_run(oracle, tpl, seeds, scens, nb)
     eL, xL = compare(L, oL)
@@ -501,6 +586,35 @@ def test_gpu_cfg_keys(oracle, name):
     assert max(eL, eR) <= TOL
     for i in range(n):
         assert float(np.abs(oL[i]).max()) > 1e-3
+    eng.close()
+
+
+def test_gpu_retune_mid_phrase(oracle, tunings):
+    """§8(f) row 3, the MTS-ESP retune (tbf_instance_retune = the CLAP reinitToneGen,
+    src/clap.cpp:129-157): 6 instances switch mid-phrase to a 19-TET template built on
+    the device (tbf_templates_create) and later back to their 12-TET template; held keys
+    drop, drawbars / vibrato come back from the CLAP parameters (their defaults where
+    never set), the routing word stays, preamp / reverb / whirl state goes on.  Against
+    the oracle's orc_inst_retune (itself bit-identical to the reference's own calls,
+    test_oracle_cpu.py::test_oracle_retune_vs_reference), every stage tap."""
+    from orc_bind import Template
+    m19 = np.asarray(tunings["19TET"], np.float64)
+    n, nb = 6, 64
+    eng = _engine()
+    tid12 = eng.template(seed=7)
+    tid19 = eng.templates([8], mts128=m19[None])[0]
+    seeds = [1000 + 17 * i for i in range(n)]
+    eng.add_instances([tid12] * n, seeds)
+    t12, t19 = Template(oracle, seed=7), Template(oracle, mts128=m19, seed=8)
+    scens = [S.retune_scenario(i, at=20, to=1) + [(44, "retune", 0, 0), (44, "note", 62 + i, 1)] for i in range(n)]
+    L, R = engine_run(eng, scens, nb, tids=[tid12, tid19])
+    oL, oR, *_ = oracle_run(oracle, t12, seeds, scens, nb, templates=[t12, t19])
+    eL, xL = compare(L, oL)
+    eR, xR = compare(R, oR)
+    print(f"retune: max|err| L={eL:.3g} R={eR:.3g} bit-exact L={xL:.6f} R={xR:.6f}")
+    assert max(eL, eR) <= TOL
+    for i in range(n):
+        assert float(np.abs(oL[i, 21 * 128:44 * 128]).max()) > 1e-3  # the retuned organ sounds
     eng.close()
 
 

@@ -124,8 +124,8 @@ def _events_by_block(scen):
 
 
 @pytest.mark.parametrize("lazy", [False, True])
-@pytest.mark.parametrize("scen", ["events", "sweep", "reroute"])
-def test_control_plane_programs_match_oracle(oracle, lazy, scen):
+@pytest.mark.parametrize("scen", ["events", "sweep", "reroute", "retune"])
+def test_control_plane_programs_match_oracle(oracle, lazy, scen, tunings):
     """Block-by-block core programs of the host control plane vs the oracle's
     oscGenerateFragment (active list order, wheel, envelope row, all six gains).
     lazy=False steps the tonegen control every block (tbf_debug_step); lazy=True makes
@@ -138,11 +138,15 @@ def test_control_plane_programs_match_oracle(oracle, lazy, scen):
     tpl = Template(oracle, seed=7)
     eng = T.Engine(device=-1)
     tid = eng.template(seed=7)
+    # retune: the instances switch to a 19-TET template and back (tbf_instance_retune)
+    m19 = np.array(tunings["19TET"], np.float64)
+    tpls, tids = [tpl, Template(oracle, mts128=m19, seed=8)], [tid, eng.template(mts128=m19, seed=8)]
     n_inst, nblocks = 3, 64
     seeds = [1000 + i for i in range(n_inst)]
     eng.add_instances([tid] * n_inst, seeds)
     chains = [Chain(oracle, tpl, s) for s in seeds]
-    fn = {"events": S.event_scenario, "sweep": S.sweep_scenario, "reroute": S.reroute_scenario}[scen]
+    fn = {"events": S.event_scenario, "sweep": S.sweep_scenario, "reroute": S.reroute_scenario,
+          "retune": lambda i: S.retune_scenario(i, at=20, to=1) + [(44, "retune", 0, 0), (44, "note", 62, 1)]}[scen]
     scens = [_events_by_block(fn(i)) for i in range(n_inst)]
     checked = 0
     for blk in range(nblocks):
@@ -151,6 +155,9 @@ def test_control_plane_programs_match_oracle(oracle, lazy, scen):
                 if kind == "note":
                     eng.note(i, a, v)
                     chains[i].note(a, v)
+                elif kind == "retune":
+                    eng.retune(i, tids[a])
+                    chains[i].retune(tpls[a])
                 else:
                     eng.set_param(i, a, v)
                     chains[i].param(a, v)
@@ -401,7 +408,19 @@ def test_config_api_semantics():
         with pytest.raises(T.TbfError, match="-22"):
             eng.config_set(k, v)
     assert eng.config_set("osc.transformer-crosstalk", 0) == 0
-    # geometry beyond the reference's 2048-sample ring is refused and leaves the engine as it was
+    # the compact whirl ring window follows the geometry (512 / 1024 / 2048) ...
+    e2 = T.Engine(device=-1)
+    assert e2.layout()["wring_len"] == 512
+    e2.config_set("whirl.horn.radius", 60)
+    assert e2.layout()["wring_len"] == 1024
+    e2.close()
+    e2 = T.Engine(sample_rate=96000.0, device=-1)
+    assert e2.layout()["wring_len"] == 1024
+    e2.config_set("whirl.horn.radius", 80)
+    assert e2.layout()["wring_len"] == 2048
+    e2.close()
+    # ... and geometry beyond the reference's 2048-sample ring is refused, leaving the
+    # engine as it was
     with pytest.raises(T.TbfError, match="-22"):
         eng.config_set("whirl.horn.radius", 1000)
     assert eng.config_set("whirl.horn.radius", 25) == 0

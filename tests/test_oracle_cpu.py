@@ -293,3 +293,22 @@ def test_oracle_cfg_parsing(oracle):
     assert c.set("scanner.hz", "3.9") == -1 and c.set("scanner.hz", "4") == 1
     assert c.set("WHIRL.HORN.RADIUS", "20") == 1  # strcasecmp
     assert c.set("midi.upper.channel", "1") == 0
+
+
+# --------------------------------------------------------------------------- retune
+def test_oracle_retune_vs_reference(oracle, refchk, tunings):
+    """§8(f) row 3, the MTS-ESP retune: the CLAP plugin's reinitToneGen
+    (src/clap.cpp:129-157) on a new template mid-phrase -- the oracle (orc_inst_retune)
+    against the reference's own calls (ref_inst_retune: allocTonegen tables,
+    init_vibrato, setDrawBar / setVibratoUpper / setVibratoFromInt from the parameters,
+    newRouting kept), bit for bit at every stage tap; 4 variants (parameters set / at
+    their CLAP defaults, percussion on / off) and retunes to 19-TET and back to 12-TET."""
+    t12 = Template(oracle, sr=48000.0, seed=7)
+    t19 = Template(oracle, sr=48000.0, mts128=np.array(tunings["19TET"], np.float64), seed=8)
+    for i in range(4):
+        sc = S.retune_scenario(i, at=20, to=1) + [(40, "retune", 0, 0), (41, "note", 60 + i, 1)]
+        a = S.run(Chain(oracle, t12, 600 + i), sc, 56, stages=True, templates=[t12, t19])
+        b = S.run(Chain(refchk, t12, 600 + i, ref=True), sc, 56, stages=True, templates=[t12, t19])
+        for k, x, y in zip("LRABC", a, b):
+            assert np.array_equal(x.view(np.uint32), y.view(np.uint32)), (i, k)
+        assert float(np.abs(a[0][21 * 128:]).max()) > 1e-3

@@ -9,6 +9,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <stddef.h>
+
 #include <algorithm>
 #include <memory>
 #include <string>
@@ -434,6 +436,24 @@ int tbf_template_bank (tbf_engine* e, uint32_t tid, float* out, uint64_t cap, ui
 	return (int)t.bank.size ();
 }
 
+/* the CLAP parameters' default values (clap_plugin_params get_info, src/clap.cpp:383-545;
+ * the plugin's init copies them into its parameter array, 1062-1067) */
+static void clapParamDefaults (double* params)
+{
+	static const float drawbar[9] = {7.0f, 8.0f, 8.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+	static const float top[9] = {1, 3, 1, 2, 3, 4, 5, 6, 8}, bottom[9] = {2, 2, 1, 1, 1, 1, 1, 1, 1};
+	for (int i = 0; i < 64; i++)
+		params[i] = 0.0;
+	for (int i = 0; i < 9; i++) {
+		params[TBF_P_DRAWBAR_MIN + i] = drawbar[i];
+		params[20 + i]                = top[i];    /* P_RATIO_TOP_MIN */
+		params[29 + i]                = bottom[i]; /* P_RATIO_BOTTOM_MIN */
+	}
+	params[TBF_P_DRUM]   = 1.0f;
+	params[TBF_P_HORN]   = 1.0f;
+	params[TBF_P_REVERB] = 0.1f;
+}
+
 int tbf_instances_add (tbf_engine* e, uint32_t n, const uint32_t* tpl_ids, const uint32_t* seeds, uint32_t* first)
 {
 	if (!e || (n && (!tpl_ids || !seeds)))
@@ -451,7 +471,7 @@ int tbf_instances_add (tbf_engine* e, uint32_t n, const uint32_t* tpl_ids, const
 		memset (&in.k, 0, sizeof (in.k));
 		memset (&in.s0, 0, sizeof (in.s0));
 		memset (&in.ctl, 0, sizeof (in.ctl));
-		memset (in.params, 0, sizeof (in.params));
+		clapParamDefaults (in.params);
 		in.k.tpl = in.tpl;
 		/* allocSynth order: allocReverb (rand x16 vib phases, fpdL, fpdR), allocWhirl,
 		 * allocTonegen, allocPreamp (rand fpd)  -- b_synth/lv2.cpp:336-353 */
@@ -508,6 +528,41 @@ int tbf_instances_add (tbf_engine* e, uint32_t n, const uint32_t* tpl_ids, const
 }
 
 uint32_t tbf_instance_count (const tbf_engine* e) { return e ? (uint32_t)e->inst.size () : 0; }
+
+int tbf_instance_retune (tbf_engine* e, uint32_t i, uint32_t tpl_id)
+{
+	if (!e || i >= e->inst.size ())
+		return fail (-22, "bad instance");
+	if (tpl_id >= e->tpls.size ())
+		return fail (-22, "bad template id");
+	Instance&          in         = e->inst[i];
+	const unsigned int newRouting = in.tg.newRouting;
+	/* reinitToneGen (src/clap.cpp:129-157): allocTonegen + initToneGenerator + init_vibrato
+	 * on the new tables ... */
+	in.tpl   = tpl_id;
+	in.k.tpl = tpl_id;
+	in.tg.init (e->tpls[tpl_id].get (), e->conf);
+	/* ... setToneGenParam (108-121) for the drawbars, vibrato switch and type from the
+	 * parameter values (float) ... */
+	for (int b = 0; b < 9; b++)
+		in.tg.setDrawBar (b, (unsigned)rintf ((float)in.params[TBF_P_DRAWBAR_MIN + b]));
+	in.tg.setVibratoUpper ((int)rintf ((float)in.params[TBF_P_VIBRATO]));
+	in.tg.setVibratoFromInt ((int)floorf ((float)in.params[TBF_P_VIBRATO_TYPE]));
+	/* ... and the routing word kept */
+	in.tg.newRouting = newRouting;
+	/* the device side: the instance's tone-generator + scanner state (wheel positions, key
+	 * compression, percussion envelope and high-pass, stator, scanner ring) starts fresh
+	 * at the next block; the preamp fields of tbf_tg_state, reverb and whirl go on */
+	tbf_tg_state& g = in.s0.tg;
+	memset (&g, 0, offsetof (tbf_tg_state, iirA));
+	g.keyCompLevel = 1.0f;
+	g.outPos       = 1023 / 2;
+	if (std::find (e->retuned.begin (), e->retuned.end (), i) == e->retuned.end ())
+		e->retuned.push_back (i);
+	in.progDirty = in.ctlDirty = true;
+	markActive (e, i);
+	return 0;
+}
 
 int tbf_note (tbf_engine* e, uint32_t i, int32_t key, int32_t on)
 {
@@ -847,6 +902,19 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 	const uint32_t n = (uint32_t)e->inst.size ();
 	if (n == 0 || nblocks == 0)
 		return 0;
+	if (!e->retuned.empty ()) {
+		/* retuned instances (tbf_instance_retune): fresh tone-generator state and the new
+		 * template id, after every launch so far, before this call's first block */
+		if ((rc = joinStages (e, s)))
+			return rc;
+		for (uint32_t i : e->retuned) {
+			HIPCHK (hipMemcpyAsync (&e->st.p[i].tg, &e->inst[i].s0.tg, offsetof (tbf_tg_state, iirA),
+			                        hipMemcpyHostToDevice, s));
+			HIPCHK (hipMemcpyAsync (&e->cst.p[i].tpl, &e->inst[i].k.tpl, sizeof (uint32_t), hipMemcpyHostToDevice, s));
+		}
+		HIPCHK (hipStreamSynchronize (s));
+		e->retuned.clear ();
+	}
 	if (stride < (uint64_t)nblocks * TBF_BLK)
 		return fail (-22, "stride smaller than nblocks*128");
 	if (e->actAll || e->inAct.size () != n) { /* new instances: step every one */
@@ -1132,20 +1200,38 @@ int tbf_synth_sound (tbf_engine* e, uint32_t nframes, float* outL, float* outR, 
 	if (stride < nframes)
 		return fail (-22, "stride smaller than nframes");
 	const uint32_t n = (uint32_t)e->inst.size ();
-	e->fifoL.resize ((size_t)n * TBF_BLK);
-	e->fifoR.resize ((size_t)n * TBF_BLK);
+	if (n != e->fifoN) {
+		/* instances added since the FIFO was filled: they join at the next block (zeros
+		 * for the rest of the current one); the others keep their buffered samples */
+		std::vector<float> L ((size_t)n * e->fifoLen, 0.f), R ((size_t)n * e->fifoLen, 0.f);
+		for (uint32_t i = 0; i < std::min (n, e->fifoN); i++) {
+			std::copy_n (e->fifoL.begin () + (size_t)i * e->fifoLen, e->fifoLen, L.begin () + (size_t)i * e->fifoLen);
+			std::copy_n (e->fifoR.begin () + (size_t)i * e->fifoLen, e->fifoLen, R.begin () + (size_t)i * e->fifoLen);
+		}
+		e->fifoL.swap (L);
+		e->fifoR.swap (R);
+		e->fifoN = n;
+	}
 	uint32_t written = 0;
 	while (written < nframes) {
-		if (e->boffset >= TBF_BLK) {
+		if (e->boffset >= e->fifoLen) {
+			/* the 128-sample FIFO of synthSound (b_synth/lv2.cpp:1270-1287, src/clap.cpp
+			 * PluginRenderAudio) ran dry: render every block this call still needs in one
+			 * launch (no event can land between them, so the samples are those of
+			 * block-by-block rendering) */
+			const uint32_t m = std::min<uint32_t> ((nframes - written + TBF_BLK - 1) / TBF_BLK, 64);
+			e->fifoLen       = m * TBF_BLK;
+			e->fifoL.resize ((size_t)n * e->fifoLen);
+			e->fifoR.resize ((size_t)n * e->fifoLen);
 			e->boffset = 0;
-			int rc     = tbf_render (e, 1, e->fifoL.data (), e->fifoR.data (), TBF_BLK);
+			int rc     = tbf_render (e, m, e->fifoL.data (), e->fifoR.data (), e->fifoLen);
 			if (rc)
 				return rc;
 		}
-		const uint32_t nread = std::min (nframes - written, (uint32_t)TBF_BLK - e->boffset);
+		const uint32_t nread = std::min (nframes - written, e->fifoLen - e->boffset);
 		for (uint32_t i = 0; i < n; i++) {
-			memcpy (outL + (size_t)i * stride + written, e->fifoL.data () + (size_t)i * TBF_BLK + e->boffset, nread * 4);
-			memcpy (outR + (size_t)i * stride + written, e->fifoR.data () + (size_t)i * TBF_BLK + e->boffset, nread * 4);
+			memcpy (outL + (size_t)i * stride + written, e->fifoL.data () + (size_t)i * e->fifoLen + e->boffset, nread * 4);
+			memcpy (outR + (size_t)i * stride + written, e->fifoR.data () + (size_t)i * e->fifoLen + e->boffset, nread * 4);
 		}
 		written += nread;
 		e->boffset += nread;
@@ -1202,6 +1288,16 @@ int tbf_debug_tables (tbf_engine* e, uint32_t tid, float* attack, float* release
 	if (attack) memcpy (attack, t.attackEnv, sizeof (t.attackEnv));
 	if (release) memcpy (release, t.releaseEnv, sizeof (t.releaseEnv));
 	if (keycomp) memcpy (keycomp, t.keyCompTable, sizeof (t.keyCompTable));
+	return 0;
+}
+
+int tbf_debug_layout (const tbf_engine* e, uint32_t* wring_len, float* max_ahead, uint32_t* slab_len)
+{
+	if (!e)
+		return fail (-22, "null argument");
+	if (wring_len) *wring_len = e->wringLen;
+	if (max_ahead) *max_ahead = e->wt.maxAhead;
+	if (slab_len) *slab_len = e->slabLen;
 	return 0;
 }
 

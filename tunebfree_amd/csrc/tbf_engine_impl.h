@@ -103,6 +103,7 @@ struct tbf_engine {
 	uint32_t                                wringLen  = 512;
 	std::vector<std::unique_ptr<TgTemplate>> tpls;
 	std::vector<Instance>                   inst;
+	std::vector<uint32_t>                   retuned; /* tbf_instance_retune: device state to reset */
 	/* reverb ring layout (identical for all instances: A..F are fixed) */
 	uint32_t                                slabLen = 0;
 	/* device side */
@@ -162,7 +163,9 @@ struct tbf_engine {
 	int                                     pgmOffset = 1;
 	/* synth_sound FIFO */
 	std::vector<float>                      fifoL, fifoR;
-	uint32_t                                boffset = TBF_BLK;
+	uint32_t                                boffset = TBF_BLK; /* read position in the FIFO ... */
+	uint32_t                                fifoLen = TBF_BLK; /* ... of fifoLen samples per instance ... */
+	uint32_t                                fifoN   = 0;       /* ... for fifoN instances */
 };
 
 namespace tbf {

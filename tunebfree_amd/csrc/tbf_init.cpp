@@ -683,7 +683,8 @@ void WhirlTables::build (double rate, const Config& c)
 /* ------------------------------------------------------------------ tonegen control */
 void TgControl::init (const TgTemplate* t, const Config& c)
 {
-	tpl = t;
+	*this = TgControl (); /* allocTonegen: initValues (src/tonegen.cpp:238-331) */
+	tpl   = t;
 	/* oscConfig's runtime keys (src/tonegen.cpp:2206-2237), set before initToneGenerator's
 	 * setters below read them */
 	percSendBusA         = (unsigned)c.percSendBusA;

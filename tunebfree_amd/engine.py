@@ -43,6 +43,7 @@ SIGNATURES = {
     "tbf_templates_create": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, _u32p, _u32p]),
     "tbf_instances_add": (C.c_int, [C.c_void_p, C.c_uint32, _u32p, _u32p, _u32p]),
     "tbf_instance_count": (C.c_uint32, [C.c_void_p]),
+    "tbf_instance_retune": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32]),
     "tbf_note": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int32, C.c_int32]),
     "tbf_set_param": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int32, C.c_double]),
     "tbf_render": (C.c_int, [C.c_void_p, C.c_uint32, _fp, _fp, C.c_uint64]),
@@ -124,6 +125,16 @@ class Engine:
         """A cfg file's text; returns the number of keys applied."""
         return _check(self._lib.tbf_config_parse(self._h, text.encode()))
 
+    def layout(self):
+        """The cfg-derived layout (tbf_debug_layout): compact whirl ring window, the
+        geometry's largest write-ahead, reverb slab length."""
+        f = self._lib.tbf_debug_layout
+        f.restype = C.c_int
+        f.argtypes = [C.c_void_p, _u32p, _fp, _u32p]
+        w, a, s = C.c_uint32(), C.c_float(), C.c_uint32()
+        _check(f(self._h, C.byref(w), C.byref(a), C.byref(s)))
+        return {"wring_len": w.value, "max_ahead": a.value, "slab_len": s.value}
+
     def template(self, mts128=None, ratio9=None, seed=1):
         m = None if mts128 is None else np.ascontiguousarray(mts128, dtype=np.float64)
         r = None if ratio9 is None else np.ascontiguousarray(ratio9, dtype=np.float64)
@@ -151,6 +162,10 @@ class Engine:
         out = np.zeros(n, np.float32)
         _check(self._lib.tbf_template_bank(self._h, int(tpl), out.ctypes.data_as(_fp), n, None))
         return out, lens
+
+    def retune(self, inst, tpl_id):
+        """tbf_instance_retune: the CLAP reinitToneGen on another template, from the next block"""
+        _check(self._lib.tbf_instance_retune(self._h, int(inst), int(tpl_id)))
 
     def add_instances(self, tpl_ids, seeds):
         t = np.ascontiguousarray(tpl_ids, dtype=np.uint32)

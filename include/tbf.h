@@ -235,6 +235,14 @@ int tbf_template_bank (tbf_engine* e, uint32_t tpl_id, float* out, uint64_t cap,
 /* play-matrix entries of one key (keyContrib, src/tonegen.cpp:1122-1213) */
 int tbf_debug_contrib (tbf_engine* e, uint32_t tpl_id, int32_t key, int16_t* wheel, int16_t* bus, float* level,
                        uint32_t cap);
+/* the program the instance's next block plays unless its control changes (the persistent
+ * pool entry, read back from the device after synchronizing): 9 floats per instruction
+ * as tbf_debug_render_program; works with either control path */
+int tbf_debug_device_program (tbf_engine* e, uint32_t inst, float* entries9, uint32_t cap);
+/* host control time: wall-clock the render calls spent stepping the control plane
+ * (events, message queues, active lists, routing, per-block programmes) since the last
+ * reset, and the blocks it covered */
+int tbf_debug_host_time (tbf_engine* e, int32_t reset, double* ms, uint64_t* blocks);
 /* the cfg-derived HBM layout: the compact whirl ring window (512 / 1024 / 2048 samples
  * per ring, from the geometry's largest write-ahead) and the reverb slab length */
 int tbf_debug_layout (const tbf_engine* e, uint32_t* wring_len, float* max_ahead, uint32_t* slab_len);

@@ -618,6 +618,66 @@ def test_gpu_retune_mid_phrase(oracle, tunings):
     eng.close()
 
 
+@pytest.mark.parametrize("scen", ["events", "sweep", "reroute", "retune"])
+def test_gpu_device_control_programs(oracle, tunings, scen):
+    """§8(f) row 1: the per-wheel control on the device (k_tgctl: message queue ->
+    activated-oscillator table -> active list -> routed sums -> core program) emits, block
+    by block, the oracle's oscGenerateFragment programs (wheel order, envelope rows, all
+    six gains bit for bit), read back from the device's program pool after each
+    one-block render."""
+    import ctypes as C
+    import tunebfree_amd as T
+    from orc_bind import Chain, Template
+    from test_host_cpu import _events_by_block, _oracle_program, _orc_bind_debug
+    _orc_bind_debug(oracle)
+    lib = T.load_library()
+    fn = lib.tbf_debug_device_program
+    fn.restype, fn.argtypes = C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]
+    m19 = np.asarray(tunings["19TET"], np.float64)
+    eng = _engine()
+    tpls = [Template(oracle, seed=7), Template(oracle, mts128=m19, seed=8)]
+    tids = [eng.template(seed=7), eng.template(mts128=m19, seed=8)]
+    n_inst, nblocks = 3, 56
+    seeds = [1000 + i for i in range(n_inst)]
+    eng.add_instances([tids[0]] * n_inst, seeds)
+    chains = [Chain(oracle, tpls[0], sd) for sd in seeds]
+    gen = {"events": S.event_scenario, "sweep": S.sweep_scenario, "reroute": S.reroute_scenario,
+           "retune": lambda i: S.retune_scenario(i, at=20, to=1) + [(44, "retune", 0, 0), (44, "note", 62, 1)]}[scen]
+    scens = [_events_by_block(gen(i)) for i in range(n_inst)]
+    buf = np.zeros(9 * 600, np.float32)
+    checked = 0
+    for blk in range(nblocks):
+        for i in range(n_inst):
+            for (kind, a, v) in scens[i].get(blk, []):
+                if kind == "note":
+                    eng.note(i, a, v)
+                    chains[i].note(a, v)
+                elif kind == "retune":
+                    eng.retune(i, tids[a])
+                    chains[i].retune(tpls[a])
+                else:
+                    eng.set_param(i, a, v)
+                    chains[i].param(a, v)
+            chains[i].render(1)
+        eng.render(1)
+        for i in range(n_inst):
+            op = _oracle_program(oracle, chains[i].ptr)
+            n = fn(eng._h, i, buf.ctypes.data, 600)
+            assert n == len(op), (blk, i, n, len(op))
+            pp = buf[: 9 * n].reshape(n, 9)
+            for (w, env, r, g), q in zip(op, pp):
+                assert (w, env) == (int(q[0]), int(q[1])), (blk, i)
+                if env:
+                    assert r == int(q[2]), (blk, i)
+                    assert np.array_equal(g.view(np.uint32), q[3:9].view(np.uint32)), (blk, i, w)
+                else:
+                    assert np.array_equal(g[:3].view(np.uint32), q[3:6].view(np.uint32)), (blk, i, w)
+                checked += 1
+    print(f"device control programs ({scen}): {checked} instructions bit-exact")
+    assert checked > 500
+    eng.close()
+
+
 def test_gpu_reroute_without_key_events(oracle):
     """Drawbar / vibrato-routing / percussion changes while keys are held, with no key
     event in the block (scenarios.reroute_scenario): the new sums must take effect from

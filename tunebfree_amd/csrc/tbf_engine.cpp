@@ -12,6 +12,7 @@
 #include <stddef.h>
 
 #include <algorithm>
+#include <chrono>
 #include <memory>
 #include <string>
 #include <vector>
@@ -26,6 +27,7 @@
 
 extern "C" int tbf_launch_stage (const tbf_launch* P, int k, hipStream_t stream);
 extern "C" int tbf_chain_stages (uint32_t chain);
+extern "C" int tbf_launch_tgctl (const tbf_launch* P, hipStream_t stream);
 extern "C" int tbf_launch_calibrate (int op, void* buf, uint64_t n, hipStream_t s);
 
 using namespace tbf;
@@ -46,14 +48,19 @@ int tbf::fail (int code, const std::string& msg)
 	} while (0)
 
 
-#define PROG_CAP (TBF_NW + 1)
+/* program slots (tbf_types.h TBF_PROG_SLOT: header + entries).  The device program pool
+ * holds two persistent slots per instance (2 i, 2 i + 1; the host-controlled path uses
+ * the first), then the chunk's delta programs */
+#define SLOT ((size_t)TBF_PROG_SLOT)
+#define PERSIST(n) ((size_t)(n) * 2 * SLOT)
 /* blocks per kernel launch chunk: bounds the inter-stage buffers to
  * n_inst x TBF_CHUNK x 128 floats each (134 MB at 4096 instances) */
 #ifndef TBF_CHUNK
 #define TBF_CHUNK 64
 #endif
-/* delta program entries one chunk may add (a chunk ends early when they would not fit) */
-#define DPROG_CAP(n) ((size_t)(n) * PROG_CAP * 2 + 4096)
+/* host-controlled path: delta program entries one chunk may add (a chunk ends early when
+ * they would not fit); the device-controlled path sizes its delta slots on demand */
+#define DPROG_CAP(n) ((size_t)(n) * SLOT * 2 + 4096)
 #define TBF_NSTAGES 5 /* k_tonegen, k_rv_in, k_rv_core, k_rv_out, k_whirl */
 
 /* ------------------------------------------------------------------ construction */
@@ -253,6 +260,10 @@ int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
 		HIPCHK (hipEventCreateWithFlags (&e->sjoin, hipEventDisableTiming));
 		const char* pl = getenv ("TBF_PIPELINE");
 		e->pipeline    = !(pl && pl[0] == '0');
+		/* TBF_HOST_CONTROL=1: the per-wheel tone-generator control on the host (the
+		 * reference path for A/B); default: on the device (k_tgctl) */
+		const char* hc = getenv ("TBF_HOST_CONTROL");
+		e->devCtl      = !(hc && hc[0] == '1');
 		/* TBF_PIPE_WAIT="w0,w1,...": stage k of a chunk also waits for stage w_k >= k of the
 		 * previous chunk (default w_k = k), which moves which stages of neighbouring chunks
 		 * co-run; any such table is exact (it only adds dependencies) */
@@ -295,6 +306,12 @@ int tbf_engine_destroy (tbf_engine* e)
 	e->rslab.release ();
 	e->ctl.release ();
 	e->prog.release ();
+	e->tgc.release ();
+	e->drec.release ();
+	e->dmsg.release ();
+	e->dctlInst.release ();
+	e->coff.release ();
+	e->contrib.release ();
 	e->vib.release ();
 	e->xsj.release ();
 	e->whTab.release ();
@@ -714,6 +731,25 @@ static int joinStages (tbf_engine* e, hipStream_t s)
 	return 0;
 }
 
+/* the device program pool with room for `entries`; the persistent slots of the first
+ * `keep` instances are carried over */
+static int growProg (tbf_engine* e, size_t entries, uint32_t keep)
+{
+	if (entries <= e->prog.cap)
+		return 0;
+	if (e->prog.p) /* rare: let every launch that may read the old pool finish */
+		HIPCHK (hipDeviceSynchronize ());
+	e->stagesBusy = false;
+	DevBuf<tbf_prog_entry> np;
+	if (np.ensure (entries + entries / 4))
+		return fail (-12, "out of device memory (programs)");
+	if (keep && e->prog.p)
+		HIPCHK (hipMemcpy (np.p, e->prog.p, PERSIST (keep) * sizeof (tbf_prog_entry), hipMemcpyDeviceToDevice));
+	e->prog.release ();
+	e->prog = np;
+	return 0;
+}
+
 static int ensureDevice (tbf_engine* e)
 {
 	if (e->deviceReady)
@@ -759,6 +795,22 @@ static int ensureDevice (tbf_engine* e)
 	}
 	HIPCHK (hipMemcpy (e->bank.p, ext.data (), total * sizeof (float), hipMemcpyHostToDevice));
 	HIPCHK (hipMemcpy (e->tplDesc.p, desc.data (), desc.size () * sizeof (tbf_tpl_desc), hipMemcpyHostToDevice));
+	if (e->devCtl) { /* the templates' play matrices (keyContrib) for k_tgctl */
+		std::vector<uint32_t>    off (e->tpls.size () * 385);
+		std::vector<tbf_contrib> ent;
+		for (size_t q = 0; q < e->tpls.size (); q++)
+			for (int k = 0; k <= 384; k++) {
+				off[q * 385 + k] = (uint32_t)ent.size ();
+				if (k < 384)
+					for (const Contrib& c : e->tpls[q]->keyContrib[k])
+						ent.push_back ({(uint16_t)c.wheel, (uint16_t)c.bus, c.level});
+			}
+		if (e->coff.ensure (off.size ()) || e->contrib.ensure (std::max<size_t> (ent.size (), 1)))
+			return fail (-12, "out of device memory (play matrices)");
+		HIPCHK (hipMemcpy (e->coff.p, off.data (), off.size () * 4, hipMemcpyHostToDevice));
+		if (!ent.empty ())
+			HIPCHK (hipMemcpy (e->contrib.p, ent.data (), ent.size () * sizeof (tbf_contrib), hipMemcpyHostToDevice));
+	}
 	/* shared tables */
 	if (e->vib.ensure (e->vibTab.size ()) || e->whTab.ensure (4 * (size_t)TBF_WH_TSTRIDE) || e->whBw.ensure (e->wt.bw.size ()) ||
 	    e->err.ensure (4))
@@ -817,13 +869,32 @@ static int ensureDevice (tbf_engine* e)
 		std::vector<tbf_inst_const> k (n);
 		for (uint32_t i = 0; i < n; i++)
 			k[i] = e->inst[i].k;
-		if (e->cst.ensure (n) || e->ctl.ensure ((size_t)n * (TBF_CHUNK + 2)) ||
-		    e->prog.ensure ((size_t)n * PROG_CAP + DPROG_CAP (n)) || e->ctlIdx.ensure ((size_t)n * TBF_CHUNK))
+		if (e->cst.ensure (n) || e->ctl.ensure ((size_t)n * (TBF_CHUNK + 2)) || e->ctlIdx.ensure ((size_t)n * TBF_CHUNK))
 			return fail (-12, "out of device memory (control)");
+		/* program pool: the existing instances' persistent programs move along (the device
+		 * control path keeps them only there); new instances start with empty ones */
+		if (int rc = growProg (e, PERSIST (n) + (e->devCtl ? PERSIST (n) : DPROG_CAP (n)), old))
+			return rc;
+		HIPCHK (hipMemset (e->prog.p + PERSIST (old), 0, (PERSIST (n) - PERSIST (old)) * sizeof (tbf_prog_entry)));
+		if (e->devCtl) {
+			DevBuf<tbf_tgc_state> ng;
+			if (ng.ensure (n))
+				return fail (-12, "out of device memory (control state)");
+			if (old)
+				HIPCHK (hipMemcpy (ng.p, e->tgc.p, old * sizeof (tbf_tgc_state), hipMemcpyDeviceToDevice));
+			HIPCHK (hipMemset (ng.p + old, 0, (n - old) * sizeof (tbf_tgc_state)));
+			e->tgc.release ();
+			e->tgc = ng;
+		}
 		e->persistStale = true;
 		HIPCHK (hipMemcpy (e->cst.p, k.data (), n * sizeof (tbf_inst_const), hipMemcpyHostToDevice));
 		e->hCtl.resize (n);
-		e->hProg.resize ((size_t)n * PROG_CAP);
+		e->hProg.resize (PERSIST (n));
+		e->pslot.resize (n, 0);
+		for (uint32_t i = old; i < n; i++) {
+			e->hCtl[i].prog_off = (uint32_t)(2 * i * SLOT);
+			e->hProg[2 * i * SLOT].wheel = 0xFFFF; /* empty program header */
+		}
 		e->devInst = n;
 	}
 	e->deviceReady = true;
@@ -853,7 +924,7 @@ static int applyEvent (tbf_engine* e, const tbf_event& ev)
  * part of oscGenerateFragment and the effect setters' per-block constants).  Updates
  * the instance's current control e->hCtl[i] / program e->hProg; returns true when the
  * control the next block renders with changed. */
-static bool stepControl (tbf_engine* e, uint32_t i, bool& progChanged)
+static bool stepControl (tbf_engine* e, uint32_t i, bool& progChanged, tbf_tgc_rec* rec = nullptr)
 {
 	Instance&    in      = e->inst[i];
 	tbf_seg_ctl& c       = e->hCtl[i];
@@ -861,15 +932,29 @@ static bool stepControl (tbf_engine* e, uint32_t i, bool& progChanged)
 	const bool   tgDirty = in.tg.dirty ();
 	if (!tgDirty && !in.progDirty && !in.ctlDirty && in.revOpt < 0)
 		return false;
-	if (tgDirty) {
+	if (tgDirty && rec) {
+		/* device control: the front end here, the per-wheel part in k_tgctl */
+		in.tg.stepFront (e->hMsg, *rec, c);
+		in.progDirty = false;
+		in.ctlDirty  = true;
+		progChanged  = true;
+	} else if (tgDirty) {
 		in.tg.step (in.prog, c);
 		in.progDirty = true;
 		in.ctlDirty  = true;
 	}
+	if (rec)
+		in.progDirty = false; /* device control: programs come from k_tgctl only */
 	if (in.progDirty) {
-		if (in.prog.size () > PROG_CAP)
-			in.prog.resize (PROG_CAP);
-		std::copy (in.prog.begin (), in.prog.end (), e->hProg.begin () + (size_t)i * PROG_CAP);
+		/* host control: the program in the instance's first slot, behind its header */
+		const size_t    np   = std::min (in.prog.size (), SLOT - 1);
+		tbf_prog_entry* slot = e->hProg.data () + 2 * i * SLOT;
+		slot[0]              = tbf_prog_entry {};
+		slot[0].wheel        = 0xFFFF;
+		slot[0].pad          = (uint32_t)np;
+		std::copy (in.prog.begin (), in.prog.begin () + (long)np, slot + 1);
+		c.prog_off   = (uint32_t)(2 * i * SLOT);
+		c.prog_len   = (uint32_t)np;
 		in.progDirty = false;
 		progChanged  = true;
 	}
@@ -882,8 +967,6 @@ static bool stepControl (tbf_engine* e, uint32_t i, bool& progChanged)
 		c.vibTable         = in.tg.vibTable;
 		c.vibMixed         = in.tg.vibMixed;
 	}
-	c.prog_off = i * PROG_CAP;
-	c.prog_len = (uint32_t)in.prog.size ();
 	odCtl (in, e->cfg.sample_rate, c);
 	c.rvWet       = in.rvG;
 	c.whBypass    = (uint32_t)in.whBypass;
@@ -911,6 +994,13 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			HIPCHK (hipMemcpyAsync (&e->st.p[i].tg, &e->inst[i].s0.tg, offsetof (tbf_tg_state, iirA),
 			                        hipMemcpyHostToDevice, s));
 			HIPCHK (hipMemcpyAsync (&e->cst.p[i].tpl, &e->inst[i].k.tpl, sizeof (uint32_t), hipMemcpyHostToDevice, s));
+			if (e->devCtl) { /* a fresh per-wheel control state and an empty program */
+				HIPCHK (hipMemsetAsync (e->tgc.p + i, 0, sizeof (tbf_tgc_state), s));
+				HIPCHK (hipMemsetAsync (e->prog.p + 2 * i * SLOT, 0, 2 * SLOT * sizeof (tbf_prog_entry), s));
+				e->pslot[i]         = 0;
+				e->hCtl[i].prog_off = (uint32_t)(2 * i * SLOT);
+				e->persistStale     = true;
+			}
 		}
 		HIPCHK (hipStreamSynchronize (s));
 		e->retuned.clear ();
@@ -933,7 +1023,6 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 	P.wring     = e->wring.p;
 	P.rslab     = e->rslab.p;
 	P.ctl       = e->ctl.p;
-	P.prog      = e->prog.p;
 	P.vibTab    = e->vib.p;
 	P.xsJump    = e->xsj.p;
 	P.whTab     = e->whTab.p;
@@ -984,22 +1073,28 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			if ((rc = joinStages (e, s)))
 				return rc;
 			HIPCHK (hipMemcpyAsync (e->ctl.p, e->hCtl.data (), n * sizeof (tbf_seg_ctl), hipMemcpyHostToDevice, s));
-			HIPCHK (hipMemcpyAsync (e->prog.p, e->hProg.data (), (size_t)n * PROG_CAP * sizeof (tbf_prog_entry),
-			                        hipMemcpyHostToDevice, s));
+			if (!e->devCtl) /* device control keeps the persistent programs on the device */
+				HIPCHK (hipMemcpyAsync (e->prog.p, e->hProg.data (), PERSIST (n) * sizeof (tbf_prog_entry),
+				                        hipMemcpyHostToDevice, s));
 			HIPCHK (hipStreamSynchronize (s));
 			e->persistStale = false;
 		}
 		e->dCtl.clear ();
 		e->dProg.clear ();
+		e->hRec.clear ();
+		e->hMsg.clear ();
+		e->hCtlInst.clear ();
+		e->stepped.assign (n, 0);
 		e->hIdx.resize ((size_t)want * n);
 		std::vector<uint32_t>& cur = e->curIdx;
 		cur.resize (n);
 		for (uint32_t i = 0; i < n; i++)
 			cur[i] = i;
-		bool     delta = false;
-		uint32_t len   = 0;
+		bool       delta = false;
+		uint32_t   len   = 0;
+		const auto hc0   = std::chrono::steady_clock::now ();
 		for (; len < want; len++) {
-			if (e->dProg.size () + (size_t)n * PROG_CAP > dprogCap && len > 0)
+			if (!e->devCtl && e->dProg.size () + (size_t)n * SLOT > dprogCap && len > 0)
 				break; /* delta program pool full: end the chunk here */
 			for (; evi < nev && ev[evi].block <= b0 + len; evi++) {
 				rc = applyEvent (e, ev[evi]);
@@ -1014,12 +1109,28 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			for (size_t a = 0; a < e->actList.size (); a++) {
 				const uint32_t i = e->actList[a];
 				bool           pc;
-				if (stepControl (e, i, pc)) {
+				tbf_tgc_rec    rec;
+				if (stepControl (e, i, pc, e->devCtl ? &rec : nullptr)) {
 					tbf_seg_ctl c = e->hCtl[i];
-					if (pc) {
-						c.prog_off = (uint32_t)((size_t)n * PROG_CAP + e->dProg.size ());
-						e->dProg.insert (e->dProg.end (), e->hProg.begin () + (size_t)i * PROG_CAP,
-						                 e->hProg.begin () + (size_t)i * PROG_CAP + c.prog_len);
+					if (e->devCtl) {
+						/* a stepped delta gets its own program slot, which k_tgctl fills; the
+						 * others play the program before them */
+						if (pc) {
+							c.prog_off = (uint32_t)(PERSIST (n) + e->dCtl.size () * SLOT);
+							if (!e->stepped[i]) {
+								e->stepped[i] = 1;
+								e->hCtlInst.push_back (i);
+							}
+						} else {
+							memset (&rec, 0, sizeof (rec));
+							if (cur[i] >= n)
+								c.prog_off = e->dCtl[cur[i] - n].prog_off;
+						}
+						e->hRec.push_back (rec);
+					} else if (pc) {
+						c.prog_off = (uint32_t)(PERSIST (n) + e->dProg.size ());
+						e->dProg.insert (e->dProg.end (), e->hProg.begin () + 2 * i * SLOT,
+						                 e->hProg.begin () + 2 * i * SLOT + 1 + c.prog_len);
 					} else if (cur[i] >= n)
 						c.prog_off = e->dCtl[cur[i] - n].prog_off; /* program of the previous delta */
 					cur[i] = n + (uint32_t)e->dCtl.size ();
@@ -1041,6 +1152,10 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 				std::copy (cur.begin (), cur.end (), e->hIdx.begin () + (size_t)len * n);
 			}
 		}
+		e->hostCtlNs += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds> (
+		                    std::chrono::steady_clock::now () - hc0)
+		                    .count ();
+		e->hostCtlBlocks += len;
 		const bool     par     = (e->chunkSeq++ & 1) != 0;
 		const bool     piped   = pipe && !delta;
 		P.mid1 = e->mid1.p ? e->mid1.p + (par ? need : 0) : nullptr;
@@ -1050,17 +1165,43 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		if (!piped && (rc = joinStages (e, s)))
 			return rc;
 		if (delta) {
+			if (e->devCtl && (rc = growProg (e, PERSIST (n) + e->dCtl.size () * SLOT, n)))
+				return rc; /* (after joinStages: no launch still reads the pool) */
 			HIPCHK (hipMemcpyAsync (e->ctl.p + n, e->dCtl.data (), e->dCtl.size () * sizeof (tbf_seg_ctl),
 			                        hipMemcpyHostToDevice, s));
 			if (!e->dProg.empty ())
-				HIPCHK (hipMemcpyAsync (e->prog.p + (size_t)n * PROG_CAP, e->dProg.data (),
+				HIPCHK (hipMemcpyAsync (e->prog.p + PERSIST (n), e->dProg.data (),
 				                        e->dProg.size () * sizeof (tbf_prog_entry), hipMemcpyHostToDevice, s));
 			HIPCHK (hipMemcpyAsync (e->ctlIdx.p, e->hIdx.data (), (size_t)len * n * sizeof (uint32_t),
 			                        hipMemcpyHostToDevice, s));
 		}
+		P.prog      = e->prog.p;
 		P.ctlIdx    = delta ? e->ctlIdx.p : nullptr;
 		P.nBlocks   = len;
 		P.outOffset = (uint64_t)b0 * TBF_BLK;
+		P.nCtlInst  = 0;
+		if (e->devCtl && !e->hCtlInst.empty ()) {
+			/* k_tgctl: the stepped blocks' programs, ahead of k_tonegen on this stream */
+			if (e->drec.ensure (e->hRec.size ()) || e->dmsg.ensure (std::max<size_t> (e->hMsg.size (), 1)) ||
+			    e->dctlInst.ensure (e->hCtlInst.size ()))
+				return fail (-12, "out of device memory (control records)");
+			HIPCHK (hipMemcpyAsync (e->drec.p, e->hRec.data (), e->hRec.size () * sizeof (tbf_tgc_rec),
+			                        hipMemcpyHostToDevice, s));
+			if (!e->hMsg.empty ())
+				HIPCHK (hipMemcpyAsync (e->dmsg.p, e->hMsg.data (), e->hMsg.size () * sizeof (uint16_t),
+				                        hipMemcpyHostToDevice, s));
+			HIPCHK (hipMemcpyAsync (e->dctlInst.p, e->hCtlInst.data (), e->hCtlInst.size () * 4, hipMemcpyHostToDevice,
+			                        s));
+			P.tgc      = e->tgc.p;
+			P.rec      = e->drec.p;
+			P.msgs     = e->dmsg.p;
+			P.ctlInst  = e->dctlInst.p;
+			P.nCtlInst = (uint32_t)e->hCtlInst.size ();
+			P.coff     = e->coff.p;
+			P.contrib  = e->contrib.p;
+			if ((rc = tbf_launch_tgctl (&P, s)))
+				return fail (rc, std::string ("k_tgctl launch failed: ") + hipGetErrorString (hipGetLastError ()));
+		}
 		const int nst = tbf_chain_stages (P.chain);
 		if (piped) {
 			hipStream_t sp = e->sstr[par];
@@ -1124,10 +1265,16 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 					hi                     = std::max (hi, i + 1);
 					e->chg[i]              = 0;
 				}
+			/* device control: k_tgctl left each stepped instance's last program in its other
+			 * persistent slot */
+			for (uint32_t i : e->hCtlInst) {
+				e->pslot[i] ^= 1;
+				e->hCtl[i].prog_off = (uint32_t)((2 * i + e->pslot[i]) * SLOT);
+			}
 			HIPCHK (hipMemcpyAsync (e->ctl.p, e->hCtl.data (), n * sizeof (tbf_seg_ctl), hipMemcpyHostToDevice, s));
-			if (hi > lo)
-				HIPCHK (hipMemcpyAsync (e->prog.p + (size_t)lo * PROG_CAP, e->hProg.data () + (size_t)lo * PROG_CAP,
-				                        (size_t)(hi - lo) * PROG_CAP * sizeof (tbf_prog_entry), hipMemcpyHostToDevice, s));
+			if (hi > lo && !e->devCtl)
+				HIPCHK (hipMemcpyAsync (e->prog.p + lo * 2 * SLOT, e->hProg.data () + lo * 2 * SLOT,
+				                        (size_t)(hi - lo) * 2 * SLOT * sizeof (tbf_prog_entry), hipMemcpyHostToDevice, s));
 			HIPCHK (hipStreamSynchronize (s));
 		}
 		b0 += len;
@@ -1291,6 +1438,38 @@ int tbf_debug_tables (tbf_engine* e, uint32_t tid, float* attack, float* release
 	return 0;
 }
 
+int tbf_debug_device_program (tbf_engine* e, uint32_t i, float* out, uint32_t cap)
+{
+	if (!e || i >= e->inst.size () || e->cfg.device < 0 || i >= e->hCtl.size ())
+		return fail (-22, "bad instance");
+	HIPCHK (hipSetDevice (e->cfg.device));
+	if (int rc = drainStages (e))
+		return rc;
+	HIPCHK (hipStreamSynchronize (e->stream));
+	HIPCHK (hipDeviceSynchronize ());
+	std::vector<tbf_prog_entry> v (SLOT);
+	HIPCHK (hipMemcpy (v.data (), e->prog.p + e->hCtl[i].prog_off, SLOT * sizeof (tbf_prog_entry), hipMemcpyDeviceToHost));
+	const uint32_t np = std::min<uint32_t> (v[0].pad, (uint32_t)SLOT - 1);
+	for (uint32_t q = 0; q < np && q < cap; q++) {
+		const tbf_prog_entry& p = v[1 + q];
+		float*                o = out + 9 * q;
+		o[0] = p.wheel; o[1] = p.env; o[2] = p.row;
+		o[3] = p.sg; o[4] = p.pg; o[5] = p.vg; o[6] = p.nsg; o[7] = p.npg; o[8] = p.nvg;
+	}
+	return (int)np;
+}
+
+int tbf_debug_host_time (tbf_engine* e, int32_t reset, double* ms, uint64_t* blocks)
+{
+	if (!e)
+		return fail (-22, "null argument");
+	if (ms) *ms = (double)e->hostCtlNs * 1e-6;
+	if (blocks) *blocks = e->hostCtlBlocks;
+	if (reset)
+		e->hostCtlNs = e->hostCtlBlocks = 0;
+	return 0;
+}
+
 int tbf_debug_layout (const tbf_engine* e, uint32_t* wring_len, float* max_ahead, uint32_t* slab_len)
 {
 	if (!e)
@@ -1305,6 +1484,8 @@ int tbf_debug_step (tbf_engine* e, uint32_t i, float* out, uint32_t cap)
 {
 	if (!e || i >= e->inst.size ())
 		return fail (-22, "bad instance");
+	if (e->devCtl)
+		return fail (-95, "host programs: the per-wheel control runs on the device (TBF_HOST_CONTROL=1 for the host path)");
 	Instance& in = e->inst[i];
 	tbf_seg_ctl c;
 	memset (&c, 0, sizeof (c));
@@ -1324,10 +1505,12 @@ int tbf_debug_render_program (tbf_engine* e, uint32_t i, float* out, uint32_t ca
 {
 	if (!e || i >= e->inst.size ())
 		return fail (-22, "bad instance");
+	if (e->devCtl)
+		return fail (-95, "host programs: the per-wheel control runs on the device (TBF_HOST_CONTROL=1 for the host path)");
 	const size_t n = e->inst.size ();
 	if (e->hCtl.size () < n) { /* a host-only engine never sized the pool */
 		e->hCtl.resize (n);
-		e->hProg.resize (n * PROG_CAP);
+		e->hProg.resize (PERSIST (n));
 	}
 	bool pc;
 	(void)stepControl (e, i, pc); /* exactly the per-block step renderImpl makes */

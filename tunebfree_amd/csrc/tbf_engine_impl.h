@@ -104,6 +104,7 @@ struct tbf_engine {
 	std::vector<std::unique_ptr<TgTemplate>> tpls;
 	std::vector<Instance>                   inst;
 	std::vector<uint32_t>                   retuned; /* tbf_instance_retune: device state to reset */
+	uint64_t                                hostCtlNs = 0, hostCtlBlocks = 0; /* tbf_debug_host_time */
 	/* reverb ring layout (identical for all instances: A..F are fixed) */
 	uint32_t                                slabLen = 0;
 	/* device side */
@@ -117,6 +118,19 @@ struct tbf_engine {
 	DevBuf<double>                          rslab;
 	DevBuf<tbf_seg_ctl>                     ctl;
 	DevBuf<tbf_prog_entry>                  prog;
+	/* device-side tone-generator control (k_tgctl, tbf_ctl.hip) */
+	bool                                    devCtl = false;
+	DevBuf<tbf_tgc_state>                   tgc;
+	DevBuf<tbf_tgc_rec>                     drec;
+	DevBuf<uint16_t>                        dmsg;
+	DevBuf<uint32_t>                        dctlInst;
+	DevBuf<uint32_t>                        coff;
+	DevBuf<tbf_contrib>                     contrib;
+	std::vector<tbf_tgc_rec>                hRec;     /* per delta of the chunk */
+	std::vector<uint16_t>                   hMsg;     /* the chunk's key messages */
+	std::vector<uint32_t>                   hCtlInst; /* instances with a stepped delta */
+	std::vector<uint8_t>                    stepped;  /* membership of hCtlInst */
+	std::vector<uint8_t>                    pslot;    /* persistent program slot (0/1) per instance */
 	DevBuf<uint32_t>                        vib;
 	DevBuf<uint32_t>                        xsj; /* xorshift32 jump table */
 	DevBuf<float>                           whTab, whBw;

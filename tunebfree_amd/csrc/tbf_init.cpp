@@ -949,7 +949,34 @@ void TgControl::step (std::vector<tbf_prog_entry>& prog, tbf_seg_ctl& ctl)
 	 * with no key event: this block still plays the old sums, the next the new ones) */
 	steadyPending = anyEnv || removedEnd > 0 || anyRoute;
 
-	/* mixdown control (3712-3777) */
+	mixCtl (ctl);
+}
+
+void TgControl::stepFront (std::vector<uint16_t>& msgs, tbf_tgc_rec& rec, tbf_seg_ctl& ctl)
+{
+	memset (&rec, 0, sizeof (rec));
+	rec.msgOff = (uint32_t)msgs.size ();
+	rec.nMsg   = (uint16_t)std::min<size_t> (msg.size (), 0xFFFF);
+	msgs.insert (msgs.end (), msg.begin (), msg.begin () + rec.nMsg);
+	const bool recompute = oldRouting != newRouting;
+	if (recompute)
+		oldRouting = newRouting;
+	rec.flags       = (uint8_t)(0x80 | (drawBarChange ? 1 : 0) | (recompute ? 2 : 0));
+	rec.oldRouting  = (uint8_t)oldRouting;
+	rec.percSendBus = percSendBus;
+	memcpy (rec.drawBarGain, drawBarGain, sizeof (rec.drawBarGain));
+	/* a block with inputs makes the next block's program differ (envelopes end, released
+	 * wheels leave, rerouted sums take over: the device's steadyPending); a block with
+	 * none leaves it unchanged, so stepping once after each input block is exact */
+	steadyPending = rec.nMsg > 0 || (rec.flags & 3) != 0;
+	msg.clear ();
+	drawBarChange = 0;
+	mixCtl (ctl);
+}
+
+/* mixdown control (src/tonegen.cpp:3712-3777) */
+void TgControl::mixCtl (tbf_seg_ctl& ctl) const
+{
 	ctl.routing          = oldRouting;
 	ctl.swellPedalGain   = swellPedalGain;
 	ctl.outputGain       = swellPedalGain * percDrawbarGain;

@@ -381,8 +381,9 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 {
 	const int             lane = threadIdx.x;
 	tbf_tg_state&         st   = sm.st;
-	const tbf_prog_entry* __restrict__ prog = P.prog + G.prog_off;
-	const int             np   = (int)G.prog_len;
+	/* the program slot: header (entry count) then the entries */
+	const tbf_prog_entry* __restrict__ prog = P.prog + G.prog_off + 1;
+	const int             np   = (int)P.prog[G.prog_off].pad;
 
 	/* core interpreter.  Prologue, lane per entry: resolve the wheel's bank position and
 	 * advance st.pos (each wheel appears once per program).  The device bank repeats each

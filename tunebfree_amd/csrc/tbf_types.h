@@ -29,6 +29,46 @@ typedef struct tbf_prog_entry {
 	uint32_t pad;
 } tbf_prog_entry;
 
+/* A program slot is a header entry (wheel = 0xFFFF, pad = entry count) followed by the
+ * entries; seg_ctl.prog_off indexes the header.  TBF_PROG_SLOT entries per slot. */
+#define TBF_PROG_SLOT (TBF_NW + 2)
+
+/* device-side tone-generator control (k_tgctl): the per-wheel part
+ * of oscGenerateFragment's control (src/tonegen.cpp:3257-3594: the message queue's
+ * activated-oscillator-table updates, the active list, routing sums and the core
+ * program) runs on the device; the host keeps the key / drawbar / routing front end and
+ * hands each stepped block this record */
+typedef struct tbf_tgc_rec {
+	uint32_t msgOff;         /* the block's key messages (0x1000 | key: on, key: off) ... */
+	uint16_t nMsg;           /* ... msgs[msgOff .. msgOff + nMsg) */
+	uint8_t  flags;          /* 1 drawBarChange, 2 recomputeRouting, 0x80 stepped */
+	uint8_t  oldRouting;     /* routing word after this block's update */
+	uint32_t percSendBus;
+	float    drawBarGain[27];
+} tbf_tgc_rec;
+
+/* one keyContrib element on the device (Contrib): a key's list is sorted by wheel, then
+ * bus (compilePlayMatrix's insertion sort, src/tonegen.cpp:1183-1201) */
+typedef struct tbf_contrib {
+	uint16_t wheel, bus;
+	float    level;
+} tbf_contrib;
+
+/* per instance device control state (the runtime fields of struct b_tonegen that the
+ * per-wheel control touches); aclPos1 = aclPos + 1 so that zeroed memory is the initial
+ * state (no wheel in the list) */
+typedef struct tbf_tgc_state {
+	float    busLevel[TBF_NW + 1][27];
+	float    sums[TBF_NW + 1][6]; /* sumUpper, sumLower, sumPedal, sumPercn, sumSwell, sumScanr */
+	int32_t  refCount[TBF_NW + 1];
+	uint16_t list[TBF_NW + 1];    /* activeOscList */
+	int16_t  aclPos1[TBF_NW + 1];
+	uint8_t  rflags[TBF_NW + 1];
+	uint8_t  pad0[3];
+	uint32_t listEnd;             /* activeOscLEnd */
+	uint32_t pad1[3];
+} tbf_tgc_state;
+
 /* per instance, per launch segment: control state that is constant over the
  * segment's blocks (events land on segment boundaries) */
 typedef struct tbf_seg_ctl {
@@ -168,6 +208,15 @@ typedef struct tbf_launch {
 	uint32_t              slabLen;
 	uint32_t              dbg;       /* TBF_DEBUG_* bits of tbf_engine_config.debug_flags */
 	uint32_t*             errFlags;  /* TBF_PATH_* bits: which rare paths a launch took */
+	/* device-side control (k_tgctl) */
+	tbf_tgc_state*        tgc;       /* [inst] */
+	const tbf_tgc_rec*    rec;       /* [pool index - nInst]: inputs of the chunk's deltas */
+	const uint16_t*       msgs;
+	const uint32_t*       ctlInst;   /* instances with a stepped delta in this chunk */
+	uint32_t              nCtlInst;
+	uint32_t              pad2;
+	const uint32_t*       coff;      /* [tpl][385] keyContrib offsets into contrib */
+	const tbf_contrib*    contrib;
 	uint64_t*             prof;      /* [inst][TBF_PROF_SLOTS] stage cycle sums, or NULL */
 } tbf_launch;
 

@@ -259,6 +259,14 @@ class Engine:
         _check(fn(self._h, 0, ms.ctypes.data, cnt.ctypes.data))
         return {k: (float(ms[i]), int(cnt[i])) for i, k in enumerate(STAGES)}
 
+    def host_time(self, reset=True):
+        """tbf_debug_host_time: (ms of host control stepping, blocks) since the last reset"""
+        fn = self._lib.tbf_debug_host_time
+        fn.restype, fn.argtypes = C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
+        ms, nb = C.c_double(), C.c_uint64()
+        _check(fn(self._h, 1 if reset else 0, C.byref(ms), C.byref(nb)))
+        return ms.value, nb.value
+
     def error_flags(self):
         f = C.c_uint32()
         _check(self._lib.tbf_error_flags(self._h, C.byref(f)))

@@ -258,6 +258,8 @@ int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
 		for (int k = 0; k < TBF_NSTAGES; k++)
 			HIPCHK (hipEventCreateWithFlags (&e->sdone[k], hipEventDisableTiming));
 		HIPCHK (hipEventCreateWithFlags (&e->sjoin, hipEventDisableTiming));
+		HIPCHK (hipEventCreateWithFlags (&e->upEv, hipEventDisableTiming));
+		HIPCHK (hipEventCreateWithFlags (&e->upEvB, hipEventDisableTiming));
 		const char* pl = getenv ("TBF_PIPELINE");
 		e->pipeline    = !(pl && pl[0] == '0');
 		/* TBF_HOST_CONTROL=1: the per-wheel tone-generator control on the host (the
@@ -333,6 +335,9 @@ int tbf_engine_destroy (tbf_engine* e)
 			(void)hipEventDestroy (e->sdone[k]);
 	if (e->sjoin)
 		(void)hipEventDestroy (e->sjoin);
+	for (hipEvent_t ev : {e->upEv, e->upEvB})
+		if (ev)
+			(void)hipEventDestroy (ev);
 	delete e;
 	return 0;
 }
@@ -934,7 +939,9 @@ static bool stepControl (tbf_engine* e, uint32_t i, bool& progChanged, tbf_tgc_r
 		return false;
 	if (tgDirty && rec) {
 		/* device control: the front end here, the per-wheel part in k_tgctl */
-		in.tg.stepFront (e->hMsg, *rec, c);
+		const uint32_t at = (uint32_t)e->hMsg.size ();
+		e->hMsg.resize (at + std::min<size_t> (in.tg.msg.size (), 0xFFFF));
+		in.tg.stepFront (e->hMsg.data () + at, at, *rec, c);
 		in.progDirty = false;
 		in.ctlDirty  = true;
 		progChanged  = true;
@@ -1079,6 +1086,17 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			HIPCHK (hipStreamSynchronize (s));
 			e->persistStale = false;
 		}
+		if (e->devCtl) {
+			/* staging of the chunk before last (its uploads are done once its event is) */
+			e->dCtl.swap (e->dCtlB);
+			e->hRec.swap (e->hRecB);
+			e->hMsg.swap (e->hMsgB);
+			e->hCtlInst.swap (e->hCtlInstB);
+			e->hIdx.swap (e->hIdxB);
+			e->hCtlPin.swap (e->hCtlPinB);
+			std::swap (e->upEv, e->upEvB);
+			HIPCHK (hipEventSynchronize (e->upEv));
+		}
 		e->dCtl.clear ();
 		e->dProg.clear ();
 		e->hRec.clear ();
@@ -1202,6 +1220,8 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			if ((rc = tbf_launch_tgctl (&P, s)))
 				return fail (rc, std::string ("k_tgctl launch failed: ") + hipGetErrorString (hipGetLastError ()));
 		}
+		if (e->devCtl)
+			HIPCHK (hipEventRecord (e->upEv, s)); /* this parity's staging is free after it */
 		const int nst = tbf_chain_stages (P.chain);
 		if (piped) {
 			hipStream_t sp = e->sstr[par];
@@ -1271,11 +1291,21 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 				e->pslot[i] ^= 1;
 				e->hCtl[i].prog_off = (uint32_t)((2 * i + e->pslot[i]) * SLOT);
 			}
-			HIPCHK (hipMemcpyAsync (e->ctl.p, e->hCtl.data (), n * sizeof (tbf_seg_ctl), hipMemcpyHostToDevice, s));
-			if (hi > lo && !e->devCtl)
-				HIPCHK (hipMemcpyAsync (e->prog.p + lo * 2 * SLOT, e->hProg.data () + lo * 2 * SLOT,
-				                        (size_t)(hi - lo) * 2 * SLOT * sizeof (tbf_prog_entry), hipMemcpyHostToDevice, s));
-			HIPCHK (hipStreamSynchronize (s));
+			if (e->devCtl) {
+				/* from a pinned snapshot, so the next chunk's control can run on the host
+				 * while this one renders */
+				e->hCtlPin.resize (n);
+				memcpy ((void*)e->hCtlPin.data (), e->hCtl.data (), n * sizeof (tbf_seg_ctl));
+				HIPCHK (hipMemcpyAsync (e->ctl.p, e->hCtlPin.data (), n * sizeof (tbf_seg_ctl), hipMemcpyHostToDevice, s));
+				HIPCHK (hipEventRecord (e->upEv, s));
+			} else {
+				HIPCHK (hipMemcpyAsync (e->ctl.p, e->hCtl.data (), n * sizeof (tbf_seg_ctl), hipMemcpyHostToDevice, s));
+				if (hi > lo)
+					HIPCHK (hipMemcpyAsync (e->prog.p + lo * 2 * SLOT, e->hProg.data () + lo * 2 * SLOT,
+					                        (size_t)(hi - lo) * 2 * SLOT * sizeof (tbf_prog_entry), hipMemcpyHostToDevice,
+					                        s));
+				HIPCHK (hipStreamSynchronize (s));
+			}
 		}
 		b0 += len;
 	}

@@ -8,9 +8,13 @@
 
 #include <hip/hip_runtime.h>
 
+#include <stdlib.h>
+#include <string.h>
+
 #include <memory>
 #include <string>
 #include <utility>
+#include <algorithm>
 #include <vector>
 
 #include "../../include/tbf.h"
@@ -61,6 +65,71 @@ struct Instance {
 	bool           ctlDirty = true;
 	bool           progDirty = true;
 	std::vector<tbf_prog_entry> prog;
+};
+
+/* host staging in pinned memory (pageable memory if no device: host-only engines), so
+ * uploads from it are truly asynchronous; the renderer double-buffers these by chunk */
+template <typename T>
+struct PinnedVec {
+	T*     p      = nullptr;
+	size_t n      = 0, cap = 0;
+	bool   pinned = false;
+	PinnedVec ()  = default;
+	PinnedVec (const PinnedVec&) = delete;
+	PinnedVec& operator= (const PinnedVec&) = delete;
+	~PinnedVec () { release (); }
+	void release ()
+	{
+		if (p && pinned)
+			(void)hipHostFree (p);
+		else
+			free (p);
+		p   = nullptr;
+		n   = cap = 0;
+	}
+	void reserve (size_t c)
+	{
+		if (c <= cap)
+			return;
+		const size_t nc = std::max<size_t> (std::max<size_t> (c, 2 * cap), 1024);
+		T*           q  = nullptr;
+		bool         pq = hipHostMalloc ((void**)&q, nc * sizeof (T), 0) == hipSuccess;
+		if (!pq)
+			q = (T*)malloc (nc * sizeof (T));
+		if (n)
+			memcpy ((void*)q, (const void*)p, n * sizeof (T));
+		const size_t keep = n;
+		release ();
+		p      = q;
+		n      = keep;
+		cap    = nc;
+		pinned = pq;
+	}
+	void   push_back (const T& v)
+	{
+		if (n == cap)
+			reserve (n + 1);
+		p[n++] = v;
+	}
+	void   resize (size_t m)
+	{
+		reserve (m);
+		n = m;
+	}
+	void   clear () { n = 0; }
+	size_t size () const { return n; }
+	bool   empty () const { return n == 0; }
+	T*     data () { return p; }
+	T*     begin () { return p; }
+	T*     end () { return p + n; }
+	T&     operator[] (size_t i) { return p[i]; }
+	void   swap (PinnedVec& o)
+	{
+		std::swap (p, o.p);
+		std::swap (n, o.n);
+		std::swap (cap, o.cap);
+		std::swap (pinned, o.pinned);
+	}
 };
 
 template <typename T>
@@ -126,9 +195,16 @@ struct tbf_engine {
 	DevBuf<uint32_t>                        dctlInst;
 	DevBuf<uint32_t>                        coff;
 	DevBuf<tbf_contrib>                     contrib;
-	std::vector<tbf_tgc_rec>                hRec;     /* per delta of the chunk */
-	std::vector<uint16_t>                   hMsg;     /* the chunk's key messages */
-	std::vector<uint32_t>                   hCtlInst; /* instances with a stepped delta */
+	PinnedVec<tbf_tgc_rec>                  hRec;     /* per delta of the chunk */
+	PinnedVec<uint16_t>                     hMsg;     /* the chunk's key messages */
+	PinnedVec<uint32_t>                     hCtlInst; /* instances with a stepped delta */
+	/* the other parity of the chunk staging (the previous chunk's, in flight), and the
+	 * events after each parity's uploads */
+	PinnedVec<tbf_seg_ctl>                  dCtlB, hCtlPin, hCtlPinB;
+	PinnedVec<tbf_tgc_rec>                  hRecB;
+	PinnedVec<uint16_t>                     hMsgB;
+	PinnedVec<uint32_t>                     hCtlInstB, hIdxB;
+	hipEvent_t                              upEv = nullptr, upEvB = nullptr;
 	std::vector<uint8_t>                    stepped;  /* membership of hCtlInst */
 	std::vector<uint8_t>                    pslot;    /* persistent program slot (0/1) per instance */
 	DevBuf<uint32_t>                        vib;
@@ -147,9 +223,9 @@ struct tbf_engine {
 	std::vector<tbf_seg_ctl>                hCtl;  /* current control per instance (pool entries 0..n-1) */
 	std::vector<tbf_prog_entry>             hProg; /* current program per instance (slots i * PROG_CAP) */
 	/* per-chunk control deltas (tbf_render_events / renderImpl) */
-	std::vector<tbf_seg_ctl>                dCtl;
+	PinnedVec<tbf_seg_ctl>                  dCtl;
 	std::vector<tbf_prog_entry>             dProg;
-	std::vector<uint32_t>                   hIdx;
+	PinnedVec<uint32_t>                     hIdx;
 	std::vector<uint8_t>                    chg;
 	/* instances whose control may change at the next block (renderImpl steps only
 	 * these): every entry point that changes an instance marks it (markActive) */

@@ -187,9 +187,10 @@ struct TgControl {
 	/* one block of control: returns the block's program and mixdown control */
 	void step (std::vector<tbf_prog_entry>& prog, tbf_seg_ctl& ctl);
 	/* the same block with the per-wheel part left to the device (k_tgctl): the block's
-	 * key messages (appended to msgs) and drawbar / routing inputs in rec, the mixdown
-	 * control in ctl.  aot / active list / rflags are not used. */
-	void stepFront (std::vector<uint16_t>& msgs, tbf_tgc_rec& rec, tbf_seg_ctl& ctl);
+	 * key messages (msg.size () of them, written to msgDst = the chunk's message array
+	 * at msgOff) and drawbar / routing inputs in rec, the mixdown control in ctl.
+	 * aot / active list / rflags are not used. */
+	void stepFront (uint16_t* msgDst, uint32_t msgOff, tbf_tgc_rec& rec, tbf_seg_ctl& ctl);
 	void mixCtl (tbf_seg_ctl& ctl) const;
 };
 

@@ -952,12 +952,12 @@ void TgControl::step (std::vector<tbf_prog_entry>& prog, tbf_seg_ctl& ctl)
 	mixCtl (ctl);
 }
 
-void TgControl::stepFront (std::vector<uint16_t>& msgs, tbf_tgc_rec& rec, tbf_seg_ctl& ctl)
+void TgControl::stepFront (uint16_t* msgDst, uint32_t msgOff, tbf_tgc_rec& rec, tbf_seg_ctl& ctl)
 {
 	memset (&rec, 0, sizeof (rec));
-	rec.msgOff = (uint32_t)msgs.size ();
+	rec.msgOff = msgOff;
 	rec.nMsg   = (uint16_t)std::min<size_t> (msg.size (), 0xFFFF);
-	msgs.insert (msgs.end (), msg.begin (), msg.begin () + rec.nMsg);
+	std::copy (msg.begin (), msg.begin () + rec.nMsg, msgDst);
 	const bool recompute = oldRouting != newRouting;
 	if (recompute)
 		oldRouting = newRouting;

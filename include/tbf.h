@@ -70,7 +70,7 @@ typedef struct tbf_engine tbf_engine;
                                    * fallbacks; slow) */
 
 typedef struct tbf_engine_config {
-	double   sample_rate; /* Hz, 22050 .. 96000 */
+	double   sample_rate; /* Hz, 8000 .. 192000 */
 	int32_t  device;      /* HIP device ordinal */
 	uint32_t chain_mode;  /* TBF_CHAIN_* */
 	uint32_t debug_flags; /* TBF_DEBUG_*, 0 in production */

@@ -12,7 +12,9 @@
 #include <stddef.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <thread>
 #include <memory>
 #include <string>
 #include <vector>
@@ -229,6 +231,38 @@ static int buildShared (tbf_engine* e)
 	return 0;
 }
 
+/* host worker threads for per-template work: the process's lease (OMP_NUM_THREADS, set
+ * on the GPU boxes) or the hardware, at most 16 */
+static unsigned hostThreads ()
+{
+	unsigned    t   = std::thread::hardware_concurrency ();
+	const char* omp = getenv ("OMP_NUM_THREADS");
+	if (omp && atoi (omp) > 0)
+		t = (unsigned)atoi (omp);
+	return std::max (1u, std::min (t, 16u));
+}
+
+/* run f(t) for t < n on up to hostThreads () threads */
+template <typename F>
+static void parallelFor (uint32_t n, F f)
+{
+	const unsigned nt = std::min<unsigned> (hostThreads (), n);
+	if (nt <= 1) {
+		for (uint32_t t = 0; t < n; t++)
+			f (t);
+		return;
+	}
+	std::atomic<uint32_t>    next {0};
+	std::vector<std::thread> pool;
+	for (unsigned k = 0; k < nt; k++)
+		pool.emplace_back ([&] {
+			for (uint32_t t; (t = next.fetch_add (1)) < n;)
+				f (t);
+		});
+	for (auto& th : pool)
+		th.join ();
+}
+
 extern "C" {
 
 int tbf_abi_version (void) { return TBF_ABI_VERSION; }
@@ -258,6 +292,25 @@ int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
 		for (int k = 0; k < TBF_NSTAGES; k++)
 			HIPCHK (hipEventCreateWithFlags (&e->sdone[k], hipEventDisableTiming));
 		HIPCHK (hipEventCreateWithFlags (&e->sjoin, hipEventDisableTiming));
+		if (const char* pm = getenv ("TBF_PIPE_MODE"))
+			e->pipeMode = atoi (pm) == 1 ? 1 : 0;
+		if (const char* pg = getenv ("TBF_PIPE_GROUPS")) { /* "g0,g1,g2,g3,g4", groups 0..2, non-decreasing */
+			for (int k = 0; k < TBF_NSTAGES && *pg; k++) {
+				const int g = atoi (pg);
+				if (g >= 0 && g < 3 && (k == 0 || g >= e->grp[k - 1]))
+					e->grp[k] = g;
+				while (*pg && *pg != ',')
+					pg++;
+				if (*pg == ',')
+					pg++;
+			}
+		}
+		if (e->pipeMode == 1) {
+			HIPCHK (hipStreamCreateWithFlags (&e->gstr3, hipStreamNonBlocking));
+			for (int p = 0; p < 2; p++)
+				for (int k = 0; k < TBF_NSTAGES; k++)
+					HIPCHK (hipEventCreateWithFlags (&e->pdone[p][k], hipEventDisableTiming));
+		}
 		HIPCHK (hipEventCreateWithFlags (&e->upEv, hipEventDisableTiming));
 		HIPCHK (hipEventCreateWithFlags (&e->upEvB, hipEventDisableTiming));
 		const char* pl = getenv ("TBF_PIPELINE");
@@ -300,6 +353,8 @@ int tbf_engine_destroy (tbf_engine* e)
 	for (int p = 0; p < 2; p++)
 		if (e->sstr[p])
 			(void)hipStreamSynchronize (e->sstr[p]);
+	if (e->gstr3)
+		(void)hipStreamSynchronize (e->gstr3);
 	e->bank.release ();
 	e->tplDesc.release ();
 	e->cst.release ();
@@ -330,6 +385,12 @@ int tbf_engine_destroy (tbf_engine* e)
 	for (int p = 0; p < 2; p++)
 		if (e->sstr[p])
 			(void)hipStreamDestroy (e->sstr[p]);
+	if (e->gstr3)
+		(void)hipStreamDestroy (e->gstr3);
+	for (int p = 0; p < 2; p++)
+		for (int k = 0; k < TBF_NSTAGES; k++)
+			if (e->pdone[p][k])
+				(void)hipEventDestroy (e->pdone[p][k]);
 	for (int k = 0; k < TBF_NSTAGES; k++)
 		if (e->sdone[k])
 			(void)hipEventDestroy (e->sdone[k]);
@@ -371,14 +432,19 @@ int tbf_templates_create (tbf_engine* e, uint32_t n, const double* mts128, const
 	std::vector<tbf_tpl_wheel>               wh ((size_t)n * TBF_NW);
 	uint64_t                                 sum = 0;
 	uint32_t                                 maxChunks = 0, maxLen = 0;
-	for (uint32_t t = 0; t < n; t++) {
+	/* the rand-free tables of each template (frequencies, play matrix, wheel lengths and
+	 * spectra) and its rand() window, one template per host thread */
+	parallelFor (n, [&] (uint32_t t) {
 		ts[t].reset (new TgTemplate ());
-		TgTemplate& T = *ts[t];
-		T.prepare (sr, mts128 ? mts128 + 128 * (size_t)t : nullptr, ratio9 ? ratio9 + 9 * (size_t)t : nullptr, e->conf);
+		ts[t]->prepare (sr, mts128 ? mts128 + 128 * (size_t)t : nullptr, ratio9 ? ratio9 + 9 * (size_t)t : nullptr,
+		                e->conf);
 		uint32_t  W[31];
 		GlibcRand rnd (seeds[t]);
 		rnd.window (W);
 		gr_extend (W, &E[61 * (size_t)t]);
+	});
+	for (uint32_t t = 0; t < n; t++) {
+		TgTemplate& T = *ts[t];
 		total[t] = T.total;
 		base[t]  = sum;
 		sum += T.total;
@@ -429,12 +495,14 @@ int tbf_templates_create (tbf_engine* e, uint32_t n, const double* mts128, const
 	dE.release (), dTot.release (), dBase.release (), dWh.release (), dLsb.release (), dBank.release ();
 	if (rc)
 		return rc;
-	for (uint32_t t = 0; t < n; t++) {
+	parallelFor (n, [&] (uint32_t t) {
 		TgTemplate& T = *ts[t];
 		T.bank.assign (hb.begin () + base[t], hb.begin () + base[t] + total[t]);
 		GlibcRand rnd (seeds[t]);
 		rnd.discard (T.total); /* the draws of the bank */
 		T.finish (rnd);
+	});
+	for (uint32_t t = 0; t < n; t++) {
 		ids[t] = (uint32_t)e->tpls.size ();
 		e->tpls.push_back (std::move (ts[t]));
 	}
@@ -719,6 +787,8 @@ static int drainStages (tbf_engine* e)
 		return 0;
 	for (int p = 0; p < 2; p++)
 		HIPCHK (hipStreamSynchronize (e->sstr[p]));
+	if (e->gstr3)
+		HIPCHK (hipStreamSynchronize (e->gstr3));
 	e->stagesBusy = false;
 	return 0;
 }
@@ -728,8 +798,11 @@ static int joinStages (tbf_engine* e, hipStream_t s)
 {
 	if (!e->stagesBusy)
 		return 0;
-	for (int p = 0; p < 2; p++) {
-		HIPCHK (hipEventRecord (e->sjoin, e->sstr[p]));
+	for (int p = 0; p < 3; p++) {
+		hipStream_t q = p < 2 ? e->sstr[p] : e->gstr3;
+		if (!q)
+			continue;
+		HIPCHK (hipEventRecord (e->sjoin, q));
 		HIPCHK (hipStreamWaitEvent (s, e->sjoin, 0));
 	}
 	e->stagesBusy = false;
@@ -1223,6 +1296,51 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		if (e->devCtl)
 			HIPCHK (hipEventRecord (e->upEv, s)); /* this parity's staging is free after it */
 		const int nst = tbf_chain_stages (P.chain);
+		if (piped && e->pipeMode == 1) {
+			/* stage-group streams: every chunk's stage k on stream grp[k], so a stage runs as
+			 * soon as this chunk's previous stage and the previous chunk's same stage are
+			 * done, whatever the later stages of the previous chunk are doing.  Buffer parity
+			 * par was last read by the chunk before last: wait for those readers (stage k's
+			 * output mid1 is read by k_rv_in and k_rv_out, rvA by k_rv_core, rvB by k_rv_out,
+			 * mid2 by k_whirl) when they run on another stream. */
+			static const int readers[5][2] = {{1, 3}, {2, -1}, {3, -1}, {4, -1}, {-1, -1}};
+			auto strm = [&] (int k) { const int g = e->grp[k]; return g < 2 ? e->sstr[g] : e->gstr3; };
+			for (int k = 0; k < nst; k++) {
+				hipStream_t sk = strm (k);
+				if (k == 0 && !e->stagesBusy) { /* after the caller's stream (uploads, earlier chunks) */
+					HIPCHK (hipEventRecord (e->sjoin, s));
+					HIPCHK (hipStreamWaitEvent (sk, e->sjoin, 0));
+				}
+				if (k == nst - 1 && !outWait) { /* the output stage writes the caller's buffers */
+					HIPCHK (hipEventRecord (e->sjoin, s));
+					HIPCHK (hipStreamWaitEvent (sk, e->sjoin, 0));
+					outWait = true;
+				}
+				if (k > 0 && strm (k - 1) != sk)
+					HIPCHK (hipStreamWaitEvent (sk, e->sdone[k - 1], 0));
+				for (int r : readers[k])
+					if (r >= 0 && r < nst && strm (r) != sk)
+						HIPCHK (hipStreamWaitEvent (sk, e->pdone[par][r], 0));
+				hipEvent_t e0 = nullptr, e1 = nullptr;
+				if (e->timeOn) {
+					HIPCHK (hipEventCreate (&e0));
+					HIPCHK (hipEventCreate (&e1));
+					HIPCHK (hipEventRecord (e0, sk));
+				}
+				rc = tbf_launch_stage (&P, k, sk);
+				if (rc)
+					return fail (rc, std::string ("kernel launch failed: ") + hipGetErrorString (hipGetLastError ()));
+				if (e->timeOn) {
+					HIPCHK (hipEventRecord (e1, sk));
+					e->tev.push_back ({k, {e0, e1}});
+				}
+				HIPCHK (hipEventRecord (e->sdone[k], sk));
+				HIPCHK (hipEventRecord (e->pdone[par][k], sk));
+			}
+			e->stagesBusy = true;
+			b0 += len;
+			continue;
+		}
 		if (piped) {
 			hipStream_t sp = e->sstr[par];
 			if (!e->stagesBusy) {

@@ -248,6 +248,14 @@ struct tbf_engine {
 	bool                                    stagesBusy = false; /* pipelined work may be outstanding */
 	bool                                    pipeline = true;    /* TBF_PIPELINE=0 disables */
 	int                                     pipeWait[5] = {0, 1, 2, 3, 4}; /* stage k of a chunk waits for stage pipeWait[k] >= k of the previous one */
+	/* pipeMode 1 (default): streams by stage group (stage k of every chunk on stream
+	 * grp[k]; the stages of one chunk chained by events; a stage waits for the
+	 * chunk-before-last's readers of the buffer parity it overwrites).  TBF_PIPE_MODE=0:
+	 * streams by chunk parity (round 1) */
+	int                                     pipeMode = 1;
+	int                                     grp[5]   = {0, 1, 1, 2, 2};
+	hipStream_t                             gstr3    = nullptr; /* the third group's stream (groups 0, 1 use sstr) */
+	hipEvent_t                              pdone[2][5] = {};
 	/* programme table (.pgm), src/program.h:26 MAXPROGS; pgm.controller.offset */
 	std::vector<Programme>                  progs = std::vector<Programme> (129);
 	int                                     pgmOffset = 1;

@@ -242,8 +242,8 @@ static void playMatrix (TgTemplate& t)
 			}
 		}
 	/* compilePlayMatrix + cpmInsert (1061-1213) */
-	static unsigned char cpmBus[TBF_NW + 1][27];
-	static float         cpmGain[TBF_NW][27];
+	static thread_local unsigned char cpmBus[TBF_NW + 1][27]; /* templates build in parallel */
+	static thread_local float         cpmGain[TBF_NW][27];
 	short                wheelNumber[TBF_NW + 1];
 	short                rowLength[TBF_NW];
 	for (int k = 0; k < 384; k++) {

@@ -63,6 +63,9 @@ int tbf::fail (int code, const std::string& msg)
 /* host-controlled path: delta program entries one chunk may add (a chunk ends early when
  * they would not fit); the device-controlled path sizes its delta slots on demand */
 #define DPROG_CAP(n) ((size_t)(n) * SLOT * 2 + 4096)
+/* control pool region (one per chunk parity on the device-controlled path; the host path
+ * uses region 0): n persistent entries + up to one delta per instance and block */
+#define CTL_REGION(n) ((size_t)(n) * (TBF_CHUNK + 1))
 #define TBF_NSTAGES 5 /* k_tonegen, k_rv_in, k_rv_core, k_rv_out, k_whirl */
 
 /* ------------------------------------------------------------------ construction */
@@ -367,6 +370,9 @@ int tbf_engine_destroy (tbf_engine* e)
 	e->drec.release ();
 	e->dmsg.release ();
 	e->dctlInst.release ();
+	e->drecB.release ();
+	e->dmsgB.release ();
+	e->dctlInstB.release ();
 	e->coff.release ();
 	e->contrib.release ();
 	e->vib.release ();
@@ -947,8 +953,9 @@ static int ensureDevice (tbf_engine* e)
 		std::vector<tbf_inst_const> k (n);
 		for (uint32_t i = 0; i < n; i++)
 			k[i] = e->inst[i].k;
-		if (e->cst.ensure (n) || e->ctl.ensure ((size_t)n * (TBF_CHUNK + 2)) || e->ctlIdx.ensure ((size_t)n * TBF_CHUNK))
+		if (e->cst.ensure (n) || e->ctl.ensure (2 * CTL_REGION (n)) || e->ctlIdx.ensure (2 * (size_t)n * TBF_CHUNK))
 			return fail (-12, "out of device memory (control)");
+		e->ctlVer++; /* both regions' persistent entries need the new pool */
 		/* program pool: the existing instances' persistent programs move along (the device
 		 * control path keeps them only there); new instances start with empty ones */
 		if (int rc = growProg (e, PERSIST (n) + (e->devCtl ? PERSIST (n) : DPROG_CAP (n)), old))
@@ -1140,11 +1147,63 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 	bool         outWait = false; /* the output stage has waited for the caller's stream */
 	const size_t dprogCap = DPROG_CAP (n);
 	e->chg.assign (n, 0);
+	/* after a chunk with control deltas: the instances' final entries become their current
+	 * (pool 0..n-1) control for the next chunk (one-shots cleared).  Device control: k_tgctl
+	 * left each stepped instance's last program in its other persistent slot; the regions'
+	 * persistent entries refresh at the start of the chunks that use them.  Host control:
+	 * uploaded now, and the staging is reused, so it synchronizes. */
+	auto endDelta = [&] () -> int {
+		uint32_t lo = n, hi = 0;
+		for (uint32_t i = 0; i < n; i++)
+			if (e->chg[i]) {
+				e->hCtl[i].whRevOption = -1;
+				lo                     = std::min (lo, i);
+				hi                     = std::max (hi, i + 1);
+				e->chg[i]              = 0;
+			}
+		if (e->devCtl) {
+			for (uint32_t i : e->hCtlInst) {
+				e->pslot[i] ^= 1;
+				e->hCtl[i].prog_off = (uint32_t)((2 * i + e->pslot[i]) * SLOT);
+			}
+			e->ctlVer++;
+			return 0;
+		}
+		HIPCHK (hipMemcpyAsync (e->ctl.p, e->hCtl.data (), n * sizeof (tbf_seg_ctl), hipMemcpyHostToDevice, s));
+		if (hi > lo)
+			HIPCHK (hipMemcpyAsync (e->prog.p + lo * 2 * SLOT, e->hProg.data () + lo * 2 * SLOT,
+			                        (size_t)(hi - lo) * 2 * SLOT * sizeof (tbf_prog_entry), hipMemcpyHostToDevice, s));
+		HIPCHK (hipStreamSynchronize (s));
+		return 0;
+	};
 	uint32_t b0 = 0, evi = 0;
 	while (b0 < nblocks) {
 		/* host control for the chunk, block by block: entry indices per (block, instance),
 		 * new pool entries only where an instance's control changes */
 		const uint32_t want = std::min<uint32_t> (TBF_CHUNK, nblocks - b0);
+		const bool     par  = (e->chunkSeq++ & 1) != 0;
+		const int      rp   = e->devCtl ? (int)par : 0; /* control region of this chunk */
+		/* device control, stage-group pipelining: a delta chunk pipelines like any other; its
+		 * uploads go on the first stage group's stream after the chunk before last (the
+		 * previous user of this region) has finished every stage */
+		const bool     dpipe = e->devCtl && pipe && e->pipeMode == 1;
+		hipStream_t    us    = dpipe ? e->sstr[e->grp[0] < 2 ? e->grp[0] : 0] : s;
+		bool           usWaited = false;
+		auto           usWait   = [&] () -> int {
+            if (usWaited || !dpipe)
+                return 0;
+            usWaited = true;
+            if (!e->stagesBusy) { /* after the caller's stream (earlier non-pipelined work) */
+                HIPCHK (hipEventRecord (e->sjoin, s));
+                HIPCHK (hipStreamWaitEvent (us, e->sjoin, 0));
+            }
+            HIPCHK (hipStreamWaitEvent (us, e->pdone[par][tbf_chain_stages (P.chain) - 1], 0));
+            return 0;
+		};
+		if (e->devCtl && e->persistStale) {
+			e->ctlVer++; /* the regions refresh below */
+			e->persistStale = false;
+		}
 		if (e->persistStale) {
 			/* the persistent pool (entry i = instance i's current control and programme) as
 			 * of the START of this chunk: an instance without a delta at some block renders
@@ -1169,6 +1228,19 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			e->hCtlPin.swap (e->hCtlPinB);
 			std::swap (e->upEv, e->upEvB);
 			HIPCHK (hipEventSynchronize (e->upEv));
+		}
+		if (e->devCtl && e->regionVer[rp] != e->ctlVer) {
+			/* this region's persistent entries: the control as of the START of this chunk (an
+			 * instance renders its blocks before its first delta with entry i) */
+			if (!dpipe && (rc = joinStages (e, s)))
+				return rc;
+			if ((rc = usWait ()))
+				return rc;
+			e->hCtlPin.resize (n);
+			memcpy ((void*)e->hCtlPin.data (), e->hCtl.data (), n * sizeof (tbf_seg_ctl));
+			HIPCHK (hipMemcpyAsync (e->ctl.p + rp * CTL_REGION (n), e->hCtlPin.data (), n * sizeof (tbf_seg_ctl),
+			                        hipMemcpyHostToDevice, us));
+			e->regionVer[rp] = e->ctlVer;
 		}
 		e->dCtl.clear ();
 		e->dProg.clear ();
@@ -1207,7 +1279,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 						/* a stepped delta gets its own program slot, which k_tgctl fills; the
 						 * others play the program before them */
 						if (pc) {
-							c.prog_off = (uint32_t)(PERSIST (n) + e->dCtl.size () * SLOT);
+							c.prog_off = (uint32_t)(PERSIST (n) + ((size_t)rp * n * TBF_CHUNK + e->dCtl.size ()) * SLOT);
 							if (!e->stepped[i]) {
 								e->stepped[i] = 1;
 								e->hCtlInst.push_back (i);
@@ -1247,8 +1319,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		                    std::chrono::steady_clock::now () - hc0)
 		                    .count ();
 		e->hostCtlBlocks += len;
-		const bool     par     = (e->chunkSeq++ & 1) != 0;
-		const bool     piped   = pipe && !delta;
+		const bool     piped   = pipe && (!delta || dpipe);
 		P.mid1 = e->mid1.p ? e->mid1.p + (par ? need : 0) : nullptr;
 		P.mid2 = e->mid2.p ? e->mid2.p + (par ? need : 0) : nullptr;
 		P.rvA  = e->rvA.p ? e->rvA.p + (par ? 2 * need : 0) : nullptr;
@@ -1256,45 +1327,58 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		if (!piped && (rc = joinStages (e, s)))
 			return rc;
 		if (delta) {
-			if (e->devCtl && (rc = growProg (e, PERSIST (n) + e->dCtl.size () * SLOT, n)))
-				return rc; /* (after joinStages: no launch still reads the pool) */
-			HIPCHK (hipMemcpyAsync (e->ctl.p + n, e->dCtl.data (), e->dCtl.size () * sizeof (tbf_seg_ctl),
-			                        hipMemcpyHostToDevice, s));
+			/* device control: both regions' delta slots, sized once for a delta per
+			 * instance and block (growProg synchronizes the device when it grows) */
+			if (e->devCtl && (rc = growProg (e, PERSIST (n) + 2 * (size_t)n * TBF_CHUNK * SLOT, n)))
+				return rc;
+			if ((rc = usWait ()))
+				return rc;
+			HIPCHK (hipMemcpyAsync (e->ctl.p + rp * CTL_REGION (n) + n, e->dCtl.data (),
+			                        e->dCtl.size () * sizeof (tbf_seg_ctl), hipMemcpyHostToDevice, us));
 			if (!e->dProg.empty ())
 				HIPCHK (hipMemcpyAsync (e->prog.p + PERSIST (n), e->dProg.data (),
-				                        e->dProg.size () * sizeof (tbf_prog_entry), hipMemcpyHostToDevice, s));
-			HIPCHK (hipMemcpyAsync (e->ctlIdx.p, e->hIdx.data (), (size_t)len * n * sizeof (uint32_t),
-			                        hipMemcpyHostToDevice, s));
+				                        e->dProg.size () * sizeof (tbf_prog_entry), hipMemcpyHostToDevice, us));
+			HIPCHK (hipMemcpyAsync (e->ctlIdx.p + (size_t)rp * n * TBF_CHUNK, e->hIdx.data (),
+			                        (size_t)len * n * sizeof (uint32_t), hipMemcpyHostToDevice, us));
 		}
 		P.prog      = e->prog.p;
-		P.ctlIdx    = delta ? e->ctlIdx.p : nullptr;
+		P.ctl       = e->ctl.p + rp * CTL_REGION (n);
+		P.ctlIdx    = delta ? e->ctlIdx.p + (size_t)rp * n * TBF_CHUNK : nullptr;
 		P.nBlocks   = len;
 		P.outOffset = (uint64_t)b0 * TBF_BLK;
 		P.nCtlInst  = 0;
 		if (e->devCtl && !e->hCtlInst.empty ()) {
 			/* k_tgctl: the stepped blocks' programs, ahead of k_tonegen on this stream */
-			if (e->drec.ensure (e->hRec.size ()) || e->dmsg.ensure (std::max<size_t> (e->hMsg.size (), 1)) ||
-			    e->dctlInst.ensure (e->hCtlInst.size ()))
+			/* records per region parity: k_tgctl of the chunk before last (same stream, or
+			 * the caller's stream when not pipelined) read the other set */
+			DevBuf<tbf_tgc_rec>& drec = rp ? e->drecB : e->drec;
+			DevBuf<uint16_t>&    dmsg = rp ? e->dmsgB : e->dmsg;
+			DevBuf<uint32_t>&    dci  = rp ? e->dctlInstB : e->dctlInst;
+			if (drec.cap < e->hRec.size () || dmsg.cap < e->hMsg.size () || dci.cap < e->hCtlInst.size ())
+				HIPCHK (hipDeviceSynchronize ()); /* growing: nothing may still read the old buffers */
+			if (drec.ensure (e->hRec.size ()) || dmsg.ensure (std::max<size_t> (e->hMsg.size (), 1)) ||
+			    dci.ensure (e->hCtlInst.size ()))
 				return fail (-12, "out of device memory (control records)");
-			HIPCHK (hipMemcpyAsync (e->drec.p, e->hRec.data (), e->hRec.size () * sizeof (tbf_tgc_rec),
-			                        hipMemcpyHostToDevice, s));
+			HIPCHK (hipMemcpyAsync (drec.p, e->hRec.data (), e->hRec.size () * sizeof (tbf_tgc_rec),
+			                        hipMemcpyHostToDevice, us));
 			if (!e->hMsg.empty ())
-				HIPCHK (hipMemcpyAsync (e->dmsg.p, e->hMsg.data (), e->hMsg.size () * sizeof (uint16_t),
-				                        hipMemcpyHostToDevice, s));
-			HIPCHK (hipMemcpyAsync (e->dctlInst.p, e->hCtlInst.data (), e->hCtlInst.size () * 4, hipMemcpyHostToDevice,
-			                        s));
+				HIPCHK (hipMemcpyAsync (dmsg.p, e->hMsg.data (), e->hMsg.size () * sizeof (uint16_t),
+				                        hipMemcpyHostToDevice, us));
+			HIPCHK (hipMemcpyAsync (dci.p, e->hCtlInst.data (), e->hCtlInst.size () * 4, hipMemcpyHostToDevice, us));
 			P.tgc      = e->tgc.p;
-			P.rec      = e->drec.p;
-			P.msgs     = e->dmsg.p;
-			P.ctlInst  = e->dctlInst.p;
+			P.rec      = drec.p;
+			P.msgs     = dmsg.p;
+			P.ctlInst  = dci.p;
 			P.nCtlInst = (uint32_t)e->hCtlInst.size ();
 			P.coff     = e->coff.p;
 			P.contrib  = e->contrib.p;
-			if ((rc = tbf_launch_tgctl (&P, s)))
+			if ((rc = tbf_launch_tgctl (&P, us)))
 				return fail (rc, std::string ("k_tgctl launch failed: ") + hipGetErrorString (hipGetLastError ()));
 		}
 		if (e->devCtl)
-			HIPCHK (hipEventRecord (e->upEv, s)); /* this parity's staging is free after it */
+			HIPCHK (hipEventRecord (e->upEv, us)); /* this parity's staging is free after it */
+		if (usWaited && piped) /* the stage streams now follow the uploads on us */
+			e->stagesBusy = true;
 		const int nst = tbf_chain_stages (P.chain);
 		if (piped && e->pipeMode == 1) {
 			/* stage-group streams: every chunk's stage k on stream grp[k], so a stage runs as
@@ -1338,6 +1422,8 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 				HIPCHK (hipEventRecord (e->pdone[par][k], sk));
 			}
 			e->stagesBusy = true;
+			if (delta && (rc = endDelta ()))
+				return rc;
 			b0 += len;
 			continue;
 		}
@@ -1392,39 +1478,8 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 				e->tev.push_back ({k, {e0, e1}});
 			}
 		}
-		if (delta) {
-			/* the instances' final entries become their current (pool 0..n-1) control for
-			 * the next chunk (one-shots cleared); staging buffers are reused, so keep order */
-			uint32_t lo = n, hi = 0;
-			for (uint32_t i = 0; i < n; i++)
-				if (e->chg[i]) {
-					e->hCtl[i].whRevOption = -1;
-					lo                     = std::min (lo, i);
-					hi                     = std::max (hi, i + 1);
-					e->chg[i]              = 0;
-				}
-			/* device control: k_tgctl left each stepped instance's last program in its other
-			 * persistent slot */
-			for (uint32_t i : e->hCtlInst) {
-				e->pslot[i] ^= 1;
-				e->hCtl[i].prog_off = (uint32_t)((2 * i + e->pslot[i]) * SLOT);
-			}
-			if (e->devCtl) {
-				/* from a pinned snapshot, so the next chunk's control can run on the host
-				 * while this one renders */
-				e->hCtlPin.resize (n);
-				memcpy ((void*)e->hCtlPin.data (), e->hCtl.data (), n * sizeof (tbf_seg_ctl));
-				HIPCHK (hipMemcpyAsync (e->ctl.p, e->hCtlPin.data (), n * sizeof (tbf_seg_ctl), hipMemcpyHostToDevice, s));
-				HIPCHK (hipEventRecord (e->upEv, s));
-			} else {
-				HIPCHK (hipMemcpyAsync (e->ctl.p, e->hCtl.data (), n * sizeof (tbf_seg_ctl), hipMemcpyHostToDevice, s));
-				if (hi > lo)
-					HIPCHK (hipMemcpyAsync (e->prog.p + lo * 2 * SLOT, e->hProg.data () + lo * 2 * SLOT,
-					                        (size_t)(hi - lo) * 2 * SLOT * sizeof (tbf_prog_entry), hipMemcpyHostToDevice,
-					                        s));
-				HIPCHK (hipStreamSynchronize (s));
-			}
-		}
+		if (delta && (rc = endDelta ()))
+			return rc;
 		b0 += len;
 	}
 	for (; evi < nev; evi++) { /* events at or after the last block apply to the next render */

@@ -207,6 +207,14 @@ struct tbf_engine {
 	hipEvent_t                              upEv = nullptr, upEvB = nullptr;
 	std::vector<uint8_t>                    stepped;  /* membership of hCtlInst */
 	std::vector<uint8_t>                    pslot;    /* persistent program slot (0/1) per instance */
+	/* device control, pipelined delta chunks: the control pool (persistent entries +
+	 * deltas), the index table and the control records come in two regions by chunk
+	 * parity; region p's persistent entries are refreshed from hCtl when they are older
+	 * than its version (ctlVer counts the changes of hCtl) */
+	uint64_t                                ctlVer = 1, regionVer[2] = {0, 0};
+	DevBuf<tbf_tgc_rec>                     drecB;
+	DevBuf<uint16_t>                        dmsgB;
+	DevBuf<uint32_t>                        dctlInstB;
 	DevBuf<uint32_t>                        vib;
 	DevBuf<uint32_t>                        xsj; /* xorshift32 jump table */
 	DevBuf<float>                           whTab, whBw;

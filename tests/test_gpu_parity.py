@@ -259,6 +259,72 @@ def test_gpu_render_events_dense_across_chunks(oracle):
     assert max(eL, eR) <= TOL
 
 
+def test_gpu_dense_events_threaded_host_control(oracle):
+    """§8(f) row 1 at scale: 1200 instances with events on every block (a key released
+    and one pressed, a drawbar move, a control function every 5 blocks) over 80 blocks
+    (across the chunk edge).  With this many active instances the host front end steps
+    on worker threads by instance range (stepChunkParallel); the output must equal, bit
+    for bit, an engine stepping serially (TBF_HOST_SERIAL=1) for every instance, and the
+    oracle for a sample of instances."""
+    import os
+    import torch
+    import tunebfree_amd as T
+    from orc_bind import Template
+    n, nb = 1200, 80
+    seeds = [3000 + i for i in range(n)]
+    cid = None
+    rows, oscen = [], [[] for _ in range(n)]
+    for i in range(n):
+        for (k, a, v) in S.jazz1_params():
+            rows.append((0, i, 1, a, float(v)))
+            oscen[i].append((0, k, a, v))
+        for k in S.chord_for(i):
+            rows.append((0, i, 0, k, 1.0))
+            oscen[i].append((0, "note", k, 1))
+        for b in range(1, nb):
+            k0, k1 = 72 + (i + b - 1) % 12, 72 + (i + b) % 12
+            rows.append((b, i, 0, k0, 0.0))
+            oscen[i].append((b, "note", k0, 0))
+            rows.append((b, i, 0, k1, 1.0))
+            oscen[i].append((b, "note", k1, 1))
+            rows.append((b, i, 1, S.P_DRAWBAR + 4, float((i + b) % 9)))
+            oscen[i].append((b, "param", S.P_DRAWBAR + 4, (i + b) % 9))
+    outs = []
+    for serial in (False, True):
+        if serial:
+            os.environ["TBF_HOST_SERIAL"] = "1"
+        try:
+            eng = T.Engine(sample_rate=48000.0, device=0)
+        finally:
+            os.environ.pop("TBF_HOST_SERIAL", None)
+        tid = eng.template(seed=7)
+        eng.add_instances([tid] * n, seeds)
+        cid = eng.control_id("upper.drawbar4")
+        extra = [(b, i, 2, cid, float((7 * i + b) % 128)) for i in range(0, n, 3) for b in range(2, nb, 5)]
+        ev = eng.events(rows + extra)
+        L = torch.zeros((n, nb * 128), dtype=torch.float32, device="cuda")
+        R = torch.zeros_like(L)
+        eng.render_events_device(nb, ev, L.data_ptr(), R.data_ptr(), nb * 128)
+        eng.synchronize()
+        ht, _ = eng.host_time()
+        outs.append((L.cpu().numpy(), R.cpu().numpy()))
+        print(f"{'serial' if serial else 'threaded'} host control: {ht:.1f} ms")
+        eng.close()
+        del L, R
+    assert np.array_equal(outs[0][0].view(np.uint32), outs[1][0].view(np.uint32))
+    assert np.array_equal(outs[0][1].view(np.uint32), outs[1][1].view(np.uint32))
+    # the control-function events: upper.drawbar4 <- CC v is setDrawBar (3, rint ((127 - v) * 8 / 127))
+    for (b, i, _k, _c, v) in [(b, i, 2, cid, float((7 * i + b) % 128)) for i in range(0, n, 3) for b in range(2, nb, 5)]:
+        oscen[i].append((b, "param", S.P_DRAWBAR + 3, int(np.rint((127 - v) * 8.0 / 127.0))))
+    sample = [0, 1, 3, 599, 1000, n - 1]
+    tpl = Template(oracle, seed=7)
+    oL, oR, *_ = oracle_run(oracle, tpl, [seeds[i] for i in sample], [sorted(oscen[i], key=lambda r: r[0]) for i in sample], nb)
+    eL, xL = compare(outs[0][0][sample], oL)
+    eR, xR = compare(outs[0][1][sample], oR)
+    print(f"threaded dense events vs oracle ({len(sample)} instances): max|err| L={eL:.3g} R={eR:.3g}")
+    assert max(eL, eR) <= TOL
+
+
 def test_gpu_synth_sound_irregular_periods(oracle, tunings):
     """tbf_synth_sound (the synthSound FIFO of b_synth/lv2.cpp:1270-1287) with irregular
     period sizes (1 .. 700 frames; a call that needs several blocks renders them in one

@@ -278,13 +278,14 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_tgctl (
 		ctl_block (sm, G, R, (tbf_prog_entry*)P.prog + off);
 		last = off;
 	}
-	/* the instance's last program becomes its persistent one, in the slot the current
-	 * persistent entry does not use (the host flips its entry the same way after the
-	 * chunk) */
+	/* the instance's last program becomes its persistent one, in the slot after the current
+	 * persistent entry's (mod TBF_PROG_PSLOTS; the host advances its entry the same way
+	 * after the chunk) */
 	if (last >= 0) {
 		const uint32_t cur   = P.ctl[inst].prog_off;
-		const uint32_t slot0 = 2u * inst * TBF_PROG_SLOT;
-		const uint32_t dst   = cur == slot0 ? slot0 + TBF_PROG_SLOT : slot0;
+		const uint32_t slot0 = (uint32_t)TBF_PROG_PSLOTS * inst * TBF_PROG_SLOT;
+		const uint32_t nxt   = ((cur - slot0) / TBF_PROG_SLOT + 1) % TBF_PROG_PSLOTS;
+		const uint32_t dst   = slot0 + nxt * TBF_PROG_SLOT;
 		const tbf_prog_entry* src = P.prog + last;
 		tbf_prog_entry*       d   = (tbf_prog_entry*)P.prog + dst;
 		const uint32_t        cnt = src[0].pad + 1;

@@ -35,6 +35,7 @@ extern "C" int tbf_launch_calibrate (int op, void* buf, uint64_t n, hipStream_t 
 using namespace tbf;
 
 static thread_local std::string g_err;
+thread_local std::vector<uint32_t>* tbf::tlAct = nullptr;
 
 int tbf::fail (int code, const std::string& msg)
 {
@@ -54,7 +55,8 @@ int tbf::fail (int code, const std::string& msg)
  * holds two persistent slots per instance (2 i, 2 i + 1; the host-controlled path uses
  * the first), then the chunk's delta programs */
 #define SLOT ((size_t)TBF_PROG_SLOT)
-#define PERSIST(n) ((size_t)(n) * 2 * SLOT)
+#define PSLOTS ((size_t)TBF_PROG_PSLOTS)
+#define PERSIST(n) ((size_t)(n) * PSLOTS * SLOT)
 /* blocks per kernel launch chunk: bounds the inter-stage buffers to
  * n_inst x TBF_CHUNK x 128 floats each (134 MB at 4096 instances) */
 #ifndef TBF_CHUNK
@@ -240,7 +242,10 @@ static unsigned hostThreads ()
 {
 	unsigned    t   = std::thread::hardware_concurrency ();
 	const char* omp = getenv ("OMP_NUM_THREADS");
-	if (omp && atoi (omp) > 0)
+	const char* ht  = getenv ("TBF_HOST_THREADS");
+	if (ht && atoi (ht) > 0)
+		t = (unsigned)atoi (ht);
+	else if (omp && atoi (omp) > 0)
 		t = (unsigned)atoi (omp);
 	return std::max (1u, std::min (t, 16u));
 }
@@ -310,6 +315,7 @@ int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
 		}
 		if (e->pipeMode == 1) {
 			HIPCHK (hipStreamCreateWithFlags (&e->gstr3, hipStreamNonBlocking));
+			HIPCHK (hipStreamCreateWithFlags (&e->cstr, hipStreamNonBlocking));
 			for (int p = 0; p < 2; p++)
 				for (int k = 0; k < TBF_NSTAGES; k++)
 					HIPCHK (hipEventCreateWithFlags (&e->pdone[p][k], hipEventDisableTiming));
@@ -322,6 +328,8 @@ int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
 		 * reference path for A/B); default: on the device (k_tgctl) */
 		const char* hc = getenv ("TBF_HOST_CONTROL");
 		e->devCtl      = !(hc && hc[0] == '1');
+		const char* hs = getenv ("TBF_HOST_SERIAL"); /* the serial loop (A/B); TBF_HOST_THREADS: workers */
+		e->parCtl      = !(hs && hs[0] == '1');
 		/* TBF_PIPE_WAIT="w0,w1,...": stage k of a chunk also waits for stage w_k >= k of the
 		 * previous chunk (default w_k = k), which moves which stages of neighbouring chunks
 		 * co-run; any such table is exact (it only adds dependencies) */
@@ -358,6 +366,8 @@ int tbf_engine_destroy (tbf_engine* e)
 			(void)hipStreamSynchronize (e->sstr[p]);
 	if (e->gstr3)
 		(void)hipStreamSynchronize (e->gstr3);
+	if (e->cstr)
+		(void)hipStreamSynchronize (e->cstr);
 	e->bank.release ();
 	e->tplDesc.release ();
 	e->cst.release ();
@@ -393,6 +403,8 @@ int tbf_engine_destroy (tbf_engine* e)
 			(void)hipStreamDestroy (e->sstr[p]);
 	if (e->gstr3)
 		(void)hipStreamDestroy (e->gstr3);
+	if (e->cstr)
+		(void)hipStreamDestroy (e->cstr);
 	for (int p = 0; p < 2; p++)
 		for (int k = 0; k < TBF_NSTAGES; k++)
 			if (e->pdone[p][k])
@@ -795,6 +807,8 @@ static int drainStages (tbf_engine* e)
 		HIPCHK (hipStreamSynchronize (e->sstr[p]));
 	if (e->gstr3)
 		HIPCHK (hipStreamSynchronize (e->gstr3));
+	if (e->cstr)
+		HIPCHK (hipStreamSynchronize (e->cstr));
 	e->stagesBusy = false;
 	return 0;
 }
@@ -804,8 +818,8 @@ static int joinStages (tbf_engine* e, hipStream_t s)
 {
 	if (!e->stagesBusy)
 		return 0;
-	for (int p = 0; p < 3; p++) {
-		hipStream_t q = p < 2 ? e->sstr[p] : e->gstr3;
+	for (int p = 0; p < 4; p++) {
+		hipStream_t q = p < 2 ? e->sstr[p] : p == 2 ? e->gstr3 : e->cstr;
 		if (!q)
 			continue;
 		HIPCHK (hipEventRecord (e->sjoin, q));
@@ -977,8 +991,8 @@ static int ensureDevice (tbf_engine* e)
 		e->hProg.resize (PERSIST (n));
 		e->pslot.resize (n, 0);
 		for (uint32_t i = old; i < n; i++) {
-			e->hCtl[i].prog_off = (uint32_t)(2 * i * SLOT);
-			e->hProg[2 * i * SLOT].wheel = 0xFFFF; /* empty program header */
+			e->hCtl[i].prog_off = (uint32_t)(PSLOTS * i * SLOT);
+			e->hProg[PSLOTS * i * SLOT].wheel = 0xFFFF; /* empty program header */
 		}
 		e->devInst = n;
 	}
@@ -1009,7 +1023,8 @@ static int applyEvent (tbf_engine* e, const tbf_event& ev)
  * part of oscGenerateFragment and the effect setters' per-block constants).  Updates
  * the instance's current control e->hCtl[i] / program e->hProg; returns true when the
  * control the next block renders with changed. */
-static bool stepControl (tbf_engine* e, uint32_t i, bool& progChanged, tbf_tgc_rec* rec = nullptr)
+static bool stepControl (tbf_engine* e, uint32_t i, bool& progChanged, tbf_tgc_rec* rec = nullptr,
+                         std::vector<uint16_t>* msgOut = nullptr)
 {
 	Instance&    in      = e->inst[i];
 	tbf_seg_ctl& c       = e->hCtl[i];
@@ -1019,9 +1034,16 @@ static bool stepControl (tbf_engine* e, uint32_t i, bool& progChanged, tbf_tgc_r
 		return false;
 	if (tgDirty && rec) {
 		/* device control: the front end here, the per-wheel part in k_tgctl */
-		const uint32_t at = (uint32_t)e->hMsg.size ();
-		e->hMsg.resize (at + std::min<size_t> (in.tg.msg.size (), 0xFFFF));
-		in.tg.stepFront (e->hMsg.data () + at, at, *rec, c);
+		const size_t k = std::min<size_t> (in.tg.msg.size (), 0xFFFF);
+		if (msgOut) { /* a host worker's own message list (renderImpl merges them) */
+			const uint32_t at = (uint32_t)msgOut->size ();
+			msgOut->resize (at + k);
+			in.tg.stepFront (msgOut->data () + at, at, *rec, c);
+		} else {
+			const uint32_t at = (uint32_t)e->hMsg.size ();
+			e->hMsg.resize (at + k);
+			in.tg.stepFront (e->hMsg.data () + at, at, *rec, c);
+		}
 		in.progDirty = false;
 		in.ctlDirty  = true;
 		progChanged  = true;
@@ -1035,12 +1057,12 @@ static bool stepControl (tbf_engine* e, uint32_t i, bool& progChanged, tbf_tgc_r
 	if (in.progDirty) {
 		/* host control: the program in the instance's first slot, behind its header */
 		const size_t    np   = std::min (in.prog.size (), SLOT - 1);
-		tbf_prog_entry* slot = e->hProg.data () + 2 * i * SLOT;
+		tbf_prog_entry* slot = e->hProg.data () + PSLOTS * i * SLOT;
 		slot[0]              = tbf_prog_entry {};
 		slot[0].wheel        = 0xFFFF;
 		slot[0].pad          = (uint32_t)np;
 		std::copy (in.prog.begin (), in.prog.begin () + (long)np, slot + 1);
-		c.prog_off   = (uint32_t)(2 * i * SLOT);
+		c.prog_off   = (uint32_t)(PSLOTS * i * SLOT);
 		c.prog_len   = (uint32_t)np;
 		in.progDirty = false;
 		progChanged  = true;
@@ -1063,6 +1085,146 @@ static bool stepControl (tbf_engine* e, uint32_t i, bool& progChanged, tbf_tgc_r
 	return true;
 }
 
+/* Device control: one chunk's host control (events + front-end steps) on host worker
+ * threads, one contiguous instance range each.  Instances are independent and each keeps
+ * its own events' order, so this equals the serial loop; only where the deltas sit in the
+ * pool differs: worker t writes its k-th delta to position (first instance of its range) *
+ * want + k of the staging (a range of m instances has at most m * want deltas), so nothing
+ * is moved afterwards and the kernels reach the deltas through hIdx; dSeg lists the filled
+ * segments for the uploads.  Events are [evBeg, evEnd) of ev (block < b0 + want; programme
+ * changes excluded by the caller: randomizeDrawbars writes the shared programme table).
+ * Fills what the serial loop fills: dCtl, hRec, hMsg, hCtlInst, stepped, hIdx (every row),
+ * curIdx, chg, actList. */
+static int stepChunkParallel (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0, const tbf_event* ev,
+                              uint32_t evBeg, uint32_t evEnd, int rp, bool& delta)
+{
+	const unsigned T   = std::max (1u, std::min<unsigned> (hostThreads (), (n + 255) / 256));
+	const uint32_t per = (n + T - 1) / T;
+	auto&          out = e->parStep;
+	out.resize (T);
+	for (auto& o : out) {
+		o.msgs.clear ();
+		o.act.clear ();
+		o.ctlInst.clear ();
+		o.evs.clear ();
+		o.nd = 0;
+		o.rc = 0;
+	}
+	for (uint32_t a : e->actList) /* the active list by range, in order */
+		out[a / per].act.push_back (a);
+	for (uint32_t k = evBeg; k < evEnd; k++)
+		out[ev[k].inst / per].evs.push_back (k);
+	e->dCtl.resize ((size_t)n * want);
+	e->hRec.resize ((size_t)n * want);
+	std::vector<uint32_t>& cur = e->curIdx;
+	const auto             ph0 = std::chrono::steady_clock::now ();
+	std::vector<uint64_t>  thNs (T);
+	const bool scratch = getenv ("TBF_PAR_SCRATCH") != nullptr;
+	parallelFor (T, [&] (uint32_t t) {
+		const auto           th0  = std::chrono::steady_clock::now ();
+		tbf_engine::ParStep& o    = out[t];
+		const uint32_t       i0   = t * per, i1 = std::min (n, i0 + per);
+		const uint32_t       base = i0 * want;
+		if (scratch) {
+			o.sc.resize ((size_t)(i1 - i0) * want);
+			o.sr.resize ((size_t)(i1 - i0) * want);
+		}
+		tbf_seg_ctl* Cc = scratch ? o.sc.data () : e->dCtl.data () + base;
+		tbf_tgc_rec* Rr = scratch ? o.sr.data () : e->hRec.data () + base;
+		tlAct                     = &o.act;
+		size_t ep                 = 0;
+		for (uint32_t i = i0; i < i1; i++)
+			cur[i] = i;
+		for (uint32_t len = 0; len < want && !o.rc; len++) {
+			for (; ep < o.evs.size () && ev[o.evs[ep]].block <= b0 + len; ep++) {
+				if ((o.rc = applyEvent (e, ev[o.evs[ep]])))
+					break;
+				markActive (e, ev[o.evs[ep]].inst); /* (control-function events do not mark) */
+			}
+			size_t keep = 0;
+			for (size_t a = 0; a < o.act.size (); a++) {
+				const uint32_t i = o.act[a];
+				bool           pc;
+				tbf_tgc_rec&   rec = Rr[o.nd];
+				if (stepControl (e, i, pc, &rec, &o.msgs)) {
+					const uint32_t d = base + o.nd;
+					tbf_seg_ctl&   c = Cc[o.nd++];
+					c                = e->hCtl[i];
+					if (pc) {
+						c.prog_off = (uint32_t)(PERSIST (n) + ((size_t)rp * n * TBF_CHUNK + d) * SLOT);
+						if (!e->stepped[i]) {
+							e->stepped[i] = 1;
+							o.ctlInst.push_back (i);
+						}
+					} else {
+						memset (&rec, 0, sizeof (rec));
+						if (cur[i] >= n)
+							c.prog_off = Cc[cur[i] - n - base].prog_off;
+					}
+					cur[i]        = n + d;
+					e->chg[i]     = 1;
+					o.act[keep++] = i;
+				} else
+					e->inAct[i] = 0;
+			}
+			o.act.resize (keep);
+			for (uint32_t i = i0; i < i1; i++)
+				e->hIdx[(size_t)len * n + i] = cur[i];
+		}
+		tlAct = nullptr;
+		thNs[t] = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds> (std::chrono::steady_clock::now () - th0).count ();
+	});
+	const auto ph1 = std::chrono::steady_clock::now ();
+	std::vector<size_t> mb (T);
+	size_t              nm = 0;
+	e->dSeg.clear ();
+	for (unsigned t = 0; t < T; t++) {
+		if (out[t].rc)
+			return out[t].rc;
+		mb[t] = nm;
+		nm += out[t].msgs.size ();
+		if (out[t].nd) {
+			e->dSeg.push_back ({t * per * want, out[t].nd});
+			delta = true;
+		}
+	}
+	if (e->dSeg.empty ())
+		e->dSeg.push_back ({0, 0});
+	e->hMsg.resize (nm);
+	if (nm || scratch)
+		parallelFor (T, [&] (uint32_t t) { /* message offsets: worker-local -> chunk */
+			const tbf_engine::ParStep& o    = out[t];
+			const size_t               base = (size_t)t * per * want;
+			if (scratch && o.nd) {
+				memcpy ((void*)(e->dCtl.data () + base), o.sc.data (), o.nd * sizeof (tbf_seg_ctl));
+				memcpy ((void*)(e->hRec.data () + base), o.sr.data (), o.nd * sizeof (tbf_tgc_rec));
+			}
+			for (size_t d = base; d < base + o.nd; d++)
+				if (e->hRec[d].flags & 0x80)
+					e->hRec[d].msgOff += (uint32_t)mb[t];
+			if (!o.msgs.empty ())
+				memcpy (e->hMsg.data () + mb[t], o.msgs.data (), o.msgs.size () * sizeof (uint16_t));
+		});
+	e->actList.clear ();
+	for (unsigned t = 0; t < T; t++) {
+		e->actList.insert (e->actList.end (), out[t].act.begin (), out[t].act.end ());
+		for (uint32_t i : out[t].ctlInst)
+			e->hCtlInst.push_back (i);
+	}
+	if (getenv ("TBF_DEBUG_HOST_PHASES")) {
+		const auto ph2 = std::chrono::steady_clock::now ();
+		auto       ms  = [] (auto a, auto b) { return std::chrono::duration<double, std::milli> (b - a).count (); };
+		uint64_t   mx = 0, sum = 0;
+		for (uint64_t v : thNs) {
+			mx = std::max (mx, v);
+			sum += v;
+		}
+		fprintf (stderr, "stepChunkParallel T=%u: step %.3f ms (thread max %.3f, mean %.3f) merge %.3f ms\n", T,
+		         ms (ph0, ph1), mx / 1e6, sum / 1e6 / T, ms (ph1, ph2));
+	}
+	return 0;
+}
+
 static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, uint64_t stride, hipStream_t s,
                        const tbf_event* ev = nullptr, uint32_t nev = 0)
 {
@@ -1083,9 +1245,9 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			HIPCHK (hipMemcpyAsync (&e->cst.p[i].tpl, &e->inst[i].k.tpl, sizeof (uint32_t), hipMemcpyHostToDevice, s));
 			if (e->devCtl) { /* a fresh per-wheel control state and an empty program */
 				HIPCHK (hipMemsetAsync (e->tgc.p + i, 0, sizeof (tbf_tgc_state), s));
-				HIPCHK (hipMemsetAsync (e->prog.p + 2 * i * SLOT, 0, 2 * SLOT * sizeof (tbf_prog_entry), s));
+				HIPCHK (hipMemsetAsync (e->prog.p + PSLOTS * i * SLOT, 0, PSLOTS * SLOT * sizeof (tbf_prog_entry), s));
 				e->pslot[i]         = 0;
-				e->hCtl[i].prog_off = (uint32_t)(2 * i * SLOT);
+				e->hCtl[i].prog_off = (uint32_t)(PSLOTS * i * SLOT);
 				e->persistStale     = true;
 			}
 		}
@@ -1163,16 +1325,16 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			}
 		if (e->devCtl) {
 			for (uint32_t i : e->hCtlInst) {
-				e->pslot[i] ^= 1;
-				e->hCtl[i].prog_off = (uint32_t)((2 * i + e->pslot[i]) * SLOT);
+				e->pslot[i]         = (uint8_t)((e->pslot[i] + 1) % PSLOTS);
+				e->hCtl[i].prog_off = (uint32_t)((PSLOTS * i + e->pslot[i]) * SLOT);
 			}
 			e->ctlVer++;
 			return 0;
 		}
 		HIPCHK (hipMemcpyAsync (e->ctl.p, e->hCtl.data (), n * sizeof (tbf_seg_ctl), hipMemcpyHostToDevice, s));
 		if (hi > lo)
-			HIPCHK (hipMemcpyAsync (e->prog.p + lo * 2 * SLOT, e->hProg.data () + lo * 2 * SLOT,
-			                        (size_t)(hi - lo) * 2 * SLOT * sizeof (tbf_prog_entry), hipMemcpyHostToDevice, s));
+			HIPCHK (hipMemcpyAsync (e->prog.p + lo * PSLOTS * SLOT, e->hProg.data () + lo * PSLOTS * SLOT,
+			                        (size_t)(hi - lo) * PSLOTS * SLOT * sizeof (tbf_prog_entry), hipMemcpyHostToDevice, s));
 		HIPCHK (hipStreamSynchronize (s));
 		return 0;
 	};
@@ -1184,10 +1346,12 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		const bool     par  = (e->chunkSeq++ & 1) != 0;
 		const int      rp   = e->devCtl ? (int)par : 0; /* control region of this chunk */
 		/* device control, stage-group pipelining: a delta chunk pipelines like any other; its
-		 * uploads go on the first stage group's stream after the chunk before last (the
-		 * previous user of this region) has finished every stage */
+		 * uploads and k_tgctl go on the control stream cstr after the chunk before last (the
+		 * previous user of this region) has finished every stage, so they overlap the
+		 * previous chunk's k_tonegen (three persistent program slots make that exact); the
+		 * chunk's first stage waits for them (upEv) */
 		const bool     dpipe = e->devCtl && pipe && e->pipeMode == 1;
-		hipStream_t    us    = dpipe ? e->sstr[e->grp[0] < 2 ? e->grp[0] : 0] : s;
+		hipStream_t    us    = dpipe ? e->cstr : s;
 		bool           usWaited = false;
 		auto           usWait   = [&] () -> int {
             if (usWaited || !dpipe)
@@ -1243,6 +1407,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			e->regionVer[rp] = e->ctlVer;
 		}
 		e->dCtl.clear ();
+		e->dSeg.clear ();
 		e->dProg.clear ();
 		e->hRec.clear ();
 		e->hMsg.clear ();
@@ -1256,6 +1421,22 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		bool       delta = false;
 		uint32_t   len   = 0;
 		const auto hc0   = std::chrono::steady_clock::now ();
+		/* device control with many active instances: the chunk's host control on worker
+		 * threads (serial when a programme change is among the events) */
+		uint32_t evEnd = evi;
+		bool     progEv = false;
+		while (evEnd < nev && ev[evEnd].block < b0 + want) {
+			progEv = progEv || ev[evEnd].kind == TBF_EV_PROGRAM;
+			if (ev[evEnd].inst >= n)
+				return fail (-22, "event for a bad instance");
+			evEnd++;
+		}
+		if (e->devCtl && !progEv && e->parCtl && e->actList.size () >= 1024) {
+			if ((rc = stepChunkParallel (e, n, want, b0, ev, evi, evEnd, rp, delta)))
+				return rc;
+			evi = evEnd;
+			len = want;
+		}
 		for (; len < want; len++) {
 			if (!e->devCtl && e->dProg.size () + (size_t)n * SLOT > dprogCap && len > 0)
 				break; /* delta program pool full: end the chunk here */
@@ -1292,8 +1473,8 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 						e->hRec.push_back (rec);
 					} else if (pc) {
 						c.prog_off = (uint32_t)(PERSIST (n) + e->dProg.size ());
-						e->dProg.insert (e->dProg.end (), e->hProg.begin () + 2 * i * SLOT,
-						                 e->hProg.begin () + 2 * i * SLOT + 1 + c.prog_len);
+						e->dProg.insert (e->dProg.end (), e->hProg.begin () + PSLOTS * i * SLOT,
+						                 e->hProg.begin () + PSLOTS * i * SLOT + 1 + c.prog_len);
 					} else if (cur[i] >= n)
 						c.prog_off = e->dCtl[cur[i] - n].prog_off; /* program of the previous delta */
 					cur[i] = n + (uint32_t)e->dCtl.size ();
@@ -1333,8 +1514,13 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 				return rc;
 			if ((rc = usWait ()))
 				return rc;
-			HIPCHK (hipMemcpyAsync (e->ctl.p + rp * CTL_REGION (n) + n, e->dCtl.data (),
-			                        e->dCtl.size () * sizeof (tbf_seg_ctl), hipMemcpyHostToDevice, us));
+			if (e->dSeg.empty ())
+				HIPCHK (hipMemcpyAsync (e->ctl.p + rp * CTL_REGION (n) + n, e->dCtl.data (),
+				                        e->dCtl.size () * sizeof (tbf_seg_ctl), hipMemcpyHostToDevice, us));
+			for (const auto& g : e->dSeg) /* threaded host control: the workers' segments */
+				if (g.second)
+					HIPCHK (hipMemcpyAsync (e->ctl.p + rp * CTL_REGION (n) + n + g.first, e->dCtl.data () + g.first,
+					                        g.second * sizeof (tbf_seg_ctl), hipMemcpyHostToDevice, us));
 			if (!e->dProg.empty ())
 				HIPCHK (hipMemcpyAsync (e->prog.p + PERSIST (n), e->dProg.data (),
 				                        e->dProg.size () * sizeof (tbf_prog_entry), hipMemcpyHostToDevice, us));
@@ -1359,8 +1545,13 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			if (drec.ensure (e->hRec.size ()) || dmsg.ensure (std::max<size_t> (e->hMsg.size (), 1)) ||
 			    dci.ensure (e->hCtlInst.size ()))
 				return fail (-12, "out of device memory (control records)");
-			HIPCHK (hipMemcpyAsync (drec.p, e->hRec.data (), e->hRec.size () * sizeof (tbf_tgc_rec),
-			                        hipMemcpyHostToDevice, us));
+			if (e->dSeg.empty ())
+				HIPCHK (hipMemcpyAsync (drec.p, e->hRec.data (), e->hRec.size () * sizeof (tbf_tgc_rec),
+				                        hipMemcpyHostToDevice, us));
+			for (const auto& g : e->dSeg)
+				if (g.second)
+					HIPCHK (hipMemcpyAsync (drec.p + g.first, e->hRec.data () + g.first,
+					                        g.second * sizeof (tbf_tgc_rec), hipMemcpyHostToDevice, us));
 			if (!e->hMsg.empty ())
 				HIPCHK (hipMemcpyAsync (dmsg.p, e->hMsg.data (), e->hMsg.size () * sizeof (uint16_t),
 				                        hipMemcpyHostToDevice, us));
@@ -1395,6 +1586,8 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 					HIPCHK (hipEventRecord (e->sjoin, s));
 					HIPCHK (hipStreamWaitEvent (sk, e->sjoin, 0));
 				}
+				if (k == 0 && usWaited) /* this chunk's control uploads and k_tgctl */
+					HIPCHK (hipStreamWaitEvent (sk, e->upEv, 0));
 				if (k == nst - 1 && !outWait) { /* the output stage writes the caller's buffers */
 					HIPCHK (hipEventRecord (e->sjoin, s));
 					HIPCHK (hipStreamWaitEvent (sk, e->sjoin, 0));

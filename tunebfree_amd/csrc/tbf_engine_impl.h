@@ -206,12 +206,27 @@ struct tbf_engine {
 	PinnedVec<uint32_t>                     hCtlInstB, hIdxB;
 	hipEvent_t                              upEv = nullptr, upEvB = nullptr;
 	std::vector<uint8_t>                    stepped;  /* membership of hCtlInst */
-	std::vector<uint8_t>                    pslot;    /* persistent program slot (0/1) per instance */
+	std::vector<uint8_t>                    pslot;    /* persistent program slot (0..TBF_PROG_PSLOTS-1) per instance */
 	/* device control, pipelined delta chunks: the control pool (persistent entries +
 	 * deltas), the index table and the control records come in two regions by chunk
 	 * parity; region p's persistent entries are refreshed from hCtl when they are older
 	 * than its version (ctlVer counts the changes of hCtl) */
 	uint64_t                                ctlVer = 1, regionVer[2] = {0, 0};
+	bool                                    parCtl = true; /* TBF_HOST_SERIAL=1 steps serially */
+	/* threaded host control (stepChunkParallel): per worker, kept between chunks so the
+	 * buffers stay allocated; worker t writes its deltas straight into the staging at pool
+	 * position base_t = (first instance of its range) * blocks, and dSeg lists the filled
+	 * segments {base_t, count_t} that are uploaded (empty: the pool is [0, dCtl.size ())) */
+	struct alignas (128) ParStep { /* own cache lines: workers bump these per delta */
+		std::vector<uint16_t> msgs;
+		std::vector<uint32_t> act, ctlInst, evs;
+		std::vector<tbf_seg_ctl> sc; /* TBF_PAR_SCRATCH (experiment): deltas staged here first */
+		std::vector<tbf_tgc_rec> sr;
+		uint32_t              nd = 0;
+		int                   rc = 0;
+	};
+	std::vector<ParStep>                    parStep;
+	std::vector<std::pair<uint32_t, uint32_t>> dSeg;
 	DevBuf<tbf_tgc_rec>                     drecB;
 	DevBuf<uint16_t>                        dmsgB;
 	DevBuf<uint32_t>                        dctlInstB;
@@ -263,6 +278,7 @@ struct tbf_engine {
 	int                                     pipeMode = 1;
 	int                                     grp[5]   = {0, 1, 1, 2, 2};
 	hipStream_t                             gstr3    = nullptr; /* the third group's stream (groups 0, 1 use sstr) */
+	hipStream_t                             cstr     = nullptr; /* device control: uploads + k_tgctl */
 	hipEvent_t                              pdone[2][5] = {};
 	/* programme table (.pgm), src/program.h:26 MAXPROGS; pgm.controller.offset */
 	std::vector<Programme>                  progs = std::vector<Programme> (129);
@@ -275,11 +291,14 @@ struct tbf_engine {
 };
 
 namespace tbf {
+/* the calling thread's active list while renderImpl steps an instance range on a host
+ * worker thread (nullptr: the engine's own list) */
+extern thread_local std::vector<uint32_t>* tlAct;
 inline void markActive (tbf_engine* e, uint32_t i)
 {
 	if (i < e->inAct.size () && !e->inAct[i]) {
 		e->inAct[i] = 1;
-		e->actList.push_back (i);
+		(tlAct ? *tlAct : e->actList).push_back (i);
 	}
 }
 } // namespace tbf

@@ -146,12 +146,20 @@ struct TgControl {
 		int   refCount;
 		float sumUpper, sumLower, sumPedal, sumPercn, sumSwell, sumScanr;
 	};
-	const TgTemplate* tpl = nullptr;
-	Aot               aot[TBF_NW + 1];
-	int               activeOscList[TBF_NW + 1];
-	int               activeOscLEnd = 0;
-	int               aclPos[TBF_NW + 1];
-	uint16_t          rflags[TBF_NW + 1];
+	/* per-wheel state of the host control path (step).  The device path (stepFront) keeps
+	 * it in tbf_tgc_state instead, so it is allocated by the first step () only: an
+	 * instance's per-block fields then sit a few KB from the next instance's, not 70 KB
+	 * (host worker threads stepping thousands of instances are bound by that footprint) */
+	struct Wheels {
+		Aot      aot[TBF_NW + 1];
+		int      activeOscList[TBF_NW + 1];
+		int      activeOscLEnd = 0;
+		int      aclPos[TBF_NW + 1];
+		uint16_t rflags[TBF_NW + 1];
+		Wheels ();
+	};
+	const TgTemplate*     tpl = nullptr;
+	std::vector<Wheels>   wh; /* empty until step () */
 	std::vector<uint16_t> msg;
 	int               keyDownCount = 0;
 	unsigned          upperKeyCount = 0;
@@ -189,7 +197,7 @@ struct TgControl {
 	/* the same block with the per-wheel part left to the device (k_tgctl): the block's
 	 * key messages (msg.size () of them, written to msgDst = the chunk's message array
 	 * at msgOff) and drawbar / routing inputs in rec, the mixdown control in ctl.
-	 * aot / active list / rflags are not used. */
+	 * wh (aot / active list / rflags) is not used. */
 	void stepFront (uint16_t* msgDst, uint32_t msgOff, tbf_tgc_rec& rec, tbf_seg_ctl& ctl);
 	void mixCtl (tbf_seg_ctl& ctl) const;
 };

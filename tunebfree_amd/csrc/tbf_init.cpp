@@ -693,11 +693,6 @@ void TgControl::init (const TgTemplate* t, const Config& c)
 	percEnvGainResetNorm = c.percEnvGainResetNorm;
 	percEnvGainResetSoft = c.percEnvGainResetSoft;
 	percEnvScaling       = c.percEnvScaling;
-	memset (aot, 0, sizeof (aot));
-	for (int i = 0; i <= TBF_NW; i++) {
-		aclPos[i] = -1;
-		rflags[i] = 0;
-	}
 	memset (activeKeys, 0, sizeof (activeKeys));
 	memset (drawBarGain, 0, sizeof (drawBarGain));
 	for (int i = 0; i < 27; i++)
@@ -822,8 +817,25 @@ bool TgControl::dirty () const
 /* src/tonegen.cpp:3250-3594: message queue, active list + program emission, removal.
  * The wrap split of each instruction (3376-3402, 3524-3555) is applied on the device
  * from the wheel position it tracks. */
+TgControl::Wheels::Wheels ()
+{
+	memset (aot, 0, sizeof (aot));
+	for (int i = 0; i <= TBF_NW; i++) {
+		aclPos[i] = -1;
+		rflags[i] = 0;
+	}
+}
+
 void TgControl::step (std::vector<tbf_prog_entry>& prog, tbf_seg_ctl& ctl)
 {
+	if (wh.empty ())
+		wh.resize (1);
+	Wheels&   W             = wh[0];
+	Aot*      aot           = W.aot;
+	int*      activeOscList = W.activeOscList;
+	int&      activeOscLEnd = W.activeOscLEnd;
+	int*      aclPos        = W.aclPos;
+	uint16_t* rflags        = W.rflags;
 	prog.clear ();
 	int      removed[TBF_NW + 1];
 	int      removedEnd = 0;

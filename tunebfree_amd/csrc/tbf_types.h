@@ -32,6 +32,10 @@ typedef struct tbf_prog_entry {
 /* A program slot is a header entry (wheel = 0xFFFF, pad = entry count) followed by the
  * entries; seg_ctl.prog_off indexes the header.  TBF_PROG_SLOT entries per slot. */
 #define TBF_PROG_SLOT (TBF_NW + 2)
+/* persistent program slots per instance (device control): k_tgctl of chunk c writes the
+ * instance's final program into the slot after the current one (mod 3), which neither
+ * chunk c nor chunk c - 1 renders from, so it may run beside chunk c - 1's k_tonegen */
+#define TBF_PROG_PSLOTS 3
 
 /* device-side tone-generator control (k_tgctl): the per-wheel part
  * of oscGenerateFragment's control (src/tonegen.cpp:3257-3594: the message queue's

@@ -10,6 +10,7 @@ chord)?  One step = one tbf_render_events call of 64 blocks; modes:
   params   each instance moves a drawbar on every block (no key change)
 
 For each: wall ms/step (HIP-synchronized), host control ms/step (tbf_debug_host_time),
+time inside the tbf_render_events calls per step (host control + enqueueing + any wait),
 events/step.  Writes JSON to --out.
 """
 from __future__ import annotations
@@ -90,14 +91,18 @@ def main():
         eng.synchronize()
         eng.host_time(reset=True)
         t0 = time.perf_counter()
+        sub = 0.0
         for s in range(a.warmup, a.warmup + a.steps):
+            ts = time.perf_counter()
             eng.render_events_device(nb, evs[s], outL.data_ptr(), outR.data_ptr(), nsamp, sptr)
+            sub += time.perf_counter() - ts
         torch.cuda.synchronize()
         eng.synchronize()
         dt = (time.perf_counter() - t0) / a.steps
         hms, hblk = eng.host_time(reset=True)
         row = {"mode": mode, "instances": B, "blocks_per_step": nb, "events_per_step": int(len(evs[-1])),
                "ms_per_step": dt * 1e3, "host_control_ms_per_step": hms / a.steps,
+               "call_ms_per_step": sub / a.steps * 1e3,
                "host_share": hms / a.steps / (dt * 1e3), "stereo_samples_per_s": B * nsamp / dt}
         rows.append(row)
         print(json.dumps(row), flush=True)

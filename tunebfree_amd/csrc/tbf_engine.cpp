@@ -1119,18 +1119,13 @@ static int stepChunkParallel (tbf_engine* e, uint32_t n, uint32_t want, uint32_t
 	std::vector<uint32_t>& cur = e->curIdx;
 	const auto             ph0 = std::chrono::steady_clock::now ();
 	std::vector<uint64_t>  thNs (T);
-	const bool scratch = getenv ("TBF_PAR_SCRATCH") != nullptr;
 	parallelFor (T, [&] (uint32_t t) {
 		const auto           th0  = std::chrono::steady_clock::now ();
 		tbf_engine::ParStep& o    = out[t];
 		const uint32_t       i0   = t * per, i1 = std::min (n, i0 + per);
 		const uint32_t       base = i0 * want;
-		if (scratch) {
-			o.sc.resize ((size_t)(i1 - i0) * want);
-			o.sr.resize ((size_t)(i1 - i0) * want);
-		}
-		tbf_seg_ctl* Cc = scratch ? o.sc.data () : e->dCtl.data () + base;
-		tbf_tgc_rec* Rr = scratch ? o.sr.data () : e->hRec.data () + base;
+		tbf_seg_ctl*         Cc   = e->dCtl.data () + base; /* the worker's part of the staging */
+		tbf_tgc_rec*         Rr   = e->hRec.data () + base;
 		tlAct                     = &o.act;
 		size_t ep                 = 0;
 		for (uint32_t i = i0; i < i1; i++)
@@ -1191,14 +1186,10 @@ static int stepChunkParallel (tbf_engine* e, uint32_t n, uint32_t want, uint32_t
 	if (e->dSeg.empty ())
 		e->dSeg.push_back ({0, 0});
 	e->hMsg.resize (nm);
-	if (nm || scratch)
+	if (nm)
 		parallelFor (T, [&] (uint32_t t) { /* message offsets: worker-local -> chunk */
 			const tbf_engine::ParStep& o    = out[t];
 			const size_t               base = (size_t)t * per * want;
-			if (scratch && o.nd) {
-				memcpy ((void*)(e->dCtl.data () + base), o.sc.data (), o.nd * sizeof (tbf_seg_ctl));
-				memcpy ((void*)(e->hRec.data () + base), o.sr.data (), o.nd * sizeof (tbf_tgc_rec));
-			}
 			for (size_t d = base; d < base + o.nd; d++)
 				if (e->hRec[d].flags & 0x80)
 					e->hRec[d].msgOff += (uint32_t)mb[t];
@@ -1391,7 +1382,11 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			e->hIdx.swap (e->hIdxB);
 			e->hCtlPin.swap (e->hCtlPinB);
 			std::swap (e->upEv, e->upEvB);
+			const auto w0 = std::chrono::steady_clock::now ();
 			HIPCHK (hipEventSynchronize (e->upEv));
+			if (getenv ("TBF_DEBUG_HOST_PHASES"))
+				fprintf (stderr, "chunk %llu: staging wait %.3f ms\n", (unsigned long long)e->chunkSeq,
+				         std::chrono::duration<double, std::milli> (std::chrono::steady_clock::now () - w0).count ());
 		}
 		if (e->devCtl && e->regionVer[rp] != e->ctlVer) {
 			/* this region's persistent entries: the control as of the START of this chunk (an
@@ -1541,7 +1536,11 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			DevBuf<uint16_t>&    dmsg = rp ? e->dmsgB : e->dmsg;
 			DevBuf<uint32_t>&    dci  = rp ? e->dctlInstB : e->dctlInst;
 			if (drec.cap < e->hRec.size () || dmsg.cap < e->hMsg.size () || dci.cap < e->hCtlInst.size ())
+			{
+				if (getenv ("TBF_DEBUG_HOST_PHASES"))
+					fprintf (stderr, "chunk %llu: control record buffers grow (device sync)\n", (unsigned long long)e->chunkSeq);
 				HIPCHK (hipDeviceSynchronize ()); /* growing: nothing may still read the old buffers */
+			}
 			if (drec.ensure (e->hRec.size ()) || dmsg.ensure (std::max<size_t> (e->hMsg.size (), 1)) ||
 			    dci.ensure (e->hCtlInst.size ()))
 				return fail (-12, "out of device memory (control records)");

@@ -220,8 +220,6 @@ struct tbf_engine {
 	struct alignas (128) ParStep { /* own cache lines: workers bump these per delta */
 		std::vector<uint16_t> msgs;
 		std::vector<uint32_t> act, ctlInst, evs;
-		std::vector<tbf_seg_ctl> sc; /* TBF_PAR_SCRATCH (experiment): deltas staged here first */
-		std::vector<tbf_tgc_rec> sr;
 		uint32_t              nd = 0;
 		int                   rc = 0;
 	};

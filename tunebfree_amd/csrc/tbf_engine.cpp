@@ -315,7 +315,14 @@ int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
 		}
 		if (e->pipeMode == 1) {
 			HIPCHK (hipStreamCreateWithFlags (&e->gstr3, hipStreamNonBlocking));
-			HIPCHK (hipStreamCreateWithFlags (&e->cstr, hipStreamNonBlocking));
+			/* TBF_CTL_STREAM=1: a delta chunk's uploads and k_tgctl on a stream of their own.
+			 * Off by default: the process has GPU_MAX_HW_QUEUES (4) hardware queues, streams
+			 * take them round-robin at creation, and a fifth engine stream pushes the caller's
+			 * stream onto the first stage group's queue, which serializes the stages (steady
+			 * bench 6.7 -> 8.1 ms per step); the dense-event step gained nothing from it */
+			const char* cs = getenv ("TBF_CTL_STREAM");
+			if (cs && cs[0] == '1')
+				HIPCHK (hipStreamCreateWithFlags (&e->cstr, hipStreamNonBlocking));
 			for (int p = 0; p < 2; p++)
 				for (int k = 0; k < TBF_NSTAGES; k++)
 					HIPCHK (hipEventCreateWithFlags (&e->pdone[p][k], hipEventDisableTiming));
@@ -1337,12 +1344,13 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		const bool     par  = (e->chunkSeq++ & 1) != 0;
 		const int      rp   = e->devCtl ? (int)par : 0; /* control region of this chunk */
 		/* device control, stage-group pipelining: a delta chunk pipelines like any other; its
-		 * uploads and k_tgctl go on the control stream cstr after the chunk before last (the
-		 * previous user of this region) has finished every stage, so they overlap the
-		 * previous chunk's k_tonegen (three persistent program slots make that exact); the
-		 * chunk's first stage waits for them (upEv) */
+		 * uploads and k_tgctl go on the first stage group's stream (or the control stream
+		 * cstr, TBF_CTL_STREAM=1, where they overlap the previous chunk's k_tonegen: three
+		 * persistent program slots make that exact, and the chunk's first stage waits for
+		 * them, upEv) after the chunk before last (the previous user of this region) has
+		 * finished every stage */
 		const bool     dpipe = e->devCtl && pipe && e->pipeMode == 1;
-		hipStream_t    us    = dpipe ? e->cstr : s;
+		hipStream_t    us    = dpipe ? (e->cstr ? e->cstr : e->sstr[e->grp[0] < 2 ? e->grp[0] : 0]) : s;
 		bool           usWaited = false;
 		auto           usWait   = [&] () -> int {
             if (usWaited || !dpipe)
@@ -1585,7 +1593,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 					HIPCHK (hipEventRecord (e->sjoin, s));
 					HIPCHK (hipStreamWaitEvent (sk, e->sjoin, 0));
 				}
-				if (k == 0 && usWaited) /* this chunk's control uploads and k_tgctl */
+				if (k == 0 && usWaited && e->cstr) /* this chunk's control uploads and k_tgctl */
 					HIPCHK (hipStreamWaitEvent (sk, e->upEv, 0));
 				if (k == nst - 1 && !outWait) { /* the output stage writes the caller's buffers */
 					HIPCHK (hipEventRecord (e->sjoin, s));

@@ -97,7 +97,8 @@
 
 /* timing-only ablations (wrong results; tools/gpu_ab.sh variants): bit 0 waveshaper sin,
  * 1 vibrato gather, 2 tonegen serial chains, 3 overdrive dither jumps, 4 whirl ring
- * accumulation, 5 whirl serial filters, 6 whirl motion table loads */
+ * accumulation, 5 whirl serial filters, 6 whirl motion table loads, 7 reverb biquad
+ * chains */
 #ifndef TBF_ABL
 #define TBF_ABL 0
 #endif
@@ -747,6 +748,9 @@ k_tonegen (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl, const tbf_tp
  * channel over 64 samples of an LDS row, in place; st7/st8 = the channel's state pair */
 __device__ __forceinline__ void rv_chain (const double* cf, double& st7, double& st8, double* row)
 {
+#if TBF_ABL & 128
+	return; /* ablation (timing only): the reverb's serial biquad chains skipped */
+#endif
 	const double c0 = cf[0], c1 = cf[1], c2 = cf[2], c3 = cf[3], c4 = cf[4];
 	double       s7 = st7, s8 = st8;
 	for (int i0 = 0; i0 < TBF_SUB; i0 += 8) {
@@ -1339,7 +1343,7 @@ k_rv_out (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 		TBF_MARK (10);
 		/* (b) serial: B over block it (q = 0), C over block it-1 (q = 1) */
 		PRIO_UP ();
-		if (lane < 4 * nj && (q == 0 ? haveB : haveC)) {
+		if (!(TBF_ABL & 128) && lane < 4 * nj && (q == 0 ? haveB : haveC)) {
 			tbf_rv_state& ss  = sm.hd[sj].get ();
 			double*       row = q == 0 ? sm.bx[sj][c] : sm.cx[sj][c];
 			double        s7 = ss.bq[1 + q][2 * c], s8 = ss.bq[1 + q][2 * c + 1];

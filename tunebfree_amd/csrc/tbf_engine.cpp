@@ -295,8 +295,17 @@ int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
 	if (cfg->device >= 0) {
 		HIPCHK (hipSetDevice (cfg->device));
 		HIPCHK (hipStreamCreateWithFlags (&e->stream, hipStreamNonBlocking));
+		/* TBF_STREAM_PRIO=k: the stream of stage group k (0..2) at the device's greatest
+		 * priority (A/B of which stage group the dispatcher should favour) */
+		const char* sp    = getenv ("TBF_STREAM_PRIO");
+		const int   spGrp = sp ? atoi (sp) : -1;
+		int         prLeast = 0, prGreatest = 0;
+		HIPCHK (hipDeviceGetStreamPriorityRange (&prLeast, &prGreatest));
 		for (int p = 0; p < 2; p++)
-			HIPCHK (hipStreamCreateWithFlags (&e->sstr[p], hipStreamNonBlocking));
+			if (p == spGrp)
+				HIPCHK (hipStreamCreateWithPriority (&e->sstr[p], hipStreamNonBlocking, prGreatest));
+			else
+				HIPCHK (hipStreamCreateWithFlags (&e->sstr[p], hipStreamNonBlocking));
 		for (int k = 0; k < TBF_NSTAGES; k++)
 			HIPCHK (hipEventCreateWithFlags (&e->sdone[k], hipEventDisableTiming));
 		HIPCHK (hipEventCreateWithFlags (&e->sjoin, hipEventDisableTiming));
@@ -314,7 +323,10 @@ int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
 			}
 		}
 		if (e->pipeMode == 1) {
-			HIPCHK (hipStreamCreateWithFlags (&e->gstr3, hipStreamNonBlocking));
+			if (spGrp == 2)
+				HIPCHK (hipStreamCreateWithPriority (&e->gstr3, hipStreamNonBlocking, prGreatest));
+			else
+				HIPCHK (hipStreamCreateWithFlags (&e->gstr3, hipStreamNonBlocking));
 			/* TBF_CTL_STREAM=1: a delta chunk's uploads and k_tgctl on a stream of their own.
 			 * Off by default: the process has GPU_MAX_HW_QUEUES (4) hardware queues, streams
 			 * take them round-robin at creation, and a fifth engine stream pushes the caller's
@@ -323,9 +335,13 @@ int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
 			const char* cs = getenv ("TBF_CTL_STREAM");
 			if (cs && cs[0] == '1')
 				HIPCHK (hipStreamCreateWithFlags (&e->cstr, hipStreamNonBlocking));
-			for (int p = 0; p < 2; p++)
+			for (int p = 0; p < 6; p++)
 				for (int k = 0; k < TBF_NSTAGES; k++)
-					HIPCHK (hipEventCreateWithFlags (&e->pdone[p][k], hipEventDisableTiming));
+					HIPCHK (hipEventCreateWithFlags (&e->pev[p][k], hipEventDisableTiming));
+			/* TBF_STAGE_BUFS=3: a third stage-buffer set, so k_tonegen of chunk c waits for
+			 * chunk c - 3's readers of mid1 instead of chunk c - 2's */
+			const char* sb = getenv ("TBF_STAGE_BUFS");
+			e->nbuf        = (sb && atoi (sb) == 3) ? 3 : 2;
 		}
 		HIPCHK (hipEventCreateWithFlags (&e->upEv, hipEventDisableTiming));
 		HIPCHK (hipEventCreateWithFlags (&e->upEvB, hipEventDisableTiming));
@@ -412,10 +428,10 @@ int tbf_engine_destroy (tbf_engine* e)
 		(void)hipStreamDestroy (e->gstr3);
 	if (e->cstr)
 		(void)hipStreamDestroy (e->cstr);
-	for (int p = 0; p < 2; p++)
+	for (int p = 0; p < 6; p++)
 		for (int k = 0; k < TBF_NSTAGES; k++)
-			if (e->pdone[p][k])
-				(void)hipEventDestroy (e->pdone[p][k]);
+			if (e->pev[p][k])
+				(void)hipEventDestroy (e->pev[p][k]);
 	for (int k = 0; k < TBF_NSTAGES; k++)
 		if (e->sdone[k])
 			(void)hipEventDestroy (e->sdone[k]);
@@ -1285,12 +1301,15 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 	P.errFlags  = e->err.p;
 	P.dbg       = e->cfg.debug_flags;
 	P.prof      = e->profOn ? e->prof.p : nullptr;
-	/* inter-stage buffers: two parities (alternate chunks), see the pipelining below */
-	const size_t need = (size_t)n * TBF_CHUNK * TBF_BLK;
+	/* inter-stage buffers: nbuf sets by chunk index (2: alternate chunks; 3 with the
+	 * stage-group streams), see the pipelining below */
+	const size_t   need = (size_t)n * TBF_CHUNK * TBF_BLK;
+	const uint32_t nbuf = e->nbuf;
 	if (e->cfg.chain_mode != TBF_CHAIN_TONEGEN) {
-		if (e->mid1.ensure (2 * need) || e->mid2.ensure (2 * need))
+		if (e->mid1.ensure (nbuf * need) || e->mid2.ensure (nbuf * need))
 			return fail (-12, "out of device memory (stage buffers)");
-		if (e->cfg.chain_mode != TBF_CHAIN_TAP_PREAMP && (e->rvA.ensure (4 * need) || e->rvB.ensure (4 * need)))
+		if (e->cfg.chain_mode != TBF_CHAIN_TAP_PREAMP &&
+		    (e->rvA.ensure (2 * nbuf * need) || e->rvB.ensure (2 * nbuf * need)))
 			return fail (-12, "out of device memory (reverb stage buffers)");
 	}
 	P.midStride = (uint64_t)TBF_CHUNK * TBF_BLK;
@@ -1341,7 +1360,9 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		/* host control for the chunk, block by block: entry indices per (block, instance),
 		 * new pool entries only where an instance's control changes */
 		const uint32_t want = std::min<uint32_t> (TBF_CHUNK, nblocks - b0);
-		const bool     par  = (e->chunkSeq++ & 1) != 0;
+		const uint64_t cix  = e->chunkSeq++;
+		const bool     par  = (cix & 1) != 0;
+		const uint32_t bset = (uint32_t)(cix % nbuf); /* stage-buffer set of this chunk */
 		const int      rp   = e->devCtl ? (int)par : 0; /* control region of this chunk */
 		/* device control, stage-group pipelining: a delta chunk pipelines like any other; its
 		 * uploads and k_tgctl go on the first stage group's stream (or the control stream
@@ -1360,7 +1381,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
                 HIPCHK (hipEventRecord (e->sjoin, s));
                 HIPCHK (hipStreamWaitEvent (us, e->sjoin, 0));
             }
-            HIPCHK (hipStreamWaitEvent (us, e->pdone[par][tbf_chain_stages (P.chain) - 1], 0));
+            HIPCHK (hipStreamWaitEvent (us, e->pev[(cix + 4) % 6][tbf_chain_stages (P.chain) - 1], 0));
             return 0;
 		};
 		if (e->devCtl && e->persistStale) {
@@ -1504,10 +1525,10 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		                    .count ();
 		e->hostCtlBlocks += len;
 		const bool     piped   = pipe && (!delta || dpipe);
-		P.mid1 = e->mid1.p ? e->mid1.p + (par ? need : 0) : nullptr;
-		P.mid2 = e->mid2.p ? e->mid2.p + (par ? need : 0) : nullptr;
-		P.rvA  = e->rvA.p ? e->rvA.p + (par ? 2 * need : 0) : nullptr;
-		P.rvB  = e->rvB.p ? e->rvB.p + (par ? 2 * need : 0) : nullptr;
+		P.mid1 = e->mid1.p ? e->mid1.p + bset * need : nullptr;
+		P.mid2 = e->mid2.p ? e->mid2.p + bset * need : nullptr;
+		P.rvA  = e->rvA.p ? e->rvA.p + 2 * bset * need : nullptr;
+		P.rvB  = e->rvB.p ? e->rvB.p + 2 * bset * need : nullptr;
 		if (!piped && (rc = joinStages (e, s)))
 			return rc;
 		if (delta) {
@@ -1604,7 +1625,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 					HIPCHK (hipStreamWaitEvent (sk, e->sdone[k - 1], 0));
 				for (int r : readers[k])
 					if (r >= 0 && r < nst && strm (r) != sk)
-						HIPCHK (hipStreamWaitEvent (sk, e->pdone[par][r], 0));
+						HIPCHK (hipStreamWaitEvent (sk, e->pev[(cix + 6 - nbuf) % 6][r], 0));
 				hipEvent_t e0 = nullptr, e1 = nullptr;
 				if (e->timeOn) {
 					HIPCHK (hipEventCreate (&e0));
@@ -1619,7 +1640,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 					e->tev.push_back ({k, {e0, e1}});
 				}
 				HIPCHK (hipEventRecord (e->sdone[k], sk));
-				HIPCHK (hipEventRecord (e->pdone[par][k], sk));
+				HIPCHK (hipEventRecord (e->pev[cix % 6][k], sk));
 			}
 			e->stagesBusy = true;
 			if (delta && (rc = endDelta ()))

@@ -277,7 +277,11 @@ struct tbf_engine {
 	int                                     grp[5]   = {0, 1, 1, 2, 2};
 	hipStream_t                             gstr3    = nullptr; /* the third group's stream (groups 0, 1 use sstr) */
 	hipStream_t                             cstr     = nullptr; /* device control: uploads + k_tgctl */
-	hipEvent_t                              pdone[2][5] = {};
+	/* stage-group pipelining: each chunk's stage-k event, in a ring by chunk index (a chunk
+	 * waits on chunk c - nbuf's readers of the stage buffers it overwrites and on chunk
+	 * c - 2's last stage for its control region); nbuf stage-buffer sets by chunk index */
+	hipEvent_t                              pev[6][5] = {};
+	uint32_t                                nbuf      = 2;
 	/* programme table (.pgm), src/program.h:26 MAXPROGS; pgm.controller.offset */
 	std::vector<Programme>                  progs = std::vector<Programme> (129);
 	int                                     pgmOffset = 1;

@@ -68,6 +68,9 @@
 #endif
 #ifndef WH_PRIO
 #define WH_PRIO 0 /* the same for k_whirl's filter pass (measured slightly slower: 4.47-4.50 vs 4.52e9) */
+#ifndef RV_CORE_PRIO
+#define RV_CORE_PRIO 0 /* wave priority of k_rv_core for its whole run (the pipelined step's critical stream) */
+#endif
 #endif
 #define PRIO_UP()                                  \
 	do {                                           \
@@ -1130,6 +1133,8 @@ k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 	const int      c    = blockIdx.x & 1;
 	if (inst >= P.nInst)
 		return;
+	if (RV_CORE_PRIO)
+		__builtin_amdgcn_s_setprio (RV_CORE_PRIO);
 	const tbf_inst_const& K    = cst[inst];
 	tbf_rv_chan*          S    = &P.st[inst].rv.ch[c];
 #ifdef RV_ABL_MEM /* ablation (timing only, wrong results): 64 slabs shared, MALL-resident */

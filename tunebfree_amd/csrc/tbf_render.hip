@@ -823,6 +823,9 @@ struct RvOutLds {
 	TBF_PROF_LDS
 };
 
+#ifndef RV_LDS_PAD
+#define RV_LDS_PAD 0
+#endif
 #define RV_WIN 72 /* tap window per line: 64 samples + max offset 2 * vibDepth (5.4) + 2 */
 
 struct RvCoreLds {
@@ -831,6 +834,9 @@ struct RvCoreLds {
 	double      sd[8][TBF_SUB];  /* sin ((n+1) D) of each line's closed-form step D ... */
 	double      cm[8][TBF_SUB];  /* ... and 1 - cos ((n+1) D) = 2 sin^2 ((n+1) D / 2) */
 	double      tabD[8];         /* the D the rows above hold (-1: none yet) */
+#if RV_LDS_PAD
+	double      pad[RV_LDS_PAD / 8]; /* A/B: fewer resident waves (their rings then fit in MALL) */
+#endif
 	TBF_PROF_LDS
 };
 

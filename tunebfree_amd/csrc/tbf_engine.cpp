@@ -1455,7 +1455,8 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 				return fail (-22, "event for a bad instance");
 			evEnd++;
 		}
-		if (e->devCtl && !progEv && e->parCtl && e->actList.size () >= 1024) {
+		/* many instances to step: active now, or touched by this chunk's events */
+		if (e->devCtl && !progEv && e->parCtl && e->actList.size () + (evEnd - evi) >= 1024) {
 			if ((rc = stepChunkParallel (e, n, want, b0, ev, evi, evEnd, rp, delta)))
 				return rc;
 			evi = evEnd;

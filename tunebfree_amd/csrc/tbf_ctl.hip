@@ -252,6 +252,8 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_tgctl (
 	}
 	if (lane == 0)
 		sm.L = G->listEnd;
+	if (lane < 27)
+		sm.dbg[lane] = G->gain[lane];
 	__syncthreads ();
 	const uint32_t n    = P.nInst;
 	uint32_t       prev = inst;
@@ -264,8 +266,8 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_tgctl (
 		const tbf_tgc_rec& R = P.rec[idx - n];
 		if (!(R.flags & 0x80))
 			continue; /* a control change without a tone-generator step */
-		if (lane < 27)
-			sm.dbg[lane] = R.drawBarGain[lane];
+		if ((R.flags & 4) && lane < 27)
+			sm.dbg[lane] = P.gains[R.gainOff + lane];
 		__syncthreads ();
 		for (uint32_t m = 0; m < R.nMsg; m++) {
 			const uint32_t msg = P.msgs[R.msgOff + m];
@@ -300,6 +302,8 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_tgctl (
 	}
 	if (lane == 0)
 		G->listEnd = sm.L;
+	if (lane < 27)
+		G->gain[lane] = sm.dbg[lane];
 }
 
 extern "C" int tbf_launch_tgctl (const tbf_launch* P, hipStream_t stream)

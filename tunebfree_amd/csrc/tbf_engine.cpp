@@ -405,6 +405,8 @@ int tbf_engine_destroy (tbf_engine* e)
 	e->dctlInst.release ();
 	e->drecB.release ();
 	e->dmsgB.release ();
+	e->dgain.release ();
+	e->dgainB.release ();
 	e->dctlInstB.release ();
 	e->coff.release ();
 	e->contrib.release ();
@@ -1047,7 +1049,7 @@ static int applyEvent (tbf_engine* e, const tbf_event& ev)
  * the instance's current control e->hCtl[i] / program e->hProg; returns true when the
  * control the next block renders with changed. */
 static bool stepControl (tbf_engine* e, uint32_t i, bool& progChanged, tbf_tgc_rec* rec = nullptr,
-                         std::vector<uint16_t>* msgOut = nullptr)
+                         std::vector<uint16_t>* msgOut = nullptr, std::vector<float>* gainOut = nullptr)
 {
 	Instance&    in      = e->inst[i];
 	tbf_seg_ctl& c       = e->hCtl[i];
@@ -1057,15 +1059,18 @@ static bool stepControl (tbf_engine* e, uint32_t i, bool& progChanged, tbf_tgc_r
 		return false;
 	if (tgDirty && rec) {
 		/* device control: the front end here, the per-wheel part in k_tgctl */
-		const size_t k = std::min<size_t> (in.tg.msg.size (), 0xFFFF);
-		if (msgOut) { /* a host worker's own message list (renderImpl merges them) */
-			const uint32_t at = (uint32_t)msgOut->size ();
+		const size_t k  = std::min<size_t> (in.tg.msg.size (), 0xFFFF);
+		const size_t kg = in.tg.gainsDue () ? 27 : 0; /* the drawbar gains, when they changed */
+		if (msgOut) { /* a host worker's own message and gain lists (renderImpl merges them) */
+			const uint32_t at = (uint32_t)msgOut->size (), ag = (uint32_t)gainOut->size ();
 			msgOut->resize (at + k);
-			in.tg.stepFront (msgOut->data () + at, at, *rec, c);
+			gainOut->resize (ag + kg);
+			in.tg.stepFront (msgOut->data () + at, at, gainOut->data () + ag, ag, *rec, c);
 		} else {
-			const uint32_t at = (uint32_t)e->hMsg.size ();
+			const uint32_t at = (uint32_t)e->hMsg.size (), ag = (uint32_t)e->hGain.size ();
 			e->hMsg.resize (at + k);
-			in.tg.stepFront (e->hMsg.data () + at, at, *rec, c);
+			e->hGain.resize (ag + kg);
+			in.tg.stepFront (e->hMsg.data () + at, at, e->hGain.data () + ag, ag, *rec, c);
 		}
 		in.progDirty = false;
 		in.ctlDirty  = true;
@@ -1127,6 +1132,7 @@ static int stepChunkParallel (tbf_engine* e, uint32_t n, uint32_t want, uint32_t
 	out.resize (T);
 	for (auto& o : out) {
 		o.msgs.clear ();
+		o.gains.clear ();
 		o.act.clear ();
 		o.ctlInst.clear ();
 		o.evs.clear ();
@@ -1164,7 +1170,7 @@ static int stepChunkParallel (tbf_engine* e, uint32_t n, uint32_t want, uint32_t
 				const uint32_t i = o.act[a];
 				bool           pc;
 				tbf_tgc_rec&   rec = Rr[o.nd];
-				if (stepControl (e, i, pc, &rec, &o.msgs)) {
+				if (stepControl (e, i, pc, &rec, &o.msgs, &o.gains)) {
 					const uint32_t d = base + o.nd;
 					tbf_seg_ctl&   c = Cc[o.nd++];
 					c                = e->hCtl[i];
@@ -1193,14 +1199,16 @@ static int stepChunkParallel (tbf_engine* e, uint32_t n, uint32_t want, uint32_t
 		thNs[t] = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds> (std::chrono::steady_clock::now () - th0).count ();
 	});
 	const auto ph1 = std::chrono::steady_clock::now ();
-	std::vector<size_t> mb (T);
-	size_t              nm = 0;
+	std::vector<size_t> mb (T), gb (T);
+	size_t              nm = 0, ng = 0;
 	e->dSeg.clear ();
 	for (unsigned t = 0; t < T; t++) {
 		if (out[t].rc)
 			return out[t].rc;
 		mb[t] = nm;
 		nm += out[t].msgs.size ();
+		gb[t] = ng;
+		ng += out[t].gains.size ();
 		if (out[t].nd) {
 			e->dSeg.push_back ({t * per * want, out[t].nd});
 			delta = true;
@@ -1209,15 +1217,22 @@ static int stepChunkParallel (tbf_engine* e, uint32_t n, uint32_t want, uint32_t
 	if (e->dSeg.empty ())
 		e->dSeg.push_back ({0, 0});
 	e->hMsg.resize (nm);
-	if (nm)
-		parallelFor (T, [&] (uint32_t t) { /* message offsets: worker-local -> chunk */
+	e->hGain.resize (ng);
+	if (nm || ng)
+		parallelFor (T, [&] (uint32_t t) { /* message and gain offsets: worker-local -> chunk */
 			const tbf_engine::ParStep& o    = out[t];
 			const size_t               base = (size_t)t * per * want;
-			for (size_t d = base; d < base + o.nd; d++)
-				if (e->hRec[d].flags & 0x80)
-					e->hRec[d].msgOff += (uint32_t)mb[t];
+			for (size_t d = base; d < base + o.nd; d++) {
+				tbf_tgc_rec& r = e->hRec[d];
+				if (r.flags & 0x80)
+					r.msgOff += (uint32_t)mb[t];
+				if (r.flags & 4)
+					r.gainOff += (uint32_t)gb[t];
+			}
 			if (!o.msgs.empty ())
 				memcpy (e->hMsg.data () + mb[t], o.msgs.data (), o.msgs.size () * sizeof (uint16_t));
+			if (!o.gains.empty ())
+				memcpy (e->hGain.data () + gb[t], o.gains.data (), o.gains.size () * sizeof (float));
 		});
 	e->actList.clear ();
 	for (unsigned t = 0; t < T; t++) {
@@ -1407,6 +1422,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			e->dCtl.swap (e->dCtlB);
 			e->hRec.swap (e->hRecB);
 			e->hMsg.swap (e->hMsgB);
+			e->hGain.swap (e->hGainB);
 			e->hCtlInst.swap (e->hCtlInstB);
 			e->hIdx.swap (e->hIdxB);
 			e->hCtlPin.swap (e->hCtlPinB);
@@ -1435,6 +1451,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		e->dProg.clear ();
 		e->hRec.clear ();
 		e->hMsg.clear ();
+		e->hGain.clear ();
 		e->hCtlInst.clear ();
 		e->stepped.assign (n, 0);
 		e->hIdx.resize ((size_t)want * n);
@@ -1564,14 +1581,17 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			 * the caller's stream when not pipelined) read the other set */
 			DevBuf<tbf_tgc_rec>& drec = rp ? e->drecB : e->drec;
 			DevBuf<uint16_t>&    dmsg = rp ? e->dmsgB : e->dmsg;
+			DevBuf<float>&       dgn  = rp ? e->dgainB : e->dgain;
 			DevBuf<uint32_t>&    dci  = rp ? e->dctlInstB : e->dctlInst;
-			if (drec.cap < e->hRec.size () || dmsg.cap < e->hMsg.size () || dci.cap < e->hCtlInst.size ())
+			if (drec.cap < e->hRec.size () || dmsg.cap < e->hMsg.size () || dci.cap < e->hCtlInst.size () ||
+			    dgn.cap < e->hGain.size ())
 			{
 				if (getenv ("TBF_DEBUG_HOST_PHASES"))
 					fprintf (stderr, "chunk %llu: control record buffers grow (device sync)\n", (unsigned long long)e->chunkSeq);
 				HIPCHK (hipDeviceSynchronize ()); /* growing: nothing may still read the old buffers */
 			}
 			if (drec.ensure (e->hRec.size ()) || dmsg.ensure (std::max<size_t> (e->hMsg.size (), 1)) ||
+			    dgn.ensure (std::max<size_t> (e->hGain.size (), 27)) ||
 			    dci.ensure (e->hCtlInst.size ()))
 				return fail (-12, "out of device memory (control records)");
 			if (e->dSeg.empty ())
@@ -1584,10 +1604,14 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			if (!e->hMsg.empty ())
 				HIPCHK (hipMemcpyAsync (dmsg.p, e->hMsg.data (), e->hMsg.size () * sizeof (uint16_t),
 				                        hipMemcpyHostToDevice, us));
+			if (!e->hGain.empty ())
+				HIPCHK (hipMemcpyAsync (dgn.p, e->hGain.data (), e->hGain.size () * sizeof (float),
+				                        hipMemcpyHostToDevice, us));
 			HIPCHK (hipMemcpyAsync (dci.p, e->hCtlInst.data (), e->hCtlInst.size () * 4, hipMemcpyHostToDevice, us));
 			P.tgc      = e->tgc.p;
 			P.rec      = drec.p;
 			P.msgs     = dmsg.p;
+			P.gains    = dgn.p;
 			P.ctlInst  = dci.p;
 			P.nCtlInst = (uint32_t)e->hCtlInst.size ();
 			P.coff     = e->coff.p;

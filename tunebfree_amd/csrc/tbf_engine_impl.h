@@ -197,6 +197,9 @@ struct tbf_engine {
 	DevBuf<tbf_contrib>                     contrib;
 	PinnedVec<tbf_tgc_rec>                  hRec;     /* per delta of the chunk */
 	PinnedVec<uint16_t>                     hMsg;     /* the chunk's key messages */
+	PinnedVec<float>                        hGain;    /* the chunk's drawbar gain sets (27 each) */
+	PinnedVec<float>                        hGainB;
+	DevBuf<float>                           dgain, dgainB;
 	PinnedVec<uint32_t>                     hCtlInst; /* instances with a stepped delta */
 	/* the other parity of the chunk staging (the previous chunk's, in flight), and the
 	 * events after each parity's uploads */
@@ -219,6 +222,7 @@ struct tbf_engine {
 	 * segments {base_t, count_t} that are uploaded (empty: the pool is [0, dCtl.size ())) */
 	struct alignas (128) ParStep { /* own cache lines: workers bump these per delta */
 		std::vector<uint16_t> msgs;
+		std::vector<float>    gains;
 		std::vector<uint32_t> act, ctlInst, evs;
 		uint32_t              nd = 0;
 		int                   rc = 0;

@@ -179,6 +179,7 @@ struct TgControl {
 	/* vibrato knob (setVibrato, src/vibrato.cpp:97-129) */
 	uint32_t          vibTable = 2, vibMixed = 0;
 	bool              steadyPending = false; /* last block emitted env entries / removals */
+	bool              gainsSent = false;     /* the device holds drawBarGain (stepFront) */
 
 	void init (const TgTemplate* t, const Config& c);
 	void keyOn (int key);
@@ -198,7 +199,10 @@ struct TgControl {
 	 * key messages (msg.size () of them, written to msgDst = the chunk's message array
 	 * at msgOff) and drawbar / routing inputs in rec, the mixdown control in ctl.
 	 * wh (aot / active list / rflags) is not used. */
-	void stepFront (uint16_t* msgDst, uint32_t msgOff, tbf_tgc_rec& rec, tbf_seg_ctl& ctl);
+	void stepFront (uint16_t* msgDst, uint32_t msgOff, float* gainDst, uint32_t gainOff, tbf_tgc_rec& rec,
+	                tbf_seg_ctl& ctl);
+	/* stepFront sends the 27 drawbar gains (gainDst) on this step */
+	bool gainsDue () const { return drawBarChange || !gainsSent; }
 	void mixCtl (tbf_seg_ctl& ctl) const;
 };
 

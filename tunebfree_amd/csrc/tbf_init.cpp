@@ -964,8 +964,10 @@ void TgControl::step (std::vector<tbf_prog_entry>& prog, tbf_seg_ctl& ctl)
 	mixCtl (ctl);
 }
 
-void TgControl::stepFront (uint16_t* msgDst, uint32_t msgOff, tbf_tgc_rec& rec, tbf_seg_ctl& ctl)
+void TgControl::stepFront (uint16_t* msgDst, uint32_t msgOff, float* gainDst, uint32_t gainOff, tbf_tgc_rec& rec,
+                           tbf_seg_ctl& ctl)
 {
+	const bool sendGains = gainsDue (); /* gainDst holds 27 floats then */
 	memset (&rec, 0, sizeof (rec));
 	rec.msgOff = msgOff;
 	rec.nMsg   = (uint16_t)std::min<size_t> (msg.size (), 0xFFFF);
@@ -973,10 +975,14 @@ void TgControl::stepFront (uint16_t* msgDst, uint32_t msgOff, tbf_tgc_rec& rec, 
 	const bool recompute = oldRouting != newRouting;
 	if (recompute)
 		oldRouting = newRouting;
-	rec.flags       = (uint8_t)(0x80 | (drawBarChange ? 1 : 0) | (recompute ? 2 : 0));
+	rec.flags       = (uint8_t)(0x80 | (drawBarChange ? 1 : 0) | (recompute ? 2 : 0) | (sendGains ? 4 : 0));
 	rec.oldRouting  = (uint8_t)oldRouting;
 	rec.percSendBus = percSendBus;
-	memcpy (rec.drawBarGain, drawBarGain, sizeof (rec.drawBarGain));
+	if (sendGains) {
+		memcpy (gainDst, drawBarGain, sizeof (drawBarGain));
+		rec.gainOff = gainOff;
+		gainsSent   = true;
+	}
 	/* a block with inputs makes the next block's program differ (envelopes end, released
 	 * wheels leave, rerouted sums take over: the device's steadyPending); a block with
 	 * none leaves it unchanged, so stepping once after each input block is exact */

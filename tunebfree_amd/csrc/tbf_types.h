@@ -45,10 +45,11 @@ typedef struct tbf_prog_entry {
 typedef struct tbf_tgc_rec {
 	uint32_t msgOff;         /* the block's key messages (0x1000 | key: on, key: off) ... */
 	uint16_t nMsg;           /* ... msgs[msgOff .. msgOff + nMsg) */
-	uint8_t  flags;          /* 1 drawBarChange, 2 recomputeRouting, 0x80 stepped */
+	uint8_t  flags;          /* 1 drawBarChange, 2 recomputeRouting, 4 gains follow, 0x80 stepped */
 	uint8_t  oldRouting;     /* routing word after this block's update */
 	uint32_t percSendBus;
-	float    drawBarGain[27];
+	uint32_t gainOff;        /* flags & 4: the instance's drawBarGain[27] at gains[gainOff ..]
+	                          * (sent when they change; k_tgctl keeps them in tbf_tgc_state) */
 } tbf_tgc_rec;
 
 /* one keyContrib element on the device (Contrib): a key's list is sorted by wheel, then
@@ -70,7 +71,8 @@ typedef struct tbf_tgc_state {
 	uint8_t  rflags[TBF_NW + 1];
 	uint8_t  pad0[3];
 	uint32_t listEnd;             /* activeOscLEnd */
-	uint32_t pad1[3];
+	float    gain[27];            /* drawBarGain as of the last record that carried it */
+	uint32_t pad1[4];
 } tbf_tgc_state;
 
 /* per instance, per launch segment: control state that is constant over the
@@ -216,6 +218,7 @@ typedef struct tbf_launch {
 	tbf_tgc_state*        tgc;       /* [inst] */
 	const tbf_tgc_rec*    rec;       /* [pool index - nInst]: inputs of the chunk's deltas */
 	const uint16_t*       msgs;
+	const float*          gains;  /* drawbar gain sets of the records with flags & 4 */
 	const uint32_t*       ctlInst;   /* instances with a stepped delta in this chunk */
 	uint32_t              nCtlInst;
 	uint32_t              pad2;

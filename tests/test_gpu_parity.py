@@ -325,6 +325,84 @@ def test_gpu_dense_events_threaded_host_control(oracle):
     assert max(eL, eR) <= TOL
 
 
+def test_gpu_engine_switches_bitexact(oracle):
+    """The scheduling switches change where and when work runs, never the output: with
+    1100 instances, events on every block (keys, drawbars, control functions) and a
+    programme change in the second chunk (that chunk's host control falls back to the
+    serial loop), rendered in two calls, every switch renders bit-identically to the
+    default engine: the serial host loop, the opt-in control stream (three persistent
+    program slots), a third stage-buffer set, the chunk-parity streams, no pipelining.
+    Instances without a programme change are also checked against the oracle."""
+    import os
+    import torch
+    import tunebfree_amd as T
+    from orc_bind import Template
+    from test_control_cpu import PGM
+    n, nb, split = 1100, 72, 40
+    seeds = [5000 + i for i in range(n)]
+    rows, oscen = [], [[] for _ in range(n)]
+    for i in range(n):
+        for (k, a, v) in S.jazz1_params():
+            rows.append((0, i, 1, a, float(v)))
+            oscen[i].append((0, k, a, v))
+        for k in S.chord_for(i):
+            rows.append((0, i, 0, k, 1.0))
+            oscen[i].append((0, "note", k, 1))
+        for b in range(1, nb):
+            k0, k1 = 60 + (2 * i + b - 1) % 24, 60 + (2 * i + b) % 24
+            rows.append((b, i, 0, k0, 0.0))
+            oscen[i].append((b, "note", k0, 0))
+            rows.append((b, i, 0, k1, 1.0))
+            oscen[i].append((b, "note", k1, 1))
+            if b % 4 == i % 4:
+                rows.append((b, i, 1, S.P_DRAWBAR + 6, float((i + b) % 9)))
+                oscen[i].append((b, "param", S.P_DRAWBAR + 6, (i + b) % 9))
+    prog_inst = {5, 700}
+    switches = [{}, {"TBF_HOST_SERIAL": "1"}, {"TBF_CTL_STREAM": "1"}, {"TBF_STAGE_BUFS": "3"},
+                {"TBF_PIPE_MODE": "0"}, {"TBF_PIPELINE": "0"}]
+    outs, cid = [], None
+    for env in switches:
+        os.environ.update(env)
+        try:
+            eng = T.Engine(sample_rate=48000.0, device=0)
+        finally:
+            for k in env:
+                os.environ.pop(k, None)
+        assert eng.program_parse(PGM) == 4
+        tid = eng.template(seed=7)
+        eng.add_instances([tid] * n, seeds)
+        cid = eng.control_id("upper.drawbar4")
+        extra = [(b, i, 2, cid, float((3 * i + b) % 128)) for i in range(0, n, 5) for b in range(3, nb, 7)]
+        extra += [(66, i, 3, 2, 0.0) for i in prog_inst]  # programme 2 in the second chunk
+        ev = eng.events(rows + extra)
+        L = torch.zeros((n, nb * 128), dtype=torch.float32, device="cuda")
+        R = torch.zeros_like(L)
+        first = ev[ev["block"] < split]
+        rest = ev[ev["block"] >= split].copy()
+        rest["block"] -= split
+        eng.render_events_device(split, first, L.data_ptr(), R.data_ptr(), nb * 128)
+        eng.render_events_device(nb - split, rest, L[:, split * 128:].data_ptr(), R[:, split * 128:].data_ptr(),
+                                 nb * 128)
+        eng.synchronize()
+        outs.append((L.cpu().numpy(), R.cpu().numpy()))
+        eng.close()
+        del L, R
+    for env, (l, r) in zip(switches[1:], outs[1:]):
+        same = np.array_equal(l.view(np.uint32), outs[0][0].view(np.uint32)) and \
+            np.array_equal(r.view(np.uint32), outs[0][1].view(np.uint32))
+        print(f"{env}: bit-identical to the default engine: {same}")
+        assert same, env
+    for (b, i, _k, _c, v) in [(b, i, 2, cid, float((3 * i + b) % 128)) for i in range(0, n, 5) for b in range(3, nb, 7)]:
+        oscen[i].append((b, "param", S.P_DRAWBAR + 3, int(np.rint((127 - v) * 8.0 / 127.0))))
+    sample = [0, 1, 4, 550, 1099]
+    tpl = Template(oracle, seed=7)
+    oL, oR, *_ = oracle_run(oracle, tpl, [seeds[i] for i in sample], [sorted(oscen[i], key=lambda r: r[0]) for i in sample], nb)
+    eL, _ = compare(outs[0][0][sample], oL)
+    eR, _ = compare(outs[0][1][sample], oR)
+    print(f"switches scenario vs oracle ({len(sample)} instances): max|err| L={eL:.3g} R={eR:.3g}")
+    assert max(eL, eR) <= TOL
+
+
 def test_gpu_synth_sound_irregular_periods(oracle, tunings):
     """tbf_synth_sound (the synthSound FIFO of b_synth/lv2.cpp:1270-1287) with irregular
     period sizes (1 .. 700 frames; a call that needs several blocks renders them in one

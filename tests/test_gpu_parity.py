@@ -325,6 +325,25 @@ def test_gpu_dense_events_threaded_host_control(oracle):
     assert max(eL, eR) <= TOL
 
 
+def test_gpu_threaded_host_control_reports_errors():
+    """A bad event met by a host worker (threaded front end, >= 1024 instances) fails the
+    call with the worker's message, as the serial loop would (the message is thread-local)."""
+    import torch
+    import tunebfree_amd as T
+    n = 1100
+    eng = T.Engine(sample_rate=48000.0, device=0)
+    tid = eng.template(seed=7)
+    eng.add_instances([tid] * n, [9000 + i for i in range(n)])
+    rows = [(b, i, 0, 60 + (i + b) % 12, float(b % 2)) for i in range(n) for b in range(0, 8)]
+    rows.append((3, 600, 1, 999, 1.0))  # no such parameter id
+    L = torch.zeros((n, 8 * 128), dtype=torch.float32, device="cuda")
+    R = torch.zeros_like(L)
+    with pytest.raises(T.engine.TbfError, match="unknown parameter id"):
+        eng.render_events_device(8, eng.events(rows), L.data_ptr(), R.data_ptr(), 8 * 128)
+    eng.synchronize()
+    eng.close()
+
+
 def test_gpu_engine_switches_bitexact(oracle):
     """The scheduling switches change where and when work runs, never the output: with
     1100 instances, events on every block (keys, drawbars, control functions) and a

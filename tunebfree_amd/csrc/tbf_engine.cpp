@@ -1138,6 +1138,7 @@ static int stepChunkParallel (tbf_engine* e, uint32_t n, uint32_t want, uint32_t
 		o.evs.clear ();
 		o.nd = 0;
 		o.rc = 0;
+		o.err.clear ();
 	}
 	for (uint32_t a : e->actList) /* the active list by range, in order */
 		out[a / per].act.push_back (a);
@@ -1161,8 +1162,10 @@ static int stepChunkParallel (tbf_engine* e, uint32_t n, uint32_t want, uint32_t
 			cur[i] = i;
 		for (uint32_t len = 0; len < want && !o.rc; len++) {
 			for (; ep < o.evs.size () && ev[o.evs[ep]].block <= b0 + len; ep++) {
-				if ((o.rc = applyEvent (e, ev[o.evs[ep]])))
+				if ((o.rc = applyEvent (e, ev[o.evs[ep]]))) {
+					o.err = g_err;
 					break;
+				}
 				markActive (e, ev[o.evs[ep]].inst); /* (control-function events do not mark) */
 			}
 			size_t keep = 0;
@@ -1204,7 +1207,7 @@ static int stepChunkParallel (tbf_engine* e, uint32_t n, uint32_t want, uint32_t
 	e->dSeg.clear ();
 	for (unsigned t = 0; t < T; t++) {
 		if (out[t].rc)
-			return out[t].rc;
+			return fail (out[t].rc, out[t].err); /* on the calling thread */
 		mb[t] = nm;
 		nm += out[t].msgs.size ();
 		gb[t] = ng;

@@ -226,6 +226,7 @@ struct tbf_engine {
 		std::vector<uint32_t> act, ctlInst, evs;
 		uint32_t              nd = 0;
 		int                   rc = 0;
+		std::string           err; /* the worker's tbf_last_error text (it is thread-local) */
 	};
 	std::vector<ParStep>                    parStep;
 	std::vector<std::pair<uint32_t, uint32_t>> dSeg;

@@ -294,6 +294,14 @@ int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
 	e->cfg = *cfg;
 	if (cfg->device >= 0) {
 		HIPCHK (hipSetDevice (cfg->device));
+		/* stream creation order matters: the process has GPU_MAX_HW_QUEUES (4) hardware
+		 * queues and streams take them round-robin at creation.  The engine's own stream
+		 * first, then the three stage-group streams: a caller's stream created after the
+		 * engine shares the engine stream's queue (idle when the caller passes its
+		 * stream); one created before shares the last stage group's, whose work the
+		 * caller's stream waits for anyway.  A stage group's queue shared with the
+		 * caller's stream would order the group's next launches behind the caller's
+		 * end-of-call wait (measured: steady step 6.7 -> 8.1 ms, TBF_CTL_STREAM below) */
 		HIPCHK (hipStreamCreateWithFlags (&e->stream, hipStreamNonBlocking));
 		/* TBF_STREAM_PRIO=k: the stream of stage group k (0..2) at the device's greatest
 		 * priority (A/B of which stage group the dispatcher should favour) */

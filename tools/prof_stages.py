@@ -21,6 +21,8 @@ NAMES = {0: "tg state load + interpreter", 1: "tg vibrato", 2: "tg mixdown", 3: 
          8: "rv_core channel L", 9: "rv_core channel R + counts",
          10: "rv_out load", 11: "rv_out B(b) + C(b-1) chains", 12: "rv_out dither + dry + store",
          13: "rv_out asin",
+         14: "rv_lds ring load", 15: "rv_lds plan", 16: "rv_lds read phase", 17: "rv_lds write phase",
+         19: "rv_lds ring store",
          26: "wh state + ring load", 20: "wh speed", 21: "wh ring rd + serial filt+angles", 22: "wh FILTER_C",
          23: "wh motions", 24: "wh accumulate", 25: "wh out + carry", 27: "wh state + ring store"}
 

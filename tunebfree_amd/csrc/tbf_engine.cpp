@@ -31,6 +31,7 @@ extern "C" int tbf_launch_stage (const tbf_launch* P, int k, hipStream_t stream)
 extern "C" int tbf_chain_stages (uint32_t chain);
 extern "C" int tbf_launch_tgctl (const tbf_launch* P, hipStream_t stream);
 extern "C" int tbf_launch_calibrate (int op, void* buf, uint64_t n, hipStream_t s);
+extern "C" int tbf_rv_lds_fits (const tbf_inst_const* k);
 
 using namespace tbf;
 
@@ -317,12 +318,16 @@ int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
 		for (int k = 0; k < TBF_NSTAGES; k++)
 			HIPCHK (hipEventCreateWithFlags (&e->sdone[k], hipEventDisableTiming));
 		HIPCHK (hipEventCreateWithFlags (&e->sjoin, hipEventDisableTiming));
+		/* TBF_RV_LDS=1: the reverb core with LDS-resident rings (k_rv_core_lds) instead of the
+		 * streaming k_rv_core */
+		if (const char* rl = getenv ("TBF_RV_LDS"))
+			e->rvLdsOn = rl[0] != '0';
 		if (const char* pm = getenv ("TBF_PIPE_MODE"))
 			e->pipeMode = atoi (pm) == 1 ? 1 : 0;
-		if (const char* pg = getenv ("TBF_PIPE_GROUPS")) { /* "g0,g1,g2,g3,g4", groups 0..2, non-decreasing */
+		if (const char* pg = getenv ("TBF_PIPE_GROUPS")) { /* "g0,g1,g2,g3,g4", groups 0..4, non-decreasing */
 			for (int k = 0; k < TBF_NSTAGES && *pg; k++) {
 				const int g = atoi (pg);
-				if (g >= 0 && g < 3 && (k == 0 || g >= e->grp[k - 1]))
+				if (g >= 0 && g < TBF_NSTAGES && (k == 0 || g >= e->grp[k - 1]))
 					e->grp[k] = g;
 				while (*pg && *pg != ',')
 					pg++;
@@ -335,6 +340,9 @@ int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
 				HIPCHK (hipStreamCreateWithPriority (&e->gstr3, hipStreamNonBlocking, prGreatest));
 			else
 				HIPCHK (hipStreamCreateWithFlags (&e->gstr3, hipStreamNonBlocking));
+			/* groups 3, 4 (more than three stage groups) */
+			for (int g = 3; g <= e->grp[TBF_NSTAGES - 1]; g++)
+				HIPCHK (hipStreamCreateWithFlags (&e->gstrM[g - 3], hipStreamNonBlocking));
 			/* TBF_CTL_STREAM=1: a delta chunk's uploads and k_tgctl on a stream of their own.
 			 * Off by default: the process has GPU_MAX_HW_QUEUES (4) hardware queues, streams
 			 * take them round-robin at creation, and a fifth engine stream pushes the caller's
@@ -397,6 +405,9 @@ int tbf_engine_destroy (tbf_engine* e)
 			(void)hipStreamSynchronize (e->sstr[p]);
 	if (e->gstr3)
 		(void)hipStreamSynchronize (e->gstr3);
+	for (hipStream_t q : e->gstrM)
+		if (q)
+			(void)hipStreamSynchronize (q);
 	if (e->cstr)
 		(void)hipStreamSynchronize (e->cstr);
 	e->bank.release ();
@@ -436,6 +447,9 @@ int tbf_engine_destroy (tbf_engine* e)
 			(void)hipStreamDestroy (e->sstr[p]);
 	if (e->gstr3)
 		(void)hipStreamDestroy (e->gstr3);
+	for (hipStream_t q : e->gstrM)
+		if (q)
+			(void)hipStreamDestroy (q);
 	if (e->cstr)
 		(void)hipStreamDestroy (e->cstr);
 	for (int p = 0; p < 6; p++)
@@ -658,9 +672,10 @@ int tbf_instances_add (tbf_engine* e, uint32_t n, const uint32_t* tpl_ids, const
 		in.s0.tg.percEnvGain  = 0.0f;
 		in.s0.tg.outPos       = 1023 / 2;
 		in.tg.init (e->tpls[in.tpl].get (), e->conf);
-		if (e->slabLen == 0)
-			e->slabLen = in.k.slabLen;
-		else if (e->slabLen != in.k.slabLen)
+		if (e->slabLen == 0) {
+			e->slabLen  = in.k.slabLen;
+			e->rvLdsFit = tbf_rv_lds_fits (&in.k) != 0; /* same geometry for every instance */
+		} else if (e->slabLen != in.k.slabLen)
 			return fail (-22, "inconsistent reverb geometry");
 	}
 	e->deviceReady = false;
@@ -840,6 +855,9 @@ static int drainStages (tbf_engine* e)
 		HIPCHK (hipStreamSynchronize (e->sstr[p]));
 	if (e->gstr3)
 		HIPCHK (hipStreamSynchronize (e->gstr3));
+	for (hipStream_t q : e->gstrM)
+		if (q)
+			HIPCHK (hipStreamSynchronize (q));
 	if (e->cstr)
 		HIPCHK (hipStreamSynchronize (e->cstr));
 	e->stagesBusy = false;
@@ -851,8 +869,8 @@ static int joinStages (tbf_engine* e, hipStream_t s)
 {
 	if (!e->stagesBusy)
 		return 0;
-	for (int p = 0; p < 4; p++) {
-		hipStream_t q = p < 2 ? e->sstr[p] : p == 2 ? e->gstr3 : e->cstr;
+	for (int p = 0; p < 6; p++) {
+		hipStream_t q = p < 2 ? e->sstr[p] : p == 2 ? e->gstr3 : p == 3 ? e->cstr : e->gstrM[p - 4];
 		if (!q)
 			continue;
 		HIPCHK (hipEventRecord (e->sjoin, q));
@@ -1327,6 +1345,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 	P.errFlags  = e->err.p;
 	P.dbg       = e->cfg.debug_flags;
 	P.prof      = e->profOn ? e->prof.p : nullptr;
+	P.rvLds     = e->rvLdsOn && e->rvLdsFit;
 	/* inter-stage buffers: nbuf sets by chunk index (2: alternate chunks; 3 with the
 	 * stage-group streams), see the pipelining below */
 	const size_t   need = (size_t)n * TBF_CHUNK * TBF_BLK;
@@ -1643,7 +1662,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			 * output mid1 is read by k_rv_in and k_rv_out, rvA by k_rv_core, rvB by k_rv_out,
 			 * mid2 by k_whirl) when they run on another stream. */
 			static const int readers[5][2] = {{1, 3}, {2, -1}, {3, -1}, {4, -1}, {-1, -1}};
-			auto strm = [&] (int k) { const int g = e->grp[k]; return g < 2 ? e->sstr[g] : e->gstr3; };
+			auto strm = [&] (int k) { const int g = e->grp[k]; return g < 2 ? e->sstr[g] : g == 2 ? e->gstr3 : e->gstrM[g - 3]; };
 			for (int k = 0; k < nst; k++) {
 				hipStream_t sk = strm (k);
 				if (k == 0 && !e->stagesBusy) { /* after the caller's stream (uploads, earlier chunks) */

@@ -280,7 +280,10 @@ struct tbf_engine {
 	 * streams by chunk parity (round 1) */
 	int                                     pipeMode = 1;
 	int                                     grp[5]   = {0, 1, 1, 2, 2};
+	bool                                    rvLdsOn  = false; /* k_rv_core_lds when the rings fit (TBF_RV_LDS=1) */
+	bool                                    rvLdsFit = false; /* the instances' rings fit k_rv_core_lds */
 	hipStream_t                             gstr3    = nullptr; /* the third group's stream (groups 0, 1 use sstr) */
+	hipStream_t                             gstrM[2] = {};      /* groups 3, 4 (TBF_PIPE_GROUPS with more than three) */
 	hipStream_t                             cstr     = nullptr; /* device control: uploads + k_tgctl */
 	/* stage-group pipelining: each chunk's stage-k event, in a ring by chunk index (a chunk
 	 * waits on chunk c - nbuf's readers of the stage buffers it overwrites and on chunk

@@ -1272,6 +1272,292 @@ k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 	prof_end (P, sm, inst);
 }
 
+/* ------------------------------------------------------------------ k_rv_core_lds
+ * The feedback network with the channel's 12 rings resident in LDS for the whole launch:
+ * loaded once at the start, stored once at the end (2 x 129 KB per channel and chunk
+ * instead of 16 B per line and sample streamed through HBM).  One workgroup of RVL_G
+ * waves per (instance, channel), one workgroup per CU (the rings fill its LDS).
+ *
+ * Why RVL_G sub-blocks can run at once: a sample's ring reads (taps at slot count+1+off,
+ * off <= 2 vibDepth + 1 < 8, allpass reads at count+1) return values written >= d - 71
+ * samples earlier, d >= 756 at the reference's fixed settings (reverbConsts; the host
+ * checks d >= RVL_G * 64 + 72).  So the RVL_G * 64 = 512 samples of a group read only
+ * slots that no sample of the group writes (the slot distance between any read and any
+ * write of the group lies in 2 .. 520 < d + 1), and all reads of a group may precede
+ * all its writes, exactly as k_rv_core's reads of a sub-block precede its writes.  The
+ * one serial term, feedback(n - 1), crosses sub-blocks through LDS (carry) between the
+ * read phase and the write phase.  Per sub-block the arithmetic is k_rv_core's: the
+ * same phases (closed form v0 + (n+1) D with the same start phases, or the literal
+ * recurrence), the same sine rows, taps, Householder mix and allpasses. */
+#ifndef RVL_G
+#define RVL_G 10 /* sub-blocks (worker waves) per group: RVL_G * 64 + 72 <= the shortest delay (756) */
+#endif
+#ifndef RVL_UNROLL
+#define RVL_UNROLL 2 /* delay lines whose taps a worker computes together */
+#endif
+#define RVL_RING 16384 /* LDS ring doubles: lines 0..11 of a channel, 8-padded (16,216 at the fixed settings) */
+#define RVL_THREADS (NL * (RVL_G + 1)) /* RVL_G worker waves + the planner wave */
+
+struct RvLds {
+	double      ring[RVL_RING];
+	double      sd[2][8][TBF_SUB];     /* sine rows of each line's closed-form step, by group parity */
+	double      cm[2][8][TBF_SUB];
+	double      tabD[2][8];            /* the step each row holds (-1: none) */
+	double      v0[2][RVL_G][8];       /* group plan: phase of line l at the start of sub-block j ... */
+	double      S[2][RVL_G][8];        /* ... and its sine and cosine (closed-form lines) */
+	double      C[2][RVL_G][8];
+	uint32_t    okm[2][RVL_G];         /* closed-form lines of sub-block j */
+	double      carry[2][RVL_G][8];    /* feedback of sub-block j's last sample */
+	tbf_rv_chan st;
+	TBF_PROF_LDS
+};
+
+/* the planner wave: the phase plan of group g into buffer b (start phases, closed-form
+ * flags, sincos of the start phases, sine rows); st.vib advanced past the group.  It
+ * depends only on the phases, so it runs while the workers process the group before. */
+__device__ __forceinline__ void rvl_plan (RvLds& sm, const tbf_inst_const& K, int nb, int b, bool force, uint32_t* errFlags)
+{
+	const int    lane = threadIdx.x & (NL - 1);
+	const int    li   = lane & 7; /* every lane analyses line lane & 7 */
+	const double d    = K.vibDelta[li];
+	const double v0   = sm.st.vib[li];
+	double       D = 0.0, cD = sm.st.phD[li], cLo = sm.st.phLo[li], cHi = sm.st.phHi[li];
+	/* the group's whole run closed-form: sub-block j starts at v0 + 64 j D exactly */
+	const bool     ok  = phase_run_cached (v0, d, TBF_SUB * nb, D, cD, cLo, cHi) && !force;
+	const uint64_t okb = __ballot (lane < 8 && ok);
+#pragma unroll 1
+	for (int l = 0; l < 8; l++) {
+		if (!((okb >> l) & 1))
+			continue;
+		const double Dl = rld (D, l);
+		if (sm.tabD[b][l] != Dl) { /* rare: a new step (binade) */
+			const double dn  = (double)(lane + 1) * Dl; /* exact */
+			const double h   = sin (dn * 0.5);
+			sm.sd[b][l][lane] = sin (dn);
+			sm.cm[b][l][lane] = 2.0 * h * h;
+			__builtin_amdgcn_wave_barrier ();
+			if (lane == 0)
+				sm.tabD[b][l] = Dl;
+		}
+	}
+	/* lane q = 8 j + l (and q + 64): sub-block j, line l */
+	for (int q = lane; q < 8 * nb; q += NL) {
+		const int j = q >> 3;
+		if (ok) {
+			const double v = v0 + (double)(TBF_SUB * j) * D; /* exact inside the binade */
+			double       sv, cv;
+			sincos (v, &sv, &cv);
+			sm.v0[b][j][li] = v;
+			sm.S[b][j][li]  = sv;
+			sm.C[b][j][li]  = cv;
+		}
+	}
+	if (lane < RVL_G)
+		sm.okm[b][lane] = lane < nb ? (uint32_t)(okb & 0xff) : 0u;
+	__builtin_amdgcn_wave_barrier ();
+	if (lane < 8) {
+		sm.st.phD[li]  = cD;
+		sm.st.phLo[li] = cLo;
+		sm.st.phHi[li] = cHi;
+		double v = v0;
+		if (ok) {
+			v = v0 + (double)(TBF_SUB * nb) * D;
+		} else {
+			/* rare (a binade crossing or a rounding tie in the group, or forced): walk the
+			 * sub-blocks like k_rv_core; one is closed-form when its own run is and the
+			 * line's rows hold its step, else the literal recurrence (64 adds) */
+			atomicOr (errFlags, (uint32_t)TBF_PATH_RV_PHASE);
+			for (int j = 0; j < nb; j++) {
+				sm.v0[b][j][li] = v;
+				double     Dj = 0.0, c1 = cD, c2 = cLo, c3 = cHi;
+				const bool oj = phase_run_cached (v, d, TBF_SUB, Dj, c1, c2, c3) && !force && Dj == sm.tabD[b][li];
+				if (oj) {
+					double sv, cv;
+					sincos (v, &sv, &cv);
+					sm.S[b][j][li] = sv;
+					sm.C[b][j][li] = cv;
+					atomicOr (&sm.okm[b][j], 1u << li);
+					v = v + (double)TBF_SUB * Dj;
+				} else {
+					for (int i = 0; i < TBF_SUB; i++)
+						v += d;
+				}
+			}
+		}
+		sm.st.vib[li] = v;
+	}
+}
+
+__global__ void __attribute__ ((amdgpu_flat_work_group_size (RVL_THREADS, RVL_THREADS)))
+k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
+{
+	__shared__ RvLds sm;
+	const int      tid  = threadIdx.x;
+	const int      w    = tid >> 6; /* worker: the sub-block within a group; w == RVL_G: planner */
+	const int      n    = tid & (NL - 1);
+	const uint32_t inst = (blockIdx.x >> 1) + P.instBase;
+	const int      c    = blockIdx.x & 1;
+	if (inst >= P.nInst)
+		return;
+	const tbf_inst_const& K     = cst[inst];
+	tbf_rv_chan*          S     = &P.st[inst].rv.ch[c];
+	const uint32_t        rbase = K.ringOff[c * 13];
+	const uint32_t        rlen2 = (K.ringOff[c * 13 + 12] - rbase) / 2; /* lines 0..11 (contiguous), double2 */
+	double*               slab  = P.rslab + (size_t)inst * P.slabLen + rbase;
+	const double*         a0s   = rv_buf (P.rvA, P, inst, c);
+	double*               bout  = rv_buf (P.rvB, P, inst, c);
+	prof_begin (P, sm);
+	/* rings and state to LDS: every load in flight before the first LDS store (clamped
+	 * indices keep the loads unconditional) */
+	{
+		constexpr int NR = (RVL_RING / 2 + RVL_THREADS - 1) / RVL_THREADS;
+		double2       v[NR];
+#pragma unroll
+		for (int k = 0; k < NR; k++) {
+			const uint32_t i = tid + k * RVL_THREADS;
+			v[k]             = ((const double2*)slab)[i < rlen2 ? i : 0];
+		}
+#pragma unroll
+		for (int k = 0; k < NR; k++) {
+			const uint32_t i = tid + k * RVL_THREADS;
+			if (i < rlen2)
+				((double2*)sm.ring)[i] = v[k];
+		}
+	}
+	if (w == 0) { /* copy_words: threads 0..63 */
+		copy_words (&sm.st, S);
+		if (n < 16)
+			(&sm.tabD[0][0])[n] = -1.0;
+	}
+	/* lane l < 12: delay, LDS ring offset and counter of line l */
+	const int dlyv = n < 12 ? K.delay[n] : 0;
+	const int lofv = n < 12 ? (int)(K.ringOff[c * 13 + n] - rbase) : 0;
+	const uint32_t nSub  = P.nBlocks * (TBF_BLK / TBF_SUB);
+	const uint32_t nGrp  = (nSub + RVL_G - 1) / RVL_G;
+	const bool     force = (P.dbg & TBF_DEBUG_FORCE_SERIAL) != 0;
+	__syncthreads ();
+	if (w == RVL_G && nGrp > 0)
+		rvl_plan (sm, K, (int)min ((uint32_t)RVL_G, nSub), 0, force, P.errFlags);
+	int cntv = n < 12 ? sm.st.count[n] : 0;
+	cntv     = (cntv < 0 || cntv > dlyv) ? dlyv : cntv; /* see k_rv_core */
+	/* this worker's sub-block counter (RVL_G * 64 + 72 <= d: one wrap at most) */
+	int cw = wrap_slot (cntv + TBF_SUB * (w < RVL_G ? w : 0), dlyv);
+	if (w == 0 && n < 8)
+		sm.carry[1][RVL_G - 1][n] = sm.st.fb[n]; /* as the "previous group's" last feedback */
+	const double oneMB = 1.0 - K.blend;
+	double       a0    = 0.0;
+	if ((uint32_t)w < nSub && w < RVL_G)
+		a0 = a0s[(size_t)w * TBF_SUB + n];
+	__syncthreads ();
+	TBF_MARK (14);
+#pragma unroll 1
+	for (uint32_t g = 0; g < nGrp; g++) {
+		const int  nb  = (int)min ((uint32_t)RVL_G, nSub - g * RVL_G);
+		const int  par = g & 1;
+		const bool act = w < nb;
+		/* ---- read phase (workers): taps, mix, allpass reads; nothing is written to the
+		 * rings.  The planner plans the next group meanwhile. ---- */
+		double apw[4], ap[4], fb[8];
+		if (act) {
+			const uint32_t s  = g * RVL_G + (uint32_t)w;
+			const size_t   o  = (size_t)s * TBF_SUB + n;
+			const uint32_t om = sm.okm[par][w];
+			double         I[8];
+#pragma unroll RVL_UNROLL
+			for (int l = 0; l < 8; l++) {
+				double sn;
+				if ((om >> l) & 1) {
+					const double Sv = sm.S[par][w][l], Cv = sm.C[par][w][l];
+					sn              = Sv + ((Cv * sm.sd[par][l][n]) - (Sv * sm.cm[par][l][n]));
+				} else {
+					const double dl = K.vibDelta[l];
+					double       v  = sm.v0[par][w][l];
+					for (int i = 0; i <= n; i++)
+						v += dl;
+					sn = sin (v);
+				}
+				const double  off = (sn + 1.0) * K.vibDepth;
+				const int     d   = rl (dlyv, l);
+				const double* rg  = sm.ring + rl (lofv, l);
+				const int     cn  = wrap_slot (rl (cw, l) + n + 1, d);
+				const int     wk  = (int)(cn + off);
+				const double  fr  = off - floor (off);
+				const double  r0 = rg[wrap_slot (wk, d)], r1 = rg[wrap_slot (wk + 1, d)];
+				double        x  = (r0 * (1 - fr));
+				x += (r1 * fr);
+				I[l] = (oneMB * x) + (r0 * K.blend);
+			}
+			I[0]  = (I[0] * K.oneMinusAbsCm) + (I[4] * K.crossmod);
+			I[4]  = (I[4] * K.oneMinusAbsCm) + (I[0] * K.crossmod);
+			fb[0] = (I[0] - (I[1] + I[2] + I[3])) * K.regen;
+			fb[1] = (I[1] - (I[0] + I[2] + I[3])) * K.regen;
+			fb[2] = (I[2] - (I[0] + I[1] + I[3])) * K.regen;
+			fb[3] = (I[3] - (I[0] + I[1] + I[2])) * K.regen;
+			fb[4] = (I[4] - (I[5] + I[6] + I[7])) * K.regen;
+			fb[5] = (I[5] - (I[4] + I[6] + I[7])) * K.regen;
+			fb[6] = (I[6] - (I[4] + I[5] + I[7])) * K.regen;
+			fb[7] = (I[7] - (I[4] + I[5] + I[6])) * K.regen;
+			const double mix = (I[0] + I[1] + I[2] + I[3] + I[4] + I[5] + I[6] + I[7]) / 8.0;
+#pragma unroll
+			for (int l = 8; l < 12; l++) {
+				const int    d   = rl (dlyv, l);
+				const double old = sm.ring[rl (lofv, l) + wrap_slot (rl (cw, l) + n + 1, d)];
+				double       a   = a0;
+				a -= old * 0.5;
+				apw[l - 8] = a;
+				a *= 0.5;
+				a += old;
+				ap[l - 8] = a;
+			}
+			rv_st (&bout[o], mix);
+			if (n == NL - 1) {
+#pragma unroll
+				for (int l = 0; l < 8; l++)
+					sm.carry[par][w][l] = fb[l];
+			}
+		} else if (w == RVL_G && g + 1 < nGrp) {
+			rvl_plan (sm, K, (int)min ((uint32_t)RVL_G, nSub - (g + 1) * RVL_G), par ^ 1, force, P.errFlags);
+		}
+		__syncthreads ();
+		TBF_MARK (16);
+		/* ---- write phase ---- */
+		if (act) {
+#pragma unroll
+			for (int l = 8; l < 12; l++)
+				sm.ring[rl (lofv, l) + wrap_slot (rl (cw, l) + n, rl (dlyv, l))] = apw[l - 8];
+			const int srcAp[8] = {3, 2, 1, 0, 0, 1, 2, 3};
+#pragma unroll
+			for (int l = 0; l < 8; l++) {
+				const double up   = lane_shr1 (fb[l]);
+				const double cprv = w == 0 ? sm.carry[par ^ 1][RVL_G - 1][l] : sm.carry[par][w - 1][l];
+				const double prev = n == 0 ? cprv : up;
+				sm.ring[rl (lofv, l) + wrap_slot (rl (cw, l) + n, rl (dlyv, l))] = ap[srcAp[l]] + prev;
+			}
+			/* the next group's input */
+			const uint32_t sn = (g + 1) * RVL_G + (uint32_t)w;
+			if (sn < nSub)
+				a0 = a0s[(size_t)sn * TBF_SUB + n];
+		}
+		cw = wrap_slot (cw + TBF_SUB * RVL_G, dlyv);
+		__syncthreads ();
+		TBF_MARK (17);
+	}
+	/* state: counters after nSub * 64 steps, the last sample's feedback */
+	if (w == 0) {
+		if (n < 12)
+			sm.st.count[n] = (int)(((uint32_t)cntv + (uint64_t)nSub * TBF_SUB) % (uint32_t)(dlyv + 1));
+		if (n < 8 && nGrp > 0)
+			sm.st.fb[n] = sm.carry[(nGrp - 1) & 1][(nSub - 1) % RVL_G][n];
+	}
+	__syncthreads ();
+	for (uint32_t i = tid; i < rlen2; i += RVL_THREADS)
+		((double2*)slab)[i] = ((const double2*)sm.ring)[i];
+	if (w == 0)
+		copy_words (S, &sm.st);
+	TBF_MARK (19);
+	prof_end (P, sm, inst);
+}
+
 /* k_rv_out: biquadB -> clamp + asin -> biquadC -> dry mix, dither, (L+R)/sqrt2, in
  * 128-sample blocks, software-pipelined so biquadB of block b and biquadC of block b-1
  * advance in the same serial instruction stream (lane 4j + 2q + c: instance j of the
@@ -2126,7 +2412,10 @@ extern "C" int tbf_launch_stage (const tbf_launch* P, int k, hipStream_t stream)
 		hipLaunchKernelGGL (k_rv_in<RVIN_IPW>, dim3 ((P->nInst + RVIN_IPW - 1) / RVIN_IPW), block, 0, stream, *P, P->cst,
 		                    P->ctl);
 	else if (k == 2)
-		hipLaunchKernelGGL (k_rv_core, dim3 (2 * P->nInst), block, 0, stream, *P, P->cst);
+		if (P->rvLds)
+			hipLaunchKernelGGL (k_rv_core_lds, dim3 (2 * P->nInst), dim3 (RVL_THREADS), 0, stream, *P, P->cst);
+		else
+			hipLaunchKernelGGL (k_rv_core, dim3 (2 * P->nInst), block, 0, stream, *P, P->cst);
 	else if (k == 3)
 		hipLaunchKernelGGL (k_rv_out<RVOUT_IPW>, dim3 ((P->nInst + RVOUT_IPW - 1) / RVOUT_IPW), block, 0, stream, *P,
 		                    P->cst, P->ctl);
@@ -2140,6 +2429,18 @@ extern "C" int tbf_launch_stage (const tbf_launch* P, int k, hipStream_t stream)
 	} else
 		return -22;
 	return hipGetLastError () == hipSuccess ? 0 : -5;
+}
+
+/* whether k_rv_core_lds can run an instance with these reverb constants: a channel's 12
+ * rings fit its LDS ring and every delay leaves a group's reads clear of its writes */
+extern "C" int tbf_rv_lds_fits (const tbf_inst_const* k)
+{
+	if (k->ringOff[12] - k->ringOff[0] > RVL_RING || k->ringOff[25] - k->ringOff[13] > RVL_RING)
+		return 0;
+	for (int l = 0; l < 12; l++)
+		if (k->delay[l] < RVL_G * TBF_SUB + 72)
+			return 0;
+	return 1;
 }
 
 /* number of stages the chain mode runs */

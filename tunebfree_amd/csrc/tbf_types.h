@@ -221,7 +221,7 @@ typedef struct tbf_launch {
 	const float*          gains;  /* drawbar gain sets of the records with flags & 4 */
 	const uint32_t*       ctlInst;   /* instances with a stepped delta in this chunk */
 	uint32_t              nCtlInst;
-	uint32_t              pad2;
+	uint32_t              rvLds;     /* 1: the reverb core with its rings resident in LDS (k_rv_core_lds) */
 	const uint32_t*       coff;      /* [tpl][385] keyContrib offsets into contrib */
 	const tbf_contrib*    contrib;
 	uint64_t*             prof;      /* [inst][TBF_PROF_SLOTS] stage cycle sums, or NULL */

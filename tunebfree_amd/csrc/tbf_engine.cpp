@@ -318,8 +318,7 @@ int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
 		for (int k = 0; k < TBF_NSTAGES; k++)
 			HIPCHK (hipEventCreateWithFlags (&e->sdone[k], hipEventDisableTiming));
 		HIPCHK (hipEventCreateWithFlags (&e->sjoin, hipEventDisableTiming));
-		/* TBF_RV_LDS=1: the reverb core with LDS-resident rings (k_rv_core_lds) instead of the
-		 * streaming k_rv_core */
+		/* TBF_RV_LDS=0: the streaming reverb core (k_rv_core) instead of k_rv_core_lds */
 		if (const char* rl = getenv ("TBF_RV_LDS"))
 			e->rvLdsOn = rl[0] != '0';
 		if (const char* pm = getenv ("TBF_PIPE_MODE"))

@@ -280,7 +280,7 @@ struct tbf_engine {
 	 * streams by chunk parity (round 1) */
 	int                                     pipeMode = 1;
 	int                                     grp[5]   = {0, 1, 1, 2, 2};
-	bool                                    rvLdsOn  = false; /* k_rv_core_lds when the rings fit (TBF_RV_LDS=1) */
+	bool                                    rvLdsOn  = true; /* k_rv_core_lds when the rings fit (TBF_RV_LDS=0: k_rv_core) */
 	bool                                    rvLdsFit = false; /* the instances' rings fit k_rv_core_lds */
 	hipStream_t                             gstr3    = nullptr; /* the third group's stream (groups 0, 1 use sstr) */
 	hipStream_t                             gstrM[2] = {};      /* groups 3, 4 (TBF_PIPE_GROUPS with more than three) */

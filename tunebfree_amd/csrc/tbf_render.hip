@@ -1292,8 +1292,11 @@ k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 #ifndef RVL_G
 #define RVL_G 10 /* sub-blocks (worker waves) per group: RVL_G * 64 + 72 <= the shortest delay (756) */
 #endif
+#ifndef RVL_ABL
+#define RVL_ABL 0 /* timing-only ablations of k_rv_core_lds: 1 no planning after the first group, 2 no ring load/store, 4 no write phase */
+#endif
 #ifndef RVL_UNROLL
-#define RVL_UNROLL 2 /* delay lines whose taps a worker computes together */
+#define RVL_UNROLL 8 /* delay lines whose taps a worker computes together (8: 2.39 ms alone, 2: 3.0) */
 #endif
 #define RVL_RING 16384 /* LDS ring doubles: lines 0..11 of a channel, 8-padded (16,216 at the fixed settings) */
 #define RVL_THREADS (NL * (RVL_G + 1)) /* RVL_G worker waves + the planner wave */
@@ -1315,11 +1318,10 @@ struct RvLds {
 /* the planner wave: the phase plan of group g into buffer b (start phases, closed-form
  * flags, sincos of the start phases, sine rows); st.vib advanced past the group.  It
  * depends only on the phases, so it runs while the workers process the group before. */
-__device__ __forceinline__ void rvl_plan (RvLds& sm, const tbf_inst_const& K, int nb, int b, bool force, uint32_t* errFlags)
+__device__ __forceinline__ void rvl_plan (RvLds& sm, double d, int nb, int b, bool force, uint32_t* errFlags)
 {
 	const int    lane = threadIdx.x & (NL - 1);
-	const int    li   = lane & 7; /* every lane analyses line lane & 7 */
-	const double d    = K.vibDelta[li];
+	const int    li   = lane & 7; /* every lane analyses line lane & 7; d = vibDelta[li] */
 	const double v0   = sm.st.vib[li];
 	double       D = 0.0, cD = sm.st.phD[li], cLo = sm.st.phLo[li], cHi = sm.st.phHi[li];
 	/* the group's whole run closed-form: sub-block j starts at v0 + 64 j D exactly */
@@ -1415,7 +1417,7 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 #pragma unroll
 		for (int k = 0; k < NR; k++) {
 			const uint32_t i = tid + k * RVL_THREADS;
-			v[k]             = ((const double2*)slab)[i < rlen2 ? i : 0];
+			v[k]             = (RVL_ABL & 2) ? double2 {0.0, 0.0} : ((const double2*)slab)[i < rlen2 ? i : 0];
 		}
 #pragma unroll
 		for (int k = 0; k < NR; k++) {
@@ -1432,12 +1434,13 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 	/* lane l < 12: delay, LDS ring offset and counter of line l */
 	const int dlyv = n < 12 ? K.delay[n] : 0;
 	const int lofv = n < 12 ? (int)(K.ringOff[c * 13 + n] - rbase) : 0;
+	const double vdl = K.vibDelta[n & 7]; /* lane-held: no vector load of K inside the loop */
 	const uint32_t nSub  = P.nBlocks * (TBF_BLK / TBF_SUB);
 	const uint32_t nGrp  = (nSub + RVL_G - 1) / RVL_G;
 	const bool     force = (P.dbg & TBF_DEBUG_FORCE_SERIAL) != 0;
 	__syncthreads ();
 	if (w == RVL_G && nGrp > 0)
-		rvl_plan (sm, K, (int)min ((uint32_t)RVL_G, nSub), 0, force, P.errFlags);
+		rvl_plan (sm, vdl, (int)min ((uint32_t)RVL_G, nSub), 0, force, P.errFlags);
 	int cntv = n < 12 ? sm.st.count[n] : 0;
 	cntv     = (cntv < 0 || cntv > dlyv) ? dlyv : cntv; /* see k_rv_core */
 	/* this worker's sub-block counter (RVL_G * 64 + 72 <= d: one wrap at most) */
@@ -1445,9 +1448,13 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 	if (w == 0 && n < 8)
 		sm.carry[1][RVL_G - 1][n] = sm.st.fb[n]; /* as the "previous group's" last feedback */
 	const double oneMB = 1.0 - K.blend;
-	double       a0    = 0.0;
-	if ((uint32_t)w < nSub && w < RVL_G)
+	/* the network input two groups ahead: a0 for this group, a0n for the next (an HBM
+	 * load waited for in the same group's read phase would expose its latency) */
+	double a0 = 0.0, a0n = 0.0;
+	if (w < RVL_G && (uint32_t)w < nSub)
 		a0 = a0s[(size_t)w * TBF_SUB + n];
+	if (w < RVL_G && (uint32_t)(RVL_G + w) < nSub)
+		a0n = a0s[(size_t)(RVL_G + w) * TBF_SUB + n];
 	__syncthreads ();
 	TBF_MARK (14);
 #pragma unroll 1
@@ -1457,10 +1464,9 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 		const bool act = w < nb;
 		/* ---- read phase (workers): taps, mix, allpass reads; nothing is written to the
 		 * rings.  The planner plans the next group meanwhile. ---- */
-		double apw[4], ap[4], fb[8];
+		double       apw[4], ap[4], fb[8], mix;
+		const size_t o = ((size_t)g * RVL_G + (uint32_t)w) * TBF_SUB + n;
 		if (act) {
-			const uint32_t s  = g * RVL_G + (uint32_t)w;
-			const size_t   o  = (size_t)s * TBF_SUB + n;
 			const uint32_t om = sm.okm[par][w];
 			double         I[8];
 #pragma unroll RVL_UNROLL
@@ -1470,7 +1476,7 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 					const double Sv = sm.S[par][w][l], Cv = sm.C[par][w][l];
 					sn              = Sv + ((Cv * sm.sd[par][l][n]) - (Sv * sm.cm[par][l][n]));
 				} else {
-					const double dl = K.vibDelta[l];
+					const double dl = rld (vdl, l);
 					double       v  = sm.v0[par][w][l];
 					for (int i = 0; i <= n; i++)
 						v += dl;
@@ -1497,7 +1503,7 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 			fb[5] = (I[5] - (I[4] + I[6] + I[7])) * K.regen;
 			fb[6] = (I[6] - (I[4] + I[5] + I[7])) * K.regen;
 			fb[7] = (I[7] - (I[4] + I[5] + I[6])) * K.regen;
-			const double mix = (I[0] + I[1] + I[2] + I[3] + I[4] + I[5] + I[6] + I[7]) / 8.0;
+			mix = (I[0] + I[1] + I[2] + I[3] + I[4] + I[5] + I[6] + I[7]) / 8.0;
 #pragma unroll
 			for (int l = 8; l < 12; l++) {
 				const int    d   = rl (dlyv, l);
@@ -1509,19 +1515,24 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 				a += old;
 				ap[l - 8] = a;
 			}
-			rv_st (&bout[o], mix);
 			if (n == NL - 1) {
 #pragma unroll
 				for (int l = 0; l < 8; l++)
 					sm.carry[par][w][l] = fb[l];
 			}
-		} else if (w == RVL_G && g + 1 < nGrp) {
-			rvl_plan (sm, K, (int)min ((uint32_t)RVL_G, nSub - (g + 1) * RVL_G), par ^ 1, force, P.errFlags);
+		} else if (w == RVL_G && g + 1 < nGrp && !(RVL_ABL & 1)) {
+			rvl_plan (sm, vdl, (int)min ((uint32_t)RVL_G, nSub - (g + 1) * RVL_G), par ^ 1, force, P.errFlags);
 		}
 		__syncthreads ();
 		TBF_MARK (16);
 		/* ---- write phase ---- */
-		if (act) {
+		if (act && !(RVL_ABL & 4)) {
+			/* the previous sub-block's last feedback, all 8 lines read before any ring write */
+			const double* cp = w == 0 ? sm.carry[par ^ 1][RVL_G - 1] : sm.carry[par][w - 1];
+			double        cprv[8];
+#pragma unroll
+			for (int l = 0; l < 8; l++)
+				cprv[l] = cp[l];
 #pragma unroll
 			for (int l = 8; l < 12; l++)
 				sm.ring[rl (lofv, l) + wrap_slot (rl (cw, l) + n, rl (dlyv, l))] = apw[l - 8];
@@ -1529,14 +1540,16 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 #pragma unroll
 			for (int l = 0; l < 8; l++) {
 				const double up   = lane_shr1 (fb[l]);
-				const double cprv = w == 0 ? sm.carry[par ^ 1][RVL_G - 1][l] : sm.carry[par][w - 1][l];
-				const double prev = n == 0 ? cprv : up;
+				const double prev = n == 0 ? cprv[l] : up;
 				sm.ring[rl (lofv, l) + wrap_slot (rl (cw, l) + n, rl (dlyv, l))] = ap[srcAp[l]] + prev;
 			}
-			/* the next group's input */
-			const uint32_t sn = (g + 1) * RVL_G + (uint32_t)w;
+			/* the tap mix (stored here, a phase after it was formed, so that no wait on the
+			 * store lands in this phase) and the next group's input */
+			rv_st (&bout[o], mix);
+			a0                 = a0n;
+			const uint32_t sn = (g + 2) * RVL_G + (uint32_t)w;
 			if (sn < nSub)
-				a0 = a0s[(size_t)sn * TBF_SUB + n];
+				a0n = a0s[(size_t)sn * TBF_SUB + n];
 		}
 		cw = wrap_slot (cw + TBF_SUB * RVL_G, dlyv);
 		__syncthreads ();
@@ -1550,7 +1563,7 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 			sm.st.fb[n] = sm.carry[(nGrp - 1) & 1][(nSub - 1) % RVL_G][n];
 	}
 	__syncthreads ();
-	for (uint32_t i = tid; i < rlen2; i += RVL_THREADS)
+	for (uint32_t i = tid; i < rlen2 && !(RVL_ABL & 2); i += RVL_THREADS)
 		((double2*)slab)[i] = ((const double2*)sm.ring)[i];
 	if (w == 0)
 		copy_words (S, &sm.st);

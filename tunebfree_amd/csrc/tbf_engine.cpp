@@ -353,6 +353,11 @@ int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
 			for (int p = 0; p < 6; p++)
 				for (int k = 0; k < TBF_NSTAGES; k++)
 					HIPCHK (hipEventCreateWithFlags (&e->pev[p][k], hipEventDisableTiming));
+			for (int k = 0; k < TBF_NSTAGES; k++)
+				HIPCHK (hipEventCreateWithFlags (&e->exEv[k], hipEventDisableTiming));
+			HIPCHK (hipEventCreateWithFlags (&e->coreEv, hipEventDisableTiming));
+			if (const char* rx = getenv ("TBF_RV_EXCL"))
+				e->rvExcl = atoi (rx);
 			/* TBF_STAGE_BUFS=3: a third stage-buffer set, so k_tonegen of chunk c waits for
 			 * chunk c - 3's readers of mid1 instead of chunk c - 2's */
 			const char* sb = getenv ("TBF_STAGE_BUFS");
@@ -460,6 +465,11 @@ int tbf_engine_destroy (tbf_engine* e)
 			(void)hipEventDestroy (e->sdone[k]);
 	if (e->sjoin)
 		(void)hipEventDestroy (e->sjoin);
+	for (hipEvent_t& x : e->exEv)
+		if (x)
+			(void)hipEventDestroy (x);
+	if (e->coreEv)
+		(void)hipEventDestroy (e->coreEv);
 	for (hipEvent_t ev : {e->upEv, e->upEvB})
 		if (ev)
 			(void)hipEventDestroy (ev);
@@ -1677,6 +1687,17 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 				}
 				if (k > 0 && strm (k - 1) != sk)
 					HIPCHK (hipStreamWaitEvent (sk, e->sdone[k - 1], 0));
+				const int excl = (e->rvExcl && P.rvLds && nst > 2) ? e->rvExcl : 0;
+				if (excl && k == 0 && e->coreRec) /* after the last chunk's k_rv_core_lds */
+					HIPCHK (hipStreamWaitEvent (sk, e->coreEv, 0));
+				if (excl == 1 && k == 2) /* k_rv_core_lds alone: after every other stage stream's work */
+					for (int q = 0; q < nst; q++)
+						if (strm (q) != sk) {
+							HIPCHK (hipEventRecord (e->exEv[q], strm (q)));
+							HIPCHK (hipStreamWaitEvent (sk, e->exEv[q], 0));
+						}
+				if (excl == 2 && k == 2) /* ... beside the previous chunk's k_whirl only */
+					HIPCHK (hipStreamWaitEvent (sk, e->sdone[3], 0));
 				for (int r : readers[k])
 					if (r >= 0 && r < nst && strm (r) != sk)
 						HIPCHK (hipStreamWaitEvent (sk, e->pev[(cix + 6 - nbuf) % 6][r], 0));
@@ -1695,6 +1716,10 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 				}
 				HIPCHK (hipEventRecord (e->sdone[k], sk));
 				HIPCHK (hipEventRecord (e->pev[cix % 6][k], sk));
+				if (excl && k == 2) {
+					HIPCHK (hipEventRecord (e->coreEv, sk));
+					e->coreRec = true;
+				}
 			}
 			e->stagesBusy = true;
 			if (delta && (rc = endDelta ()))

@@ -289,6 +289,12 @@ struct tbf_engine {
 	 * waits on chunk c - nbuf's readers of the stage buffers it overwrites and on chunk
 	 * c - 2's last stage for its control region); nbuf stage-buffer sets by chunk index */
 	hipEvent_t                              pev[6][5] = {};
+	/* TBF_RV_EXCL: k_rv_core_lds (a whole CU's LDS per workgroup) runs alone: it waits for
+	 * every other stage stream (exEv) and the next chunk's first stage waits for it (coreEv) */
+	int                                     rvExcl    = 0; /* 1: alone, 2: beside k_whirl only (A/B; 0 measured best) */
+	bool                                    coreRec   = false; /* coreEv recorded at least once */
+	hipEvent_t                              exEv[5]   = {};
+	hipEvent_t                              coreEv    = nullptr;
 	uint32_t                                nbuf      = 2;
 	/* programme table (.pgm), src/program.h:26 MAXPROGS; pgm.controller.offset */
 	std::vector<Programme>                  progs = std::vector<Programme> (129);

@@ -408,6 +408,11 @@ def main():
                     "step_bytes_per_stereo_sample": step_bytes, "step_gbs_per_gpu": step_gbs,
                     "step_frac": step_gbs / HBM_PEAK_GBS,
                     "kernels_ms_per_launch": kern, "kernels_ms_isolated": kern_iso,
+                    "reverb_core": ("k_rv_core_lds: a channel's 12 rings LDS-resident for the launch "
+                                    "(loaded and stored once per 64-block chunk), so its HBM traffic is "
+                                    "far below the algorithmic ring bytes it is quoted against"
+                                    if os.environ.get("TBF_RV_LDS", "1") != "0" else
+                                    "k_rv_core: rings streamed through HBM every sample"),
                     "timing": "HIP events on each launch's stream while neighbouring chunks' "
                               "kernels overlap (cross-chunk pipelining, as in the timed region)"}
         cpu = cpu_baseline(a.cpu_instances, a.cpu_blocks, a.sr) \

@@ -350,7 +350,9 @@ def test_gpu_engine_switches_bitexact(oracle):
     programme change in the second chunk (that chunk's host control falls back to the
     serial loop), rendered in two calls, every switch renders bit-identically to the
     default engine: the serial host loop, the opt-in control stream (three persistent
-    program slots), a third stage-buffer set, the chunk-parity streams, no pipelining.
+    program slots), a third stage-buffer set, the chunk-parity streams, no pipelining,
+    the streaming reverb network kernel (k_rv_core instead of k_rv_core_lds), the LDS
+    kernel run alone or beside k_whirl only, and four stage-group streams.
     Instances without a programme change are also checked against the oracle."""
     import os
     import torch
@@ -378,7 +380,8 @@ def test_gpu_engine_switches_bitexact(oracle):
                 oscen[i].append((b, "param", S.P_DRAWBAR + 6, (i + b) % 9))
     prog_inst = {5, 700}
     switches = [{}, {"TBF_HOST_SERIAL": "1"}, {"TBF_CTL_STREAM": "1"}, {"TBF_STAGE_BUFS": "3"},
-                {"TBF_PIPE_MODE": "0"}, {"TBF_PIPELINE": "0"}]
+                {"TBF_PIPE_MODE": "0"}, {"TBF_PIPELINE": "0"}, {"TBF_RV_LDS": "0"}, {"TBF_RV_EXCL": "1"},
+                {"TBF_RV_EXCL": "2"}, {"TBF_PIPE_GROUPS": "0,1,2,3,3"}]
     outs, cid = [], None
     for env in switches:
         os.environ.update(env)

@@ -1298,6 +1298,7 @@ k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 #ifndef RVL_UNROLL
 #define RVL_UNROLL 8 /* delay lines whose taps a worker computes together (8: 2.39 ms alone, 2: 3.0) */
 #endif
+#define RVL_MIN_BLOCKS 8 /* shorter launches take the streaming k_rv_core */
 #define RVL_RING 16384 /* LDS ring doubles: lines 0..11 of a channel, 8-padded (16,216 at the fixed settings) */
 #define RVL_THREADS (NL * (RVL_G + 1)) /* RVL_G worker waves + the planner wave */
 
@@ -2425,7 +2426,10 @@ extern "C" int tbf_launch_stage (const tbf_launch* P, int k, hipStream_t stream)
 		hipLaunchKernelGGL (k_rv_in<RVIN_IPW>, dim3 ((P->nInst + RVIN_IPW - 1) / RVIN_IPW), block, 0, stream, *P, P->cst,
 		                    P->ctl);
 	else if (k == 2)
-		if (P->rvLds)
+		/* the LDS kernel loads and stores a channel's 129.7 KB of rings per launch; the
+		 * streaming kernel moves 24.6 KB per block: below 8 blocks the streaming one
+		 * moves fewer bytes (real-time periods of one or two blocks) */
+		if (P->rvLds && P->nBlocks >= RVL_MIN_BLOCKS)
 			hipLaunchKernelGGL (k_rv_core_lds, dim3 (2 * P->nInst), dim3 (RVL_THREADS), 0, stream, *P, P->cst);
 		else
 			hipLaunchKernelGGL (k_rv_core, dim3 (2 * P->nInst), block, 0, stream, *P, P->cst);

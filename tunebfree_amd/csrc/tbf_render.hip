@@ -1298,6 +1298,12 @@ k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 #ifndef RVL_UNROLL
 #define RVL_UNROLL 8 /* delay lines whose taps a worker computes together (8: 2.39 ms alone, 2: 3.0) */
 #endif
+/* the network's ring geometry at the reference's fixed settings (reverbConsts: size =
+ * 0.4f^2 * 90 + 10, delay = (int)(dmul * size); rings 8-padded): compile-time constants, so
+ * the ring addressing needs no per-line lane reads; tbf_rv_lds_fits checks an instance
+ * against them */
+constexpr int RVL_DLY[12] = {1927, 1781, 1732, 1634, 1488, 1439, 1293, 1146, 1049, 1000, 902, 756};
+constexpr int RVL_OFS[12] = {0, 1928, 3712, 5448, 7088, 8584, 10024, 11320, 12472, 13528, 14536, 15440};
 #define RVL_MIN_BLOCKS 8 /* shorter launches take the streaming k_rv_core */
 #define RVL_RING 16384 /* LDS ring doubles: lines 0..11 of a channel, 8-padded (16,216 at the fixed settings) */
 #define RVL_THREADS (NL * (RVL_G + 1)) /* RVL_G worker waves + the planner wave */
@@ -1432,9 +1438,8 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 		if (n < 16)
 			(&sm.tabD[0][0])[n] = -1.0;
 	}
-	/* lane l < 12: delay, LDS ring offset and counter of line l */
+	/* lane l < 12: delay and counter of line l (the LDS ring offsets are RVL_OFS) */
 	const int dlyv = n < 12 ? K.delay[n] : 0;
-	const int lofv = n < 12 ? (int)(K.ringOff[c * 13 + n] - rbase) : 0;
 	const double vdl = K.vibDelta[n & 7]; /* lane-held: no vector load of K inside the loop */
 	const uint32_t nSub  = P.nBlocks * (TBF_BLK / TBF_SUB);
 	const uint32_t nGrp  = (nSub + RVL_G - 1) / RVL_G;
@@ -1484,8 +1489,8 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 					sn = sin (v);
 				}
 				const double  off = (sn + 1.0) * K.vibDepth;
-				const int     d   = rl (dlyv, l);
-				const double* rg  = sm.ring + rl (lofv, l);
+				const int     d   = RVL_DLY[l];
+				const double* rg  = sm.ring + RVL_OFS[l];
 				const int     cn  = wrap_slot (rl (cw, l) + n + 1, d);
 				const int     wk  = (int)(cn + off);
 				const double  fr  = off - floor (off);
@@ -1507,8 +1512,8 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 			mix = (I[0] + I[1] + I[2] + I[3] + I[4] + I[5] + I[6] + I[7]) / 8.0;
 #pragma unroll
 			for (int l = 8; l < 12; l++) {
-				const int    d   = rl (dlyv, l);
-				const double old = sm.ring[rl (lofv, l) + wrap_slot (rl (cw, l) + n + 1, d)];
+				const int    d   = RVL_DLY[l];
+				const double old = sm.ring[RVL_OFS[l] + wrap_slot (rl (cw, l) + n + 1, d)];
 				double       a   = a0;
 				a -= old * 0.5;
 				apw[l - 8] = a;
@@ -1536,13 +1541,13 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 				cprv[l] = cp[l];
 #pragma unroll
 			for (int l = 8; l < 12; l++)
-				sm.ring[rl (lofv, l) + wrap_slot (rl (cw, l) + n, rl (dlyv, l))] = apw[l - 8];
+				sm.ring[RVL_OFS[l] + wrap_slot (rl (cw, l) + n, RVL_DLY[l])] = apw[l - 8];
 			const int srcAp[8] = {3, 2, 1, 0, 0, 1, 2, 3};
 #pragma unroll
 			for (int l = 0; l < 8; l++) {
 				const double up   = lane_shr1 (fb[l]);
 				const double prev = n == 0 ? cprv[l] : up;
-				sm.ring[rl (lofv, l) + wrap_slot (rl (cw, l) + n, rl (dlyv, l))] = ap[srcAp[l]] + prev;
+				sm.ring[RVL_OFS[l] + wrap_slot (rl (cw, l) + n, RVL_DLY[l])] = ap[srcAp[l]] + prev;
 			}
 			/* the tap mix (stored here, a phase after it was formed, so that no wait on the
 			 * store lands in this phase) and the next group's input */
@@ -2454,9 +2459,13 @@ extern "C" int tbf_rv_lds_fits (const tbf_inst_const* k)
 {
 	if (k->ringOff[12] - k->ringOff[0] > RVL_RING || k->ringOff[25] - k->ringOff[13] > RVL_RING)
 		return 0;
-	for (int l = 0; l < 12; l++)
-		if (k->delay[l] < RVL_G * TBF_SUB + 72)
+	for (int l = 0; l < 12; l++) {
+		if (k->delay[l] < RVL_G * TBF_SUB + 72 || k->delay[l] != RVL_DLY[l])
 			return 0;
+		for (int c = 0; c < 2; c++)
+			if ((int)(k->ringOff[c * 13 + l] - k->ringOff[c * 13]) != RVL_OFS[l])
+				return 0;
+	}
 	return 1;
 }
 

@@ -36,6 +36,10 @@ ALGO_BYTES = {"k_tonegen": 0, "k_rv_in": 32, "k_rv_core": 384, "k_rv_out": 0, "k
 STEP_ALGO_BYTES = 424  # cfg 3/4/5, bytes per stereo sample of the whole chain
 DOMINANT = "k_rv_core"  # the HBM-streaming kernel the roofline is quoted for
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# MI355X_MICROARCH.md, LDS/L2 gather table: rows shared by every workgroup of an XCD come
+# from its L2 at 16.8-18.8 TB/s chip-wide (measured); the tonegen-only workload's wave-bank
+# gathers are that pattern (one shared bank, every instance reading the same wheels)
+L2_PEAK_GBS = 18800.0
 TRAFFIC_JSON = ROOT / "profiles" / "traffic.json"  # written by tools/traffic_from_pmc.py
 CHUNK = 64  # blocks per launch set (TBF_CHUNK, csrc/tbf_engine.cpp)
 
@@ -381,6 +385,18 @@ def main():
     dry_sum = reduce(chk[0] % (1 << 50), "sum") if a.dry_run else None
     max_err = reduce(max_err or 0.0) if (a.check and not a.dry_run) else None
 
+    bank_entries = None
+    if a.chain == 1 and not a.dry_run:
+        # tonegen only (configs[1]) is L2-bound: every program entry of a
+        # block gathers one wheel's 128 samples from the shared bank, 4 B per entry and
+        # sample.  Entries per block: the device programs of up to 32 instances.
+        import ctypes as C
+        fn = T.load_library().tbf_debug_device_program
+        fn.restype, fn.argtypes = C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]
+        pbuf = np.zeros(9 * 600, np.float32)
+        cnt = [fn(eng._h, i, pbuf.ctypes.data, 600) for i in range(0, B, max(1, B // 32))]
+        bank_entries = float(np.mean([c for c in cnt if c >= 0])) if cnt else None
+
     if rank == 0:
         samples_launch = B * min(a.blocks, CHUNK) * 128  # stereo samples one launch of a stage renders
         algo = dict(ALGO_BYTES)
@@ -415,6 +431,15 @@ def main():
                                     "k_rv_core: rings streamed through HBM every sample"),
                     "timing": "HIP events on each launch's stream while neighbouring chunks' "
                               "kernels overlap (cross-chunk pipelining, as in the timed region)"}
+        if roof is not None and bank_entries is not None and "k_tonegen" in kern:
+            l2b = 4.0 * bank_entries  # L2 bytes per (mono = stereo) sample
+            l2a = samples_launch * l2b / (kern["k_tonegen"] * 1e-3) / 1e9
+            roof.update({"bound": "l2", "achieved": l2a, "peak": L2_PEAK_GBS, "frac": l2a / L2_PEAK_GBS,
+                         "kernel": "k_tonegen", "kernel_ms_per_launch": kern["k_tonegen"],
+                         "algorithmic_bytes_per_launch": samples_launch * l2b, "bytes_per_stereo_sample": l2b,
+                         "bank_entries_per_block": bank_entries,
+                         "note": "tonegen only: the wave-bank gathers, 4 B x program entries per sample, "
+                                 "from the shared L2-resident bank; HBM moves only the 8 B output"})
         cpu = cpu_baseline(a.cpu_instances, a.cpu_blocks, a.sr) \
             if (a.cpu_baseline and world == 1 and a.workload == "cfg3" and not a.dry_run) else None
         line = {

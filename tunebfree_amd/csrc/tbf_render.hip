@@ -1278,19 +1278,22 @@ k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
  * instead of 16 B per line and sample streamed through HBM).  One workgroup of RVL_G
  * waves per (instance, channel), one workgroup per CU (the rings fill its LDS).
  *
- * Why RVL_G sub-blocks can run at once: a sample's ring reads (taps at slot count+1+off,
- * off <= 2 vibDepth + 1 < 8, allpass reads at count+1) return values written >= d - 71
- * samples earlier, d >= 756 at the reference's fixed settings (reverbConsts; the host
- * checks d >= RVL_G * 64 + 72).  So the RVL_G * 64 = 512 samples of a group read only
- * slots that no sample of the group writes (the slot distance between any read and any
- * write of the group lies in 2 .. 520 < d + 1), and all reads of a group may precede
- * all its writes, exactly as k_rv_core's reads of a sub-block precede its writes.  The
+ * Why RVL_G sub-blocks can run at once: a sample at time t reads, on a delay line of
+ * delay d, the value written at time t + j - d: taps at slot count+1+j (j <= 71, the
+ * window; off < 8 in fact), allpasses at count+1 (j = 0).  With 64 RVL_G <= d on the
+ * allpass lines (d >= 756) and 64 RVL_G + 72 <= d on the tap lines (d >= 1146) at the
+ * reference's fixed settings (the host checks both, tbf_rv_lds_fits), every read of a
+ * group of RVL_G sub-blocks returns a value written before the group, and a write of
+ * the group only ever replaces a value that the group's earlier samples read.  So all
+ * reads of a group may precede all its writes, exactly as k_rv_core's reads of a
+ * sub-block precede its writes; a worker's writes wait (barrier) for the reads of the
+ * 72 samples before its first, which lie in the previous worker's sub-block.  The
  * one serial term, feedback(n - 1), crosses sub-blocks through LDS (carry) between the
  * read phase and the write phase.  Per sub-block the arithmetic is k_rv_core's: the
  * same phases (closed form v0 + (n+1) D with the same start phases, or the literal
  * recurrence), the same sine rows, taps, Householder mix and allpasses. */
 #ifndef RVL_G
-#define RVL_G 10 /* sub-blocks (worker waves) per group: RVL_G * 64 + 72 <= the shortest delay (756) */
+#define RVL_G 11 /* sub-blocks (worker waves) per group: 64 RVL_G <= the shortest allpass delay (756), 64 RVL_G + 72 <= the shortest tap-line delay (1146) */
 #endif
 #ifndef RVL_ABL
 #define RVL_ABL 0 /* timing-only ablations of k_rv_core_lds: 1 no planning after the first group, 2 no ring load/store, 4 no write phase */
@@ -1449,7 +1452,7 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 		rvl_plan (sm, vdl, (int)min ((uint32_t)RVL_G, nSub), 0, force, P.errFlags);
 	int cntv = n < 12 ? sm.st.count[n] : 0;
 	cntv     = (cntv < 0 || cntv > dlyv) ? dlyv : cntv; /* see k_rv_core */
-	/* this worker's sub-block counter (RVL_G * 64 + 72 <= d: one wrap at most) */
+	/* this worker's sub-block counter (64 RVL_G <= d: one wrap at most) */
 	int cw = wrap_slot (cntv + TBF_SUB * (w < RVL_G ? w : 0), dlyv);
 	if (w == 0 && n < 8)
 		sm.carry[1][RVL_G - 1][n] = sm.st.fb[n]; /* as the "previous group's" last feedback */
@@ -2460,7 +2463,9 @@ extern "C" int tbf_rv_lds_fits (const tbf_inst_const* k)
 	if (k->ringOff[12] - k->ringOff[0] > RVL_RING || k->ringOff[25] - k->ringOff[13] > RVL_RING)
 		return 0;
 	for (int l = 0; l < 12; l++) {
-		if (k->delay[l] < RVL_G * TBF_SUB + 72 || k->delay[l] != RVL_DLY[l])
+		/* a group's reads must find only data written before the group: tap lines read up
+		 * to 71 slots past count+1, the allpasses read count+1 */
+		if (k->delay[l] < RVL_G * TBF_SUB + (l < 8 ? 72 : 0) || k->delay[l] != RVL_DLY[l])
 			return 0;
 		for (int c = 0; c < 2; c++)
 			if ((int)(k->ringOff[c * 13 + l] - k->ringOff[c * 13]) != RVL_OFS[l])

@@ -642,6 +642,37 @@ def test_gpu_pipelined_chunks_across_calls(oracle):
     assert max(eL, eR) <= TOL
 
 
+def test_gpu_reverb_network_group_boundaries(oracle):
+    """k_rv_core_lds runs a launch in groups of eleven 64-sample sub-blocks, and launches
+    of fewer than 8 blocks use k_rv_core; both keep the same ring and counter state.
+    Render calls of 7, 8, 11, 12, 17, 22 and 33 blocks (14 sub-blocks on k_rv_core, then
+    16 = 11 + 5, 22 = 2 x 11, 24 = 22 + 2, 34 = 33 + 1, 44 = 4 x 11, 66 = 6 x 11) switch
+    kernels and end groups at every offset pattern: bit-identical to the oracle, and to an
+    engine that runs k_rv_core throughout (TBF_RV_LDS=0)."""
+    import os
+    calls = [7, 8, 11, 12, 17, 22, 33]
+    outs = []
+    for env in ({}, {"TBF_RV_LDS": "0"}):
+        os.environ.update(env)
+        try:
+            eng, tpl, seeds, scens = _setup(oracle, 6, S.bench_scenario)
+        finally:
+            for k in env:
+                os.environ.pop(k, None)
+        parts = [engine_run(eng, scens, 1)]  # block 0 carries the scenario's events
+        parts += [eng.render(nb) for nb in calls]
+        eng.close()
+        outs.append((np.concatenate([p[0] for p in parts], axis=1), np.concatenate([p[1] for p in parts], axis=1)))
+    total = 1 + sum(calls)
+    oL, oR, *_ = oracle_run(oracle, tpl, seeds, scens, total)
+    eL, xL = compare(outs[0][0], oL)
+    eR, xR = compare(outs[0][1], oR)
+    print(f"group boundaries: {total} blocks, max|err| L={eL:.3g} R={eR:.3g} bit-exact L={xL:.6f} R={xR:.6f}")
+    assert max(eL, eR) <= TOL
+    for a, b in zip(outs[0], outs[1]):
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
 def test_gpu_full_size_bench_batch(oracle):
     """BASELINE configs[2] at its full size (4096 instances x 64 blocks, one call, the
     bench's render): instances spread over the whole batch (both ends and the middle of

@@ -1464,6 +1464,9 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 		a0 = a0s[(size_t)w * TBF_SUB + n];
 	if (w < RVL_G && (uint32_t)(RVL_G + w) < nSub)
 		a0n = a0s[(size_t)(RVL_G + w) * TBF_SUB + n];
+	double pmix = 0.0; /* the previous group's tap mix, stored a group late */
+	size_t po   = 0;
+	bool   pst  = false;
 	__syncthreads ();
 	TBF_MARK (14);
 #pragma unroll 1
@@ -1475,6 +1478,14 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 		 * rings.  The planner plans the next group meanwhile. ---- */
 		double       apw[4], ap[4], fb[8], mix;
 		const size_t o = ((size_t)g * RVL_G + (uint32_t)w) * TBF_SUB + n;
+		/* HBM traffic at the start of the group, a whole group ahead of any wait on it: the
+		 * input two groups ahead (every wave, the index clamped, so that no branch joins
+		 * the loaded register) and the previous group's tap mix.  Issued at the end of
+		 * the write phase, the copy a0n <- load at the loop's back edge waited for the
+		 * load, and for the store, right away. */
+		const double nxt = a0s[(size_t)min ((g + 2) * RVL_G + (uint32_t)min (w, RVL_G - 1), nSub - 1) * TBF_SUB + n];
+		if (pst)
+			rv_st (&bout[po], pmix);
 		if (act) {
 			const uint32_t om = sm.okm[par][w];
 			double         I[8];
@@ -1552,18 +1563,19 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 				const double prev = n == 0 ? cprv[l] : up;
 				sm.ring[RVL_OFS[l] + wrap_slot (rl (cw, l) + n, RVL_DLY[l])] = ap[srcAp[l]] + prev;
 			}
-			/* the tap mix (stored here, a phase after it was formed, so that no wait on the
-			 * store lands in this phase) and the next group's input */
-			rv_st (&bout[o], mix);
-			a0                 = a0n;
-			const uint32_t sn = (g + 2) * RVL_G + (uint32_t)w;
-			if (sn < nSub)
-				a0n = a0s[(size_t)sn * TBF_SUB + n];
+			/* the tap mix, stored at the start of the next group (see above) */
+			pmix = mix;
+			po   = o;
 		}
+		pst = act && !(RVL_ABL & 4);
+		a0  = a0n;
+		a0n = nxt;
 		cw = wrap_slot (cw + TBF_SUB * RVL_G, dlyv);
 		__syncthreads ();
 		TBF_MARK (17);
 	}
+	if (pst)
+		rv_st (&bout[po], pmix);
 	/* state: counters after nSub * 64 steps, the last sample's feedback */
 	if (w == 0) {
 		if (n < 12)

@@ -1419,43 +1419,50 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 	const double*         a0s   = rv_buf (P.rvA, P, inst, c);
 	double*               bout  = rv_buf (P.rvB, P, inst, c);
 	prof_begin (P, sm);
-	/* rings and state to LDS: every load in flight before the first LDS store (clamped
-	 * indices keep the loads unconditional) */
-	{
-		constexpr int NR = (RVL_RING / 2 + RVL_THREADS - 1) / RVL_THREADS;
-		double2       v[NR];
-#pragma unroll
-		for (int k = 0; k < NR; k++) {
-			const uint32_t i = tid + k * RVL_THREADS;
-			v[k]             = (RVL_ABL & 2) ? double2 {0.0, 0.0} : ((const double2*)slab)[i < rlen2 ? i : 0];
-		}
-#pragma unroll
-		for (int k = 0; k < NR; k++) {
-			const uint32_t i = tid + k * RVL_THREADS;
-			if (i < rlen2)
-				((double2*)sm.ring)[i] = v[k];
-		}
-	}
-	if (w == 0) { /* copy_words: threads 0..63 */
-		copy_words (&sm.st, S);
-		if (n < 16)
-			(&sm.tabD[0][0])[n] = -1.0;
-	}
 	/* lane l < 12: delay and counter of line l (the LDS ring offsets are RVL_OFS) */
 	const int dlyv = n < 12 ? K.delay[n] : 0;
 	const double vdl = K.vibDelta[n & 7]; /* lane-held: no vector load of K inside the loop */
 	const uint32_t nSub  = P.nBlocks * (TBF_BLK / TBF_SUB);
 	const uint32_t nGrp  = (nSub + RVL_G - 1) / RVL_G;
 	const bool     force = (P.dbg & TBF_DEBUG_FORCE_SERIAL) != 0;
+	if (w < RVL_G) {
+		/* the workers load the rings: every load in flight before the first LDS store
+		 * (clamped indices keep the loads unconditional) */
+		constexpr int WT = NL * RVL_G;
+		constexpr int NR = (RVL_RING / 2 + WT - 1) / WT;
+		double2       v[NR];
+#pragma unroll
+		for (int k = 0; k < NR; k++) {
+			const uint32_t i = tid + k * WT;
+			v[k]             = (RVL_ABL & 2) ? double2 {0.0, 0.0} : ((const double2*)slab)[i < rlen2 ? i : 0];
+		}
+#pragma unroll
+		for (int k = 0; k < NR; k++) {
+			const uint32_t i = tid + k * WT;
+			if (i < rlen2)
+				((double2*)sm.ring)[i] = v[k];
+		}
+	} else {
+		/* meanwhile the planner loads the channel state and plans the first group, which
+		 * reads no ring */
+		const uint32_t* src = (const uint32_t*)S;
+		uint32_t*       dst = (uint32_t*)&sm.st;
+		for (uint32_t i = (uint32_t)n; i < sizeof (tbf_rv_chan) / 4; i += NL)
+			dst[i] = src[i];
+		if (n < 16)
+			(&sm.tabD[0][0])[n] = -1.0;
+		__builtin_amdgcn_fence (__ATOMIC_SEQ_CST, "wavefront");
+		__builtin_amdgcn_wave_barrier ();
+		if (n < 8)
+			sm.carry[1][RVL_G - 1][n] = sm.st.fb[n]; /* as the "previous group's" last feedback */
+		if (nGrp > 0)
+			rvl_plan (sm, vdl, (int)min ((uint32_t)RVL_G, nSub), 0, force, P.errFlags);
+	}
 	__syncthreads ();
-	if (w == RVL_G && nGrp > 0)
-		rvl_plan (sm, vdl, (int)min ((uint32_t)RVL_G, nSub), 0, force, P.errFlags);
 	int cntv = n < 12 ? sm.st.count[n] : 0;
 	cntv     = (cntv < 0 || cntv > dlyv) ? dlyv : cntv; /* see k_rv_core */
 	/* this worker's sub-block counter (64 RVL_G <= d: one wrap at most) */
 	int cw = wrap_slot (cntv + TBF_SUB * (w < RVL_G ? w : 0), dlyv);
-	if (w == 0 && n < 8)
-		sm.carry[1][RVL_G - 1][n] = sm.st.fb[n]; /* as the "previous group's" last feedback */
 	const double oneMB = 1.0 - K.blend;
 	/* the network input two groups ahead: a0 for this group, a0n for the next (an HBM
 	 * load waited for in the same group's read phase would expose its latency) */

@@ -28,12 +28,11 @@ sys.path.insert(0, str(ROOT / "tests"))
 # Only what the algorithm itself must move counts: the reverb's 13 delay lines x 2
 # channels streamed once per cycle (8 B write + 8 B read, FP64) and the 8 B L/R output.
 #   k_rv_core = the 12 network lines (A..L) x 2 ch x 16 B              = 384 B
-#   k_rv_in   = the predelay line M x 2 ch x 16 B                      =  32 B
+#   k_rv_pre  = the predelay line M x 2 ch x 16 B                      =  32 B
 #   k_whirl   = L/R float32 output                                     =   8 B
-# The implementation's inter-stage streams (mid1/rvA/rvB/mid2, 92 B) are NOT algorithmic;
-# they show up in the PMC `traffic` figure instead.  Step total: 424 B.
-ALGO_BYTES = {"k_tonegen": 0, "k_rv_in": 32, "k_rv_core": 384, "k_rv_out": 0, "k_whirl": 8}
-STEP_ALGO_BYTES = 424  # cfg 3/4/5, bytes per stereo sample of the whole chain
+# The implementation's inter-stage streams (mid1/rvA/rvB/mid2) are NOT algorithmic; they
+# show up in the PMC `traffic` figure instead.  Step total: 424 B.
+ALGO_BYTES = {"k_tonegen": 0, "k_rv_pre": 32, "k_rv_core": 384, "k_rv_post": 0, "k_whirl": 8}
 DOMINANT = "k_rv_core"  # the HBM-streaming kernel the roofline is quoted for
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # MI355X_MICROARCH.md, LDS/L2 gather table: rows shared by every workgroup of an XCD come
@@ -413,10 +412,14 @@ def main():
                         and dom in tj.get("kernels", {}):
                     traffic = tj["kernels"][dom]["bytes_per_launch"]
                     traffic_src = tj.get("source")
-            step_bytes = STEP_ALGO_BYTES if a.chain == 0 else sum(algo.values())
+            # the algorithmic bytes of the kernels this chain mode runs (424 B for the full chain)
+            step_bytes = sum(algo[k] for k in kern)
             step_gbs = B * nsamp * step_bytes / (elapsed / a.steps) / 1e9  # per GPU
+            ms = kern[dom]
             roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                    # the HBM bytes the kernel really moves (PMC) over the same time
+                    "hbm_frac_actual": (traffic / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
                     "kernel": dom, "kernel_ms_per_launch": kern[dom],
                     "algorithmic_bytes_per_launch": samples_launch * algo[dom],
                     "bytes_per_stereo_sample": algo[dom], "traffic_source": traffic_src,
@@ -429,6 +432,10 @@ def main():
                                     "far below the algorithmic ring bytes it is quoted against"
                                     if os.environ.get("TBF_RV_LDS", "1") != "0" else
                                     "k_rv_core: rings streamed through HBM every sample"),
+                    "limited_by": ("not HBM: latency of the per-sample network (LDS tap reads, two "
+                                   "barriers per 704-sample group) at one 12-wave workgroup per CU, and "
+                                   "waiting for whole CUs to drain beside the other stages (hbm_frac_actual)"
+                                   if dom == "k_rv_core" and os.environ.get("TBF_RV_LDS", "1") != "0" else None),
                     "timing": "HIP events on each launch's stream while neighbouring chunks' "
                               "kernels overlap (cross-chunk pipelining, as in the timed region)"}
         if roof is not None and bank_entries is not None and "k_tonegen" in kern:

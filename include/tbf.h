@@ -266,14 +266,11 @@ int tbf_debug_control (tbf_engine* e, uint32_t inst, double* out, uint32_t cap);
  * hits), op 5 glibc rand() jump (in: seed, k, - -> out: next draw after GlibcRand::discard
  * (k), after k literal draws); n records */
 int tbf_debug_exact (int32_t op, const double* in3, double* out2, uint32_t n);
-/* stage timing: enable 1 zeroes per-instance counters and turns the kernel's marks on;
- * 0 copies out [inst][32] cycle sums (returns the count); -1 turns the marks off */
-int tbf_debug_profile (tbf_engine* e, int32_t enable, uint64_t* out, uint32_t cap);
 /* per-stage kernel timing with HIP events on each launch's stream: enable 1 / -1 turns
  * recording on / off (1: as rendered, launches of neighbouring chunks overlapping; 2:
  * with the cross-chunk pipelining off, each kernel alone on the GPU); 0 returns the
- * summed milliseconds and launch counts of the five stage kernels k_tonegen, k_rv_in,
- * k_rv_core, k_rv_out, k_whirl since the last query (ms5[5], count5[5]) */
+ * summed milliseconds and launch counts of the five stage kernels k_tonegen, k_rv_pre,
+ * k_rv_core, k_rv_post, k_whirl since the last query (ms5[5], count5[5]) */
 int tbf_debug_kernel_times (tbf_engine* e, int32_t enable, double* ms5, uint32_t* count5);
 /* PMC calibration: op 0 streams n doubles from d_buf (8 B/lane reads, the reverb ring
  * pattern), op 1 writes them; enqueued on `stream` (NULL = legacy default stream) */

@@ -65,14 +65,14 @@ def test_gpu_full_chain_bench(oracle):
 
 
 def test_gpu_full_chain_odd_batch_mixed_scenarios(oracle):
-    """k_rv_in and k_rv_out serve two instances per wave: an odd batch leaves the last
-    wave with one, and neighbouring instances with different scripts (events, a quiet
-    one, reverb-heavy) must not leak into each other."""
+    """k_rv_pre and k_rv_post serve 32 instances per workgroup (a chain per lane): a batch
+    of 37 leaves the second workgroup with 5, and neighbouring instances with different
+    scripts (events, quiet ones, reverb-heavy) must not leak into each other."""
     def scen(i):
-        if i == 2:
-            return []  # silent instance between two playing ones
+        if i in (2, 33):
+            return []  # silent instances between playing ones
         return S.event_scenario(i) if i % 2 else S.bench_scenario(i)
-    eng, tpl, seeds, scens = _setup(oracle, 5, scen)
+    eng, tpl, seeds, scens = _setup(oracle, 37, scen)
     L, R = engine_run(eng, scens, 40)
     oL, oR, *_ = oracle_run(oracle, tpl, seeds, scens, 40)
     eL, xL = compare(L, oL)

@@ -69,7 +69,7 @@ int tbf::fail (int code, const std::string& msg)
 /* control pool region (one per chunk parity on the device-controlled path; the host path
  * uses region 0): n persistent entries + up to one delta per instance and block */
 #define CTL_REGION(n) ((size_t)(n) * (TBF_CHUNK + 1))
-#define TBF_NSTAGES 5 /* k_tonegen, k_rv_in, k_rv_core, k_rv_out, k_whirl */
+#define TBF_NSTAGES 5 /* k_tonegen, k_rv_pre, k_rv_core, k_rv_post, k_whirl */
 
 /* ------------------------------------------------------------------ construction */
 
@@ -111,7 +111,10 @@ static void reverbConsts (tbf_inst_const& k, double sr, float A, float B, float 
 	for (int c = 0; c < 2; c++)
 		for (int l = 0; l < 13; l++) {
 			k.ringOff[c * 13 + l] = o;
-			o += (uint32_t)((k.delay[l] + 1 + 7) & ~7);
+			/* line 12 of channel 0 holds the predelay history (TBF_PD_HIST floats) instead
+			 * of a ring; channel 1's stays unused */
+			const int len = (l == 12 && c == 0) ? std::max (k.delay[l] + 1, TBF_PD_HIST / 2) : k.delay[l] + 1;
+			o += (uint32_t)((len + 7) & ~7);
 		}
 	k.slabLen = o;
 }
@@ -658,11 +661,14 @@ int tbf_instances_add (tbf_engine* e, uint32_t n, const uint32_t* tpl_ids, const
 			f = (uint32_t)rnd.next () * 0xFFFFFFFFu;
 		in.s0.tg.odFpd  = f;
 		in.s0.tg.fpFlip = 1;
-		in.s0.rv.countM = 1;
+		in.s0.rv.pdAge = 0; /* countM = 1 and zeroed rings: the first delayM outputs are 0 */
+		in.s0.rv.pdPos = 0;
 		for (int c = 0; c < 2; c++)
 			for (int l = 0; l < 12; l++)
 				in.s0.rv.ch[c].count[l] = 1;
 		reverbConsts (in.k, sr, 1.0f, 0.2f, 0.0f, 0.0f, 0.4f, 0.8f);
+		if (in.k.delay[12] < 0 || in.k.delay[12] >= TBF_PD_HIST) /* 560 at the fixed settings */
+			return fail (-22, "predelay longer than its history");
 		whirlConsts (in.k, e->wt, e->conf);
 		in.rvG      = e->conf.reverbMix;  /* reverbConfig: setReverbMix */
 		in.whBypass = e->conf.bypass;     /* whirlConfig: whirl.bypass */
@@ -1353,7 +1359,6 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 	P.slabLen   = e->slabLen;
 	P.errFlags  = e->err.p;
 	P.dbg       = e->cfg.debug_flags;
-	P.prof      = e->profOn ? e->prof.p : nullptr;
 	P.rvLds     = e->rvLdsOn && e->rvLdsFit;
 	/* inter-stage buffers: nbuf sets by chunk index (2: alternate chunks; 3 with the
 	 * stage-group streams), see the pipelining below */
@@ -1372,11 +1377,11 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 	 * stage k of chunk c-1 (event sdone[k], the other stream); its output buffer parity
 	 * c % 2 was last read by chunk c-2 on the same stream.  The kernels of neighbouring
 	 * chunks (and of consecutive render calls) then fill each other's tails on the GPU.
-	 * Used for the full chain on chunks without control uploads; uploads, tap modes and
-	 * the profiling hook run on the caller's stream after joining.  With
+	 * Used for the full chain on chunks without control uploads; uploads and tap modes
+	 * run on the caller's stream after joining.  With
 	 * tbf_debug_kernel_times on, each launch is bracketed by events on its own stream
 	 * (durations then include the overlap with the other stream's kernels). */
-	const bool   pipe  = e->pipeline && e->cfg.chain_mode == TBF_CHAIN_FULL && !e->profOn && !e->timeSerial;
+	const bool   pipe  = e->pipeline && e->cfg.chain_mode == TBF_CHAIN_FULL && !e->timeSerial;
 	bool         outWait = false; /* the output stage has waited for the caller's stream */
 	const size_t dprogCap = DPROG_CAP (n);
 	e->chg.assign (n, 0);
@@ -1668,7 +1673,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			 * soon as this chunk's previous stage and the previous chunk's same stage are
 			 * done, whatever the later stages of the previous chunk are doing.  Buffer parity
 			 * par was last read by the chunk before last: wait for those readers (stage k's
-			 * output mid1 is read by k_rv_in and k_rv_out, rvA by k_rv_core, rvB by k_rv_out,
+			 * output mid1 is read by k_rv_pre and k_rv_post, rvA by k_rv_core, rvB by k_rv_post,
 			 * mid2 by k_whirl) when they run on another stream. */
 			static const int readers[5][2] = {{1, 3}, {2, -1}, {3, -1}, {4, -1}, {-1, -1}};
 			auto strm = [&] (int k) { const int g = e->grp[k]; return g < 2 ? e->sstr[g] : g == 2 ? e->gstr3 : e->gstrM[g - 3]; };
@@ -2025,35 +2030,6 @@ int tbf_debug_render_program (tbf_engine* e, uint32_t i, float* out, uint32_t ca
 		o[3] = p.sg; o[4] = p.pg; o[5] = p.vg; o[6] = p.nsg; o[7] = p.npg; o[8] = p.nvg;
 	}
 	return (int)prog.size ();
-}
-
-int tbf_debug_profile (tbf_engine* e, int32_t enable, uint64_t* out, uint32_t cap)
-{
-	if (!e)
-		return fail (-22, "null engine");
-	const size_t n = (size_t)e->inst.size () * TBF_PROF_SLOTS;
-	if (enable == 1) {
-		if (e->cfg.device < 0)
-			return fail (-19, "host-only engine");
-		HIPCHK (hipSetDevice (e->cfg.device));
-		if (e->prof.ensure (n))
-			return fail (-12, "out of device memory");
-		HIPCHK (hipMemset (e->prof.p, 0, n * sizeof (uint64_t)));
-		e->profOn = true;
-		return 0;
-	}
-	if (enable == 0) {
-		if (!e->profOn)
-			return fail (-22, "profiling not enabled");
-		HIPCHK (hipStreamSynchronize (e->stream));
-		HIPCHK (hipDeviceSynchronize ());
-		const size_t m = std::min<size_t> (n, cap);
-		if (out && m)
-			HIPCHK (hipMemcpy (out, e->prof.p, m * sizeof (uint64_t), hipMemcpyDeviceToHost));
-		return (int)n;
-	}
-	e->profOn = false;
-	return 0;
 }
 
 int tbf_debug_exact (int32_t op, const double* in, double* out, uint32_t n)

@@ -237,8 +237,6 @@ struct tbf_engine {
 	DevBuf<uint32_t>                        xsj; /* xorshift32 jump table */
 	DevBuf<float>                           whTab, whBw;
 	DevBuf<uint32_t>                        err;
-	DevBuf<uint64_t>                        prof; /* tbf_debug_profile */
-	bool                                    profOn = false;
 	/* tbf_debug_kernel_times: HIP events around every stage launch */
 	bool                                    timeOn = false;
 	bool                                    timeSerial = false; /* time with pipelining off */

@@ -33,137 +33,13 @@
 #define NL 64
 
 /* occupancy targets (waves per SIMD); LDS and VGPR budgets are sized for them */
-#ifndef TG_WAVES
 #define TG_WAVES 4
-#endif
-#ifndef RV_WAVES
 #define RV_WAVES 3
-#endif
-#ifndef RVIO_WAVES
-#define RVIO_WAVES 4
-#endif
-#ifndef WH_WAVES
 #define WH_WAVES 3
-#endif
-#ifndef RV_PAD
-#define RV_PAD 2 /* doubles of padding per serial-chain LDS row (rows read together by lanes 0..3 on distinct banks) */
-#endif
-#ifndef RV_NT
-#define RV_NT 2 /* k_rv_core streaming accesses nontemporal: 2 ring and tap-mix stores (kept), 1 loads too (k_rv_core 2.94 -> 4.23 ms) */
-#endif
-#ifndef STREAM_NT
-#define STREAM_NT 0 /* stage-stream stores (mid1, rvA, mid2, output, predelay ring) nontemporal */
-#endif
-#ifndef XS_NIB
-#define XS_NIB 1 /* dither jumps from the nibble-sliced table: 8 coalesced loads per state */
-#endif
-#ifndef RVIN_IPW
-#define RVIN_IPW 2 /* k_rv_in instances per wave (their biquadA chains share one serial pass) */
-#endif
-#ifndef RVOUT_IPW
-#define RVOUT_IPW 2 /* k_rv_out instances per wave (their biquadB/C chains share one serial pass) */
-#endif
-#ifndef SERIAL_PRIO
-#define SERIAL_PRIO 1 /* wave priority raised (s_setprio) while a wave runs a serial chain */
-#endif
-#ifndef WH_PRIO
-#define WH_PRIO 0 /* the same for k_whirl's filter pass (measured slightly slower: 4.47-4.50 vs 4.52e9) */
-#ifndef RV_CORE_PRIO
-#define RV_CORE_PRIO 0 /* wave priority of k_rv_core for its whole run (the pipelined step's critical stream) */
-#endif
-#endif
-#define PRIO_UP()                                  \
-	do {                                           \
-		if (SERIAL_PRIO)                           \
-			__builtin_amdgcn_s_setprio (SERIAL_PRIO); \
-	} while (0)
-#define PRIO_DOWN()                        \
-	do {                                   \
-		if (SERIAL_PRIO)                   \
-			__builtin_amdgcn_s_setprio (0); \
-	} while (0)
-#ifndef RV_TAP_UNROLL
-#define RV_TAP_UNROLL 2 /* k_rv_core delay lines whose taps are computed together */
-#endif
-#ifndef WH_SB_UNROLL
-#define WH_SB_UNROLL 1 /* k_whirl sub-blocks of a block unrolled */
-#endif
-#ifndef WH_MG
-#define WH_MG 4 /* k_whirl rings whose motions are computed before their adds */
-#endif
-#ifndef WH_RING_UNROLL
-#define WH_RING_UNROLL 4 /* k_whirl rings whose motions are computed together */
-#endif
-#ifndef TG_UNROLL
-#define TG_UNROLL 4 /* program entries of the tonegen interpreter in flight */
-#endif
-
-/* timing-only ablations (wrong results; tools/gpu_ab.sh variants): bit 0 waveshaper sin,
- * 1 vibrato gather, 2 tonegen serial chains, 3 overdrive dither jumps, 4 whirl ring
- * accumulation, 5 whirl serial filters, 6 whirl motion table loads, 7 reverb biquad
- * chains */
-#ifndef TBF_ABL
-#define TBF_ABL 0
-#endif
-
-/* optional stage timing (tbf_debug_profile): wave-clock cycles accumulated per mark.
- * Compiled in only with -DTBF_STAGE_PROF=1 (tools/prof_stages.py builds such a variant):
- * the product kernels keep their LDS for co-resident workgroups of the other chunk. */
-#ifndef TBF_STAGE_PROF
-#define TBF_STAGE_PROF 0
-#endif
-#if TBF_STAGE_PROF
-#define TBF_PROF_LDS                                                                     \
-	unsigned long long prof[TBF_PROF_SLOTS];                                             \
-	unsigned long long plast;
-#define TBF_MARK(k)                                                                      \
-	do {                                                                                 \
-		if (P.prof) {                                                                    \
-			__syncthreads ();                                                            \
-			if (threadIdx.x == 0) {                                                      \
-				const unsigned long long _t = __builtin_amdgcn_s_memtime ();              \
-				sm.prof[k] += _t - sm.plast;                                             \
-				sm.plast = _t;                                                           \
-			}                                                                            \
-			__syncthreads ();                                                            \
-		}                                                                                \
-	} while (0)
-
-template <typename L>
-__device__ __forceinline__ void prof_begin (const tbf_launch& P, L& sm)
-{
-	if (P.prof) {
-		if (threadIdx.x < TBF_PROF_SLOTS)
-			sm.prof[threadIdx.x] = 0;
-		if (threadIdx.x == 0)
-			sm.plast = __builtin_amdgcn_s_memtime ();
-	}
-}
-
-template <typename L>
-__device__ __forceinline__ void prof_end (const tbf_launch& P, L& sm, uint32_t inst)
-{
-	if (P.prof && threadIdx.x < TBF_PROF_SLOTS)
-		P.prof[(size_t)inst * TBF_PROF_SLOTS + threadIdx.x] += sm.prof[threadIdx.x];
-}
-#else
-#define TBF_PROF_LDS
-#define TBF_MARK(k) \
-	do {        \
-	} while (0)
-template <typename L> __device__ __forceinline__ void prof_begin (const tbf_launch&, L&) {}
-template <typename L> __device__ __forceinline__ void prof_end (const tbf_launch&, L&, uint32_t) {}
-#endif
-
-/* a stage-stream store (STREAM_NT: nontemporal) */
-template <typename T> __device__ __forceinline__ void stream_st (T* p, T v)
-{
-#if STREAM_NT
-	__builtin_nontemporal_store (v, p);
-#else
-	*p = v;
-#endif
-}
+/* wave priority raised (s_setprio 1) while a wave runs a serial chain, so the SIMD issues
+ * the chain's dependent instructions ahead of other waves' lane-parallel work */
+#define PRIO_UP() __builtin_amdgcn_s_setprio (1)
+#define PRIO_DOWN() __builtin_amdgcn_s_setprio (0)
 
 /* ------------------------------------------------------------------ LDS layouts */
 struct TgLds {
@@ -192,7 +68,6 @@ struct TgLds {
 			uint32_t fpd[TBF_BLK + 1];
 		} od;
 	} u;
-	TBF_PROF_LDS
 };
 
 
@@ -213,7 +88,6 @@ struct WhLds {
 	float        aOut[TBF_SUB];       /* horn A output of the current sub-block */
 	int          brake;
 	int          aReady;              /* aOut holds the current sub-block's horn A output */
-	TBF_PROF_LDS
 };
 
 /* the control entry of instance `inst` for block `blk` of the chunk: events land at
@@ -235,44 +109,12 @@ __device__ __forceinline__ void copy_words (T* dst, const T* src)
 		d[i] = s[i];
 }
 
-/* the reverb state's shared head (predelay, dither streams, biquad states) without the
- * feedback-network channels, which k_rv_core owns */
-__device__ __forceinline__ void copy_head (tbf_rv_state* dst, const tbf_rv_state* src)
-{
-	const uint32_t* s = (const uint32_t*)src;
-	uint32_t*       d = (uint32_t*)dst;
-	for (uint32_t i = threadIdx.x; i < offsetof (tbf_rv_state, ch) / 4; i += NL)
-		d[i] = s[i];
-}
-
 __device__ __forceinline__ uint32_t xorshift (uint32_t s)
 {
 	s ^= s << 13;
 	s ^= s >> 17;
 	s ^= s << 5;
 	return s;
-}
-
-/* xorshift32 state after k steps from x0 (uniform), k per lane (0 .. 128), by the
- * GF(2) jump table: 32 coalesced row reads, selected by the bits of x0 */
-__device__ __forceinline__ uint32_t xs_jump (const uint32_t* __restrict__ J, uint32_t x0, int k)
-{
-	x0 = __builtin_amdgcn_readfirstlane (x0);
-	/* opaque k: keeps the loop-invariant table loads inside the block loop instead of
-	 * pinning 32 VGPRs for the whole kernel */
-	asm volatile ("" : "+v"(k));
-	uint32_t r = 0;
-#pragma unroll
-	for (int h = 0; h < 32; h += 16) {
-		uint32_t v[16];
-#pragma unroll
-		for (int j = 0; j < 16; j++) /* 16 row loads in flight together */
-			v[j] = J[(h + j) * TBF_XS_JUMP + k];
-#pragma unroll
-		for (int j = 0; j < 16; j++)
-			r ^= ((x0 >> (h + j)) & 1u) ? v[j] : 0u;
-	}
-	return r;
 }
 
 /* xorshift32 state after a per-lane k steps from a uniform x0, from the nibble-sliced table
@@ -286,29 +128,6 @@ __device__ __forceinline__ uint32_t xs_jump_n (const uint32_t* __restrict__ J, u
 	for (int i = 0; i < 8; i++)
 		v[i] = N[(i * 16 + ((x0 >> (4 * i)) & 15u)) * TBF_XS_JUMP + k];
 	return ((v[0] ^ v[1]) ^ (v[2] ^ v[3])) ^ ((v[4] ^ v[5]) ^ (v[6] ^ v[7]));
-}
-
-/* xs_jump with the lane's 32 table entries (rows j, column k) already in registers */
-__device__ __forceinline__ uint32_t xs_jump_reg (const uint32_t* jr, uint32_t x0)
-{
-	x0         = __builtin_amdgcn_readfirstlane (x0);
-	uint32_t r = 0;
-#pragma unroll
-	for (int j = 0; j < 32; j++)
-		r ^= ((x0 >> j) & 1u) ? jr[j] : 0u;
-	return r;
-}
-
-/* xorshift32 state after a uniform k steps from a per-lane x: column k of the table is
- * uniform, so its 32 words come in as scalar loads */
-__device__ __forceinline__ uint32_t xs_jump_u (const uint32_t* __restrict__ J, uint32_t x, int k)
-{
-	asm volatile ("" : "+s"(k));
-	uint32_t r = 0;
-#pragma unroll
-	for (int j = 0; j < 32; j++)
-		r ^= ((x >> j) & 1u) ? J[j * TBF_XS_JUMP + k] : 0u;
-	return r;
 }
 
 __device__ __forceinline__ int wave_min (int v)
@@ -413,7 +232,7 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 	 * equals the reference's copy (CR_CPY). */
 	f2v sw = {-0.f, -0.f}, vb = {-0.f, -0.f}, pc = {-0.f, -0.f};
 	if (!anyEnv) { /* steady program: x * g (src/tonegen.cpp:3667-3685) */
-#pragma unroll TG_UNROLL
+#pragma unroll 4
 		for (int e = 0; e < np; e++) {
 			const float* __restrict__ bp = P.bank + sm.u.ent.base[e];
 			const f2v                 x  = {bp[lane], bp[lane + NL]};
@@ -424,7 +243,7 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 		}
 	} else { /* envelope entries x * (g + e (ng - g)) (3640-3662); steady entries take the same
 	          * expression with e = -0 and ng - g = +0: g + (-0 * +0) == g for every g */
-#pragma unroll TG_UNROLL
+#pragma unroll 4
 		for (int e = 0; e < np; e++) {
 			const float* __restrict__ bp = P.bank + sm.u.ent.base[e];
 			const f2v                 x  = {bp[lane], bp[lane + NL]};
@@ -450,7 +269,6 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 	__syncthreads ();
 
 	const uint32_t routing = G.routing;
-	TBF_MARK (0);
 	/* vibrato scanner, src/vibrato.cpp:365-411 */
 	if (routing & 0x03) {
 		const uint32_t* otab  = P.vibTab + 2048u * G.vibTable;
@@ -486,10 +304,7 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 		bad = __any (bad) || (P.dbg & TBF_DEBUG_FORCE_SERIAL);
 		dmn = wave_min (dmn);
 		dmx = wave_max (dmx);
-		if (TBF_ABL & 2) {
-			sm.u.v.vout[lane] = sm.vin[lane];
-			sm.u.v.vout[lane + NL] = sm.vin[lane + NL];
-		} else if (!bad) {
+		if (!bad) {
 			/* sample m reaches slot wo iff m + d_m is wo or wo - 1: m in [wo-1-dmax, wo-dmin] */
 			for (int wo = lane; wo < TBF_BLK + 32; wo += NL) {
 				const uint32_t slot = (out0 + wo) & (TBF_VRING - 1);
@@ -534,14 +349,10 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 		}
 	}
 
-	TBF_MARK (1);
 	/* mixdown, src/tonegen.cpp:3712-3777: the two per-sample gain chases run as
 	 * independent chains, lane 0 keyCompLevel += delta, lane 1 percEnvGain *= decay */
 	PRIO_UP ();
-	if ((TBF_ABL & 4) && lane < 2) {
-		for (int k = 0; k < TBF_BLK; k++)
-			(lane == 0 ? sm.u.v.kc : sm.u.v.pe)[k] = 0.5f;
-	} else if (lane < 2) {
+	if (lane < 2) {
 		const float keyCompDelta = (G.keyCompTarget - st.keyCompLevel) / (float)TBF_BLK;
 		const bool  perc         = (routing & 0x0C) != 0;
 		const float dec          = G.percEnvGainDecay;
@@ -589,7 +400,6 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 	if (lane == 0 && (routing & 0x0C))
 		st.pz = sm.prc[TBF_BLK - 1];
 	__syncthreads ();
-	TBF_MARK (2);
 }
 
 /* preamp / airwindows_density, src/overdrive.cpp:60-170 (FP64) */
@@ -606,17 +416,8 @@ __device__ void stage_overdrive (const tbf_launch& P, TgLds& sm, const tbf_seg_c
 	/* xorshift dither states F[0..128] (F[n+1] after sample n) by GF(2) jumps */
 	{
 		const uint32_t f0 = st.odFpd;
-#if TBF_ABL & 8
-		sm.u.od.fpd[lane + 1]      = f0 + lane;
-		sm.u.od.fpd[lane + 1 + NL] = f0 - lane;
-#elif XS_NIB
 		sm.u.od.fpd[lane + 1]      = xs_jump_n (P.xsJump, f0, lane + 1);
 		sm.u.od.fpd[lane + 1 + NL] = xs_jump_n (P.xsJump, f0, lane + 1 + NL);
-#else
-		const uint32_t lo          = xs_jump (P.xsJump, f0, lane + 1);
-		sm.u.od.fpd[lane + 1]      = lo;
-		sm.u.od.fpd[lane + 1 + NL] = xs_jump_u (P.xsJump, lo, NL);
-#endif
 		__syncthreads (); /* all lanes have read st.odFpd */
 		if (lane == 0) {
 			sm.u.od.fpd[0] = f0;
@@ -633,10 +434,7 @@ __device__ void stage_overdrive (const tbf_launch& P, TgLds& sm, const tbf_seg_c
 	}
 	__syncthreads ();
 	PRIO_UP ();
-	if ((TBF_ABL & 4) && lane < 2) {
-		for (int k = lane; k < TBF_BLK; k += 2)
-			sm.u.od.odh[k] = sm.u.od.odx[k];
-	} else if (lane < 2) {
+	if (lane < 2) {
 		/* alternating one-pole HPF (fpFlip): lane 0 carries iirSampleA over the samples it
 		 * owns, lane 1 iirSampleB over the others; 128 samples keep fpFlip unchanged */
 		const int    start = ((lane == 0) == (st.fpFlip != 0)) ? 0 : 1;
@@ -660,7 +458,6 @@ __device__ void stage_overdrive (const tbf_launch& P, TgLds& sm, const tbf_seg_c
 	}
 	PRIO_DOWN ();
 	__syncthreads ();
-	TBF_MARK (3);
 	for (int k = 0; k < 2; k++) {
 		const int n   = lane + k * NL;
 		double    x   = sm.u.od.odh[n];
@@ -670,13 +467,13 @@ __device__ void stage_overdrive (const tbf_launch& P, TgLds& sm, const tbf_seg_c
 			br = fabs (x) * 1.57079633;
 			if (br > 1.57079633)
 				br = 1.57079633;
-			br = (TBF_ABL & 1) ? br * 0.9 : sin (br);
+			br = sin (br);
 			x  = (x > 0.0) ? br : -br;
 		}
 		br = fabs (x) * 1.57079633;
 		if (br > 1.57079633)
 			br = 1.57079633;
-		br = (TBF_ABL & 1) ? br * 0.9 : (G.odDensityPos ? sin (br) : 1 - cos (br));
+		br = G.odDensityPos ? sin (br) : 1 - cos (br);
 		if (x > 0)
 			x = (x * (1 - G.odOut)) + (br * G.odOut);
 		else
@@ -689,7 +486,6 @@ __device__ void stage_overdrive (const tbf_launch& P, TgLds& sm, const tbf_seg_c
 		sm.bufB[n] = (float)x;
 	}
 	__syncthreads ();
-	TBF_MARK (4);
 }
 
 __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL), amdgpu_waves_per_eu (TG_WAVES)))
@@ -703,7 +499,6 @@ k_tonegen (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl, const tbf_tp
 		return;
 	const tbf_tpl_desc* T = tpls + cst[inst].tpl;
 	tbf_tg_state*       S = &P.st[inst].tg;
-	prof_begin (P, sm);
 	copy_words (&sm.st, S);
 	__syncthreads ();
 	for (uint32_t blk = 0; blk < P.nBlocks; blk++) {
@@ -718,8 +513,8 @@ k_tonegen (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl, const tbf_tp
 		}
 		stage_overdrive (P, sm, G);
 		float* o = P.mid1 + (size_t)inst * P.midStride + (size_t)blk * TBF_BLK;
-		stream_st (&o[lane], sm.bufB[lane]);
-		stream_st (&o[lane + NL], sm.bufB[lane + NL]);
+		o[lane] = sm.bufB[lane];
+		o[lane + NL] = sm.bufB[lane + NL];
 		if (P.chain == TBF_CHAIN_TAP_PREAMP) {
 			float* oL = P.outL + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
 			float* oR = P.outR + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
@@ -729,8 +524,6 @@ k_tonegen (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl, const tbf_tp
 	}
 	__syncthreads ();
 	copy_words (S, &sm.st);
-	TBF_MARK (18);
-	prof_end (P, sm, inst);
 }
 
 /* ================================================================== reverb */
@@ -738,94 +531,16 @@ k_tonegen (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl, const tbf_tp
  * FP64 biquads sit outside its feedback network: biquadA filters the predelayed input
  * before the allpasses (src/reverb.cpp:361-375), biquadB -> asin -> biquadC filter the
  * tap mix on its way out (733-764).  So:
- *   k_rv_in    predelay ring, biquadA, sin(x * wet)            -> a0[c][n] (FP64)
+ *   k_rv_pre   predelay, biquadA, sin(x * wet)                 -> rvA [inst][c][n] (FP64)
  *   k_rv_core  allpasses, 16 modulated taps, Householder feedback, ring writes
- *                                                               -> tap mix b[c][n] (FP64)
- *   k_rv_out   biquadB, clamp + asin, biquadC, dry mix, dither, (L+R)/sqrt2 -> mid2
+ *                                                               -> tap mix rvB (FP64)
+ *   k_rv_post  biquadB, clamp + asin, biquadC, dry mix, dither, (L+R)/sqrt2 -> mid2
  * k_rv_core has no serial recurrence besides the one-sample feedback shift, so it runs
- * lane-parallel at high occupancy; the two chain kernels are small.  Each kernel
- * regenerates what it needs of the xorshift dither streams (fpdL/fpdR advance once
- * per sample regardless of the signal, src/reverb.cpp:775-783). */
+ * lane-parallel (one workgroup per instance and channel); the two chain kernels run the
+ * serial biquads with one chain per lane (chain blocks, below).  The xorshift dither
+ * streams (fpdL/fpdR advance once per sample regardless of the signal,
+ * src/reverb.cpp:775-783) are carried by both chain kernels. */
 
-/* Serial IIR chain (biquadA/B/C, src/reverb.cpp:361-369, 733-741, 756-764) of one
- * channel over 64 samples of an LDS row, in place; st7/st8 = the channel's state pair */
-__device__ __forceinline__ void rv_chain (const double* cf, double& st7, double& st8, double* row)
-{
-#if TBF_ABL & 128
-	return; /* ablation (timing only): the reverb's serial biquad chains skipped */
-#endif
-	const double c0 = cf[0], c1 = cf[1], c2 = cf[2], c3 = cf[3], c4 = cf[4];
-	double       s7 = st7, s8 = st8;
-	for (int i0 = 0; i0 < TBF_SUB; i0 += 8) {
-		double xv[8];
-#pragma unroll
-		for (int k = 0; k < 8; k++)
-			xv[k] = row[i0 + k];
-#pragma unroll
-		for (int k = 0; k < 8; k++) {
-			const double x = xv[k];
-			const double t = (x * c0) + s7;
-			s7             = (x * c1) - (t * c3) + s8;
-			s8             = (x * c2) - (t * c4);
-			row[i0 + k]    = t;
-		}
-	}
-	st7 = s7;
-	st8 = s8;
-}
-
-/* the reverb state's head (everything before the channels' network state) in LDS: k_rv_in
- * and k_rv_out use only these fields */
-struct RvHeadLds {
-	alignas (16) unsigned char b[offsetof (tbf_rv_state, ch)];
-	__device__ tbf_rv_state&   get () { return *reinterpret_cast<tbf_rv_state*> (b); }
-};
-
-/* xorshift dither streams of one sub-block by GF(2) jumps: fpd[c][0] = state before
- * sample 0, fpd[c][n + 1] = state after sample n; jr = the lane's jump-table entries
- * for k = lane + 1 (loaded once per launch) */
-__device__ __forceinline__ void rv_dither (const uint32_t* __restrict__ J, const uint32_t* jr, uint32_t& sL,
-                                           uint32_t& sR, uint32_t (*fpd)[TBF_SUB + 1])
-{
-	const int      lane = threadIdx.x;
-	const uint32_t gL = sL, gR = sR;
-#if XS_NIB
-	fpd[0][lane + 1] = xs_jump_n (J, gL, lane + 1);
-	fpd[1][lane + 1] = xs_jump_n (J, gR, lane + 1);
-#else
-	fpd[0][lane + 1]  = xs_jump_reg (jr, gL);
-	fpd[1][lane + 1]  = xs_jump_reg (jr, gR);
-#endif
-	__syncthreads (); /* all lanes have read sL/sR */
-	if (lane == 0) {
-		fpd[0][0] = gL;
-		fpd[1][0] = gR;
-		sL        = fpd[0][TBF_SUB];
-		sR        = fpd[1][TBF_SUB];
-	}
-	__syncthreads ();
-}
-
-template <int IPW>
-struct RvInLds {
-	RvHeadLds    hd[IPW];
-	double       a[IPW][2][TBF_SUB + RV_PAD];
-	uint32_t     fpd[IPW][2][TBF_SUB + 1];
-	TBF_PROF_LDS
-};
-
-template <int IPW>
-struct RvOutLds {
-	RvHeadLds    hd[IPW];
-	double       bx[IPW][2][TBF_BLK + RV_PAD]; /* block b: tap mix -> biquadB output */
-	double       cx[IPW][2][TBF_BLK + RV_PAD]; /* block b-1: asin output -> biquadC output */
-	uint32_t     fpd[IPW][2][TBF_BLK + 1];
-	TBF_PROF_LDS
-};
-
-#ifndef RV_LDS_PAD
-#define RV_LDS_PAD 0
-#endif
 #define RV_WIN 72 /* tap window per line: 64 samples + max offset 2 * vibDepth (5.4) + 2 */
 
 struct RvCoreLds {
@@ -834,154 +549,12 @@ struct RvCoreLds {
 	double      sd[8][TBF_SUB];  /* sin ((n+1) D) of each line's closed-form step D ... */
 	double      cm[8][TBF_SUB];  /* ... and 1 - cos ((n+1) D) = 2 sin^2 ((n+1) D / 2) */
 	double      tabD[8];         /* the D the rows above hold (-1: none yet) */
-#if RV_LDS_PAD
-	double      pad[RV_LDS_PAD / 8]; /* A/B: fewer resident waves (their rings then fit in MALL) */
-#endif
-	TBF_PROF_LDS
 };
 
 /* FP64 stage buffers of one chunk: [inst][c][midStride] */
 __device__ __forceinline__ double* rv_buf (double* base, const tbf_launch& P, uint32_t inst, int c)
 {
 	return base + ((size_t)inst * 2 + c) * P.midStride;
-}
-
-/* k_rv_in, IPW instances per wave: the biquadA chains of all IPW instances' channels run
- * in one serial pass (lanes 0 .. 2 IPW - 1), so a pass's FP64 instructions serve 2 IPW
- * chains instead of 2; the lane-parallel parts loop over the instances */
-template <int IPW>
-__global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL), amdgpu_waves_per_eu (RVIO_WAVES)))
-k_rv_in (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_seg_ctl* __restrict__ ctl)
-{
-	__shared__ RvInLds<IPW> sm;
-	const int      lane  = threadIdx.x;
-	const uint32_t inst0 = blockIdx.x * IPW + P.instBase;
-	if (inst0 >= P.nInst)
-		return;
-	const int nj = (int)min ((uint32_t)IPW, P.nInst - inst0); /* instances of this wave */
-	prof_begin (P, sm);
-#pragma unroll
-	for (int j = 0; j < IPW; j++)
-		if (j < nj)
-			copy_head (&sm.hd[j].get (), &P.st[inst0 + j].rv);
-	__syncthreads ();
-	/* software-pipelined: the predelay reads and the input of sub-block g+1 are issued
-	 * before sub-block g's writes and serial chain, so their latency overlaps it (the
-	 * reads lie at count+65 .. count+128, the writes at count .. count+63, and the ring
-	 * holds >= 561 slots) */
-	const uint32_t nSub = P.nBlocks * (TBF_BLK / TBF_SUB);
-	double         pL[IPW], pR[IPW];
-	float          pIn[IPW];
-#if XS_NIB
-	const uint32_t* jr = nullptr;
-#else
-	uint32_t       jr[32]; /* the dither jump table's column k = lane + 1, for every sub-block */
-#pragma unroll
-	for (int j = 0; j < 32; j++)
-		jr[j] = P.xsJump[j * TBF_XS_JUMP + lane + 1];
-#endif
-#pragma unroll
-	for (int j = 0; j < IPW; j++) {
-		pL[j] = pR[j] = 0.0;
-		pIn[j]        = 0.f;
-		const uint32_t        inst = inst0 + j;
-		const tbf_inst_const& K    = cst[inst];
-		if (j < nj && nSub > 0) {
-			const double* slab = P.rslab + (size_t)inst * P.slabLen;
-			const int     cMr  = cnt_adv (sm.hd[j].get ().countM, K.delay[12], lane + 1);
-			pL[j]              = slab[K.ringOff[12] + cMr];
-			pR[j]              = slab[K.ringOff[13 + 12] + cMr];
-			pIn[j]             = P.mid1[(size_t)inst * P.midStride + lane];
-		}
-	}
-	/* serial lane roles: instance lane >> 1, channel lane & 1 */
-	const int     sj  = min (lane >> 1, IPW - 1), sc = lane & 1;
-	const double* scf = cst[inst0 + min (sj, nj - 1)].bq[0];
-#pragma unroll 1
-	for (uint32_t g = 0; g < nSub; g++) {
-		const uint32_t blk = g / (TBF_BLK / TBF_SUB), sb = g % (TBF_BLK / TBF_SUB);
-		const int      n   = lane;
-#pragma unroll
-		for (int j = 0; j < IPW; j++)
-			if (j < nj)
-				rv_dither (P.xsJump, jr, sm.hd[j].get ().fpdL, sm.hd[j].get ().fpdR, sm.fpd[j]);
-		TBF_MARK (5);
-		float inS[IPW];
-#pragma unroll
-		for (int j = 0; j < IPW; j++) {
-			inS[j]         = pIn[j];
-			sm.a[j][0][n] = pL[j];
-			sm.a[j][1][n] = pR[j];
-			if (j < nj && g + 1 < nSub) {
-				const uint32_t        inst = inst0 + j;
-				const tbf_inst_const& K    = cst[inst];
-				const double*         slab = P.rslab + (size_t)inst * P.slabLen;
-				const int cMr = cnt_adv (sm.hd[j].get ().countM, K.delay[12], TBF_SUB + n + 1);
-				pL[j]         = slab[K.ringOff[12] + cMr];
-				pR[j]         = slab[K.ringOff[13 + 12] + cMr];
-				pIn[j]        = P.mid1[(size_t)inst * P.midStride + (size_t)(g + 1) * TBF_SUB + n];
-			}
-		}
-		__syncthreads (); /* every read of the sub-block precedes its writes */
-#pragma unroll
-		for (int j = 0; j < IPW; j++) {
-			if (j >= nj)
-				continue;
-			/* predelay M (src/reverb.cpp:350-358): write at count, read at count + 1 */
-			const uint32_t        inst = inst0 + j;
-			const tbf_inst_const& K    = cst[inst];
-			double*               slab = P.rslab + (size_t)inst * P.slabLen;
-			const int             cMn  = cnt_adv (sm.hd[j].get ().countM, K.delay[12], n);
-#pragma unroll
-			for (int c = 0; c < 2; c++) {
-				double x = (double)inS[j];
-				if (fabs (x) < 1.18e-23)
-					x = sm.fpd[j][c][n] * 1.18e-17;
-				stream_st (&slab[K.ringOff[13 * c + 12] + cMn], x);
-			}
-		}
-		/* biquadA, every instance and channel: lanes 0 .. 2 IPW - 1 */
-		PRIO_UP ();
-		if (lane < 2 * nj) {
-			tbf_rv_state& ss = sm.hd[sj].get ();
-			rv_chain (scf, ss.bq[0][2 * sc], ss.bq[0][2 * sc + 1], sm.a[sj][sc]);
-		}
-		PRIO_DOWN ();
-		__syncthreads ();
-		TBF_MARK (6);
-#pragma unroll
-		for (int j = 0; j < IPW; j++) {
-			if (j >= nj)
-				continue;
-			const uint32_t inst = inst0 + j;
-			const double   wet  = ctl_of (P, ctl, blk, inst).rvWet;
-			const size_t   o    = (size_t)blk * TBF_BLK + sb * TBF_SUB + n;
-			stream_st (&rv_buf (P.rvA, P, inst, 0)[o], sin (sm.a[j][0][n] * wet));
-			stream_st (&rv_buf (P.rvA, P, inst, 1)[o], sin (sm.a[j][1][n] * wet));
-		}
-		__syncthreads ();
-		if (lane < nj) {
-			tbf_rv_state& ss = sm.hd[lane].get ();
-			ss.countM        = cnt_adv (ss.countM, cst[inst0 + lane].delay[12], TBF_SUB);
-		}
-		__syncthreads ();
-		TBF_MARK (7);
-	}
-	__syncthreads ();
-	if (lane < nj) { /* only k_rv_in's own fields: the other reverb kernels of neighbouring
-	                  * chunks may run concurrently (cross-chunk pipelining) */
-		const tbf_rv_state& ss = sm.hd[lane].get ();
-		tbf_rv_state*       S  = &P.st[inst0 + lane].rv;
-		S->countM              = ss.countM;
-		S->fpdL                = ss.fpdL;
-		S->fpdR                = ss.fpdR;
-		for (int q = 0; q < 4; q++)
-			S->bq[0][q] = ss.bq[0][q];
-	}
-#pragma unroll
-	for (int j = 0; j < IPW; j++) /* each instance's slots get the wave's stage times */
-		if (j < nj)
-			prof_end (P, sm, inst0 + j);
 }
 
 /* One channel of the feedback network, 64-sample sub-blocks: allpasses I..L (lines
@@ -1000,7 +573,7 @@ struct RvFetch {
 	double wlo[8]; /* line l, slot count+1+lane */
 	double whi;    /* lane 8l+j: line l, slot count+65+j */
 	double apOld[4]; /* allpass reads at count+1+lane */
-	double a0;       /* network input (k_rv_in output) */
+	double a0;       /* network input (k_rv_pre output) */
 };
 
 __device__ __forceinline__ int rl (int v, int l) { return __builtin_amdgcn_readlane (v, l); }
@@ -1019,22 +592,9 @@ __device__ __forceinline__ int wrap_slot (int s, int d) { return s - ((s > d) ? 
  * carry: only slots count+9 .. count+72 (into wlo), since slots +1..+8 are the previous
  * sub-block's +65..+72, still in its window and not written since (the sub-block in
  * between writes slots count-64 .. count-1) */
-template <typename T> __device__ __forceinline__ T rv_ld (const T* p)
-{
-#if RV_NT == 1
-	return __builtin_nontemporal_load (p);
-#else
-	return *p;
-#endif
-}
-template <typename T> __device__ __forceinline__ void rv_st (T* p, T v)
-{
-#if RV_NT >= 1
-	__builtin_nontemporal_store (v, p);
-#else
-	*p = v;
-#endif
-}
+template <typename T> __device__ __forceinline__ T rv_ld (const T* p) { return *p; }
+/* ring and tap-mix stores are nontemporal (2.94 -> 2.90 ms; nontemporal loads: 4.23 ms) */
+template <typename T> __device__ __forceinline__ void rv_st (T* p, T v) { __builtin_nontemporal_store (v, p); }
 
 __device__ __forceinline__ void rv_core_fetch (const double* slab, int cntv, int dlyv, int roffv,
                                                const double* __restrict__ a0s, size_t o, RvFetch& f, bool carry)
@@ -1113,9 +673,6 @@ __device__ __forceinline__ double rv_core_tap (RvCoreLds& sm, const tbf_inst_con
 		}
 		const double S = rld (Sx, l), C = rld (Cx, l);
 		s              = S + ((C * sm.sd[l][n]) - (S * sm.cm[l][n]));
-#ifdef RV_ABL_SIN /* ablation (timing only, wrong results): cheap sine */
-		s = (double)__sinf ((float)(rld (v0x, l) + dn));
-#endif
 	} else {
 		const double dl = K.vibDelta[l];
 		double       v  = rld (v0x, l);
@@ -1139,18 +696,11 @@ k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 	const int      c    = blockIdx.x & 1;
 	if (inst >= P.nInst)
 		return;
-	if (RV_CORE_PRIO)
-		__builtin_amdgcn_s_setprio (RV_CORE_PRIO);
 	const tbf_inst_const& K    = cst[inst];
 	tbf_rv_chan*          S    = &P.st[inst].rv.ch[c];
-#ifdef RV_ABL_MEM /* ablation (timing only, wrong results): 64 slabs shared, MALL-resident */
-	double* slab = P.rslab + (size_t)(inst & 63) * P.slabLen;
-#else
 	double* slab = P.rslab + (size_t)inst * P.slabLen;
-#endif
 	const double*         a0s  = rv_buf (P.rvA, P, inst, c);
 	double*               bout = rv_buf (P.rvB, P, inst, c);
-	prof_begin (P, sm);
 	copy_words (&sm.st, S);
 	if (lane < 8)
 		sm.tabD[lane] = -1.0;
@@ -1196,7 +746,7 @@ k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 		__syncthreads ();
 		/* two-tap interpolation and blend */
 		double I[8];
-#pragma unroll RV_TAP_UNROLL
+#pragma unroll 2
 		for (int l = 0; l < 8; l++) {
 			const double off = rv_core_tap (sm, K, l, okm, v0x, Sx, Cx, Dx);
 			const int    d   = rl (dlyv, l);
@@ -1261,7 +811,6 @@ k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 		}
 		fbv  = fbn;
 		cntv = ncv;
-		TBF_MARK (8 + c);
 	}
 	if (lane < 12)
 		sm.st.count[lane] = cntv;
@@ -1269,7 +818,6 @@ k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 		sm.st.fb[lane] = fbv;
 	__syncthreads ();
 	copy_words (S, &sm.st);
-	prof_end (P, sm, inst);
 }
 
 /* ------------------------------------------------------------------ k_rv_core_lds
@@ -1295,12 +843,6 @@ k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 #ifndef RVL_G
 #define RVL_G 11 /* sub-blocks (worker waves) per group: 64 RVL_G <= the shortest allpass delay (756), 64 RVL_G + 72 <= the shortest tap-line delay (1146) */
 #endif
-#ifndef RVL_ABL
-#define RVL_ABL 0 /* timing-only ablations of k_rv_core_lds: 1 no planning after the first group, 2 no ring load/store, 4 no write phase */
-#endif
-#ifndef RVL_UNROLL
-#define RVL_UNROLL 8 /* delay lines whose taps a worker computes together (8: 2.39 ms alone, 2: 3.0) */
-#endif
 /* the network's ring geometry at the reference's fixed settings (reverbConsts: size =
  * 0.4f^2 * 90 + 10, delay = (int)(dmul * size); rings 8-padded): compile-time constants, so
  * the ring addressing needs no per-line lane reads; tbf_rv_lds_fits checks an instance
@@ -1322,7 +864,6 @@ struct RvLds {
 	uint32_t    okm[2][RVL_G];         /* closed-form lines of sub-block j */
 	double      carry[2][RVL_G][8];    /* feedback of sub-block j's last sample */
 	tbf_rv_chan st;
-	TBF_PROF_LDS
 };
 
 /* the planner wave: the phase plan of group g into buffer b (start phases, closed-form
@@ -1418,7 +959,6 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 	double*               slab  = P.rslab + (size_t)inst * P.slabLen + rbase;
 	const double*         a0s   = rv_buf (P.rvA, P, inst, c);
 	double*               bout  = rv_buf (P.rvB, P, inst, c);
-	prof_begin (P, sm);
 	/* lane l < 12: delay and counter of line l (the LDS ring offsets are RVL_OFS) */
 	const int dlyv = n < 12 ? K.delay[n] : 0;
 	const double vdl = K.vibDelta[n & 7]; /* lane-held: no vector load of K inside the loop */
@@ -1434,7 +974,7 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 #pragma unroll
 		for (int k = 0; k < NR; k++) {
 			const uint32_t i = tid + k * WT;
-			v[k]             = (RVL_ABL & 2) ? double2 {0.0, 0.0} : ((const double2*)slab)[i < rlen2 ? i : 0];
+			v[k]             = ((const double2*)slab)[i < rlen2 ? i : 0];
 		}
 #pragma unroll
 		for (int k = 0; k < NR; k++) {
@@ -1475,7 +1015,6 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 	size_t po   = 0;
 	bool   pst  = false;
 	__syncthreads ();
-	TBF_MARK (14);
 #pragma unroll 1
 	for (uint32_t g = 0; g < nGrp; g++) {
 		const int  nb  = (int)min ((uint32_t)RVL_G, nSub - g * RVL_G);
@@ -1496,7 +1035,7 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 		if (act) {
 			const uint32_t om = sm.okm[par][w];
 			double         I[8];
-#pragma unroll RVL_UNROLL
+#pragma unroll
 			for (int l = 0; l < 8; l++) {
 				double sn;
 				if ((om >> l) & 1) {
@@ -1547,13 +1086,12 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 				for (int l = 0; l < 8; l++)
 					sm.carry[par][w][l] = fb[l];
 			}
-		} else if (w == RVL_G && g + 1 < nGrp && !(RVL_ABL & 1)) {
+		} else if (w == RVL_G && g + 1 < nGrp) {
 			rvl_plan (sm, vdl, (int)min ((uint32_t)RVL_G, nSub - (g + 1) * RVL_G), par ^ 1, force, P.errFlags);
 		}
 		__syncthreads ();
-		TBF_MARK (16);
 		/* ---- write phase ---- */
-		if (act && !(RVL_ABL & 4)) {
+		if (act) {
 			/* the previous sub-block's last feedback, all 8 lines read before any ring write */
 			const double* cp = w == 0 ? sm.carry[par ^ 1][RVL_G - 1] : sm.carry[par][w - 1];
 			double        cprv[8];
@@ -1574,12 +1112,11 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 			pmix = mix;
 			po   = o;
 		}
-		pst = act && !(RVL_ABL & 4);
+		pst = act;
 		a0  = a0n;
 		a0n = nxt;
 		cw = wrap_slot (cw + TBF_SUB * RVL_G, dlyv);
 		__syncthreads ();
-		TBF_MARK (17);
 	}
 	if (pst)
 		rv_st (&bout[po], pmix);
@@ -1591,220 +1128,445 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 			sm.st.fb[n] = sm.carry[(nGrp - 1) & 1][(nSub - 1) % RVL_G][n];
 	}
 	__syncthreads ();
-	for (uint32_t i = tid; i < rlen2 && !(RVL_ABL & 2); i += RVL_THREADS)
+	for (uint32_t i = tid; i < rlen2; i += RVL_THREADS)
 		((double2*)slab)[i] = ((const double2*)sm.ring)[i];
 	if (w == 0)
 		copy_words (S, &sm.st);
-	TBF_MARK (19);
-	prof_end (P, sm, inst);
 }
 
-/* k_rv_out: biquadB -> clamp + asin -> biquadC -> dry mix, dither, (L+R)/sqrt2, in
- * 128-sample blocks, software-pipelined so biquadB of block b and biquadC of block b-1
- * advance in the same serial instruction stream (lane 4j + 2q + c: instance j of the
- * wave, q = 0 B / 1 C, channel c).  One serial pass per block serves the 4 IPW chains of
- * the wave's IPW instances; the lane-parallel parts loop over the instances. */
-template <int IPW>
-__global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL), amdgpu_waves_per_eu (RVIO_WAVES / IPW)))
-k_rv_out (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_seg_ctl* __restrict__ ctl)
+/* ------------------------------------------------------------------ chain blocks
+ * The reverb's serial FP64 biquads with one chain per lane.  A workgroup serves RVC_CB
+ * instances, i.e. RVC_NC = 2 RVC_CB chains (chain r = 2 j + c: instance j, channel c), in
+ * tiles of RVC_T samples staged in LDS as [chain][sample] rows of odd stride RVC_S, so a
+ * column (one sample of every chain) is one conflict-free ds_read_b64:
+ *   wave 0     the serial recurrences, lane = chain: one FP64 instruction stream advances
+ *              64 chains (one wave per instance would serve 2)
+ *   wave 1     the chains' xorshift dither streams (fpdL/fpdR, src/reverb.cpp:775-783),
+ *              lane = chain, written ahead as f[chain][n] = state before sample n
+ *   waves 2..  lane-parallel work, one instance at a time (wave-uniform, so its constants
+ *              come in as scalar loads): lane = (channel, sample of the tile); HBM loads
+ *              one tile ahead, predelay ring, denormal guard, sin / asin, dry mix,
+ *              dither, mono sum, stores
+ * A tile's stages advance one per iteration, with one barrier per iteration.  Every
+ * chain runs the reference's operations in its order, so the bits are the reference's. */
+#ifndef RVC_CB
+#define RVC_CB 32 /* instances per workgroup */
+#endif
+#define RVC_NC (2 * RVC_CB)      /* chains per workgroup (<= 64: one per lane of wave 0) */
+#define RVC_T 32                 /* samples per tile: one per lane of a half-wave */
+#define RVC_S (RVC_T + 1)        /* LDS row stride (odd: conflict-free columns) */
+#ifndef RVC_H
+#define RVC_H 8 /* helper waves */
+#endif
+#define RVC_TASKS RVC_CB          /* helper tasks per tile: one instance each */
+#define RVC_NTK (RVC_TASKS / RVC_H)
+static_assert (RVC_TASKS % RVC_H == 0, "helper tasks split evenly");
+#define RVC_THREADS (NL * (2 + RVC_H))
+static_assert (RVC_NC <= NL && RVC_T * 2 == NL && TBF_BLK % RVC_T == 0, "chain-block geometry");
+
+/* one transposed-DF2 biquad step (biquadA/B/C, src/reverb.cpp:361-369, 733-741, 756-764) */
+__device__ __forceinline__ double rvc_bq (double x, double c0, double c1, double c2, double c3, double c4, double& s7,
+                                          double& s8)
 {
-	__shared__ RvOutLds<IPW> sm;
-	const int      lane  = threadIdx.x;
-	const uint32_t inst0 = blockIdx.x * IPW + P.instBase;
+	const double t = (x * c0) + s7;
+	s7             = (x * c1) - (t * c3) + s8;
+	s8             = (x * c2) - (t * c4);
+	return t;
+}
+
+/* the xorshift states of one tile of every chain: f[n] = state before sample n (n = 0 ..
+ * RVC_T; entry RVC_T = the state after the tile) */
+__device__ __forceinline__ void rvc_dither_row (uint32_t* f, uint32_t& s)
+{
+#pragma unroll 8
+	for (int n = 0; n < RVC_T; n++) {
+		f[n] = s;
+		s    = xs_step (s);
+	}
+	f[RVC_T] = s;
+}
+
+/* the predelay slot k samples after counter c in [0, d] (k <= d + 1): cnt_adv's steady state */
+__device__ __forceinline__ int rvc_slot (int c, int d, int k)
+{
+	const int v = c + k;
+	return v > d ? v - d - 1 : v;
+}
+
+/* a helper task's per-block reverb wet level, lane b = block b of the launch (<= 64 blocks) */
+__device__ __forceinline__ double rvc_wet_lanes (const tbf_launch& P, const tbf_seg_ctl* __restrict__ ctl, uint32_t inst)
+{
+	const uint32_t b = threadIdx.x & (NL - 1);
+	return b < P.nBlocks ? ctl_of (P, ctl, b, inst).rvWet : 0.0;
+}
+
+/* the serial chains of one tile, in place: one biquad (q = 1) or two interleaved */
+template <int Q>
+__device__ __forceinline__ void rvc_serial (double* const (&row)[Q], const double (&c)[Q][5], double (&s)[Q][2])
+{
+	PRIO_UP ();
+	for (int i0 = 0; i0 < RVC_T; i0 += 8) {
+		double xv[Q][8];
+#pragma unroll
+		for (int k = 0; k < 8; k++)
+#pragma unroll
+			for (int q = 0; q < Q; q++)
+				xv[q][k] = row[q][i0 + k];
+#pragma unroll
+		for (int k = 0; k < 8; k++)
+#pragma unroll
+			for (int q = 0; q < Q; q++)
+				row[q][i0 + k] = rvc_bq (xv[q][k], c[q][0], c[q][1], c[q][2], c[q][3], c[q][4], s[q][0], s[q][1]);
+	}
+	PRIO_DOWN ();
+}
+
+struct RvPreLds {
+	double   x[2][RVC_NC][RVC_S]; /* predelayed input -> biquadA output, in place */
+	uint32_t f[2][RVC_NC][RVC_S]; /* fpdL / fpdR of the sample delayM back (the predelay's input guard) */
+};
+
+/* predelay, denormal guard, biquadA, sin (x * wet) (src/reverb.cpp:339-375) -> rvA.
+ * The predelay ring slot read at sample m holds the input of sample m - delayM guarded
+ * with that sample's dither state (or 0 while m < delayM), so the kernel reads the input
+ * delayM samples back, from this chunk's mid1 or the history of earlier chunks
+ * (TBF_PD_HIST), and the dither wave runs the stream delayM samples behind.
+ * A tile is loaded at iteration k (its HBM reads issued at k - 2), filtered at k + 1 and
+ * stored at k + 2.  Each role runs its own loop with the same barriers.  The HBM reads
+ * are unconditional (indices clamped): a read under a branch joins its register with the
+ * old value, and that copy waits for the read right away. */
+__global__ void __launch_bounds__ (RVC_THREADS)
+k_rv_pre (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_seg_ctl* __restrict__ ctl)
+{
+	__shared__ RvPreLds sm;
+	const int      w = __builtin_amdgcn_readfirstlane (threadIdx.x >> 6), lane = threadIdx.x & (NL - 1);
+	const uint32_t inst0 = P.instBase + blockIdx.x * RVC_CB;
 	if (inst0 >= P.nInst)
 		return;
-	const int  nj  = (int)min ((uint32_t)IPW, P.nInst - inst0); /* instances of this wave */
-	const bool tap = P.chain == TBF_CHAIN_TAP_REVERB;
-	prof_begin (P, sm);
-#pragma unroll
-	for (int j = 0; j < IPW; j++)
-		if (j < nj)
-			copy_head (&sm.hd[j].get (), &P.st[inst0 + j].rv);
-	__syncthreads ();
-	/* serial lane roles */
-	const int     sj = min (lane >> 2, IPW - 1), q = (lane >> 1) & 1, c = lane & 1;
-	const double* cf = cst[inst0 + min (sj, nj - 1)].bq[1 + q];
-	const double  c0 = cf[0], c1 = cf[1], c2 = cf[2], c3 = cf[3], c4 = cf[4];
-	/* software-pipelined loads: the tap mix of block it+1 and the dry input of block it-1
-	 * are issued before block it's serial pass and consumed after it */
-#if !XS_NIB
-	uint32_t jr[32]; /* the dither jump table's column k = lane + 1, for every block */
-#pragma unroll
-	for (int j = 0; j < 32; j++)
-		jr[j] = P.xsJump[j * TBF_XS_JUMP + lane + 1];
-#endif
-	double pb[IPW][4];
-#pragma unroll
-	for (int j = 0; j < IPW; j++) {
-		pb[j][0] = pb[j][1] = pb[j][2] = pb[j][3] = 0.0;
-		if (j < nj && P.nBlocks > 0) {
-			const double* bL = rv_buf (P.rvB, P, inst0 + j, 0);
-			const double* bR = rv_buf (P.rvB, P, inst0 + j, 1);
-			pb[j][0]         = bL[lane];
-			pb[j][1]         = bL[lane + NL];
-			pb[j][2]         = bR[lane];
-			pb[j][3]         = bR[lane + NL];
-		}
-	}
-	for (uint32_t it = 0; it <= P.nBlocks; it++) {
-		const bool haveB = it < P.nBlocks, haveC = it > 0;
-		float      pIn[IPW][2];
-#pragma unroll
-		for (int j = 0; j < IPW; j++) {
-			pIn[j][0] = pIn[j][1] = 0.f;
-			if (j >= nj)
-				continue;
-			const uint32_t inst = inst0 + j;
-			/* (a) tap mix of block `it` */
-			if (haveB) {
-				sm.bx[j][0][lane]      = pb[j][0];
-				sm.bx[j][0][lane + NL] = pb[j][1];
-				sm.bx[j][1][lane]      = pb[j][2];
-				sm.bx[j][1][lane + NL] = pb[j][3];
-				if (it + 1 < P.nBlocks) {
-					const double* bL = rv_buf (P.rvB, P, inst, 0);
-					const double* bR = rv_buf (P.rvB, P, inst, 1);
-					const size_t  o  = (size_t)(it + 1) * TBF_BLK;
-					pb[j][0]         = bL[o + lane];
-					pb[j][1]         = bL[o + lane + NL];
-					pb[j][2]         = bR[o + lane];
-					pb[j][3]         = bR[o + lane + NL];
-				}
-			}
-			if (haveC) {
-				const float* in = P.mid1 + (size_t)inst * P.midStride + (size_t)(it - 1) * TBF_BLK;
-				pIn[j][0]       = in[lane];
-				pIn[j][1]       = in[lane + NL];
-			}
-		}
+	const int nj  = (int)min ((uint32_t)RVC_CB, P.nInst - inst0);
+	const int nT  = (int)P.nBlocks * (TBF_BLK / RVC_T);
+	const int nIt = nT + 2;
+	/* waves 0, 1: lane = chain 2 j + c */
+	const int     cj = lane >> 1, cc = lane & 1;
+	const bool    cok = cj < nj;
+	tbf_rv_state* CS  = &P.st[inst0 + (cok ? cj : 0)].rv;
+	if (w == 0) {
+		const double* cf   = cst[inst0 + (cok ? cj : 0)].bq[0];
+		const double  c[1][5] = {{cf[0], cf[1], cf[2], cf[3], cf[4]}};
+		double        s[1][2] = {{CS->bq[0][2 * cc], CS->bq[0][2 * cc + 1]}};
 		__syncthreads ();
-		TBF_MARK (10);
-		/* (b) serial: B over block it (q = 0), C over block it-1 (q = 1) */
-		PRIO_UP ();
-		if (!(TBF_ABL & 128) && lane < 4 * nj && (q == 0 ? haveB : haveC)) {
-			tbf_rv_state& ss  = sm.hd[sj].get ();
-			double*       row = q == 0 ? sm.bx[sj][c] : sm.cx[sj][c];
-			double        s7 = ss.bq[1 + q][2 * c], s8 = ss.bq[1 + q][2 * c + 1];
-			for (int i0 = 0; i0 < TBF_BLK; i0 += 8) {
-				double xv[8];
-#pragma unroll
-				for (int k = 0; k < 8; k++)
-					xv[k] = row[i0 + k];
-#pragma unroll
-				for (int k = 0; k < 8; k++) {
-					const double x = xv[k];
-					const double t = (x * c0) + s7;
-					s7             = (x * c1) - (t * c3) + s8;
-					s8             = (x * c2) - (t * c4);
-					row[i0 + k]    = t;
-				}
-			}
-			ss.bq[1 + q][2 * c]     = s7;
-			ss.bq[1 + q][2 * c + 1] = s8;
-		}
-		PRIO_DOWN ();
-		__syncthreads ();
-		TBF_MARK (11);
-		/* (c) output of block it-1: dry mix, dither, mono sum (src/reverb.cpp:766-787) */
-		if (haveC) {
-			const uint32_t ob = it - 1;
-			/* dither states F[0..128] of both streams of every instance for the block */
-#pragma unroll
-			for (int j = 0; j < IPW; j++) {
-				if (j >= nj)
-					continue;
-				const tbf_rv_state& ss = sm.hd[j].get ();
-#if XS_NIB
-				sm.fpd[j][0][lane + 1]      = xs_jump_n (P.xsJump, ss.fpdL2, lane + 1);
-				sm.fpd[j][1][lane + 1]      = xs_jump_n (P.xsJump, ss.fpdR2, lane + 1);
-				sm.fpd[j][0][lane + 1 + NL] = xs_jump_n (P.xsJump, ss.fpdL2, lane + 1 + NL);
-				sm.fpd[j][1][lane + 1 + NL] = xs_jump_n (P.xsJump, ss.fpdR2, lane + 1 + NL);
-#else
-				const uint32_t l1 = xs_jump_reg (jr, ss.fpdL2), r1 = xs_jump_reg (jr, ss.fpdR2);
-				sm.fpd[j][0][lane + 1]      = l1;
-				sm.fpd[j][1][lane + 1]      = r1;
-				sm.fpd[j][0][lane + 1 + NL] = xs_jump_u (P.xsJump, l1, NL);
-				sm.fpd[j][1][lane + 1 + NL] = xs_jump_u (P.xsJump, r1, NL);
-#endif
-			}
-			__syncthreads (); /* all lanes have read the states */
-			if (lane < nj) {
-				tbf_rv_state& ss    = sm.hd[lane].get ();
-				sm.fpd[lane][0][0] = ss.fpdL2;
-				sm.fpd[lane][1][0] = ss.fpdR2;
-				ss.fpdL2           = sm.fpd[lane][0][TBF_BLK];
-				ss.fpdR2           = sm.fpd[lane][1][TBF_BLK];
+#pragma unroll 1
+		for (int it = 0; it < nIt; it++) {
+			if (it >= 1 && it - 1 < nT) { /* biquadA of tile it - 1 */
+				double* const row[1] = {sm.x[(it - 1) & 1][lane]};
+				rvc_serial<1> (row, c, s);
 			}
 			__syncthreads ();
+		}
+		if (cok) {
+			CS->bq[0][2 * cc]     = s[0][0];
+			CS->bq[0][2 * cc + 1] = s[0][1];
+		}
+		return;
+	}
+	if (w == 1) {
+		/* the dither stream delayM samples behind: it advances only over samples whose
+		 * delayed input exists (instance age >= delayM) */
+		const int d    = cst[inst0 + (cok ? cj : 0)].delay[12];
+		const int age0 = min (max (CS->pdAge, 0), d);
+		uint32_t  fs   = cc ? CS->fpdR : CS->fpdL;
+		auto      row  = [&] (int k) {
+            const int lead = min (max (d - age0 - k * RVC_T, 0), RVC_T); /* samples with no input yet */
+            uint32_t* f    = sm.f[k & 1][lane];
+#pragma unroll 8
+            for (int n = 0; n < RVC_T; n++) {
+                f[n] = fs;
+                fs   = n >= lead ? xs_step (fs) : fs;
+            }
+		};
+		if (nT > 0)
+			row (0);
+		__syncthreads ();
+#pragma unroll 1
+		for (int it = 0; it < nIt; it++) {
+			if (it + 1 < nT)
+				row (it + 1);
+			__syncthreads ();
+		}
+		if (cok) {
+			if (cc)
+				CS->fpdR = fs;
+			else
+				CS->fpdL = fs;
+		}
+		return;
+	}
+	/* helpers: task t = instance h + RVC_H t (wave-uniform); lane = channel hc, sample n.
+	 * HBM reads run two tiles ahead, into two register sets that alternate by iteration
+	 * parity (the loop is unrolled by two, so the sets stay static) */
+	const int    h = w - 2, hc = lane >> 5, n = lane & (RVC_T - 1);
+	float        pIn[2][RVC_NTK];
+	double       wetv[RVC_NTK];
+	int          dM[RVC_NTK], age[RVC_NTK];
+	uint32_t     pos[RVC_NTK];
+	const float* in[RVC_NTK];
+	float*       hst[RVC_NTK]; /* the predelay history */
+	double*      ra[RVC_NTK];
+	/* the input delayM samples before sample k of the chunk (lane n: k = 32 tile + n) */
+	auto src = [&] (int t, int tile) {
+		const int p = tile * RVC_T + n - dM[t];
+		return p >= 0 ? in[t] + p : hst[t] + ((pos[t] + (uint32_t)p) & (TBF_PD_HIST - 1));
+	};
 #pragma unroll
-			for (int j = 0; j < IPW; j++) {
-				if (j >= nj)
-					continue;
-				const uint32_t inst = inst0 + j;
-				const double   wet  = ctl_of (P, ctl, ob, inst).rvWet;
-				float*         out  = tap ? P.outL + (size_t)inst * P.outStride + P.outOffset + (size_t)ob * TBF_BLK
-				                          : P.mid2 + (size_t)inst * P.midStride + (size_t)ob * TBF_BLK;
+	for (int t = 0; t < RVC_NTK; t++) {
+		const int             j    = h + t * RVC_H;
+		const uint32_t        inst = inst0 + (j < nj ? j : nj - 1);
+		const tbf_inst_const& K    = cst[inst];
+		const tbf_rv_state&   S    = P.st[inst].rv;
+		hst[t]  = (float*)(P.rslab + (size_t)inst * P.slabLen + K.ringOff[12]);
+		in[t]   = P.mid1 + (size_t)inst * P.midStride;
+		ra[t]   = rv_buf (P.rvA, P, inst, hc) + n;
+		dM[t]   = K.delay[12];
+		age[t]  = min (max (S.pdAge, 0), dM[t]);
+		pos[t]  = S.pdPos;
+		wetv[t] = rvc_wet_lanes (P, ctl, inst);
+		pIn[0][t] = *src (t, 0);
+		pIn[1][t] = *src (t, min (1, nT - 1));
+	}
+	__syncthreads ();
+	auto step = [&] (const int it, float (&qIn)[RVC_NTK]) {
+		const int b = it & 1; /* tiles it and it - 2 share the buffer */
+		double    sv[RVC_NTK];
+		/* the filtered tile it - 2, read before tile it overwrites it */
 #pragma unroll
-				for (int h = 0; h < 2; h++) {
-					const int    n   = lane + h * NL;
-					const double inS = (double)pIn[j][h];
-					double       ov[2];
+		for (int t = 0; t < RVC_NTK; t++)
+			sv[t] = sm.x[b][2 * (h + t * RVC_H) + hc][n];
+		/* tile it: the predelayed samples (src/reverb.cpp:339-358): the input delayM back,
+		 * guarded with its dither state, or the zeroed ring's 0 before the instance's
+		 * first delayM samples */
+		if (it < nT) {
 #pragma unroll
-					for (int cc = 0; cc < 2; cc++) {
-						double x = sm.cx[j][cc][n];
-						if (wet != 1.0) {
-							double dry = inS;
-							if (fabs (dry) < 1.18e-23)
-								dry = sm.fpd[j][cc][n] * 1.18e-17;
-							x += (dry * (1.0 - wet));
-						}
-						ov[cc] = dither_add (x, sm.fpd[j][cc][n + 1]);
-					}
-					const float y = (float)(0.7071067811865476 * (ov[0] + ov[1]));
-					stream_st (&out[n], y);
-					if (tap)
-						P.outR[(size_t)inst * P.outStride + P.outOffset + (size_t)ob * TBF_BLK + n] = y;
+			for (int t = 0; t < RVC_NTK; t++) {
+				const int r = 2 * (h + t * RVC_H) + hc;
+				double    x = (double)qIn[t];
+				if (fabs (x) < 1.18e-23)
+					x = sm.f[b][r][n] * 1.18e-17;
+				sm.x[b][r][n] = age[t] + it * RVC_T + n >= dM[t] ? x : 0.0;
+			}
+		}
+		/* HBM reads of tile it + 2 into the set just consumed (clamped past the last tile:
+		 * a harmless re-read, so the loads need no branch) */
+		const int tl = min (it + 2, nT - 1);
+#pragma unroll
+		for (int t = 0; t < RVC_NTK; t++)
+			qIn[t] = *src (t, tl);
+		/* sin (x * wet) of tile it - 2 */
+		if (it >= 2) {
+			const int k2 = it - 2;
+#pragma unroll
+			for (int t = 0; t < RVC_NTK; t++)
+				if (h + t * RVC_H < nj)
+					ra[t][(size_t)k2 * RVC_T] = sin (sv[t] * rld (wetv[t], (k2 * RVC_T) / TBF_BLK));
+		}
+		__syncthreads ();
+	};
+#pragma unroll 1
+	for (int it = 0; it < nIt; it += 2) {
+		step (it, pIn[0]);
+		if (it + 1 < nIt)
+			step (it + 1, pIn[1]);
+	}
+	/* the chunk's last inputs into the history (after every read of it above, in this
+	 * wave's program order), the position and the age */
+	const int nS = nT * RVC_T;
+#pragma unroll
+	for (int t = 0; t < RVC_NTK; t++) {
+		const int j = h + t * RVC_H;
+		if (j >= nj)
+			continue;
+		for (int m = max (0, nS - TBF_PD_HIST) + lane; m < nS; m += NL)
+			hst[t][(pos[t] + (uint32_t)m) & (TBF_PD_HIST - 1)] = in[t][m];
+		if (lane == 0) {
+			tbf_rv_state& S = P.st[inst0 + j].rv;
+			S.pdPos         = (pos[t] + (uint32_t)nS) & (TBF_PD_HIST - 1);
+			S.pdAge         = min (age[t] + nS, dM[t]);
+		}
+	}
+}
+
+struct RvPostLds {
+	double   y[2][RVC_NC][RVC_S]; /* tap mix -> biquadB output, in place */
+	double   z[2][RVC_NC][RVC_S]; /* asin output -> biquadC output, in place */
+	uint32_t f[2][RVC_NC][RVC_S]; /* fpdL / fpdR before each sample (entry RVC_T: after the tile) */
+};
+
+/* biquadB, clamp + asin, biquadC, dry mix, dither, (L + R) / sqrt 2 (src/reverb.cpp:733-787)
+ * -> mid2.  A tile is loaded at iteration k (its HBM reads issued at k - 2), biquadB at
+ * k + 1, asin at k + 2, biquadC at k + 3, output at k + 4. */
+__global__ void __launch_bounds__ (RVC_THREADS)
+k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_seg_ctl* __restrict__ ctl)
+{
+	__shared__ RvPostLds sm;
+	const int      w = __builtin_amdgcn_readfirstlane (threadIdx.x >> 6), lane = threadIdx.x & (NL - 1);
+	const uint32_t inst0 = P.instBase + blockIdx.x * RVC_CB;
+	if (inst0 >= P.nInst)
+		return;
+	const int     nj  = (int)min ((uint32_t)RVC_CB, P.nInst - inst0);
+	const int     nT  = (int)P.nBlocks * (TBF_BLK / RVC_T);
+	const int     nIt = nT + 4;
+	const int     cj = lane >> 1, cc = lane & 1;
+	const bool    cok = cj < nj;
+	tbf_rv_state* CS  = &P.st[inst0 + (cok ? cj : 0)].rv;
+	if (w == 0) {
+		/* biquadB of tile it - 1 and biquadC of tile it - 3, two chains per lane in one
+		 * instruction stream */
+		const tbf_inst_const& K = cst[inst0 + (cok ? cj : 0)];
+		const double c[2][5] = {{K.bq[1][0], K.bq[1][1], K.bq[1][2], K.bq[1][3], K.bq[1][4]},
+		                        {K.bq[2][0], K.bq[2][1], K.bq[2][2], K.bq[2][3], K.bq[2][4]}};
+		double s[2][2] = {{CS->bq[1][2 * cc], CS->bq[1][2 * cc + 1]}, {CS->bq[2][2 * cc], CS->bq[2][2 * cc + 1]}};
+		__syncthreads ();
+#pragma unroll 1
+		for (int it = 0; it < nIt; it++) {
+			const bool doB = it >= 1 && it - 1 < nT, doC = it >= 3 && it - 3 < nT;
+			double*    rb  = sm.y[(it - 1) & 1][lane];
+			double*    rc  = sm.z[(it - 1) & 1][lane];
+			if (doB && doC) {
+				double* const row[2] = {rb, rc};
+				rvc_serial<2> (row, c, s);
+			} else if (doB) {
+				double* const row[1] = {rb};
+				const double  c1[1][5] = {{c[0][0], c[0][1], c[0][2], c[0][3], c[0][4]}};
+				double        s1[1][2] = {{s[0][0], s[0][1]}};
+				rvc_serial<1> (row, c1, s1);
+				s[0][0] = s1[0][0];
+				s[0][1] = s1[0][1];
+			} else if (doC) {
+				double* const row[1] = {rc};
+				const double  c1[1][5] = {{c[1][0], c[1][1], c[1][2], c[1][3], c[1][4]}};
+				double        s1[1][2] = {{s[1][0], s[1][1]}};
+				rvc_serial<1> (row, c1, s1);
+				s[1][0] = s1[0][0];
+				s[1][1] = s1[0][1];
+			}
+			__syncthreads ();
+		}
+		if (cok) {
+			CS->bq[1][2 * cc]     = s[0][0];
+			CS->bq[1][2 * cc + 1] = s[0][1];
+			CS->bq[2][2 * cc]     = s[1][0];
+			CS->bq[2][2 * cc + 1] = s[1][1];
+		}
+		return;
+	}
+	if (w == 1) {
+		uint32_t fs = cc ? CS->fpdR2 : CS->fpdL2;
+		__syncthreads ();
+#pragma unroll 1
+		for (int it = 0; it < nIt; it++) {
+			if (it >= 3 && it - 3 < nT)
+				rvc_dither_row (sm.f[(it - 3) & 1][lane], fs);
+			__syncthreads ();
+		}
+		if (cok) {
+			if (cc)
+				CS->fpdR2 = fs;
+			else
+				CS->fpdL2 = fs;
+		}
+		return;
+	}
+	/* helpers: HBM reads two tiles ahead into two register sets alternating by iteration
+	 * parity (see k_rv_pre) */
+	const bool   tap = P.chain == TBF_CHAIN_TAP_REVERB;
+	const int    h = w - 2, hc = lane >> 5, n = lane & (RVC_T - 1);
+	double       pB[2][RVC_NTK], wetv[RVC_NTK];
+	float        pIn[2][RVC_NTK];
+	const double* rb[RVC_NTK];
+	const float*  in[RVC_NTK];
+	float*        out[RVC_NTK];
+#pragma unroll
+	for (int t = 0; t < RVC_NTK; t++) {
+		const int      j    = h + t * RVC_H;
+		const uint32_t inst = inst0 + (j < nj ? j : nj - 1);
+		rb[t]     = rv_buf (P.rvB, P, inst, hc) + n;
+		in[t]     = P.mid1 + (size_t)inst * P.midStride + n;
+		out[t]    = tap ? (hc ? P.outR : P.outL) + (size_t)inst * P.outStride + P.outOffset + n
+		                : P.mid2 + (size_t)inst * P.midStride + n;
+		wetv[t]   = rvc_wet_lanes (P, ctl, inst);
+		pB[0][t]  = rb[t][0];
+		pB[1][t]  = rb[t][(size_t)min (1, nT - 1) * RVC_T];
+		pIn[0][t] = pIn[1][t] = 0.f;
+	}
+	__syncthreads ();
+	auto step = [&] (const int it, double (&qB)[RVC_NTK], float (&qIn)[RVC_NTK]) {
+		const int b = it & 1; /* tiles it, it - 2 and it - 4 share the buffers */
+		/* output of tile it - 4: dry mix, dither, mono sum (src/reverb.cpp:766-787); the
+		 * half-waves hold L and R, and 0.7071 (L + R) == 0.7071 (R + L) */
+		float yv[RVC_NTK];
+		if (it >= 4) {
+			const int ob = ((it - 4) * RVC_T) / TBF_BLK;
+#pragma unroll
+			for (int t = 0; t < RVC_NTK; t++) {
+				const double wet = rld (wetv[t], ob);
+				const int    r   = 2 * (h + t * RVC_H) + hc;
+				double       x   = sm.z[b][r][n];
+				if (wet != 1.0) {
+					double dry = (double)qIn[t];
+					if (fabs (dry) < 1.18e-23)
+						dry = sm.f[b][r][n] * 1.18e-17;
+					x += (dry * (1.0 - wet));
 				}
+				const double ov = dither_add (x, sm.f[b][r][n + 1]);
+				const double ow = __shfl_xor (ov, 32);
+				yv[t]           = (float)(0.7071067811865476 * (ov + ow));
 			}
 		}
-		__syncthreads ();
-		TBF_MARK (12);
-		/* (d) clamp + asin of block it's biquadB output -> C input of the next pass
-		 * (src/reverb.cpp:743-751) */
-		if (haveB) {
+		/* clamp + asin of tile it - 2 (src/reverb.cpp:743-751); the tap mix of tile it,
+		 * which reuses the biquadB buffer, after the reads */
+		double av[RVC_NTK];
 #pragma unroll
-			for (int j = 0; j < IPW; j++) {
-				if (j >= nj)
-					continue;
+		for (int t = 0; t < RVC_NTK; t++)
+			av[t] = sm.y[b][2 * (h + t * RVC_H) + hc][n];
+		if (it < nT) {
 #pragma unroll
-				for (int h = 0; h < 2; h++)
+			for (int t = 0; t < RVC_NTK; t++)
+				sm.y[b][2 * (h + t * RVC_H) + hc][n] = qB[t];
+		}
+		/* HBM reads into the set just consumed (indices clamped, so the loads need no
+		 * branch): the tap mix of tile it + 2, the dry input of tile it - 2 (output at
+		 * iteration it + 2) */
+		const int tb = min (it + 2, nT - 1), ti = max (0, min (it - 2, nT - 1));
 #pragma unroll
-					for (int cc = 0; cc < 2; cc++) {
-						const int n = lane + h * NL;
-						double    y = sm.bx[j][cc][n];
-						if (y > 1.0) y = 1.0;
-						if (y < -1.0) y = -1.0;
-						sm.cx[j][cc][n] = asin (y);
-					}
+		for (int t = 0; t < RVC_NTK; t++) {
+			qB[t]  = rb[t][(size_t)tb * RVC_T];
+			qIn[t] = in[t][(size_t)ti * RVC_T];
+		}
+		if (it >= 2 && it - 2 < nT) {
+#pragma unroll
+			for (int t = 0; t < RVC_NTK; t++) {
+				double y = av[t];
+				if (y > 1.0)
+					y = 1.0;
+				if (y < -1.0)
+					y = -1.0;
+				sm.z[b][2 * (h + t * RVC_H) + hc][n] = asin (y);
 			}
 		}
-		__syncthreads ();
-		TBF_MARK (13);
-	}
-	if (lane < nj) { /* only k_rv_out's own fields (see k_rv_in) */
-		const tbf_rv_state& ss = sm.hd[lane].get ();
-		tbf_rv_state*       S  = &P.st[inst0 + lane].rv;
-		S->fpdL2               = ss.fpdL2;
-		S->fpdR2               = ss.fpdR2;
-		for (int k = 0; k < 4; k++) {
-			S->bq[1][k] = ss.bq[1][k];
-			S->bq[2][k] = ss.bq[2][k];
-		}
-	}
+		if (it >= 4) {
+			const size_t so = (size_t)(it - 4) * RVC_T;
 #pragma unroll
-	for (int j = 0; j < IPW; j++)
-		if (j < nj)
-			prof_end (P, sm, inst0 + j);
+			for (int t = 0; t < RVC_NTK; t++)
+				if (h + t * RVC_H < nj && (tap || hc == 0))
+					out[t][so] = yv[t];
+		}
+		__syncthreads ();
+	};
+#pragma unroll 1
+	for (int it = 0; it < nIt; it += 2) {
+		step (it, pB[0], pIn[0]);
+		if (it + 1 < nIt)
+			step (it + 1, pB[1], pIn[1]);
+	}
 }
 
 /* ================================================================== k_whirl */
@@ -2065,14 +1827,12 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 		sm.brake = brake;
 	}
 	__syncthreads ();
-	TBF_MARK (20);
 	const double   hornIncr = st.hornIncr, drumIncr = st.drumIncr;
 	const uint32_t WM       = (uint32_t)W - 1u;
 	/* serial filter coefficients: lane 0 horn A, lane 1 horn B, lanes 2-3 drum shelf */
 	const float* cfa = lane == 0 ? K.hafw : (lane == 1 ? K.hbfw : K.drf);
 	const float  fa0 = cfa[0], fa1 = cfa[1]; /* a1, a2 of the serial state recurrences */
 
-#pragma unroll WH_SB_UNROLL
 	for (int sb = 0; sb < TBF_BLK / TBF_SUB; sb++) {
 		const int      n      = lane;
 		const uint32_t outpos = (st.outpos + (uint32_t)n) & 2047u;
@@ -2118,18 +1878,11 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 			sm.aOut[n]      = (T0[n + 2] * K.hafw[2]) + (K.hafw[3] * T0[n + 1]) + (K.hafw[4] * T0[n]);
 			__syncthreads ();
 		}
-		if (WH_PRIO)
-			PRIO_UP ();
-		if ((TBF_ABL & 32) && lane < 4) {
-			for (int k = 0; k < TBF_SUB; k++)
-				sm.tmp[lane][2 + k] = 0.5f;
-		} else if (lane < 4 && (lane > 0 || aNext)) {
+		if (lane < 4 && (lane > 0 || aNext)) {
 			const float* ip = lane == 0 ? sm.xn : (lane == 1 ? sm.aOut : sm.rd[lane - 2]);
 			/* crossing into the next block: A's state gets that block's NaN scrub first */
 			wh_serial (ip, sm.tmp[lane], st.fz[lane], fa0, fa1, lane == 0 && sb + 1 == TBF_BLK / TBF_SUB);
 		}
-		if (WH_PRIO)
-			PRIO_DOWN ();
 		__syncthreads ();
 		{
 			/* filter outputs: horn B -> xf, drum shelves in place, horn A of the next
@@ -2188,7 +1941,6 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 				st.drumAngle = okd ? d0 + (double)TBF_SUB * Dd : wrap1 (angBuf[2 * TBF_SUB - 1] + drumIncr);
 		}
 		__syncthreads ();
-		TBF_MARK (21);
 		/* reflection filters FILTER_C (src/whirl.cpp:1472-1477), lane-parallel */
 		const float xf   = sm.xf[n + 4];
 		const float xfp  = n == 0 ? st.z[0] : sm.xf[n + 3];
@@ -2205,16 +1957,15 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 		sm.x2[n + 4]     = x2v;
 		const float xd2v = (float)((0.4 * xd1v) + (0.4 * sm.xd1[n]));
 		__syncthreads ();
-		TBF_MARK (22);
 
-		/* ---- rings (HL, HR, DL, DR) in groups of WH_MG: the group's motions first (their
+		/* ---- rings (HL, HR, DL, DR) in groups of 4: the group's motions first (their
 		 * table loads in flight together), then each ring's ordered adds ---- */
 #pragma unroll
-		for (int r0 = 0; r0 < 4; r0 += WH_MG) {
-			int   mu[WH_MG][3];
-			float ma[WH_MG][3], mb[WH_MG][3];
+		for (int r0 = 0; r0 < 4; r0 += 4) {
+			int   mu[4][3];
+			float ma[4][3], mb[4][3];
 #pragma unroll
-			for (int gi = 0; gi < WH_MG; gi++) {
+			for (int gi = 0; gi < 4; gi++) {
 				const int r = r0 + gi;
 	#pragma unroll
 				for (int q = 0; q < 3; q++) {
@@ -2230,20 +1981,12 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 						const float    h1   = (float)(ang * (unsigned int)16384 + K.hornPhase[p]);
 						const float    hd   = frac1 (h1);
 						const unsigned hl   = ((unsigned int)floorf (h1)) & 16383u;
-#if TBF_ABL & 64
-						const f2u      dp   = {hd, h1};
-#else
 						const f2u      dp   = *(const f2u*)(dsp + hl); /* dsp[hl], dsp[(hl + 1) & 16383] */
-#endif
 						const float    intp = dp.x * (1.f - hd) + hd * dp.y;
 						const unsigned kk   = ((unsigned int)roundf (h1)) & 16383u;
 						t                   = K.hornSpacing[p] + intp + (float)outpos;
 						const float* b      = bw + 5 * kk;
-#if TBF_ABL & 64
-						const f4u    b4     = {hd, intp, h1, t};
-#else
 						const f4u    b4     = *(const f4u*)b;
-#endif
 						xa                  = b4.x * hist[n + 4];
 						xa += b4.y * hist[n + 3];
 						xa += b4.z * hist[n + 2];
@@ -2267,17 +2010,16 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 					mb[gi][q]          = qq;
 				}
 			}
-			TBF_MARK (23);
 			/* fast path preconditions (wave votes), per ring: each motion's slot
 			 * non-decreasing in n with groups of <= 2 equal slots, and the ring's motions
 			 * >= 2 slots apart in source order at every sample (so passes farthest-first
 			 * keep the per-slot order: a farther motion reaches a slot only at earlier
 			 * samples); per motion: unit steps (unit_add instead of motion_add) */
-			bool     okr[WH_MG];
+			bool     okr[4];
 			uint32_t unit = 0;
 			bool     allOk = !(P.dbg & TBF_DEBUG_FORCE_SERIAL);
 #pragma unroll
-			for (int gi = 0; gi < WH_MG; gi++) {
+			for (int gi = 0; gi < 4; gi++) {
 				int ok = (mu[gi][1] >= mu[gi][0] + 2) && (mu[gi][2] >= mu[gi][1] + 2);
 	#pragma unroll
 				for (int q = 0; q < 3; q++) {
@@ -2293,16 +2035,13 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 				okr[gi] = __all (ok) && !(P.dbg & TBF_DEBUG_FORCE_SERIAL);
 				allOk   = allOk && okr[gi];
 			}
-			if (TBF_ABL & 16) {
-				if (lane == 0)
-					sm.wring[r0][mu[0][0] & (W - 1)] += ma[0][0] + mb[0][1] + ma[0][2];
-			} else if (allOk) {
+			if (allOk) {
 				/* every ring on its fast path: the rings are independent, so each pass
 				 * (farthest motion first) updates all of them in one LDS round trip */
 	#pragma unroll
 				for (int q = 2; q >= 0; q--) {
 	#pragma unroll
-					for (int gi = 0; gi < WH_MG; gi++) {
+					for (int gi = 0; gi < 4; gi++) {
 						if ((unit >> (gi * 3 + q)) & 1u)
 							unit_add<W> (sm.wring[r0 + gi], mu[gi][q], ma[gi][q], mb[gi][q], lane);
 						else
@@ -2312,7 +2051,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 				}
 			} else {
 #pragma unroll
-				for (int gi = 0; gi < WH_MG; gi++) {
+				for (int gi = 0; gi < 4; gi++) {
 					float* ring = sm.wring[r0 + gi];
 					if (okr[gi]) {
 						motion_add<W> (ring, mu[gi][2], ma[gi][2], mb[gi][2], lane);
@@ -2341,7 +2080,6 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 					}
 				}
 			}
-			TBF_MARK (24);
 		}
 		/* ---- outputs (whirlProc2 outHL/outHR/outDL/outDR + whirlProc3 mix) ---- */
 		{
@@ -2350,8 +2088,8 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 			const float hR   = K.hornLevel * hrv + leak;
 			const float dL   = sm.rd[0][n];
 			const float dR   = sm.rd[1][n];
-			stream_st (&oL[sb * TBF_SUB + n], hL * K.mic[0] + hR * K.mic[1] + dL * K.mic[2] + dR * K.mic[3]);
-			stream_st (&oR[sb * TBF_SUB + n], hL * K.mic[4] + hR * K.mic[5] + dL * K.mic[6] + dR * K.mic[7]);
+			oL[sb * TBF_SUB + n] = hL * K.mic[0] + hR * K.mic[1] + dL * K.mic[2] + dR * K.mic[3];
+			oR[sb * TBF_SUB + n] = hL * K.mic[4] + hR * K.mic[5] + dL * K.mic[6] + dR * K.mic[7];
 		}
 		/* ---- carry filter taps and histories ---- */
 		if (lane == NL - 1) {
@@ -2370,7 +2108,6 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 			st.outpos = (st.outpos + TBF_SUB) & 2047u;
 		}
 		__syncthreads ();
-		TBF_MARK (25);
 	}
 	if (lane == 0) {
 		/* NaN scrub, src/whirl.cpp:1622-1630 */
@@ -2398,14 +2135,12 @@ k_whirl (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 	const tbf_inst_const& K  = cst[inst];
 	tbf_wh_state*         S  = &P.st[inst].wh;
 	float*                wr = P.wring + (size_t)inst * 4 * W;
-	prof_begin (P, sm);
 	copy_words (&sm.st, S);
 	if (threadIdx.x == 0)
 		sm.aReady = 0;
 	for (uint32_t i = threadIdx.x; i < 4u * W; i += NL)
 		(&sm.wring[0][0])[i] = wr[i];
 	__syncthreads ();
-	TBF_MARK (26);
 	/* the input (lane n: samples n and n + 64 of a block) is loaded one block ahead, so
 	 * its latency overlaps a whole block instead of stalling a sub-block start */
 	const float* inBase = P.mid2 + (size_t)inst * P.midStride;
@@ -2433,12 +2168,10 @@ k_whirl (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 	copy_words (S, &sm.st);
 	for (uint32_t i = threadIdx.x; i < 4u * W; i += NL)
 		wr[i] = (&sm.wring[0][0])[i];
-	TBF_MARK (27);
-	prof_end (P, sm, inst);
 }
 
 /* ------------------------------------------------------------------ launch */
-/* stage k (0 k_tonegen, 1 k_rv_in, 2 k_rv_core, 3 k_rv_out, 4 k_whirl) of one launch chunk; the chain mode
+/* stage k (0 k_tonegen, 1 k_rv_pre, 2 k_rv_core, 3 k_rv_post, 4 k_whirl) of one launch chunk; the chain mode
  * decides which stages run (tbf_chain_stages) */
 extern "C" int tbf_launch_stage (const tbf_launch* P, int k, hipStream_t stream)
 {
@@ -2446,12 +2179,14 @@ extern "C" int tbf_launch_stage (const tbf_launch* P, int k, hipStream_t stream)
 		return 0;
 	if (P->chain != TBF_CHAIN_TONEGEN && (uint64_t)P->nBlocks * TBF_BLK > P->midStride)
 		return -22;
+	if ((k == 1 || k == 3) && P->nBlocks > NL) /* a launch's per-block wet levels sit one per lane */
+		return -22;
 	const dim3 grid (P->nInst), block (NL);
+	const dim3 cgrid ((P->nInst + RVC_CB - 1) / RVC_CB), cblock (RVC_THREADS);
 	if (k == 0)
 		hipLaunchKernelGGL (k_tonegen, grid, block, 0, stream, *P, P->ctl, P->tpls, P->cst);
 	else if (k == 1)
-		hipLaunchKernelGGL (k_rv_in<RVIN_IPW>, dim3 ((P->nInst + RVIN_IPW - 1) / RVIN_IPW), block, 0, stream, *P, P->cst,
-		                    P->ctl);
+		hipLaunchKernelGGL (k_rv_pre, cgrid, cblock, 0, stream, *P, P->cst, P->ctl);
 	else if (k == 2)
 		/* the LDS kernel loads and stores a channel's 129.7 KB of rings per launch; the
 		 * streaming kernel moves 24.6 KB per block: below 8 blocks the streaming one
@@ -2461,8 +2196,7 @@ extern "C" int tbf_launch_stage (const tbf_launch* P, int k, hipStream_t stream)
 		else
 			hipLaunchKernelGGL (k_rv_core, dim3 (2 * P->nInst), block, 0, stream, *P, P->cst);
 	else if (k == 3)
-		hipLaunchKernelGGL (k_rv_out<RVOUT_IPW>, dim3 ((P->nInst + RVOUT_IPW - 1) / RVOUT_IPW), block, 0, stream, *P,
-		                    P->cst, P->ctl);
+		hipLaunchKernelGGL (k_rv_post, cgrid, cblock, 0, stream, *P, P->cst, P->ctl);
 	else if (k == 4) {
 		switch (P->wringLen) {
 			case 512: hipLaunchKernelGGL (k_whirl<512>, grid, block, 0, stream, *P, P->cst, P->ctl); break;

@@ -13,7 +13,6 @@
 #define TBF_BLK 128   /* BUFFER_SIZE_SAMPLES, src/tonegen.h:53 */
 #define TBF_SUB 64    /* sub-block for reverb/whirl: one sample per lane of a wave64 */
 #define TBF_NW 256    /* NOF_WHEELS, src/tonegen.h:79 */
-#define TBF_PROF_SLOTS 32
 #define TBF_VRING 256
 #define TBF_WH_TSTRIDE 16388 /* device stride of the whirl displacement tables (16-byte aligned rows) */
 #define TBF_XS_JUMP 129 /* dither jump table columns: k = 0 .. 128 steps */ /* compact vibrato ring (reference 1024; live window <= 21+128) */
@@ -147,11 +146,19 @@ typedef struct tbf_rv_chan { /* one channel of the feedback network: k_rv_core w
 	double   phHi[8];
 } tbf_rv_chan;
 
-typedef struct tbf_rv_state { /* reverb: k_rv_in / k_rv_core / k_rv_out */
-	int32_t     countM;       /* predelay counter (k_rv_in) */
-	uint32_t    fpdL, fpdR;   /* dither streams as advanced by k_rv_in ... */
-	uint32_t    fpdL2, fpdR2; /* ... and the identical copies advanced by k_rv_out */
-	uint32_t    pad0[3];
+/* the predelay (src/reverb.cpp:350-358) as a history of raw inputs: the ring slot read at
+ * sample m holds the guarded input of sample m - delayM, so k_rv_pre reads the chunk's
+ * input (or this history, for the first delayM samples of a chunk) delayM samples back
+ * and guards it with the dither state of that sample.  TBF_PD_HIST floats per instance,
+ * indexed by absolute sample position mod TBF_PD_HIST, in the slab's line-12 region. */
+#define TBF_PD_HIST 1024
+
+typedef struct tbf_rv_state { /* reverb: k_rv_pre / k_rv_core / k_rv_post */
+	int32_t     pdAge;        /* samples rendered, saturating at delayM (the predelay reads 0 before) */
+	uint32_t    fpdL, fpdR;   /* dither streams as advanced by k_rv_pre: the state delayM samples back ... */
+	uint32_t    fpdL2, fpdR2; /* ... and the stream itself, advanced by k_rv_post */
+	uint32_t    pdPos;        /* history position of the next input (mod TBF_PD_HIST) */
+	uint32_t    pad0[2];
 	double      bq[3][4]; /* [A/B/C][L7, L8, R9, R10] */
 	tbf_rv_chan ch[2];
 } tbf_rv_state;
@@ -190,8 +197,8 @@ typedef struct tbf_launch {
 	float*                wring; /* [inst][4][wring_len] */
 	float*                mid1;  /* [inst][midStride] preamp output of the chunk */
 	float*                mid2;  /* [inst][midStride] reverb output of the chunk */
-	double*               rvA;   /* [inst][2][midStride] k_rv_in -> k_rv_core: sin(biquadA * wet) */
-	double*               rvB;   /* [inst][2][midStride] k_rv_core -> k_rv_out: tap mix */
+	double*               rvA;   /* [inst][2][midStride] k_rv_pre -> k_rv_core: sin(biquadA * wet) */
+	double*               rvB;   /* [inst][2][midStride] k_rv_core -> k_rv_post: tap mix */
 	uint64_t              midStride;
 	double*               rslab; /* [inst][slabLen] */
 	const tbf_seg_ctl*    ctl;    /* control pool: [0, nInst) current per instance, then this chunk's deltas */
@@ -224,7 +231,6 @@ typedef struct tbf_launch {
 	uint32_t              rvLds;     /* 1: the reverb core with its rings resident in LDS (k_rv_core_lds) */
 	const uint32_t*       coff;      /* [tpl][385] keyContrib offsets into contrib */
 	const tbf_contrib*    contrib;
-	uint64_t*             prof;      /* [inst][TBF_PROF_SLOTS] stage cycle sums, or NULL */
 } tbf_launch;
 
 #endif

@@ -16,7 +16,7 @@ _u32p = C.POINTER(C.c_uint32)
 
 
 # the render kernels of one launch chunk, in stream order (tbf_debug_kernel_times)
-STAGES = ("k_tonegen", "k_rv_in", "k_rv_core", "k_rv_out", "k_whirl")
+STAGES = ("k_tonegen", "k_rv_pre", "k_rv_core", "k_rv_post", "k_whirl")
 
 
 class TbfError(RuntimeError):

@@ -112,7 +112,8 @@ int tbf_engine_destroy (tbf_engine* e);
  * src/tonegen.cpp:914-927). */
 int tbf_config_set (tbf_engine* e, const char* key, const char* value);
 /* a cfg file's text (`name = value` lines, '#' comments): returns the number of keys
- * applied, or < 0 with tbf_last_error () = "line N: message" */
+ * applied, or < 0 with tbf_last_error () = "line N: message".  All or nothing: a bad line
+ * (or a table-shaping key after tbf_instances_add) applies none of the text's keys. */
 int tbf_config_parse (tbf_engine* e, const char* text);
 
 /* Tone-generator template (initToneGenerator's shared tables: wave bank, play matrix,
@@ -218,7 +219,7 @@ int tbf_render_events (tbf_engine* e, uint32_t nblocks, const tbf_event* ev, uin
                        float* d_outR, uint64_t stride, void* stream);
 
 int tbf_synchronize (tbf_engine* e);
-/* Which exact-but-slow paths the kernels took since the engine was created (cumulative,
+/* Which exact-but-slow paths the kernels took since the engine's first render (cumulative,
  * informational; the results are bit-identical either way).  Waits for the engine's
  * own stream and the pipelined stage streams; a caller rendering on its own stream must
  * synchronize that stream first. */

@@ -483,6 +483,78 @@ def test_gpu_synth_sound_irregular_periods(oracle, tunings):
     eng.close()
 
 
+def test_gpu_lv2_synth_sound_run_loop(oracle):
+    """The LV2 binding of INTEGRATION.md section 2, compiled verbatim (libtbf_lv2.so),
+    driven like the plugin's run() (b_synth/lv2.cpp:1120-1140): per period, for each MIDI
+    event at frame t, `written = synthSound (b3s, written, t)` when written + 128 < t < n,
+    then the event; finally `written = synthSound (b3s, written, n)`.  Irregular periods
+    (1 .. 700 frames) and events inside them: each event lands at the next block the FIFO
+    renders, so the audio equals the oracle's render with the events at those blocks."""
+    import ctypes as C
+    from pathlib import Path
+    import tunebfree_amd as T
+    from orc_bind import Template
+    lv2 = C.CDLL(str(Path(__file__).resolve().parents[1] / "tunebfree_amd" / "libtbf_lv2.so"))
+    lv2.tbf_lv2_synth_sound.restype = C.c_uint32
+    lv2.tbf_lv2_synth_sound.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]
+    lv2.tbf_lv2_key.restype = None
+    lv2.tbf_lv2_key.argtypes = [C.c_void_p, C.c_int, C.c_int]
+    lv2.tbf_lv2_instantiate.restype = C.c_void_p
+    lv2.tbf_lv2_instantiate.argtypes = [C.c_double]
+    # tbf_instantiate_engine itself (seeded by time(NULL), so no oracle twin): it must build
+    # and render finite audio through synthSound
+    h = lv2.tbf_lv2_instantiate(48000.0)
+    assert h
+    buf = np.zeros((2, 300), np.float32)
+    lv2.tbf_lv2_key(h, 60, 1)
+    assert lv2.tbf_lv2_synth_sound(h, 0, 300, buf[0].ctypes.data, buf[1].ctypes.data) == 300
+    assert np.isfinite(buf).all()
+    T.load_library().tbf_engine_destroy(C.c_void_p(h))
+
+    eng = _engine()
+    tid = eng.template(seed=7)
+    eng.add_instances([tid], [3001])
+    tpl = Template(oracle, seed=7)
+    for (k, a, v) in S.jazz1_params():
+        eng.set_param(0, a, v)
+    oscen = [[(0, k, a, v) for (k, a, v) in S.jazz1_params()]]
+    rng = np.random.default_rng(11)
+    served, out = 0, []  # frames the FIFO has served
+    keys_down = []
+    for c in range(48):
+        n = int(rng.choice([1, 37, 64, 128, 129, 256, 300, 515, 700]))
+        L = np.zeros(n, np.float32)
+        R = np.zeros(n, np.float32)
+        nev = int(rng.integers(0, 3))
+        frames = sorted(int(x) for x in rng.integers(0, n, size=nev))
+        written = 0
+        for t in frames:
+            if written + 128 < t < n:
+                written = lv2.tbf_lv2_synth_sound(eng._h, written, t, L.ctypes.data, R.ctypes.data)
+            key = 48 + int(rng.integers(0, 36))
+            on = 0 if (keys_down and rng.random() < 0.4) else 1
+            if not on:
+                key = keys_down.pop(0)
+            else:
+                keys_down.append(key)
+            lv2.tbf_lv2_key(eng._h, key, on)
+            oscen[0].append((-(-(served + written) // 128), "note", key, on))
+        written = lv2.tbf_lv2_synth_sound(eng._h, written, n, L.ctypes.data, R.ctypes.data)
+        assert written == n
+        served += n
+        out.append((L, R))
+    L = np.concatenate([o[0] for o in out])[None]
+    R = np.concatenate([o[1] for o in out])[None]
+    nb = -(-served // 128)
+    oL, oR, *_ = oracle_run(oracle, tpl, [3001], oscen, nb)
+    eL, xL = compare(L, oL[:, :served])
+    eR, xR = compare(R, oR[:, :served])
+    print(f"lv2 run loop: {served} frames, {len(oscen[0])} events: max|err| L={eL:.3g} R={eR:.3g} "
+          f"bit-exact L={xL:.6f} R={xR:.6f}")
+    assert max(eL, eR) <= TOL
+    eng.close()
+
+
 def test_gpu_cli_host_synth_sound(oracle, tmp_path):
     """§8(f) row 3: the headless host shell (tunebfree_amd/tbf_cli, the counterpart of
     src/main.cpp:243-292 and b_synth/lv2.cpp:212-239) pulls 256-frame periods through

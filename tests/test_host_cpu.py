@@ -40,6 +40,22 @@ def test_abi_exports_every_declared_symbol():
     assert lib.tbf_abi_version() == 1
 
 
+def test_integration_lv2_binding_is_the_compiled_one():
+    """INTEGRATION.md section 2's synthSound patch is the marked section of
+    tunebfree_amd/hosts/lv2_synth.h, which libtbf_lv2.so compiles (b_synth/lv2.cpp:212's
+    uint32_t synthSound (B3S*, uint32_t written, uint32_t nframes, float**))."""
+    h = (ROOT / "tunebfree_amd" / "hosts" / "lv2_synth.h").read_text()
+    blk = h.split("/* --8<-- INTEGRATION.md section 2 */\n", 1)[1].split("/* -->8-- */", 1)[0].rstrip()
+    doc = (ROOT / "INTEGRATION.md").read_text()
+    sec = doc.split("## 2.", 1)[1].split("## 3.", 1)[0]
+    code = sec.split("```c++\n", 1)[1].split("```", 1)[0]
+    assert code == '#include "tbf.h"\n\n' + blk + "\n"
+    assert "static uint32_t synthSound (B3S* b3s, uint32_t written, uint32_t nframes, float** out)" in blk
+    lv2 = C.CDLL(str(ROOT / "tunebfree_amd" / "libtbf_lv2.so"))
+    for n in ("tbf_lv2_synth_sound", "tbf_lv2_key", "tbf_lv2_instantiate"):
+        assert hasattr(lv2, n), n
+
+
 def _bind_debug(lib):
     lib.tbf_debug_contrib.restype = C.c_int
     lib.tbf_debug_contrib.argtypes = [C.c_void_p, C.c_uint32, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -430,6 +446,13 @@ def test_config_api_semantics():
         eng.config_parse("reverb.mix=0.2\nnot a key value line\n")
     with pytest.raises(T.TbfError, match="line 3"):
         eng.config_parse("reverb.mix=0.2\n\nscanner.hz=30\n")
+    # all or nothing: a bad line leaves even the earlier, well-formed keys unapplied
+    w0 = eng.layout()["wring_len"]
+    with pytest.raises(T.TbfError, match="line 2"):
+        eng.config_parse("whirl.horn.radius = 80\nnot a key value line\n")
+    assert eng.layout()["wring_len"] == w0
+    assert eng.config_parse("whirl.horn.radius = 80\n") == 1 and eng.layout()["wring_len"] > w0
+    assert eng.config_parse("whirl.horn.radius = 25\n") == 1 and eng.layout()["wring_len"] == w0
     tid = eng.template(seed=3)
     eng.add_instances([tid], [5])
     # engine-wide tables are fixed once instances exist; per-instance / template keys are not

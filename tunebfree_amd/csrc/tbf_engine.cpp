@@ -827,9 +827,13 @@ int tbf_config_parse (tbf_engine* e, const char* text)
 	if (!e || !text)
 		return fail (-22, "null argument");
 	/* parseConfigurationLine (src/cfgParser.cpp:94-160): `name = value`, '#' comments,
-	 * surrounding blanks trimmed */
-	int         applied = 0, line = 0;
-	const char* p       = text;
+	 * surrounding blanks trimmed.  All or nothing: every line is validated into a copy of
+	 * the configuration first, and the copy replaces the engine's only when all pass, so
+	 * a caller that gets an error knows that no key took effect. */
+	Config      c       = e->conf;
+	int         applied = 0, line = 0, scope = 0;
+	std::string sharedKey;
+	const char* p = text;
 	while (*p) {
 		const char* q = p;
 		while (*q && *q != '\n')
@@ -848,12 +852,30 @@ int tbf_config_parse (tbf_engine* e, const char* text)
 		if (trim (ln).empty ())
 			continue;
 		if (eq == std::string::npos)
-			return fail (-22, "line " + std::to_string (line) + ": expected name=value");
+			return fail (-22, "line " + std::to_string (line) + ": expected name=value (nothing applied)");
 		const std::string k = trim (ln.substr (0, eq)), v = trim (ln.substr (eq + 1));
-		const int         rc = tbf_config_set (e, k.c_str (), v.c_str ());
-		if (rc < 0)
-			return fail (rc, "line " + std::to_string (line) + ": " + tbf_last_error ());
-		applied += rc == 0;
+		int               sc = 0;
+		const int         rc = configSet (c, k.c_str (), v.c_str (), &sc);
+		if (rc == -1)
+			return fail (-22, "line " + std::to_string (line) + ": bad value for " + k + ": " + v + " (nothing applied)");
+		if (rc == 0)
+			continue; /* not a key of the hot path: ignored, as the reference ignores it */
+		if ((sc & CFG_SHARED) && sharedKey.empty ())
+			sharedKey = k;
+		scope |= sc;
+		applied++;
+	}
+	if ((scope & CFG_SHARED) && !e->inst.empty ())
+		return fail (-16, sharedKey + " shapes the engine-wide tables: set it before tbf_instances_add (nothing applied)");
+	const Config old = e->conf;
+	e->conf          = c;
+	if (scope & CFG_SHARED) {
+		if (int r = buildShared (e)) {
+			e->conf = old;
+			(void)buildShared (e);
+			return r;
+		}
+		e->deviceReady = false;
 	}
 	return applied;
 }
@@ -976,6 +998,7 @@ static int ensureDevice (tbf_engine* e)
 			HIPCHK (hipMemcpy (e->contrib.p, ent.data (), ent.size () * sizeof (tbf_contrib), hipMemcpyHostToDevice));
 	}
 	/* shared tables */
+	const bool errNew = e->err.p == nullptr; /* the path flags are cumulative from the first allocation */
 	if (e->vib.ensure (e->vibTab.size ()) || e->whTab.ensure (4 * (size_t)TBF_WH_TSTRIDE) || e->whBw.ensure (e->wt.bw.size ()) ||
 	    e->err.ensure (4))
 		return fail (-12, "out of device memory (tables)");
@@ -1003,7 +1026,8 @@ static int ensureDevice (tbf_engine* e)
 		HIPCHK (hipMemcpy (e->whTab.p, padded.data (), padded.size () * 4, hipMemcpyHostToDevice));
 	}
 	HIPCHK (hipMemcpy (e->whBw.p, e->wt.bw.data (), e->wt.bw.size () * 4, hipMemcpyHostToDevice));
-	HIPCHK (hipMemset (e->err.p, 0, 16));
+	if (errNew)
+		HIPCHK (hipMemset (e->err.p, 0, 16));
 	/* per-instance buffers: new instances start from their initial state, existing
 	 * instances keep their device state */
 	const uint32_t old = e->devInst;
@@ -1100,7 +1124,7 @@ static bool stepControl (tbf_engine* e, uint32_t i, bool& progChanged, tbf_tgc_r
 		return false;
 	if (tgDirty && rec) {
 		/* device control: the front end here, the per-wheel part in k_tgctl */
-		const size_t k  = std::min<size_t> (in.tg.msg.size (), 0xFFFF);
+		const size_t k  = in.tg.msg.size ();
 		const size_t kg = in.tg.gainsDue () ? 27 : 0; /* the drawbar gains, when they changed */
 		if (msgOut) { /* a host worker's own message and gain lists (renderImpl merges them) */
 			const uint32_t at = (uint32_t)msgOut->size (), ag = (uint32_t)gainOut->size ();

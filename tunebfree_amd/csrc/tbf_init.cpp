@@ -970,14 +970,14 @@ void TgControl::stepFront (uint16_t* msgDst, uint32_t msgOff, float* gainDst, ui
 	const bool sendGains = gainsDue (); /* gainDst holds 27 floats then */
 	memset (&rec, 0, sizeof (rec));
 	rec.msgOff = msgOff;
-	rec.nMsg   = (uint16_t)std::min<size_t> (msg.size (), 0xFFFF);
+	rec.nMsg   = (uint32_t)msg.size (); /* every message of the block, as the host path */
 	std::copy (msg.begin (), msg.begin () + rec.nMsg, msgDst);
 	const bool recompute = oldRouting != newRouting;
 	if (recompute)
 		oldRouting = newRouting;
 	rec.flags       = (uint8_t)(0x80 | (drawBarChange ? 1 : 0) | (recompute ? 2 : 0) | (sendGains ? 4 : 0));
 	rec.oldRouting  = (uint8_t)oldRouting;
-	rec.percSendBus = percSendBus;
+	rec.percSendBus = (uint16_t)percSendBus;
 	if (sendGains) {
 		memcpy (gainDst, drawBarGain, sizeof (drawBarGain));
 		rec.gainOff = gainOff;

@@ -43,12 +43,12 @@ typedef struct tbf_prog_entry {
  * hands each stepped block this record */
 typedef struct tbf_tgc_rec {
 	uint32_t msgOff;         /* the block's key messages (0x1000 | key: on, key: off) ... */
-	uint16_t nMsg;           /* ... msgs[msgOff .. msgOff + nMsg) */
-	uint8_t  flags;          /* 1 drawBarChange, 2 recomputeRouting, 4 gains follow, 0x80 stepped */
-	uint8_t  oldRouting;     /* routing word after this block's update */
-	uint32_t percSendBus;
+	uint32_t nMsg;           /* ... msgs[msgOff .. msgOff + nMsg), all of the block's */
 	uint32_t gainOff;        /* flags & 4: the instance's drawBarGain[27] at gains[gainOff ..]
 	                          * (sent when they change; k_tgctl keeps them in tbf_tgc_state) */
+	uint8_t  flags;          /* 1 drawBarChange, 2 recomputeRouting, 4 gains follow, 0x80 stepped */
+	uint8_t  oldRouting;     /* routing word after this block's update */
+	uint16_t percSendBus;    /* a bus index (< 27) */
 } tbf_tgc_rec;
 
 /* one keyContrib element on the device (Contrib): a key's list is sorted by wheel, then

@@ -1,0 +1,42 @@
+"""Build-variant generator (profiling only, never the product): a copy of
+csrc/tbf_render.hip whose k_whirl accumulates s_memtime cycles per phase of stage_whirl on
+lane 0 and writes them, as floats, over the first 16 output samples of instances 0..7
+(tools/whirl_prof.py reads them back).  usage: python tools/whirl_prof_patch.py OUT.hip"""
+import sys
+from pathlib import Path
+
+src = (Path(__file__).resolve().parents[1] / "tunebfree_amd" / "csrc" / "tbf_render.hip").read_text()
+
+
+def ins_after(s, anchor, text, nth=1):
+    i = -1
+    for _ in range(nth):
+        i = s.index(anchor, i + 1)
+    j = i + len(anchor)
+    return s[:j] + text + s[j:]
+
+
+s = src
+s = s.replace("\tint          aReady;              /* aOut holds the current sub-block's horn A output */",
+              "\tint          aReady;              /* aOut holds the current sub-block's horn A output */\n"
+              "\tunsigned long long wp[16], wplast;")
+mark = lambda k: f"\n\t\tif (threadIdx.x == 0) {{ const unsigned long long _t = __builtin_amdgcn_s_memtime (); sm.wp[{k}] += _t - sm.wplast; sm.wplast = _t; }}"
+# block start (whirl_speed) and per-sub-block phases
+s = ins_after(s, "\t\tsm.brake = brake;\n\t}\n\twave_sync ();", mark(9))
+s = ins_after(s, "\t\t\tsm.x2[i] = st.adx[2][(st.adi[2] + 3 - i) & 7];\n\t\t}\n\t\twave_sync ();", mark(1))
+s = ins_after(s, "\t\t\twh_serial (ip, sm.tmp[lane], st.fz[lane], fa0, fa1, lane == 0 && sb + 1 == TBF_BLK / TBF_SUB);\n\t\t}\n\t\twave_sync ();", mark(3))
+s = ins_after(s, "\t\t\t\tst.drumAngle = okd ? d0 + (double)TBF_SUB * Dd : wrap1 (angBuf[2 * TBF_SUB - 1] + drumIncr);\n\t\t}\n\t\twave_sync ();", mark(4))
+s = ins_after(s, "\t\tconst float xd2v = (float)((0.4 * xd1v) + (0.4 * sm.xd1[n]));\n\t\twave_sync ();", mark(5))
+s = s.replace("\t\t\tbool     okr[4];", mark(6).replace("\n\t\t", "\n\t\t\t") + "\n\t\t\tbool     okr[4];")
+s = s.replace("\t\t/* ---- outputs (whirlProc2 outHL/outHR/outDL/outDR + whirlProc3 mix) ---- */",
+              mark(7)[1:] + "\n\t\t/* ---- outputs (whirlProc2 outHL/outHR/outDL/outDR + whirlProc3 mix) ---- */")
+s = ins_after(s, "\t\t\tst.outpos = (st.outpos + TBF_SUB) & 2047u;\n\t\twave_sync ();", mark(8))
+# init and write-out in k_whirl
+s = s.replace("\tif (threadIdx.x == 0)\n\t\tsm.aReady = 0;",
+              "\tif (threadIdx.x == 0)\n\t\tsm.aReady = 0;\n\tif (threadIdx.x < 16) sm.wp[threadIdx.x] = 0;\n"
+              "\tif (threadIdx.x == 0) sm.wplast = __builtin_amdgcn_s_memtime ();")
+s = s.replace("\twave_sync ();\n\tcopy_words (S, &sm.st);\n\tfor (uint32_t i = threadIdx.x; i < 4u * W; i += NL)\n\t\twr[i] = (&sm.wring[0][0])[i];\n}",
+              "\twave_sync ();\n\tcopy_words (S, &sm.st);\n\tfor (uint32_t i = threadIdx.x; i < 4u * W; i += NL)\n\t\twr[i] = (&sm.wring[0][0])[i];\n"
+              "\tif (inst < 8 && threadIdx.x < 16) P.outL[(size_t)inst * P.outStride + P.outOffset + threadIdx.x] = (float)sm.wp[threadIdx.x];\n}")
+assert s.count("sm.wp[") >= 10, s.count("sm.wp[")
+Path(sys.argv[1]).write_text(s)

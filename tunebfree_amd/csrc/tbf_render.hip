@@ -144,6 +144,16 @@ __device__ __forceinline__ int wave_max (int v)
 	return v;
 }
 
+/* LDS ordering between the lanes of a one-wave workgroup: a wave's LDS instructions
+ * execute in issue order, so a read after a write sees it without a wait; only the
+ * compiler must not move LDS accesses across this point (s_barrier and its lgkmcnt(0)
+ * drain would expose the LDS latency at every sync) */
+__device__ __forceinline__ void wave_sync ()
+{
+	__builtin_amdgcn_fence (__ATOMIC_ACQ_REL, "wavefront");
+	__builtin_amdgcn_wave_barrier ();
+}
+
 /* Whole-wave lane shifts by DPP (wave_shr:1 / wave_shl:1, GFX9 DPP controls 0x138 /
  * 0x130): lane i receives lane i-1 (shr) or i+1 (shl); the lane with no source keeps
  * its own value (callers mask it).  VALU-only, unlike __shfl_up/down (ds_bpermute). */
@@ -848,23 +858,40 @@ k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
  * the ring addressing needs no per-line lane reads; tbf_rv_lds_fits checks an instance
  * against them */
 constexpr int RVL_DLY[12] = {1927, 1781, 1732, 1634, 1488, 1439, 1293, 1146, 1049, 1000, 902, 756};
-constexpr int RVL_OFS[12] = {0, 1928, 3712, 5448, 7088, 8584, 10024, 11320, 12472, 13528, 14536, 15440};
+constexpr int RVL_OFS[12] = {0, 1928, 3712, 5448, 7088, 8584, 10024, 11320, 12472, 13528, 14536, 15440}; /* in HBM */
+/* In LDS each line of delay d holds its d + 1 slots followed by a mirror of slots
+ * 0 .. RVL_MIR - 1, so the reads of a sub-block (slots count + 1 .. count + 71 for the
+ * taps, count + 1 .. count + 64 for the allpasses, with count in [0, d]) never wrap: a tap
+ * pair is two adjacent doubles (one ds_read2_b64) at a plain index.  A write to a slot
+ * below RVL_MIR also writes its mirror. */
+#define RVL_MIR 72
+constexpr int rvl_lofs (int l) { return l == 0 ? 0 : rvl_lofs (l - 1) + ((RVL_DLY[l - 1] + 1 + RVL_MIR + 1) & ~1); }
+constexpr int RVL_LOFS[12] = {rvl_lofs (0), rvl_lofs (1), rvl_lofs (2),  rvl_lofs (3),  rvl_lofs (4),  rvl_lofs (5),
+                              rvl_lofs (6), rvl_lofs (7), rvl_lofs (8), rvl_lofs (9), rvl_lofs (10), rvl_lofs (11)};
+#define RVL_RING (rvl_lofs (12)) /* LDS ring doubles of a channel's lines 0..11 with their mirrors */
 #define RVL_MIN_BLOCKS 8 /* shorter launches take the streaming k_rv_core */
-#define RVL_RING 16384 /* LDS ring doubles: lines 0..11 of a channel, 8-padded (16,216 at the fixed settings) */
 #define RVL_THREADS (NL * (RVL_G + 1)) /* RVL_G worker waves + the planner wave */
 
 struct RvLds {
 	double      ring[RVL_RING];
-	double      sd[2][8][TBF_SUB];     /* sine rows of each line's closed-form step, by group parity */
-	double      cm[2][8][TBF_SUB];
+	double2     sc[2][8][TBF_SUB];     /* sine rows of each line's closed-form step, by group parity:
+	                                    * {sin ((n+1) D), 2 sin^2 ((n+1) D / 2)}, one 16-B read */
 	double      tabD[2][8];            /* the step each row holds (-1: none) */
 	double      v0[2][RVL_G][8];       /* group plan: phase of line l at the start of sub-block j ... */
-	double      S[2][RVL_G][8];        /* ... and its sine and cosine (closed-form lines) */
-	double      C[2][RVL_G][8];
+	double2     SC[2][RVL_G][8];       /* ... and its {sine, cosine} (closed-form lines) */
 	uint32_t    okm[2][RVL_G];         /* closed-form lines of sub-block j */
 	double      carry[2][RVL_G][8];    /* feedback of sub-block j's last sample */
 	tbf_rv_chan st;
 };
+static_assert (sizeof (RvLds) <= 160 * 1024, "k_rv_core_lds: a channel's rings fill gfx950's 160 KB of LDS");
+
+/* a ring write at slot i of a line of delay d, and at its mirror when i < RVL_MIR */
+__device__ __forceinline__ void rvl_write (double* rg, int i, int d, double v)
+{
+	rg[i] = v;
+	if (i < RVL_MIR)
+		rg[i + d + 1] = v;
+}
 
 /* the planner wave: the phase plan of group g into buffer b (start phases, closed-form
  * flags, sincos of the start phases, sine rows); st.vib advanced past the group.  It
@@ -886,8 +913,7 @@ __device__ __forceinline__ void rvl_plan (RvLds& sm, double d, int nb, int b, bo
 		if (sm.tabD[b][l] != Dl) { /* rare: a new step (binade) */
 			const double dn  = (double)(lane + 1) * Dl; /* exact */
 			const double h   = sin (dn * 0.5);
-			sm.sd[b][l][lane] = sin (dn);
-			sm.cm[b][l][lane] = 2.0 * h * h;
+			sm.sc[b][l][lane] = double2 {sin (dn), 2.0 * h * h};
 			__builtin_amdgcn_wave_barrier ();
 			if (lane == 0)
 				sm.tabD[b][l] = Dl;
@@ -901,8 +927,7 @@ __device__ __forceinline__ void rvl_plan (RvLds& sm, double d, int nb, int b, bo
 			double       sv, cv;
 			sincos (v, &sv, &cv);
 			sm.v0[b][j][li] = v;
-			sm.S[b][j][li]  = sv;
-			sm.C[b][j][li]  = cv;
+			sm.SC[b][j][li] = double2 {sv, cv};
 		}
 	}
 	if (lane < RVL_G)
@@ -927,8 +952,7 @@ __device__ __forceinline__ void rvl_plan (RvLds& sm, double d, int nb, int b, bo
 				if (oj) {
 					double sv, cv;
 					sincos (v, &sv, &cv);
-					sm.S[b][j][li] = sv;
-					sm.C[b][j][li] = cv;
+					sm.SC[b][j][li] = double2 {sv, cv};
 					atomicOr (&sm.okm[b][j], 1u << li);
 					v = v + (double)TBF_SUB * Dj;
 				} else {
@@ -955,32 +979,38 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 	const tbf_inst_const& K     = cst[inst];
 	tbf_rv_chan*          S     = &P.st[inst].rv.ch[c];
 	const uint32_t        rbase = K.ringOff[c * 13];
-	const uint32_t        rlen2 = (K.ringOff[c * 13 + 12] - rbase) / 2; /* lines 0..11 (contiguous), double2 */
-	double*               slab  = P.rslab + (size_t)inst * P.slabLen + rbase;
+	double*               slab  = P.rslab + (size_t)inst * P.slabLen + rbase; /* lines 0..11 at RVL_OFS */
 	const double*         a0s   = rv_buf (P.rvA, P, inst, c);
 	double*               bout  = rv_buf (P.rvB, P, inst, c);
-	/* lane l < 12: delay and counter of line l (the LDS ring offsets are RVL_OFS) */
+	/* lane l < 12: delay and counter of line l (the LDS ring offsets are RVL_LOFS) */
 	const int dlyv = n < 12 ? K.delay[n] : 0;
 	const double vdl = K.vibDelta[n & 7]; /* lane-held: no vector load of K inside the loop */
 	const uint32_t nSub  = P.nBlocks * (TBF_BLK / TBF_SUB);
 	const uint32_t nGrp  = (nSub + RVL_G - 1) / RVL_G;
 	const bool     force = (P.dbg & TBF_DEBUG_FORCE_SERIAL) != 0;
 	if (w < RVL_G) {
-		/* the workers load the rings: every load in flight before the first LDS store
-		 * (clamped indices keep the loads unconditional) */
+		/* the workers load the rings and fill the mirrors: every load in flight before the
+		 * first LDS store (clamped indices keep the loads unconditional) */
 		constexpr int WT = NL * RVL_G;
-		constexpr int NR = (RVL_RING / 2 + WT - 1) / WT;
-		double2       v[NR];
 #pragma unroll
-		for (int k = 0; k < NR; k++) {
-			const uint32_t i = tid + k * WT;
-			v[k]             = ((const double2*)slab)[i < rlen2 ? i : 0];
-		}
+		for (int l0 = 0; l0 < 12; l0 += 6) { /* six lines' loads in flight at a time */
+			double v[6][(RVL_DLY[0] + 1 + RVL_MIR + WT - 1) / WT];
 #pragma unroll
-		for (int k = 0; k < NR; k++) {
-			const uint32_t i = tid + k * WT;
-			if (i < rlen2)
-				((double2*)sm.ring)[i] = v[k];
+			for (int l = l0; l < l0 + 6; l++)
+#pragma unroll
+				for (int k = 0; k * WT < RVL_DLY[l] + 1 + RVL_MIR; k++) {
+					const int i = tid + k * WT; /* LDS slot: i <= d canonical, then the mirror */
+					const int j = i <= RVL_DLY[l] ? i : (i - RVL_DLY[l] - 1 < RVL_MIR ? i - RVL_DLY[l] - 1 : 0);
+					v[l - l0][k] = slab[RVL_OFS[l] + j];
+				}
+#pragma unroll
+			for (int l = l0; l < l0 + 6; l++)
+#pragma unroll
+				for (int k = 0; k * WT < RVL_DLY[l] + 1 + RVL_MIR; k++) {
+					const int i = tid + k * WT;
+					if (i < RVL_DLY[l] + 1 + RVL_MIR)
+						sm.ring[RVL_LOFS[l] + i] = v[l - l0][k];
+				}
 		}
 	} else {
 		/* meanwhile the planner loads the channel state and plans the first group, which
@@ -1033,28 +1063,41 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 		if (pst)
 			rv_st (&bout[po], pmix);
 		if (act) {
-			const uint32_t om = sm.okm[par][w];
-			double         I[8];
+			/* the lines' vibrato sines: closed form on every line (wave-uniform, the rule), or
+			 * per line the closed form or the literal recurrence and sin */
+			const uint32_t om = __builtin_amdgcn_readfirstlane (sm.okm[par][w]);
+			double         sn[8];
+			if (om == 0xffu) {
+#pragma unroll
+				for (int l = 0; l < 8; l++) {
+					const double2 SC = sm.SC[par][w][l], q = sm.sc[par][l][n];
+					sn[l]            = SC.x + ((SC.y * q.x) - (SC.x * q.y));
+				}
+			} else {
+#pragma unroll
+				for (int l = 0; l < 8; l++) {
+					if ((om >> l) & 1) {
+						const double2 SC = sm.SC[par][w][l], q = sm.sc[par][l][n];
+						sn[l]            = SC.x + ((SC.y * q.x) - (SC.x * q.y));
+					} else {
+						const double dl = rld (vdl, l);
+						double       v  = sm.v0[par][w][l];
+						for (int i = 0; i <= n; i++)
+							v += dl;
+						sn[l] = sin (v);
+					}
+				}
+			}
+			double I[8];
 #pragma unroll
 			for (int l = 0; l < 8; l++) {
-				double sn;
-				if ((om >> l) & 1) {
-					const double Sv = sm.S[par][w][l], Cv = sm.C[par][w][l];
-					sn              = Sv + ((Cv * sm.sd[par][l][n]) - (Sv * sm.cm[par][l][n]));
-				} else {
-					const double dl = rld (vdl, l);
-					double       v  = sm.v0[par][w][l];
-					for (int i = 0; i <= n; i++)
-						v += dl;
-					sn = sin (v);
-				}
-				const double  off = (sn + 1.0) * K.vibDepth;
+				const double  off = (sn[l] + 1.0) * K.vibDepth;
 				const int     d   = RVL_DLY[l];
-				const double* rg  = sm.ring + RVL_OFS[l];
+				const double* rg  = sm.ring + RVL_LOFS[l];
 				const int     cn  = wrap_slot (rl (cw, l) + n + 1, d);
-				const int     wk  = (int)(cn + off);
+				const int     wk  = (int)(cn + off); /* <= d + 5: the mirror covers wk + 1 */
 				const double  fr  = off - floor (off);
-				const double  r0 = rg[wrap_slot (wk, d)], r1 = rg[wrap_slot (wk + 1, d)];
+				const double  r0 = rg[wk], r1 = rg[wk + 1];
 				double        x  = (r0 * (1 - fr));
 				x += (r1 * fr);
 				I[l] = (oneMB * x) + (r0 * K.blend);
@@ -1073,7 +1116,7 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 #pragma unroll
 			for (int l = 8; l < 12; l++) {
 				const int    d   = RVL_DLY[l];
-				const double old = sm.ring[RVL_OFS[l] + wrap_slot (rl (cw, l) + n + 1, d)];
+				const double old = sm.ring[RVL_LOFS[l] + rl (cw, l) + n + 1]; /* <= d + 64: mirror */
 				double       a   = a0;
 				a -= old * 0.5;
 				apw[l - 8] = a;
@@ -1100,13 +1143,13 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 				cprv[l] = cp[l];
 #pragma unroll
 			for (int l = 8; l < 12; l++)
-				sm.ring[RVL_OFS[l] + wrap_slot (rl (cw, l) + n, RVL_DLY[l])] = apw[l - 8];
+				rvl_write (sm.ring + RVL_LOFS[l], wrap_slot (rl (cw, l) + n, RVL_DLY[l]), RVL_DLY[l], apw[l - 8]);
 			const int srcAp[8] = {3, 2, 1, 0, 0, 1, 2, 3};
 #pragma unroll
 			for (int l = 0; l < 8; l++) {
 				const double up   = lane_shr1 (fb[l]);
 				const double prev = n == 0 ? cprv[l] : up;
-				sm.ring[RVL_OFS[l] + wrap_slot (rl (cw, l) + n, RVL_DLY[l])] = ap[srcAp[l]] + prev;
+				rvl_write (sm.ring + RVL_LOFS[l], wrap_slot (rl (cw, l) + n, RVL_DLY[l]), RVL_DLY[l], ap[srcAp[l]] + prev);
 			}
 			/* the tap mix, stored at the start of the next group (see above) */
 			pmix = mix;
@@ -1128,8 +1171,10 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 			sm.st.fb[n] = sm.carry[(nGrp - 1) & 1][(nSub - 1) % RVL_G][n];
 	}
 	__syncthreads ();
-	for (uint32_t i = tid; i < rlen2; i += RVL_THREADS)
-		((double2*)slab)[i] = ((const double2*)sm.ring)[i];
+#pragma unroll
+	for (int l = 0; l < 12; l++) /* the canonical slots */
+		for (int i = tid; i <= RVL_DLY[l]; i += RVL_THREADS)
+			slab[RVL_OFS[l] + i] = sm.ring[RVL_LOFS[l] + i];
 	if (w == 0)
 		copy_words (S, &sm.st);
 }
@@ -1572,98 +1617,110 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 /* ================================================================== k_whirl */
 __device__ void whirl_speed (tbf_wh_state& st, const tbf_inst_const& K, int revOpt, int& brake)
 {
+	/* the rotor state in registers: its LDS reads issued together, not one per branch */
+	double hornAngle = st.hornAngle, drumAngle = st.drumAngle, hornIncr = st.hornIncr, drumIncr = st.drumIncr;
+	double hornTarget = st.hornTarget, drumTarget = st.drumTarget;
+	int    hornAcDc = st.hornAcDc, drumAcDc = st.drumAcDc;
 	/* useRevOption (src/whirl.cpp:174-196) for an event landing before this block */
 	if (revOpt >= 0) {
 		const int i   = revOpt % 9;
-		st.hornTarget = K.revHorn[i];
-		st.drumTarget = K.revDrum[i];
-		if (st.hornIncr < st.hornTarget)
-			st.hornAcDc = 1;
-		else if (st.hornTarget < st.hornIncr)
-			st.hornAcDc = -1;
-		if (st.drumIncr < st.drumTarget)
-			st.drumAcDc = 1;
-		else if (st.drumTarget < st.drumIncr)
-			st.drumAcDc = -1;
+		hornTarget = K.revHorn[i];
+		drumTarget = K.revDrum[i];
+		if (hornIncr < hornTarget)
+			hornAcDc = 1;
+		else if (hornTarget < hornIncr)
+			hornAcDc = -1;
+		if (drumIncr < drumTarget)
+			drumAcDc = 1;
+		else if (drumTarget < drumIncr)
+			drumAcDc = -1;
 	}
 	/* src/whirl.cpp:1219-1374 */
-	if (st.hornAcDc) {
+	if (hornAcDc) {
 		int flywheel = 0;
-		if (K.hnBrakePos > 0 && st.hornTarget == 0 && st.hornIncr > 0 && st.hornIncr < K.hnHardstop) {
+		if (K.hnBrakePos > 0 && hornTarget == 0 && hornIncr > 0 && hornIncr < K.hnHardstop) {
 			const double targetPos = fmod (1.25 - K.hnBrakePos, 1.0);
-			if (fabs (st.hornAngle - targetPos) < (2.0 / 16384)) {
-				st.hornAngle = targetPos;
-				st.hornIncr  = 0;
+			if (fabs (hornAngle - targetPos) < (2.0 / 16384)) {
+				hornAngle = targetPos;
+				hornIncr  = 0;
 			} else {
-				const float diffinc = (float)(fmod (1. + targetPos - st.hornAngle, 1.0) / (float)TBF_BLK);
-				if (st.hornIncr > diffinc)
-					st.hornIncr = diffinc;
-				else if (st.hornIncr < K.minspeed)
-					st.hornIncr = K.minspeed;
+				const float diffinc = (float)(fmod (1. + targetPos - hornAngle, 1.0) / (float)TBF_BLK);
+				if (hornIncr > diffinc)
+					hornIncr = diffinc;
+				else if (hornIncr < K.minspeed)
+					hornIncr = K.minspeed;
 				flywheel = 1;
 			}
 		}
 		if (!flywheel) {
-			const double l = st.hornAcDc > 0 ? K.lAcc[0] : K.lAcc[1];
-			st.hornIncr += (1 - l) * (st.hornTarget - st.hornIncr);
+			const double l = hornAcDc > 0 ? K.lAcc[0] : K.lAcc[1];
+			hornIncr += (1 - l) * (hornTarget - hornIncr);
 		}
-		if (fabs (st.hornTarget - st.hornIncr) < K.deadzone) {
-			st.hornAcDc = 0;
-			st.hornIncr = st.hornTarget;
+		if (fabs (hornTarget - hornIncr) < K.deadzone) {
+			hornAcDc = 0;
+			hornIncr = hornTarget;
 		}
 	}
-	if (st.drumAcDc) {
+	if (drumAcDc) {
 		int flywheel = 0;
-		if (K.drBrakePos > 0 && st.drumTarget == 0 && st.drumIncr > 0 && st.drumIncr < K.drHardstop) {
+		if (K.drBrakePos > 0 && drumTarget == 0 && drumIncr > 0 && drumIncr < K.drHardstop) {
 			const double targetPos = fmod (K.drBrakePos + .75, 1.0);
-			if (fabs (st.drumAngle - targetPos) < (2.0 / 16384)) {
-				st.drumAngle = targetPos;
-				st.drumIncr  = 0;
+			if (fabs (drumAngle - targetPos) < (2.0 / 16384)) {
+				drumAngle = targetPos;
+				drumIncr  = 0;
 			} else {
-				const float diffinc = (float)(fmod (1. + targetPos - st.drumAngle, 1.0) / (float)TBF_BLK);
-				if (st.drumIncr > diffinc)
-					st.drumIncr = diffinc;
-				else if (st.drumIncr < K.minspeed)
-					st.drumIncr = K.minspeed;
+				const float diffinc = (float)(fmod (1. + targetPos - drumAngle, 1.0) / (float)TBF_BLK);
+				if (drumIncr > diffinc)
+					drumIncr = diffinc;
+				else if (drumIncr < K.minspeed)
+					drumIncr = K.minspeed;
 				flywheel = 1;
 			}
 		}
 		if (!flywheel) {
-			const double l = st.drumAcDc > 0 ? K.lAcc[2] : K.lAcc[3];
-			st.drumIncr += (1 - l) * (st.drumTarget - st.drumIncr);
+			const double l = drumAcDc > 0 ? K.lAcc[2] : K.lAcc[3];
+			drumIncr += (1 - l) * (drumTarget - drumIncr);
 		}
-		if (fabs (st.drumTarget - st.drumIncr) < K.deadzone) {
-			st.drumAcDc = 0;
-			st.drumIncr = st.drumTarget;
+		if (fabs (drumTarget - drumIncr) < K.deadzone) {
+			drumAcDc = 0;
+			drumIncr = drumTarget;
 		}
 	}
 	brake = 0;
 	if (K.hnBrakePos > 0) {
 		const double targetPos = fmod (1.25 - K.hnBrakePos, 1.0);
-		if (!st.hornAcDc && st.hornIncr == 0 && st.hornAngle != targetPos) {
+		if (!hornAcDc && hornIncr == 0 && hornAngle != targetPos) {
 			brake |= 1;
-			if (fabs (st.hornAngle - targetPos) < (2.0 / 16384)) {
-				st.hornAngle = targetPos;
+			if (fabs (hornAngle - targetPos) < (2.0 / 16384)) {
+				hornAngle = targetPos;
 			} else {
-				st.hornIncr = fmod (1. + targetPos - st.hornAngle, 1.0) / (float)TBF_BLK;
-				if (st.hornIncr > K.hnLimit)
-					st.hornIncr = K.hnLimit;
+				hornIncr = fmod (1. + targetPos - hornAngle, 1.0) / (float)TBF_BLK;
+				if (hornIncr > K.hnLimit)
+					hornIncr = K.hnLimit;
 			}
 		}
 	}
 	if (K.drBrakePos > 0) {
 		const double targetPos = fmod (K.drBrakePos + .75, 1.0);
-		if (!st.drumAcDc && st.drumIncr == 0 && st.drumAngle != targetPos) {
+		if (!drumAcDc && drumIncr == 0 && drumAngle != targetPos) {
 			brake |= 2;
-			if (fabs (st.drumAngle - targetPos) < (2.0 / 16384)) {
-				st.drumAngle = targetPos;
+			if (fabs (drumAngle - targetPos) < (2.0 / 16384)) {
+				drumAngle = targetPos;
 			} else {
-				st.drumIncr = fmod (1. + targetPos - st.drumAngle, 1.0) / (float)TBF_BLK;
-				if (st.drumIncr > K.drLimit)
-					st.drumIncr = K.drLimit;
+				drumIncr = fmod (1. + targetPos - drumAngle, 1.0) / (float)TBF_BLK;
+				if (drumIncr > K.drLimit)
+					drumIncr = K.drLimit;
 			}
 		}
 	}
+	st.hornAngle  = hornAngle;
+	st.drumAngle  = drumAngle;
+	st.hornIncr   = hornIncr;
+	st.drumIncr   = drumIncr;
+	st.hornTarget = hornTarget;
+	st.drumTarget = drumTarget;
+	st.hornAcDc   = hornAcDc;
+	st.drumAcDc   = drumAcDc;
 }
 
 /* One motion's ordered adds into a ring for a 64-sample sub-block (HN_MOTION /
@@ -1797,7 +1854,7 @@ __device__ __forceinline__ void wh_serial (const float* ip, float* tp, float* fz
 
 /* whirlProc2 (src/whirl.cpp:1191-1638) + whirlProc3 mic mix (1653-1681) */
 template <int W>
-__device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ctl& G, const tbf_inst_const& K,
+__device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypass, const int revOpt, const tbf_inst_const& K,
                              const float in0, const float in1, const float nin0, const bool hasNext,
                              float* __restrict__ oL, float* __restrict__ oR)
 {
@@ -1810,7 +1867,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 	const float*  bfw   = P.whBw;
 	const float*  bbw   = P.whBw + 16384 * 5;
 
-	if (G.whBypass) {
+	if (bypass) {
 		/* whirlProc2 bypass (src/whirl.cpp:1197-1215) + whirlProc3 mix */
 		for (int k = 0; k < 2; k++) {
 			const int   n = lane + k * NL;
@@ -1823,10 +1880,10 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 	if (lane == 0) {
 		int brake;
 		/* a control entry carrying a rotary selection is used for exactly one block */
-		whirl_speed (st, K, G.whRevOption, brake);
+		whirl_speed (st, K, revOpt, brake);
 		sm.brake = brake;
 	}
-	__syncthreads ();
+	wave_sync ();
 	const double   hornIncr = st.hornIncr, drumIncr = st.drumIncr;
 	const uint32_t WM       = (uint32_t)W - 1u;
 	/* serial filter coefficients: lane 0 horn A, lane 1 horn B, lanes 2-3 drum shelf */
@@ -1857,7 +1914,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 			sm.x1[i] = st.adx[1][(st.adi[1] + 3 - i) & 7];
 			sm.x2[i] = st.adx[2][(st.adi[2] + 3 - i) & 7];
 		}
-		__syncthreads ();
+		wave_sync ();
 		/* DF2 biquads (EQ_IIR, src/whirl.cpp:1479-1485): only the state recurrence
 		 * temp[n] = (x - a1 temp[n-1]) - a2 temp[n-2] is serial; the output
 		 * y[n] = (b0 temp[n] + b1 temp[n-1]) + b2 temp[n-2] is the same expression
@@ -1869,21 +1926,21 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 		const bool aNext = sb + 1 < TBF_BLK / TBF_SUB || hasNext;
 		if (aNext)
 			sm.xn[n] = (float)((double)(sb + 1 < TBF_BLK / TBF_SUB ? in1 : nin0) + 1e-14);
-		__syncthreads ();
+		wave_sync ();
 		if (!sm.aReady) {
 			if (lane == 0)
 				wh_serial (sm.xx + 1, sm.tmp[0], st.fz[0], K.hafw[0], K.hafw[1], false);
-			__syncthreads ();
+			wave_sync ();
 			const float* T0 = sm.tmp[0];
 			sm.aOut[n]      = (T0[n + 2] * K.hafw[2]) + (K.hafw[3] * T0[n + 1]) + (K.hafw[4] * T0[n]);
-			__syncthreads ();
+			wave_sync ();
 		}
 		if (lane < 4 && (lane > 0 || aNext)) {
 			const float* ip = lane == 0 ? sm.xn : (lane == 1 ? sm.aOut : sm.rd[lane - 2]);
 			/* crossing into the next block: A's state gets that block's NaN scrub first */
 			wh_serial (ip, sm.tmp[lane], st.fz[lane], fa0, fa1, lane == 0 && sb + 1 == TBF_BLK / TBF_SUB);
 		}
-		__syncthreads ();
+		wave_sync ();
 		{
 			/* filter outputs: horn B -> xf, drum shelves in place, horn A of the next
 			 * sub-block -> aOut */
@@ -1913,7 +1970,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 			const bool   frc = (P.dbg & TBF_DEBUG_FORCE_SERIAL) != 0;
 			const bool   okh = phase_run (h0, hornIncr, TBF_SUB, Dh) && !frc;
 			const bool   okd = phase_run (d0, drumIncr, TBF_SUB, Dd) && !frc;
-			__syncthreads (); /* every lane has read the filter scratch and the start angles */
+			wave_sync (); /* every lane has read the filter scratch and the start angles */
 			if (lane == 0 && !(okh && okd))
 				atomicOr (P.errFlags, (uint32_t)TBF_PATH_WH_ANGLE);
 			if ((lane == 1 && !okh) || (lane == 2 && !okd)) {
@@ -1932,7 +1989,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 						row[i0 + k] = av[k];
 				}
 			}
-			__syncthreads ();
+			wave_sync ();
 			ha = okh ? h0 + (double)n * Dh : angBuf[n];
 			da = okd ? d0 + (double)n * Dd : angBuf[TBF_SUB + n];
 			if (lane == 1)
@@ -1940,7 +1997,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 			if (lane == 2)
 				st.drumAngle = okd ? d0 + (double)TBF_SUB * Dd : wrap1 (angBuf[2 * TBF_SUB - 1] + drumIncr);
 		}
-		__syncthreads ();
+		wave_sync ();
 		/* reflection filters FILTER_C (src/whirl.cpp:1472-1477), lane-parallel */
 		const float xf   = sm.xf[n + 4];
 		const float xfp  = n == 0 ? st.z[0] : sm.xf[n + 3];
@@ -1951,12 +2008,12 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 		sm.xd1[n + 1]    = xd1v;
 		if (lane == 0)
 			sm.xd1[0] = st.z[3];
-		__syncthreads ();
+		wave_sync ();
 		const float x1p  = n == 0 ? st.z[1] : sm.x1[n + 3];
 		const float x2v  = (float)((0.4 * x1v) + (0.4 * x1p));
 		sm.x2[n + 4]     = x2v;
 		const float xd2v = (float)((0.4 * xd1v) + (0.4 * sm.xd1[n]));
-		__syncthreads ();
+		wave_sync ();
 
 		/* ---- rings (HL, HR, DL, DR) in groups of 4: the group's motions first (their
 		 * table loads in flight together), then each ring's ordered adds ---- */
@@ -2047,7 +2104,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 						else
 							motion_add<W> (sm.wring[r0 + gi], mu[gi][q], ma[gi][q], mb[gi][q], lane);
 					}
-					__syncthreads ();
+					wave_sync ();
 				}
 			} else {
 #pragma unroll
@@ -2055,11 +2112,11 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 					float* ring = sm.wring[r0 + gi];
 					if (okr[gi]) {
 						motion_add<W> (ring, mu[gi][2], ma[gi][2], mb[gi][2], lane);
-						__syncthreads ();
+						wave_sync ();
 						motion_add<W> (ring, mu[gi][1], ma[gi][1], mb[gi][1], lane);
-						__syncthreads ();
+						wave_sync ();
 						motion_add<W> (ring, mu[gi][0], ma[gi][0], mb[gi][0], lane);
-						__syncthreads ();
+						wave_sync ();
 					} else {
 						/* serial replay in the reference order: sample-major, motions in source order */
 						if (lane == 0)
@@ -2076,7 +2133,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 								}
 							}
 						}
-						__syncthreads ();
+						wave_sync ();
 					}
 				}
 			}
@@ -2098,30 +2155,32 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const tbf_seg_ct
 			st.z[2] = xin;
 			st.z[3] = xd1v;
 		}
-		__syncthreads ();
-		if (lane == 0) {
-			for (int j = 0; j < 8; j++) {
-				st.adx[0][(st.adi[0] + j) & 7] = sm.xf[4 + TBF_SUB - 1 - j];
-				st.adx[1][(st.adi[1] + j) & 7] = sm.x1[4 + TBF_SUB - 1 - j];
-				st.adx[2][(st.adi[2] + j) & 7] = sm.x2[4 + TBF_SUB - 1 - j];
-			}
-			st.outpos = (st.outpos + TBF_SUB) & 2047u;
+		wave_sync ();
+		if (lane < 24) { /* history k = lane / 8, entry j = lane % 8, one lane each */
+			const int    k = lane >> 3, j = lane & 7;
+			const float* h = k == 0 ? sm.xf : (k == 1 ? sm.x1 : sm.x2);
+			st.adx[k][(st.adi[k] + j) & 7] = h[4 + TBF_SUB - 1 - j];
 		}
-		__syncthreads ();
+		if (lane == 0)
+			st.outpos = (st.outpos + TBF_SUB) & 2047u;
+		wave_sync ();
+	}
+	/* NaN scrub (src/whirl.cpp:1622-1630), a lane per value: lanes 0..7 the filter states
+	 * fz (horn A's only when it did not run ahead: then it got its scrub when it crossed
+	 * into the next block), lanes 8..11 z */
+	if (lane < 8) {
+		const int f = lane >> 1, j = lane & 1;
+		if ((f > 0 || !sm.aReady) && isnan (st.fz[f][j]))
+			st.fz[f][j] = 0.f;
+	} else if (lane < 12) {
+		if (isnan (st.z[lane - 8]))
+			st.z[lane - 8] = 0.f;
 	}
 	if (lane == 0) {
-		/* NaN scrub, src/whirl.cpp:1622-1630 */
-		for (int f = sm.aReady ? 1 : 0; f < 4; f++)
-			for (int j = 0; j < 2; j++)
-				if (isnan (st.fz[f][j]))
-					st.fz[f][j] = 0.f;
-		for (int j = 0; j < 4; j++)
-			if (isnan (st.z[j]))
-				st.z[j] = 0.f;
 		if (sm.brake & 1) st.hornIncr = 0;
 		if (sm.brake & 2) st.drumIncr = 0;
 	}
-	__syncthreads ();
+	wave_sync ();
 }
 
 template <int W>
@@ -2140,11 +2199,19 @@ k_whirl (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 		sm.aReady = 0;
 	for (uint32_t i = threadIdx.x; i < 4u * W; i += NL)
 		(&sm.wring[0][0])[i] = wr[i];
-	__syncthreads ();
+	wave_sync ();
 	/* the input (lane n: samples n and n + 64 of a block) is loaded one block ahead, so
 	 * its latency overlaps a whole block instead of stalling a sub-block start */
 	const float* inBase = P.mid2 + (size_t)inst * P.midStride;
-	float        c0 = 0.f, c1 = 0.f;
+	/* the launch's per-block control (bypass, rotary selection), lane b = block b (<= 64
+	 * blocks): read once, so no block waits on the two dependent control loads */
+	int byv = 0, rvv = -1;
+	if (threadIdx.x < P.nBlocks) {
+		const tbf_seg_ctl& Gb = ctl_of (P, ctl, threadIdx.x, inst);
+		byv                   = Gb.whBypass != 0;
+		rvv                   = Gb.whRevOption;
+	}
+	float c0 = 0.f, c1 = 0.f;
 	if (P.nBlocks > 0) {
 		c0 = inBase[threadIdx.x];
 		c1 = inBase[threadIdx.x + NL];
@@ -2159,12 +2226,12 @@ k_whirl (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 			n1 = inBase[(size_t)(blk + 1) * TBF_BLK + threadIdx.x + NL];
 		}
 		/* horn filter A may run ahead into the next block unless that one is bypassed */
-		const bool hasNext = more && !ctl_of (P, ctl, blk + 1, inst).whBypass;
-		stage_whirl<W> (P, sm, ctl_of (P, ctl, blk, inst), K, c0, c1, n0, hasNext, oL, oR);
+		const bool hasNext = more && !rl (byv, (int)min (blk + 1, (uint32_t)NL - 1));
+		stage_whirl<W> (P, sm, rl (byv, (int)blk) != 0, rl (rvv, (int)blk), K, c0, c1, n0, hasNext, oL, oR);
 		c0 = n0;
 		c1 = n1;
 	}
-	__syncthreads ();
+	wave_sync ();
 	copy_words (S, &sm.st);
 	for (uint32_t i = threadIdx.x; i < 4u * W; i += NL)
 		wr[i] = (&sm.wring[0][0])[i];
@@ -2179,7 +2246,7 @@ extern "C" int tbf_launch_stage (const tbf_launch* P, int k, hipStream_t stream)
 		return 0;
 	if (P->chain != TBF_CHAIN_TONEGEN && (uint64_t)P->nBlocks * TBF_BLK > P->midStride)
 		return -22;
-	if ((k == 1 || k == 3) && P->nBlocks > NL) /* a launch's per-block wet levels sit one per lane */
+	if ((k == 1 || k == 3 || k == 4) && P->nBlocks > NL) /* a launch's per-block controls sit one per lane */
 		return -22;
 	const dim3 grid (P->nInst), block (NL);
 	const dim3 cgrid ((P->nInst + RVC_CB - 1) / RVC_CB), cblock (RVC_THREADS);
@@ -2213,7 +2280,9 @@ extern "C" int tbf_launch_stage (const tbf_launch* P, int k, hipStream_t stream)
  * rings fit its LDS ring and every delay leaves a group's reads clear of its writes */
 extern "C" int tbf_rv_lds_fits (const tbf_inst_const* k)
 {
-	if (k->ringOff[12] - k->ringOff[0] > RVL_RING || k->ringOff[25] - k->ringOff[13] > RVL_RING)
+	/* tap offsets (sin + 1) * vibDepth < 7: the taps stay inside the staged window (72
+	 * slots past count, for the group argument below) and the LDS mirror */
+	if (!(k->vibDepth >= 0.0 && 2.0 * k->vibDepth < 7.0))
 		return 0;
 	for (int l = 0; l < 12; l++) {
 		/* a group's reads must find only data written before the group: tap lines read up

@@ -130,6 +130,16 @@ __device__ __forceinline__ uint32_t xs_jump_n (const uint32_t* __restrict__ J, u
 	return ((v[0] ^ v[1]) ^ (v[2] ^ v[3])) ^ ((v[4] ^ v[5]) ^ (v[6] ^ v[7]));
 }
 
+/* lane l's value, wave-uniform (l uniform) */
+__device__ __forceinline__ int rl (int v, int l) { return __builtin_amdgcn_readlane (v, l); }
+
+__device__ __forceinline__ double rld (double v, int l)
+{
+	const unsigned long long u = __double_as_longlong (v);
+	const unsigned lo = __builtin_amdgcn_readlane ((unsigned)u, l), hi = __builtin_amdgcn_readlane ((unsigned)(u >> 32), l);
+	return __longlong_as_double ((long long)(((unsigned long long)hi << 32) | lo));
+}
+
 __device__ __forceinline__ int wave_min (int v)
 {
 	for (int o = 32; o > 0; o >>= 1)
@@ -586,14 +596,6 @@ struct RvFetch {
 	double a0;       /* network input (k_rv_pre output) */
 };
 
-__device__ __forceinline__ int rl (int v, int l) { return __builtin_amdgcn_readlane (v, l); }
-
-__device__ __forceinline__ double rld (double v, int l)
-{
-	const unsigned long long u = __double_as_longlong (v);
-	const unsigned lo = __builtin_amdgcn_readlane ((unsigned)u, l), hi = __builtin_amdgcn_readlane ((unsigned)(u >> 32), l);
-	return __longlong_as_double ((long long)(((unsigned long long)hi << 32) | lo));
-}
 
 __device__ __forceinline__ int wrap_slot (int s, int d) { return s - ((s > d) ? d + 1 : 0); }
 
@@ -1115,7 +1117,6 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 			mix = (I[0] + I[1] + I[2] + I[3] + I[4] + I[5] + I[6] + I[7]) / 8.0;
 #pragma unroll
 			for (int l = 8; l < 12; l++) {
-				const int    d   = RVL_DLY[l];
 				const double old = sm.ring[RVL_LOFS[l] + rl (cw, l) + n + 1]; /* <= d + 64: mirror */
 				double       a   = a0;
 				a -= old * 0.5;

@@ -595,6 +595,61 @@ def test_gpu_cli_host_synth_sound(oracle, tmp_path):
     assert worst <= TOL
 
 
+def _random_mts(seed):
+    """A seeded random MTS-ESP table: 12-TET moved by a random transposition (-700 ..
+    +700 cents) and per-key offsets (-50 .. +50 cents), so the wheels' sine arguments
+    cover ranges the fixed tunings do not."""
+    r = np.random.default_rng(seed)
+    cents = r.uniform(-700, 700) + r.uniform(-50, 50, 128)
+    return 440.0 * 2.0 ** ((np.arange(128) - 69) / 12.0 + cents / 1200.0)
+
+
+def _oracle_bank_worker(args):
+    sr, seeds = args
+    import hashlib
+    from orc_bind import Template, load_oracle
+    lib = load_oracle()
+    out = []
+    for sd in seeds:
+        b, l = Template(lib, sr=sr, mts128=_random_mts(sd), seed=sd).bank()
+        out.append((sd, b.astype(np.float32).tobytes(), np.asarray(l).tobytes()))
+    return out
+
+
+@pytest.mark.parametrize("sr", [48000.0, 96000.0])
+def test_gpu_device_banks_random_mts_no_flips(oracle, sr):
+    """the device wave banks (k_tpl_wave: FP64 sin of the device library,
+    rounded to float) against the oracle's (glibc sin) for 200 seeded random MTS tables
+    per sample rate: the number of float samples that differ (a 1-ulp FP64 sin
+    difference flipping a float rounding) must be 0."""
+    import multiprocessing as mp
+    import os
+    import tunebfree_amd as T
+    seeds = [7000 + int(sr) // 1000 * 1000 + k for k in range(200)]
+    workers = max(1, min(16, (os.cpu_count() or 1)))
+    parts = [seeds[k::workers] for k in range(workers)]
+    with mp.get_context("spawn").Pool(workers) as pool:
+        ref = {sd: (b, l) for part in pool.map(_oracle_bank_worker, [(sr, p) for p in parts]) for sd, b, l in part}
+    eng = T.Engine(sample_rate=sr, device=0)
+    ids = eng.templates(seeds, mts128=np.stack([_random_mts(sd) for sd in seeds]))
+    flips, samples, worst = 0, 0, 0.0
+    for tid, sd in zip(ids, seeds):
+        bank, lens = eng.template_bank(tid)
+        ob = np.frombuffer(ref[sd][0], np.float32)
+        ol = np.frombuffer(ref[sd][1], np.asarray(lens).dtype)
+        assert np.array_equal(np.asarray(lens), ol), sd
+        assert bank.shape == ob.shape, sd
+        d = bank.view(np.uint32) != ob.view(np.uint32)
+        flips += int(d.sum())
+        samples += bank.size
+        if d.any():
+            worst = max(worst, float(np.abs(bank[d].astype(np.float64) - ob[d]).max()))
+    eng.close()
+    print(f"device banks, {len(seeds)} random MTS tables at {sr:.0f} Hz: {samples} samples, "
+          f"{flips} differ from the oracle (max |diff| {worst:.3g})")
+    assert flips == 0
+
+
 @pytest.mark.parametrize("sr", [48000.0, 96000.0])
 def test_gpu_device_templates_match_oracle_and_reference(oracle, sr):
     """§8(f) row 2: templates built on the device (tbf_templates_create: per-chunk
@@ -807,6 +862,30 @@ def test_gpu_parameter_sweep(oracle, debug_flags):
     if debug_flags:
         want = T.engine.PATH_VIB_SERIAL | T.engine.PATH_WH_ANGLE | T.engine.PATH_WH_MOTION | T.engine.PATH_RV_PHASE
         assert flags & want == want, hex(flags)
+
+
+def test_gpu_random_character_and_reverb_mix(oracle):
+    """seeded random overdrive character (0..1) and reverb mix (0..1)
+    per instance, changed mid-render, against the oracle: the overdrive's FP64 sin
+    passes and the reverb's sin / asin on the device library across continuous parameter
+    values, not only the fixed sweep points."""
+    rng = np.random.default_rng(2024)
+    n, nb = 16, 48
+    ch = rng.uniform(0.0, 1.0, size=(n, 2))
+    rv = rng.uniform(0.0, 1.0, size=(n, 2))
+
+    def scen(i):
+        ev = [(0, k, a, b) for (k, a, b) in S.jazz1_params(character=float(ch[i, 0]), reverb=float(rv[i, 0]))]
+        ev += [(0, "note", k, 1) for k in S.chord_for(i)]
+        ev += [(24, "param", S.P_CHARACTER, float(ch[i, 1])), (24, "param", S.P_REVERB, float(rv[i, 1]))]
+        return ev
+    eng, tpl, seeds, scens = _setup(oracle, n, scen)
+    L, R = engine_run(eng, scens, nb)
+    oL, oR, *_ = oracle_run(oracle, tpl, seeds, scens, nb)
+    eL, xL = compare(L, oL)
+    eR, xR = compare(R, oR)
+    print(f"random character / reverb: max|err| L={eL:.3g} R={eR:.3g} bit-exact L={xL:.6f} R={xR:.6f}")
+    assert max(eL, eR) <= TOL and min(xL, xR) == 1.0
 
 
 def _ring_window(max_ahead):

@@ -178,9 +178,11 @@ int tbf_synth_sound (tbf_engine* e, uint32_t nframes, float* outL, float* outR, 
  * function name of src/midi.cpp:100-170 that reaches the DSP chain: upper|lower|pedal.
  * drawbar16/513/8/4/223/2/135/113/1, percussion.enable|volume|decay|harmonic,
  * vibrato.knob|routing|upper|lower, swellpedal1|2, overdrive.enable|character,
- * reverb.mix, rotary.speed-preset|speed-select|speed-toggle.  value 0..127 (clamped).
- * Returns 0 when applied, 1 for any other name (ignored, as the reference ignores
- * names without a registered function). */
+ * reverb.mix, rotary.speed-preset|speed-select|speed-toggle, and the whirl's
+ * whirl.horn.filter.a|b.type|hz|q|gain, whirl.horn|drum.brakepos,
+ * whirl.horn|drum.acceleration|deceleration (src/whirl.cpp:699-889, registered 966-981;
+ * from the next block).  value 0..127 (clamped).  Returns 0 when applied, 1 for any
+ * other name (ignored, as the reference ignores names without a registered function). */
 int tbf_midi_control (tbf_engine* e, uint32_t inst, const char* fn, int32_t value);
 /* programme definitions in the .pgm syntax (src/pgmParser.cpp:65-73, properties of
  * bindToProgram src/program.cpp:133-603) into the engine's programme table; returns the
@@ -257,7 +259,8 @@ int tbf_debug_step (tbf_engine* e, uint32_t inst, float* entries9, uint32_t cap)
 int tbf_debug_render_program (tbf_engine* e, uint32_t inst, float* entries9, uint32_t cap);
 /* an instance's host control state: odClean, odA, odC, rvG, revOpt, revSelect, whBypass,
  * newRouting, swellPedalGain, percEnabled, percIsSoft, percIsFast, percSendBus, vibTable,
- * vibMixed, percDrawbarGain, drawBarGain[27]; returns the count (43) */
+ * vibMixed, percDrawbarGain, drawBarGain[27], the whirl's haT haF haQ haG hbT hbF hbQ hbG
+ * hornAcc hornDec drumAcc drumDec hnBrakePos drBrakePos; returns the count (57) */
 int tbf_debug_control (tbf_engine* e, uint32_t inst, double* out, uint32_t cap);
 /* the kernel's exact shortcuts of serial recurrences, evaluated on the host (same source,
  * csrc/tbf_exact.h): op 0 phase_run (in: v0, d, m -> out: ok, D), op 1 cnt_adv (in: c0,

@@ -181,6 +181,10 @@ void      orc_param_defaults (double* params64);
 void      orc_note (orc_inst* p, int key, int on);                 /* oscKeyOn/Off */
 void      orc_set_param (orc_inst* p, int pid, double value);      /* CLAP setParam */
 void      orc_set_chain (orc_inst* p, int mode);                   /* 0 full, 1 tonegen only */
+/* a MIDI control function by name, value 0..127: the whirl's runtime parameters
+ * (whirl.horn.filter.{a,b}.{type,hz,q,gain}, whirl.{horn,drum}.brakepos,
+ * whirl.{horn,drum}.{acceleration,deceleration}); -1 for any other name */
+int       orc_control (orc_inst* p, const char* name, int value);
 /* render nblocks of the synthSound quartet; any output pointer may be NULL.
  * sA/sB/sC receive the tonegen, preamp and reverb stage outputs. */
 void orc_render (orc_inst* p, int nblocks, float* L, float* R, float* sA, float* sB, float* sC);

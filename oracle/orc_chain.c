@@ -95,6 +95,13 @@ void orc_note (orc_inst* p, int key, int on)
 
 void orc_set_chain (orc_inst* p, int mode) { p->chain = mode; }
 
+/* callMIDIControlFunction (src/midi.cpp) for the whirl's registered functions */
+int orc_control (orc_inst* p, const char* name, int value)
+{
+	const unsigned char uc = (unsigned char)(value < 0 ? 0 : (value > 127 ? 127 : value));
+	return orc_whirl_control (p->wh, name, uc);
+}
+
 /* src/clap.cpp:108-121 setToneGenParam and 162-207 setParam */
 void orc_set_param (orc_inst* p, int index, double v)
 {

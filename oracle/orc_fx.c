@@ -459,6 +459,51 @@ static void setIIRFilter (float W[], int T, const double F, const double Q, cons
 	W[fb2] = (float)C[2];
 }
 
+/* the MIDI control functions initWhirl registers (src/whirl.cpp:966-981), setters 699-889:
+ * the value mapped into the field's range in double, stored in the (float or double)
+ * field, then UPDATE_A_FILTER / UPDATE_B_FILTER (679-689) for the horn filters.  The speed
+ * ramps read hornAcc .. drumDec at every block (whirlProc2, 1255-1257).  Returns 0, or -1
+ * for a name that is not one of them. */
+int orc_whirl_control (struct orc_whirl* w, const char* fn, unsigned char uc)
+{
+	const double u = (double)uc;
+	if (!strcmp (fn, "whirl.horn.filter.a.type"))
+		w->haT = (int)(uc / 15);
+	else if (!strcmp (fn, "whirl.horn.filter.a.hz"))
+		w->haF = 250.0 + ((8000.0 - 250.0) * ((u * u) / 16129.0));
+	else if (!strcmp (fn, "whirl.horn.filter.a.q"))
+		w->haQ = 0.01 + ((6.00 - 0.01) * (u / 127.0));
+	else if (!strcmp (fn, "whirl.horn.filter.a.gain"))
+		w->haG = -48.0 + ((48.0 - -48.0) * (u / 127.0));
+	else if (!strcmp (fn, "whirl.horn.filter.b.type"))
+		w->hbT = (int)(uc / 15);
+	else if (!strcmp (fn, "whirl.horn.filter.b.hz"))
+		w->hbF = 250.0 + ((8000.0 - 250.0) * ((u * u) / 16129.0));
+	else if (!strcmp (fn, "whirl.horn.filter.b.q"))
+		w->hbQ = 0.01 + ((6.00 - 0.01) * (u / 127.0));
+	else if (!strcmp (fn, "whirl.horn.filter.b.gain"))
+		w->hbG = -48.0 + ((48.0 - -48.0) * (u / 127.0));
+	else if (!strcmp (fn, "whirl.horn.brakepos"))
+		w->hnBrakePos = u / 127.0;
+	else if (!strcmp (fn, "whirl.drum.brakepos"))
+		w->drBrakePos = u / 127.0;
+	else if (!strcmp (fn, "whirl.horn.acceleration"))
+		w->hornAcc = .01 + u / 80.0;
+	else if (!strcmp (fn, "whirl.horn.deceleration"))
+		w->hornDec = .01 + u / 80.0;
+	else if (!strcmp (fn, "whirl.drum.acceleration"))
+		w->drumAcc = .01 + u / 14.0;
+	else if (!strcmp (fn, "whirl.drum.deceleration"))
+		w->drumDec = .01 + u / 14.0;
+	else
+		return -1;
+	if (!strncmp (fn, "whirl.horn.filter.a.", 20))
+		setIIRFilter (w->hafw, (int)w->haT, w->haF, w->haQ, w->haG, w->SampleRateD);
+	else if (!strncmp (fn, "whirl.horn.filter.b.", 20))
+		setIIRFilter (w->hbfw, (int)w->hbT, w->hbF, w->hbQ, w->hbG, w->SampleRateD);
+	return 0;
+}
+
 /* src/whirl.cpp:174-224 useRevOption */
 void orc_whirl_use_rev_option (struct orc_whirl* w, int n, int signals)
 {

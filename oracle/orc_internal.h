@@ -174,6 +174,7 @@ struct orc_reverb* orc_reverb_alloc (orc_rand* rnd, double sr);
 void orc_reverb_run (struct orc_reverb* r, const float* in, float* out, int n);
 struct orc_whirl* orc_whirl_alloc (double sr, const orc_cfg* c);
 void orc_whirl_use_rev_option (struct orc_whirl* w, int n, int signals);
+int  orc_whirl_control (struct orc_whirl* w, const char* fn, unsigned char uc);
 void orc_whirl_run3 (struct orc_whirl* w, const float* in, float* L, float* R, float* tL, float* tR, size_t n);
 void orc_eq_compute (int type, double fqHz, double Q, double dbG, double* C, double sr);
 

@@ -26,6 +26,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "eqcomp.h"
 #include "overdrive.h"
 #include "reverb.h"
 #include "tonegen.h"
@@ -329,6 +330,66 @@ API void ref_set_param (ref_inst* p, int index, double v)
 		p->t->swellPedalGain = (p->t->outputLevelTrim * ((double)u)) / 127.0;
 	} else if (index == 132)
 		p->w->bypass = (int)rint (value);
+}
+
+/* The whirl's MIDI control functions (src/whirl.cpp:699-889) sit in the LV2-only part the
+ * CLAP define compiles out, and registering them needs midi.cpp, so the harness sets the
+ * reference struct's fields with the setters' mappings and recomputes the horn filters
+ * with setIIRFilter's range guard (147-172) over the reference's own eqCompute; the
+ * processing that reads the fields (whirlProc2/3) is the reference's. */
+static void ref_iir (iir_t W[], int T, double F, double Q, double G, double SR)
+{
+	double C[6];
+	if (Q <= 0.1 || Q >= 6.00 || F / SR <= 0.0002 || F / SR >= 0.4998 || G <= -48.0 || G >= 48.0 || T < EQC_LPF || T > EQC_HIGH)
+		return;
+	eqCompute (T, F, Q, G, C, SR);
+	W[a1] = C[EQC_A1];
+	W[a2] = C[EQC_A2];
+	W[b0] = C[EQC_B0];
+	W[b1] = C[EQC_B1];
+	W[b2] = C[EQC_B2];
+}
+
+API int ref_control (ref_inst* p, const char* fn, int value)
+{
+	b_whirl*            w  = p->w;
+	const unsigned char uc = (unsigned char)(value < 0 ? 0 : (value > 127 ? 127 : value));
+	const double        u  = (double)uc;
+	if (!strcmp (fn, "whirl.horn.filter.a.type"))
+		w->haT = (int)(uc / 15);
+	else if (!strcmp (fn, "whirl.horn.filter.a.hz"))
+		w->haF = 250.0 + ((8000.0 - 250.0) * ((u * u) / 16129.0));
+	else if (!strcmp (fn, "whirl.horn.filter.a.q"))
+		w->haQ = 0.01 + ((6.00 - 0.01) * (u / 127.0));
+	else if (!strcmp (fn, "whirl.horn.filter.a.gain"))
+		w->haG = -48.0 + ((48.0 - -48.0) * (u / 127.0));
+	else if (!strcmp (fn, "whirl.horn.filter.b.type"))
+		w->hbT = (int)(uc / 15);
+	else if (!strcmp (fn, "whirl.horn.filter.b.hz"))
+		w->hbF = 250.0 + ((8000.0 - 250.0) * ((u * u) / 16129.0));
+	else if (!strcmp (fn, "whirl.horn.filter.b.q"))
+		w->hbQ = 0.01 + ((6.00 - 0.01) * (u / 127.0));
+	else if (!strcmp (fn, "whirl.horn.filter.b.gain"))
+		w->hbG = -48.0 + ((48.0 - -48.0) * (u / 127.0));
+	else if (!strcmp (fn, "whirl.horn.brakepos"))
+		w->hnBrakePos = u / 127.0;
+	else if (!strcmp (fn, "whirl.drum.brakepos"))
+		w->drBrakePos = u / 127.0;
+	else if (!strcmp (fn, "whirl.horn.acceleration"))
+		w->hornAcc = .01 + u / 80.0;
+	else if (!strcmp (fn, "whirl.horn.deceleration"))
+		w->hornDec = .01 + u / 80.0;
+	else if (!strcmp (fn, "whirl.drum.acceleration"))
+		w->drumAcc = .01 + u / 14.0;
+	else if (!strcmp (fn, "whirl.drum.deceleration"))
+		w->drumDec = .01 + u / 14.0;
+	else
+		return -1;
+	if (!strncmp (fn, "whirl.horn.filter.a.", 20))
+		ref_iir (w->hafw, (int)w->haT, w->haF, w->haQ, w->haG, w->SampleRateD);
+	else if (!strncmp (fn, "whirl.horn.filter.b.", 20))
+		ref_iir (w->hbfw, (int)w->hbT, w->hbF, w->hbQ, w->hbG, w->SampleRateD);
+	return 0;
 }
 
 API void ref_render (ref_inst* p, int nblocks, float* L, float* R, float* sA, float* sB, float* sC)

@@ -9,7 +9,8 @@ import scenarios as S
 def engine_run(eng, scens, nblocks, tids=None):
     """scens: list (one per instance) of scenario event lists; events land at block
     boundaries exactly like the reference's MIDI (b_synth/lv2.cpp:1130-1134).
-    ("retune", j, 0) retunes the instance to template tids[j] (tbf_instance_retune)."""
+    ("retune", j, 0) retunes the instance to template tids[j] (tbf_instance_retune);
+    ("control", name, value) calls a MIDI control function (tbf_midi_control)."""
     bounds = {0, nblocks}
     for sc in scens:
         bounds.update(b for (b, *_r) in sc if b < nblocks)
@@ -24,6 +25,8 @@ def engine_run(eng, scens, nblocks, tids=None):
                     eng.note(i, a, v)
                 elif kind == "retune":
                     eng.retune(i, tids[a])
+                elif kind == "control":
+                    assert eng.midi_control(i, a, v)
                 else:
                     eng.set_param(i, a, v)
         L, R = eng.render(e - s)

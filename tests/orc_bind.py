@@ -54,6 +54,8 @@ def load_oracle():
     lib.orc_note.argtypes = [C.c_void_p, C.c_int, C.c_int]
     lib.orc_set_param.argtypes = [C.c_void_p, C.c_int, C.c_double]
     lib.orc_set_chain.argtypes = [C.c_void_p, C.c_int]
+    lib.orc_control.restype = C.c_int
+    lib.orc_control.argtypes = [C.c_void_p, C.c_char_p, C.c_int]
     lib.orc_render.argtypes = [C.c_void_p, C.c_int, _fp, _fp, _fp, _fp, _fp]
     lib.orc_cfg_size.restype = C.c_size_t
     lib.orc_cfg_default.argtypes = [C.c_void_p]
@@ -99,6 +101,8 @@ def load_ref(fast=False):
     lib.ref_note.argtypes = [C.c_void_p, C.c_int, C.c_int]
     lib.ref_set_param.argtypes = [C.c_void_p, C.c_int, C.c_double]
     lib.ref_set_chain.argtypes = [C.c_void_p, C.c_int]
+    lib.ref_control.restype = C.c_int
+    lib.ref_control.argtypes = [C.c_void_p, C.c_char_p, C.c_int]
     lib.ref_render.argtypes = [C.c_void_p, C.c_int, _fp, _fp, _fp, _fp, _fp]
     lib.ref_whirl_new.restype = C.c_void_p
     lib.ref_whirl_new.argtypes = [C.c_double]
@@ -267,6 +271,7 @@ class Chain:
         self._render = getattr(lib, f"{p}_render")
         self._free = getattr(lib, f"{p}_inst_free")
         self._retune = getattr(lib, f"{p}_inst_retune")
+        self._control = getattr(lib, f"{p}_control")
         self.cfg = cfg if cfg is not None else tpl.cfg
         self.ptr = self._new(tpl.ptr, int(seed), None if self.cfg is None else self.cfg.ptr)
         self.tpl = tpl
@@ -279,6 +284,11 @@ class Chain:
 
     def chain(self, mode):
         self._chain(self.ptr, int(mode))
+
+    def control(self, name, value):
+        """a whirl MIDI control function by name (value 0..127), from the next block"""
+        if self._control(self.ptr, name.encode(), int(value)) != 0:
+            raise ValueError(f"not a whirl control function: {name}")
 
     def retune(self, tpl: Template):
         """the CLAP reinitToneGen on another template, from the next block"""

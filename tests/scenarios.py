@@ -194,6 +194,54 @@ def cfg_scenario(i):
     return ev
 
 
+WHIRL_CONTROLS = tuple(f"whirl.horn.filter.{ab}.{k}" for ab in "ab" for k in ("type", "hz", "q", "gain")) + (
+    "whirl.horn.brakepos", "whirl.drum.brakepos", "whirl.horn.acceleration", "whirl.horn.deceleration",
+    "whirl.drum.acceleration", "whirl.drum.deceleration")
+
+
+def whirl_control_scenario(i, seed=None):
+    """cfg_scenario's rotor script (stop 6, fast 9, stop 26, slow 48, stop 60) with the
+    whirl's MIDI control functions (src/whirl.cpp:699-889) at seeded random values: both
+    horn filters at the start, horn filter A changed on consecutive blocks (its one
+    sub-block run-ahead), brake positions before the stops, ramp times before the speed
+    changes, out-of-range filter settings that leave the coefficients as they were (Q at
+    0, gain at +-48 dB), a brake released during the stop and a filter change while the
+    whirl is bypassed."""
+    import numpy as np
+    g = np.random.default_rng(7000 + i if seed is None else seed)
+    ev = cfg_scenario(i)
+
+    def c(b, name, v=None):
+        ev.append((b, "control", name, int(g.integers(0, 128) if v is None else v)))
+    for ab in "ab":
+        for k in ("type", "hz", "q", "gain"):
+            c(0, f"whirl.horn.filter.{ab}.{k}")
+    c(3, "whirl.horn.filter.a.hz")
+    c(4, "whirl.horn.filter.a.q", 20 + int(g.integers(0, 100)))
+    c(5, "whirl.horn.filter.b.gain")
+    c(5, "whirl.horn.brakepos", 1 + int(g.integers(0, 127)))
+    c(5, "whirl.drum.brakepos", 1 + int(g.integers(0, 127)))
+    c(8, "whirl.horn.acceleration")
+    c(8, "whirl.drum.acceleration")
+    c(24, "whirl.horn.deceleration")
+    c(24, "whirl.drum.deceleration")
+    c(30, "whirl.horn.filter.a.q", 0)
+    c(31, "whirl.horn.filter.b.gain", 127)
+    c(32, "whirl.horn.filter.a.gain", 0)
+    c(33, "whirl.horn.filter.a.type", 127)
+    c(36, "whirl.horn.brakepos", 0 if i & 1 else None)
+    c(40, "whirl.drum.brakepos")
+    c(47, "whirl.horn.acceleration")
+    c(47, "whirl.drum.deceleration")
+    ev.append((50, "param", P_WHIRL_BYPASS, 1))
+    c(51, "whirl.horn.filter.a.hz")
+    ev.append((53, "param", P_WHIRL_BYPASS, 0))
+    c(53, "whirl.horn.filter.b.hz")
+    c(58, "whirl.horn.brakepos", 1 + int(g.integers(0, 127)))
+    c(58, "whirl.drum.brakepos", 1 + int(g.integers(0, 127)))
+    return sorted(ev, key=lambda r: r[0])
+
+
 def random_drawbar_scenario(i, seed=None):
     """BASELINE config 5: upper drawbars from randomizeDrawbars (`rand() % 9` x 9,
     src/program.cpp:716-729) after srand(seed), rest of the Jazz-1 registration,
@@ -222,6 +270,8 @@ def run(chain, scenario, nblocks, stages=False, templates=None):
                 chain.note(a, v)
             elif kind == "retune":
                 chain.retune(templates[a])
+            elif kind == "control":
+                chain.control(a, v)
             else:
                 chain.param(a, v)
         outs.append(chain.render(e - s, stages=stages))

@@ -45,7 +45,7 @@ def _ctl(lib, eng, i):
     fn.restype, fn.argtypes = C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]
     out = np.zeros(64, np.float64)
     n = fn(eng._h, i, out.ctypes.data, 64)
-    assert n == 43
+    assert n == 57
     return out[:n]
 
 
@@ -166,6 +166,29 @@ def test_midi_control_functions():
     assert c[4] == 4 and c[5] == 0
     eng.midi_control(0, "rotary.speed-toggle", 10)  # release: nothing
     assert _ctl(lib, eng, 0)[4] == 4
+    # the whirl's functions (src/whirl.cpp:699-889): the struct fields, float or double
+    f32 = lambda x: float(np.float32(x))
+    for u in (0, 1, 64, 126, 127):
+        for ab, o in (("a", 43), ("b", 47)):
+            assert eng.midi_control(0, f"whirl.horn.filter.{ab}.type", u)
+            assert eng.midi_control(0, f"whirl.horn.filter.{ab}.hz", u)
+            assert eng.midi_control(0, f"whirl.horn.filter.{ab}.q", u)
+            assert eng.midi_control(0, f"whirl.horn.filter.{ab}.gain", u)
+            c = _ctl(lib, eng, 0)
+            assert c[o] == u // 15
+            assert c[o + 1] == f32(250.0 + (8000.0 - 250.0) * (u * u / 16129.0))
+            assert c[o + 2] == f32(0.01 + (6.00 - 0.01) * (u / 127.0))
+            assert c[o + 3] == f32(-48.0 + 96.0 * (u / 127.0))
+        for name, j, fn in (("horn.acceleration", 51, lambda u: f32(.01 + u / 80.0)),
+                            ("horn.deceleration", 52, lambda u: f32(.01 + u / 80.0)),
+                            ("drum.acceleration", 53, lambda u: f32(.01 + u / 14.0)),
+                            ("drum.deceleration", 54, lambda u: f32(.01 + u / 14.0)),
+                            ("horn.brakepos", 55, lambda u: u / 127.0), ("drum.brakepos", 56, lambda u: u / 127.0)):
+            assert eng.midi_control(0, "whirl." + name, u)
+            assert _ctl(lib, eng, 0)[j] == fn(u), (name, u)
+    # ... and each has a TBF_EV_CONTROL id
+    ids = [eng.control_id(nm) for nm in S.WHIRL_CONTROLS]
+    assert min(ids) >= 0 and len(set(ids)) == len(ids) == 14
     # names without a hot-path function are ignored like the reference does
     assert not eng.midi_control(0, "reverb.mix-preset", 100)
     assert not eng.midi_control(0, "xov.ctl_biased", 3)

@@ -888,6 +888,75 @@ def test_gpu_random_character_and_reverb_mix(oracle):
     assert max(eL, eR) <= TOL and min(xL, xR) == 1.0
 
 
+def test_gpu_whirl_control_functions(oracle):
+    """the whirl's MIDI control functions (src/whirl.cpp:699-889:
+    horn filters A/B type, frequency, Q, gain; horn/drum brake positions; horn/drum
+    acceleration and deceleration) through tbf_midi_control between renders, at seeded
+    random values over the rotor stop -> fast -> stop -> slow -> stop script
+    (scenarios.whirl_control_scenario: consecutive filter changes, out-of-range settings,
+    a change while bypassed), against the oracle's orc_control, itself bit-identical to the
+    reference's whirlProc under the same fields (test_oracle_whirl_controls_vs_reference)."""
+    n, nb = 8, 72
+    eng, tpl, seeds, scens = _setup(oracle, n, S.whirl_control_scenario)
+    L, R = engine_run(eng, scens, nb)
+    oL, oR, *_ = oracle_run(oracle, tpl, seeds, scens, nb)
+    eL, xL = compare(L, oL)
+    eR, xR = compare(R, oR)
+    print(f"whirl control functions: max|err| L={eL:.3g} R={eR:.3g} bit-exact L={xL:.6f} R={xR:.6f}")
+    assert max(eL, eR) == 0.0 and min(xL, xR) == 1.0
+    eng.close()
+
+
+def test_gpu_whirl_control_events_threaded(oracle):
+    """The same control functions as TBF_EV_CONTROL events inside one render of 72 blocks
+    (across the 64-block chunk edge) for 1100 instances: the threaded host front end
+    (stepChunkParallel: each worker's parameter sets rebased into the chunk's list) equals
+    serial stepping bit for bit, and the oracle for instances from every worker's range."""
+    import os
+    import torch
+    import tunebfree_amd as T
+    from orc_bind import Template
+    n, nb = 1100, 72
+    seeds = [5000 + i for i in range(n)]
+    scens = [S.whirl_control_scenario(i) for i in range(n)]
+    outs = []
+    for serial in (False, True):
+        if serial:
+            os.environ["TBF_HOST_SERIAL"] = "1"
+        try:
+            eng = T.Engine(sample_rate=48000.0, device=0)
+        finally:
+            os.environ.pop("TBF_HOST_SERIAL", None)
+        tid = eng.template(seed=7)
+        eng.add_instances([tid] * n, seeds)
+        rows = []
+        for i, sc in enumerate(scens):
+            for (b, kind, a, v) in sc:
+                if kind == "note":
+                    rows.append((b, i, 0, a, float(v)))
+                elif kind == "control":
+                    rows.append((b, i, 2, eng.control_id(a), float(v)))
+                else:
+                    rows.append((b, i, 1, a, float(v)))
+        ev = eng.events(rows)
+        L = torch.zeros((n, nb * 128), dtype=torch.float32, device="cuda")
+        R = torch.zeros_like(L)
+        eng.render_events_device(nb, ev, L.data_ptr(), R.data_ptr(), nb * 128)
+        eng.synchronize()
+        outs.append((L.cpu().numpy(), R.cpu().numpy()))
+        eng.close()
+        del L, R
+    assert np.array_equal(outs[0][0].view(np.uint32), outs[1][0].view(np.uint32))
+    assert np.array_equal(outs[0][1].view(np.uint32), outs[1][1].view(np.uint32))
+    sample = [0, 1, 219, 220, 221, 440, 659, 660, 880, 1099]  # both sides of the 220-instance ranges
+    tpl = Template(oracle, seed=7)
+    oL, oR, *_ = oracle_run(oracle, tpl, [seeds[i] for i in sample], [scens[i] for i in sample], nb)
+    eL, xL = compare(outs[0][0][sample], oL)
+    eR, xR = compare(outs[0][1][sample], oR)
+    print(f"whirl control events, threaded ({len(sample)} instances vs oracle): max|err| L={eL:.3g} R={eR:.3g}")
+    assert max(eL, eR) == 0.0 and min(xL, xR) == 1.0
+
+
 def _ring_window(max_ahead):
     """the compact whirl ring: the smallest of 512 / 1024 / 2048 holding the geometry's
     write-ahead + 2 + one 64-sample sub-block + 2 (tbf_engine.cpp buildShared)"""

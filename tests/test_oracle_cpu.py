@@ -282,6 +282,35 @@ def test_oracle_cfg_vs_reference(oracle, refchk, name):
         assert float(np.abs(a[0]).max()) > 1e-3
 
 
+def test_oracle_whirl_controls_vs_reference(oracle, refchk):
+    """the whirl's MIDI control functions (horn filters, brake
+    positions, ramp times; src/whirl.cpp:699-889) mid-run.  The oracle (orc_control) and
+    the harness (ref_control: the reference's struct fields and its own eqCompute; the
+    setters themselves are compiled out under the CLAP define) feed the reference's own
+    whirlProc2/3, bit-identical at every stage tap over the rotor script."""
+    tpl = Template(oracle, sr=48000.0, seed=7)
+    for i in range(4):
+        sc = S.whirl_control_scenario(i)
+        a = S.run(Chain(oracle, tpl, 700 + i), sc, 72, stages=True)
+        b = S.run(Chain(refchk, tpl, 700 + i, ref=True), sc, 72, stages=True)
+        for k, x, y in zip("LRABC", a, b):
+            assert np.array_equal(x.view(np.uint32), y.view(np.uint32)), (i, k)
+        # the controls change the output (against the same script without them)
+        c = S.run(Chain(oracle, tpl, 700 + i), [e for e in sc if e[1] != "control"], 72)
+        assert not np.array_equal(a[0], c[0])
+
+
+def test_oracle_whirl_control_names(oracle):
+    """orc_control knows exactly the 14 functions initWhirl registers (966-981)."""
+    tpl = Template(oracle, sr=48000.0, seed=7)
+    ch = Chain(oracle, tpl, 1)
+    for name in S.WHIRL_CONTROLS:
+        ch.control(name, 64)
+    for bad in ("whirl.horn.filter.c.type", "whirl.drum.filter.hz", "rotary.speed-toggle", "whirl.horn.brakepos "):
+        with pytest.raises(ValueError):
+            ch.control(bad, 1)
+
+
 def test_oracle_cfg_parsing(oracle):
     """orc_cfg_set follows getConfigParameter_*: ranges are inclusive, a bad or
     out-of-range value assigns nothing (-1), unknown keys are ignored (0)."""

@@ -130,7 +130,9 @@ bool controlFunction (Instance& in, const char* fn, unsigned char u)
 	else if (!strcmp (fn, "rotary.speed-toggle")) { /* setWhirlSustainPedal, 252-261 */
 		if (u > 63)
 			useRevOption (in, in.revSelect == WHIRL_SLOW ? revselects[WHIRL_FAST] : revselects[WHIRL_SLOW], 3);
-	} else
+	} else if (in.whr.control (fn, u)) /* whirl.horn.filter.*, brakepos, acceleration (src/whirl.cpp:699-889) */
+		in.whDirty = true;
+	else
 		return false;
 	in.ctlDirty = true;
 	return true;
@@ -147,7 +149,11 @@ const char* const kControlNames[] = {
     "percussion.enable", "percussion.decay", "percussion.harmonic", "percussion.volume",
     "swellpedal1", "swellpedal2", "vibrato.knob", "vibrato.routing", "vibrato.upper", "vibrato.lower",
     "overdrive.enable", "overdrive.character", "reverb.mix",
-    "rotary.speed-preset", "rotary.speed-select", "rotary.speed-toggle"};
+    "rotary.speed-preset", "rotary.speed-select", "rotary.speed-toggle",
+    "whirl.horn.filter.a.type", "whirl.horn.filter.a.hz", "whirl.horn.filter.a.q", "whirl.horn.filter.a.gain",
+    "whirl.horn.filter.b.type", "whirl.horn.filter.b.hz", "whirl.horn.filter.b.q", "whirl.horn.filter.b.gain",
+    "whirl.horn.brakepos", "whirl.drum.brakepos", "whirl.horn.acceleration", "whirl.horn.deceleration",
+    "whirl.drum.acceleration", "whirl.drum.deceleration"};
 const int kNControls = (int)(sizeof (kControlNames) / sizeof (kControlNames[0]));
 
 /* ---------------------------------------------------------------- .pgm parser */
@@ -592,7 +598,7 @@ int tbf_debug_control (tbf_engine* e, uint32_t inst, double* out, uint32_t cap)
 		return fail (-22, "bad argument");
 	const Instance& in = e->inst[inst];
 	const TgControl& t = in.tg;
-	double v[48];
+	double v[64];
 	int    k = 0;
 	v[k++] = in.odClean;
 	v[k++] = in.odA;
@@ -612,6 +618,11 @@ int tbf_debug_control (tbf_engine* e, uint32_t inst, double* out, uint32_t cap)
 	v[k++] = t.percDrawbarGain;
 	for (int b = 0; b < 27; b++)
 		v[k++] = t.drawBarGain[b];
+	const WhirlRt& w = in.whr;
+	for (float f : {w.haT, w.haF, w.haQ, w.haG, w.hbT, w.hbF, w.hbQ, w.hbG, w.hornAcc, w.hornDec, w.drumAcc, w.drumDec})
+		v[k++] = f;
+	v[k++] = w.cur.hnBrakePos;
+	v[k++] = w.cur.drBrakePos;
 	const uint32_t n = (uint32_t)k < cap ? (uint32_t)k : cap;
 	for (uint32_t i = 0; i < n; i++)
 		out[i] = v[i];

@@ -121,8 +121,6 @@ static void reverbConsts (tbf_inst_const& k, double sr, float A, float B, float 
 
 static void whirlConsts (tbf_inst_const& k, const WhirlTables& wt, const Config& c)
 {
-	memcpy (k.hafw, wt.hafw, sizeof (k.hafw));
-	memcpy (k.hbfw, wt.hbfw, sizeof (k.hbfw));
 	memcpy (k.drf, wt.drf, sizeof (k.drf));
 	memcpy (k.hornSpacing, wt.hornSpacing, sizeof (k.hornSpacing));
 	memcpy (k.drumSpacing, wt.drumSpacing, sizeof (k.drumSpacing));
@@ -156,12 +154,9 @@ static void whirlConsts (tbf_inst_const& k, const WhirlTables& wt, const Config&
 	/* HN_MOTION / DR_MOTION angle offsets (src/whirl.cpp:1396-1400) */
 	k.fwAng = c.micAngle * .25;
 	k.bwAng = 1. + c.micAngle * -.25;
-	memcpy (k.lAcc, wt.lAcc, sizeof (k.lAcc));
 	k.deadzone = (.05 / (60.f * wt.sr));
 	memcpy (k.revHorn, wt.revHorn, sizeof (k.revHorn));
 	memcpy (k.revDrum, wt.revDrum, sizeof (k.revDrum));
-	k.hnBrakePos = c.hnBrakePos;
-	k.drBrakePos = c.drBrakePos;
 	k.hnHardstop = (float)(10.f / (60.f * wt.sr));
 	k.drHardstop = (float)(8.f / (60.f * wt.sr));
 	k.minspeed   = (float)(3.f / (60.f * wt.sr));
@@ -433,6 +428,8 @@ int tbf_engine_destroy (tbf_engine* e)
 	e->dmsgB.release ();
 	e->dgain.release ();
 	e->dgainB.release ();
+	e->dwh.release ();
+	e->dwhB.release ();
 	e->dctlInstB.release ();
 	e->coff.release ();
 	e->contrib.release ();
@@ -670,6 +667,8 @@ int tbf_instances_add (tbf_engine* e, uint32_t n, const uint32_t* tpl_ids, const
 		if (in.k.delay[12] < 0 || in.k.delay[12] >= TBF_PD_HIST) /* 560 at the fixed settings */
 			return fail (-22, "predelay longer than its history");
 		whirlConsts (in.k, e->wt, e->conf);
+		in.whr.init (e->wt.sr, e->conf); /* the runtime whirl parameters, as the cfg left them */
+		in.s0.wh.prm = in.whr.cur;
 		in.rvG      = e->conf.reverbMix;  /* reverbConfig: setReverbMix */
 		in.whBypass = e->conf.bypass;     /* whirlConfig: whirl.bypass */
 		/* initWhirl -> computeRotationSpeeds -> setRevSelect(revSelect) ->
@@ -1114,7 +1113,8 @@ static int applyEvent (tbf_engine* e, const tbf_event& ev)
  * the instance's current control e->hCtl[i] / program e->hProg; returns true when the
  * control the next block renders with changed. */
 static bool stepControl (tbf_engine* e, uint32_t i, bool& progChanged, tbf_tgc_rec* rec = nullptr,
-                         std::vector<uint16_t>* msgOut = nullptr, std::vector<float>* gainOut = nullptr)
+                         std::vector<uint16_t>* msgOut = nullptr, std::vector<float>* gainOut = nullptr,
+                         std::vector<tbf_wh_params>* whOut = nullptr)
 {
 	Instance&    in      = e->inst[i];
 	tbf_seg_ctl& c       = e->hCtl[i];
@@ -1174,7 +1174,19 @@ static bool stepControl (tbf_engine* e, uint32_t i, bool& progChanged, tbf_tgc_r
 	c.whBypass    = (uint32_t)in.whBypass;
 	c.whRevOption = in.revOpt; /* a one-shot: the next block gets a fresh entry without it */
 	in.revOpt     = -1;
-	in.ctlDirty   = (c.whRevOption >= 0);
+	c.whSet       = 0;         /* a one-shot too: the whirl keeps a set until the next one */
+	if (in.whDirty) {
+		const tbf_wh_params& p = in.whr.cur;
+		if (whOut) { /* a host worker's own list (worker-local index, renderImpl rebases it) */
+			whOut->push_back (p);
+			c.whSet = (uint32_t)whOut->size ();
+		} else {
+			e->hWh.push_back (p);
+			c.whSet = (uint32_t)e->hWh.size ();
+		}
+		in.whDirty = false;
+	}
+	in.ctlDirty = (c.whRevOption >= 0) || c.whSet;
 	return true;
 }
 
@@ -1198,6 +1210,7 @@ static int stepChunkParallel (tbf_engine* e, uint32_t n, uint32_t want, uint32_t
 	for (auto& o : out) {
 		o.msgs.clear ();
 		o.gains.clear ();
+		o.whs.clear ();
 		o.act.clear ();
 		o.ctlInst.clear ();
 		o.evs.clear ();
@@ -1238,7 +1251,7 @@ static int stepChunkParallel (tbf_engine* e, uint32_t n, uint32_t want, uint32_t
 				const uint32_t i = o.act[a];
 				bool           pc;
 				tbf_tgc_rec&   rec = Rr[o.nd];
-				if (stepControl (e, i, pc, &rec, &o.msgs, &o.gains)) {
+				if (stepControl (e, i, pc, &rec, &o.msgs, &o.gains, &o.whs)) {
 					const uint32_t d = base + o.nd;
 					tbf_seg_ctl&   c = Cc[o.nd++];
 					c                = e->hCtl[i];
@@ -1267,8 +1280,8 @@ static int stepChunkParallel (tbf_engine* e, uint32_t n, uint32_t want, uint32_t
 		thNs[t] = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds> (std::chrono::steady_clock::now () - th0).count ();
 	});
 	const auto ph1 = std::chrono::steady_clock::now ();
-	std::vector<size_t> mb (T), gb (T);
-	size_t              nm = 0, ng = 0;
+	std::vector<size_t> mb (T), gb (T), wb (T);
+	size_t              nm = 0, ng = 0, nw = 0;
 	e->dSeg.clear ();
 	for (unsigned t = 0; t < T; t++) {
 		if (out[t].rc)
@@ -1277,6 +1290,8 @@ static int stepChunkParallel (tbf_engine* e, uint32_t n, uint32_t want, uint32_t
 		nm += out[t].msgs.size ();
 		gb[t] = ng;
 		ng += out[t].gains.size ();
+		wb[t] = nw;
+		nw += out[t].whs.size ();
 		if (out[t].nd) {
 			e->dSeg.push_back ({t * per * want, out[t].nd});
 			delta = true;
@@ -1286,8 +1301,9 @@ static int stepChunkParallel (tbf_engine* e, uint32_t n, uint32_t want, uint32_t
 		e->dSeg.push_back ({0, 0});
 	e->hMsg.resize (nm);
 	e->hGain.resize (ng);
-	if (nm || ng)
-		parallelFor (T, [&] (uint32_t t) { /* message and gain offsets: worker-local -> chunk */
+	e->hWh.resize (nw);
+	if (nm || ng || nw)
+		parallelFor (T, [&] (uint32_t t) { /* message, gain and whirl set offsets: worker-local -> chunk */
 			const tbf_engine::ParStep& o    = out[t];
 			const size_t               base = (size_t)t * per * want;
 			for (size_t d = base; d < base + o.nd; d++) {
@@ -1296,7 +1312,11 @@ static int stepChunkParallel (tbf_engine* e, uint32_t n, uint32_t want, uint32_t
 					r.msgOff += (uint32_t)mb[t];
 				if (r.flags & 4)
 					r.gainOff += (uint32_t)gb[t];
+				if (e->dCtl[d].whSet)
+					e->dCtl[d].whSet += (uint32_t)wb[t];
 			}
+			if (!o.whs.empty ())
+				memcpy ((void*)(e->hWh.data () + wb[t]), o.whs.data (), o.whs.size () * sizeof (tbf_wh_params));
 			if (!o.msgs.empty ())
 				memcpy (e->hMsg.data () + mb[t], o.msgs.data (), o.msgs.size () * sizeof (uint16_t));
 			if (!o.gains.empty ())
@@ -1419,6 +1439,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		for (uint32_t i = 0; i < n; i++)
 			if (e->chg[i]) {
 				e->hCtl[i].whRevOption = -1;
+				e->hCtl[i].whSet       = 0;
 				lo                     = std::min (lo, i);
 				hi                     = std::max (hi, i + 1);
 				e->chg[i]              = 0;
@@ -1491,6 +1512,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			e->hRec.swap (e->hRecB);
 			e->hMsg.swap (e->hMsgB);
 			e->hGain.swap (e->hGainB);
+			e->hWh.swap (e->hWhB);
 			e->hCtlInst.swap (e->hCtlInstB);
 			e->hIdx.swap (e->hIdxB);
 			e->hCtlPin.swap (e->hCtlPinB);
@@ -1520,6 +1542,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		e->hRec.clear ();
 		e->hMsg.clear ();
 		e->hGain.clear ();
+		e->hWh.clear ();
 		e->hCtlInst.clear ();
 		e->stepped.assign (n, 0);
 		e->hIdx.resize ((size_t)want * n);
@@ -1636,6 +1659,17 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 				                        e->dProg.size () * sizeof (tbf_prog_entry), hipMemcpyHostToDevice, us));
 			HIPCHK (hipMemcpyAsync (e->ctlIdx.p + (size_t)rp * n * TBF_CHUNK, e->hIdx.data (),
 			                        (size_t)len * n * sizeof (uint32_t), hipMemcpyHostToDevice, us));
+		}
+		P.whSets = nullptr;
+		if (delta && !e->hWh.empty ()) {
+			/* the whirl parameter sets of the chunk's deltas, by region parity like the records */
+			DevBuf<tbf_wh_params>& dw = rp ? e->dwhB : e->dwh;
+			if (dw.cap < e->hWh.size ())
+				HIPCHK (hipDeviceSynchronize ()); /* growing: nothing may still read the old buffer */
+			if (dw.ensure (std::max<size_t> (e->hWh.size (), 64)))
+				return fail (-12, "out of device memory (whirl parameter sets)");
+			HIPCHK (hipMemcpyAsync (dw.p, e->hWh.data (), e->hWh.size () * sizeof (tbf_wh_params), hipMemcpyHostToDevice, us));
+			P.whSets = dw.p;
 		}
 		P.prog      = e->prog.p;
 		P.ctl       = e->ctl.p + rp * CTL_REGION (n);

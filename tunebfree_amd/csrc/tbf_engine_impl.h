@@ -61,6 +61,8 @@ struct Instance {
 	int            whBypass = 0;
 	int            revOpt = -1;   /* useRevOption (n) pending for the next block */
 	int            revSelect = 0; /* whirl revSelect: WHIRL_SLOW after initWhirl (src/whirl.cpp:1131) */
+	WhirlRt        whr;           /* the whirl's MIDI-settable fields ... */
+	bool           whDirty = false; /* ... changed since the last block's parameter set */
 	GlibcRand      ctlRand{1};    /* control-plane rand() stream (randomizeDrawbars) */
 	bool           ctlDirty = true;
 	bool           progDirty = true;
@@ -200,6 +202,8 @@ struct tbf_engine {
 	PinnedVec<float>                        hGain;    /* the chunk's drawbar gain sets (27 each) */
 	PinnedVec<float>                        hGainB;
 	DevBuf<float>                           dgain, dgainB;
+	PinnedVec<tbf_wh_params>                hWh, hWhB; /* the chunk's whirl parameter sets (tbf_seg_ctl.whSet) */
+	DevBuf<tbf_wh_params>                   dwh, dwhB;
 	PinnedVec<uint32_t>                     hCtlInst; /* instances with a stepped delta */
 	/* the other parity of the chunk staging (the previous chunk's, in flight), and the
 	 * events after each parity's uploads */
@@ -223,6 +227,7 @@ struct tbf_engine {
 	struct alignas (128) ParStep { /* own cache lines: workers bump these per delta */
 		std::vector<uint16_t> msgs;
 		std::vector<float>    gains;
+		std::vector<tbf_wh_params> whs;
 		std::vector<uint32_t> act, ctlInst, evs;
 		uint32_t              nd = 0;
 		int                   rc = 0;

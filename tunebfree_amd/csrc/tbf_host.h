@@ -131,11 +131,24 @@ struct WhirlTables {
 	std::vector<float> bw;    /* bfw, bbw: 2 x 16384 x 5 */
 	float              hornSpacing[6], drumSpacing[6];
 	int32_t            phase[6];
-	float              hafw[5], hbfw[5], drf[5];
+	float              drf[5];
 	double             revHorn[9], revDrum[9];
-	double             lAcc[4];
 	float              maxAhead; /* largest write-ahead in samples */
 	void build (double sr, const Config& c);
+};
+
+/* the whirl fields the MIDI control functions set (struct b_whirl, src/whirl.h; setters
+ * src/whirl.cpp:699-889), with the reference's field types, and the parameter set k_whirl
+ * renders with: the horn filters through setIIRFilter (UPDATE_A_FILTER / UPDATE_B_FILTER),
+ * the speed-ramp factors of whirlProc2 (1255-1257, 1306-1308) */
+struct WhirlRt {
+	float         haT = 0, haF = 0, haQ = 0, haG = 0, hbT = 0, hbF = 0, hbQ = 0, hbG = 0;
+	float         hornAcc = 0, hornDec = 0, drumAcc = 0, drumDec = 0;
+	double        sr = 0;
+	tbf_wh_params cur = {}; /* the set as of the last setter (hnBrakePos / drBrakePos live here) */
+	void init (double sr, const Config& c); /* initValues + whirlConfig + initialize */
+	bool control (const char* fn, unsigned char u); /* false: not a whirl parameter */
+	void ramps ();
 };
 
 /* per-instance tonegen control state (runtime fields of struct b_tonegen) */

@@ -3,6 +3,7 @@
  * Each function cites the reference code whose arithmetic it reproduces.
  */
 #include <math.h>
+#include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
@@ -580,11 +581,11 @@ static void eqCompute (int type, double fqHz, double Q, double dbG, double* C, d
 	C[5] /= C[3];
 }
 
-/* setIIRFilter (src/whirl.cpp:147-172) -> {a1, a2, b0, b1, b2} */
-static void iirCoef (float* W, int T, double F, double Q, double G, double SR)
+/* setIIRFilter (src/whirl.cpp:147-172) -> {a1, a2, b0, b1, b2}: out-of-range settings
+ * leave the coefficients as they were */
+static void iirSet (float* W, int T, double F, double Q, double G, double SR)
 {
 	double C[6];
-	W[0] = W[1] = W[2] = W[3] = W[4] = 0.f;
 	if (Q <= 0.1 || Q >= 6.00 || F / SR <= 0.0002 || F / SR >= 0.4998 || G <= -48.0 || G >= 48.0 || T < 0 || T > 8)
 		return;
 	eqCompute (T, F, Q, G, C, SR);
@@ -593,6 +594,13 @@ static void iirCoef (float* W, int T, double F, double Q, double G, double SR)
 	W[2] = (float)C[0];
 	W[3] = (float)C[1];
 	W[4] = (float)C[2];
+}
+
+/* ... on the zeroed filter of allocWhirl's calloc (src/whirl.cpp:136-143) */
+static void iirCoef (float* W, int T, double F, double Q, double G, double SR)
+{
+	W[0] = W[1] = W[2] = W[3] = W[4] = 0.f;
+	iirSet (W, T, F, Q, G, SR);
 }
 
 void WhirlTables::build (double rate, const Config& c)
@@ -658,10 +666,8 @@ void WhirlTables::build (double rate, const Config& c)
 			obfw[(size_t)i * 5 + j]                  = v;
 			obbw[(size_t)(16384 - i - 1) * 5 + j] = v;
 		}
-	/* initialize (626-662): drum hi-shelf, horn A low-pass, horn B low-shelf */
+	/* initialize (626-662): drum hi-shelf (the horn filters: WhirlRt) */
 	iirCoef (drf, c.lpT, c.lpF, c.lpQ, c.lpG, sr);
-	iirCoef (hafw, (int)c.haT, c.haF, c.haQ, c.haG, sr);
-	iirCoef (hbfw, (int)c.hbT, c.hbF, c.hbQ, c.hbG, sr);
 	/* computeRotationSpeeds (270-293) */
 	const float  hornRPMslow = c.hornRPMslow, hornRPMfast = c.hornRPMfast;
 	const float  drumRPMslow = c.drumRPMslow, drumRPMfast = c.drumRPMfast;
@@ -673,11 +679,89 @@ void WhirlTables::build (double rate, const Config& c)
 		revHorn[i] = H[i];
 		revDrum[i] = D[i];
 	}
-	/* speed-ramp factors of whirlProc2 (1255-1257, 1306-1308), block = 128 */
-	const float hornAcc = c.hornAcc, hornDec = c.hornDec, drumAcc = c.drumAcc, drumDec = c.drumDec;
-	const float acc[4]  = {hornAcc, hornDec, drumAcc, drumDec};
+}
+
+void WhirlRt::init (double rate, const Config& c)
+{
+	sr         = rate;
+	haT        = c.haT;
+	haF        = c.haF;
+	haQ        = c.haQ;
+	haG        = c.haG;
+	hbT        = c.hbT;
+	hbF        = c.hbF;
+	hbQ        = c.hbQ;
+	hbG        = c.hbG;
+	hornAcc    = c.hornAcc;
+	hornDec    = c.hornDec;
+	drumAcc    = c.drumAcc;
+	drumDec    = c.drumDec;
+	/* initialize (626-662): horn A low-pass, horn B low-shelf */
+	iirCoef (cur.hafw, (int)haT, haF, haQ, haG, sr);
+	iirCoef (cur.hbfw, (int)hbT, hbF, hbQ, hbG, sr);
+	ramps ();
+	cur.hnBrakePos = c.hnBrakePos;
+	cur.drBrakePos = c.drBrakePos;
+}
+
+/* the speed-ramp factors of whirlProc2 (1255-1257, 1306-1308), block = 128 */
+void WhirlRt::ramps ()
+{
+	const float acc[4] = {hornAcc, hornDec, drumAcc, drumDec};
 	for (int i = 0; i < 4; i++)
-		lAcc[i] = exp (-1.0 / (sr / (size_t)TBF_BLK * acc[i]));
+		cur.lAcc[i] = exp (-1.0 / (sr / (size_t)TBF_BLK * acc[i]));
+}
+
+/* the MIDI control functions initWhirl registers (src/whirl.cpp:966-981), setters 699-889:
+ * each maps the 7-bit value into the field's range in double and stores it in the field */
+bool WhirlRt::control (const char* fn, unsigned char uc)
+{
+	static const char pre[] = "whirl.";
+	if (strncmp (fn, pre, sizeof (pre) - 1))
+		return false;
+	const char*  f = fn + sizeof (pre) - 1;
+	const double u = (double)uc;
+	for (int ab = 0; ab < 2; ab++) {
+		float* T = ab ? &hbT : &haT;
+		float* F = ab ? &hbF : &haF;
+		float* Q = ab ? &hbQ : &haQ;
+		float* G = ab ? &hbG : &haG;
+		char   nm[32];
+		snprintf (nm, sizeof (nm), "horn.filter.%c.", ab ? 'b' : 'a');
+		const size_t l = strlen (nm);
+		if (strncmp (f, nm, l))
+			continue;
+		const char* k = f + l;
+		if (!strcmp (k, "type")) /* setHornFilterAType / BType */
+			*T = (float)(int)(uc / 15);
+		else if (!strcmp (k, "hz")) /* ... Frequency: 250 .. 8000, quadratic */
+			*F = (float)(250.0 + ((8000.0 - 250.0) * ((u * u) / 16129.0)));
+		else if (!strcmp (k, "q")) /* ... Q: 0.01 .. 6 */
+			*Q = (float)(0.01 + ((6.00 - 0.01) * (u / 127.0)));
+		else if (!strcmp (k, "gain")) /* ... Gain: -48 .. 48 dB */
+			*G = (float)(-48.0 + ((48.0 - -48.0) * (u / 127.0)));
+		else
+			return false;
+		/* UPDATE_A_FILTER / UPDATE_B_FILTER (679-689) */
+		iirSet (ab ? cur.hbfw : cur.hafw, (int)*T, *F, *Q, *G, sr);
+		return true;
+	}
+	if (!strcmp (f, "horn.brakepos")) /* setHornBrakePosition */
+		cur.hnBrakePos = u / 127.0;
+	else if (!strcmp (f, "drum.brakepos")) /* setDrumBrakePosition */
+		cur.drBrakePos = u / 127.0;
+	else if (!strcmp (f, "horn.acceleration")) /* setHornAcceleration */
+		hornAcc = (float)(.01 + u / 80.0);
+	else if (!strcmp (f, "horn.deceleration"))
+		hornDec = (float)(.01 + u / 80.0);
+	else if (!strcmp (f, "drum.acceleration")) /* setDrumAcceleration */
+		drumAcc = (float)(.01 + u / 14.0);
+	else if (!strcmp (f, "drum.deceleration"))
+		drumDec = (float)(.01 + u / 14.0);
+	else
+		return false;
+	ramps ();
+	return true;
 }
 
 /* ------------------------------------------------------------------ tonegen control */

@@ -1622,6 +1622,7 @@ __device__ void whirl_speed (tbf_wh_state& st, const tbf_inst_const& K, int revO
 	double hornAngle = st.hornAngle, drumAngle = st.drumAngle, hornIncr = st.hornIncr, drumIncr = st.drumIncr;
 	double hornTarget = st.hornTarget, drumTarget = st.drumTarget;
 	int    hornAcDc = st.hornAcDc, drumAcDc = st.drumAcDc;
+	const double hnBrakePos = st.prm.hnBrakePos, drBrakePos = st.prm.drBrakePos;
 	/* useRevOption (src/whirl.cpp:174-196) for an event landing before this block */
 	if (revOpt >= 0) {
 		const int i   = revOpt % 9;
@@ -1639,8 +1640,8 @@ __device__ void whirl_speed (tbf_wh_state& st, const tbf_inst_const& K, int revO
 	/* src/whirl.cpp:1219-1374 */
 	if (hornAcDc) {
 		int flywheel = 0;
-		if (K.hnBrakePos > 0 && hornTarget == 0 && hornIncr > 0 && hornIncr < K.hnHardstop) {
-			const double targetPos = fmod (1.25 - K.hnBrakePos, 1.0);
+		if (hnBrakePos > 0 && hornTarget == 0 && hornIncr > 0 && hornIncr < K.hnHardstop) {
+			const double targetPos = fmod (1.25 - hnBrakePos, 1.0);
 			if (fabs (hornAngle - targetPos) < (2.0 / 16384)) {
 				hornAngle = targetPos;
 				hornIncr  = 0;
@@ -1654,7 +1655,7 @@ __device__ void whirl_speed (tbf_wh_state& st, const tbf_inst_const& K, int revO
 			}
 		}
 		if (!flywheel) {
-			const double l = hornAcDc > 0 ? K.lAcc[0] : K.lAcc[1];
+			const double l = hornAcDc > 0 ? st.prm.lAcc[0] : st.prm.lAcc[1];
 			hornIncr += (1 - l) * (hornTarget - hornIncr);
 		}
 		if (fabs (hornTarget - hornIncr) < K.deadzone) {
@@ -1664,8 +1665,8 @@ __device__ void whirl_speed (tbf_wh_state& st, const tbf_inst_const& K, int revO
 	}
 	if (drumAcDc) {
 		int flywheel = 0;
-		if (K.drBrakePos > 0 && drumTarget == 0 && drumIncr > 0 && drumIncr < K.drHardstop) {
-			const double targetPos = fmod (K.drBrakePos + .75, 1.0);
+		if (drBrakePos > 0 && drumTarget == 0 && drumIncr > 0 && drumIncr < K.drHardstop) {
+			const double targetPos = fmod (drBrakePos + .75, 1.0);
 			if (fabs (drumAngle - targetPos) < (2.0 / 16384)) {
 				drumAngle = targetPos;
 				drumIncr  = 0;
@@ -1679,7 +1680,7 @@ __device__ void whirl_speed (tbf_wh_state& st, const tbf_inst_const& K, int revO
 			}
 		}
 		if (!flywheel) {
-			const double l = drumAcDc > 0 ? K.lAcc[2] : K.lAcc[3];
+			const double l = drumAcDc > 0 ? st.prm.lAcc[2] : st.prm.lAcc[3];
 			drumIncr += (1 - l) * (drumTarget - drumIncr);
 		}
 		if (fabs (drumTarget - drumIncr) < K.deadzone) {
@@ -1688,8 +1689,8 @@ __device__ void whirl_speed (tbf_wh_state& st, const tbf_inst_const& K, int revO
 		}
 	}
 	brake = 0;
-	if (K.hnBrakePos > 0) {
-		const double targetPos = fmod (1.25 - K.hnBrakePos, 1.0);
+	if (hnBrakePos > 0) {
+		const double targetPos = fmod (1.25 - hnBrakePos, 1.0);
 		if (!hornAcDc && hornIncr == 0 && hornAngle != targetPos) {
 			brake |= 1;
 			if (fabs (hornAngle - targetPos) < (2.0 / 16384)) {
@@ -1701,8 +1702,8 @@ __device__ void whirl_speed (tbf_wh_state& st, const tbf_inst_const& K, int revO
 			}
 		}
 	}
-	if (K.drBrakePos > 0) {
-		const double targetPos = fmod (K.drBrakePos + .75, 1.0);
+	if (drBrakePos > 0) {
+		const double targetPos = fmod (drBrakePos + .75, 1.0);
 		if (!drumAcDc && drumIncr == 0 && drumAngle != targetPos) {
 			brake |= 2;
 			if (fabs (drumAngle - targetPos) < (2.0 / 16384)) {
@@ -1887,9 +1888,16 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 	wave_sync ();
 	const double   hornIncr = st.hornIncr, drumIncr = st.drumIncr;
 	const uint32_t WM       = (uint32_t)W - 1u;
-	/* serial filter coefficients: lane 0 horn A, lane 1 horn B, lanes 2-3 drum shelf */
-	const float* cfa = lane == 0 ? K.hafw : (lane == 1 ? K.hbfw : K.drf);
-	const float  fa0 = cfa[0], fa1 = cfa[1]; /* a1, a2 of the serial state recurrences */
+	/* the horn filters' coefficients of this block (the runtime set in the state); serial
+	 * filter coefficients: lane 0 horn A, lane 1 horn B, lanes 2-3 drum shelf */
+	float ha[5], hb[5];
+#pragma unroll
+	for (int j = 0; j < 5; j++) {
+		ha[j] = st.prm.hafw[j];
+		hb[j] = st.prm.hbfw[j];
+	}
+	const float fa0 = lane == 0 ? ha[0] : (lane == 1 ? hb[0] : K.drf[0]);
+	const float fa1 = lane == 0 ? ha[1] : (lane == 1 ? hb[1] : K.drf[1]); /* a1, a2 of the serial state recurrences */
 
 	for (int sb = 0; sb < TBF_BLK / TBF_SUB; sb++) {
 		const int      n      = lane;
@@ -1930,10 +1938,10 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 		wave_sync ();
 		if (!sm.aReady) {
 			if (lane == 0)
-				wh_serial (sm.xx + 1, sm.tmp[0], st.fz[0], K.hafw[0], K.hafw[1], false);
+				wh_serial (sm.xx + 1, sm.tmp[0], st.fz[0], ha[0], ha[1], false);
 			wave_sync ();
 			const float* T0 = sm.tmp[0];
-			sm.aOut[n]      = (T0[n + 2] * K.hafw[2]) + (K.hafw[3] * T0[n + 1]) + (K.hafw[4] * T0[n]);
+			sm.aOut[n]      = (T0[n + 2] * ha[2]) + (ha[3] * T0[n + 1]) + (ha[4] * T0[n]);
 			wave_sync ();
 		}
 		if (lane < 4 && (lane > 0 || aNext)) {
@@ -1946,7 +1954,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 			/* filter outputs: horn B -> xf, drum shelves in place, horn A of the next
 			 * sub-block -> aOut */
 			const float* T1 = sm.tmp[1];
-			sm.xf[4 + n]    = (T1[n + 2] * K.hbfw[2]) + (K.hbfw[3] * T1[n + 1]) + (K.hbfw[4] * T1[n]);
+			sm.xf[4 + n]    = (T1[n + 2] * hb[2]) + (hb[3] * T1[n + 1]) + (hb[4] * T1[n]);
 #pragma unroll
 			for (int c = 0; c < 2; c++) {
 				const float* Tc = sm.tmp[2 + c];
@@ -1954,7 +1962,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 			}
 			if (aNext) {
 				const float* T0 = sm.tmp[0];
-				sm.aOut[n]      = (T0[n + 2] * K.hafw[2]) + (K.hafw[3] * T0[n + 1]) + (K.hafw[4] * T0[n]);
+				sm.aOut[n]      = (T0[n + 2] * ha[2]) + (ha[3] * T0[n + 1]) + (ha[4] * T0[n]);
 			}
 			if (lane == 0)
 				sm.aReady = aNext;
@@ -2184,6 +2192,8 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 	wave_sync ();
 }
 
+static_assert (sizeof (tbf_wh_params) % 4 == 0 && sizeof (tbf_wh_params) <= 4 * NL, "one dword per lane");
+
 template <int W>
 __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL), amdgpu_waves_per_eu (W <= 512 ? WH_WAVES : (W <= 1024 ? 2 : 1))))
 k_whirl (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_seg_ctl* __restrict__ ctl)
@@ -2206,11 +2216,12 @@ k_whirl (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 	const float* inBase = P.mid2 + (size_t)inst * P.midStride;
 	/* the launch's per-block control (bypass, rotary selection), lane b = block b (<= 64
 	 * blocks): read once, so no block waits on the two dependent control loads */
-	int byv = 0, rvv = -1;
+	int byv = 0, rvv = -1, wsv = 0;
 	if (threadIdx.x < P.nBlocks) {
 		const tbf_seg_ctl& Gb = ctl_of (P, ctl, threadIdx.x, inst);
 		byv                   = Gb.whBypass != 0;
 		rvv                   = Gb.whRevOption;
+		wsv                   = (int)Gb.whSet;
 	}
 	float c0 = 0.f, c1 = 0.f;
 	if (P.nBlocks > 0) {
@@ -2226,8 +2237,18 @@ k_whirl (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 			n0 = inBase[(size_t)(blk + 1) * TBF_BLK + threadIdx.x];
 			n1 = inBase[(size_t)(blk + 1) * TBF_BLK + threadIdx.x + NL];
 		}
-		/* horn filter A may run ahead into the next block unless that one is bypassed */
-		const bool hasNext = more && !rl (byv, (int)min (blk + 1, (uint32_t)NL - 1));
+		/* a new parameter set (MIDI control functions) from this block on */
+		const int ws = rl (wsv, (int)blk);
+		if (ws) {
+			const uint32_t* src = (const uint32_t*)(P.whSets + (ws - 1));
+			if (threadIdx.x < sizeof (tbf_wh_params) / 4)
+				((uint32_t*)&sm.st.prm)[threadIdx.x] = src[threadIdx.x];
+			wave_sync ();
+		}
+		/* horn filter A may run ahead into the next block unless that one is bypassed or
+		 * changes its coefficients */
+		const int  nx      = (int)min (blk + 1, (uint32_t)NL - 1);
+		const bool hasNext = more && !rl (byv, nx) && !rl (wsv, nx);
 		stage_whirl<W> (P, sm, rl (byv, (int)blk) != 0, rl (rvv, (int)blk), K, c0, c1, n0, hasNext, oL, oR);
 		c0 = n0;
 		c1 = n1;

@@ -92,9 +92,21 @@ typedef struct tbf_seg_ctl {
 	uint32_t odDensityPos;   /* density > 0 */
 	uint32_t whBypass;
 	int32_t  whRevOption;    /* >= 0: useRevOption(n) before the first block */
+	uint32_t whSet;          /* > 0: the whirl takes whSets[whSet - 1] before this block */
+	uint32_t pad0;
 	double   odOut, odOutput, odWet, odDry, odIir;
 	double   rvWet;
 } tbf_seg_ctl;
+
+/* the whirl parameters the MIDI control functions set (src/whirl.cpp:699-889: the horn
+ * filters' coefficients, brake positions and the speed-ramp factors derived from the
+ * acceleration / deceleration times).  k_whirl keeps the current set in tbf_wh_state and
+ * replaces it before a block whose control entry carries one (tbf_seg_ctl.whSet). */
+typedef struct tbf_wh_params {
+	float    hafw[5], hbfw[5]; /* horn filters A, B: a1, a2, b0, b1, b2 */
+	double   lAcc[4];          /* exp() speed-ramp factors: horn acc, horn dec, drum acc, drum dec */
+	double   hnBrakePos, drBrakePos;
+} tbf_wh_params;
 
 /* per instance, constant over its lifetime */
 typedef struct tbf_inst_const {
@@ -109,16 +121,14 @@ typedef struct tbf_inst_const {
 	uint32_t slabLen;
 	uint32_t vibClosedForm; /* 1: phase increments have no rounding ties (host-checked) */
 	/* whirl (src/whirl.cpp init) */
-	float    hafw[5], hbfw[5], drf[5]; /* a1, a2, b0, b1, b2 */
+	float    drf[5];  /* drum shelf: a1, a2, b0, b1, b2 (the horn filters: tbf_wh_params) */
 	float    hornSpacing[6], drumSpacing[6];
 	int32_t  hornPhase[6];
 	float    leakage, hornLevel;
 	float    mic[8]; /* hll hlr dll dlr hrl hrr drl drr */
 	double   fwAng, bwAng;
-	double   lAcc[4]; /* exp() speed-ramp factors: horn acc, horn dec, drum acc, drum dec */
 	double   deadzone;
 	double   revHorn[9], revDrum[9];
-	double   hnBrakePos, drBrakePos;
 	float    hnHardstop, drHardstop, minspeed, hnLimit, drLimit;
 	float    pad0;
 	double   sr;
@@ -172,6 +182,7 @@ typedef struct tbf_wh_state { /* whirl: k_whirl */
 	float    adx[3][8];
 	int32_t  adi[3];
 	int32_t  pad1[2];
+	tbf_wh_params prm; /* the current runtime parameters */
 } tbf_wh_state;
 
 typedef struct tbf_inst_state {
@@ -208,6 +219,7 @@ typedef struct tbf_launch {
 	const uint32_t*       xsJump; /* [32][TBF_XS_JUMP]: xorshift32^k (1 << j), k = 0..128; then [8][16][TBF_XS_JUMP] nibble-sliced */
 	const float*          whTab;  /* hnFwd, hnBwd, drFwd, drBwd [4][TBF_WH_TSTRIDE]: 16384 + [0] again + pad */
 	const float*          whBw;   /* bfw, bbw [2][16384][5] */
+	const tbf_wh_params*  whSets; /* the chunk's whirl parameter sets (tbf_seg_ctl.whSet) */
 	float*                outL;
 	float*                outR;
 	uint64_t              outStride; /* floats between instances */

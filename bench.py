@@ -30,9 +30,9 @@ sys.path.insert(0, str(ROOT / "tests"))
 #   k_rv_core = the 12 network lines (A..L) x 2 ch x 16 B              = 384 B
 #   k_rv_pre  = the predelay line M x 2 ch x 16 B                      =  32 B
 #   k_whirl   = L/R float32 output                                     =   8 B
-# The implementation's inter-stage streams (mid1/rvA/rvB/mid2) are NOT algorithmic; they
+# The implementation's inter-stage streams (mid0/mid1/rvA/rvB/mid2) are NOT algorithmic; they
 # show up in the PMC `traffic` figure instead.  Step total: 424 B.
-ALGO_BYTES = {"k_tonegen": 0, "k_rv_pre": 32, "k_rv_core": 384, "k_rv_post": 0, "k_whirl": 8}
+ALGO_BYTES = {"k_tonegen": 0, "k_mixpre": 0, "k_rv_pre": 32, "k_rv_core": 384, "k_rv_post": 0, "k_whirl": 8}
 DOMINANT = "k_rv_core"  # the HBM-streaming kernel the roofline is quoted for
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # MI355X_MICROARCH.md, LDS/L2 gather table: rows shared by every workgroup of an XCD come
@@ -399,8 +399,8 @@ def main():
     if rank == 0:
         samples_launch = B * min(a.blocks, CHUNK) * 128  # stereo samples one launch of a stage renders
         algo = dict(ALGO_BYTES)
-        if a.chain == 1:  # tonegen only: k_tonegen writes L and R (8 B); bank reads are L2-resident
-            algo["k_tonegen"] = 8
+        if a.chain == 1:  # tonegen only: k_mixpre writes L and R (8 B); bank reads are L2-resident
+            algo["k_mixpre"] = 8
         roof = None
         if kern:
             dom = DOMINANT if DOMINANT in kern else max(kern, key=kern.get)

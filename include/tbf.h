@@ -249,6 +249,10 @@ int tbf_debug_host_time (tbf_engine* e, int32_t reset, double* ms, uint64_t* blo
 /* the cfg-derived HBM layout: the compact whirl ring window (512 / 1024 / 2048 samples
  * per ring, from the geometry's largest write-ahead) and the reverb slab length */
 int tbf_debug_layout (const tbf_engine* e, uint32_t* wring_len, float* max_ahead, uint32_t* slab_len);
+/* test hook: set the reverb vibrato phase of line 0..7 of channel ch (b_reverb vib[ch][line],
+ * src/reverb.cpp:479-496) of an instance, effective from the next block; parity tests use
+ * it to place a phase just below a power of two (a binade crossing inside a launch) */
+int tbf_debug_reverb_phase (tbf_engine* e, uint32_t inst, int32_t ch, int32_t line, double value);
 /* envelopes (9 x 128 each) and key-compression table (128) of a template */
 int tbf_debug_tables (tbf_engine* e, uint32_t tpl_id, float* attack, float* release, float* keycomp);
 /* run one block of the tonegen control plane for an instance and return the core
@@ -273,9 +277,9 @@ int tbf_debug_exact (int32_t op, const double* in3, double* out2, uint32_t n);
 /* per-stage kernel timing with HIP events on each launch's stream: enable 1 / -1 turns
  * recording on / off (1: as rendered, launches of neighbouring chunks overlapping; 2:
  * with the cross-chunk pipelining off, each kernel alone on the GPU); 0 returns the
- * summed milliseconds and launch counts of the five stage kernels k_tonegen, k_rv_pre,
- * k_rv_core, k_rv_post, k_whirl since the last query (ms5[5], count5[5]) */
-int tbf_debug_kernel_times (tbf_engine* e, int32_t enable, double* ms5, uint32_t* count5);
+ * summed milliseconds and launch counts of the six stage kernels k_tonegen, k_mixpre,
+ * k_rv_pre, k_rv_core, k_rv_post, k_whirl since the last query (ms6[6], count6[6]) */
+int tbf_debug_kernel_times (tbf_engine* e, int32_t enable, double* ms6, uint32_t* count6);
 /* PMC calibration: op 0 streams n doubles from d_buf (8 B/lane reads, the reverb ring
  * pattern), op 1 writes them; enqueued on `stream` (NULL = legacy default stream) */
 int tbf_debug_calibrate (int32_t op, void* d_buf, uint64_t n_doubles, void* stream);

@@ -191,6 +191,8 @@ void orc_render (orc_inst* p, int nblocks, float* L, float* R, float* sA, float*
 /* the core program of the last orc_render block: 9 floats per instruction
  * {wheel, opr, envRow, sg, pg, vg, nsg, npg, nvg} (wrap-split halves included) */
 int           orc_debug_program (const orc_inst* p, float* out9, int cap);
+/* test hook: set the reverb vibrato phase vib[c][l] (lines 0..7) */
+void          orc_debug_rv_phase (orc_inst* p, int c, int l, double value);
 
 /* parameter ids (src/clap.cpp:31-48) */
 #define ORC_P_DRAWBAR_MIN 0

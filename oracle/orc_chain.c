@@ -173,6 +173,12 @@ void orc_render (orc_inst* p, int nblocks, float* L, float* R, float* sA, float*
 	}
 }
 
+/* test hook: the reverb vibrato phase vib[c][l] (tbf_debug_reverb_phase's counterpart) */
+void orc_debug_rv_phase (orc_inst* p, int c, int l, double value)
+{
+	p->rev->vib[c][l] = value;
+}
+
 int orc_debug_program (const orc_inst* p, float* out, int cap)
 {
 	int i;

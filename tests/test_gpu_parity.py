@@ -800,6 +800,53 @@ def test_gpu_reverb_network_group_boundaries(oracle):
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
+def test_gpu_reverb_phase_binade_crossing(oracle):
+    """A reverb vibrato phase that crosses a binade inside a launch (phases placed just
+    below powers of two, both signs) makes k_rv_core_lds walk that group sub-block by
+    sub-block; a sub-block after the crossing is closed-form with its new step and rows
+    computed inline, exactly as k_rv_core does it.  So the LDS network kernel (one 64-block
+    call, or 23 + 41), the streaming kernel (TBF_RV_LDS=0) and a 7 + 57 split (k_rv_core
+    for the first call) are bit-identical, and all match the oracle (literal sin)."""
+    import ctypes as C
+    import os
+    from orc_bind import Chain
+    n, nb = 4, 64
+    pokes = [(0, 0, 2.0 ** 20 - 0.5), (0, 3, -(2.0 ** 19) - 0.3), (1, 5, 2.0 ** 21 - 0.9), (1, 7, 2.0 ** 10 - 0.2)]
+    runs = []
+    for env, split in (({}, [64]), ({}, [23, 41]), ({}, [7, 57]), ({"TBF_RV_LDS": "0"}, [64])):
+        os.environ.update(env)
+        try:
+            eng, tpl, seeds, scens = _setup(oracle, n, S.bench_scenario)
+        finally:
+            for k in env:
+                os.environ.pop(k, None)
+        for i in range(n):
+            for (c, l, v) in pokes:
+                eng.debug_reverb_phase(i, c, l, v - 0.0131 * i)
+        parts = [engine_run(eng, scens, split[0])] + [eng.render(k) for k in split[1:]]
+        assert eng.error_flags() & 8, "no phase run left its closed form: the crossing was not exercised"
+        eng.close()
+        runs.append((np.concatenate([p[0] for p in parts], axis=1), np.concatenate([p[1] for p in parts], axis=1)))
+    fn = oracle.orc_debug_rv_phase
+    fn.restype, fn.argtypes = None, [C.c_void_p, C.c_int, C.c_int, C.c_double]
+    oL, oR = [], []
+    for i, (seed, sc) in enumerate(zip(seeds, scens)):
+        ch = Chain(oracle, tpl, seed)
+        for (c, l, v) in pokes:
+            fn(ch.ptr, c, l, v - 0.0131 * i)
+        L, R, *_ = S.run(ch, sc, nb, stages=True)
+        oL.append(L)
+        oR.append(R)
+    eL, xL = compare(runs[0][0], np.stack(oL))
+    eR, xR = compare(runs[0][1], np.stack(oR))
+    print(f"binade crossing: max|err| L={eL:.3g} R={eR:.3g} bit-exact L={xL:.6f} R={xR:.6f}")
+    assert max(eL, eR) <= TOL
+    for k, r in enumerate(runs[1:], 1):
+        same = all(np.array_equal(a.view(np.uint32), b.view(np.uint32)) for a, b in zip(runs[0], r))
+        print(f"variant {k}: bit-identical to the single LDS call: {same}")
+        assert same
+
+
 def test_gpu_full_size_bench_batch(oracle):
     """BASELINE configs[2] at its full size (4096 instances x 64 blocks, one call, the
     bench's render): instances spread over the whole batch (both ends and the middle of

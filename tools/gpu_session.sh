@@ -8,6 +8,9 @@
 #           traffic.json, the full-size kernel summary, then the default bench with traffic
 #   kpmc    per-kernel SQ counters (occupancy, waits, LDS activity and bank conflicts)
 #   cfg     secondary lines: configs[1] at 256 instances, configs[4] shape, dense events
+#   iso     the default bench with each kernel also timed alone (--isolated 1)
+#   bench   the default bench without the CPU leg
+#   ab:V=X  the default bench with environment switch V=X
 set -u
 TAG=${1:-dev}; shift || true
 STEPS=${*:-"tests full kpmc"}
@@ -51,6 +54,11 @@ for s in $STEPS; do
 		run dense 500 python3 -u tools/dense_events.py --out "$OUT/dense_events.json"
 		run rt 300 python3 -u tools/rt_latency.py --out "$OUT/rt_latency.json"
 		;;
+	iso) run iso 300 python3 bench.py --isolated 1 --cpu-baseline 0 ;;
+	bench) run bench 300 python3 bench.py --cpu-baseline 0 ;;
+	ab:*) # ab:VAR=VALUE -- the default bench with one environment switch (A/B)
+		kv=${s#ab:}
+		run "ab_${kv//[^A-Za-z0-9_]/_}" 300 env "$kv" python3 bench.py --cpu-baseline 0 ;;
 	*) echo "unknown step $s" ;;
 	esac
 done

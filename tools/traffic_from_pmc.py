@@ -13,7 +13,7 @@ from collections import defaultdict
 from pathlib import Path
 
 FETCH_SCALE, WRITE_SCALE = 2.0, 1.0
-KERNELS = ("k_tonegen", "k_rv_pre", "k_rv_core", "k_rv_post", "k_whirl")
+KERNELS = ("k_tonegen", "k_mixpre", "k_rv_pre", "k_rv_core", "k_rv_post", "k_whirl")
 
 
 def per_dispatch(d, counter):

@@ -69,7 +69,6 @@ int tbf::fail (int code, const std::string& msg)
 /* control pool region (one per chunk parity on the device-controlled path; the host path
  * uses region 0): n persistent entries + up to one delta per instance and block */
 #define CTL_REGION(n) ((size_t)(n) * (TBF_CHUNK + 1))
-#define TBF_NSTAGES 5 /* k_tonegen, k_rv_pre, k_rv_core, k_rv_post, k_whirl */
 
 /* ------------------------------------------------------------------ construction */
 
@@ -300,31 +299,12 @@ int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
 		 * stream); one created before shares the last stage group's, whose work the
 		 * caller's stream waits for anyway.  A stage group's queue shared with the
 		 * caller's stream would order the group's next launches behind the caller's
-		 * end-of-call wait (measured: steady step 6.7 -> 8.1 ms, TBF_CTL_STREAM below) */
+		 * end-of-call wait (measured with a fifth engine stream: steady step 6.7 -> 8.1 ms) */
 		HIPCHK (hipStreamCreateWithFlags (&e->stream, hipStreamNonBlocking));
-		/* TBF_STREAM_PRIO=k: the stream of stage group k (0..2) at the device's greatest
-		 * priority (A/B of which stage group the dispatcher should favour) */
-		const char* sp    = getenv ("TBF_STREAM_PRIO");
-		const int   spGrp = sp ? atoi (sp) : -1;
-		int         prLeast = 0, prGreatest = 0;
-		HIPCHK (hipDeviceGetStreamPriorityRange (&prLeast, &prGreatest));
-		for (int p = 0; p < 2; p++)
-			if (p == spGrp)
-				HIPCHK (hipStreamCreateWithPriority (&e->sstr[p], hipStreamNonBlocking, prGreatest));
-			else
-				HIPCHK (hipStreamCreateWithFlags (&e->sstr[p], hipStreamNonBlocking));
-		for (int k = 0; k < TBF_NSTAGES; k++)
-			HIPCHK (hipEventCreateWithFlags (&e->sdone[k], hipEventDisableTiming));
-		HIPCHK (hipEventCreateWithFlags (&e->sjoin, hipEventDisableTiming));
-		/* TBF_RV_LDS=0: the streaming reverb core (k_rv_core) instead of k_rv_core_lds */
-		if (const char* rl = getenv ("TBF_RV_LDS"))
-			e->rvLdsOn = rl[0] != '0';
-		if (const char* pm = getenv ("TBF_PIPE_MODE"))
-			e->pipeMode = atoi (pm) == 1 ? 1 : 0;
-		if (const char* pg = getenv ("TBF_PIPE_GROUPS")) { /* "g0,g1,g2,g3,g4", groups 0..4, non-decreasing */
+		if (const char* pg = getenv ("TBF_PIPE_GROUPS")) { /* "g0,...,g5": groups 0..5, non-decreasing, from 0 */
 			for (int k = 0; k < TBF_NSTAGES && *pg; k++) {
 				const int g = atoi (pg);
-				if (g >= 0 && g < TBF_NSTAGES && (k == 0 || g >= e->grp[k - 1]))
+				if (g >= 0 && g < TBF_NSTAGES && (k == 0 ? g == 0 : (g >= e->grp[k - 1] && g <= e->grp[k - 1] + 1)))
 					e->grp[k] = g;
 				while (*pg && *pg != ',')
 					pg++;
@@ -332,35 +312,25 @@ int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
 					pg++;
 			}
 		}
-		if (e->pipeMode == 1) {
-			if (spGrp == 2)
-				HIPCHK (hipStreamCreateWithPriority (&e->gstr3, hipStreamNonBlocking, prGreatest));
-			else
-				HIPCHK (hipStreamCreateWithFlags (&e->gstr3, hipStreamNonBlocking));
-			/* groups 3, 4 (more than three stage groups) */
-			for (int g = 3; g <= e->grp[TBF_NSTAGES - 1]; g++)
-				HIPCHK (hipStreamCreateWithFlags (&e->gstrM[g - 3], hipStreamNonBlocking));
-			/* TBF_CTL_STREAM=1: a delta chunk's uploads and k_tgctl on a stream of their own.
-			 * Off by default: the process has GPU_MAX_HW_QUEUES (4) hardware queues, streams
-			 * take them round-robin at creation, and a fifth engine stream pushes the caller's
-			 * stream onto the first stage group's queue, which serializes the stages (steady
-			 * bench 6.7 -> 8.1 ms per step); the dense-event step gained nothing from it */
-			const char* cs = getenv ("TBF_CTL_STREAM");
-			if (cs && cs[0] == '1')
-				HIPCHK (hipStreamCreateWithFlags (&e->cstr, hipStreamNonBlocking));
-			for (int p = 0; p < 6; p++)
-				for (int k = 0; k < TBF_NSTAGES; k++)
-					HIPCHK (hipEventCreateWithFlags (&e->pev[p][k], hipEventDisableTiming));
-			for (int k = 0; k < TBF_NSTAGES; k++)
-				HIPCHK (hipEventCreateWithFlags (&e->exEv[k], hipEventDisableTiming));
-			HIPCHK (hipEventCreateWithFlags (&e->coreEv, hipEventDisableTiming));
-			if (const char* rx = getenv ("TBF_RV_EXCL"))
-				e->rvExcl = atoi (rx);
-			/* TBF_STAGE_BUFS=3: a third stage-buffer set, so k_tonegen of chunk c waits for
-			 * chunk c - 3's readers of mid1 instead of chunk c - 2's */
-			const char* sb = getenv ("TBF_STAGE_BUFS");
-			e->nbuf        = (sb && atoi (sb) == 3) ? 3 : 2;
+		for (int g = 0; g <= e->grp[TBF_NSTAGES - 1]; g++)
+			HIPCHK (hipStreamCreateWithFlags (&e->gs[g], hipStreamNonBlocking));
+		for (int k = 0; k < TBF_NSTAGES; k++) {
+			HIPCHK (hipEventCreateWithFlags (&e->sdone[k], hipEventDisableTiming));
+			for (int p = 0; p < 4; p++)
+				HIPCHK (hipEventCreateWithFlags (&e->pev[p][k], hipEventDisableTiming));
 		}
+		HIPCHK (hipEventCreateWithFlags (&e->sjoin, hipEventDisableTiming));
+		/* TBF_RV_LDS=0: the streaming reverb core (k_rv_core) instead of k_rv_core_lds */
+		if (const char* rl = getenv ("TBF_RV_LDS"))
+			e->rvLdsOn = rl[0] != '0';
+		/* k_rv_core_lds runs one persistent workgroup per CU (TBF_RV_PERSIST=0: one per
+		 * instance and channel, the round-2 grid) */
+		int ncu = 0;
+		HIPCHK (hipDeviceGetAttribute (&ncu, hipDeviceAttributeMultiprocessorCount, cfg->device));
+		const char* rp = getenv ("TBF_RV_PERSIST");
+		e->rvGrid      = (rp && rp[0] == '0') ? 0u : (uint32_t)std::max (ncu, 1);
+		if (e->rvWork.ensure (1))
+			return fail (-12, "out of device memory");
 		HIPCHK (hipEventCreateWithFlags (&e->upEv, hipEventDisableTiming));
 		HIPCHK (hipEventCreateWithFlags (&e->upEvB, hipEventDisableTiming));
 		const char* pl = getenv ("TBF_PIPELINE");
@@ -371,22 +341,6 @@ int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
 		e->devCtl      = !(hc && hc[0] == '1');
 		const char* hs = getenv ("TBF_HOST_SERIAL"); /* the serial loop (A/B); TBF_HOST_THREADS: workers */
 		e->parCtl      = !(hs && hs[0] == '1');
-		/* TBF_PIPE_WAIT="w0,w1,...": stage k of a chunk also waits for stage w_k >= k of the
-		 * previous chunk (default w_k = k), which moves which stages of neighbouring chunks
-		 * co-run; any such table is exact (it only adds dependencies) */
-		for (int k = 0; k < TBF_NSTAGES; k++)
-			e->pipeWait[k] = k;
-		if (const char* pw = getenv ("TBF_PIPE_WAIT")) {
-			for (int k = 0; k < TBF_NSTAGES && *pw; k++) {
-				const int w = atoi (pw);
-				if (w >= k && w < TBF_NSTAGES)
-					e->pipeWait[k] = w;
-				while (*pw && *pw != ',')
-					pw++;
-				if (*pw == ',')
-					pw++;
-			}
-		}
 	}
 	if (int rc = buildShared (e.get ()))
 		return rc;
@@ -402,16 +356,9 @@ int tbf_engine_destroy (tbf_engine* e)
 		(void)hipSetDevice (e->cfg.device);
 	if (e->stream)
 		(void)hipStreamSynchronize (e->stream);
-	for (int p = 0; p < 2; p++)
-		if (e->sstr[p])
-			(void)hipStreamSynchronize (e->sstr[p]);
-	if (e->gstr3)
-		(void)hipStreamSynchronize (e->gstr3);
-	for (hipStream_t q : e->gstrM)
+	for (hipStream_t q : e->gs)
 		if (q)
 			(void)hipStreamSynchronize (q);
-	if (e->cstr)
-		(void)hipStreamSynchronize (e->cstr);
 	e->bank.release ();
 	e->tplDesc.release ();
 	e->cst.release ();
@@ -440,36 +387,26 @@ int tbf_engine_destroy (tbf_engine* e)
 	e->err.release ();
 	e->outL.release ();
 	e->outR.release ();
+	e->mid0.release ();
 	e->mid1.release ();
 	e->mid2.release ();
 	e->rvA.release ();
 	e->rvB.release ();
+	e->rvWork.release ();
 	if (e->stream)
 		(void)hipStreamDestroy (e->stream);
-	for (int p = 0; p < 2; p++)
-		if (e->sstr[p])
-			(void)hipStreamDestroy (e->sstr[p]);
-	if (e->gstr3)
-		(void)hipStreamDestroy (e->gstr3);
-	for (hipStream_t q : e->gstrM)
+	for (hipStream_t q : e->gs)
 		if (q)
 			(void)hipStreamDestroy (q);
-	if (e->cstr)
-		(void)hipStreamDestroy (e->cstr);
-	for (int p = 0; p < 6; p++)
-		for (int k = 0; k < TBF_NSTAGES; k++)
-			if (e->pev[p][k])
-				(void)hipEventDestroy (e->pev[p][k]);
-	for (int k = 0; k < TBF_NSTAGES; k++)
+	for (int k = 0; k < TBF_NSTAGES; k++) {
 		if (e->sdone[k])
 			(void)hipEventDestroy (e->sdone[k]);
+		for (int p = 0; p < 4; p++)
+			if (e->pev[p][k])
+				(void)hipEventDestroy (e->pev[p][k]);
+	}
 	if (e->sjoin)
 		(void)hipEventDestroy (e->sjoin);
-	for (hipEvent_t& x : e->exEv)
-		if (x)
-			(void)hipEventDestroy (x);
-	if (e->coreEv)
-		(void)hipEventDestroy (e->coreEv);
 	for (hipEvent_t ev : {e->upEv, e->upEvB})
 		if (ev)
 			(void)hipEventDestroy (ev);
@@ -656,8 +593,8 @@ int tbf_instances_add (tbf_engine* e, uint32_t n, const uint32_t* tpl_ids, const
 		f          = 1;
 		while (f < 16386)
 			f = (uint32_t)rnd.next () * 0xFFFFFFFFu;
-		in.s0.tg.odFpd  = f;
-		in.s0.tg.fpFlip = 1;
+		in.s0.mo.odFpd  = f;
+		in.s0.mo.fpFlip = 1;
 		in.s0.rv.pdAge = 0; /* countM = 1 and zeroed rings: the first delayM outputs are 0 */
 		in.s0.rv.pdPos = 0;
 		for (int c = 0; c < 2; c++)
@@ -682,8 +619,8 @@ int tbf_instances_add (tbf_engine* e, uint32_t n, const uint32_t* tpl_ids, const
 		w.hornAcDc       = w.hornIncr < w.hornTarget ? 1 : (w.hornTarget < w.hornIncr ? -1 : 0);
 		w.drumAcDc       = w.drumIncr < w.drumTarget ? 1 : (w.drumTarget < w.drumIncr ? -1 : 0);
 		/* tonegen + vibrato runtime state (initToneGenerator, reset_vibrato) */
-		in.s0.tg.keyCompLevel = 1.0f;
-		in.s0.tg.percEnvGain  = 0.0f;
+		in.s0.mo.keyCompLevel = 1.0f;
+		in.s0.mo.percEnvGain  = 0.0f;
 		in.s0.tg.outPos       = 1023 / 2;
 		in.tg.init (e->tpls[in.tpl].get (), e->conf);
 		if (e->slabLen == 0) {
@@ -722,11 +659,12 @@ int tbf_instance_retune (tbf_engine* e, uint32_t i, uint32_t tpl_id)
 	in.tg.newRouting = newRouting;
 	/* the device side: the instance's tone-generator + scanner state (wheel positions, key
 	 * compression, percussion envelope and high-pass, stator, scanner ring) starts fresh
-	 * at the next block; the preamp fields of tbf_tg_state, reverb and whirl go on */
+	 * at the next block; the preamp fields of tbf_mo_state, reverb and whirl go on */
 	tbf_tg_state& g = in.s0.tg;
-	memset (&g, 0, offsetof (tbf_tg_state, iirA));
-	g.keyCompLevel = 1.0f;
-	g.outPos       = 1023 / 2;
+	memset (&g, 0, sizeof (g));
+	g.outPos                = 1023 / 2;
+	in.s0.mo.keyCompLevel = 1.0f;
+	in.s0.mo.percEnvGain  = 0.0f;
 	if (std::find (e->retuned.begin (), e->retuned.end (), i) == e->retuned.end ())
 		e->retuned.push_back (i);
 	in.progDirty = in.ctlDirty = true;
@@ -887,15 +825,9 @@ static int drainStages (tbf_engine* e)
 {
 	if (!e->stagesBusy)
 		return 0;
-	for (int p = 0; p < 2; p++)
-		HIPCHK (hipStreamSynchronize (e->sstr[p]));
-	if (e->gstr3)
-		HIPCHK (hipStreamSynchronize (e->gstr3));
-	for (hipStream_t q : e->gstrM)
+	for (hipStream_t q : e->gs)
 		if (q)
 			HIPCHK (hipStreamSynchronize (q));
-	if (e->cstr)
-		HIPCHK (hipStreamSynchronize (e->cstr));
 	e->stagesBusy = false;
 	return 0;
 }
@@ -905,8 +837,7 @@ static int joinStages (tbf_engine* e, hipStream_t s)
 {
 	if (!e->stagesBusy)
 		return 0;
-	for (int p = 0; p < 6; p++) {
-		hipStream_t q = p < 2 ? e->sstr[p] : p == 2 ? e->gstr3 : p == 3 ? e->cstr : e->gstrM[p - 4];
+	for (hipStream_t q : e->gs) {
 		if (!q)
 			continue;
 		HIPCHK (hipEventRecord (e->sjoin, q));
@@ -1357,7 +1288,9 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		if ((rc = joinStages (e, s)))
 			return rc;
 		for (uint32_t i : e->retuned) {
-			HIPCHK (hipMemcpyAsync (&e->st.p[i].tg, &e->inst[i].s0.tg, offsetof (tbf_tg_state, iirA),
+			HIPCHK (hipMemcpyAsync (&e->st.p[i].mo, &e->inst[i].s0.mo, offsetof (tbf_mo_state, iirA),
+			                        hipMemcpyHostToDevice, s));
+			HIPCHK (hipMemcpyAsync (&e->st.p[i].tg, &e->inst[i].s0.tg, sizeof (tbf_tg_state),
 			                        hipMemcpyHostToDevice, s));
 			HIPCHK (hipMemcpyAsync (&e->cst.p[i].tpl, &e->inst[i].k.tpl, sizeof (uint32_t), hipMemcpyHostToDevice, s));
 			if (e->devCtl) { /* a fresh per-wheel control state and an empty program */
@@ -1404,27 +1337,26 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 	P.errFlags  = e->err.p;
 	P.dbg       = e->cfg.debug_flags;
 	P.rvLds     = e->rvLdsOn && e->rvLdsFit;
-	/* inter-stage buffers: nbuf sets by chunk index (2: alternate chunks; 3 with the
-	 * stage-group streams), see the pipelining below */
-	const size_t   need = (size_t)n * TBF_CHUNK * TBF_BLK;
-	const uint32_t nbuf = e->nbuf;
-	if (e->cfg.chain_mode != TBF_CHAIN_TONEGEN) {
-		if (e->mid1.ensure (nbuf * need) || e->mid2.ensure (nbuf * need))
+	P.rvGrid    = e->rvGrid;
+	P.rvWork    = e->rvWork.p;
+	/* inter-stage buffers: two sets, by chunk parity (see the pipelining below) */
+	const size_t need = (size_t)n * TBF_CHUNK * TBF_BLK;
+	if (e->mid0.ensure (2 * 2 * need))
+		return fail (-12, "out of device memory (stage buffers)");
+	if (e->cfg.chain_mode != TBF_CHAIN_TONEGEN && e->cfg.chain_mode != TBF_CHAIN_TAP_PREAMP) {
+		if (e->mid1.ensure (2 * need) || e->mid2.ensure (2 * need))
 			return fail (-12, "out of device memory (stage buffers)");
-		if (e->cfg.chain_mode != TBF_CHAIN_TAP_PREAMP &&
-		    (e->rvA.ensure (2 * nbuf * need) || e->rvB.ensure (2 * nbuf * need)))
+		if (e->rvA.ensure (2 * 2 * need) || e->rvB.ensure (2 * 2 * need))
 			return fail (-12, "out of device memory (reverb stage buffers)");
 	}
 	P.midStride = (uint64_t)TBF_CHUNK * TBF_BLK;
 	/* Cross-chunk pipelining.  Every stage is causal and keeps its own state, so stage k
-	 * of chunk c depends only on stage k-1 of chunk c (same stream sstr[c % 2]) and on
-	 * stage k of chunk c-1 (event sdone[k], the other stream); its output buffer parity
-	 * c % 2 was last read by chunk c-2 on the same stream.  The kernels of neighbouring
-	 * chunks (and of consecutive render calls) then fill each other's tails on the GPU.
-	 * Used for the full chain on chunks without control uploads; uploads and tap modes
-	 * run on the caller's stream after joining.  With
-	 * tbf_debug_kernel_times on, each launch is bracketed by events on its own stream
-	 * (durations then include the overlap with the other stream's kernels). */
+	 * of chunk c depends only on stage k-1 of chunk c and on stage k of chunk c-1, which
+	 * runs on the same stage-group stream; the stage buffers alternate by chunk parity.
+	 * Used for the full chain; tap modes and a host-control chunk's uploads run on the
+	 * caller's stream after joining.  With tbf_debug_kernel_times on, each launch is
+	 * bracketed by events on its own stream (durations then include the overlap with the
+	 * other streams' kernels). */
 	const bool   pipe  = e->pipeline && e->cfg.chain_mode == TBF_CHAIN_FULL && !e->timeSerial;
 	bool         outWait = false; /* the output stage has waited for the caller's stream */
 	const size_t dprogCap = DPROG_CAP (n);
@@ -1466,16 +1398,13 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		const uint32_t want = std::min<uint32_t> (TBF_CHUNK, nblocks - b0);
 		const uint64_t cix  = e->chunkSeq++;
 		const bool     par  = (cix & 1) != 0;
-		const uint32_t bset = (uint32_t)(cix % nbuf); /* stage-buffer set of this chunk */
+		const uint32_t bset = (uint32_t)(cix & 1); /* stage-buffer set of this chunk */
 		const int      rp   = e->devCtl ? (int)par : 0; /* control region of this chunk */
 		/* device control, stage-group pipelining: a delta chunk pipelines like any other; its
-		 * uploads and k_tgctl go on the first stage group's stream (or the control stream
-		 * cstr, TBF_CTL_STREAM=1, where they overlap the previous chunk's k_tonegen: three
-		 * persistent program slots make that exact, and the chunk's first stage waits for
-		 * them, upEv) after the chunk before last (the previous user of this region) has
-		 * finished every stage */
-		const bool     dpipe = e->devCtl && pipe && e->pipeMode == 1;
-		hipStream_t    us    = dpipe ? (e->cstr ? e->cstr : e->sstr[e->grp[0] < 2 ? e->grp[0] : 0]) : s;
+		 * uploads and k_tgctl go on the first stage group's stream after the chunk before
+		 * last (the previous user of this control region) has finished every stage */
+		const bool     dpipe = e->devCtl && pipe;
+		hipStream_t    us    = dpipe ? e->gs[0] : s;
 		bool           usWaited = false;
 		auto           usWait   = [&] () -> int {
             if (usWaited || !dpipe)
@@ -1485,7 +1414,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
                 HIPCHK (hipEventRecord (e->sjoin, s));
                 HIPCHK (hipStreamWaitEvent (us, e->sjoin, 0));
             }
-            HIPCHK (hipStreamWaitEvent (us, e->pev[(cix + 4) % 6][tbf_chain_stages (P.chain) - 1], 0));
+            HIPCHK (hipStreamWaitEvent (us, e->pev[(cix + 2) & 3][tbf_chain_stages (P.chain) - 1], 0));
             return 0;
 		};
 		if (e->devCtl && e->persistStale) {
@@ -1634,6 +1563,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		                    .count ();
 		e->hostCtlBlocks += len;
 		const bool     piped   = pipe && (!delta || dpipe);
+		P.mid0 = e->mid0.p + 2 * bset * need;
 		P.mid1 = e->mid1.p ? e->mid1.p + bset * need : nullptr;
 		P.mid2 = e->mid2.p ? e->mid2.p + bset * need : nullptr;
 		P.rvA  = e->rvA.p ? e->rvA.p + 2 * bset * need : nullptr;
@@ -1726,23 +1656,21 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		if (usWaited && piped) /* the stage streams now follow the uploads on us */
 			e->stagesBusy = true;
 		const int nst = tbf_chain_stages (P.chain);
-		if (piped && e->pipeMode == 1) {
-			/* stage-group streams: every chunk's stage k on stream grp[k], so a stage runs as
-			 * soon as this chunk's previous stage and the previous chunk's same stage are
+		if (piped) {
+			/* stage-group streams: every chunk's stage k on stream gs[grp[k]], so a stage runs
+			 * as soon as this chunk's previous stage and the previous chunk's same stage are
 			 * done, whatever the later stages of the previous chunk are doing.  Buffer parity
 			 * par was last read by the chunk before last: wait for those readers (stage k's
-			 * output mid1 is read by k_rv_pre and k_rv_post, rvA by k_rv_core, rvB by k_rv_post,
-			 * mid2 by k_whirl) when they run on another stream. */
-			static const int readers[5][2] = {{1, 3}, {2, -1}, {3, -1}, {4, -1}, {-1, -1}};
-			auto strm = [&] (int k) { const int g = e->grp[k]; return g < 2 ? e->sstr[g] : g == 2 ? e->gstr3 : e->gstrM[g - 3]; };
+			 * output mid0 is read by k_mixpre, mid1 by k_rv_pre and k_rv_post, rvA by
+			 * k_rv_core, rvB by k_rv_post, mid2 by k_whirl) when they run on another stream. */
+			static const int readers[TBF_NSTAGES][2] = {{1, -1}, {2, 4}, {3, -1}, {4, -1}, {5, -1}, {-1, -1}};
+			auto strm = [&] (int k) { return e->gs[e->grp[k]]; };
 			for (int k = 0; k < nst; k++) {
 				hipStream_t sk = strm (k);
 				if (k == 0 && !e->stagesBusy) { /* after the caller's stream (uploads, earlier chunks) */
 					HIPCHK (hipEventRecord (e->sjoin, s));
 					HIPCHK (hipStreamWaitEvent (sk, e->sjoin, 0));
 				}
-				if (k == 0 && usWaited && e->cstr) /* this chunk's control uploads and k_tgctl */
-					HIPCHK (hipStreamWaitEvent (sk, e->upEv, 0));
 				if (k == nst - 1 && !outWait) { /* the output stage writes the caller's buffers */
 					HIPCHK (hipEventRecord (e->sjoin, s));
 					HIPCHK (hipStreamWaitEvent (sk, e->sjoin, 0));
@@ -1750,20 +1678,9 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 				}
 				if (k > 0 && strm (k - 1) != sk)
 					HIPCHK (hipStreamWaitEvent (sk, e->sdone[k - 1], 0));
-				const int excl = (e->rvExcl && P.rvLds && nst > 2) ? e->rvExcl : 0;
-				if (excl && k == 0 && e->coreRec) /* after the last chunk's k_rv_core_lds */
-					HIPCHK (hipStreamWaitEvent (sk, e->coreEv, 0));
-				if (excl == 1 && k == 2) /* k_rv_core_lds alone: after every other stage stream's work */
-					for (int q = 0; q < nst; q++)
-						if (strm (q) != sk) {
-							HIPCHK (hipEventRecord (e->exEv[q], strm (q)));
-							HIPCHK (hipStreamWaitEvent (sk, e->exEv[q], 0));
-						}
-				if (excl == 2 && k == 2) /* ... beside the previous chunk's k_whirl only */
-					HIPCHK (hipStreamWaitEvent (sk, e->sdone[3], 0));
 				for (int r : readers[k])
 					if (r >= 0 && r < nst && strm (r) != sk)
-						HIPCHK (hipStreamWaitEvent (sk, e->pev[(cix + 6 - nbuf) % 6][r], 0));
+						HIPCHK (hipStreamWaitEvent (sk, e->pev[(cix + 2) & 3][r], 0));
 				hipEvent_t e0 = nullptr, e1 = nullptr;
 				if (e->timeOn) {
 					HIPCHK (hipEventCreate (&e0));
@@ -1778,51 +1695,11 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 					e->tev.push_back ({k, {e0, e1}});
 				}
 				HIPCHK (hipEventRecord (e->sdone[k], sk));
-				HIPCHK (hipEventRecord (e->pev[cix % 6][k], sk));
-				if (excl && k == 2) {
-					HIPCHK (hipEventRecord (e->coreEv, sk));
-					e->coreRec = true;
-				}
+				HIPCHK (hipEventRecord (e->pev[cix & 3][k], sk));
 			}
 			e->stagesBusy = true;
 			if (delta && (rc = endDelta ()))
 				return rc;
-			b0 += len;
-			continue;
-		}
-		if (piped) {
-			hipStream_t sp = e->sstr[par];
-			if (!e->stagesBusy) {
-				/* from the caller's stream (uploads, earlier serialized chunks) */
-				HIPCHK (hipEventRecord (e->sjoin, s));
-				HIPCHK (hipStreamWaitEvent (sp, e->sjoin, 0));
-				outWait = true;
-			}
-			e->stagesBusy = true;
-			for (int k = 0; k < nst; k++) {
-				if (k == nst - 1 && !outWait) {
-					/* the output stage writes the caller's buffers: after the caller's work */
-					HIPCHK (hipEventRecord (e->sjoin, s));
-					HIPCHK (hipStreamWaitEvent (sp, e->sjoin, 0));
-					outWait = true;
-				}
-				/* stage k of the previous chunk (or a later one of it, TBF_PIPE_WAIT) */
-				HIPCHK (hipStreamWaitEvent (sp, e->sdone[std::min (e->pipeWait[k], nst - 1)], 0));
-				hipEvent_t e0 = nullptr, e1 = nullptr;
-				if (e->timeOn) { /* launch duration on the launch stream, dependencies met */
-					HIPCHK (hipEventCreate (&e0));
-					HIPCHK (hipEventCreate (&e1));
-					HIPCHK (hipEventRecord (e0, sp));
-				}
-				rc = tbf_launch_stage (&P, k, sp);
-				if (rc)
-					return fail (rc, std::string ("kernel launch failed: ") + hipGetErrorString (hipGetLastError ()));
-				if (e->timeOn) {
-					HIPCHK (hipEventRecord (e1, sp));
-					e->tev.push_back ({k, {e0, e1}});
-				}
-				HIPCHK (hipEventRecord (e->sdone[k], sp));
-			}
 			b0 += len;
 			continue;
 		}
@@ -2046,6 +1923,21 @@ int tbf_debug_layout (const tbf_engine* e, uint32_t* wring_len, float* max_ahead
 	return 0;
 }
 
+int tbf_debug_reverb_phase (tbf_engine* e, uint32_t i, int32_t ch, int32_t line, double value)
+{
+	if (!e || i >= e->inst.size () || ch < 0 || ch > 1 || line < 0 || line > 7)
+		return fail (-22, "bad arguments");
+	e->inst[i].s0.rv.ch[ch].vib[line] = value; /* an instance not on the device yet takes it at upload */
+	if (e->deviceReady && i < e->devInst) {
+		HIPCHK (hipSetDevice (e->cfg.device));
+		if (int rc = drainStages (e))
+			return rc;
+		HIPCHK (hipStreamSynchronize (e->stream));
+		HIPCHK (hipMemcpy (&e->st.p[i].rv.ch[ch].vib[line], &value, sizeof (double), hipMemcpyHostToDevice));
+	}
+	return 0;
+}
+
 int tbf_debug_step (tbf_engine* e, uint32_t i, float* out, uint32_t cap)
 {
 	if (!e || i >= e->inst.size ())
@@ -2172,7 +2064,7 @@ int tbf_debug_calibrate (int32_t op, void* buf, uint64_t n, void* stream)
 	return rc ? fail (rc, "calibration launch failed") : 0;
 }
 
-int tbf_debug_kernel_times (tbf_engine* e, int32_t enable, double* ms3, uint32_t* count3)
+int tbf_debug_kernel_times (tbf_engine* e, int32_t enable, double* ms6, uint32_t* count6)
 {
 	if (!e)
 		return fail (-22, "null engine");
@@ -2196,8 +2088,8 @@ int tbf_debug_kernel_times (tbf_engine* e, int32_t enable, double* ms3, uint32_t
 	}
 	e->tev.clear ();
 	for (int k = 0; k < TBF_NSTAGES; k++) {
-		if (ms3) ms3[k] = ms[k];
-		if (count3) count3[k] = cnt[k];
+		if (ms6) ms6[k] = ms[k];
+		if (count6) count6[k] = cnt[k];
 	}
 	return 0;
 }

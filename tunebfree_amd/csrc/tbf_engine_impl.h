@@ -164,6 +164,8 @@ struct DevBuf {
 
 using namespace tbf; /* private header: the engine's own translation units only */
 
+#define TBF_NSTAGES 6 /* k_tonegen, k_mixpre, k_rv_pre, k_rv_core, k_rv_post, k_whirl */
+
 struct tbf_engine {
 	tbf_engine_config                       cfg;
 	Config                                  conf; /* cfg keys (tbf_config_set) for tables built from now on */
@@ -247,7 +249,7 @@ struct tbf_engine {
 	bool                                    timeSerial = false; /* time with pipelining off */
 	std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> tev;
 	DevBuf<float>                           outL, outR;
-	DevBuf<float>                           mid1, mid2; /* inter-stage blocks of one launch chunk */
+	DevBuf<float>                           mid0, mid1, mid2; /* inter-stage blocks of one launch chunk */
 	DevBuf<double>                          rvA, rvB;   /* reverb inter-kernel streams (FP64) */
 	std::vector<tbf_seg_ctl>                hCtl;  /* current control per instance (pool entries 0..n-1) */
 	std::vector<tbf_prog_entry>             hProg; /* current program per instance (slots i * PROG_CAP) */
@@ -264,41 +266,25 @@ struct tbf_engine {
 	std::vector<uint32_t>                   curIdx;  /* pool entry per instance, current block */
 	DevBuf<uint32_t>                        ctlIdx;
 	bool                                    persistStale = true; /* device pool entries 0..n-1 need upload */
-	/* cross-chunk pipelining (renderImpl): the stages of chunk c run in order on stream
-	 * sstr[c % 2]; stage k of chunk c waits for stage k of chunk c-1 (event sdone[k])
-	 * on the other stream, so the two streams overlap neighbouring chunks' kernels (and
-	 * consecutive render calls'); inter-stage buffers alternate with the same parity, so
-	 * their reuse is ordered by the stream itself.  Two streams, not one per stage: the
-	 * device exposes few hardware queues per process and streams sharing one serialize */
-	hipStream_t                             sstr[2] = {};
-	hipEvent_t                              sdone[5] = {};
+	/* cross-chunk pipelining (renderImpl): stage k of every chunk runs on the stream of its
+	 * stage group grp[k] (so the stage's own state is ordered by its stream), the stages of
+	 * one chunk are chained by events, and a stage that overwrites a stage buffer of parity
+	 * c % 2 waits for chunk c - 2's readers of it on other streams.  A stage therefore starts
+	 * as soon as its inputs are ready, whatever the later stages of earlier chunks do.
+	 * Three groups: the device exposes few hardware queues per process (GPU_MAX_HW_QUEUES 4)
+	 * and streams sharing one serialize. */
+	hipStream_t                             gs[TBF_NSTAGES] = {};     /* groups 0 .. grp[TBF_NSTAGES - 1] */
+	hipEvent_t                              sdone[TBF_NSTAGES] = {};  /* the last launched chunk's stage k */
+	hipEvent_t                              pev[4][TBF_NSTAGES] = {}; /* chunk c's stage k, ring by c mod 4 */
 	hipEvent_t                              sjoin = nullptr;
 	uint64_t                                chunkSeq = 0;
 	bool                                    stagesBusy = false; /* pipelined work may be outstanding */
 	bool                                    pipeline = true;    /* TBF_PIPELINE=0 disables */
-	int                                     pipeWait[5] = {0, 1, 2, 3, 4}; /* stage k of a chunk waits for stage pipeWait[k] >= k of the previous one */
-	/* pipeMode 1 (default): streams by stage group (stage k of every chunk on stream
-	 * grp[k]; the stages of one chunk chained by events; a stage waits for the
-	 * chunk-before-last's readers of the buffer parity it overwrites).  TBF_PIPE_MODE=0:
-	 * streams by chunk parity (round 1) */
-	int                                     pipeMode = 1;
-	int                                     grp[5]   = {0, 1, 1, 2, 2};
-	bool                                    rvLdsOn  = true; /* k_rv_core_lds when the rings fit (TBF_RV_LDS=0: k_rv_core) */
+	int                                     grp[TBF_NSTAGES] = {0, 0, 1, 1, 2, 2}; /* TBF_PIPE_GROUPS */
+	bool                                    rvLdsOn  = true;  /* k_rv_core_lds when the rings fit (TBF_RV_LDS=0: k_rv_core) */
 	bool                                    rvLdsFit = false; /* the instances' rings fit k_rv_core_lds */
-	hipStream_t                             gstr3    = nullptr; /* the third group's stream (groups 0, 1 use sstr) */
-	hipStream_t                             gstrM[2] = {};      /* groups 3, 4 (TBF_PIPE_GROUPS with more than three) */
-	hipStream_t                             cstr     = nullptr; /* device control: uploads + k_tgctl */
-	/* stage-group pipelining: each chunk's stage-k event, in a ring by chunk index (a chunk
-	 * waits on chunk c - nbuf's readers of the stage buffers it overwrites and on chunk
-	 * c - 2's last stage for its control region); nbuf stage-buffer sets by chunk index */
-	hipEvent_t                              pev[6][5] = {};
-	/* TBF_RV_EXCL: k_rv_core_lds (a whole CU's LDS per workgroup) runs alone: it waits for
-	 * every other stage stream (exEv) and the next chunk's first stage waits for it (coreEv) */
-	int                                     rvExcl    = 0; /* 1: alone, 2: beside k_whirl only (A/B; 0 measured best) */
-	bool                                    coreRec   = false; /* coreEv recorded at least once */
-	hipEvent_t                              exEv[5]   = {};
-	hipEvent_t                              coreEv    = nullptr;
-	uint32_t                                nbuf      = 2;
+	uint32_t                                rvGrid   = 0;     /* k_rv_core_lds persistent workgroups (TBF_RV_PERSIST=0: one per pair) */
+	DevBuf<uint32_t>                        rvWork;           /* its work counter */
 	/* programme table (.pgm), src/program.h:26 MAXPROGS; pgm.controller.offset */
 	std::vector<Programme>                  progs = std::vector<Programme> (129);
 	int                                     pgmOffset = 1;

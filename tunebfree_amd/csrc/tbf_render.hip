@@ -44,8 +44,6 @@
 /* ------------------------------------------------------------------ LDS layouts */
 struct TgLds {
 	tbf_tg_state st;
-	float        bufA[TBF_BLK];
-	float        bufB[TBF_BLK];
 	float        swl[TBF_BLK];
 	float        vin[TBF_BLK];
 	float        prc[TBF_BLK];
@@ -54,19 +52,12 @@ struct TgLds {
 			uint32_t base[TBF_NW + 8]; /* bank index of the wheel's current sample (the device
 			                            * bank repeats each wave's first 128 samples after it) */
 		} ent;
-		struct { /* vibrato + mixdown */
+		struct { /* vibrato */
 			float   vout[TBF_BLK];
 			float   va[TBF_BLK];
 			float   vg[TBF_BLK];
 			int32_t vh[TBF_BLK];
-			float   pe[TBF_BLK];
-			float   kc[TBF_BLK];
 		} v;
-		struct { /* overdrive */
-			double   odx[TBF_BLK];
-			double   odh[TBF_BLK];
-			uint32_t fpd[TBF_BLK + 1];
-		} od;
 	} u;
 };
 
@@ -220,7 +211,8 @@ __device__ __forceinline__ float eq_iir (float c0, float c1, float c2, float c3,
 /* ================================================================== k_tonegen */
 
 /* oscGenerateFragment core interpreter + vibratoProc + mixdown, src/tonegen.cpp:3607-3777 */
-__device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl& G, const tbf_tpl_desc* T)
+__device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl& G, const tbf_tpl_desc* T,
+                              float2* __restrict__ out)
 {
 	const int             lane = threadIdx.x;
 	tbf_tg_state&         st   = sm.st;
@@ -369,142 +361,20 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 		}
 	}
 
-	/* mixdown, src/tonegen.cpp:3712-3777: the two per-sample gain chases run as
-	 * independent chains, lane 0 keyCompLevel += delta, lane 1 percEnvGain *= decay */
-	PRIO_UP ();
-	if (lane < 2) {
-		const float keyCompDelta = (G.keyCompTarget - st.keyCompLevel) / (float)TBF_BLK;
-		const bool  perc         = (routing & 0x0C) != 0;
-		const float dec          = G.percEnvGainDecay;
-		float       v            = lane == 0 ? st.keyCompLevel : st.percEnvGain;
-		float*      out          = lane == 0 ? sm.u.v.kc : sm.u.v.pe;
-		for (int i0 = 0; i0 < TBF_BLK; i0 += 8) {
-			float o[8];
-#pragma unroll
-			for (int k = 0; k < 8; k++) {
-				o[k]           = v;
-				const float va = v + keyCompDelta;
-				const float vm = perc ? v * dec : v;
-				v              = lane == 0 ? va : vm;
-			}
-#pragma unroll
-			for (int k = 0; k < 8; k++)
-				out[i0 + k] = o[k];
-		}
-		if (lane == 0)
-			st.keyCompLevel = v;
-		else
-			st.percEnvGain = G.resetPercAtEnd ? G.percEnvGainReset : v;
-	}
-	PRIO_DOWN ();
-	__syncthreads ();
+	/* the mixdown's per-sample terms (src/tonegen.cpp:3712-3777) without its two gain chases
+	 * (keyCompLevel += delta, percEnvGain *= decay), which k_mixpre runs with one chain per
+	 * lane: s = the swell bus, plus the scanner output when the vibrato is routed in; p =
+	 * HIPASS_PERCUSSION's first difference of the percussion bus (3719-3731) */
 	for (int k = 0; k < 2; k++) {
 		const int   n = lane + k * NL;
 		const float x = sm.swl[n];
-		float       y;
-		if (routing & 0x0C) {
-			/* HIPASS_PERCUSSION first difference, tonegen.cpp:3719-3731 */
-			const float p = (n == 0 ? st.pz : sm.prc[n - 1]) - sm.prc[n];
-			if (routing & 0x03)
-				y = (G.outputGain * sm.u.v.kc[n] * ((x + sm.u.v.vout[n]) + (p * sm.u.v.pe[n])));
-			else
-				y = (G.outputGain * sm.u.v.kc[n] * (x + (p * sm.u.v.pe[n])));
-		} else if (routing & 0x03) {
-			y = (G.swellPedalGain * sm.u.v.kc[n] * (x + sm.u.v.vout[n]));
-		} else {
-			y = (G.swellPedalGain * sm.u.v.kc[n] * x);
-		}
-		sm.bufA[n] = y;
+		const float s = (routing & 0x03) ? (x + sm.u.v.vout[n]) : x;
+		const float p = (routing & 0x0C) ? ((n == 0 ? st.pz : sm.prc[n - 1]) - sm.prc[n]) : 0.f;
+		out[n]        = make_float2 (s, p);
 	}
-	__syncthreads ();
+	__syncthreads (); /* every lane has read st.pz */
 	if (lane == 0 && (routing & 0x0C))
 		st.pz = sm.prc[TBF_BLK - 1];
-	__syncthreads ();
-}
-
-/* preamp / airwindows_density, src/overdrive.cpp:60-170 (FP64) */
-__device__ void stage_overdrive (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl& G)
-{
-	const int     lane = threadIdx.x;
-	tbf_tg_state& st   = sm.st;
-	if (G.odClean) {
-		sm.bufB[lane]      = sm.bufA[lane];
-		sm.bufB[lane + NL] = sm.bufA[lane + NL];
-		__syncthreads ();
-		return;
-	}
-	/* xorshift dither states F[0..128] (F[n+1] after sample n) by GF(2) jumps */
-	{
-		const uint32_t f0 = st.odFpd;
-		sm.u.od.fpd[lane + 1]      = xs_jump_n (P.xsJump, f0, lane + 1);
-		sm.u.od.fpd[lane + 1 + NL] = xs_jump_n (P.xsJump, f0, lane + 1 + NL);
-		__syncthreads (); /* all lanes have read st.odFpd */
-		if (lane == 0) {
-			sm.u.od.fpd[0] = f0;
-			st.odFpd       = sm.u.od.fpd[TBF_BLK];
-		}
-	}
-	__syncthreads ();
-	for (int k = 0; k < 2; k++) { /* denormal guard, dry copy */
-		const int n = lane + k * NL;
-		double    x = (double)sm.bufA[n];
-		if (fabs (x) < 1.18e-23)
-			x = sm.u.od.fpd[n] * 1.18e-17;
-		sm.u.od.odx[n] = x;
-	}
-	__syncthreads ();
-	PRIO_UP ();
-	if (lane < 2) {
-		/* alternating one-pole HPF (fpFlip): lane 0 carries iirSampleA over the samples it
-		 * owns, lane 1 iirSampleB over the others; 128 samples keep fpFlip unchanged */
-		const int    start = ((lane == 0) == (st.fpFlip != 0)) ? 0 : 1;
-		const double a     = G.odIir;
-		double       iir   = lane == 0 ? st.iirA : st.iirB;
-		for (int i0 = 0; i0 < TBF_BLK / 2; i0 += 8) {
-			double xv[8];
-#pragma unroll
-			for (int k = 0; k < 8; k++)
-				xv[k] = sm.u.od.odx[start + 2 * (i0 + k)];
-#pragma unroll
-			for (int k = 0; k < 8; k++) {
-				iir                                = (iir * (1.0 - a)) + (xv[k] * a);
-				sm.u.od.odh[start + 2 * (i0 + k)] = xv[k] - iir;
-			}
-		}
-		if (lane == 0)
-			st.iirA = iir;
-		else
-			st.iirB = iir;
-	}
-	PRIO_DOWN ();
-	__syncthreads ();
-	for (int k = 0; k < 2; k++) {
-		const int n   = lane + k * NL;
-		double    x   = sm.u.od.odh[n];
-		double    dry = sm.u.od.odx[n];
-		double    br;
-		for (int c = 0; c < G.odIter; c++) {
-			br = fabs (x) * 1.57079633;
-			if (br > 1.57079633)
-				br = 1.57079633;
-			br = sin (br);
-			x  = (x > 0.0) ? br : -br;
-		}
-		br = fabs (x) * 1.57079633;
-		if (br > 1.57079633)
-			br = 1.57079633;
-		br = G.odDensityPos ? sin (br) : 1 - cos (br);
-		if (x > 0)
-			x = (x * (1 - G.odOut)) + (br * G.odOut);
-		else
-			x = (x * (1 - G.odOut)) - (br * G.odOut);
-		if (G.odOutput < 1.0)
-			x *= G.odOutput;
-		if (G.odWet < 1.0)
-			x = (dry * G.odDry) + (x * G.odWet);
-		x = dither_add (x, sm.u.od.fpd[n + 1]);
-		sm.bufB[n] = (float)x;
-	}
 	__syncthreads ();
 }
 
@@ -513,37 +383,343 @@ k_tonegen (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl, const tbf_tp
            const tbf_inst_const* __restrict__ cst)
 {
 	__shared__ TgLds sm;
-	const int      lane = threadIdx.x;
 	const uint32_t inst = blockIdx.x + P.instBase;
 	if (inst >= P.nInst)
 		return;
 	const tbf_tpl_desc* T = tpls + cst[inst].tpl;
 	tbf_tg_state*       S = &P.st[inst].tg;
+	float2*             o = (float2*)P.mid0 + (size_t)inst * P.midStride;
 	copy_words (&sm.st, S);
 	__syncthreads ();
-	for (uint32_t blk = 0; blk < P.nBlocks; blk++) {
-		const tbf_seg_ctl& G = ctl_of (P, ctl, blk, inst);
-		stage_tonegen (P, sm, G, T);
-		if (P.chain == TBF_CHAIN_TONEGEN) {
-			float* oL = P.outL + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
-			float* oR = P.outR + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
-			oL[lane] = oR[lane] = sm.bufA[lane];
-			oL[lane + NL] = oR[lane + NL] = sm.bufA[lane + NL];
-			continue;
-		}
-		stage_overdrive (P, sm, G);
-		float* o = P.mid1 + (size_t)inst * P.midStride + (size_t)blk * TBF_BLK;
-		o[lane] = sm.bufB[lane];
-		o[lane + NL] = sm.bufB[lane + NL];
-		if (P.chain == TBF_CHAIN_TAP_PREAMP) {
-			float* oL = P.outL + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
-			float* oR = P.outR + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
-			oL[lane] = oR[lane] = sm.bufB[lane];
-			oL[lane + NL] = oR[lane + NL] = sm.bufB[lane + NL];
-		}
-	}
+	for (uint32_t blk = 0; blk < P.nBlocks; blk++)
+		stage_tonegen (P, sm, ctl_of (P, ctl, blk, inst), T, o + (size_t)blk * TBF_BLK);
 	__syncthreads ();
 	copy_words (S, &sm.st);
+}
+
+/* ================================================================== k_mixpre
+ * The mixdown's two gain chases (src/tonegen.cpp:3734-3777: keyCompLevel += delta and
+ * percEnvGain *= decay, once per sample) and the preamp (preamp / airwindows_density,
+ * src/overdrive.cpp:60-170, FP64) as a chain block: MP_CB instances per workgroup, in tiles of
+ * MP_T samples staged in LDS:
+ *   wave 0     the serial recurrences, one chain per lane: lane 2j runs instance j's
+ *              keyCompLevel chase and the preamp high-pass's iirSampleA chain, lane 2j + 1 its
+ *              percEnvGain chase and iirSampleB (fpFlip hands the two high-pass chains
+ *              alternate samples, so each covers half a tile).  One FP64 instruction stream
+ *              advances 64 chains; a wave per instance served 2.
+ *   wave 1     the preamp's xorshift dither stream (fpd), lane j = instance j
+ *   waves 2..  lane-parallel work, two instances per task (a half-wave each): the gain
+ *              products, the denormal guard, the waveshaper, blend and dither, the stores
+ * Iteration it: the chases of tile it, the products of tile it - 1, the high-pass of tile
+ * it - 2, the waveshaper of tile it - 3; one barrier per iteration.  Every chain runs the
+ * reference's operations in its order.  Tonegen-only chains (configs[1]) stop after the
+ * products, which are then the output. */
+#define MP_CB 32                  /* instances per workgroup */
+#define MP_T 32                   /* samples per tile: one per lane of a half-wave */
+#define MP_S (MP_T + 1)           /* row stride of the per-sample rows (odd: conflict-free columns) */
+#define MP_HS (MP_T / 2 + 1)      /* row stride of the high-pass rows (a chain's MP_T / 2 samples) */
+#define MP_H 8                    /* helper waves */
+#define MP_NTK (MP_CB / 2 / MP_H) /* helper tasks (instance pairs) per tile */
+#define MP_THREADS (NL * (2 + MP_H))
+#define MP_TPB (TBF_BLK / MP_T)   /* tiles per block */
+static_assert (2 * MP_CB == NL && 2 * MP_T == NL && MP_CB % (2 * MP_H) == 0, "k_mixpre geometry");
+
+/* one block's control of an instance as k_mixpre uses it, staged in LDS by the dither wave
+ * a block ahead (so no global load sits on an iteration's path) */
+struct MpCtl {
+	float    gain;    /* percussion routed ? outputGain : swellPedalGain */
+	float    keyCompTarget, decay, reset;
+	uint32_t flags;   /* MPF_* */
+	int32_t  iter;    /* odIter */
+	double   iir, out, output, wet, dry;
+};
+#define MPF_PERC 1u  /* percussion routed (routing & 0x0C) */
+#define MPF_CLEAN 2u /* preamp off */
+#define MPF_DPOS 4u  /* density > 0 */
+#define MPF_RST 8u   /* percEnvGain resets at the block end */
+
+__device__ __forceinline__ MpCtl mp_ctl (const tbf_seg_ctl& G)
+{
+	MpCtl c;
+	const bool perc = (G.routing & 0x0C) != 0;
+	c.gain          = perc ? G.outputGain : G.swellPedalGain;
+	c.keyCompTarget = G.keyCompTarget;
+	c.decay         = G.percEnvGainDecay;
+	c.reset         = G.percEnvGainReset;
+	c.flags = (perc ? MPF_PERC : 0u) | (G.odClean ? MPF_CLEAN : 0u) | (G.odDensityPos ? MPF_DPOS : 0u) | (G.resetPercAtEnd ? MPF_RST : 0u);
+	c.iter   = G.odIter;
+	c.iir    = G.odIir;
+	c.out    = G.odOut;
+	c.output = G.odOutput;
+	c.wet    = G.odWet;
+	c.dry    = G.odDry;
+	return c;
+}
+
+struct MixPreLds {
+	float    g[2][2 * MP_CB][MP_S];  /* chase values before each sample, by tile parity: row 2j
+	                                  * keyCompLevel, 2j + 1 percEnvGain of instance j */
+	double   x[4][2 * MP_CB][MP_HS]; /* preamp input (guarded), by tile mod 4: row 2j + q holds the
+	                                  * samples of instance j's high-pass chain q */
+	double   h[2][2 * MP_CB][MP_HS]; /* high-pass output, same rows, by tile parity */
+	uint32_t f[4][MP_CB][MP_S];      /* fpd before each sample (entry MP_T: after the tile), by tile mod 4 */
+	MpCtl    c[2][MP_CB];            /* the control of block b in slot b & 1 */
+};
+
+/* the preamp after its high-pass (src/overdrive.cpp:117-168): density waveshaper, output
+ * level, dry/wet blend, dither (f1 = the stream after this sample's step) */
+__device__ __forceinline__ float preamp_shape (double x, double dry, const MpCtl& C, uint32_t f1)
+{
+	double br;
+	for (int c = 0; c < C.iter; c++) {
+		br = fabs (x) * 1.57079633;
+		if (br > 1.57079633)
+			br = 1.57079633;
+		br = sin (br);
+		x  = (x > 0.0) ? br : -br;
+	}
+	br = fabs (x) * 1.57079633;
+	if (br > 1.57079633)
+		br = 1.57079633;
+	br = (C.flags & MPF_DPOS) ? sin (br) : 1 - cos (br);
+	if (x > 0)
+		x = (x * (1 - C.out)) + (br * C.out);
+	else
+		x = (x * (1 - C.out)) - (br * C.out);
+	if (C.output < 1.0)
+		x *= C.output;
+	if (C.wet < 1.0)
+		x = (dry * C.dry) + (x * C.wet);
+	return (float)dither_add (x, f1);
+}
+
+__global__ void __launch_bounds__ (MP_THREADS)
+k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
+{
+	__shared__ MixPreLds sm;
+	const int      w = __builtin_amdgcn_readfirstlane (threadIdx.x >> 6), lane = threadIdx.x & (NL - 1);
+	const uint32_t inst0 = P.instBase + blockIdx.x * MP_CB;
+	if (inst0 >= P.nInst)
+		return;
+	const int  nj  = (int)min ((uint32_t)MP_CB, P.nInst - inst0);
+	const int  nT  = (int)P.nBlocks * MP_TPB;
+	const int  nIt = nT + 3;
+	const bool pre = P.chain != TBF_CHAIN_TONEGEN; /* tonegen only: no preamp */
+	if (w == 0) {
+		const int      j = lane >> 1, q = lane & 1;
+		const bool     ok   = j < nj;
+		tbf_mo_state*  M    = &P.st[inst0 + (ok ? j : 0)].mo;
+		float          v    = q ? M->percEnvGain : M->keyCompLevel;
+		double         iir  = q ? M->iirB : M->iirA;
+		/* chase step v = v m + a: keyCompLevel + delta is (v 1) + delta, percEnvGain * decay is
+		 * (v decay) + 0 (or (v 1) + 0 without percussion), the same values (v >= +0) */
+		float  m = 1.f, a = 0.f, rsv = 0.f;
+		bool   rs = false, hp = false;
+		double ia = 0.0;
+		__syncthreads ();
+#pragma unroll 1
+		for (int it = 0; it < nIt; it++) {
+			if (it < nT) {
+				if (it % MP_TPB == 0) {
+					const MpCtl& C = sm.c[(it / MP_TPB) & 1][j];
+					m   = q ? ((C.flags & MPF_PERC) ? C.decay : 1.f) : 1.f;
+					a   = q ? 0.f : (C.keyCompTarget - v) / (float)TBF_BLK; /* keyCompDelta at the block start */
+					rs  = q && (C.flags & MPF_RST);
+					rsv = C.reset;
+				}
+				float* row = sm.g[it & 1][lane];
+				PRIO_UP ();
+				for (int i0 = 0; i0 < MP_T; i0 += 8) {
+					float o[8];
+#pragma unroll
+					for (int k = 0; k < 8; k++) {
+						o[k] = v;
+						v    = (v * m) + a;
+					}
+#pragma unroll
+					for (int k = 0; k < 8; k++)
+						row[i0 + k] = o[k];
+				}
+				PRIO_DOWN ();
+				if (it % MP_TPB == MP_TPB - 1 && rs)
+					v = rsv;
+			}
+			const int th = it - 2; /* the high-pass (src/overdrive.cpp:104-115) of tile th */
+			if (pre && th >= 0 && th < nT) {
+				if (th % MP_TPB == 0) {
+					const MpCtl& C = sm.c[(th / MP_TPB) & 1][j];
+					hp             = !(C.flags & MPF_CLEAN);
+					ia             = C.iir;
+				}
+				if (hp) {
+					const double* xr = sm.x[th & 3][lane];
+					double*       hr = sm.h[th & 1][lane];
+					const double  om = 1.0 - ia;
+					PRIO_UP ();
+#pragma unroll
+					for (int i0 = 0; i0 < MP_T / 2; i0 += 8) {
+						double xv[8];
+#pragma unroll
+						for (int k = 0; k < 8; k++)
+							xv[k] = xr[i0 + k];
+#pragma unroll
+						for (int k = 0; k < 8; k++) {
+							iir        = (iir * om) + (xv[k] * ia);
+							hr[i0 + k] = xv[k] - iir;
+						}
+					}
+					PRIO_DOWN ();
+				}
+			}
+			__syncthreads ();
+		}
+		if (ok) {
+			if (q) {
+				M->percEnvGain = v;
+				M->iirB        = iir;
+			} else {
+				M->keyCompLevel = v;
+				M->iirA         = iir;
+			}
+		}
+		return;
+	}
+	if (w == 1) {
+		/* the control staging (block b into slot b & 1 at iteration 4 b - 1, from registers
+		 * loaded a block earlier) and the dither stream: it advances once per sample of every
+		 * block the preamp runs (src/overdrive.cpp:153-159), f[n] = the state before sample
+		 * n's step */
+		const bool     ok   = lane < nj;
+		const uint32_t inst = inst0 + (ok ? lane : 0);
+		tbf_mo_state*  M    = &P.st[inst].mo;
+		uint32_t       fs   = M->odFpd;
+		const int      nB   = (int)P.nBlocks;
+		MpCtl          nxt;
+		if (lane < MP_CB) {
+			sm.c[0][lane] = mp_ctl (ctl_of (P, ctl, 0, inst));
+			nxt           = mp_ctl (ctl_of (P, ctl, (uint32_t)min (1, nB - 1), inst));
+		}
+		bool adv = false;
+		__syncthreads ();
+#pragma unroll 1
+		for (int it = 0; it < nIt; it++) {
+			if (lane < MP_CB) {
+				if (pre && it < nT) {
+					if (it % MP_TPB == 0)
+						adv = !(sm.c[(it / MP_TPB) & 1][lane].flags & MPF_CLEAN);
+					uint32_t* f = sm.f[it & 3][lane];
+#pragma unroll 8
+					for (int n = 0; n < MP_T; n++) {
+						f[n] = fs;
+						fs   = adv ? xs_step (fs) : fs;
+					}
+					f[MP_T] = fs;
+				}
+				const int b = (it + 1) / MP_TPB; /* the block starting at the next iteration */
+				if ((it + 1) % MP_TPB == 0 && b < nB) {
+					sm.c[b & 1][lane] = nxt;
+					nxt               = mp_ctl (ctl_of (P, ctl, (uint32_t)min (b + 1, nB - 1), inst));
+				}
+			}
+			__syncthreads ();
+		}
+		if (ok && pre && lane < MP_CB)
+			M->odFpd = fs;
+		return;
+	}
+	/* helpers: task t = instances 2 (h + MP_H t) + {0, 1}, half-wave hj each; lane n of the
+	 * half-wave = sample n of the tile.  The (s, p) input is read two iterations before its
+	 * use, into two register sets alternating by iteration parity (the loop is unrolled by
+	 * two, so the sets stay static) */
+	const int     h = w - 2, hj = lane >> 5, n = lane & (MP_T - 1);
+	const float2* in[MP_NTK];
+	float*        o1[MP_NTK];
+	float*        oL[MP_NTK];
+	float*        oR[MP_NTK];
+	int           jT[MP_NTK], rT[MP_NTK];
+	bool          okT[MP_NTK];
+	float2        pS[2][MP_NTK];
+#pragma unroll
+	for (int t = 0; t < MP_NTK; t++) {
+		const int j       = 2 * (h + MP_H * t) + hj;
+		okT[t]            = j < nj;
+		jT[t]             = okT[t] ? j : nj - 1;
+		const uint32_t is = inst0 + jT[t];
+		in[t]             = (const float2*)P.mid0 + (size_t)is * P.midStride + n;
+		o1[t]             = P.mid1 ? P.mid1 + (size_t)is * P.midStride + n : nullptr;
+		oL[t]             = P.outL + (size_t)is * P.outStride + P.outOffset + n;
+		oR[t]             = P.outR + (size_t)is * P.outStride + P.outOffset + n;
+		/* sample n's high-pass chain: iirSampleA takes the samples of parity 0 when fpFlip
+		 * is set at the block start (128 samples leave it unchanged), else parity 1 */
+		const int q0      = P.st[is].mo.fpFlip ? 0 : 1;
+		rT[t]             = 2 * jT[t] + ((n & 1) ^ q0);
+		pS[0][t]          = in[t][0];
+		pS[1][t]          = in[t][(size_t)min (1, nT - 1) * MP_T];
+	}
+	const bool tap = P.chain == TBF_CHAIN_TAP_PREAMP;
+	__syncthreads ();
+	auto step = [&] (const int it, float2 (&qS)[MP_NTK]) {
+		/* the waveshaper of tile it - 3: high-pass output, dry input, the dither state after
+		 * the sample's step */
+		const int kw = it - 3;
+		if (pre && kw >= 0 && kw < nT) {
+			const size_t so = (size_t)kw * MP_T;
+#pragma unroll
+			for (int t = 0; t < MP_NTK; t++) {
+				const MpCtl& C  = sm.c[(kw / MP_TPB) & 1][jT[t]];
+				const double xd = sm.x[kw & 3][rT[t]][n >> 1];
+				float        y;
+				if (C.flags & MPF_CLEAN)
+					y = (float)xd;
+				else
+					y = preamp_shape (sm.h[kw & 1][rT[t]][n >> 1], xd, C, sm.f[kw & 3][jT[t]][n + 1]);
+				if (okT[t]) {
+					if (tap) {
+						oL[t][so] = y;
+						oR[t][so] = y;
+					} else
+						o1[t][so] = y;
+				}
+			}
+		}
+		/* the products of tile it - 1 (src/tonegen.cpp:3734-3777) and the preamp input:
+		 * denormal guard with the dither state before the sample (src/overdrive.cpp:95-100) */
+		const int kp = it - 1;
+		if (kp >= 0 && kp < nT) {
+#pragma unroll
+			for (int t = 0; t < MP_NTK; t++) {
+				const MpCtl& C  = sm.c[(kp / MP_TPB) & 1][jT[t]];
+				const float  kc = sm.g[kp & 1][2 * jT[t]][n];
+				const float  pe = sm.g[kp & 1][2 * jT[t] + 1][n];
+				const float2 sp = qS[t];
+				const float  y  = (C.flags & MPF_PERC) ? (C.gain * kc * (sp.x + (sp.y * pe))) : (C.gain * kc * sp.x);
+				if (!pre) {
+					if (okT[t]) {
+						oL[t][(size_t)kp * MP_T] = y;
+						oR[t][(size_t)kp * MP_T] = y;
+					}
+				} else {
+					double x = (double)y;
+					if (!(C.flags & MPF_CLEAN) && fabs (x) < 1.18e-23)
+						x = sm.f[kp & 3][jT[t]][n] * 1.18e-17;
+					sm.x[kp & 3][rT[t]][n >> 1] = x;
+				}
+			}
+		}
+		/* the input of tile it + 1 into the set just consumed (clamped past the last tile: a
+		 * harmless re-read, so the loads need no branch) */
+		const int tl = min (it + 1, nT - 1);
+#pragma unroll
+		for (int t = 0; t < MP_NTK; t++)
+			qS[t] = in[t][(size_t)tl * MP_T];
+		__syncthreads ();
+	};
+#pragma unroll 1
+	for (int it = 0; it < nIt; it += 2) {
+		step (it, pS[1]);
+		if (it + 1 < nIt)
+			step (it + 1, pS[0]);
+	}
 }
 
 /* ================================================================== reverb */
@@ -881,7 +1057,10 @@ struct RvLds {
 	double      tabD[2][8];            /* the step each row holds (-1: none) */
 	double      v0[2][RVL_G][8];       /* group plan: phase of line l at the start of sub-block j ... */
 	double2     SC[2][RVL_G][8];       /* ... and its {sine, cosine} (closed-form lines) */
-	uint32_t    okm[2][RVL_G];         /* closed-form lines of sub-block j */
+	uint32_t    okm[2][RVL_G];         /* closed-form lines of sub-block j (the rows sc hold its step) ... */
+	uint32_t    okx[2][RVL_G];         /* ... closed-form lines whose step Dx is not the rows' (a group
+	                                    * crossing a binade: the rows are computed inline) */
+	double      Dx[2][RVL_G][8];
 	double      carry[2][RVL_G][8];    /* feedback of sub-block j's last sample */
 	tbf_rv_chan st;
 };
@@ -932,8 +1111,10 @@ __device__ __forceinline__ void rvl_plan (RvLds& sm, double d, int nb, int b, bo
 			sm.SC[b][j][li] = double2 {sv, cv};
 		}
 	}
-	if (lane < RVL_G)
+	if (lane < RVL_G) {
 		sm.okm[b][lane] = lane < nb ? (uint32_t)(okb & 0xff) : 0u;
+		sm.okx[b][lane] = 0u;
+	}
 	__builtin_amdgcn_wave_barrier ();
 	if (lane < 8) {
 		sm.st.phD[li]  = cD;
@@ -944,18 +1125,25 @@ __device__ __forceinline__ void rvl_plan (RvLds& sm, double d, int nb, int b, bo
 			v = v0 + (double)(TBF_SUB * nb) * D;
 		} else {
 			/* rare (a binade crossing or a rounding tie in the group, or forced): walk the
-			 * sub-blocks like k_rv_core; one is closed-form when its own run is and the
-			 * line's rows hold its step, else the literal recurrence (64 adds) */
+			 * sub-blocks like k_rv_core: one is closed-form when its own run is (with the
+			 * line's rows when they hold its step, else rows computed inline), else the
+			 * literal recurrence (64 adds).  So the two network kernels agree however a
+			 * render is split into launches and groups. */
 			atomicOr (errFlags, (uint32_t)TBF_PATH_RV_PHASE);
 			for (int j = 0; j < nb; j++) {
 				sm.v0[b][j][li] = v;
 				double     Dj = 0.0, c1 = cD, c2 = cLo, c3 = cHi;
-				const bool oj = phase_run_cached (v, d, TBF_SUB, Dj, c1, c2, c3) && !force && Dj == sm.tabD[b][li];
+				const bool oj = phase_run_cached (v, d, TBF_SUB, Dj, c1, c2, c3) && !force;
 				if (oj) {
 					double sv, cv;
 					sincos (v, &sv, &cv);
 					sm.SC[b][j][li] = double2 {sv, cv};
-					atomicOr (&sm.okm[b][j], 1u << li);
+					if (Dj == sm.tabD[b][li])
+						atomicOr (&sm.okm[b][j], 1u << li);
+					else {
+						sm.Dx[b][j][li] = Dj;
+						atomicOr (&sm.okx[b][j], 1u << li);
+					}
 					v = v + (double)TBF_SUB * Dj;
 				} else {
 					for (int i = 0; i < TBF_SUB; i++)
@@ -967,17 +1155,13 @@ __device__ __forceinline__ void rvl_plan (RvLds& sm, double d, int nb, int b, bo
 	}
 }
 
-__global__ void __attribute__ ((amdgpu_flat_work_group_size (RVL_THREADS, RVL_THREADS)))
-k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
+/* one (instance, channel) of a k_rv_core_lds launch */
+__device__ __forceinline__ void rvl_pair (const tbf_launch& P, const tbf_inst_const* __restrict__ cst, RvLds& sm,
+                                          const uint32_t inst, const int c)
 {
-	__shared__ RvLds sm;
 	const int      tid  = threadIdx.x;
 	const int      w    = tid >> 6; /* worker: the sub-block within a group; w == RVL_G: planner */
 	const int      n    = tid & (NL - 1);
-	const uint32_t inst = (blockIdx.x >> 1) + P.instBase;
-	const int      c    = blockIdx.x & 1;
-	if (inst >= P.nInst)
-		return;
 	const tbf_inst_const& K     = cst[inst];
 	tbf_rv_chan*          S     = &P.st[inst].rv.ch[c];
 	const uint32_t        rbase = K.ringOff[c * 13];
@@ -1076,11 +1260,18 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 					sn[l]            = SC.x + ((SC.y * q.x) - (SC.x * q.y));
 				}
 			} else {
+				const uint32_t ox = __builtin_amdgcn_readfirstlane (sm.okx[par][w]);
 #pragma unroll
 				for (int l = 0; l < 8; l++) {
 					if ((om >> l) & 1) {
 						const double2 SC = sm.SC[par][w][l], q = sm.sc[par][l][n];
 						sn[l]            = SC.x + ((SC.y * q.x) - (SC.x * q.y));
+					} else if ((ox >> l) & 1) { /* k_rv_core's rows for this step (rv_core_tap) */
+						const double2 SC = sm.SC[par][w][l];
+						const double  dn = (double)(n + 1) * sm.Dx[par][w][l]; /* exact */
+						const double  hh = sin (dn * 0.5);
+						const double  sd = sin (dn), cm = 2.0 * hh * hh;
+						sn[l]            = SC.x + ((SC.y * sd) - (SC.x * cm));
 					} else {
 						const double dl = rld (vdl, l);
 						double       v  = sm.v0[par][w][l];
@@ -1178,6 +1369,29 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 			slab[RVL_OFS[l] + i] = sm.ring[RVL_LOFS[l] + i];
 	if (w == 0)
 		copy_words (S, &sm.st);
+}
+
+/* A workgroup needs a whole CU's LDS, so it can start only on a CU that has drained, while
+ * the neighbouring chunks' kernels keep refilling freed CUs with small workgroups.  So the
+ * grid is persistent (P.rvGrid workgroups, one per CU by default): each workgroup takes
+ * (instance, channel) pairs from a work counter (P.rvWork, zeroed before the launch) until
+ * none is left, and acquires its CU once per launch instead of once per pair.  Every wave of
+ * a workgroup reads the same counter value, so all of them leave the loop together. */
+__global__ void __attribute__ ((amdgpu_flat_work_group_size (RVL_THREADS, RVL_THREADS)))
+k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
+{
+	__shared__ RvLds    sm;
+	__shared__ uint32_t next;
+	const uint32_t      nPair = 2 * (P.nInst - P.instBase);
+	for (;;) {
+		if (threadIdx.x == 0)
+			next = atomicAdd (P.rvWork, 1u);
+		__syncthreads (); /* also: the previous pair's ring and state stores have read the LDS */
+		const uint32_t q = __builtin_amdgcn_readfirstlane (next);
+		if (q >= nPair)
+			break;
+		rvl_pair (P, cst, sm, P.instBase + (q >> 1), (int)(q & 1)); /* its barriers order the next write of `next` */
+	}
 }
 
 /* ------------------------------------------------------------------ chain blocks
@@ -2260,33 +2474,39 @@ k_whirl (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 }
 
 /* ------------------------------------------------------------------ launch */
-/* stage k (0 k_tonegen, 1 k_rv_pre, 2 k_rv_core, 3 k_rv_post, 4 k_whirl) of one launch chunk; the chain mode
- * decides which stages run (tbf_chain_stages) */
+/* stage k (0 k_tonegen, 1 k_mixpre, 2 k_rv_pre, 3 k_rv_core, 4 k_rv_post, 5 k_whirl) of one
+ * launch chunk; the chain mode decides which stages run (tbf_chain_stages) */
 extern "C" int tbf_launch_stage (const tbf_launch* P, int k, hipStream_t stream)
 {
 	if (P->nInst == 0 || P->nBlocks == 0)
 		return 0;
-	if (P->chain != TBF_CHAIN_TONEGEN && (uint64_t)P->nBlocks * TBF_BLK > P->midStride)
+	if ((uint64_t)P->nBlocks * TBF_BLK > P->midStride)
 		return -22;
-	if ((k == 1 || k == 3 || k == 4) && P->nBlocks > NL) /* a launch's per-block controls sit one per lane */
+	if ((k == 2 || k == 4 || k == 5) && P->nBlocks > NL) /* a launch's per-block controls sit one per lane */
 		return -22;
 	const dim3 grid (P->nInst), block (NL);
 	const dim3 cgrid ((P->nInst + RVC_CB - 1) / RVC_CB), cblock (RVC_THREADS);
 	if (k == 0)
 		hipLaunchKernelGGL (k_tonegen, grid, block, 0, stream, *P, P->ctl, P->tpls, P->cst);
 	else if (k == 1)
-		hipLaunchKernelGGL (k_rv_pre, cgrid, cblock, 0, stream, *P, P->cst, P->ctl);
+		hipLaunchKernelGGL (k_mixpre, dim3 ((P->nInst + MP_CB - 1) / MP_CB), dim3 (MP_THREADS), 0, stream, *P, P->ctl);
 	else if (k == 2)
+		hipLaunchKernelGGL (k_rv_pre, cgrid, cblock, 0, stream, *P, P->cst, P->ctl);
+	else if (k == 3)
 		/* the LDS kernel loads and stores a channel's 129.7 KB of rings per launch; the
 		 * streaming kernel moves 24.6 KB per block: below 8 blocks the streaming one
 		 * moves fewer bytes (real-time periods of one or two blocks) */
-		if (P->rvLds && P->nBlocks >= RVL_MIN_BLOCKS)
-			hipLaunchKernelGGL (k_rv_core_lds, dim3 (2 * P->nInst), dim3 (RVL_THREADS), 0, stream, *P, P->cst);
-		else
+		if (P->rvLds && P->nBlocks >= RVL_MIN_BLOCKS) {
+			if (hipMemsetAsync (P->rvWork, 0, sizeof (uint32_t), stream) != hipSuccess)
+				return -5;
+			const uint32_t pairs = 2 * (P->nInst - P->instBase);
+			hipLaunchKernelGGL (k_rv_core_lds, dim3 (P->rvGrid && P->rvGrid < pairs ? P->rvGrid : pairs), dim3 (RVL_THREADS),
+			                    0, stream, *P, P->cst);
+		} else
 			hipLaunchKernelGGL (k_rv_core, dim3 (2 * P->nInst), block, 0, stream, *P, P->cst);
-	else if (k == 3)
+	else if (k == 4)
 		hipLaunchKernelGGL (k_rv_post, cgrid, cblock, 0, stream, *P, P->cst, P->ctl);
-	else if (k == 4) {
+	else if (k == 5) {
 		switch (P->wringLen) {
 			case 512: hipLaunchKernelGGL (k_whirl<512>, grid, block, 0, stream, *P, P->cst, P->ctl); break;
 			case 1024: hipLaunchKernelGGL (k_whirl<1024>, grid, block, 0, stream, *P, P->cst, P->ctl); break;
@@ -2321,5 +2541,5 @@ extern "C" int tbf_rv_lds_fits (const tbf_inst_const* k)
 /* number of stages the chain mode runs */
 extern "C" int tbf_chain_stages (uint32_t chain)
 {
-	return chain == TBF_CHAIN_TONEGEN || chain == TBF_CHAIN_TAP_PREAMP ? 1 : (chain == TBF_CHAIN_TAP_REVERB ? 4 : 5);
+	return chain == TBF_CHAIN_TONEGEN || chain == TBF_CHAIN_TAP_PREAMP ? 2 : (chain == TBF_CHAIN_TAP_REVERB ? 5 : 6);
 }

@@ -136,14 +136,18 @@ typedef struct tbf_inst_const {
 
 /* per instance device-resident DSP state, one sub-struct per render kernel (each
  * kernel stages only its own part in LDS); sizes are multiples of 8 bytes */
-typedef struct tbf_tg_state { /* tonegen + vibrato + overdrive: k_tonegen */
+typedef struct tbf_tg_state { /* tonegen interpreter + vibrato: k_tonegen */
 	uint32_t pos[TBF_NW + 1];
-	float    keyCompLevel, percEnvGain, pz;
+	float    pz;
 	uint32_t stator, outPos;
 	float    vring[TBF_VRING];
-	double   iirA, iirB;
-	uint32_t fpFlip, odFpd;
 } tbf_tg_state;
+
+typedef struct tbf_mo_state { /* mixdown gain chases + preamp: k_mixpre */
+	float    keyCompLevel, percEnvGain; /* tone generator (a retune resets them) ... */
+	double   iirA, iirB;                /* ... preamp (goes on through a retune) */
+	uint32_t fpFlip, odFpd;
+} tbf_mo_state;
 
 typedef struct tbf_rv_chan { /* one channel of the feedback network: k_rv_core wave */
 	int32_t  count[12]; /* delay-line counters A..L (lines 0-11) */
@@ -187,6 +191,7 @@ typedef struct tbf_wh_state { /* whirl: k_whirl */
 
 typedef struct tbf_inst_state {
 	tbf_tg_state tg;
+	tbf_mo_state mo;
 	tbf_rv_state rv;
 	tbf_wh_state wh;
 } tbf_inst_state;
@@ -206,6 +211,7 @@ typedef struct tbf_launch {
 	const tbf_inst_const* cst;
 	tbf_inst_state*       st;
 	float*                wring; /* [inst][4][wring_len] */
+	float*                mid0;  /* [inst][midStride][2] k_tonegen -> k_mixpre: {bus sum, percussion difference} */
 	float*                mid1;  /* [inst][midStride] preamp output of the chunk */
 	float*                mid2;  /* [inst][midStride] reverb output of the chunk */
 	double*               rvA;   /* [inst][2][midStride] k_rv_pre -> k_rv_core: sin(biquadA * wet) */
@@ -241,6 +247,8 @@ typedef struct tbf_launch {
 	const uint32_t*       ctlInst;   /* instances with a stepped delta in this chunk */
 	uint32_t              nCtlInst;
 	uint32_t              rvLds;     /* 1: the reverb core with its rings resident in LDS (k_rv_core_lds) */
+	uint32_t              rvGrid;    /* k_rv_core_lds workgroups (persistent; 0: one per pair) */
+	uint32_t*             rvWork;    /* k_rv_core_lds work counter */
 	const uint32_t*       coff;      /* [tpl][385] keyContrib offsets into contrib */
 	const tbf_contrib*    contrib;
 } tbf_launch;

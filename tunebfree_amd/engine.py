@@ -16,7 +16,7 @@ _u32p = C.POINTER(C.c_uint32)
 
 
 # the render kernels of one launch chunk, in stream order (tbf_debug_kernel_times)
-STAGES = ("k_tonegen", "k_rv_pre", "k_rv_core", "k_rv_post", "k_whirl")
+STAGES = ("k_tonegen", "k_mixpre", "k_rv_pre", "k_rv_core", "k_rv_post", "k_whirl")
 
 
 class TbfError(RuntimeError):
@@ -266,6 +266,12 @@ class Engine:
         ms, nb = C.c_double(), C.c_uint64()
         _check(fn(self._h, 1 if reset else 0, C.byref(ms), C.byref(nb)))
         return ms.value, nb.value
+
+    def debug_reverb_phase(self, inst, ch, line, value):
+        """test hook (tbf_debug_reverb_phase): set a reverb vibrato phase, from the next block"""
+        fn = self._lib.tbf_debug_reverb_phase
+        fn.restype, fn.argtypes = C.c_int, [C.c_void_p, C.c_uint32, C.c_int32, C.c_int32, C.c_double]
+        _check(fn(self._h, int(inst), int(ch), int(line), float(value)))
 
     def error_flags(self):
         f = C.c_uint32()

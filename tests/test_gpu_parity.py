@@ -44,6 +44,36 @@ def test_gpu_tonegen_only_bitexact(oracle):
     assert np.array_equal(L, R)
 
 
+def test_gpu_tonegen_block_ranges(oracle):
+    """A chunk without control deltas may split each instance's blocks over several waves
+    (tbf_launch.tgSplit): a range after the first starts one warm-up block early from the
+    chunk-start state advanced in closed form.  Tonegen-only and full chain, chunks of 64
+    and 40 blocks after an event block, vibrato and percussion routed: the default split,
+    ranges of one block's granularity (TBF_TG_SPLIT=5) and no split (TBF_TG_SPLIT=1) are
+    bit-identical, and match the oracle."""
+    import os
+    for chain in (1, 0):
+        outs = []
+        for env in ({}, {"TBF_TG_SPLIT": "5"}, {"TBF_TG_SPLIT": "1"}):
+            os.environ.update(env)
+            try:
+                eng, tpl, seeds, scens = _setup(oracle, 40, S.bench_scenario, chain=chain)
+            finally:
+                for k in env:
+                    os.environ.pop(k, None)
+            parts = [engine_run(eng, scens, 1), eng.render(64), eng.render(40)]
+            eng.close()
+            outs.append((np.concatenate([p[0] for p in parts], axis=1), np.concatenate([p[1] for p in parts], axis=1)))
+        pick = [0, 13, 39]
+        res = oracle_run(oracle, tpl, [seeds[i] for i in pick], [scens[i] for i in pick], 105, chain=chain)
+        ref = res[2] if chain == 1 else res[0]
+        err, exact = compare(outs[0][0][pick], ref)
+        print(f"chain {chain}: max|err|={err:.3g} bit-exact={exact:.6f}")
+        assert err <= TOL
+        for o in outs[1:]:
+            assert all(np.array_equal(a.view(np.uint32), b.view(np.uint32)) for a, b in zip(outs[0], o))
+
+
 @pytest.mark.parametrize("tap,idx", [(2, 3), (3, 4)])
 def test_gpu_stage_taps(oracle, tap, idx):
     eng, tpl, seeds, scens = _setup(oracle, 6, S.bench_scenario, chain=tap)
@@ -883,6 +913,20 @@ def test_gpu_full_size_bench_batch(oracle):
     R2 = np.concatenate([R2a, R2b], axis=1)
     assert np.array_equal(L2.view(np.uint32), L[half:].view(np.uint32))
     assert np.array_equal(R2.view(np.uint32), R[half:].view(np.uint32))
+    eng2.close()
+
+    # two more steady 64-block calls, as the bench's timed steps render them (no control
+    # deltas: k_tonegen splits each instance's blocks over waves, all six stages pipelined
+    # across chunks and calls, the network kernel persistent): still the oracle's samples
+    more = [eng.render(nb) for _ in range(2)]
+    pick = [0, 3, 2047, 4095]
+    oL, oR, *_ = oracle_run(oracle, tpl, [seeds[i] for i in pick], [scens[i] for i in pick], 3 * nb)
+    gL = np.concatenate([m[0][pick] for m in more], axis=1)
+    gR = np.concatenate([m[1][pick] for m in more], axis=1)
+    eL, xL = compare(gL, oL[:, nb * 128:])
+    eR, xR = compare(gR, oR[:, nb * 128:])
+    print(f"steady calls: max|err| L={eL:.3g} R={eR:.3g} bit-exact L={xL:.6f} R={xR:.6f}")
+    assert max(eL, eR) <= TOL
 
 
 @pytest.mark.parametrize("debug_flags", [0, 1])

@@ -327,6 +327,8 @@ int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
 		 * instance and channel, the round-2 grid) */
 		int ncu = 0;
 		HIPCHK (hipDeviceGetAttribute (&ncu, hipDeviceAttributeMultiprocessorCount, cfg->device));
+		if (const char* ts = getenv ("TBF_TG_SPLIT"))
+			e->tgSplit = atoi (ts);
 		const char* rp = getenv ("TBF_RV_PERSIST");
 		e->rvGrid      = (rp && rp[0] == '0') ? 0u : (uint32_t)std::max (ncu, 1);
 		if (e->rvWork.ensure (1))
@@ -1605,6 +1607,13 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		P.ctl       = e->ctl.p + rp * CTL_REGION (n);
 		P.ctlIdx    = delta ? e->ctlIdx.p + (size_t)rp * n * TBF_CHUNK : nullptr;
 		P.nBlocks   = len;
+		/* k_tonegen block ranges (chunks without deltas) for small batches: about 2048 waves,
+		 * ranges of >= 4 blocks (each range after the first renders one warm-up block).  At
+		 * 4096 instances a split measured no gain (0.73 ms alone either way: the kernel is
+		 * bound by its bank gathers and VALU, not by waves in flight). */
+		P.tgSplit = e->tgSplit >= 0 ? (uint32_t)std::max (e->tgSplit, 1)
+		                            : std::max (1u, std::min ({8u, 2048u / std::max (n, 1u), len / 4}));
+		P.tgSplit = std::min (P.tgSplit, std::max (len, 1u));
 		P.outOffset = (uint64_t)b0 * TBF_BLK;
 		P.nCtlInst  = 0;
 		if (e->devCtl && !e->hCtlInst.empty ()) {

@@ -285,6 +285,7 @@ struct tbf_engine {
 	bool                                    rvLdsFit = false; /* the instances' rings fit k_rv_core_lds */
 	uint32_t                                rvGrid   = 0;     /* k_rv_core_lds persistent workgroups (TBF_RV_PERSIST=0: one per pair) */
 	DevBuf<uint32_t>                        rvWork;           /* its work counter */
+	int                                     tgSplit  = -1;    /* k_tonegen block ranges (TBF_TG_SPLIT; -1: by batch size) */
 	/* programme table (.pgm), src/program.h:26 MAXPROGS; pgm.controller.offset */
 	std::vector<Programme>                  progs = std::vector<Programme> (129);
 	int                                     pgmOffset = 1;

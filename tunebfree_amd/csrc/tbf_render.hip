@@ -34,6 +34,7 @@
 
 /* occupancy targets (waves per SIMD); LDS and VGPR budgets are sized for them */
 #define TG_WAVES 4
+#define TG_SPLIT_MAX 8 /* k_tonegen block ranges (waves) per instance */
 #define RV_WAVES 3
 #define WH_WAVES 3
 /* wave priority raised (s_setprio 1) while a wave runs a serial chain, so the SIMD issues
@@ -214,7 +215,7 @@ __device__ __forceinline__ float eq_iir (float c0, float c1, float c2, float c3,
 __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl& G, const tbf_tpl_desc* T,
                               float2* __restrict__ out)
 {
-	const int             lane = threadIdx.x;
+	const int             lane = threadIdx.x & (NL - 1);
 	tbf_tg_state&         st   = sm.st;
 	/* the program slot: header (entry count) then the entries */
 	const tbf_prog_entry* __restrict__ prog = P.prog + G.prog_off + 1;
@@ -235,7 +236,7 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 		envHere |= E.env != 0;
 	}
 	const bool anyEnv = __any (envHere);
-	__syncthreads ();
+	wave_sync ();
 	/* main loop in program order (the adds keep the reference's order); a lane holds
 	 * samples lane and lane + 64 as a pair, so each bus costs one packed multiply and one
 	 * packed add (v_pk_mul_f32 / v_pk_add_f32: two IEEE float ops, no contraction).  The
@@ -274,11 +275,11 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 	}
 	if (np == 0) /* no program: the buses stay cleared (+0) */
 		sw = vb = pc = f2v{0.f, 0.f};
-	__syncthreads (); /* the entry table is overwritten below */
+	wave_sync (); /* the entry table is overwritten below */
 	sm.swl[lane] = sw.x; sm.swl[lane + NL] = sw.y;
 	sm.vin[lane] = vb.x; sm.vin[lane + NL] = vb.y;
 	sm.prc[lane] = pc.x; sm.prc[lane + NL] = pc.y;
-	__syncthreads ();
+	wave_sync ();
 
 	const uint32_t routing = G.routing;
 	/* vibrato scanner, src/vibrato.cpp:365-411 */
@@ -300,7 +301,7 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 			sm.u.v.vg[n] = g;
 			sm.u.v.vh[n] = n + (int)(((uint32_t)h - op) & 0x3FFu); /* slot offset from out0 */
 		}
-		__syncthreads ();
+		wave_sync ();
 		/* ordered gather: slot W_o collects, in sample order, x-g from samples with
 		 * H==W_o and g from samples with H+1==W_o; valid while H is non-decreasing and
 		 * within 32 ahead (checked; lane 0 replays serially otherwise) */
@@ -354,7 +355,7 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 				}
 			}
 		}
-		__syncthreads ();
+		wave_sync ();
 		if (lane == 0) {
 			st.outPos = (out0 + TBF_BLK) & 0x3FFu;
 			st.stator = (stat0 + (uint32_t)TBF_BLK * P.statorInc) & 0x07ffffffu;
@@ -370,31 +371,78 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 		const float x = sm.swl[n];
 		const float s = (routing & 0x03) ? (x + sm.u.v.vout[n]) : x;
 		const float p = (routing & 0x0C) ? ((n == 0 ? st.pz : sm.prc[n - 1]) - sm.prc[n]) : 0.f;
-		out[n]        = make_float2 (s, p);
+		if (out)
+			out[n] = make_float2 (s, p);
 	}
-	__syncthreads (); /* every lane has read st.pz */
+	wave_sync (); /* every lane has read st.pz */
 	if (lane == 0 && (routing & 0x0C))
 		st.pz = sm.prc[TBF_BLK - 1];
-	__syncthreads ();
+	wave_sync ();
 }
 
-__global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL), amdgpu_waves_per_eu (TG_WAVES)))
+/* One workgroup per instance, one wave per block range.  A chunk whose blocks all play
+ * the instance's current program (no control delta: ctlIdx == NULL) may split its blocks
+ * into P.tgSplit ranges, one wave each, for more waves in flight.  A range after the first
+ * starts one block early from the chunk-start state advanced in closed form: wheel
+ * positions (pos + 128 b) mod len for the program's wheels (a block advances them by 128,
+ * mod len >= 384; pos = len and pos = 0 read the same samples, the bank repeating each
+ * wave's first 128), the scanner's stator and output position; then the warm-up block,
+ * whose output is dropped, rebuilds what a block carries into the next: the scanner
+ * ring's next 31 slots hold only the previous block's contributions (every slot is
+ * cleared when read, and a block's scatter reaches at most 31 slots past its end), and pz
+ * is that block's last percussion sample.  The ranges of an instance share a workgroup, so
+ * every wave has read the chunk-start state (the barrier below) before the last range
+ * writes the state back; separate workgroups could start in any order. */
+__global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL * TG_SPLIT_MAX), amdgpu_waves_per_eu (TG_WAVES)))
 k_tonegen (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl, const tbf_tpl_desc* __restrict__ tpls,
            const tbf_inst_const* __restrict__ cst)
 {
-	__shared__ TgLds sm;
+	extern __shared__ TgLds smv[]; /* one per wave */
+	const uint32_t ns   = blockDim.x / NL;
+	const uint32_t part = __builtin_amdgcn_readfirstlane (threadIdx.x / NL);
+	const int      lane = threadIdx.x & (NL - 1);
 	const uint32_t inst = blockIdx.x + P.instBase;
 	if (inst >= P.nInst)
 		return;
-	const tbf_tpl_desc* T = tpls + cst[inst].tpl;
-	tbf_tg_state*       S = &P.st[inst].tg;
-	float2*             o = (float2*)P.mid0 + (size_t)inst * P.midStride;
-	copy_words (&sm.st, S);
-	__syncthreads ();
-	for (uint32_t blk = 0; blk < P.nBlocks; blk++)
+	TgLds&              sm = smv[part];
+	const tbf_tpl_desc* T  = tpls + cst[inst].tpl;
+	tbf_tg_state*       S  = &P.st[inst].tg;
+	float2*             o  = (float2*)P.mid0 + (size_t)inst * P.midStride;
+	const uint32_t      b0 = (P.nBlocks * part) / ns, b1 = (P.nBlocks * (part + 1)) / ns;
+	{
+		const uint32_t* src = (const uint32_t*)S;
+		uint32_t*       dst = (uint32_t*)&sm.st;
+		for (uint32_t i = lane; i < sizeof (tbf_tg_state) / 4; i += NL)
+			dst[i] = src[i];
+	}
+	__syncthreads (); /* every range has read the chunk-start state */
+	if (part > 0) {
+		const tbf_seg_ctl&    G    = ctl_of (P, ctl, 0, inst);
+		const tbf_prog_entry* prog = P.prog + G.prog_off + 1;
+		const int             np   = (int)P.prog[G.prog_off].pad;
+		const uint32_t        adv  = (uint32_t)TBF_BLK * (b0 - 1); /* samples before the warm-up block */
+		for (int e = lane; e < np; e += NL) {
+			const uint32_t w = prog[e].wheel;
+			sm.st.pos[w]     = (sm.st.pos[w] + adv) % T->len[w];
+		}
+		for (int i = lane; i < TBF_VRING; i += NL)
+			sm.st.vring[i] = 0.f;
+		if (lane == 0) {
+			sm.st.outPos = (sm.st.outPos + adv) & 0x3FFu;
+			sm.st.stator = (sm.st.stator + adv * P.statorInc) & 0x07ffffffu;
+		}
+		wave_sync ();
+		stage_tonegen (P, sm, G, T, nullptr);
+	}
+	for (uint32_t blk = b0; blk < b1; blk++)
 		stage_tonegen (P, sm, ctl_of (P, ctl, blk, inst), T, o + (size_t)blk * TBF_BLK);
-	__syncthreads ();
-	copy_words (S, &sm.st);
+	if (part == ns - 1) {
+		wave_sync ();
+		const uint32_t* src = (const uint32_t*)&sm.st;
+		uint32_t*       dst = (uint32_t*)S;
+		for (uint32_t i = lane; i < sizeof (tbf_tg_state) / 4; i += NL)
+			dst[i] = src[i];
+	}
 }
 
 /* ================================================================== k_mixpre
@@ -528,19 +576,26 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 					rsv = C.reset;
 				}
 				float* row = sm.g[it & 1][lane];
-				PRIO_UP ();
-				for (int i0 = 0; i0 < MP_T; i0 += 8) {
-					float o[8];
+				if (__all ((v * m) + a == v)) { /* a fixed point on every lane (no percussion, the key
+				                                  * compression settled): the whole tile is v */
+#pragma unroll 8
+					for (int k = 0; k < MP_T; k++)
+						row[k] = v;
+				} else {
+					PRIO_UP ();
+					for (int i0 = 0; i0 < MP_T; i0 += 8) {
+						float o[8];
 #pragma unroll
-					for (int k = 0; k < 8; k++) {
-						o[k] = v;
-						v    = (v * m) + a;
+						for (int k = 0; k < 8; k++) {
+							o[k] = v;
+							v    = (v * m) + a;
+						}
+#pragma unroll
+						for (int k = 0; k < 8; k++)
+							row[i0 + k] = o[k];
 					}
-#pragma unroll
-					for (int k = 0; k < 8; k++)
-						row[i0 + k] = o[k];
+					PRIO_DOWN ();
 				}
-				PRIO_DOWN ();
 				if (it % MP_TPB == MP_TPB - 1 && rs)
 					v = rsv;
 			}
@@ -2247,7 +2302,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 #pragma unroll
 			for (int gi = 0; gi < 4; gi++) {
 				const int r = r0 + gi;
-	#pragma unroll
+#pragma unroll
 				for (int q = 0; q < 3; q++) {
 					const int  p   = (r & 1) + 2 * q;
 					const bool fwd = (p == 0 || p == 3 || p == 4);
@@ -2301,7 +2356,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 #pragma unroll
 			for (int gi = 0; gi < 4; gi++) {
 				int ok = (mu[gi][1] >= mu[gi][0] + 2) && (mu[gi][2] >= mu[gi][1] + 2);
-	#pragma unroll
+#pragma unroll
 				for (int q = 0; q < 3; q++) {
 					const int up = lane_shr1 (mu[gi][q]);
 					const int un = lane_shl1 (mu[gi][q]);
@@ -2318,9 +2373,9 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 			if (allOk) {
 				/* every ring on its fast path: the rings are independent, so each pass
 				 * (farthest motion first) updates all of them in one LDS round trip */
-	#pragma unroll
+#pragma unroll
 				for (int q = 2; q >= 0; q--) {
-	#pragma unroll
+#pragma unroll
 					for (int gi = 0; gi < 4; gi++) {
 						if ((unit >> (gi * 3 + q)) & 1u)
 							unit_add<W> (sm.wring[r0 + gi], mu[gi][q], ma[gi][q], mb[gi][q], lane);
@@ -2487,7 +2542,12 @@ extern "C" int tbf_launch_stage (const tbf_launch* P, int k, hipStream_t stream)
 	const dim3 grid (P->nInst), block (NL);
 	const dim3 cgrid ((P->nInst + RVC_CB - 1) / RVC_CB), cblock (RVC_THREADS);
 	if (k == 0)
-		hipLaunchKernelGGL (k_tonegen, grid, block, 0, stream, *P, P->ctl, P->tpls, P->cst);
+	{
+		const uint32_t ns = P->tgSplit > 1 && !P->ctlIdx ? std::min (P->tgSplit, (uint32_t)TG_SPLIT_MAX) : 1u;
+		if (ns > P->nBlocks)
+			return -22;
+		hipLaunchKernelGGL (k_tonegen, grid, dim3 (NL * ns), ns * sizeof (TgLds), stream, *P, P->ctl, P->tpls, P->cst);
+	}
 	else if (k == 1)
 		hipLaunchKernelGGL (k_mixpre, dim3 ((P->nInst + MP_CB - 1) / MP_CB), dim3 (MP_THREADS), 0, stream, *P, P->ctl);
 	else if (k == 2)

@@ -248,6 +248,7 @@ typedef struct tbf_launch {
 	uint32_t              nCtlInst;
 	uint32_t              rvLds;     /* 1: the reverb core with its rings resident in LDS (k_rv_core_lds) */
 	uint32_t              rvGrid;    /* k_rv_core_lds workgroups (persistent; 0: one per pair) */
+	uint32_t              tgSplit;   /* k_tonegen block ranges per instance (chunks without deltas; <= nBlocks) */
 	uint32_t*             rvWork;    /* k_rv_core_lds work counter */
 	const uint32_t*       coff;      /* [tpl][385] keyContrib offsets into contrib */
 	const tbf_contrib*    contrib;

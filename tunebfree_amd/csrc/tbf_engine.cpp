@@ -14,6 +14,9 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <memory>
 #include <string>
@@ -165,7 +168,7 @@ static void whirlConsts (tbf_inst_const& k, const WhirlTables& wt, const Config&
 }
 
 /* preamp per-block constants, src/overdrive.cpp:64-84 and the density/out loops */
-static void odCtl (const Instance& in, double sr, tbf_seg_ctl& c)
+static void odCtlCompute (const Instance& in, double sr, tbf_seg_ctl& c)
 {
 	double overallscale = 1.0;
 	overallscale /= 44100.0;
@@ -189,6 +192,30 @@ static void odCtl (const Instance& in, double sr, tbf_seg_ctl& c)
 	c.odOut        = out;
 	c.odDensityPos = density > 0 ? 1u : 0u;
 	c.odClean      = (uint32_t)in.odClean;
+}
+
+/* the preamp fields of a control entry, recomputed only when the preamp parameters changed
+ * (the pow above costs more than the rest of a dense-event step per instance and block) */
+static void odCtl (Instance& in, double sr, tbf_seg_ctl& c)
+{
+	Instance::OdCache& k = in.odc;
+	if (!k.valid || k.A != in.odA || k.B != in.odB || k.C != in.odC || k.D != in.odD || k.clean != in.odClean) {
+		odCtlCompute (in, sr, k.ctl);
+		k.A     = in.odA;
+		k.B     = in.odB;
+		k.C     = in.odC;
+		k.D     = in.odD;
+		k.clean = in.odClean;
+		k.valid = true;
+	}
+	c.odIir        = k.ctl.odIir;
+	c.odOutput     = k.ctl.odOutput;
+	c.odWet        = k.ctl.odWet;
+	c.odDry        = k.ctl.odDry;
+	c.odIter       = k.ctl.odIter;
+	c.odOut        = k.ctl.odOut;
+	c.odDensityPos = k.ctl.odDensityPos;
+	c.odClean      = k.ctl.odClean;
 }
 
 /* fsetCharacter (src/overdrive.cpp:547-574): character A and the linear-segment output
@@ -248,25 +275,96 @@ static unsigned hostThreads ()
 	return std::max (1u, std::min (t, 16u));
 }
 
+/* A persistent pool of hostThreads () - 1 workers (the caller is the last): a dense-event
+ * chunk runs two parallel sections, and creating 16 threads for each cost ~0.3-0.8 ms.
+ * One job at a time (the mutex), so engines driven from several host threads share it. */
+class HostPool {
+  public:
+	static HostPool& get ()
+	{
+		static HostPool p;
+		return p;
+	}
+	void run (uint32_t n, const std::function<void (uint32_t)>& f)
+	{
+		std::lock_guard<std::mutex> job (jobM);
+		{
+			std::lock_guard<std::mutex> g (m);
+			fn = &f;
+			cnt = n;
+			next.store (0);
+			busy = (int)th.size ();
+			gen++;
+		}
+		cv.notify_all ();
+		work ();
+		std::unique_lock<std::mutex> g (m);
+		done.wait (g, [&] { return busy == 0; });
+		fn = nullptr;
+	}
+	unsigned workers () const { return (unsigned)th.size () + 1; }
+
+  private:
+	HostPool ()
+	{
+		const unsigned nt = hostThreads ();
+		for (unsigned k = 1; k < nt; k++)
+			th.emplace_back ([this] { loop (); });
+	}
+	~HostPool ()
+	{
+		{
+			std::lock_guard<std::mutex> g (m);
+			quit = true;
+		}
+		cv.notify_all ();
+		for (auto& t : th)
+			t.join ();
+	}
+	void work ()
+	{
+		for (uint32_t t; (t = next.fetch_add (1)) < cnt;)
+			(*fn) (t);
+	}
+	void loop ()
+	{
+		uint64_t seen = 0;
+		for (;;) {
+			{
+				std::unique_lock<std::mutex> g (m);
+				cv.wait (g, [&] { return quit || gen != seen; });
+				if (quit)
+					return;
+				seen = gen;
+			}
+			work ();
+			std::lock_guard<std::mutex> g (m);
+			if (--busy == 0)
+				done.notify_one ();
+		}
+	}
+	std::vector<std::thread>             th;
+	std::mutex                           m, jobM;
+	std::condition_variable              cv, done;
+	const std::function<void (uint32_t)>* fn = nullptr;
+	uint32_t                             cnt = 0;
+	std::atomic<uint32_t>                next {0};
+	int                                  busy = 0;
+	uint64_t                             gen  = 0;
+	bool                                 quit = false;
+};
+
 /* run f(t) for t < n on up to hostThreads () threads */
 template <typename F>
 static void parallelFor (uint32_t n, F f)
 {
-	const unsigned nt = std::min<unsigned> (hostThreads (), n);
-	if (nt <= 1) {
+	if (n <= 1 || hostThreads () <= 1) {
 		for (uint32_t t = 0; t < n; t++)
 			f (t);
 		return;
 	}
-	std::atomic<uint32_t>    next {0};
-	std::vector<std::thread> pool;
-	for (unsigned k = 0; k < nt; k++)
-		pool.emplace_back ([&] {
-			for (uint32_t t; (t = next.fetch_add (1)) < n;)
-				f (t);
-		});
-	for (auto& th : pool)
-		th.join ();
+	const std::function<void (uint32_t)> g (f);
+	HostPool::get ().run (n, g);
 }
 
 extern "C" {
@@ -329,8 +427,8 @@ int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
 		HIPCHK (hipDeviceGetAttribute (&ncu, hipDeviceAttributeMultiprocessorCount, cfg->device));
 		if (const char* ts = getenv ("TBF_TG_SPLIT"))
 			e->tgSplit = atoi (ts);
-		const char* rp = getenv ("TBF_RV_PERSIST");
-		e->rvGrid      = (rp && rp[0] == '0') ? 0u : (uint32_t)std::max (ncu, 1);
+		const char* rp = getenv ("TBF_RV_PERSIST"); /* 0: per-pair grid; n > 0: n workgroups */
+		e->rvGrid      = rp ? (uint32_t)std::max (atoi (rp), 0) : (uint32_t)std::max (ncu, 1);
 		if (e->rvWork.ensure (1))
 			return fail (-12, "out of device memory");
 		HIPCHK (hipEventCreateWithFlags (&e->upEv, hipEventDisableTiming));
@@ -395,6 +493,7 @@ int tbf_engine_destroy (tbf_engine* e)
 	e->rvA.release ();
 	e->rvB.release ();
 	e->rvWork.release ();
+	e->mixFixed.release ();
 	if (e->stream)
 		(void)hipStreamDestroy (e->stream);
 	for (hipStream_t q : e->gs)
@@ -1153,8 +1252,34 @@ static int stepChunkParallel (tbf_engine* e, uint32_t n, uint32_t want, uint32_t
 	}
 	for (uint32_t a : e->actList) /* the active list by range, in order */
 		out[a / per].act.push_back (a);
-	for (uint32_t k = evBeg; k < evEnd; k++)
-		out[ev[k].inst / per].evs.push_back (k);
+	/* the events by instance range, in order: a parallel counting partition over T segments
+	 * of the event list (a serial pass cost ~2 ms at 524k events) */
+	{
+		const uint32_t        nev = evEnd - evBeg, seg = (nev + T - 1) / T;
+		std::vector<uint32_t> cnt ((size_t)T * T, 0);
+		parallelFor (T, [&] (uint32_t sgm) {
+			const uint32_t k0 = evBeg + std::min (nev, sgm * seg), k1 = evBeg + std::min (nev, (sgm + 1) * seg);
+			for (uint32_t k = k0; k < k1; k++)
+				cnt[(size_t)sgm * T + ev[k].inst / per]++;
+		});
+		for (unsigned t = 0; t < T; t++) {
+			uint32_t tot = 0;
+			for (unsigned sgm = 0; sgm < T; sgm++) {
+				const uint32_t c                = cnt[(size_t)sgm * T + t];
+				cnt[(size_t)sgm * T + t] = tot; /* the segment's first slot in worker t's list */
+				tot += c;
+			}
+			out[t].evs.resize (tot);
+		}
+		parallelFor (T, [&] (uint32_t sgm) {
+			const uint32_t k0 = evBeg + std::min (nev, sgm * seg), k1 = evBeg + std::min (nev, (sgm + 1) * seg);
+			uint32_t*      at = cnt.data () + (size_t)sgm * T;
+			for (uint32_t k = k0; k < k1; k++) {
+				const uint32_t t = ev[k].inst / per;
+				out[t].evs[at[t]++] = k;
+			}
+		});
+	}
 	e->dCtl.resize ((size_t)n * want);
 	e->hRec.resize ((size_t)n * want);
 	std::vector<uint32_t>& cur = e->curIdx;
@@ -1341,6 +1466,9 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 	P.rvLds     = e->rvLdsOn && e->rvLdsFit;
 	P.rvGrid    = e->rvGrid;
 	P.rvWork    = e->rvWork.p;
+	if (e->cfg.chain_mode == TBF_CHAIN_TONEGEN && e->mixFixed.ensure (n))
+		return fail (-12, "out of device memory");
+	P.mixFixed = e->mixFixed.p;
 	/* inter-stage buffers: two sets, by chunk parity (see the pipelining below) */
 	const size_t need = (size_t)n * TBF_CHUNK * TBF_BLK;
 	if (e->mid0.ensure (2 * 2 * need))
@@ -1355,7 +1483,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 	/* Cross-chunk pipelining.  Every stage is causal and keeps its own state, so stage k
 	 * of chunk c depends only on stage k-1 of chunk c and on stage k of chunk c-1, which
 	 * runs on the same stage-group stream; the stage buffers alternate by chunk parity.
-	 * Used for the full chain; tap modes and a host-control chunk's uploads run on the
+	 * Used for the full chain; tonegen only, tap modes and a host-control chunk's uploads run on the
 	 * caller's stream after joining.  With tbf_debug_kernel_times on, each launch is
 	 * bracketed by events on its own stream (durations then include the overlap with the
 	 * other streams' kernels). */

@@ -56,6 +56,12 @@ struct Instance {
 	/* preamp (struct b_preamp) */
 	int            odClean = 1;
 	float          odA = 0.0f, odB = 0.0f, odC = 1.0f, odD = 0.5f;
+	struct OdCache { /* the preamp's control fields for these parameters (odCtl) */
+		float       A = 0.f, B = 0.f, C = 0.f, D = 0.f;
+		int         clean = 0;
+		bool        valid = false;
+		tbf_seg_ctl ctl;
+	} odc;
 	/* reverb mix */
 	float          rvG = 0.1f;
 	int            whBypass = 0;
@@ -285,6 +291,7 @@ struct tbf_engine {
 	bool                                    rvLdsFit = false; /* the instances' rings fit k_rv_core_lds */
 	uint32_t                                rvGrid   = 0;     /* k_rv_core_lds persistent workgroups (TBF_RV_PERSIST=0: one per pair) */
 	DevBuf<uint32_t>                        rvWork;           /* its work counter */
+	DevBuf<uint8_t>                         mixFixed;         /* tonegen only: k_tonegen wrote the output (tbf_launch.mixFixed) */
 	int                                     tgSplit  = -1;    /* k_tonegen block ranges (TBF_TG_SPLIT; -1: by batch size) */
 	/* programme table (.pgm), src/program.h:26 MAXPROGS; pgm.controller.offset */
 	std::vector<Programme>                  progs = std::vector<Programme> (129);

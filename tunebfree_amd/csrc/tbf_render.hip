@@ -213,7 +213,8 @@ __device__ __forceinline__ float eq_iir (float c0, float c1, float c2, float c3,
 
 /* oscGenerateFragment core interpreter + vibratoProc + mixdown, src/tonegen.cpp:3607-3777 */
 __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl& G, const tbf_tpl_desc* T,
-                              float2* __restrict__ out)
+                              float2* __restrict__ out, float* __restrict__ oL = nullptr, float* __restrict__ oR = nullptr,
+                              float kc = 0.f, float pe = 0.f)
 {
 	const int             lane = threadIdx.x & (NL - 1);
 	tbf_tg_state&         st   = sm.st;
@@ -371,13 +372,29 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 		const float x = sm.swl[n];
 		const float s = (routing & 0x03) ? (x + sm.u.v.vout[n]) : x;
 		const float p = (routing & 0x0C) ? ((n == 0 ? st.pz : sm.prc[n - 1]) - sm.prc[n]) : 0.f;
-		if (out)
+		if (oL) { /* the products with fixed-point gain chases (k_tonegen, tonegen only) */
+			const float y = (routing & 0x0C) ? (G.outputGain * kc * (s + (p * pe))) : (G.swellPedalGain * kc * s);
+			oL[n] = y;
+			oR[n] = y;
+		} else if (out)
 			out[n] = make_float2 (s, p);
 	}
 	wave_sync (); /* every lane has read st.pz */
 	if (lane == 0 && (routing & 0x0C))
 		st.pz = sm.prc[TBF_BLK - 1];
 	wave_sync ();
+}
+
+/* whether the mixdown's two gain chases (k_mixpre's v = v m + a) sit at a fixed point under
+ * control G: then they keep v, bit for bit, for every block with that control */
+__device__ __forceinline__ bool mix_fixed (const tbf_seg_ctl& G, const tbf_mo_state& M)
+{
+	const float kc = M.keyCompLevel, pe = M.percEnvGain;
+	const bool  perc = (G.routing & 0x0C) != 0;
+	const float kc1  = (kc * 1.f) + ((G.keyCompTarget - kc) / (float)TBF_BLK);
+	const float pe1  = (pe * (perc ? G.percEnvGainDecay : 1.f)) + 0.f;
+	return __float_as_uint (kc1) == __float_as_uint (kc) && __float_as_uint (pe1) == __float_as_uint (pe) &&
+	       !(G.resetPercAtEnd && __float_as_uint (G.percEnvGainReset) != __float_as_uint (pe));
 }
 
 /* One workgroup per instance, one wave per block range.  A chunk whose blocks all play
@@ -409,6 +426,17 @@ k_tonegen (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl, const tbf_tp
 	tbf_tg_state*       S  = &P.st[inst].tg;
 	float2*             o  = (float2*)P.mid0 + (size_t)inst * P.midStride;
 	const uint32_t      b0 = (P.nBlocks * part) / ns, b1 = (P.nBlocks * (part + 1)) / ns;
+	/* tonegen only, no control delta in the chunk (every block has the instance's current
+	 * control) and the gain chases at a fixed point: the products are computed here and
+	 * written as the output, and k_mixpre skips the instance (mixFixed).  The chain runs
+	 * its stages in order, so the preamp state read here is the previous chunk's final one. */
+	bool        fixed = false;
+	const float kcF = P.st[inst].mo.keyCompLevel, peF = P.st[inst].mo.percEnvGain;
+	if (P.chain == TBF_CHAIN_TONEGEN) {
+		fixed = !P.ctlIdx && mix_fixed (ctl_of (P, ctl, 0, inst), P.st[inst].mo);
+		if (threadIdx.x == 0)
+			P.mixFixed[inst] = fixed ? 1 : 0;
+	}
 	{
 		const uint32_t* src = (const uint32_t*)S;
 		uint32_t*       dst = (uint32_t*)&sm.st;
@@ -434,8 +462,14 @@ k_tonegen (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl, const tbf_tp
 		wave_sync ();
 		stage_tonegen (P, sm, G, T, nullptr);
 	}
-	for (uint32_t blk = b0; blk < b1; blk++)
-		stage_tonegen (P, sm, ctl_of (P, ctl, blk, inst), T, o + (size_t)blk * TBF_BLK);
+	for (uint32_t blk = b0; blk < b1; blk++) {
+		const size_t so = P.outOffset + (size_t)blk * TBF_BLK;
+		if (fixed)
+			stage_tonegen (P, sm, ctl_of (P, ctl, blk, inst), T, nullptr, P.outL + (size_t)inst * P.outStride + so,
+			               P.outR + (size_t)inst * P.outStride + so, kcF, peF);
+		else
+			stage_tonegen (P, sm, ctl_of (P, ctl, blk, inst), T, o + (size_t)blk * TBF_BLK);
+	}
 	if (part == ns - 1) {
 		wave_sync ();
 		const uint32_t* src = (const uint32_t*)&sm.st;
@@ -553,6 +587,10 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 	const int  nT  = (int)P.nBlocks * MP_TPB;
 	const int  nIt = nT + 3;
 	const bool pre = P.chain != TBF_CHAIN_TONEGEN; /* tonegen only: no preamp */
+	/* tonegen only: instances whose output k_tonegen wrote (fixed-point chases, mixFixed);
+	 * a workgroup of only those has nothing to do (their state does not change) */
+	if (!pre && __all (lane >= nj || P.mixFixed[inst0 + (lane < nj ? lane : 0)]))
+		return;
 	if (w == 0) {
 		const int      j = lane >> 1, q = lane & 1;
 		const bool     ok   = j < nj;
@@ -749,7 +787,7 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 				const float2 sp = qS[t];
 				const float  y  = (C.flags & MPF_PERC) ? (C.gain * kc * (sp.x + (sp.y * pe))) : (C.gain * kc * sp.x);
 				if (!pre) {
-					if (okT[t]) {
+					if (okT[t] && !P.mixFixed[inst0 + jT[t]]) {
 						oL[t][(size_t)kp * MP_T] = y;
 						oR[t][(size_t)kp * MP_T] = y;
 					}

@@ -249,6 +249,8 @@ typedef struct tbf_launch {
 	uint32_t              rvLds;     /* 1: the reverb core with its rings resident in LDS (k_rv_core_lds) */
 	uint32_t              rvGrid;    /* k_rv_core_lds workgroups (persistent; 0: one per pair) */
 	uint32_t              tgSplit;   /* k_tonegen block ranges per instance (chunks without deltas; <= nBlocks) */
+	uint8_t*              mixFixed;  /* tonegen only: [inst] 1 when k_tonegen wrote the chunk's output (the
+	                                  * mixdown's gain chases at a fixed point), so k_mixpre skips it */
 	uint32_t*             rvWork;    /* k_rv_core_lds work counter */
 	const uint32_t*       coff;      /* [tpl][385] keyContrib offsets into contrib */
 	const tbf_contrib*    contrib;

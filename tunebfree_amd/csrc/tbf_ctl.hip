@@ -14,7 +14,9 @@
  * each stepped block a tbf_tgc_rec; this kernel owns the per-wheel state
  * (tbf_tgc_state, HBM) and writes the block's program where k_tonegen reads it.
  *
- * One wave per instance with stepped blocks in the chunk, blocks in order:
+ * One wave per instance with stepped blocks in the chunk, blocks in order, the instance's
+ * bus levels and routed sums staged in LDS for the launch (their read-modify-writes were
+ * global round trips, one per message and list pass):
  *   messages   in queue order; the key's keyContrib list (sorted by wheel, then bus) is
  *              spread over the lanes.  Each (wheel, bus) appears once per key, so the
  *              bus-level adds are lane-parallel and keep the reference's per-(wheel, bus)
@@ -37,6 +39,8 @@
 #define NW TBF_NW
 
 struct CtlLds {
+	float    bl[NW + 1][27]; /* the instance's bus levels and routed sums, staged for the launch */
+	float    sums[NW + 1][6];
 	int32_t  ref[NW + 1];
 	uint16_t list[NW + 1];
 	int16_t  acl1[NW + 1];
@@ -50,8 +54,7 @@ struct CtlLds {
 __device__ __forceinline__ uint64_t lanemask_lt () { return (1ull << threadIdx.x) - 1ull; }
 
 /* one key message (src/tonegen.cpp:3270-3322) */
-__device__ void ctl_message (CtlLds& sm, tbf_tgc_state* __restrict__ G, const tbf_contrib* __restrict__ kc, uint32_t c0,
-                             uint32_t c1, bool on)
+__device__ void ctl_message (CtlLds& sm, const tbf_contrib* __restrict__ kc, uint32_t c0, uint32_t c1, bool on)
 {
 	const int lane = threadIdx.x;
 	for (uint32_t base = c0; base < c1; base += NL) {
@@ -77,7 +80,7 @@ __device__ void ctl_message (CtlLds& sm, tbf_tgc_state* __restrict__ G, const tb
 		const int      part  = (int)(next - (uint32_t)lane);
 		bool           join  = false;
 		if (valid) {
-			float* bl = &G->busLevel[w][bus];
+			float* bl = &sm.bl[w][bus];
 			*bl       = on ? *bl + lev : *bl - lev;
 		}
 		if (owner) {
@@ -112,7 +115,7 @@ __device__ void ctl_message (CtlLds& sm, tbf_tgc_state* __restrict__ G, const tb
 
 /* the active-list loop and the removals of one block (src/tonegen.cpp:3333-3594); writes
  * the program (header + one entry per active wheel) at out */
-__device__ void ctl_block (CtlLds& sm, tbf_tgc_state* __restrict__ G, const tbf_tgc_rec& R, tbf_prog_entry* __restrict__ out)
+__device__ void ctl_block (CtlLds& sm, const tbf_tgc_rec& R, tbf_prog_entry* __restrict__ out)
 {
 	const int      lane        = threadIdx.x;
 	const uint32_t L0          = sm.L;
@@ -131,7 +134,7 @@ __device__ void ctl_block (CtlLds& sm, tbf_tgc_state* __restrict__ G, const tbf_
 		if (valid) {
 			on                = sm.list[i];
 			const uint32_t rf = sm.rf[on];
-			float*         S  = G->sums[on];
+			float*         S  = sm.sums[on];
 			tbf_prog_entry E;
 			E.wheel = (uint16_t)on;
 			E.env = 0;
@@ -157,7 +160,7 @@ __device__ void ctl_block (CtlLds& sm, tbf_tgc_state* __restrict__ G, const tbf_
 				}
 				bool reroute = false;
 				if ((rf & 0x0004) || dbChange) {
-					const float* bl  = G->busLevel[on];
+					const float* bl  = sm.bl[on];
 					float        sum = 0.0f;
 					for (int d = 0; d < 9; d++)
 						sum += bl[d] * sm.dbg[d];
@@ -173,7 +176,7 @@ __device__ void ctl_block (CtlLds& sm, tbf_tgc_state* __restrict__ G, const tbf_
 					reroute  = true;
 				}
 				if (reroute || recompute) {
-					sumPercn = (routing & 0x0C) ? G->busLevel[on][percSendBus] : 0.0f;
+					sumPercn = (routing & 0x0C) ? sm.bl[on][percSendBus] : 0.0f;
 					sumScanr = 0.0f;
 					sumSwell = sumPedal;
 					if (routing & 0x02)
@@ -244,6 +247,10 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_tgctl (
 	tbf_tgc_state*    G    = P.tgc + inst;
 	const uint32_t    tpl  = P.cst[inst].tpl;
 	const uint32_t*   coff = P.coff + (size_t)tpl * 385;
+	for (int i = lane; i < (NW + 1) * 27; i += NL)
+		(&sm.bl[0][0])[i] = (&G->busLevel[0][0])[i];
+	for (int i = lane; i < (NW + 1) * 6; i += NL)
+		(&sm.sums[0][0])[i] = (&G->sums[0][0])[i];
 	for (int w = lane; w <= NW; w += NL) {
 		sm.ref[w]  = G->refCount[w];
 		sm.list[w] = G->list[w];
@@ -274,10 +281,10 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_tgctl (
 			const uint32_t kn  = msg & 0x0fffu;
 			if (kn >= 384)
 				continue;
-			ctl_message (sm, G, P.contrib, coff[kn], coff[kn + 1], (msg & 0xf000u) == 0x1000u);
+			ctl_message (sm, P.contrib, coff[kn], coff[kn + 1], (msg & 0xf000u) == 0x1000u);
 		}
 		const uint32_t off = P.ctl[idx].prog_off;
-		ctl_block (sm, G, R, (tbf_prog_entry*)P.prog + off);
+		ctl_block (sm, R, (tbf_prog_entry*)P.prog + off);
 		last = off;
 	}
 	/* the instance's last program becomes its persistent one, in the slot after the current
@@ -294,6 +301,11 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_tgctl (
 		for (uint32_t k = lane; k < cnt; k += NL)
 			d[k] = src[k];
 	}
+	__syncthreads ();
+	for (int i = lane; i < (NW + 1) * 27; i += NL)
+		(&G->busLevel[0][0])[i] = (&sm.bl[0][0])[i];
+	for (int i = lane; i < (NW + 1) * 6; i += NL)
+		(&G->sums[0][0])[i] = (&sm.sums[0][0])[i];
 	for (int w = lane; w <= NW; w += NL) {
 		G->refCount[w] = sm.ref[w];
 		G->list[w]     = sm.list[w];

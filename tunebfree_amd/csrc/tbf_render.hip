@@ -255,23 +255,25 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 			vb = vb + x * E.vg;
 			pc = pc + x * E.pg;
 		}
-	} else { /* envelope entries x * (g + e (ng - g)) (3640-3662); steady entries take the same
-	          * expression with e = -0 and ng - g = +0: g + (-0 * +0) == g for every g */
+	} else { /* envelope entries x * (g + e (ng - g)) (3640-3662), steady entries x * g as above
+	          * (the reference's g + e (ng - g) with e = -0 and ng - g = +0 is g for every g); the
+	          * branch is wave-uniform, so only envelope entries load envelope rows */
 #pragma unroll 4
 		for (int e = 0; e < np; e++) {
 			const float* __restrict__ bp = P.bank + sm.u.ent.base[e];
 			const f2v                 x  = {bp[lane], bp[lane + NL]};
 			const tbf_prog_entry&     E  = prog[e];
-			const int                 en = E.env;
-			const float*              ep = (en == 2 ? T->releaseEnv[E.row & 7] : T->attackEnv[E.row & 7]);
-			f2v                       ev = {ep[lane], ep[lane + NL]};
-			ev                            = en ? ev : f2v{-0.f, -0.f};
-			const float               ds = en ? E.nsg - E.sg : 0.f;
-			const float               dv = en ? E.nvg - E.vg : 0.f;
-			const float               dp = en ? E.npg - E.pg : 0.f;
-			sw = sw + x * (E.sg + (ev * ds));
-			vb = vb + x * (E.vg + (ev * dv));
-			pc = pc + x * (E.pg + (ev * dp));
+			if (E.env) {
+				const float* ep = (E.env == 2 ? T->releaseEnv[E.row & 7] : T->attackEnv[E.row & 7]);
+				const f2v    ev = {ep[lane], ep[lane + NL]};
+				sw              = sw + x * (E.sg + (ev * (E.nsg - E.sg)));
+				vb              = vb + x * (E.vg + (ev * (E.nvg - E.vg)));
+				pc              = pc + x * (E.pg + (ev * (E.npg - E.pg)));
+			} else {
+				sw = sw + x * E.sg;
+				vb = vb + x * E.vg;
+				pc = pc + x * E.pg;
+			}
 		}
 	}
 	if (np == 0) /* no program: the buses stay cleared (+0) */

@@ -188,14 +188,13 @@ typedef float f2v __attribute__ ((ext_vector_type (2)));
 typedef float f2u __attribute__ ((ext_vector_type (2), aligned (4)));
 typedef float f4u __attribute__ ((ext_vector_type (4), aligned (4)));
 
-/* fmodf (x, 1.f) (src/whirl.cpp:1436, 1458): for finite x >= 0 it is x - floorf (x),
- * which is exact (the fractional bits of x); anything else takes libm */
-__device__ __forceinline__ float frac1 (float x)
-{
-	if (x >= 0.f && x < 16777216.f)
-		return x - floorf (x);
-	return fmodf (x, 1.f);
-}
+/* fmodf (x, 1.f) of a motion's table position (src/whirl.cpp:1436, 1458): the argument is
+ * angle * 16384 + phase with the rotor angle in [0, 1) (every update is an fmod (., 1) or
+ * a brake target fmod (., 1.0)), the mic offsets fwAng = micAngle / 4 in [0, 0.25] and
+ * bwAng = 1 - micAngle / 4 in [0.75, 1] (micAngle = 1 - deg / 180, deg in [0, 180],
+ * src/whirl.cpp:1139, 1380-1381) and phases below 16384: so 0 <= x < 2^24, where fmodf
+ * (x, 1) is x - floorf (x) exactly (the fractional bits).  NaN stays NaN either way. */
+__device__ __forceinline__ float frac1 (float x) { return x - floorf (x); }
 
 /* RBJ biquad, Direct Form II in float (EQ_IIR, src/whirl.cpp:1479-1485); coefficients
  * a1 a2 b0 b1 b2 in registers */
@@ -2339,50 +2338,69 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 		for (int r0 = 0; r0 < 4; r0 += 4) {
 			int   mu[4][3];
 			float ma[4][3], mb[4][3];
+			/* the table positions of all 12 motions, then every table load (18) in flight
+			 * together, then the arithmetic: issued motion by motion, each motion's loads
+			 * were waited for before the next motion's were issued */
+			float h1v[4][3];
+#pragma unroll
+			for (int gi = 0; gi < 4; gi++)
+#pragma unroll
+				for (int q = 0; q < 3; q++) {
+					const int p = ((r0 + gi) & 1) + 2 * q;
+					if (r0 + gi < 2) /* HN_MOTION, src/whirl.cpp:1434 */
+						h1v[gi][q] = (float)((ha + ((p & 1) ? K.bwAng : K.fwAng)) * (unsigned int)16384 + K.hornPhase[p]);
+					else /* DR_MOTION, src/whirl.cpp:1457 */
+						h1v[gi][q] = (float)(da * (unsigned int)16384 + K.hornPhase[p]);
+				}
+			f2u   dpv[4][3];
+			f4u   b4v[2][3];
+			float b5v[2][3];
+#pragma unroll
+			for (int gi = 0; gi < 4; gi++)
+#pragma unroll
+				for (int q = 0; q < 3; q++) {
+					const int      p   = ((r0 + gi) & 1) + 2 * q;
+					const bool     fwd = (p == 0 || p == 3 || p == 4);
+					const float*   dsp = r0 + gi < 2 ? (fwd ? hnFwd : hnBwd) : (fwd ? drFwd : drBwd);
+					const unsigned hl  = ((unsigned int)floorf (h1v[gi][q])) & 16383u;
+					dpv[gi][q]         = *(const f2u*)(dsp + hl); /* dsp[hl], dsp[(hl + 1) & 16383] */
+					if (r0 + gi < 2) {
+						const unsigned kk = ((unsigned int)roundf (h1v[gi][q])) & 16383u;
+						const float*   b  = (fwd ? bbw : bfw) + 5 * kk;
+						b4v[gi][q]        = *(const f4u*)b;
+						b5v[gi][q]        = b[4];
+					}
+				}
 #pragma unroll
 			for (int gi = 0; gi < 4; gi++) {
 				const int r = r0 + gi;
 #pragma unroll
 				for (int q = 0; q < 3; q++) {
-					const int  p   = (r & 1) + 2 * q;
-					const bool fwd = (p == 0 || p == 3 || p == 4);
-					float      xa, t;
+					const int   p  = (r & 1) + 2 * q;
+					const float h1 = h1v[gi][q], hd = frac1 (h1);
+					const f2u   dp = dpv[gi][q];
+					const float intp = dp.x * (1.f - hd) + hd * dp.y;
+					float       xa, t;
 					if (r < 2) {
 						/* HN_MOTION, src/whirl.cpp:1432-1453 */
-						const float*   hist = p < 2 ? sm.xf : (p < 4 ? sm.x1 : sm.x2);
-						const float*   dsp  = fwd ? hnFwd : hnBwd;
-						const float*   bw   = fwd ? bbw : bfw;
-						const double   ang  = ha + ((p & 1) ? K.bwAng : K.fwAng);
-						const float    h1   = (float)(ang * (unsigned int)16384 + K.hornPhase[p]);
-						const float    hd   = frac1 (h1);
-						const unsigned hl   = ((unsigned int)floorf (h1)) & 16383u;
-						const f2u      dp   = *(const f2u*)(dsp + hl); /* dsp[hl], dsp[(hl + 1) & 16383] */
-						const float    intp = dp.x * (1.f - hd) + hd * dp.y;
-						const unsigned kk   = ((unsigned int)roundf (h1)) & 16383u;
-						t                   = K.hornSpacing[p] + intp + (float)outpos;
-						const float* b      = bw + 5 * kk;
-						const f4u    b4     = *(const f4u*)b;
-						xa                  = b4.x * hist[n + 4];
+						const float* hist = p < 2 ? sm.xf : (p < 4 ? sm.x1 : sm.x2);
+						const f4u    b4   = b4v[gi][q];
+						t                 = K.hornSpacing[p] + intp + (float)outpos;
+						xa                = b4.x * hist[n + 4];
 						xa += b4.y * hist[n + 3];
 						xa += b4.z * hist[n + 2];
 						xa += b4.w * hist[n + 1];
-						xa += b[4] * hist[n + 0];
+						xa += b5v[gi][q] * hist[n + 0];
 					} else {
 						/* DR_MOTION, src/whirl.cpp:1455-1469 */
-						xa                  = p < 2 ? xin : (p < 4 ? xd1v : xd2v);
-						const float*   dsp  = fwd ? drFwd : drBwd;
-						const float    d1   = (float)(da * (unsigned int)16384 + K.hornPhase[p]);
-						const float    dd   = frac1 (d1);
-						const unsigned dl   = ((unsigned int)floorf (d1)) & 16383u;
-						const f2u      dp   = *(const f2u*)(dsp + dl); /* dsp[dl], dsp[(dl + 1) & 16383] */
-						const float    intp = dp.x * (1.f - dd) + dd * dp.y;
-						t                   = K.drumSpacing[p] + intp + (float)outpos;
+						xa = p < 2 ? xin : (p < 4 ? xd1v : xd2v);
+						t  = K.drumSpacing[p] + intp + (float)outpos;
 					}
 					const float rr = floorf (t);
 					const float qq = xa * (t - rr);
-					mu[gi][q]          = (int32_t)((unsigned int)rr) + unwrap;
-					ma[gi][q]          = xa - qq;
-					mb[gi][q]          = qq;
+					mu[gi][q]      = (int32_t)((unsigned int)rr) + unwrap;
+					ma[gi][q]      = xa - qq;
+					mb[gi][q]      = qq;
 				}
 			}
 			/* fast path preconditions (wave votes), per ring: each motion's slot

@@ -38,23 +38,60 @@
 #define NL 64
 #define NW TBF_NW
 
+/* the per-wheel arrays, staged in dynamic LDS for the launch's wheel count P.ctlNw (the
+ * largest wheel any play matrix names, + 1: 92 for the tonewheel organ, so ~13 KB and
+ * about 11 workgroups per CU instead of 4 at TBF_NW + 1) */
+struct CtlW {
+	float*    bl;      /* [nw][27] bus levels */
+	float*    sums;    /* [nw][6]  routed sums */
+	int32_t*  ref;     /* [nw] */
+	uint16_t* list;    /* [nw] activeOscList */
+	int16_t*  acl1;    /* [nw] */
+	uint16_t* removed; /* [nw] */
+	uint8_t*  rf;      /* [nw] */
+};
+#define CTL_MSGCAP 256 /* a launch's messages prefetched into LDS (more: read per block) */
+
 struct CtlLds {
-	float    bl[NW + 1][27]; /* the instance's bus levels and routed sums, staged for the launch */
-	float    sums[NW + 1][6];
-	int32_t  ref[NW + 1];
-	uint16_t list[NW + 1];
-	int16_t  acl1[NW + 1];
-	uint16_t removed[NW + 1];
-	uint8_t  rf[NW + 1];
 	float    dbg[27];
 	uint32_t L;
 	uint32_t nrem;
+	uint32_t mc0[CTL_MSGCAP], mc1[CTL_MSGCAP]; /* each message's keyContrib range */
+	uint16_t msg[CTL_MSGCAP];
 };
+
+__host__ __device__ constexpr size_t ctl_wbytes (uint32_t nw)
+{
+	return (size_t)nw * (27 * 4 + 6 * 4 + 4 + 2 + 2 + 2 + 1);
+}
+
+__device__ __forceinline__ CtlW ctl_carve (uint8_t* p, uint32_t nw)
+{
+	CtlW w;
+	w.bl      = (float*)p;
+	w.sums    = w.bl + (size_t)nw * 27;
+	w.ref     = (int32_t*)(w.sums + (size_t)nw * 6);
+	w.list    = (uint16_t*)(w.ref + nw);
+	w.acl1    = (int16_t*)(w.list + nw);
+	w.removed = (uint16_t*)(w.acl1 + nw);
+	w.rf      = (uint8_t*)(w.removed + nw);
+	return w;
+}
 
 __device__ __forceinline__ uint64_t lanemask_lt () { return (1ull << threadIdx.x) - 1ull; }
 
+/* the workgroup is one wave: LDS accesses of a wave execute in issue order, so a read
+ * after a write sees it; only the compiler must not move LDS accesses across this point
+ * (a __syncthreads also waited for every outstanding global store: the program stores) */
+__device__ __forceinline__ void wave_sync ()
+{
+	__builtin_amdgcn_fence (__ATOMIC_ACQ_REL, "wavefront");
+	__builtin_amdgcn_wave_barrier ();
+}
+
 /* one key message (src/tonegen.cpp:3270-3322) */
-__device__ void ctl_message (CtlLds& sm, const tbf_contrib* __restrict__ kc, uint32_t c0, uint32_t c1, bool on)
+__device__ void ctl_message (CtlLds& sm, const CtlW& W, const tbf_contrib* __restrict__ kc, uint32_t c0, uint32_t c1,
+                             bool on)
 {
 	const int lane = threadIdx.x;
 	for (uint32_t base = c0; base < c1; base += NL) {
@@ -80,61 +117,58 @@ __device__ void ctl_message (CtlLds& sm, const tbf_contrib* __restrict__ kc, uin
 		const int      part  = (int)(next - (uint32_t)lane);
 		bool           join  = false;
 		if (valid) {
-			float* bl = &sm.bl[w][bus];
+			float* bl = &W.bl[w * 27 + bus];
 			*bl       = on ? *bl + lev : *bl - lev;
 		}
 		if (owner) {
-			const int r0 = sm.ref[w];
+			const int r0 = W.ref[w];
 			if (on) {
 				if (lead && r0 == 0) {
-					sm.rf[w] = 0x0006;
-					join     = sm.acl1[w] == 0;
+					W.rf[w] = 0x0006;
+					join    = W.acl1[w] == 0;
 				} else {
-					sm.rf[w] |= 0x0004;
+					W.rf[w] |= 0x0004;
 				}
-				sm.ref[w] = r0 + part;
+				W.ref[w] = r0 + part;
 			} else {
 				const int r1 = r0 - part;
-				sm.ref[w]    = r1;
-				sm.rf[w]     = r1 == 0 ? 0x0005 : (sm.rf[w] | 0x0004);
+				W.ref[w]     = r1;
+				W.rf[w]      = r1 == 0 ? 0x0005 : (W.rf[w] | 0x0004);
 			}
 		}
 		const uint64_t jb = __ballot (join);
+		const uint32_t L  = __builtin_amdgcn_readfirstlane (sm.L);
 		if (join) {
-			const uint32_t pos = sm.L + (uint32_t)__builtin_popcountll (jb & lanemask_lt ());
-			sm.list[pos]       = (uint16_t)w;
-			sm.acl1[w]         = (int16_t)(pos + 1);
+			const uint32_t pos = L + (uint32_t)__builtin_popcountll (jb & lanemask_lt ());
+			W.list[pos]        = (uint16_t)w;
+			W.acl1[w]          = (int16_t)(pos + 1);
 		}
-		__syncthreads ();
+		wave_sync ();
 		if (lane == 0)
-			sm.L += (uint32_t)__builtin_popcountll (jb);
-		__threadfence_block ();
-		__syncthreads ();
+			sm.L = L + (uint32_t)__builtin_popcountll (jb);
+		wave_sync ();
 	}
 }
 
 /* the active-list loop and the removals of one block (src/tonegen.cpp:3333-3594); writes
  * the program (header + one entry per active wheel) at out */
-__device__ void ctl_block (CtlLds& sm, const tbf_tgc_rec& R, tbf_prog_entry* __restrict__ out)
+__device__ void ctl_block (CtlLds& sm, const CtlW& W, uint32_t flags, uint32_t routing, uint32_t percSendBus,
+                           tbf_prog_entry* __restrict__ out)
 {
-	const int      lane        = threadIdx.x;
-	const uint32_t L0          = sm.L;
-	const bool     dbChange    = (R.flags & 1) != 0;
-	const bool     recompute   = (R.flags & 2) != 0;
-	const uint32_t routing     = R.oldRouting;
-	const uint32_t percSendBus = R.percSendBus;
-	if (lane == 0)
-		sm.nrem = 0;
-	__syncthreads ();
+	const int      lane      = threadIdx.x;
+	const uint32_t L0        = __builtin_amdgcn_readfirstlane (sm.L);
+	const bool     dbChange  = (flags & 1) != 0;
+	const bool     recompute = (flags & 2) != 0;
+	uint32_t       nrem      = 0;
 	for (uint32_t base = 0; base < L0; base += NL) {
 		const uint32_t i     = base + lane;
 		const bool     valid = i < L0;
 		bool           rem   = false;
 		uint32_t       on    = 0;
 		if (valid) {
-			on                = sm.list[i];
-			const uint32_t rf = sm.rf[on];
-			float*         S  = sm.sums[on];
+			on                = W.list[i];
+			const uint32_t rf = W.rf[on];
+			float*         S  = W.sums + on * 6;
 			tbf_prog_entry E;
 			E.wheel = (uint16_t)on;
 			E.env = 0;
@@ -160,7 +194,7 @@ __device__ void ctl_block (CtlLds& sm, const tbf_tgc_rec& R, tbf_prog_entry* __r
 				}
 				bool reroute = false;
 				if ((rf & 0x0004) || dbChange) {
-					const float* bl  = sm.bl[on];
+					const float* bl  = W.bl + on * 27;
 					float        sum = 0.0f;
 					for (int d = 0; d < 9; d++)
 						sum += bl[d] * sm.dbg[d];
@@ -176,7 +210,7 @@ __device__ void ctl_block (CtlLds& sm, const tbf_tgc_rec& R, tbf_prog_entry* __r
 					reroute  = true;
 				}
 				if (reroute || recompute) {
-					sumPercn = (routing & 0x0C) ? sm.bl[on][percSendBus] : 0.0f;
+					sumPercn = (routing & 0x0C) ? W.bl[on * 27 + percSendBus] : 0.0f;
 					sumScanr = 0.0f;
 					sumSwell = sumPedal;
 					if (routing & 0x02)
@@ -202,89 +236,181 @@ __device__ void ctl_block (CtlLds& sm, const tbf_tgc_rec& R, tbf_prog_entry* __r
 					E.nvg = sumScanr;
 				}
 			}
-			sm.rf[on]  = 0;
+			W.rf[on]   = 0;
 			out[1 + i] = E;
 		}
 		const uint64_t rb = __ballot (rem);
 		if (rem)
-			sm.removed[sm.nrem + (uint32_t)__builtin_popcountll (rb & lanemask_lt ())] = (uint16_t)on;
-		__syncthreads ();
-		if (lane == 0)
-			sm.nrem += (uint32_t)__builtin_popcountll (rb);
-		__syncthreads ();
+			W.removed[nrem + (uint32_t)__builtin_popcountll (rb & lanemask_lt ())] = (uint16_t)on;
+		nrem += (uint32_t)__builtin_popcountll (rb);
 	}
+	wave_sync ();
 	if (lane == 0) {
 		tbf_prog_entry H = {};
 		H.wheel          = 0xFFFF;
 		H.pad            = L0;
 		out[0]           = H;
-		/* removal list, in order (3576-3594) */
-		uint32_t L = L0;
-		for (uint32_t r = 0; r < sm.nrem; r++) {
-			const uint32_t vic = sm.removed[r];
-			const int      act = sm.acl1[vic] - 1;
-			sm.acl1[vic]       = 0;
+	}
+	/* the removals (3576-3594): in order, each swapped with the list's last entry (lane 0;
+	 * a register-held list with ballot lookups measured slower) */
+	uint32_t L = L0;
+	if (lane == 0) {
+		for (uint32_t r = 0; r < nrem; r++) {
+			const uint32_t vic = W.removed[r];
+			const int      act = W.acl1[vic] - 1;
+			W.acl1[vic]        = 0;
 			L--;
 			if (0 < L) {
-				const uint32_t mov = sm.list[L];
+				const uint32_t mov = W.list[L];
 				if (mov != vic) {
-					sm.list[act]  = (uint16_t)mov;
-					sm.acl1[mov] = (int16_t)(act + 1);
+					W.list[act]  = (uint16_t)mov;
+					W.acl1[mov] = (int16_t)(act + 1);
 				}
 			}
 		}
-		sm.L = L;
 	}
-	__threadfence_block ();
-	__syncthreads ();
+	if (lane == 0)
+		sm.L = L;
+	wave_sync ();
 }
 
+/* One wave per instance with control deltas in the chunk.  The chunk's per-block inputs
+ * are read lane-parallel up front (lane b = block b: its pool index and record), and the
+ * messages of the launch with their keyContrib ranges into LDS, so a block's work waits on
+ * no chain of dependent global loads (index -> record -> message -> range, one after the
+ * other per block before).
+ * First every delta's control entry is written to the pool: a full entry as the host sent
+ * it (fulls), a patched one from the instance's entry before it -- the last full delta
+ * before it, else the persistent entry -- with the record's key-compression target,
+ * percussion reset and routing, and the program of the last stepped delta at or before it
+ * (else the persistent program).  Then the stepped blocks' per-wheel control in order. */
 __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_tgctl (const tbf_launch P)
 {
-	__shared__ CtlLds sm;
-	const int         lane = threadIdx.x;
-	const uint32_t    inst = P.ctlInst[blockIdx.x];
-	tbf_tgc_state*    G    = P.tgc + inst;
-	const uint32_t    tpl  = P.cst[inst].tpl;
-	const uint32_t*   coff = P.coff + (size_t)tpl * 385;
-	for (int i = lane; i < (NW + 1) * 27; i += NL)
-		(&sm.bl[0][0])[i] = (&G->busLevel[0][0])[i];
-	for (int i = lane; i < (NW + 1) * 6; i += NL)
-		(&sm.sums[0][0])[i] = (&G->sums[0][0])[i];
-	for (int w = lane; w <= NW; w += NL) {
-		sm.ref[w]  = G->refCount[w];
-		sm.list[w] = G->list[w];
-		sm.acl1[w] = G->aclPos1[w];
-		sm.rf[w]   = G->rflags[w];
+	__shared__ CtlLds         sm;
+	extern __shared__ uint8_t wdyn[];
+	const int                 lane = threadIdx.x;
+	const uint32_t            nw   = P.ctlNw;
+	const CtlW                W    = ctl_carve (wdyn, nw);
+	const uint32_t            inst = P.ctlInst[blockIdx.x];
+	tbf_tgc_state*            G    = P.tgc + inst;
+	const uint32_t            tpl  = P.cst[inst].tpl;
+	const uint32_t*           coff = P.coff + (size_t)tpl * 385;
+	const uint32_t            n    = P.nInst;
+	/* lane b: block b's pool index; a block starts a delta when its index differs from the
+	 * block before's (block 0: from the instance's persistent entry) */
+	const uint32_t nb    = P.nBlocks;
+	const uint32_t idx   = (uint32_t)lane < nb ? P.ctlIdx[(size_t)lane * n + inst] : inst;
+	const uint32_t pidx  = lane == 0 ? inst : (uint32_t)__shfl_up ((int)idx, 1);
+	const bool     isNew = (uint32_t)lane < nb && idx >= n && idx != pidx;
+	tbf_tgc_rec    R     = {};
+	if (isNew)
+		R = P.rec[idx - n];
+	{
+		const uint64_t le = lane == NL - 1 ? ~0ull : ((2ull << lane) - 1ull); /* lanes <= this one */
+		const uint64_t fm = __ballot (isNew && R.full != 0) & le, km = __ballot (isNew && (R.flags & 0x80)) & le;
+		const int      lf = fm ? 63 - __builtin_clzll (fm) : 0, ls = km ? 63 - __builtin_clzll (km) : 0;
+		const uint32_t ff = (uint32_t)__shfl ((int)R.full, lf), ki = (uint32_t)__shfl ((int)idx, ls);
+		if (isNew) {
+			/* word by word (a struct copy with patched fields went through scratch) */
+			const uint32_t* src = (const uint32_t*)(fm ? P.fulls + (ff - 1) : P.ctl + inst);
+			uint32_t*       dst = (uint32_t*)((tbf_seg_ctl*)P.ctl + idx);
+			const uint32_t  pp  = km ? P.progBase + (ki - n) * (uint32_t)TBF_PROG_SLOT : P.ctl[inst].prog_off;
+			const bool      pat = R.full == 0;
+#pragma unroll
+			for (int k = 0; k < (int)(sizeof (tbf_seg_ctl) / 4); k++) {
+				uint32_t v = src[k];
+				if (pat) {
+					if (k == (int)(offsetof (tbf_seg_ctl, prog_off) / 4))
+						v = pp;
+					else if (k == (int)(offsetof (tbf_seg_ctl, keyCompTarget) / 4))
+						v = __float_as_uint (R.keyCompTarget);
+					else if (k == (int)(offsetof (tbf_seg_ctl, resetPercAtEnd) / 4))
+						v = (R.flags >> 3) & 1u;
+					else if (k == (int)(offsetof (tbf_seg_ctl, routing) / 4))
+						v = R.oldRouting;
+				}
+				dst[k] = v;
+			}
+		}
+	}
+	const uint32_t poff = P.progBase + (idx - n) * (uint32_t)TBF_PROG_SLOT; /* a stepped delta's program */
+	const bool     stepped = isNew && (R.flags & 0x80);
+	const uint64_t todo0   = __ballot (stepped);
+	if (todo0 == 0)
+		return; /* control deltas without a tone-generator step */
+	/* the messages: lane b's R.nMsg at an exclusive prefix offset */
+	uint32_t nm = stepped ? R.nMsg : 0, mpos = nm;
+	for (int d = 1; d < NL; d <<= 1) {
+		const uint32_t v = (uint32_t)__shfl_up ((int)mpos, d);
+		if (lane >= d)
+			mpos += v;
+	}
+	const uint32_t M  = (uint32_t)__shfl ((int)mpos, NL - 1);
+	mpos -= nm;
+	const bool     pre = M <= CTL_MSGCAP;
+	for (size_t i = lane; i < (size_t)nw * 27; i += NL)
+		W.bl[i] = (&G->busLevel[0][0])[i];
+	for (size_t i = lane; i < (size_t)nw * 6; i += NL)
+		W.sums[i] = (&G->sums[0][0])[i];
+	for (uint32_t w = lane; w < nw; w += NL) {
+		W.ref[w]  = G->refCount[w];
+		W.list[w] = G->list[w];
+		W.acl1[w] = G->aclPos1[w];
+		W.rf[w]   = G->rflags[w];
 	}
 	if (lane == 0)
 		sm.L = G->listEnd;
 	if (lane < 27)
 		sm.dbg[lane] = G->gain[lane];
-	__syncthreads ();
-	const uint32_t n    = P.nInst;
-	uint32_t       prev = inst;
-	int64_t        last = -1; /* prog_off of the last program written */
-	for (uint32_t b = 0; b < P.nBlocks; b++) {
-		const uint32_t idx = P.ctlIdx[(size_t)b * n + inst];
-		if (idx == prev || idx < n)
-			continue;
-		prev                 = idx;
-		const tbf_tgc_rec& R = P.rec[idx - n];
-		if (!(R.flags & 0x80))
-			continue; /* a control change without a tone-generator step */
-		if ((R.flags & 4) && lane < 27)
-			sm.dbg[lane] = P.gains[R.gainOff + lane];
-		__syncthreads ();
-		for (uint32_t m = 0; m < R.nMsg; m++) {
-			const uint32_t msg = P.msgs[R.msgOff + m];
-			const uint32_t kn  = msg & 0x0fffu;
-			if (kn >= 384)
-				continue;
-			ctl_message (sm, P.contrib, coff[kn], coff[kn + 1], (msg & 0xf000u) == 0x1000u);
+	if (pre)
+		for (uint32_t m = 0; m < nm; m++)
+			sm.msg[mpos + m] = P.msgs[R.msgOff + m];
+	wave_sync ();
+	if (pre) {
+		for (uint32_t j = lane; j < M; j += NL) {
+			const uint32_t kn = sm.msg[j] & 0x0fffu;
+			sm.mc0[j]         = kn < 384 ? coff[kn] : 0u;
+			sm.mc1[j]         = kn < 384 ? coff[kn + 1] : 0u;
 		}
-		const uint32_t off = P.ctl[idx].prog_off;
-		ctl_block (sm, R, (tbf_prog_entry*)P.prog + off);
+		wave_sync ();
+	}
+	int64_t  last = -1; /* prog_off of the last program written */
+	uint64_t todo = todo0;
+	while (todo) {
+		const int b = __builtin_ctzll (todo);
+		todo &= todo - 1;
+		const uint32_t flags = (uint32_t)__builtin_amdgcn_readlane ((int)R.flags, b);
+		if (flags & 4) {
+			const uint32_t go = (uint32_t)__builtin_amdgcn_readlane ((int)R.gainOff, b);
+			const uint32_t ng = (uint32_t)__builtin_amdgcn_readlane ((int)R.pad, b);
+			if ((uint32_t)lane < ng) {
+				const uint32_t bus = __float_as_uint (P.gains[go + 2 * lane]);
+				sm.dbg[bus < 27 ? bus : 0] = P.gains[go + 2 * lane + 1];
+			}
+			wave_sync ();
+		}
+		const uint32_t bm = (uint32_t)__builtin_amdgcn_readlane ((int)nm, b);
+		const uint32_t bp = (uint32_t)__builtin_amdgcn_readlane ((int)mpos, b);
+		const uint32_t bo = (uint32_t)__builtin_amdgcn_readlane ((int)R.msgOff, b);
+		for (uint32_t m = 0; m < bm; m++) {
+			uint32_t msg, c0, c1;
+			if (pre) {
+				msg = sm.msg[bp + m];
+				c0  = sm.mc0[bp + m];
+				c1  = sm.mc1[bp + m];
+			} else {
+				msg                = P.msgs[bo + m];
+				const uint32_t kn0 = msg & 0x0fffu;
+				c0                 = kn0 < 384 ? coff[kn0] : 0u;
+				c1                 = kn0 < 384 ? coff[kn0 + 1] : 0u;
+			}
+			if ((msg & 0x0fffu) >= 384)
+				continue;
+			ctl_message (sm, W, P.contrib, c0, c1, (msg & 0xf000u) == 0x1000u);
+		}
+		const uint32_t off = (uint32_t)__builtin_amdgcn_readlane ((int)poff, b);
+		ctl_block (sm, W, flags, (uint32_t)__builtin_amdgcn_readlane ((int)R.oldRouting, b),
+		           (uint32_t)__builtin_amdgcn_readlane ((int)R.percSendBus, b), (tbf_prog_entry*)P.prog + off);
 		last = off;
 	}
 	/* the instance's last program becomes its persistent one, in the slot after the current
@@ -301,16 +427,16 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_tgctl (
 		for (uint32_t k = lane; k < cnt; k += NL)
 			d[k] = src[k];
 	}
-	__syncthreads ();
-	for (int i = lane; i < (NW + 1) * 27; i += NL)
-		(&G->busLevel[0][0])[i] = (&sm.bl[0][0])[i];
-	for (int i = lane; i < (NW + 1) * 6; i += NL)
-		(&G->sums[0][0])[i] = (&sm.sums[0][0])[i];
-	for (int w = lane; w <= NW; w += NL) {
-		G->refCount[w] = sm.ref[w];
-		G->list[w]     = sm.list[w];
-		G->aclPos1[w]  = sm.acl1[w];
-		G->rflags[w]   = sm.rf[w];
+	wave_sync ();
+	for (size_t i = lane; i < (size_t)nw * 27; i += NL)
+		(&G->busLevel[0][0])[i] = W.bl[i];
+	for (size_t i = lane; i < (size_t)nw * 6; i += NL)
+		(&G->sums[0][0])[i] = W.sums[i];
+	for (uint32_t w = lane; w < nw; w += NL) {
+		G->refCount[w] = W.ref[w];
+		G->list[w]     = W.list[w];
+		G->aclPos1[w]  = W.acl1[w];
+		G->rflags[w]   = W.rf[w];
 	}
 	if (lane == 0)
 		G->listEnd = sm.L;
@@ -322,6 +448,8 @@ extern "C" int tbf_launch_tgctl (const tbf_launch* P, hipStream_t stream)
 {
 	if (P->nCtlInst == 0)
 		return 0;
-	hipLaunchKernelGGL (k_tgctl, dim3 (P->nCtlInst), dim3 (NL), 0, stream, *P);
+	if (P->ctlNw == 0 || P->ctlNw > TBF_NW + 1 || P->nBlocks > NL)
+		return -22; /* the wheel count the play matrices name; one lane per block */
+	hipLaunchKernelGGL (k_tgctl, dim3 (P->nCtlInst), dim3 (NL), ctl_wbytes (P->ctlNw), stream, *P);
 	return hipGetLastError () == hipSuccess ? 0 : -5;
 }

@@ -478,6 +478,8 @@ int tbf_engine_destroy (tbf_engine* e)
 	e->dwh.release ();
 	e->dwhB.release ();
 	e->dctlInstB.release ();
+	e->dfull.release ();
+	e->dfullB.release ();
 	e->coff.release ();
 	e->contrib.release ();
 	e->vib.release ();
@@ -1022,6 +1024,9 @@ static int ensureDevice (tbf_engine* e)
 					for (const Contrib& c : e->tpls[q]->keyContrib[k])
 						ent.push_back ({(uint16_t)c.wheel, (uint16_t)c.bus, c.level});
 			}
+		e->ctlNw = 1;
+		for (const tbf_contrib& c : ent)
+			e->ctlNw = std::max<uint32_t> (e->ctlNw, (uint32_t)c.wheel + 1u);
 		if (e->coff.ensure (off.size ()) || e->contrib.ensure (std::max<size_t> (ent.size (), 1)))
 			return fail (-12, "out of device memory (play matrices)");
 		HIPCHK (hipMemcpy (e->coff.p, off.data (), off.size () * 4, hipMemcpyHostToDevice));
@@ -1157,7 +1162,7 @@ static bool stepControl (tbf_engine* e, uint32_t i, bool& progChanged, tbf_tgc_r
 	if (tgDirty && rec) {
 		/* device control: the front end here, the per-wheel part in k_tgctl */
 		const size_t k  = in.tg.msg.size ();
-		const size_t kg = in.tg.gainsDue () ? 27 : 0; /* the drawbar gains, when they changed */
+		const size_t kg = 2 * (size_t)in.tg.gainPairs (); /* the changed drawbar gains: (bus, gain) pairs */
 		if (msgOut) { /* a host worker's own message and gain lists (renderImpl merges them) */
 			const uint32_t at = (uint32_t)msgOut->size (), ag = (uint32_t)gainOut->size ();
 			msgOut->resize (at + k);
@@ -1246,6 +1251,8 @@ static int stepChunkParallel (tbf_engine* e, uint32_t n, uint32_t want, uint32_t
 		o.act.clear ();
 		o.ctlInst.clear ();
 		o.evs.clear ();
+		o.dInst.clear ();
+		o.fulls.clear ();
 		o.nd = 0;
 		o.rc = 0;
 		o.err.clear ();
@@ -1280,8 +1287,10 @@ static int stepChunkParallel (tbf_engine* e, uint32_t n, uint32_t want, uint32_t
 			}
 		});
 	}
-	e->dCtl.resize ((size_t)n * want);
 	e->hRec.resize ((size_t)n * want);
+	e->lastEmit.resize (n);
+	e->lastProg.resize (n);
+	e->dseen.assign (n, 0);
 	std::vector<uint32_t>& cur = e->curIdx;
 	const auto             ph0 = std::chrono::steady_clock::now ();
 	std::vector<uint64_t>  thNs (T);
@@ -1290,56 +1299,100 @@ static int stepChunkParallel (tbf_engine* e, uint32_t n, uint32_t want, uint32_t
 		tbf_engine::ParStep& o    = out[t];
 		const uint32_t       i0   = t * per, i1 = std::min (n, i0 + per);
 		const uint32_t       base = i0 * want;
-		tbf_seg_ctl*         Cc   = e->dCtl.data () + base; /* the worker's part of the staging */
-		tbf_tgc_rec*         Rr   = e->hRec.data () + base;
-		tlAct                     = &o.act;
-		size_t ep                 = 0;
+		tbf_tgc_rec*         Rr   = e->hRec.data () + base; /* the worker's part of the staging */
+		tlAct                     = &o.act; /* (markActive's pushes; o.act is rebuilt below) */
+		/* instance-major: an instance's blocks one after another, so its host state stays in
+		 * the core's L1 over the chunk (block-major passes over the range missed it on every
+		 * block).  Instances are independent; each keeps its events in order (a stable
+		 * counting sort of the range's events by instance). */
+		std::vector<uint32_t>& eo = o.eoff;
+		std::vector<uint32_t>& es = o.esort;
+		eo.assign ((size_t)(i1 - i0) + 1, 0);
+		for (uint32_t k : o.evs)
+			eo[ev[k].inst - i0 + 1]++;
 		for (uint32_t i = i0; i < i1; i++)
-			cur[i] = i;
-		for (uint32_t len = 0; len < want && !o.rc; len++) {
-			for (; ep < o.evs.size () && ev[o.evs[ep]].block <= b0 + len; ep++) {
-				if ((o.rc = applyEvent (e, ev[o.evs[ep]]))) {
-					o.err = g_err;
-					break;
-				}
-				markActive (e, ev[o.evs[ep]].inst); /* (control-function events do not mark) */
-			}
-			size_t keep = 0;
-			for (size_t a = 0; a < o.act.size (); a++) {
-				const uint32_t i = o.act[a];
-				bool           pc;
-				tbf_tgc_rec&   rec = Rr[o.nd];
-				if (stepControl (e, i, pc, &rec, &o.msgs, &o.gains, &o.whs)) {
-					const uint32_t d = base + o.nd;
-					tbf_seg_ctl&   c = Cc[o.nd++];
-					c                = e->hCtl[i];
-					if (pc) {
-						c.prog_off = (uint32_t)(PERSIST (n) + ((size_t)rp * n * TBF_CHUNK + d) * SLOT);
-						if (!e->stepped[i]) {
-							e->stepped[i] = 1;
-							o.ctlInst.push_back (i);
-						}
-					} else {
-						memset (&rec, 0, sizeof (rec));
-						if (cur[i] >= n)
-							c.prog_off = Cc[cur[i] - n - base].prog_off;
-					}
-					cur[i]        = n + d;
-					e->chg[i]     = 1;
-					o.act[keep++] = i;
-				} else
-					e->inAct[i] = 0;
-			}
-			o.act.resize (keep);
-			for (uint32_t i = i0; i < i1; i++)
-				e->hIdx[(size_t)len * n + i] = cur[i];
+			eo[i - i0 + 1] += eo[i - i0];
+		es.resize (o.evs.size ());
+		{
+			std::vector<uint32_t>& fill = o.efill;
+			fill.assign (eo.begin (), eo.end () - 1);
+			for (uint32_t k : o.evs)
+				es[fill[ev[k].inst - i0]++] = k;
 		}
+		for (uint32_t i = i0; i < i1 && !o.rc; i++) {
+			uint32_t ci = i; /* the instance's pool entry at the current block */
+			uint32_t k = eo[i - i0], kEnd = eo[i - i0 + 1];
+			for (uint32_t len = 0; len < want; len++) {
+				for (; k < kEnd && ev[es[k]].block <= b0 + len; k++) {
+					if ((o.rc = applyEvent (e, ev[es[k]]))) {
+						o.err = g_err;
+						break;
+					}
+					markActive (e, i);
+				}
+				if (o.rc)
+					break;
+				if (e->inAct[i]) {
+					bool         pc;
+					tbf_tgc_rec& rec = Rr[o.nd];
+					if (!e->dseen[i]) { /* the entry the device holds for i at the chunk start */
+						e->dseen[i]    = 1;
+						e->lastEmit[i] = e->hCtl[i];
+					}
+					if (stepControl (e, i, pc, &rec, &o.msgs, &o.gains, &o.whs)) {
+						const uint32_t d = base + o.nd++;
+						tbf_seg_ctl    c = e->hCtl[i];
+						if (pc) {
+							c.prog_off = (uint32_t)(PERSIST (n) + ((size_t)rp * n * TBF_CHUNK + d) * SLOT);
+							if (!e->stepped[i]) {
+								e->stepped[i] = 1;
+								o.ctlInst.push_back (i);
+							}
+						} else {
+							memset (&rec, 0, sizeof (rec));
+							if (ci >= n)
+								c.prog_off = e->lastProg[i];
+						}
+						e->lastProg[i] = c.prog_off;
+						if (!e->dhas[i]) {
+							e->dhas[i] = 1;
+							o.dInst.push_back (i);
+						}
+						/* a delta that changes only what a key / drawbar step changes travels as
+						 * its record (k_tgctl rebuilds the entry); any other change as a full entry */
+						tbf_seg_ctl& le = e->lastEmit[i];
+						tbf_seg_ctl  tc = le;
+						tc.prog_off       = c.prog_off;
+						tc.keyCompTarget  = c.keyCompTarget;
+						tc.resetPercAtEnd = c.resetPercAtEnd;
+						tc.routing        = c.routing;
+						if (memcmp (&tc, &c, sizeof (c)) != 0) {
+							o.fulls.push_back (c);
+							rec.full = (uint32_t)o.fulls.size ();
+							le       = c;
+						}
+						rec.keyCompTarget = c.keyCompTarget;
+						rec.flags         = (uint8_t)((rec.flags & ~8u) | (c.resetPercAtEnd ? 8u : 0u));
+						rec.oldRouting    = (uint8_t)c.routing;
+						ci                = n + d;
+						e->chg[i]         = 1;
+					} else
+						e->inAct[i] = 0;
+				}
+				e->hIdx[(size_t)len * n + i] = ci;
+			}
+			cur[i] = ci;
+		}
+		o.act.clear (); /* the range's instances still active, in order */
+		for (uint32_t i = i0; i < i1; i++)
+			if (e->inAct[i])
+				o.act.push_back (i);
 		tlAct = nullptr;
 		thNs[t] = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds> (std::chrono::steady_clock::now () - th0).count ();
 	});
 	const auto ph1 = std::chrono::steady_clock::now ();
-	std::vector<size_t> mb (T), gb (T), wb (T);
-	size_t              nm = 0, ng = 0, nw = 0;
+	std::vector<size_t> mb (T), gb (T), wb (T), fb (T);
+	size_t              nm = 0, ng = 0, nw = 0, nf = 0;
 	e->dSeg.clear ();
 	for (unsigned t = 0; t < T; t++) {
 		if (out[t].rc)
@@ -1350,6 +1403,8 @@ static int stepChunkParallel (tbf_engine* e, uint32_t n, uint32_t want, uint32_t
 		ng += out[t].gains.size ();
 		wb[t] = nw;
 		nw += out[t].whs.size ();
+		fb[t] = nf;
+		nf += out[t].fulls.size ();
 		if (out[t].nd) {
 			e->dSeg.push_back ({t * per * want, out[t].nd});
 			delta = true;
@@ -1360,19 +1415,25 @@ static int stepChunkParallel (tbf_engine* e, uint32_t n, uint32_t want, uint32_t
 	e->hMsg.resize (nm);
 	e->hGain.resize (ng);
 	e->hWh.resize (nw);
-	if (nm || ng || nw)
-		parallelFor (T, [&] (uint32_t t) { /* message, gain and whirl set offsets: worker-local -> chunk */
-			const tbf_engine::ParStep& o    = out[t];
-			const size_t               base = (size_t)t * per * want;
+	e->hFull.resize (nf);
+	if (nm || ng || nw || nf)
+		parallelFor (T, [&] (uint32_t t) { /* message, gain, full entry and whirl set offsets: worker-local -> chunk */
+			tbf_engine::ParStep& o    = out[t];
+			const size_t         base = (size_t)t * per * want;
 			for (size_t d = base; d < base + o.nd; d++) {
 				tbf_tgc_rec& r = e->hRec[d];
 				if (r.flags & 0x80)
 					r.msgOff += (uint32_t)mb[t];
 				if (r.flags & 4)
 					r.gainOff += (uint32_t)gb[t];
-				if (e->dCtl[d].whSet)
-					e->dCtl[d].whSet += (uint32_t)wb[t];
+				if (r.full)
+					r.full += (uint32_t)fb[t];
 			}
+			for (tbf_seg_ctl& f : o.fulls)
+				if (f.whSet)
+					f.whSet += (uint32_t)wb[t];
+			if (!o.fulls.empty ())
+				memcpy ((void*)(e->hFull.data () + fb[t]), o.fulls.data (), o.fulls.size () * sizeof (tbf_seg_ctl));
 			if (!o.whs.empty ())
 				memcpy ((void*)(e->hWh.data () + wb[t]), o.whs.data (), o.whs.size () * sizeof (tbf_wh_params));
 			if (!o.msgs.empty ())
@@ -1385,6 +1446,8 @@ static int stepChunkParallel (tbf_engine* e, uint32_t n, uint32_t want, uint32_t
 		e->actList.insert (e->actList.end (), out[t].act.begin (), out[t].act.end ());
 		for (uint32_t i : out[t].ctlInst)
 			e->hCtlInst.push_back (i);
+		for (uint32_t i : out[t].dInst)
+			e->hDInst.push_back (i);
 	}
 	if (getenv ("TBF_DEBUG_HOST_PHASES")) {
 		const auto ph2 = std::chrono::steady_clock::now ();
@@ -1573,6 +1636,8 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			e->hGain.swap (e->hGainB);
 			e->hWh.swap (e->hWhB);
 			e->hCtlInst.swap (e->hCtlInstB);
+			e->hDInst.swap (e->hDInstB);
+			e->hFull.swap (e->hFullB);
 			e->hIdx.swap (e->hIdxB);
 			e->hCtlPin.swap (e->hCtlPinB);
 			std::swap (e->upEv, e->upEvB);
@@ -1603,7 +1668,10 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		e->hGain.clear ();
 		e->hWh.clear ();
 		e->hCtlInst.clear ();
+		e->hDInst.clear ();
+		e->hFull.clear ();
 		e->stepped.assign (n, 0);
+		e->dhas.assign (n, 0);
 		e->hIdx.resize ((size_t)want * n);
 		std::vector<uint32_t>& cur = e->curIdx;
 		cur.resize (n);
@@ -1662,6 +1730,12 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 							if (cur[i] >= n)
 								c.prog_off = e->dCtl[cur[i] - n].prog_off;
 						}
+						if (!e->dhas[i]) {
+							e->dhas[i] = 1;
+							e->hDInst.push_back (i);
+						}
+						e->hFull.push_back (c); /* every delta a full entry on this path */
+						rec.full = (uint32_t)e->hFull.size ();
 						e->hRec.push_back (rec);
 					} else if (pc) {
 						c.prog_off = (uint32_t)(PERSIST (n) + e->dProg.size ());
@@ -1707,13 +1781,9 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 				return rc;
 			if ((rc = usWait ()))
 				return rc;
-			if (e->dSeg.empty ())
+			if (!e->devCtl) /* device control: k_tgctl writes the deltas' entries (records + full entries) */
 				HIPCHK (hipMemcpyAsync (e->ctl.p + rp * CTL_REGION (n) + n, e->dCtl.data (),
 				                        e->dCtl.size () * sizeof (tbf_seg_ctl), hipMemcpyHostToDevice, us));
-			for (const auto& g : e->dSeg) /* threaded host control: the workers' segments */
-				if (g.second)
-					HIPCHK (hipMemcpyAsync (e->ctl.p + rp * CTL_REGION (n) + n + g.first, e->dCtl.data () + g.first,
-					                        g.second * sizeof (tbf_seg_ctl), hipMemcpyHostToDevice, us));
 			if (!e->dProg.empty ())
 				HIPCHK (hipMemcpyAsync (e->prog.p + PERSIST (n), e->dProg.data (),
 				                        e->dProg.size () * sizeof (tbf_prog_entry), hipMemcpyHostToDevice, us));
@@ -1744,7 +1814,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		P.tgSplit = std::min (P.tgSplit, std::max (len, 1u));
 		P.outOffset = (uint64_t)b0 * TBF_BLK;
 		P.nCtlInst  = 0;
-		if (e->devCtl && !e->hCtlInst.empty ()) {
+		if (e->devCtl && !e->hDInst.empty ()) {
 			/* k_tgctl: the stepped blocks' programs, ahead of k_tonegen on this stream */
 			/* records per region parity: k_tgctl of the chunk before last (same stream, or
 			 * the caller's stream when not pipelined) read the other set */
@@ -1752,8 +1822,9 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			DevBuf<uint16_t>&    dmsg = rp ? e->dmsgB : e->dmsg;
 			DevBuf<float>&       dgn  = rp ? e->dgainB : e->dgain;
 			DevBuf<uint32_t>&    dci  = rp ? e->dctlInstB : e->dctlInst;
-			if (drec.cap < e->hRec.size () || dmsg.cap < e->hMsg.size () || dci.cap < e->hCtlInst.size () ||
-			    dgn.cap < e->hGain.size ())
+			DevBuf<tbf_seg_ctl>& dfl  = rp ? e->dfullB : e->dfull;
+			if (drec.cap < e->hRec.size () || dmsg.cap < e->hMsg.size () || dci.cap < e->hDInst.size () ||
+			    dgn.cap < e->hGain.size () || dfl.cap < e->hFull.size ())
 			{
 				if (getenv ("TBF_DEBUG_HOST_PHASES"))
 					fprintf (stderr, "chunk %llu: control record buffers grow (device sync)\n", (unsigned long long)e->chunkSeq);
@@ -1761,7 +1832,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			}
 			if (drec.ensure (e->hRec.size ()) || dmsg.ensure (std::max<size_t> (e->hMsg.size (), 1)) ||
 			    dgn.ensure (std::max<size_t> (e->hGain.size (), 27)) ||
-			    dci.ensure (e->hCtlInst.size ()))
+			    dci.ensure (e->hDInst.size ()) || dfl.ensure (std::max<size_t> (e->hFull.size (), 1)))
 				return fail (-12, "out of device memory (control records)");
 			if (e->dSeg.empty ())
 				HIPCHK (hipMemcpyAsync (drec.p, e->hRec.data (), e->hRec.size () * sizeof (tbf_tgc_rec),
@@ -1776,15 +1847,21 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			if (!e->hGain.empty ())
 				HIPCHK (hipMemcpyAsync (dgn.p, e->hGain.data (), e->hGain.size () * sizeof (float),
 				                        hipMemcpyHostToDevice, us));
-			HIPCHK (hipMemcpyAsync (dci.p, e->hCtlInst.data (), e->hCtlInst.size () * 4, hipMemcpyHostToDevice, us));
+			if (!e->hFull.empty ())
+				HIPCHK (hipMemcpyAsync (dfl.p, e->hFull.data (), e->hFull.size () * sizeof (tbf_seg_ctl),
+				                        hipMemcpyHostToDevice, us));
+			HIPCHK (hipMemcpyAsync (dci.p, e->hDInst.data (), e->hDInst.size () * 4, hipMemcpyHostToDevice, us));
 			P.tgc      = e->tgc.p;
 			P.rec      = drec.p;
 			P.msgs     = dmsg.p;
 			P.gains    = dgn.p;
 			P.ctlInst  = dci.p;
-			P.nCtlInst = (uint32_t)e->hCtlInst.size ();
+			P.nCtlInst = (uint32_t)e->hDInst.size ();
+			P.fulls    = dfl.p;
+			P.progBase = (uint32_t)(PERSIST (n) + (size_t)rp * n * TBF_CHUNK * SLOT);
 			P.coff     = e->coff.p;
 			P.contrib  = e->contrib.p;
+			P.ctlNw    = e->ctlNw;
 			if ((rc = tbf_launch_tgctl (&P, us)))
 				return fail (rc, std::string ("k_tgctl launch failed: ") + hipGetErrorString (hipGetLastError ()));
 		}

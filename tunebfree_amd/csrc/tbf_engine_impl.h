@@ -204,15 +204,22 @@ struct tbf_engine {
 	DevBuf<uint16_t>                        dmsg;
 	DevBuf<uint32_t>                        dctlInst;
 	DevBuf<uint32_t>                        coff;
+	uint32_t                                ctlNw = 1; /* k_tgctl's staged wheels (largest wheel in coff/contrib + 1) */
 	DevBuf<tbf_contrib>                     contrib;
 	PinnedVec<tbf_tgc_rec>                  hRec;     /* per delta of the chunk */
 	PinnedVec<uint16_t>                     hMsg;     /* the chunk's key messages */
-	PinnedVec<float>                        hGain;    /* the chunk's drawbar gain sets (27 each) */
+	PinnedVec<float>                        hGain;    /* the chunk's changed drawbar gains: (bus, gain) pairs */
 	PinnedVec<float>                        hGainB;
 	DevBuf<float>                           dgain, dgainB;
 	PinnedVec<tbf_wh_params>                hWh, hWhB; /* the chunk's whirl parameter sets (tbf_seg_ctl.whSet) */
 	DevBuf<tbf_wh_params>                   dwh, dwhB;
 	PinnedVec<uint32_t>                     hCtlInst; /* instances with a stepped delta */
+	PinnedVec<uint32_t>                     hDInst, hDInstB; /* instances with any delta: k_tgctl's grid */
+	PinnedVec<tbf_seg_ctl>                  hFull, hFullB;   /* the chunk's full control entries (tbf_tgc_rec.full) */
+	DevBuf<tbf_seg_ctl>                     dfull, dfullB;
+	std::vector<tbf_seg_ctl>                lastEmit; /* per instance: the last full entry the device holds (parallel front end) */
+	std::vector<uint8_t>                    dseen, dhas; /* per chunk: lastEmit taken / in hDInst */
+	std::vector<uint32_t>                   lastProg;    /* per instance: the last delta's prog_off */
 	/* the other parity of the chunk staging (the previous chunk's, in flight), and the
 	 * events after each parity's uploads */
 	PinnedVec<tbf_seg_ctl>                  dCtlB, hCtlPin, hCtlPinB;
@@ -236,7 +243,8 @@ struct tbf_engine {
 		std::vector<uint16_t> msgs;
 		std::vector<float>    gains;
 		std::vector<tbf_wh_params> whs;
-		std::vector<uint32_t> act, ctlInst, evs;
+		std::vector<uint32_t> act, ctlInst, evs, dInst, eoff, esort, efill;
+		std::vector<tbf_seg_ctl> fulls;
 		uint32_t              nd = 0;
 		int                   rc = 0;
 		std::string           err; /* the worker's tbf_last_error text (it is thread-local) */

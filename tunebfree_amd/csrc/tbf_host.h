@@ -193,6 +193,7 @@ struct TgControl {
 	uint32_t          vibTable = 2, vibMixed = 0;
 	bool              steadyPending = false; /* last block emitted env entries / removals */
 	bool              gainsSent = false;     /* the device holds drawBarGain (stepFront) */
+	uint32_t          gainMask  = 0;         /* buses whose drawBarGain changed since the last send */
 
 	void init (const TgTemplate* t, const Config& c);
 	void keyOn (int key);
@@ -214,8 +215,9 @@ struct TgControl {
 	 * wh (aot / active list / rflags) is not used. */
 	void stepFront (uint16_t* msgDst, uint32_t msgOff, float* gainDst, uint32_t gainOff, tbf_tgc_rec& rec,
 	                tbf_seg_ctl& ctl);
-	/* stepFront sends the 27 drawbar gains (gainDst) on this step */
-	bool gainsDue () const { return drawBarChange || !gainsSent; }
+	/* the (bus, gain) pairs stepFront sends on this step (gainDst: 2 words each): the changed
+	 * buses, or all 27 until the device holds them */
+	uint32_t gainPairs () const { return !gainsSent ? 27u : (uint32_t)__builtin_popcount (gainMask); }
 	void mixCtl (tbf_seg_ctl& ctl) const;
 };
 

@@ -836,6 +836,7 @@ void TgControl::setDrawBar (int bus, unsigned setting)
 			return;
 	}
 	drawBarGain[bus] = drawBarLevel[bus][setting];
+	gainMask |= 1u << bus;
 }
 
 void TgControl::setVibratoUpper (int on) { newRouting = on ? (newRouting | 0x02u) : (newRouting & ~0x02u); }
@@ -857,12 +858,14 @@ void TgControl::setPercEnabled (int on)
 		newRouting |= 0x0C;
 		if (-1 < percTriggerBus) {
 			drawBarGain[percTriggerBus] = 0.0f;
+			gainMask |= 1u << percTriggerBus;
 			drawBarChange               = 1;
 		}
 	} else {
 		newRouting &= ~0x0Cu;
 		if (-1 < percTriggerBus) {
 			drawBarGain[percTriggerBus] = drawBarLevel[percTriggerBus][percTrigRestore];
+			gainMask |= 1u << percTriggerBus;
 			drawBarChange               = 1;
 		}
 	}
@@ -1051,7 +1054,7 @@ void TgControl::step (std::vector<tbf_prog_entry>& prog, tbf_seg_ctl& ctl)
 void TgControl::stepFront (uint16_t* msgDst, uint32_t msgOff, float* gainDst, uint32_t gainOff, tbf_tgc_rec& rec,
                            tbf_seg_ctl& ctl)
 {
-	const bool sendGains = gainsDue (); /* gainDst holds 27 floats then */
+	const uint32_t ng = gainPairs (); /* gainDst holds ng (bus, gain) pairs */
 	memset (&rec, 0, sizeof (rec));
 	rec.msgOff = msgOff;
 	rec.nMsg   = (uint32_t)msg.size (); /* every message of the block, as the host path */
@@ -1059,14 +1062,23 @@ void TgControl::stepFront (uint16_t* msgDst, uint32_t msgOff, float* gainDst, ui
 	const bool recompute = oldRouting != newRouting;
 	if (recompute)
 		oldRouting = newRouting;
-	rec.flags       = (uint8_t)(0x80 | (drawBarChange ? 1 : 0) | (recompute ? 2 : 0) | (sendGains ? 4 : 0));
+	rec.flags       = (uint8_t)(0x80 | (drawBarChange ? 1 : 0) | (recompute ? 2 : 0) | (ng ? 4 : 0));
 	rec.oldRouting  = (uint8_t)oldRouting;
-	rec.percSendBus = (uint16_t)percSendBus;
-	if (sendGains) {
-		memcpy (gainDst, drawBarGain, sizeof (drawBarGain));
+	rec.percSendBus = (uint8_t)percSendBus;
+	if (ng) {
+		const uint32_t m = gainsSent ? gainMask : (1u << 27) - 1u;
+		uint32_t       j = 0;
+		for (uint32_t bus = 0; bus < 27; bus++)
+			if ((m >> bus) & 1u) {
+				gainDst[2 * j]     = __builtin_bit_cast (float, bus);
+				gainDst[2 * j + 1] = drawBarGain[bus];
+				j++;
+			}
 		rec.gainOff = gainOff;
-		gainsSent   = true;
+		rec.pad     = (uint8_t)ng;
 	}
+	gainsSent = true;
+	gainMask  = 0;
 	/* a block with inputs makes the next block's program differ (envelopes end, released
 	 * wheels leave, rerouted sums take over: the device's steadyPending); a block with
 	 * none leaves it unchanged, so stepping once after each input block is exact */

@@ -35,12 +35,17 @@
 /* occupancy targets (waves per SIMD); LDS and VGPR budgets are sized for them */
 #define TG_WAVES 4
 #define TG_SPLIT_MAX 8 /* k_tonegen block ranges (waves) per instance */
+#define TG_PCAP 128    /* a delta chunk's program entries staged in LDS per block (longer: read from HBM) */
 #define RV_WAVES 3
 #define WH_WAVES 3
 /* wave priority raised (s_setprio 1) while a wave runs a serial chain, so the SIMD issues
  * the chain's dependent instructions ahead of other waves' lane-parallel work */
 #define PRIO_UP() __builtin_amdgcn_s_setprio (1)
 #define PRIO_DOWN() __builtin_amdgcn_s_setprio (0)
+
+template <bool B> struct BoolC {
+	static constexpr bool value = B;
+};
 
 /* ------------------------------------------------------------------ LDS layouts */
 struct TgLds {
@@ -52,6 +57,9 @@ struct TgLds {
 		struct { /* core-program entries resolved by the interpreter prologue */
 			uint32_t base[TBF_NW + 8]; /* bank index of the wheel's current sample (the device
 			                            * bank repeats each wave's first 128 samples after it) */
+			float4   g[TG_PCAP];       /* {sg, pg, vg, nsg} of a program of <= TG_PCAP entries ... */
+			float2   h[TG_PCAP];       /* ... {npg, nvg} */
+			uint32_t er[TG_PCAP];      /* ... env | row << 8 */
 		} ent;
 		struct { /* vibrato */
 			float   vout[TBF_BLK];
@@ -225,15 +233,26 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 	 * advance st.pos (each wheel appears once per program).  The device bank repeats each
 	 * wave's first 128 samples after its end, so the reference's wrap split
 	 * (src/tonegen.cpp:3376-3402) is plain indexing from base. */
-	int envHere = 0;
+	/* A delta chunk (P.ctlIdx) plays a program k_tgctl has just written, a new one on every
+	 * block under dense events: its entries are read once, lane-parallel, into LDS here, for
+	 * the main loop's broadcast reads (the main loop's scalar loads of them missed the
+	 * scalar cache four entries at a time).  A chunk without deltas replays one program,
+	 * whose entries stay in the scalar cache. */
+	const bool lp      = P.ctlIdx != nullptr && np <= TG_PCAP;
+	int        envHere = 0;
 	for (int e = lane; e < np; e += NL) {
-		const tbf_prog_entry& E   = prog[e];
-		const uint32_t        w   = E.wheel;
-		const uint32_t        pos = st.pos[w];
-		const uint32_t        len = T->len[w];
-		sm.u.ent.base[e]          = T->off[w] + pos;
-		st.pos[w]                 = (len < pos + TBF_BLK) ? pos + TBF_BLK - len : pos + TBF_BLK;
-		envHere |= E.env != 0;
+		const uint32_t w   = prog[e].wheel;
+		const uint32_t pos = st.pos[w];
+		const uint32_t len = T->len[w];
+		sm.u.ent.base[e]   = T->off[w] + pos;
+		st.pos[w]          = (len < pos + TBF_BLK) ? pos + TBF_BLK - len : pos + TBF_BLK;
+		envHere |= prog[e].env != 0;
+		if (lp) {
+			const uint4 a = ((const uint4*)(prog + e))[0], b = ((const uint4*)(prog + e))[1];
+			sm.u.ent.g[e] = make_float4 (__uint_as_float (a.y), __uint_as_float (a.z), __uint_as_float (a.w), __uint_as_float (b.x));
+			sm.u.ent.h[e] = make_float2 (__uint_as_float (b.y), __uint_as_float (b.z));
+			sm.u.ent.er[e] = a.x >> 16; /* env | row << 8 */
+		}
 	}
 	const bool anyEnv = __any (envHere);
 	wave_sync ();
@@ -243,38 +262,64 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 	 * loops have no data-dependent branch, so the unrolled entries' loads are in flight
 	 * together.  The sums start at -0.f: -0 + a == a for every a, so the first entry's add
 	 * equals the reference's copy (CR_CPY). */
-	f2v sw = {-0.f, -0.f}, vb = {-0.f, -0.f}, pc = {-0.f, -0.f};
-	if (!anyEnv) { /* steady program: x * g (src/tonegen.cpp:3667-3685) */
-#pragma unroll 4
-		for (int e = 0; e < np; e++) {
-			const float* __restrict__ bp = P.bank + sm.u.ent.base[e];
-			const f2v                 x  = {bp[lane], bp[lane + NL]};
-			const tbf_prog_entry&     E  = prog[e];
-			sw = sw + x * E.sg;
-			vb = vb + x * E.vg;
-			pc = pc + x * E.pg;
-		}
-	} else { /* envelope entries x * (g + e (ng - g)) (3640-3662), steady entries x * g as above
-	          * (the reference's g + e (ng - g) with e = -0 and ng - g = +0 is g for every g); the
-	          * branch is wave-uniform, so only envelope entries load envelope rows */
-#pragma unroll 4
-		for (int e = 0; e < np; e++) {
-			const float* __restrict__ bp = P.bank + sm.u.ent.base[e];
-			const f2v                 x  = {bp[lane], bp[lane + NL]};
-			const tbf_prog_entry&     E  = prog[e];
-			if (E.env) {
-				const float* ep = (E.env == 2 ? T->releaseEnv[E.row & 7] : T->attackEnv[E.row & 7]);
-				const f2v    ev = {ep[lane], ep[lane + NL]};
-				sw              = sw + x * (E.sg + (ev * (E.nsg - E.sg)));
-				vb              = vb + x * (E.vg + (ev * (E.nvg - E.vg)));
-				pc              = pc + x * (E.pg + (ev * (E.npg - E.pg)));
+	f2v  sw = {-0.f, -0.f}, vb = {-0.f, -0.f}, pc = {-0.f, -0.f};
+	auto loops = [&] (auto LP) {
+		constexpr bool L = decltype (LP)::value;
+		/* entry e's gains {sg, pg, vg, nsg, npg, nvg} and env | row << 8 */
+		auto ent = [&] (int e, float (&g)[6], uint32_t& er) {
+			if constexpr (L) {
+				const float4 a = sm.u.ent.g[e];
+				const float2 b = sm.u.ent.h[e];
+				g[0] = a.x; g[1] = a.y; g[2] = a.z; g[3] = a.w; g[4] = b.x; g[5] = b.y;
+				er = sm.u.ent.er[e];
 			} else {
-				sw = sw + x * E.sg;
-				vb = vb + x * E.vg;
-				pc = pc + x * E.pg;
+				const tbf_prog_entry& E = prog[e];
+				g[0] = E.sg; g[1] = E.pg; g[2] = E.vg; g[3] = E.nsg; g[4] = E.npg; g[5] = E.nvg;
+				er = (uint32_t)E.env | ((uint32_t)E.row << 8);
+			}
+		};
+		if (!anyEnv) { /* steady program: x * g (src/tonegen.cpp:3667-3685) */
+#pragma unroll 4
+			for (int e = 0; e < np; e++) {
+				const float* __restrict__ bp = P.bank + sm.u.ent.base[e];
+				const f2v                 x  = {bp[lane], bp[lane + NL]};
+				float                     g[6];
+				uint32_t                  er;
+				ent (e, g, er);
+				sw = sw + x * g[0];
+				vb = vb + x * g[2];
+				pc = pc + x * g[1];
+			}
+		} else { /* envelope entries x * (g + e (ng - g)) (3640-3662), steady entries x * g as
+		          * above.  Every entry loads an envelope row (a steady entry's row 0 of the
+		          * attack table, an L1 hit) and selects its gains: no load sits under a branch,
+		          * so the unrolled entries' loads stay in flight together */
+#pragma unroll 4
+			for (int e = 0; e < np; e++) {
+				const float* __restrict__ bp = P.bank + sm.u.ent.base[e];
+				const f2v                 x  = {bp[lane], bp[lane + NL]};
+				float                     g[6];
+				uint32_t                  er;
+				ent (e, g, er);
+				const uint32_t env = er & 0xffu, row = (er >> 8) & 7u;
+				const float*   ep  = (env == 2 ? T->releaseEnv[row] : T->attackEnv[row]);
+				const f2v      ev  = {ep[lane], ep[lane + NL]};
+				f2v            gs = {g[0], g[0]}, gv = {g[2], g[2]}, gp = {g[1], g[1]};
+				if (env) {
+					gs = g[0] + (ev * (g[3] - g[0]));
+					gv = g[2] + (ev * (g[5] - g[2]));
+					gp = g[1] + (ev * (g[4] - g[1]));
+				}
+				sw = sw + x * gs;
+				vb = vb + x * gv;
+				pc = pc + x * gp;
 			}
 		}
-	}
+	};
+	if (lp)
+		loops (BoolC<true> {});
+	else
+		loops (BoolC<false> {});
 	if (np == 0) /* no program: the buses stay cleared (+0) */
 		sw = vb = pc = f2v{0.f, 0.f};
 	wave_sync (); /* the entry table is overwritten below */

@@ -44,11 +44,18 @@ typedef struct tbf_prog_entry {
 typedef struct tbf_tgc_rec {
 	uint32_t msgOff;         /* the block's key messages (0x1000 | key: on, key: off) ... */
 	uint32_t nMsg;           /* ... msgs[msgOff .. msgOff + nMsg), all of the block's */
-	uint32_t gainOff;        /* flags & 4: the instance's drawBarGain[27] at gains[gainOff ..]
-	                          * (sent when they change; k_tgctl keeps them in tbf_tgc_state) */
-	uint8_t  flags;          /* 1 drawBarChange, 2 recomputeRouting, 4 gains follow, 0x80 stepped */
+	uint32_t gainOff;        /* flags & 4: pad (bus, drawBarGain[bus]) pairs at gains[gainOff ..], the
+	                          * bus as the float's bits (the buses that changed; k_tgctl keeps all 27
+	                          * in tbf_tgc_state) */
+	uint32_t full;           /* > 0: the delta's control entry is fulls[full - 1]; 0: the instance's
+	                          * entry before it with the fields below (a key / drawbar step changes
+	                          * no others), so only these 24 B cross PCIe, not the 120-B entry */
+	float    keyCompTarget;  /* (full == 0) keyCompTable[keyDownCount] */
+	uint8_t  flags;          /* 1 drawBarChange, 2 recomputeRouting, 4 gains follow, 8 resetPercAtEnd
+	                          * (full == 0), 0x80 stepped */
 	uint8_t  oldRouting;     /* routing word after this block's update */
-	uint16_t percSendBus;    /* a bus index (< 27) */
+	uint8_t  percSendBus;    /* a bus index (< 27) */
+	uint8_t  pad;            /* flags & 4: the number of gain pairs */
 } tbf_tgc_rec;
 
 /* one keyContrib element on the device (Contrib): a key's list is sorted by wheel, then
@@ -254,6 +261,9 @@ typedef struct tbf_launch {
 	uint32_t*             rvWork;    /* k_rv_core_lds work counter */
 	const uint32_t*       coff;      /* [tpl][385] keyContrib offsets into contrib */
 	const tbf_contrib*    contrib;
+	uint32_t              ctlNw;     /* k_tgctl's staged wheels: the largest wheel a play matrix names, + 1 */
+	const tbf_seg_ctl*    fulls;     /* the chunk's full control entries (tbf_tgc_rec.full) */
+	uint32_t              progBase;  /* program slot of delta d (pool index nInst + d): progBase + d * TBF_PROG_SLOT */
 } tbf_launch;
 
 #endif

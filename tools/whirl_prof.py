@@ -8,7 +8,7 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "tests"))
 
-NAMES = {9: "speed (lane 0)", 1: "ring read/clear", 3: "xn + serial filters", 4: "filter outputs + angles",
+NAMES = {10: "block start", 9: "speed (lane 0)", 1: "ring read/clear", 3: "xn + serial filters", 4: "filter outputs + angles",
          5: "FILTER_C", 6: "motions (tables)", 7: "ring adds", 8: "outputs + carry"}
 
 

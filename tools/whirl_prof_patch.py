@@ -31,6 +31,7 @@ s = s.replace("\t\t\tbool     okr[4];", mark(6).replace("\n\t\t", "\n\t\t\t") + 
 s = s.replace("\t\t/* ---- outputs (whirlProc2 outHL/outHR/outDL/outDR + whirlProc3 mix) ---- */",
               mark(7)[1:] + "\n\t\t/* ---- outputs (whirlProc2 outHL/outHR/outDL/outDR + whirlProc3 mix) ---- */")
 s = ins_after(s, "\t\t\tst.outpos = (st.outpos + TBF_SUB) & 2047u;\n\t\twave_sync ();", mark(8))
+s = s.replace("\tif (lane == 0) {\n\t\tint brake;", mark(10)[1:].replace("\t\tif", "\tif", 1) + "\n\tif (lane == 0) {\n\t\tint brake;")
 # init and write-out in k_whirl
 s = s.replace("\tif (threadIdx.x == 0)\n\t\tsm.aReady = 0;",
               "\tif (threadIdx.x == 0)\n\t\tsm.aReady = 0;\n\tif (threadIdx.x < 16) sm.wp[threadIdx.x] = 0;\n"

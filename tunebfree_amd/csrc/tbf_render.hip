@@ -46,6 +46,9 @@
 template <bool B> struct BoolC {
 	static constexpr bool value = B;
 };
+template <int K> struct IntC {
+	static constexpr int value = K;
+};
 
 /* ------------------------------------------------------------------ LDS layouts */
 struct TgLds {
@@ -268,53 +271,64 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 		/* entry e's gains {sg, pg, vg, nsg, npg, nvg} and env | row << 8 */
 		auto ent = [&] (int e, float (&g)[6], uint32_t& er) {
 			if constexpr (L) {
+				/* broadcast reads made wave-uniform (readfirstlane): the envelope branch below
+				 * is then a scalar branch, so a steady entry skips the envelope arithmetic */
 				const float4 a = sm.u.ent.g[e];
 				const float2 b = sm.u.ent.h[e];
-				g[0] = a.x; g[1] = a.y; g[2] = a.z; g[3] = a.w; g[4] = b.x; g[5] = b.y;
-				er = sm.u.ent.er[e];
+				auto rfl = [] (float v) { return __int_as_float (__builtin_amdgcn_readfirstlane (__float_as_int (v))); };
+				g[0] = rfl (a.x); g[1] = rfl (a.y); g[2] = rfl (a.z); g[3] = rfl (a.w); g[4] = rfl (b.x); g[5] = rfl (b.y);
+				er = (uint32_t)__builtin_amdgcn_readfirstlane ((int)sm.u.ent.er[e]);
 			} else {
 				const tbf_prog_entry& E = prog[e];
 				g[0] = E.sg; g[1] = E.pg; g[2] = E.vg; g[3] = E.nsg; g[4] = E.npg; g[5] = E.nvg;
 				er = (uint32_t)E.env | ((uint32_t)E.row << 8);
 			}
 		};
-		if (!anyEnv) { /* steady program: x * g (src/tonegen.cpp:3667-3685) */
-#pragma unroll 4
-			for (int e = 0; e < np; e++) {
-				const float* __restrict__ bp = P.bank + sm.u.ent.base[e];
-				const f2v                 x  = {bp[lane], bp[lane + NL]};
-				float                     g[6];
-				uint32_t                  er;
-				ent (e, g, er);
-				sw = sw + x * g[0];
-				vb = vb + x * g[2];
-				pc = pc + x * g[1];
-			}
-		} else { /* envelope entries x * (g + e (ng - g)) (3640-3662), steady entries x * g as
-		          * above.  Every entry loads an envelope row (a steady entry's row 0 of the
-		          * attack table, an L1 hit) and selects its gains: no load sits under a branch,
-		          * so the unrolled entries' loads stay in flight together */
-#pragma unroll 4
-			for (int e = 0; e < np; e++) {
-				const float* __restrict__ bp = P.bank + sm.u.ent.base[e];
-				const f2v                 x  = {bp[lane], bp[lane + NL]};
-				float                     g[6];
-				uint32_t                  er;
-				ent (e, g, er);
-				const uint32_t env = er & 0xffu, row = (er >> 8) & 7u;
-				const float*   ep  = (env == 2 ? T->releaseEnv[row] : T->attackEnv[row]);
-				const f2v      ev  = {ep[lane], ep[lane + NL]};
-				f2v            gs = {g[0], g[0]}, gv = {g[2], g[2]}, gp = {g[1], g[1]};
-				if (env) {
-					gs = g[0] + (ev * (g[3] - g[0]));
-					gv = g[2] + (ev * (g[5] - g[2]));
-					gp = g[1] + (ev * (g[4] - g[1]));
+		/* groups of four entries: every load of a group (bank samples, envelope rows) is
+		 * issued before its arithmetic, the remainder one entry at a time */
+		auto group = [&] (int e, auto KC, auto EC) {
+			constexpr int  K  = decltype (KC)::value;
+			constexpr bool EN = decltype (EC)::value; /* the block has envelope entries */
+			f2v      xs[K], evs[K];
+			float    gg[K][6];
+			uint32_t ers[K];
+#pragma unroll
+			for (int k = 0; k < K; k++) {
+				const float* __restrict__ bp = P.bank + sm.u.ent.base[e + k];
+				xs[k]                        = f2v {bp[lane], bp[lane + NL]};
+				ent (e + k, gg[k], ers[k]);
+				if constexpr (EN) { /* (a steady entry loads row 0 of the attack table: an L1 hit) */
+					const uint32_t env = ers[k] & 0xffu, row = (ers[k] >> 8) & 7u;
+					const float*   ep  = (env == 2 ? T->releaseEnv[row] : T->attackEnv[row]);
+					evs[k]             = f2v {ep[lane], ep[lane + NL]};
 				}
-				sw = sw + x * gs;
-				vb = vb + x * gv;
-				pc = pc + x * gp;
 			}
-		}
+#pragma unroll
+			for (int k = 0; k < K; k++) {
+				const float* g = gg[k];
+				if (EN && (ers[k] & 0xffu)) {
+					/* envelope entry x * (g + e (ng - g)) (src/tonegen.cpp:3640-3662) */
+					sw = sw + xs[k] * (g[0] + (evs[k] * (g[3] - g[0])));
+					vb = vb + xs[k] * (g[2] + (evs[k] * (g[5] - g[2])));
+					pc = pc + xs[k] * (g[1] + (evs[k] * (g[4] - g[1])));
+				} else { /* x * g (3667-3685) */
+					sw = sw + xs[k] * g[0];
+					vb = vb + xs[k] * g[2];
+					pc = pc + xs[k] * g[1];
+				}
+			}
+		};
+		auto run = [&] (auto EC) {
+			int e = 0;
+			for (; e + 4 <= np; e += 4)
+				group (e, IntC<4> {}, EC);
+			for (; e < np; e++)
+				group (e, IntC<1> {}, EC);
+		};
+		if (anyEnv)
+			run (BoolC<true> {});
+		else
+			run (BoolC<false> {});
 	};
 	if (lp)
 		loops (BoolC<true> {});

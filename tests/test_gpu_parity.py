@@ -357,6 +357,74 @@ def test_gpu_dense_events_threaded_host_control(oracle):
     assert max(eL, eR) <= TOL
 
 
+def test_gpu_mixed_events_threaded_full_and_patched_entries(oracle):
+    """The threaded front end sends a control delta as a 24-B record when only what a key
+    or drawbar step changes has changed, and k_tgctl rebuilds its entry from the entry
+    before it; any other change travels as a full entry.  1100 instances, 70 blocks: a key
+    change on every block (records) mixed with overdrive character, rotor speed (a one-shot
+    field), reverb mix, swell and percussion changes (full entries and routing patches) at
+    staggered blocks.  Bit for bit against the serial front end (every delta a full entry)
+    and against the oracle for a sample."""
+    import os
+    import torch
+    import tunebfree_amd as T
+    from orc_bind import Template
+    n, nb = 1100, 70
+    seeds = [5000 + i for i in range(n)]
+    rows, oscen = [], [[] for _ in range(n)]
+
+    def ev(b, i, kind, a, v):
+        rows.append((b, i, 0 if kind == "note" else 1, a, float(v)))
+        oscen[i].append((b, kind, a, v))
+
+    for i in range(n):
+        for (k, a, v) in S.jazz1_params():
+            ev(0, i, k, a, v)
+        for k in S.chord_for(i):
+            ev(0, i, "note", k, 1)
+        for b in range(1, nb):
+            ev(b, i, "note", 60 + (i + b - 1) % 12, 0)
+            ev(b, i, "note", 60 + (i + b) % 12, 1)
+            if i % 3 == 0 and b % 6 == 0:
+                ev(b, i, "param", S.P_CHARACTER, ((i + b) % 10) / 10.0)
+            if i % 3 == 1 and b % 9 == 0:
+                ev(b, i, "param", S.P_HORN, (b // 9) % 3)
+            if i % 5 == 0 and b % 11 == 0:
+                ev(b, i, "param", S.P_REVERB, ((i + b) % 7) / 7.0)
+            if i % 7 == 0 and b % 10 == 0:
+                ev(b, i, "param", S.P_SWELL, ((i + b) % 5) / 5.0)
+            if i % 3 == 2 and b % 13 == 0:
+                ev(b, i, "param", S.P_PERC, (b // 13) % 2)
+    rows.sort(key=lambda r: r[0])
+    outs = []
+    for serial in (False, True):
+        if serial:
+            os.environ["TBF_HOST_SERIAL"] = "1"
+        try:
+            eng = T.Engine(sample_rate=48000.0, device=0)
+        finally:
+            os.environ.pop("TBF_HOST_SERIAL", None)
+        tid = eng.template(seed=7)
+        eng.add_instances([tid] * n, seeds)
+        evs = eng.events(rows)
+        L = torch.zeros((n, nb * 128), dtype=torch.float32, device="cuda")
+        R = torch.zeros_like(L)
+        eng.render_events_device(nb, evs, L.data_ptr(), R.data_ptr(), nb * 128)
+        eng.synchronize()
+        outs.append((L.cpu().numpy(), R.cpu().numpy()))
+        eng.close()
+        del L, R
+    assert np.array_equal(outs[0][0].view(np.uint32), outs[1][0].view(np.uint32))
+    assert np.array_equal(outs[0][1].view(np.uint32), outs[1][1].view(np.uint32))
+    sample = [0, 1, 2, 35, 700, n - 1]
+    tpl = Template(oracle, seed=7)
+    oL, oR, *_ = oracle_run(oracle, tpl, [seeds[i] for i in sample], [sorted(oscen[i], key=lambda r: r[0]) for i in sample], nb)
+    eL, xL = compare(outs[0][0][sample], oL)
+    eR, xR = compare(outs[0][1][sample], oR)
+    print(f"mixed events, threaded vs oracle: max|err| L={eL:.3g} R={eR:.3g} bit-exact {xL:.6f} {xR:.6f}")
+    assert max(eL, eR) <= TOL
+
+
 def test_gpu_threaded_host_control_reports_errors():
     """A bad event met by a host worker (threaded front end, >= 1024 instances) fails the
     call with the worker's message, as the serial loop would (the message is thread-local)."""

@@ -425,6 +425,75 @@ def test_gpu_mixed_events_threaded_full_and_patched_entries(oracle):
     assert max(eL, eR) <= TOL
 
 
+def test_gpu_device_front_end_note_chunks(oracle):
+    """Chunks whose events are all notes, over instances with no other control change
+    pending, are stepped on the device (k_front): the messages, stepped blocks, control
+    records and index table come from the key states at the chunk start and the events.
+    1100 instances over 256 blocks (four chunks): the registration and first chords (host),
+    a note-only chunk (device), a chunk with drawbar and percussion changes among the notes
+    (host), a note-only chunk again (device); held keys re-pressed and releases of keys
+    that are up included.  Bit for bit against the host
+    front end (TBF_DEVICE_FRONT=0) and against the oracle for a sample."""
+    import os
+    import torch
+    import tunebfree_amd as T
+    from orc_bind import Template
+    n, nb = 1100, 256
+    seeds = [7000 + i for i in range(n)]
+    rows, oscen = [], [[] for _ in range(n)]
+
+    def ev(b, i, kind, a, v):
+        rows.append((b, i, 0 if kind == "note" else 1, a, float(v)))
+        oscen[i].append((b, kind, a, v))
+
+    for i in range(n):
+        for (k, a, v) in S.jazz1_params():
+            ev(0, i, k, a, v)
+        for k in S.chord_for(i):
+            ev(0, i, "note", k, 1)
+        for b in range(1, nb):
+            if (i + b) % 3 == 0:
+                continue  # a block without events: the block after one with messages still steps
+            ev(b, i, "note", 55 + (i + b - 1) % 17, 0)
+            ev(b, i, "note", 55 + (i + b) % 17, 1)
+            if b % 5 == 0:
+                ev(b, i, "note", 55 + (i + b) % 17, 1)  # a held key pressed again
+            if b % 7 == 0:
+                ev(b, i, "note", 100, 0)  # a key that is up
+            if 128 <= b < 192 and b % 9 == 0 and i % 2 == 0:
+                ev(b, i, "param", S.P_DRAWBAR + 2, (i + b) % 9)
+            if 128 <= b < 192 and b % 16 == 0 and i % 3 == 0:
+                ev(b, i, "param", S.P_PERC, (b // 16) % 2)
+    rows.sort(key=lambda r: r[0])
+    outs = []
+    for front in (True, False):
+        if not front:
+            os.environ["TBF_DEVICE_FRONT"] = "0"
+        try:
+            eng = T.Engine(sample_rate=48000.0, device=0)
+        finally:
+            os.environ.pop("TBF_DEVICE_FRONT", None)
+        tid = eng.template(seed=7)
+        eng.add_instances([tid] * n, seeds)
+        evs = eng.events(rows)
+        L = torch.zeros((n, nb * 128), dtype=torch.float32, device="cuda")
+        R = torch.zeros_like(L)
+        eng.render_events_device(nb, evs, L.data_ptr(), R.data_ptr(), nb * 128)
+        eng.synchronize()
+        outs.append((L.cpu().numpy(), R.cpu().numpy()))
+        eng.close()
+        del L, R
+    assert np.array_equal(outs[0][0].view(np.uint32), outs[1][0].view(np.uint32))
+    assert np.array_equal(outs[0][1].view(np.uint32), outs[1][1].view(np.uint32))
+    sample = [0, 1, 2, 3, 550, n - 1]
+    tpl = Template(oracle, seed=7)
+    oL, oR, *_ = oracle_run(oracle, tpl, [seeds[i] for i in sample], [sorted(oscen[i], key=lambda r: r[0]) for i in sample], nb)
+    eL, xL = compare(outs[0][0][sample], oL)
+    eR, xR = compare(outs[0][1][sample], oR)
+    print(f"device front end vs oracle: max|err| L={eL:.3g} R={eR:.3g} bit-exact {xL:.6f} {xR:.6f}")
+    assert max(eL, eR) <= TOL
+
+
 def test_gpu_threaded_host_control_reports_errors():
     """A bad event met by a host worker (threaded front end, >= 1024 instances) fails the
     call with the worker's message, as the serial loop would (the message is thread-local)."""

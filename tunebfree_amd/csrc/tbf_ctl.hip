@@ -444,6 +444,86 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_tgctl (
 		G->gain[lane] = sm.dbg[lane];
 }
 
+/* The device front end of a chunk whose events are all notes (src/tonegen.cpp:3096-3166
+ * oscKeyOn / oscKeyOff, and the per-block step of TgControl::stepFront / mixCtl): one wave
+ * per instance, lane 0 walking the instance's events in order from its key state at the
+ * chunk start.  A key event updates activeKeys and the key counts and queues its messages;
+ * a block with messages, or right after one (steadyPending), is stepped: it gets a control
+ * delta (pool index nInst + inst * nBlocks + k) whose record k_tgctl turns into the entry
+ * (the persistent entry with this block's keyCompTarget and percussion reset) and the
+ * program.  Writes the records, the messages and the chunk's index table. */
+__global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_front (const tbf_launch P)
+{
+	__shared__ uint32_t keys[12];
+	const int             lane = threadIdx.x;
+	const uint32_t        inst = blockIdx.x;
+	const uint32_t        n = P.nInst, nb = P.nBlocks;
+	const tbf_front_state& F   = P.front[inst];
+	if (lane < 12)
+		keys[lane] = F.keys[lane];
+	wave_sync ();
+	if (lane != 0)
+		return;
+	uint32_t*      ctlIdx = (uint32_t*)P.ctlIdx;
+	uint16_t*      msgs   = (uint16_t*)P.msgs;
+	tbf_tgc_rec*   rec    = (tbf_tgc_rec*)P.rec;
+	const float*   kct    = P.keyComp + (size_t)P.cst[inst].tpl * 128;
+	const uint32_t routing = P.ctl[inst].routing;
+	int            kdc = F.keyDown, ukc = F.upperDown;
+	bool           pending = F.pending != 0;
+	uint32_t       e = P.fevOff[inst], eEnd = P.fevOff[inst + 1];
+	uint32_t       mo = 2 * e; /* the instance's message slots: at most two per event */
+	uint32_t       idx = inst, k = 0;
+	for (uint32_t b = 0; b < nb; b++) {
+		const uint32_t m0 = mo;
+		for (; e < eEnd && (P.fev[e] >> 16) == b; e++) {
+			const uint32_t v = P.fev[e], key = v & 0x0fffu;
+			const bool     on = (v >> 12) & 1u;
+			const uint32_t w = key >> 5, bit = 1u << (key & 31);
+			if (keys[w] & bit) { /* keyOff, or keyOn's release of a held key first */
+				keys[w] &= ~bit;
+				if (key < 128)
+					ukc--;
+				kdc--;
+				msgs[mo++] = (uint16_t)key;
+			}
+			if (on) {
+				keys[w] |= bit;
+				if (key < 128)
+					ukc++;
+				kdc++;
+				msgs[mo++] = (uint16_t)(0x1000u | key);
+			}
+		}
+		const uint32_t nm = mo - m0;
+		if (nm > 0 || pending) {
+			const uint32_t d = inst * nb + k++;
+			tbf_tgc_rec    R;
+			R.msgOff        = m0;
+			R.nMsg          = nm;
+			R.gainOff       = 0;
+			R.full          = 0;
+			R.keyCompTarget = kct[kdc < 0 ? 0 : (kdc > 127 ? 127 : kdc)];
+			R.flags         = (uint8_t)(0x80u | (ukc == 0 ? 8u : 0u));
+			R.oldRouting    = (uint8_t)routing;
+			R.percSendBus   = (uint8_t)F.percSendBus;
+			R.pad           = 0;
+			rec[d]          = R;
+			idx             = n + d;
+			pending         = nm > 0;
+		}
+		ctlIdx[(size_t)b * n + inst] = idx;
+	}
+}
+
+extern "C" int tbf_launch_front (const tbf_launch* P, hipStream_t stream)
+{
+	if (P->nInst == 0 || P->nBlocks > NL || P->instBase != 0)
+		return -22;
+	hipLaunchKernelGGL (k_front, dim3 (P->nInst), dim3 (NL), 0, stream, *P);
+	return hipGetLastError () == hipSuccess ? 0 : -5;
+}
+
 extern "C" int tbf_launch_tgctl (const tbf_launch* P, hipStream_t stream)
 {
 	if (P->nCtlInst == 0)

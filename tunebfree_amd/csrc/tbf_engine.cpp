@@ -33,6 +33,7 @@
 extern "C" int tbf_launch_stage (const tbf_launch* P, int k, hipStream_t stream);
 extern "C" int tbf_chain_stages (uint32_t chain);
 extern "C" int tbf_launch_tgctl (const tbf_launch* P, hipStream_t stream);
+extern "C" int tbf_launch_front (const tbf_launch* P, hipStream_t stream);
 extern "C" int tbf_launch_calibrate (int op, void* buf, uint64_t n, hipStream_t s);
 extern "C" int tbf_rv_lds_fits (const tbf_inst_const* k);
 
@@ -441,6 +442,8 @@ int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
 		e->devCtl      = !(hc && hc[0] == '1');
 		const char* hs = getenv ("TBF_HOST_SERIAL"); /* the serial loop (A/B); TBF_HOST_THREADS: workers */
 		e->parCtl      = !(hs && hs[0] == '1');
+		const char* df = getenv ("TBF_DEVICE_FRONT"); /* 0: note-only chunks step on the host too (A/B) */
+		e->frontOn     = !(df && df[0] == '0');
 	}
 	if (int rc = buildShared (e.get ()))
 		return rc;
@@ -480,6 +483,14 @@ int tbf_engine_destroy (tbf_engine* e)
 	e->dctlInstB.release ();
 	e->dfull.release ();
 	e->dfullB.release ();
+	e->dfront.release ();
+	e->dfrontB.release ();
+	e->dfev.release ();
+	e->dfevB.release ();
+	e->dfoff.release ();
+	e->dfoffB.release ();
+	e->dkeyComp.release ();
+	e->dident.release ();
 	e->coff.release ();
 	e->contrib.release ();
 	e->vib.release ();
@@ -1027,6 +1038,13 @@ static int ensureDevice (tbf_engine* e)
 		e->ctlNw = 1;
 		for (const tbf_contrib& c : ent)
 			e->ctlNw = std::max<uint32_t> (e->ctlNw, (uint32_t)c.wheel + 1u);
+		std::vector<float> kc (e->tpls.size () * 128);
+		for (size_t q = 0; q < e->tpls.size (); q++)
+			memcpy (kc.data () + q * 128, e->tpls[q]->keyCompTable, 128 * sizeof (float));
+		if (e->dkeyComp.ensure (std::max<size_t> (kc.size (), 1)))
+			return fail (-12, "out of device memory (key compression tables)");
+		if (!kc.empty ())
+			HIPCHK (hipMemcpy (e->dkeyComp.p, kc.data (), kc.size () * sizeof (float), hipMemcpyHostToDevice));
 		if (e->coff.ensure (off.size ()) || e->contrib.ensure (std::max<size_t> (ent.size (), 1)))
 			return fail (-12, "out of device memory (play matrices)");
 		HIPCHK (hipMemcpy (e->coff.p, off.data (), off.size () * 4, hipMemcpyHostToDevice));
@@ -1463,6 +1481,153 @@ static int stepChunkParallel (tbf_engine* e, uint32_t n, uint32_t want, uint32_t
 	return 0;
 }
 
+/* Device front end: a chunk whose events are all notes, over instances whose control is
+ * otherwise settled (no parameter, programme, rotor or whirl change pending, no drawbar or
+ * routing step), is stepped by k_front on the device (csrc/tbf_ctl.hip): the messages, the
+ * stepped blocks, the control records and the index table come from the instances' key
+ * state at the chunk start and their note events.  The host only partitions the events
+ * by instance and applies them to its own key state (the truth for any later host-stepped
+ * chunk): no per-block step, no records, no index table. */
+static bool frontClean (const Instance& in)
+{
+	const TgControl& t = in.tg;
+	return !in.ctlDirty && !in.progDirty && in.revOpt < 0 && !in.whDirty && t.msg.empty () && !t.drawBarChange &&
+	       t.oldRouting == t.newRouting && t.gainsSent && t.gainMask == 0;
+}
+
+static bool frontEligible (tbf_engine* e, const tbf_event* ev, uint32_t evBeg, uint32_t evEnd)
+{
+	for (uint32_t i : e->actList)
+		if (!frontClean (e->inst[i]))
+			return false;
+	const unsigned    T   = std::max (1u, std::min (hostThreads (), (evEnd - evBeg + 32767) / 32768));
+	const uint32_t    nev = evEnd - evBeg, seg = (nev + T - 1) / T;
+	std::vector<char> ok (T, 1);
+	parallelFor (T, [&] (uint32_t t) {
+		const uint32_t k0 = evBeg + std::min (nev, t * seg), k1 = evBeg + std::min (nev, (t + 1) * seg);
+		for (uint32_t k = k0; k < k1; k++)
+			if (ev[k].kind != TBF_EV_NOTE || !frontClean (e->inst[ev[k].inst])) {
+				ok[t] = 0;
+				return;
+			}
+	});
+	for (char c : ok)
+		if (!c)
+			return false;
+	return true;
+}
+
+static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0, const tbf_event* ev, uint32_t evBeg,
+                           uint32_t evEnd, bool& delta)
+{
+	const unsigned T   = std::max (1u, std::min<unsigned> (hostThreads (), (n + 255) / 256));
+	const uint32_t per = (n + T - 1) / T;
+	auto&          out = e->parStep;
+	out.resize (T);
+	for (auto& o : out) {
+		o.act.clear ();
+		o.ctlInst.clear ();
+		o.evs.clear ();
+	}
+	{ /* the events by instance range, in order (a parallel counting partition) */
+		const uint32_t        nev = evEnd - evBeg, seg = (nev + T - 1) / T;
+		std::vector<uint32_t> cnt ((size_t)T * T, 0);
+		parallelFor (T, [&] (uint32_t sgm) {
+			const uint32_t k0 = evBeg + std::min (nev, sgm * seg), k1 = evBeg + std::min (nev, (sgm + 1) * seg);
+			for (uint32_t k = k0; k < k1; k++)
+				cnt[(size_t)sgm * T + ev[k].inst / per]++;
+		});
+		for (unsigned t = 0; t < T; t++) {
+			uint32_t tot = 0;
+			for (unsigned sgm = 0; sgm < T; sgm++) {
+				const uint32_t c         = cnt[(size_t)sgm * T + t];
+				cnt[(size_t)sgm * T + t] = tot;
+				tot += c;
+			}
+			out[t].evs.resize (tot);
+		}
+		parallelFor (T, [&] (uint32_t sgm) {
+			const uint32_t k0 = evBeg + std::min (nev, sgm * seg), k1 = evBeg + std::min (nev, (sgm + 1) * seg);
+			uint32_t*      at = cnt.data () + (size_t)sgm * T;
+			for (uint32_t k = k0; k < k1; k++) {
+				const uint32_t t = ev[k].inst / per;
+				out[t].evs[at[t]++] = k;
+			}
+		});
+	}
+	std::vector<uint32_t> wbase (T + 1, 0);
+	for (unsigned t = 0; t < T; t++)
+		wbase[t + 1] = wbase[t] + (uint32_t)out[t].evs.size ();
+	e->hFevOff.resize (n + 1);
+	e->hFev.resize (std::max<uint32_t> (wbase[T], 1));
+	e->hFront.resize (n);
+	parallelFor (T, [&] (uint32_t t) {
+		tbf_engine::ParStep&   o  = out[t];
+		const uint32_t         i0 = t * per, i1 = std::min (n, i0 + per);
+		std::vector<uint32_t>& eo = o.eoff;
+		std::vector<uint32_t>& es = o.esort;
+		eo.assign ((size_t)(i1 > i0 ? i1 - i0 : 0) + 1, 0);
+		for (uint32_t k : o.evs)
+			eo[ev[k].inst - i0 + 1]++;
+		for (uint32_t i = i0; i < i1; i++)
+			eo[i - i0 + 1] += eo[i - i0];
+		es.resize (o.evs.size ());
+		{
+			std::vector<uint32_t>& fill = o.efill;
+			fill.assign (eo.begin (), eo.end () - 1);
+			for (uint32_t k : o.evs)
+				es[fill[ev[k].inst - i0]++] = k;
+		}
+		for (uint32_t i = i0; i < i1; i++) {
+			Instance&        in = e->inst[i];
+			TgControl&       tg = in.tg;
+			tbf_front_state& F  = e->hFront[i];
+			memset (&F, 0, sizeof (F));
+			for (int k = 0; k < 384; k++)
+				if (tg.activeKeys[k])
+					F.keys[k >> 5] |= 1u << (k & 31);
+			F.keyDown     = tg.keyDownCount;
+			F.upperDown   = (int32_t)tg.upperKeyCount;
+			F.pending     = tg.steadyPending ? 1u : 0u;
+			F.percSendBus = tg.percSendBus;
+			e->hFevOff[i] = wbase[t] + eo[i - i0];
+			uint32_t msgs = 0, last = 0;
+			for (uint32_t j = eo[i - i0]; j < eo[i - i0 + 1]; j++) {
+				const tbf_event& E   = ev[es[j]];
+				const uint32_t   blk = E.block - b0;
+				const bool       on  = E.value != 0.0;
+				const bool       ok  = E.id >= 0 && E.id < 384; /* oscKeyOn/Off ignore keys >= MAX_KEYS */
+				e->hFev[wbase[t] + j] = (ok ? (uint32_t)E.id : 0x0fffu) | (on ? 1u << 12 : 0u) | (blk << 16);
+				const int m = ok ? tg.noteCount (E.id, on) : 0;
+				msgs += (uint32_t)m;
+				if (blk == want - 1)
+					last += (uint32_t)m;
+			}
+			if (msgs > 0 || F.pending) { /* stepped blocks: control deltas */
+				e->stepped[i] = 1;
+				o.ctlInst.push_back (i);
+				e->chg[i] = 1;
+				const int kd = tg.keyDownCount;
+				e->hCtl[i].keyCompTarget  = tg.tpl->keyCompTable[kd < 0 ? 0 : (kd > 127 ? 127 : kd)];
+				e->hCtl[i].resetPercAtEnd = tg.upperKeyCount == 0;
+			}
+			tg.steadyPending = last > 0;
+			e->inAct[i]      = tg.steadyPending ? 1 : 0;
+			if (e->inAct[i])
+				o.act.push_back (i);
+		}
+	});
+	e->hFevOff[n] = wbase[T];
+	e->actList.clear ();
+	for (unsigned t = 0; t < T; t++) {
+		e->actList.insert (e->actList.end (), out[t].act.begin (), out[t].act.end ());
+		for (uint32_t i : out[t].ctlInst)
+			e->hCtlInst.push_back (i);
+	}
+	delta = !e->hCtlInst.empty ();
+	return 0;
+}
+
 static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, uint64_t stride, hipStream_t s,
                        const tbf_event* ev = nullptr, uint32_t nev = 0)
 {
@@ -1638,6 +1803,9 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			e->hCtlInst.swap (e->hCtlInstB);
 			e->hDInst.swap (e->hDInstB);
 			e->hFull.swap (e->hFullB);
+			e->hFront.swap (e->hFrontB);
+			e->hFev.swap (e->hFevB);
+			e->hFevOff.swap (e->hFevOffB);
 			e->hIdx.swap (e->hIdxB);
 			e->hCtlPin.swap (e->hCtlPinB);
 			std::swap (e->upEv, e->upEvB);
@@ -1690,8 +1858,20 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 				return fail (-22, "event for a bad instance");
 			evEnd++;
 		}
+		/* a chunk of note events only: the device front end */
+		bool dfront = false;
+		if (e->devCtl && dpipe && e->frontOn && !progEv && evEnd - evi >= 1024 && frontEligible (e, ev, evi, evEnd)) {
+			if ((rc = stepChunkFront (e, n, want, b0, ev, evi, evEnd, delta)))
+				return rc;
+			evi    = evEnd;
+			len    = want;
+			dfront = true;
+			if (getenv ("TBF_DEBUG_HOST_PHASES"))
+				fprintf (stderr, "chunk %llu: device front end, %u note events\n", (unsigned long long)e->chunkSeq,
+				         e->hFevOff[n]);
+		}
 		/* many instances to step: active now, or touched by this chunk's events */
-		if (e->devCtl && !progEv && e->parCtl && e->actList.size () + (evEnd - evi) >= 1024) {
+		else if (e->devCtl && !progEv && e->parCtl && e->actList.size () + (evEnd - evi) >= 1024) {
 			if ((rc = stepChunkParallel (e, n, want, b0, ev, evi, evEnd, rp, delta)))
 				return rc;
 			evi = evEnd;
@@ -1787,8 +1967,9 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			if (!e->dProg.empty ())
 				HIPCHK (hipMemcpyAsync (e->prog.p + PERSIST (n), e->dProg.data (),
 				                        e->dProg.size () * sizeof (tbf_prog_entry), hipMemcpyHostToDevice, us));
-			HIPCHK (hipMemcpyAsync (e->ctlIdx.p + (size_t)rp * n * TBF_CHUNK, e->hIdx.data (),
-			                        (size_t)len * n * sizeof (uint32_t), hipMemcpyHostToDevice, us));
+			if (!dfront) /* (k_front writes the index table) */
+				HIPCHK (hipMemcpyAsync (e->ctlIdx.p + (size_t)rp * n * TBF_CHUNK, e->hIdx.data (),
+				                        (size_t)len * n * sizeof (uint32_t), hipMemcpyHostToDevice, us));
 		}
 		P.whSets = nullptr;
 		if (delta && !e->hWh.empty ()) {
@@ -1814,7 +1995,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		P.tgSplit = std::min (P.tgSplit, std::max (len, 1u));
 		P.outOffset = (uint64_t)b0 * TBF_BLK;
 		P.nCtlInst  = 0;
-		if (e->devCtl && !e->hDInst.empty ()) {
+		if (e->devCtl && (dfront ? delta : !e->hDInst.empty ())) {
 			/* k_tgctl: the stepped blocks' programs, ahead of k_tonegen on this stream */
 			/* records per region parity: k_tgctl of the chunk before last (same stream, or
 			 * the caller's stream when not pipelined) read the other set */
@@ -1823,40 +2004,70 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			DevBuf<float>&       dgn  = rp ? e->dgainB : e->dgain;
 			DevBuf<uint32_t>&    dci  = rp ? e->dctlInstB : e->dctlInst;
 			DevBuf<tbf_seg_ctl>& dfl  = rp ? e->dfullB : e->dfull;
-			if (drec.cap < e->hRec.size () || dmsg.cap < e->hMsg.size () || dci.cap < e->hDInst.size () ||
-			    dgn.cap < e->hGain.size () || dfl.cap < e->hFull.size ())
+			const size_t nRec = dfront ? (size_t)n * len : e->hRec.size ();
+			const size_t nMsg = dfront ? 2 * (size_t)e->hFevOff[n] : e->hMsg.size ();
+			if (drec.cap < nRec || dmsg.cap < nMsg || dci.cap < e->hDInst.size () || dgn.cap < e->hGain.size () ||
+			    dfl.cap < e->hFull.size ())
 			{
 				if (getenv ("TBF_DEBUG_HOST_PHASES"))
 					fprintf (stderr, "chunk %llu: control record buffers grow (device sync)\n", (unsigned long long)e->chunkSeq);
 				HIPCHK (hipDeviceSynchronize ()); /* growing: nothing may still read the old buffers */
 			}
-			if (drec.ensure (e->hRec.size ()) || dmsg.ensure (std::max<size_t> (e->hMsg.size (), 1)) ||
+			if (drec.ensure (std::max<size_t> (nRec, 1)) || dmsg.ensure (std::max<size_t> (nMsg, 1)) ||
 			    dgn.ensure (std::max<size_t> (e->hGain.size (), 27)) ||
 			    dci.ensure (e->hDInst.size ()) || dfl.ensure (std::max<size_t> (e->hFull.size (), 1)))
 				return fail (-12, "out of device memory (control records)");
-			if (e->dSeg.empty ())
+			if (dfront) {
+				/* k_front: the records, messages and index table from the key states and events */
+				DevBuf<tbf_front_state>& dfs = rp ? e->dfrontB : e->dfront;
+				DevBuf<uint32_t>&        dfe = rp ? e->dfevB : e->dfev;
+				DevBuf<uint32_t>&        dfo = rp ? e->dfoffB : e->dfoff;
+				if (dfs.cap < n || dfe.cap < e->hFev.size () || dfo.cap < (size_t)n + 1 || e->dident.cap < n)
+					HIPCHK (hipDeviceSynchronize ()); /* growing: nothing may still read the old buffers */
+				if (dfs.ensure (n) || dfe.ensure (e->hFev.size ()) || dfo.ensure ((size_t)n + 1) || e->dident.ensure (n))
+					return fail (-12, "out of device memory (front end)");
+				if (e->hIdent.size () != n) {
+					e->hIdent.resize (n);
+					for (uint32_t i = 0; i < n; i++)
+						e->hIdent[i] = i;
+					HIPCHK (hipMemcpy (e->dident.p, e->hIdent.data (), (size_t)n * 4, hipMemcpyHostToDevice));
+				}
+				HIPCHK (hipMemcpyAsync (dfs.p, e->hFront.data (), (size_t)n * sizeof (tbf_front_state), hipMemcpyHostToDevice, us));
+				HIPCHK (hipMemcpyAsync (dfe.p, e->hFev.data (), e->hFev.size () * 4, hipMemcpyHostToDevice, us));
+				HIPCHK (hipMemcpyAsync (dfo.p, e->hFevOff.data (), ((size_t)n + 1) * 4, hipMemcpyHostToDevice, us));
+				P.front   = dfs.p;
+				P.fev     = dfe.p;
+				P.fevOff  = dfo.p;
+				P.keyComp = e->dkeyComp.p;
+				P.rec     = drec.p;
+				P.msgs    = dmsg.p;
+				if ((rc = tbf_launch_front (&P, us)))
+					return fail (rc, std::string ("k_front launch failed: ") + hipGetErrorString (hipGetLastError ()));
+			}
+			if (!dfront && e->dSeg.empty ())
 				HIPCHK (hipMemcpyAsync (drec.p, e->hRec.data (), e->hRec.size () * sizeof (tbf_tgc_rec),
 				                        hipMemcpyHostToDevice, us));
 			for (const auto& g : e->dSeg)
-				if (g.second)
+				if (!dfront && g.second)
 					HIPCHK (hipMemcpyAsync (drec.p + g.first, e->hRec.data () + g.first,
 					                        g.second * sizeof (tbf_tgc_rec), hipMemcpyHostToDevice, us));
-			if (!e->hMsg.empty ())
+			if (!dfront && !e->hMsg.empty ())
 				HIPCHK (hipMemcpyAsync (dmsg.p, e->hMsg.data (), e->hMsg.size () * sizeof (uint16_t),
 				                        hipMemcpyHostToDevice, us));
-			if (!e->hGain.empty ())
+			if (!dfront && !e->hGain.empty ())
 				HIPCHK (hipMemcpyAsync (dgn.p, e->hGain.data (), e->hGain.size () * sizeof (float),
 				                        hipMemcpyHostToDevice, us));
-			if (!e->hFull.empty ())
+			if (!dfront && !e->hFull.empty ())
 				HIPCHK (hipMemcpyAsync (dfl.p, e->hFull.data (), e->hFull.size () * sizeof (tbf_seg_ctl),
 				                        hipMemcpyHostToDevice, us));
-			HIPCHK (hipMemcpyAsync (dci.p, e->hDInst.data (), e->hDInst.size () * 4, hipMemcpyHostToDevice, us));
+			if (!dfront)
+				HIPCHK (hipMemcpyAsync (dci.p, e->hDInst.data (), e->hDInst.size () * 4, hipMemcpyHostToDevice, us));
 			P.tgc      = e->tgc.p;
 			P.rec      = drec.p;
 			P.msgs     = dmsg.p;
 			P.gains    = dgn.p;
-			P.ctlInst  = dci.p;
-			P.nCtlInst = (uint32_t)e->hDInst.size ();
+			P.ctlInst  = dfront ? e->dident.p : dci.p;
+			P.nCtlInst = dfront ? n : (uint32_t)e->hDInst.size ();
 			P.fulls    = dfl.p;
 			P.progBase = (uint32_t)(PERSIST (n) + (size_t)rp * n * TBF_CHUNK * SLOT);
 			P.coff     = e->coff.p;

@@ -220,6 +220,16 @@ struct tbf_engine {
 	std::vector<tbf_seg_ctl>                lastEmit; /* per instance: the last full entry the device holds (parallel front end) */
 	std::vector<uint8_t>                    dseen, dhas; /* per chunk: lastEmit taken / in hDInst */
 	std::vector<uint32_t>                   lastProg;    /* per instance: the last delta's prog_off */
+	/* device front end (k_front) for note-only chunks: per instance key state at the chunk
+	 * start, the instances' note events by instance, their offsets; by chunk parity */
+	bool                                    frontOn = true; /* TBF_DEVICE_FRONT=0 disables */
+	PinnedVec<tbf_front_state>              hFront, hFrontB;
+	PinnedVec<uint32_t>                     hFev, hFevB, hFevOff, hFevOffB;
+	DevBuf<tbf_front_state>                 dfront, dfrontB;
+	DevBuf<uint32_t>                        dfev, dfevB, dfoff, dfoffB;
+	DevBuf<float>                           dkeyComp;   /* [tpl][128] keyCompTable */
+	DevBuf<uint32_t>                        dident;     /* 0 .. n-1: k_tgctl's grid over every instance */
+	std::vector<uint32_t>                   hIdent;
 	/* the other parity of the chunk staging (the previous chunk's, in flight), and the
 	 * events after each parity's uploads */
 	PinnedVec<tbf_seg_ctl>                  dCtlB, hCtlPin, hCtlPinB;

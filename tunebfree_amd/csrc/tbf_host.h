@@ -198,6 +198,9 @@ struct TgControl {
 	void init (const TgTemplate* t, const Config& c);
 	void keyOn (int key);
 	void keyOff (int key);
+	/* keyOn / keyOff without queueing the messages (the device front end derives them):
+	 * returns the number of messages the key event makes */
+	int noteCount (int key, bool on);
 	void setDrawBar (int bus, unsigned setting);
 	void setVibratoUpper (int on);
 	void setVibratoLower (int on);

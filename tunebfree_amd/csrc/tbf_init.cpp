@@ -824,6 +824,28 @@ void TgControl::keyOn (int key)
 	msg.push_back ((uint16_t)(0x1000 | (key & 0x0fff)));
 }
 
+int TgControl::noteCount (int key, bool on)
+{
+	if (key < 0 || key >= 384)
+		return 0;
+	int m = 0;
+	if (activeKeys[key]) { /* keyOff, or keyOn's release of a held key first */
+		activeKeys[key] = 0;
+		if (key < 128)
+			upperKeyCount--;
+		keyDownCount--;
+		m++;
+	}
+	if (on) {
+		activeKeys[key] = 1;
+		if (key < 128)
+			upperKeyCount++;
+		keyDownCount++;
+		m++;
+	}
+	return m;
+}
+
 /* src/tonegen.cpp:2738-2750 */
 void TgControl::setDrawBar (int bus, unsigned setting)
 {

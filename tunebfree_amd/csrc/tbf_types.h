@@ -58,6 +58,15 @@ typedef struct tbf_tgc_rec {
 	uint8_t  pad;            /* flags & 4: the number of gain pairs */
 } tbf_tgc_rec;
 
+/* device front end (note-only chunks, k_front): an instance's key state at the chunk start */
+typedef struct tbf_front_state {
+	uint32_t keys[12];    /* activeKeys, 384 bits */
+	int32_t  keyDown;     /* keyDownCount */
+	int32_t  upperDown;   /* upperKeyCount */
+	uint32_t pending;     /* steadyPending: the block before had inputs */
+	uint32_t percSendBus;
+} tbf_front_state;
+
 /* one keyContrib element on the device (Contrib): a key's list is sorted by wheel, then
  * bus (compilePlayMatrix's insertion sort, src/tonegen.cpp:1183-1201) */
 typedef struct tbf_contrib {
@@ -263,6 +272,10 @@ typedef struct tbf_launch {
 	const tbf_contrib*    contrib;
 	uint32_t              ctlNw;     /* k_tgctl's staged wheels: the largest wheel a play matrix names, + 1 */
 	const tbf_seg_ctl*    fulls;     /* the chunk's full control entries (tbf_tgc_rec.full) */
+	const tbf_front_state* front;    /* k_front: [inst] key state at the chunk start ... */
+	const uint32_t*       fevOff;    /* ... [inst + 1] offsets into fev ... */
+	const uint32_t*       fev;       /* ... an instance's note events in order: key | on << 12 | block << 16 */
+	const float*          keyComp;   /* [tpl][128] keyCompTable */
 	uint32_t              progBase;  /* program slot of delta d (pool index nInst + d): progBase + d * TBF_PROG_SLOT */
 } tbf_launch;
 

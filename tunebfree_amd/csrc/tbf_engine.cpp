@@ -1497,8 +1497,20 @@ static bool frontClean (const Instance& in)
 
 static bool frontEligible (tbf_engine* e, const tbf_event* ev, uint32_t evBeg, uint32_t evEnd)
 {
+	/* per instance once (an event list visits every instance's host state many times) */
+	const uint32_t        n  = (uint32_t)e->inst.size ();
+	std::vector<uint8_t>& cl = e->fclean;
+	cl.resize (n);
+	{
+		const unsigned T   = std::max (1u, std::min<unsigned> (hostThreads (), (n + 255) / 256));
+		const uint32_t per = (n + T - 1) / T;
+		parallelFor (T, [&] (uint32_t t) {
+			for (uint32_t i = t * per; i < std::min (n, (t + 1) * per); i++)
+				cl[i] = frontClean (e->inst[i]) ? 1 : 0;
+		});
+	}
 	for (uint32_t i : e->actList)
-		if (!frontClean (e->inst[i]))
+		if (!cl[i])
 			return false;
 	const unsigned    T   = std::max (1u, std::min (hostThreads (), (evEnd - evBeg + 32767) / 32768));
 	const uint32_t    nev = evEnd - evBeg, seg = (nev + T - 1) / T;
@@ -1506,7 +1518,7 @@ static bool frontEligible (tbf_engine* e, const tbf_event* ev, uint32_t evBeg, u
 	parallelFor (T, [&] (uint32_t t) {
 		const uint32_t k0 = evBeg + std::min (nev, t * seg), k1 = evBeg + std::min (nev, (t + 1) * seg);
 		for (uint32_t k = k0; k < k1; k++)
-			if (ev[k].kind != TBF_EV_NOTE || !frontClean (e->inst[ev[k].inst])) {
+			if (ev[k].kind != TBF_EV_NOTE || !cl[ev[k].inst]) {
 				ok[t] = 0;
 				return;
 			}

@@ -230,6 +230,7 @@ struct tbf_engine {
 	DevBuf<float>                           dkeyComp;   /* [tpl][128] keyCompTable */
 	DevBuf<uint32_t>                        dident;     /* 0 .. n-1: k_tgctl's grid over every instance */
 	std::vector<uint32_t>                   hIdent;
+	std::vector<uint8_t>                    fclean; /* per instance: no control change pending but notes */
 	/* the other parity of the chunk staging (the previous chunk's, in flight), and the
 	 * events after each parity's uploads */
 	PinnedVec<tbf_seg_ctl>                  dCtlB, hCtlPin, hCtlPinB;

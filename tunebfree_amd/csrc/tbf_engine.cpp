@@ -1535,6 +1535,7 @@ static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0
 	const unsigned T   = std::max (1u, std::min<unsigned> (hostThreads (), (n + 255) / 256));
 	const uint32_t per = (n + T - 1) / T;
 	auto&          out = e->parStep;
+	const auto     f0  = std::chrono::steady_clock::now ();
 	out.resize (T);
 	for (auto& o : out) {
 		o.act.clear ();
@@ -1567,6 +1568,7 @@ static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0
 			}
 		});
 	}
+	const auto            f1 = std::chrono::steady_clock::now ();
 	std::vector<uint32_t> wbase (T + 1, 0);
 	for (unsigned t = 0; t < T; t++)
 		wbase[t + 1] = wbase[t] + (uint32_t)out[t].evs.size ();
@@ -1637,6 +1639,11 @@ static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0
 			e->hCtlInst.push_back (i);
 	}
 	delta = !e->hCtlInst.empty ();
+	if (getenv ("TBF_DEBUG_HOST_PHASES")) {
+		auto ms = [] (auto a, auto b) { return std::chrono::duration<double, std::milli> (b - a).count (); };
+		fprintf (stderr, "stepChunkFront T=%u: partition %.3f ms, instances %.3f ms\n", T, ms (f0, f1),
+		         ms (f1, std::chrono::steady_clock::now ()));
+	}
 	return 0;
 }
 
@@ -1862,13 +1869,38 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		const auto hc0   = std::chrono::steady_clock::now ();
 		/* device control with many active instances: the chunk's host control on worker
 		 * threads (serial when a programme change is among the events) */
+		/* the chunk's events (sorted by block: a binary search), checked in parallel (a serial
+		 * pass cost ~0.5 ms at 524k events) */
 		uint32_t evEnd = evi;
-		bool     progEv = false;
-		while (evEnd < nev && ev[evEnd].block < b0 + want) {
-			progEv = progEv || ev[evEnd].kind == TBF_EV_PROGRAM;
-			if (ev[evEnd].inst >= n)
-				return fail (-22, "event for a bad instance");
-			evEnd++;
+		{
+			uint32_t lo = evi, hi = nev;
+			while (lo < hi) {
+				const uint32_t mid = lo + (hi - lo) / 2;
+				if (ev[mid].block < b0 + want)
+					lo = mid + 1;
+				else
+					hi = mid;
+			}
+			evEnd = lo;
+		}
+		bool progEv = false;
+		{
+			const uint32_t    ne = evEnd - evi;
+			const unsigned    T  = std::max (1u, std::min (hostThreads (), (ne + 32767) / 32768));
+			const uint32_t    sg = (ne + T - 1) / T;
+			std::vector<char> pe (T, 0), bad (T, 0);
+			parallelFor (T, [&] (uint32_t t) {
+				const uint32_t k0 = evi + std::min (ne, t * sg), k1 = evi + std::min (ne, (t + 1) * sg);
+				for (uint32_t k = k0; k < k1; k++) {
+					pe[t]  = pe[t] || ev[k].kind == TBF_EV_PROGRAM;
+					bad[t] = bad[t] || ev[k].inst >= n;
+				}
+			});
+			for (unsigned t = 0; t < T; t++) {
+				if (bad[t])
+					return fail (-22, "event for a bad instance");
+				progEv = progEv || pe[t];
+			}
 		}
 		/* a chunk of note events only: the device front end */
 		bool dfront = false;

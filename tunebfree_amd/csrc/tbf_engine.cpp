@@ -2223,9 +2223,22 @@ int tbf_render_events (tbf_engine* e, uint32_t nblocks, const tbf_event* ev, uin
 		return fail (-22, "null argument");
 	if (e->cfg.device < 0)
 		return fail (-19, "host-only engine (device -1) cannot render");
-	for (uint32_t k = 1; k < nev; k++)
-		if (ev[k].block < ev[k - 1].block)
-			return fail (-22, "events must be sorted by block");
+	{ /* sorted by block (in parallel: large event lists) */
+		const unsigned    T  = std::max (1u, std::min (hostThreads (), (nev + 32767) / 32768));
+		const uint32_t    sg = (nev + T - 1) / T;
+		std::vector<char> bad (T, 0);
+		parallelFor (T, [&] (uint32_t t) {
+			const uint32_t k0 = std::max (1u, std::min (nev, t * sg)), k1 = std::min (nev, (t + 1) * sg);
+			for (uint32_t k = k0; k < k1; k++)
+				if (ev[k].block < ev[k - 1].block) {
+					bad[t] = 1;
+					return;
+				}
+		});
+		for (char b : bad)
+			if (b)
+				return fail (-22, "events must be sorted by block");
+	}
 	HIPCHK (hipSetDevice (e->cfg.device));
 	return renderImpl (e, nblocks, dL, dR, stride, stream ? (hipStream_t)stream : e->stream, ev, nev);
 }

@@ -1891,10 +1891,13 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			std::vector<char> pe (T, 0), bad (T, 0);
 			parallelFor (T, [&] (uint32_t t) {
 				const uint32_t k0 = evi + std::min (ne, t * sg), k1 = evi + std::min (ne, (t + 1) * sg);
+				bool           p = false, b = false; /* locals: the flags share a cache line */
 				for (uint32_t k = k0; k < k1; k++) {
-					pe[t]  = pe[t] || ev[k].kind == TBF_EV_PROGRAM;
-					bad[t] = bad[t] || ev[k].inst >= n;
+					p = p || ev[k].kind == TBF_EV_PROGRAM;
+					b = b || ev[k].inst >= n;
 				}
+				pe[t]  = p;
+				bad[t] = b;
 			});
 			for (unsigned t = 0; t < T; t++) {
 				if (bad[t])

@@ -185,6 +185,10 @@ void      orc_set_chain (orc_inst* p, int mode);                   /* 0 full, 1 
  * (whirl.horn.filter.{a,b}.{type,hz,q,gain}, whirl.{horn,drum}.brakepos,
  * whirl.{horn,drum}.{acceleration,deceleration}); -1 for any other name */
 int       orc_control (orc_inst* p, const char* name, int value);
+/* the whirl fields the control functions write (test hook, for the setter pin
+ * oracle/ref_whirl_pin.cpp): haT haF haQ haG hafw[1..5] hbT hbF hbQ hbG hbfw[1..5]
+ * hnBrakePos drBrakePos hornAcc hornDec drumAcc drumDec; returns the count (24) */
+int       orc_whirl_fields (const orc_inst* p, double* out);
 /* render nblocks of the synthSound quartet; any output pointer may be NULL.
  * sA/sB/sC receive the tonegen, preamp and reverb stage outputs. */
 void orc_render (orc_inst* p, int nblocks, float* L, float* R, float* sA, float* sB, float* sC);

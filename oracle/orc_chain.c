@@ -102,6 +102,31 @@ int orc_control (orc_inst* p, const char* name, int value)
 	return orc_whirl_control (p->wh, name, uc);
 }
 
+int orc_whirl_fields (const orc_inst* p, double* out)
+{
+	const struct orc_whirl* w = p->wh;
+	int                     k = 0;
+	out[k++]                  = w->haT;
+	out[k++]                  = w->haF;
+	out[k++]                  = w->haQ;
+	out[k++]                  = w->haG;
+	for (int i = 1; i <= 5; i++)
+		out[k++] = w->hafw[i];
+	out[k++] = w->hbT;
+	out[k++] = w->hbF;
+	out[k++] = w->hbQ;
+	out[k++] = w->hbG;
+	for (int i = 1; i <= 5; i++)
+		out[k++] = w->hbfw[i];
+	out[k++] = w->hnBrakePos;
+	out[k++] = w->drBrakePos;
+	out[k++] = w->hornAcc;
+	out[k++] = w->hornDec;
+	out[k++] = w->drumAcc;
+	out[k++] = w->drumDec;
+	return k;
+}
+
 /* src/clap.cpp:108-121 setToneGenParam and 162-207 setParam */
 void orc_set_param (orc_inst* p, int index, double v)
 {

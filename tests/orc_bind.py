@@ -16,6 +16,7 @@ ROOT = Path(__file__).resolve().parents[1]
 ORC_SO = ROOT / "oracle" / "liborc.so"
 REF_SO = ROOT / "oracle" / "_ref" / "libtbfref.so"
 PIN_SO = ROOT / "oracle" / "_ref" / "libtbfpin.so"
+WPIN_SO = ROOT / "oracle" / "_ref" / "libtbfwpin.so"
 # the same reference TUs built with the reference's release flags (common.mak:16-18):
 # the CPU baseline's timing build (bench.py), never a parity checker
 REF_FAST_SO = ROOT / "oracle" / "_ref" / "fast" / "libtbfref.so"
@@ -57,6 +58,8 @@ def load_oracle():
     lib.orc_control.restype = C.c_int
     lib.orc_control.argtypes = [C.c_void_p, C.c_char_p, C.c_int]
     lib.orc_render.argtypes = [C.c_void_p, C.c_int, _fp, _fp, _fp, _fp, _fp]
+    lib.orc_whirl_fields.restype = C.c_int
+    lib.orc_whirl_fields.argtypes = [C.c_void_p, _dp]
     lib.orc_cfg_size.restype = C.c_size_t
     lib.orc_cfg_default.argtypes = [C.c_void_p]
     lib.orc_cfg_set.restype = C.c_int
@@ -317,3 +320,19 @@ class Chain:
 
 def fptr(a):
     return _f(a)
+
+
+def load_wpin():
+    """The whirl-setter pin harness (oracle/ref_whirl_pin.cpp: src/whirl.cpp's own static
+    MIDI control setters, built without the CLAP define); None when not built."""
+    if not WPIN_SO.exists():
+        return None
+    lib = C.CDLL(str(WPIN_SO))
+    lib.wpin_new.restype = C.c_void_p
+    lib.wpin_new.argtypes = [C.c_double]
+    lib.wpin_free.argtypes = [C.c_void_p]
+    lib.wpin_control.restype = C.c_int
+    lib.wpin_control.argtypes = [C.c_void_p, C.c_char_p, C.c_int]
+    lib.wpin_fields.restype = C.c_int
+    lib.wpin_fields.argtypes = [C.c_void_p, _dp]
+    return lib

@@ -460,6 +460,11 @@ def test_gpu_device_front_end_note_chunks(oracle):
                 ev(b, i, "note", 55 + (i + b) % 17, 1)  # a held key pressed again
             if b % 7 == 0:
                 ev(b, i, "note", 100, 0)  # a key that is up
+            if (i + b) % 11 == 0:  # keys outside [0, MAX_KEYS): ignored (src/tonegen.cpp:3098)
+                bad = (-1, 384, 400, 4095)[(i + b) % 4]
+                ev(b, i, "note", bad, 1)
+                if b % 2:
+                    ev(b, i, "note", bad, 0)
             if 128 <= b < 192 and b % 9 == 0 and i % 2 == 0:
                 ev(b, i, "param", S.P_DRAWBAR + 2, (i + b) % 9)
             if 128 <= b < 192 and b % 16 == 0 and i % 3 == 0:
@@ -1124,8 +1129,10 @@ def test_gpu_whirl_control_functions(oracle):
     acceleration and deceleration) through tbf_midi_control between renders, at seeded
     random values over the rotor stop -> fast -> stop -> slow -> stop script
     (scenarios.whirl_control_scenario: consecutive filter changes, out-of-range settings,
-    a change while bypassed), against the oracle's orc_control, itself bit-identical to the
-    reference's whirlProc under the same fields (test_oracle_whirl_controls_vs_reference)."""
+    a change while bypassed), against the oracle's orc_control.  The oracle's setter
+    mapping equals the reference's own setters field for field (whirl.cpp built without
+    CLAP, test_oracle_whirl_setters_pinned_to_reference), and the reference's whirlProc
+    under those fields equals the oracle's (test_oracle_whirl_controls_vs_reference)."""
     n, nb = 8, 72
     eng, tpl, seeds, scens = _setup(oracle, n, S.whirl_control_scenario)
     L, R = engine_run(eng, scens, nb)

@@ -300,6 +300,45 @@ def test_oracle_whirl_controls_vs_reference(oracle, refchk):
         assert not np.array_equal(a[0], c[0])
 
 
+def test_oracle_whirl_setters_pinned_to_reference(oracle):
+    """The whirl's MIDI control setters (src/whirl.cpp:699-909) pinned to the reference's
+    own functions: oracle/ref_whirl_pin.cpp #includes whirl.cpp without the CLAP define
+    and calls its static setters by the names initWhirl registers (970-981).  Over every
+    function x every value 0..127 at three rates, and a seeded random sequence of
+    controls, the fields each setter writes (filter type / Hz / Q / gain with the
+    recomputed biquad after setIIRFilter's range guard, brake positions, ramp rates)
+    equal the oracle's orc_control's field for field."""
+    from orc_bind import load_wpin
+    wp = load_wpin()
+    if wp is None:
+        pytest.skip("oracle/_ref/libtbfwpin.so not built (no /root/reference here)")
+    tpl = Template(oracle, sr=48000.0, seed=7)
+
+    def fields(getter, h):
+        out = np.zeros(24, np.float64)
+        assert getter(h, out.ctypes.data_as(C.POINTER(C.c_double))) == 24
+        return out
+
+    rng = np.random.default_rng(5)
+    for sr in (44100.0, 48000.0, 96000.0):
+        t = tpl if sr == 48000.0 else Template(oracle, sr=sr, seed=7)
+        ch = Chain(oracle, t, 1)
+        w = wp.wpin_new(sr)
+        try:
+            assert np.array_equal(fields(oracle.orc_whirl_fields, ch.ptr), fields(wp.wpin_fields, w)), sr
+            script = [(n, v) for n in S.WHIRL_CONTROLS for v in range(128)]
+            script += [(S.WHIRL_CONTROLS[int(rng.integers(len(S.WHIRL_CONTROLS)))], int(rng.integers(128)))
+                       for _ in range(2000)]
+            for name, v in script:
+                ch.control(name, v)
+                assert wp.wpin_control(w, name.encode(), v) == 0
+                a, b = fields(oracle.orc_whirl_fields, ch.ptr), fields(wp.wpin_fields, w)
+                assert np.array_equal(a.view(np.uint64), b.view(np.uint64)), (sr, name, v, a, b)
+            assert wp.wpin_control(w, b"rotary.speed-toggle", 1) == -1
+        finally:
+            wp.wpin_free(w)
+
+
 def test_oracle_whirl_control_names(oracle):
     """orc_control knows exactly the 14 functions initWhirl registers (966-981)."""
     tpl = Template(oracle, sr=48000.0, seed=7)

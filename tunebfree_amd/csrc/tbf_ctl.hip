@@ -479,6 +479,8 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_front (
 		for (; e < eEnd && (P.fev[e] >> 16) == b; e++) {
 			const uint32_t v = P.fev[e], key = v & 0x0fffu;
 			const bool     on = (v >> 12) & 1u;
+			if (key >= 384) /* the host packs keys outside [0, MAX_KEYS) as 0x0fff: ignored (3098) */
+				continue;
 			const uint32_t w = key >> 5, bit = 1u << (key & 31);
 			if (keys[w] & bit) { /* keyOff, or keyOn's release of a held key first */
 				keys[w] &= ~bit;

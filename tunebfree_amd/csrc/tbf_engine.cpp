@@ -401,9 +401,11 @@ int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
 		 * end-of-call wait (measured with a fifth engine stream: steady step 6.7 -> 8.1 ms) */
 		HIPCHK (hipStreamCreateWithFlags (&e->stream, hipStreamNonBlocking));
 		if (const char* pg = getenv ("TBF_PIPE_GROUPS")) { /* "g0,...,g5": groups 0..5, non-decreasing, from 0 */
+			/* stages 0 and 1 always share a stream: the tonegen-only chain's mixFixed flags
+			 * (one buffer for every chunk) are written by k_tonegen and read by k_mixpre */
 			for (int k = 0; k < TBF_NSTAGES && *pg; k++) {
 				const int g = atoi (pg);
-				if (g >= 0 && g < TBF_NSTAGES && (k == 0 ? g == 0 : (g >= e->grp[k - 1] && g <= e->grp[k - 1] + 1)))
+				if (g >= 0 && g < TBF_NSTAGES && (k == 0 ? g == 0 : k == 1 ? g == e->grp[0] : (g >= e->grp[k - 1] && g <= e->grp[k - 1] + 1)))
 					e->grp[k] = g;
 				while (*pg && *pg != ',')
 					pg++;

@@ -23,9 +23,14 @@ static int tbf_instantiate_engine (B3S* b3s, double rate, const double* mts128)
 {
 	tbf_engine_config cfg = { rate, /*device*/ 0, TBF_CHAIN_FULL, /*debug_flags*/ 0, {0, 0, 0} };
 	uint32_t tpl, first, seed = (uint32_t)time (NULL);   /* srand(time(NULL)), lv2.cpp:949 */
+	b3s->tbf = NULL;
 	if (tbf_engine_create (&cfg, &b3s->tbf)) return -1;
-	if (tbf_template_create (b3s->tbf, mts128, NULL, seed, &tpl)) return -1;
-	if (tbf_instances_add (b3s->tbf, 1, &tpl, &seed, &first)) return -1;
+	if (tbf_template_create (b3s->tbf, mts128, NULL, seed, &tpl) ||
+	    tbf_instances_add (b3s->tbf, 1, &tpl, &seed, &first)) {
+		tbf_engine_destroy (b3s->tbf);   /* no half-built engine left behind */
+		b3s->tbf = NULL;
+		return -1;
+	}
 	/* initSynth's setDrawBars(inst, 0, {8,8,6,...}), lv2.cpp:167-180 */
 	static const int bars[9] = {8, 8, 6, 0, 0, 0, 0, 0, 0};
 	for (int i = 0; i < 9; ++i)

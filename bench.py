@@ -40,7 +40,6 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # gathers are that pattern (one shared bank, every instance reading the same wheels)
 L2_PEAK_GBS = 18800.0
 TRAFFIC_JSON = ROOT / "profiles" / "traffic.json"  # written by tools/traffic_from_pmc.py
-CHUNK = 64  # blocks per launch set (TBF_CHUNK, csrc/tbf_engine.cpp)
 
 
 def parse():
@@ -352,7 +351,10 @@ def main():
     value = total_samples / elapsed
 
     kern, kern_iso, max_err, exact, per_stage = {}, None, None, None, None
-    launches = -(-a.blocks // CHUNK)  # launch sets per step (one per 64-block chunk)
+    # launch sets per step: the timed steps have no control deltas, so each chunk is up to the
+    # engine's steady chunk (TBF_STEADY_CHUNK, default 256 blocks; 64 with deltas)
+    chunk = eng.chunks()[1] if not a.dry_run else 64
+    launches = -(-a.blocks // chunk)
     ksteps = a.steps if a.kernel_steps is None else a.kernel_steps
     if not a.dry_run:
         # per-kernel launch durations (HIP events on each launch's stream, inside the
@@ -397,7 +399,7 @@ def main():
         bank_entries = float(np.mean([c for c in cnt if c >= 0])) if cnt else None
 
     if rank == 0:
-        samples_launch = B * min(a.blocks, CHUNK) * 128  # stereo samples one launch of a stage renders
+        samples_launch = B * min(a.blocks, chunk) * 128  # stereo samples one launch of a stage renders
         algo = dict(ALGO_BYTES)
         if a.chain == 1:  # tonegen only: k_mixpre writes L and R (8 B); bank reads are L2-resident
             algo["k_mixpre"] = 8

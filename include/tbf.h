@@ -249,6 +249,8 @@ int tbf_debug_host_time (tbf_engine* e, int32_t reset, double* ms, uint64_t* blo
 /* the cfg-derived HBM layout: the compact whirl ring window (512 / 1024 / 2048 samples
  * per ring, from the geometry's largest write-ahead) and the reverb slab length */
 int tbf_debug_layout (const tbf_engine* e, uint32_t* wring_len, float* max_ahead, uint32_t* slab_len);
+/* blocks per render chunk: with control deltas (64) and without (TBF_STEADY_CHUNK, up to 256) */
+int tbf_debug_chunks (const tbf_engine* e, uint32_t* delta_blocks, uint32_t* steady_blocks);
 /* test hook: set the reverb vibrato phase of line 0..7 of channel ch (b_reverb vib[ch][line],
  * src/reverb.cpp:479-496) of an instance, effective from the next block; parity tests use
  * it to place a phase just below a power of two (a binade crossing inside a launch) */
@@ -281,7 +283,8 @@ int tbf_debug_exact (int32_t op, const double* in3, double* out2, uint32_t n);
  * k_rv_pre, k_rv_core, k_rv_post, k_whirl since the last query (ms6[6], count6[6]) */
 int tbf_debug_kernel_times (tbf_engine* e, int32_t enable, double* ms6, uint32_t* count6);
 /* PMC calibration: op 0 streams n doubles from d_buf (8 B/lane reads, the reverb ring
- * pattern), op 1 writes them; enqueued on `stream` (NULL = legacy default stream) */
+ * pattern), op 1 writes them; ops 2 / 3 the same starting 64 B into a cache line (n >= 16);
+ * enqueued on `stream` (NULL = legacy default stream) */
 int tbf_debug_calibrate (int32_t op, void* d_buf, uint64_t n_doubles, void* stream);
 
 #ifdef __cplusplus

@@ -499,6 +499,57 @@ def test_gpu_device_front_end_note_chunks(oracle):
     assert max(eL, eR) <= TOL
 
 
+def test_gpu_steady_chunks(oracle):
+    """A chunk in which no instance's control changes (every block plays each instance's
+    current entry) runs up to TBF_STEADY_CHUNK blocks (default 256) per launch instead of
+    64, and ends at the next event's block.  Events at blocks 0..48 (chords, drawbars,
+    rotary, a note-off), then a reverb change and a whirl bypass toggle at blocks 300 / 330
+    / 340 inside one 450-block call, and a second call: bit for bit the render of 64-block
+    chunks (TBF_STEADY_CHUNK=64), and the oracle."""
+    import os
+    import torch
+    import tunebfree_amd as T
+    from orc_bind import Template
+    n, nb1, nb2 = 48, 450, 300
+    seeds = [5000 + i for i in range(n)]
+    oscen = [S.event_scenario(i) if i % 2 else S.bench_scenario(i) for i in range(n)]
+    for i in (3, 10):
+        oscen[i] = oscen[i] + [(300, "param", S.P_REVERB, 0.6)]
+    for i in (5, 10):
+        oscen[i] = oscen[i] + [(330, "param", S.P_WHIRL_BYPASS, 1), (340, "param", S.P_WHIRL_BYPASS, 0)]
+    rows = sorted(((b, i, 0 if k == "note" else 1, a, float(v)) for i, sc in enumerate(oscen) for (b, k, a, v) in sc),
+                  key=lambda r: r[0])
+    outs = []
+    for steady in (None, "64"):
+        if steady:
+            os.environ["TBF_STEADY_CHUNK"] = steady
+        try:
+            eng = T.Engine(sample_rate=48000.0, device=0)
+        finally:
+            os.environ.pop("TBF_STEADY_CHUNK", None)
+        tid = eng.template(seed=7)
+        eng.add_instances([tid] * n, seeds)
+        evs = eng.events(rows)
+        L = torch.zeros((n, (nb1 + nb2) * 128), dtype=torch.float32, device="cuda")
+        R = torch.zeros_like(L)
+        eng.render_events_device(nb1, evs, L.data_ptr(), R.data_ptr(), (nb1 + nb2) * 128)
+        eng.render_device(nb2, L[:, nb1 * 128:].data_ptr(), R[:, nb1 * 128:].data_ptr(), (nb1 + nb2) * 128)
+        eng.synchronize()
+        outs.append((L.cpu().numpy(), R.cpu().numpy()))
+        eng.close()
+        del L, R
+    assert np.array_equal(outs[0][0].view(np.uint32), outs[1][0].view(np.uint32))
+    assert np.array_equal(outs[0][1].view(np.uint32), outs[1][1].view(np.uint32))
+    sample = [0, 3, 5, 10, n - 1]
+    tpl = Template(oracle, seed=7)
+    oL, oR, *_ = oracle_run(oracle, tpl, [seeds[i] for i in sample], [sorted(oscen[i], key=lambda r: r[0]) for i in sample],
+                            nb1 + nb2)
+    eL, xL = compare(outs[0][0][sample], oL)
+    eR, xR = compare(outs[0][1][sample], oR)
+    print(f"steady chunks vs oracle: max|err| L={eL:.3g} R={eR:.3g} bit-exact {xL:.6f} {xR:.6f}")
+    assert max(eL, eR) <= TOL
+
+
 def test_gpu_threaded_host_control_reports_errors():
     """A bad event met by a host worker (threaded front end, >= 1024 instances) fails the
     call with the worker's message, as the serial loop would (the message is thread-local)."""

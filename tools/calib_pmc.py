@@ -1,7 +1,7 @@
 """Known-byte streams for FETCH_SIZE / WRITE_SIZE calibration (run under rocprofv3 --pmc).
 Streams N doubles (default 2 GiB, far beyond the 256 MiB MALL) with the render kernel's
 8-B/lane pattern: 3 read launches then 3 write launches.
-usage: rocprofv3 --pmc FETCH_SIZE -- python3 tools/calib_pmc.py [GiB]"""
+usage: rocprofv3 --pmc FETCH_SIZE -- python3 tools/calib_pmc.py [GiB] [ops, e.g. 0,2,1,3: 2/3 = misaligned by 64 B]"""
 import ctypes as C
 import sys
 from pathlib import Path
@@ -20,7 +20,8 @@ def main():
     n = int(gib * (1 << 30)) // 8
     buf = torch.zeros(n, dtype=torch.float64, device="cuda")
     torch.cuda.synchronize()
-    for op in (0, 0, 0, 1, 1, 1):
+    ops = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0, 0, 0, 1, 1, 1]
+    for op in ops:
         assert lib.tbf_debug_calibrate(op, C.c_void_p(buf.data_ptr()), n, None) == 0
     torch.cuda.synchronize()
     print(f"calibration: {n} doubles = {n * 8} bytes per launch")

@@ -11,6 +11,8 @@
 #   iso     the default bench with each kernel also timed alone (--isolated 1)
 #   bench   the default bench without the CPU leg
 #   ab:V=X  the default bench with environment switch V=X
+#   prof    k_rv_core_lds / k_whirl phase clocks (profiling build variants)
+#   calib   PMC byte counters on known aligned / misaligned streams
 set -u
 TAG=${1:-dev}; shift || true
 STEPS=${*:-"tests full kpmc"}
@@ -55,6 +57,12 @@ for s in $STEPS; do
 		run rt 300 python3 -u tools/rt_latency.py --out "$OUT/rt_latency.json"
 		;;
 	iso) run iso 300 python3 bench.py --isolated 1 --cpu-baseline 0 ;;
+	prof) # phase clocks of k_rv_core_lds and k_whirl (build variants from tools/*_prof_patch.py)
+		run rvl_prof 200 env TBF_LIB=tunebfree_amd/_variants/libtbf_rvlprof.so python3 tools/rvl_prof.py
+		run whirl_prof 200 env TBF_LIB=tunebfree_amd/_variants/libtbf_whprof.so python3 tools/whirl_prof.py ;;
+	calib) # FETCH_SIZE / WRITE_SIZE of known streams: aligned and 64 B misaligned 8-B/lane reads and writes
+		run calib_f 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/calib_f" -o run --output-format csv -- python3 tools/calib_pmc.py 2 0,2,1,3
+		run calib_w 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/calib_w" -o run --output-format csv -- python3 tools/calib_pmc.py 2 0,2,1,3 ;;
 	bench) run bench 300 python3 bench.py --cpu-baseline 0 ;;
 	ab:*) # ab:VAR=VALUE -- the default bench with one environment switch (A/B)
 		kv=${s#ab:}

@@ -34,6 +34,10 @@ extern "C" int tbf_launch_calibrate (int op, void* buf, uint64_t n, hipStream_t 
 		hipLaunchKernelGGL (tbf_calib_read_f64, grid, block, 0, s, (const double*)buf, n, (double*)buf);
 	else if (op == 1)
 		hipLaunchKernelGGL (tbf_calib_write_f64, grid, block, 0, s, (double*)buf, n);
+	else if (op == 2) /* the read with every wave's 512 B starting 64 B into a cache line */
+		hipLaunchKernelGGL (tbf_calib_read_f64, grid, block, 0, s, (const double*)buf + 8, n - 8, (double*)buf);
+	else if (op == 3) /* the write, likewise misaligned */
+		hipLaunchKernelGGL (tbf_calib_write_f64, grid, block, 0, s, (double*)buf + 8, n - 8);
 	else
 		return -22;
 	return hipGetLastError () == hipSuccess ? 0 : -5;

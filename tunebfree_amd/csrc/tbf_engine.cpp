@@ -117,7 +117,7 @@ static void reverbConsts (tbf_inst_const& k, double sr, float A, float B, float 
 			/* line 12 of channel 0 holds the predelay history (TBF_PD_HIST floats) instead
 			 * of a ring; channel 1's stays unused */
 			const int len = (l == 12 && c == 0) ? std::max (k.delay[l] + 1, TBF_PD_HIST / 2) : k.delay[l] + 1;
-			o += (uint32_t)((len + 7) & ~7);
+			o += (uint32_t)((len + TBF_RING_ALIGN - 1) & ~(TBF_RING_ALIGN - 1));
 		}
 	k.slabLen = o;
 }
@@ -430,6 +430,8 @@ int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
 		HIPCHK (hipDeviceGetAttribute (&ncu, hipDeviceAttributeMultiprocessorCount, cfg->device));
 		if (const char* ts = getenv ("TBF_TG_SPLIT"))
 			e->tgSplit = atoi (ts);
+		if (const char* sc = getenv ("TBF_STEADY_CHUNK")) /* A/B: blocks per chunk without deltas */
+			e->steadyChunk = (uint32_t)std::min (std::max (atoi (sc), TBF_CHUNK), TBF_STEADY_MAX);
 		const char* rp = getenv ("TBF_RV_PERSIST"); /* 0: per-pair grid; n > 0: n workgroups */
 		e->rvGrid      = rp ? (uint32_t)std::max (atoi (rp), 0) : (uint32_t)std::max (ncu, 1);
 		if (e->rvWork.ensure (1))
@@ -1718,8 +1720,9 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 	if (e->cfg.chain_mode == TBF_CHAIN_TONEGEN && e->mixFixed.ensure (n))
 		return fail (-12, "out of device memory");
 	P.mixFixed = e->mixFixed.p;
-	/* inter-stage buffers: two sets, by chunk parity (see the pipelining below) */
-	const size_t need = (size_t)n * TBF_CHUNK * TBF_BLK;
+	/* inter-stage buffers: two sets, by chunk parity (see the pipelining below), each for
+	 * the longest chunk (a chunk without deltas, steadyChunk blocks) */
+	const size_t need = (size_t)n * e->steadyChunk * TBF_BLK;
 	if (e->mid0.ensure (2 * 2 * need))
 		return fail (-12, "out of device memory (stage buffers)");
 	if (e->cfg.chain_mode != TBF_CHAIN_TONEGEN && e->cfg.chain_mode != TBF_CHAIN_TAP_PREAMP) {
@@ -1728,7 +1731,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		if (e->rvA.ensure (2 * 2 * need) || e->rvB.ensure (2 * 2 * need))
 			return fail (-12, "out of device memory (reverb stage buffers)");
 	}
-	P.midStride = (uint64_t)TBF_CHUNK * TBF_BLK;
+	P.midStride = (uint64_t)e->steadyChunk * TBF_BLK;
 	/* Cross-chunk pipelining.  Every stage is causal and keeps its own state, so stage k
 	 * of chunk c depends only on stage k-1 of chunk c and on stage k of chunk c-1, which
 	 * runs on the same stage-group stream; the stage buffers alternate by chunk parity.
@@ -1774,7 +1777,16 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 	while (b0 < nblocks) {
 		/* host control for the chunk, block by block: entry indices per (block, instance),
 		 * new pool entries only where an instance's control changes */
-		const uint32_t want = std::min<uint32_t> (TBF_CHUNK, nblocks - b0);
+		uint32_t want = std::min<uint32_t> (TBF_CHUNK, nblocks - b0);
+		if (nblocks - b0 > TBF_CHUNK && e->steadyChunk > TBF_CHUNK && e->actList.empty () && !e->persistStale) {
+			/* no instance's control can change before the next event: a chunk without deltas,
+			 * up to steadyChunk blocks, ending at the next event's block */
+			uint32_t w = std::min (e->steadyChunk, nblocks - b0);
+			if (evi < nev)
+				w = std::min (w, ev[evi].block > b0 ? ev[evi].block - b0 : 0u);
+			if (w > TBF_CHUNK)
+				want = w;
+		}
 		const uint64_t cix  = e->chunkSeq++;
 		const bool     par  = (cix & 1) != 0;
 		const uint32_t bset = (uint32_t)(cix & 1); /* stage-buffer set of this chunk */
@@ -1995,6 +2007,8 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		                    std::chrono::steady_clock::now () - hc0)
 		                    .count ();
 		e->hostCtlBlocks += len;
+		if (delta && len > TBF_CHUNK)
+			return fail (-5, "internal: a chunk with control deltas longer than 64 blocks");
 		const bool     piped   = pipe && (!delta || dpipe);
 		P.mid0 = e->mid0.p + 2 * bset * need;
 		P.mid1 = e->mid1.p ? e->mid1.p + bset * need : nullptr;
@@ -2410,6 +2424,15 @@ int tbf_debug_layout (const tbf_engine* e, uint32_t* wring_len, float* max_ahead
 	return 0;
 }
 
+int tbf_debug_chunks (const tbf_engine* e, uint32_t* delta_blocks, uint32_t* steady_blocks)
+{
+	if (!e)
+		return fail (-22, "null argument");
+	if (delta_blocks) *delta_blocks = TBF_CHUNK;
+	if (steady_blocks) *steady_blocks = e->steadyChunk;
+	return 0;
+}
+
 int tbf_debug_reverb_phase (tbf_engine* e, uint32_t i, int32_t ch, int32_t line, double value)
 {
 	if (!e || i >= e->inst.size () || ch < 0 || ch > 1 || line < 0 || line > 7)
@@ -2545,7 +2568,7 @@ int tbf_debug_exact (int32_t op, const double* in, double* out, uint32_t n)
 
 int tbf_debug_calibrate (int32_t op, void* buf, uint64_t n, void* stream)
 {
-	if (!buf || (op != 0 && op != 1))
+	if (!buf || op < 0 || op > 3 || n < 16)
 		return fail (-22, "bad arguments");
 	int rc = tbf_launch_calibrate (op, buf, n, (hipStream_t)stream);
 	return rc ? fail (rc, "calibration launch failed") : 0;

@@ -312,6 +312,7 @@ struct tbf_engine {
 	DevBuf<uint32_t>                        rvWork;           /* its work counter */
 	DevBuf<uint8_t>                         mixFixed;         /* tonegen only: k_tonegen wrote the output (tbf_launch.mixFixed) */
 	int                                     tgSplit  = -1;    /* k_tonegen block ranges (TBF_TG_SPLIT; -1: by batch size) */
+	uint32_t                                steadyChunk = TBF_STEADY_MAX; /* blocks per chunk without control deltas (TBF_STEADY_CHUNK) */
 	/* programme table (.pgm), src/program.h:26 MAXPROGS; pgm.controller.offset */
 	std::vector<Programme>                  progs = std::vector<Programme> (129);
 	int                                     pgmOffset = 1;

@@ -91,6 +91,7 @@ struct WhLds {
 	float        aOut[TBF_SUB];       /* horn A output of the current sub-block */
 	int          brake;
 	int          aReady;              /* aOut holds the current sub-block's horn A output */
+	float        sink[2][TBF_SUB];    /* where a ring pass's lanes that own no slot write (motion_pass4) */
 };
 
 /* the control entry of instance `inst` for block `blk` of the chunk: events land at
@@ -1185,11 +1186,14 @@ k_rv_core (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
 #define RVL_G 11 /* sub-blocks (worker waves) per group: 64 RVL_G <= the shortest allpass delay (756), 64 RVL_G + 72 <= the shortest tap-line delay (1146) */
 #endif
 /* the network's ring geometry at the reference's fixed settings (reverbConsts: size =
- * 0.4f^2 * 90 + 10, delay = (int)(dmul * size); rings 8-padded): compile-time constants, so
+ * 0.4f^2 * 90 + 10, delay = (int)(dmul * size); lines 128-B aligned): compile-time constants, so
  * the ring addressing needs no per-line lane reads; tbf_rv_lds_fits checks an instance
  * against them */
 constexpr int RVL_DLY[12] = {1927, 1781, 1732, 1634, 1488, 1439, 1293, 1146, 1049, 1000, 902, 756};
-constexpr int RVL_OFS[12] = {0, 1928, 3712, 5448, 7088, 8584, 10024, 11320, 12472, 13528, 14536, 15440}; /* in HBM */
+/* in HBM: each line's d + 1 slots rounded up to TBF_RING_ALIGN (reverbConsts) */
+constexpr int rvl_hofs (int l) { return l == 0 ? 0 : rvl_hofs (l - 1) + ((RVL_DLY[l - 1] + TBF_RING_ALIGN) & ~(TBF_RING_ALIGN - 1)); }
+constexpr int RVL_OFS[12] = {rvl_hofs (0), rvl_hofs (1), rvl_hofs (2), rvl_hofs (3), rvl_hofs (4),  rvl_hofs (5),
+                             rvl_hofs (6), rvl_hofs (7), rvl_hofs (8), rvl_hofs (9), rvl_hofs (10), rvl_hofs (11)};
 /* In LDS each line of delay d holds its d + 1 slots followed by a mirror of slots
  * 0 .. RVL_MIR - 1, so the reads of a sub-block (slots count + 1 .. count + 71 for the
  * taps, count + 1 .. count + 64 for the allpasses, with count in [0, d]) never wrap: a tap
@@ -1384,127 +1388,144 @@ __device__ __forceinline__ void rvl_pair (const tbf_launch& P, const tbf_inst_co
 	size_t po   = 0;
 	bool   pst  = false;
 	__syncthreads ();
+	/* the workers and the planner run separate loops with the same two barriers per group, so
+	 * the registers of one role are not held live across the other's code */
+	if (w < RVL_G) {
 #pragma unroll 1
-	for (uint32_t g = 0; g < nGrp; g++) {
-		const int  nb  = (int)min ((uint32_t)RVL_G, nSub - g * RVL_G);
-		const int  par = g & 1;
-		const bool act = w < nb;
-		/* ---- read phase (workers): taps, mix, allpass reads; nothing is written to the
-		 * rings.  The planner plans the next group meanwhile. ---- */
-		double       apw[4], ap[4], fb[8], mix;
-		const size_t o = ((size_t)g * RVL_G + (uint32_t)w) * TBF_SUB + n;
-		/* HBM traffic at the start of the group, a whole group ahead of any wait on it: the
-		 * input two groups ahead (every wave, the index clamped, so that no branch joins
-		 * the loaded register) and the previous group's tap mix.  Issued at the end of
-		 * the write phase, the copy a0n <- load at the loop's back edge waited for the
-		 * load, and for the store, right away. */
-		const double nxt = a0s[(size_t)min ((g + 2) * RVL_G + (uint32_t)min (w, RVL_G - 1), nSub - 1) * TBF_SUB + n];
-		if (pst)
-			rv_st (&bout[po], pmix);
-		if (act) {
-			/* the lines' vibrato sines: closed form on every line (wave-uniform, the rule), or
-			 * per line the closed form or the literal recurrence and sin */
-			const uint32_t om = __builtin_amdgcn_readfirstlane (sm.okm[par][w]);
-			double         sn[8];
-			if (om == 0xffu) {
+		for (uint32_t g = 0; g < nGrp; g++) {
+			const int  nb  = (int)min ((uint32_t)RVL_G, nSub - g * RVL_G);
+			const int  par = g & 1;
+			const bool act = w < nb;
+			/* ---- read phase (workers): taps, mix, allpass reads; nothing is written to the
+			 * rings.  The planner plans the next group meanwhile. ---- */
+			double       apw[4], ap[4], fb[8], mix;
+			const size_t o = ((size_t)g * RVL_G + (uint32_t)w) * TBF_SUB + n;
+			/* HBM traffic at the start of the group, a whole group ahead of any wait on it: the
+			 * input two groups ahead (every wave, the index clamped, so that no branch joins
+			 * the loaded register) and the previous group's tap mix.  Issued at the end of
+			 * the write phase, the copy a0n <- load at the loop's back edge waited for the
+			 * load, and for the store, right away. */
+			const double nxt = a0s[(size_t)min ((g + 2) * RVL_G + (uint32_t)min (w, RVL_G - 1), nSub - 1) * TBF_SUB + n];
+			if (pst)
+				rv_st (&bout[po], pmix);
+			if (act) {
+				/* the lines' vibrato sines: closed form on every line (wave-uniform, the rule), or
+				 * per line the closed form or the literal recurrence and sin */
+				const uint32_t om = __builtin_amdgcn_readfirstlane (sm.okm[par][w]);
+				double         sn[8];
+				if (om == 0xffu) {
 #pragma unroll
-				for (int l = 0; l < 8; l++) {
-					const double2 SC = sm.SC[par][w][l], q = sm.sc[par][l][n];
-					sn[l]            = SC.x + ((SC.y * q.x) - (SC.x * q.y));
-				}
-			} else {
-				const uint32_t ox = __builtin_amdgcn_readfirstlane (sm.okx[par][w]);
-#pragma unroll
-				for (int l = 0; l < 8; l++) {
-					if ((om >> l) & 1) {
+					for (int l = 0; l < 8; l++) {
 						const double2 SC = sm.SC[par][w][l], q = sm.sc[par][l][n];
 						sn[l]            = SC.x + ((SC.y * q.x) - (SC.x * q.y));
-					} else if ((ox >> l) & 1) { /* k_rv_core's rows for this step (rv_core_tap) */
-						const double2 SC = sm.SC[par][w][l];
-						const double  dn = (double)(n + 1) * sm.Dx[par][w][l]; /* exact */
-						const double  hh = sin (dn * 0.5);
-						const double  sd = sin (dn), cm = 2.0 * hh * hh;
-						sn[l]            = SC.x + ((SC.y * sd) - (SC.x * cm));
-					} else {
-						const double dl = rld (vdl, l);
-						double       v  = sm.v0[par][w][l];
-						for (int i = 0; i <= n; i++)
-							v += dl;
-						sn[l] = sin (v);
+					}
+				} else {
+					const uint32_t ox = __builtin_amdgcn_readfirstlane (sm.okx[par][w]);
+#pragma unroll
+					for (int l = 0; l < 8; l++) {
+						if ((om >> l) & 1) {
+							const double2 SC = sm.SC[par][w][l], q = sm.sc[par][l][n];
+							sn[l]            = SC.x + ((SC.y * q.x) - (SC.x * q.y));
+						} else if ((ox >> l) & 1) { /* k_rv_core's rows for this step (rv_core_tap) */
+							const double2 SC = sm.SC[par][w][l];
+							const double  dn = (double)(n + 1) * sm.Dx[par][w][l]; /* exact */
+							const double  hh = sin (dn * 0.5);
+							const double  sd = sin (dn), cm = 2.0 * hh * hh;
+							sn[l]            = SC.x + ((SC.y * sd) - (SC.x * cm));
+						} else {
+							const double dl = rld (vdl, l);
+							double       v  = sm.v0[par][w][l];
+							for (int i = 0; i <= n; i++)
+								v += dl;
+							sn[l] = sin (v);
+						}
 					}
 				}
-			}
-			double I[8];
+				double I[8];
 #pragma unroll
-			for (int l = 0; l < 8; l++) {
-				const double  off = (sn[l] + 1.0) * K.vibDepth;
-				const int     d   = RVL_DLY[l];
-				const double* rg  = sm.ring + RVL_LOFS[l];
-				const int     cn  = wrap_slot (rl (cw, l) + n + 1, d);
-				const int     wk  = (int)(cn + off); /* <= d + 5: the mirror covers wk + 1 */
-				const double  fr  = off - floor (off);
-				const double  r0 = rg[wk], r1 = rg[wk + 1];
-				double        x  = (r0 * (1 - fr));
-				x += (r1 * fr);
-				I[l] = (oneMB * x) + (r0 * K.blend);
-			}
-			I[0]  = (I[0] * K.oneMinusAbsCm) + (I[4] * K.crossmod);
-			I[4]  = (I[4] * K.oneMinusAbsCm) + (I[0] * K.crossmod);
-			fb[0] = (I[0] - (I[1] + I[2] + I[3])) * K.regen;
-			fb[1] = (I[1] - (I[0] + I[2] + I[3])) * K.regen;
-			fb[2] = (I[2] - (I[0] + I[1] + I[3])) * K.regen;
-			fb[3] = (I[3] - (I[0] + I[1] + I[2])) * K.regen;
-			fb[4] = (I[4] - (I[5] + I[6] + I[7])) * K.regen;
-			fb[5] = (I[5] - (I[4] + I[6] + I[7])) * K.regen;
-			fb[6] = (I[6] - (I[4] + I[5] + I[7])) * K.regen;
-			fb[7] = (I[7] - (I[4] + I[5] + I[6])) * K.regen;
-			mix = (I[0] + I[1] + I[2] + I[3] + I[4] + I[5] + I[6] + I[7]) / 8.0;
+				for (int l = 0; l < 8; l++) {
+					const double  off = (sn[l] + 1.0) * K.vibDepth;
+					const int     d   = RVL_DLY[l];
+					const double* rg  = sm.ring + RVL_LOFS[l];
+					const int     cn  = wrap_slot (rl (cw, l) + n + 1, d);
+					const int     wk  = (int)(cn + off); /* <= d + 5: the mirror covers wk + 1 */
+					const double  fr  = off - floor (off);
+					const double  r0 = rg[wk], r1 = rg[wk + 1];
+					double        x  = (r0 * (1 - fr));
+					x += (r1 * fr);
+					I[l] = (oneMB * x) + (r0 * K.blend);
+				}
+				I[0]  = (I[0] * K.oneMinusAbsCm) + (I[4] * K.crossmod);
+				I[4]  = (I[4] * K.oneMinusAbsCm) + (I[0] * K.crossmod);
+				fb[0] = (I[0] - (I[1] + I[2] + I[3])) * K.regen;
+				fb[1] = (I[1] - (I[0] + I[2] + I[3])) * K.regen;
+				fb[2] = (I[2] - (I[0] + I[1] + I[3])) * K.regen;
+				fb[3] = (I[3] - (I[0] + I[1] + I[2])) * K.regen;
+				fb[4] = (I[4] - (I[5] + I[6] + I[7])) * K.regen;
+				fb[5] = (I[5] - (I[4] + I[6] + I[7])) * K.regen;
+				fb[6] = (I[6] - (I[4] + I[5] + I[7])) * K.regen;
+				fb[7] = (I[7] - (I[4] + I[5] + I[6])) * K.regen;
+				mix = (I[0] + I[1] + I[2] + I[3] + I[4] + I[5] + I[6] + I[7]) / 8.0;
 #pragma unroll
-			for (int l = 8; l < 12; l++) {
-				const double old = sm.ring[RVL_LOFS[l] + rl (cw, l) + n + 1]; /* <= d + 64: mirror */
-				double       a   = a0;
-				a -= old * 0.5;
-				apw[l - 8] = a;
-				a *= 0.5;
-				a += old;
-				ap[l - 8] = a;
+				for (int l = 8; l < 12; l++) {
+					const double old = sm.ring[RVL_LOFS[l] + rl (cw, l) + n + 1]; /* <= d + 64: mirror */
+					double       a   = a0;
+					a -= old * 0.5;
+					apw[l - 8] = a;
+					a *= 0.5;
+					a += old;
+					ap[l - 8] = a;
+				}
+				if (n == NL - 1) {
+#pragma unroll
+					for (int l = 0; l < 8; l++)
+						sm.carry[par][w][l] = fb[l];
+				}
 			}
-			if (n == NL - 1) {
+			__syncthreads ();
+			/* ---- write phase ---- */
+			if (act) {
+				/* the previous sub-block's last feedback, all 8 lines read before any ring write */
+				const double* cp = w == 0 ? sm.carry[par ^ 1][RVL_G - 1] : sm.carry[par][w - 1];
+				double        cprv[8];
 #pragma unroll
 				for (int l = 0; l < 8; l++)
-					sm.carry[par][w][l] = fb[l];
+					cprv[l] = cp[l];
+#pragma unroll
+				for (int l = 8; l < 12; l++)
+					rvl_write (sm.ring + RVL_LOFS[l], wrap_slot (rl (cw, l) + n, RVL_DLY[l]), RVL_DLY[l], apw[l - 8]);
+				const int srcAp[8] = {3, 2, 1, 0, 0, 1, 2, 3};
+#pragma unroll
+				for (int l = 0; l < 8; l++) {
+					const double up   = lane_shr1 (fb[l]);
+					const double prev = n == 0 ? cprv[l] : up;
+					rvl_write (sm.ring + RVL_LOFS[l], wrap_slot (rl (cw, l) + n, RVL_DLY[l]), RVL_DLY[l], ap[srcAp[l]] + prev);
+				}
+				/* the tap mix, stored at the start of the next group (see above) */
+				pmix = mix;
+				po   = o;
 			}
-		} else if (w == RVL_G && g + 1 < nGrp) {
-			rvl_plan (sm, vdl, (int)min ((uint32_t)RVL_G, nSub - (g + 1) * RVL_G), par ^ 1, force, P.errFlags);
+			pst = act;
+			a0  = a0n;
+			a0n = nxt;
+			cw = wrap_slot (cw + TBF_SUB * RVL_G, dlyv);
+			__syncthreads ();
 		}
-		__syncthreads ();
-		/* ---- write phase ---- */
-		if (act) {
-			/* the previous sub-block's last feedback, all 8 lines read before any ring write */
-			const double* cp = w == 0 ? sm.carry[par ^ 1][RVL_G - 1] : sm.carry[par][w - 1];
-			double        cprv[8];
-#pragma unroll
-			for (int l = 0; l < 8; l++)
-				cprv[l] = cp[l];
-#pragma unroll
-			for (int l = 8; l < 12; l++)
-				rvl_write (sm.ring + RVL_LOFS[l], wrap_slot (rl (cw, l) + n, RVL_DLY[l]), RVL_DLY[l], apw[l - 8]);
-			const int srcAp[8] = {3, 2, 1, 0, 0, 1, 2, 3};
-#pragma unroll
-			for (int l = 0; l < 8; l++) {
-				const double up   = lane_shr1 (fb[l]);
-				const double prev = n == 0 ? cprv[l] : up;
-				rvl_write (sm.ring + RVL_LOFS[l], wrap_slot (rl (cw, l) + n, RVL_DLY[l]), RVL_DLY[l], ap[srcAp[l]] + prev);
+	} else {
+#pragma unroll 1
+		for (uint32_t g = 0; g < nGrp; g++) {
+			if (g + 1 < nGrp) {
+				/* the planner is the youngest wave of its SIMD: at equal priority the two
+				 * workers beside it took the issue slots first and every worker waited for
+				 * the plan at the barrier (tools/rvl_prof.py: 5.7k cycles per group against
+				 * 3.3-4.8k for a worker's read phase) */
+				__builtin_amdgcn_s_setprio (2);
+				rvl_plan (sm, vdl, (int)min ((uint32_t)RVL_G, nSub - (g + 1) * RVL_G), (g & 1) ^ 1, force, P.errFlags);
+				__builtin_amdgcn_s_setprio (0);
 			}
-			/* the tap mix, stored at the start of the next group (see above) */
-			pmix = mix;
-			po   = o;
+			__syncthreads ();
+			__syncthreads ();
 		}
-		pst = act;
-		a0  = a0n;
-		a0n = nxt;
-		cw = wrap_slot (cw + TBF_SUB * RVL_G, dlyv);
-		__syncthreads ();
 	}
 	if (pst)
 		rv_st (&bout[po], pmix);
@@ -1606,7 +1627,12 @@ __device__ __forceinline__ int rvc_slot (int c, int d, int k)
 	return v > d ? v - d - 1 : v;
 }
 
-/* a helper task's per-block reverb wet level, lane b = block b of the launch (<= 64 blocks) */
+/* a launch's per-block values sit one per lane: lane b = block b.  A launch of more than 64
+ * blocks has no control deltas (every block plays the instance's current entry), so its
+ * blocks past 63 read lane 63 */
+__device__ __forceinline__ int blk_lane (int b) { return b < NL ? b : NL - 1; }
+
+/* a helper task's per-block reverb wet level, lane b = block b of the launch */
 __device__ __forceinline__ double rvc_wet_lanes (const tbf_launch& P, const tbf_seg_ctl* __restrict__ ctl, uint32_t inst)
 {
 	const uint32_t b = threadIdx.x & (NL - 1);
@@ -1779,7 +1805,7 @@ k_rv_pre (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 #pragma unroll
 			for (int t = 0; t < RVC_NTK; t++)
 				if (h + t * RVC_H < nj)
-					ra[t][(size_t)k2 * RVC_T] = sin (sv[t] * rld (wetv[t], (k2 * RVC_T) / TBF_BLK));
+					ra[t][(size_t)k2 * RVC_T] = sin (sv[t] * rld (wetv[t], blk_lane ((k2 * RVC_T) / TBF_BLK)));
 		}
 		__syncthreads ();
 	};
@@ -1917,7 +1943,7 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 		 * half-waves hold L and R, and 0.7071 (L + R) == 0.7071 (R + L) */
 		float yv[RVC_NTK];
 		if (it >= 4) {
-			const int ob = ((it - 4) * RVC_T) / TBF_BLK;
+			const int ob = blk_lane (((it - 4) * RVC_T) / TBF_BLK);
 #pragma unroll
 			for (int t = 0; t < RVC_NTK; t++) {
 				const double wet = rld (wetv[t], ob);
@@ -2169,24 +2195,31 @@ __device__ __forceinline__ void motion_add (float* ring, int U, float a, float b
 	}
 }
 
-/* motion_add for a motion whose slot advances by exactly one per sample over the
- * sub-block (U_n = U_0 + n: the common case at slow and stopped rotor speeds): slot U_n
- * receives b of sample n-1, then a of sample n; lane 63's b goes to slot U_63 + 1.  Lane
- * 0's slot got sample -1's b in the previous sub-block.  Same adds, same order. */
+/* One pass of motion_add over all four rings (motion q of each), branch-free: every lane
+ * reads its two slots of every ring, then every lane writes both, a lane that owns no slot
+ * (or no slot t + 1) into its own sink entry.  So the four rings' reads go out together
+ * and the pass costs one LDS round trip (per ring and motion, a branch on unit steps and
+ * a read-modify-write of lane 63's slot t + 1 after the others' writes had cost up to two).
+ * The same adds in the same order as motion_add. */
 template <int W>
-__device__ __forceinline__ void unit_add (float* ring, int U, float a, float b, int lane)
+__device__ __forceinline__ void motion_pass4 (float (*ring)[W], float (*sink)[TBF_SUB], const int (&mu)[4][3],
+                                              const float (&ma)[4][3], const float (&mb)[4][3], const int q, int lane)
 {
 	const uint32_t WM = (uint32_t)W - 1u;
-	const float    bp = lane_shr1 (b);
-	const uint32_t i0 = (uint32_t)U & WM;
-	float          v  = ring[i0];
-	if (lane > 0)
-		v += bp;
-	v += a;
-	ring[i0] = v;
-	if (lane == NL - 1) {
-		const uint32_t i1 = (i0 + 1u) & WM;
-		ring[i1]          = ring[i1] + b;
+	MotionOwn      m[4];
+	float          v[4], w[4];
+#pragma unroll
+	for (int gi = 0; gi < 4; gi++) {
+		m[gi] = motion_own (mu[gi][q], ma[gi][q], mb[gi][q], lane);
+		v[gi] = ring[gi][m[gi].t & WM];
+		w[gi] = ring[gi][(m[gi].t + 1) & WM];
+	}
+#pragma unroll
+	for (int gi = 0; gi < 4; gi++) {
+		const float nv = motion_sum_t (m[gi], v[gi]);
+		const float nw = motion_sum_t1 (m[gi], w[gi]);
+		*(m[gi].first ? &ring[gi][m[gi].t & WM] : &sink[0][lane])                  = nv;
+		*(m[gi].first && m[gi].own2 ? &ring[gi][(m[gi].t + 1) & WM] : &sink[1][lane]) = nw;
 	}
 }
 
@@ -2221,11 +2254,33 @@ __device__ __forceinline__ void wh_serial (const float* ip, float* tp, float* fz
 	fz[1] = z1;
 }
 
-/* whirlProc2 (src/whirl.cpp:1191-1638) + whirlProc3 mic mix (1653-1681) */
+/* A sub-block's two output stores, held back until the next sub-block has issued its
+ * motion-table loads: vmcnt retires in issue order, so a store issued before a load is
+ * waited for with it, and every sub-block waits for its table loads (and every block for
+ * its input) -- with the stores issued first, each of those waits also waited out the
+ * previous stores' write latency. */
+struct WhOut {
+	float* l;
+	float* r;
+	float  vl, vr;
+};
+
+/* the held stores; unconditional (a store under a branch makes the wait counts after it
+ * unknown, and the compiler then waits for everything) */
+__device__ __forceinline__ void wh_flush (const WhOut& o)
+{
+	*o.l = o.vl;
+	*o.r = o.vr;
+}
+
+/* whirlProc2 (src/whirl.cpp:1191-1638) + whirlProc3 mic mix (1653-1681).  in0 / in1: this
+ * block's input (samples lane, lane + 64); the next block's is loaded from inNext into
+ * nx0 / nx1 during the first sub-block (inNext may be this block's own input when there
+ * is no next block: a harmless re-read) */
 template <int W>
 __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypass, const int revOpt, const tbf_inst_const& K,
-                             const float in0, const float in1, const float nin0, const bool hasNext,
-                             float* __restrict__ oL, float* __restrict__ oR)
+                             const float in0, const float in1, const float* __restrict__ inNext, float& nx0, float& nx1,
+                             const bool hasNext, float* __restrict__ oL, float* __restrict__ oR, WhOut& pend)
 {
 	const int     lane  = threadIdx.x;
 	tbf_wh_state& st    = sm.st;
@@ -2238,12 +2293,18 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 
 	if (bypass) {
 		/* whirlProc2 bypass (src/whirl.cpp:1197-1215) + whirlProc3 mix */
-		for (int k = 0; k < 2; k++) {
-			const int   n = lane + k * NL;
-			const float x = k == 0 ? in0 : in1;
-			oL[n] = x * K.mic[0] + x * K.mic[1] + 0.f * K.mic[2] + 0.f * K.mic[3];
-			oR[n] = x * K.mic[4] + x * K.mic[5] + 0.f * K.mic[6] + 0.f * K.mic[7];
-		}
+		nx0 = inNext[lane];
+		nx1 = inNext[lane + NL];
+		wh_flush (pend);
+		oL[lane] = in0 * K.mic[0] + in0 * K.mic[1] + 0.f * K.mic[2] + 0.f * K.mic[3];
+		oR[lane] = in0 * K.mic[4] + in0 * K.mic[5] + 0.f * K.mic[6] + 0.f * K.mic[7];
+		/* the second sub-block's outputs become the held stores, so that the held
+		 * stores always carry the latest output of their lane (a later flush of an older
+		 * one would overwrite a newer value) */
+		pend.l  = oL + NL + lane;
+		pend.r  = oR + NL + lane;
+		pend.vl = in1 * K.mic[0] + in1 * K.mic[1] + 0.f * K.mic[2] + 0.f * K.mic[3];
+		pend.vr = in1 * K.mic[4] + in1 * K.mic[5] + 0.f * K.mic[6] + 0.f * K.mic[7];
 		return;
 	}
 	if (lane == 0) {
@@ -2301,7 +2362,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 		 * ahead (launch start, after a bypassed block). */
 		const bool aNext = sb + 1 < TBF_BLK / TBF_SUB || hasNext;
 		if (aNext)
-			sm.xn[n] = (float)((double)(sb + 1 < TBF_BLK / TBF_SUB ? in1 : nin0) + 1e-14);
+			sm.xn[n] = (float)((double)(sb + 1 < TBF_BLK / TBF_SUB ? in1 : nx0) + 1e-14);
 		wave_sync ();
 		if (!sm.aReady) {
 			if (lane == 0)
@@ -2430,6 +2491,13 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 						b5v[gi][q]        = b[4];
 					}
 				}
+			/* behind the table loads: the next block's input (used from the second
+			 * sub-block on; the second sub-block loads it again, so that every sub-block
+			 * issues the same memory operations in the same order and each wait is
+			 * counted exactly) and the previous sub-block's output stores */
+			nx0 = inNext[lane];
+			nx1 = inNext[lane + NL];
+			wh_flush (pend);
 #pragma unroll
 			for (int gi = 0; gi < 4; gi++) {
 				const int r = r0 + gi;
@@ -2466,10 +2534,9 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 			 * non-decreasing in n with groups of <= 2 equal slots, and the ring's motions
 			 * >= 2 slots apart in source order at every sample (so passes farthest-first
 			 * keep the per-slot order: a farther motion reaches a slot only at earlier
-			 * samples); per motion: unit steps (unit_add instead of motion_add) */
-			bool     okr[4];
-			uint32_t unit = 0;
-			bool     allOk = !(P.dbg & TBF_DEBUG_FORCE_SERIAL);
+			 * samples) */
+			bool okr[4];
+			bool allOk = !(P.dbg & TBF_DEBUG_FORCE_SERIAL);
 #pragma unroll
 			for (int gi = 0; gi < 4; gi++) {
 				int ok = (mu[gi][1] >= mu[gi][0] + 2) && (mu[gi][2] >= mu[gi][1] + 2);
@@ -2481,8 +2548,6 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 						ok = 0;
 					if (lane > 0 && lane < NL - 1 && up == mu[gi][q] && un == mu[gi][q])
 						ok = 0;
-					if (__all (lane == 0 || mu[gi][q] == up + 1))
-						unit |= 1u << (gi * 3 + q);
 				}
 				okr[gi] = __all (ok) && !(P.dbg & TBF_DEBUG_FORCE_SERIAL);
 				allOk   = allOk && okr[gi];
@@ -2492,13 +2557,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 				 * (farthest motion first) updates all of them in one LDS round trip */
 #pragma unroll
 				for (int q = 2; q >= 0; q--) {
-#pragma unroll
-					for (int gi = 0; gi < 4; gi++) {
-						if ((unit >> (gi * 3 + q)) & 1u)
-							unit_add<W> (sm.wring[r0 + gi], mu[gi][q], ma[gi][q], mb[gi][q], lane);
-						else
-							motion_add<W> (sm.wring[r0 + gi], mu[gi][q], ma[gi][q], mb[gi][q], lane);
-					}
+					motion_pass4<W> (sm.wring, sm.sink, mu, ma, mb, q, lane);
 					wave_sync ();
 				}
 			} else {
@@ -2540,8 +2599,10 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 			const float hR   = K.hornLevel * hrv + leak;
 			const float dL   = sm.rd[0][n];
 			const float dR   = sm.rd[1][n];
-			oL[sb * TBF_SUB + n] = hL * K.mic[0] + hR * K.mic[1] + dL * K.mic[2] + dR * K.mic[3];
-			oR[sb * TBF_SUB + n] = hL * K.mic[4] + hR * K.mic[5] + dL * K.mic[6] + dR * K.mic[7];
+			pend.l           = oL + sb * TBF_SUB + n;
+			pend.r           = oR + sb * TBF_SUB + n;
+			pend.vl          = hL * K.mic[0] + hR * K.mic[1] + dL * K.mic[2] + dR * K.mic[3];
+			pend.vr          = hL * K.mic[4] + hR * K.mic[5] + dL * K.mic[6] + dR * K.mic[7];
 		}
 		/* ---- carry filter taps and histories ---- */
 		if (lane == NL - 1) {
@@ -2597,8 +2658,9 @@ k_whirl (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 	for (uint32_t i = threadIdx.x; i < 4u * W; i += NL)
 		(&sm.wring[0][0])[i] = wr[i];
 	wave_sync ();
-	/* the input (lane n: samples n and n + 64 of a block) is loaded one block ahead, so
-	 * its latency overlaps a whole block instead of stalling a sub-block start */
+	/* the input (lane n: samples n and n + 64 of a block) is loaded one block ahead, in
+	 * the block's first sub-block behind its table loads (stage_whirl), so its latency
+	 * overlaps a whole sub-block and no wait for it waits for output stores */
 	const float* inBase = P.mid2 + (size_t)inst * P.midStride;
 	/* the launch's per-block control (bypass, rotary selection), lane b = block b (<= 64
 	 * blocks): read once, so no block waits on the two dependent control loads */
@@ -2614,17 +2676,20 @@ k_whirl (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 		c0 = inBase[threadIdx.x];
 		c1 = inBase[threadIdx.x + NL];
 	}
+	/* before the first sub-block's outputs exist, the held store writes 0 to the first
+	 * output sample of the lane, which the real output overwrites later (same lane, same
+	 * address: in order) */
+	WhOut pend;
+	pend.l  = P.outL + (size_t)inst * P.outStride + P.outOffset + threadIdx.x;
+	pend.r  = P.outR + (size_t)inst * P.outStride + P.outOffset + threadIdx.x;
+	pend.vl = pend.vr = 0.f;
 	for (uint32_t blk = 0; blk < P.nBlocks; blk++) {
 		float*     oL = P.outL + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
 		float*     oR = P.outR + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
-		float      n0 = 0.f, n1 = 0.f;
+		float      n0, n1;
 		const bool more = blk + 1 < P.nBlocks;
-		if (more) {
-			n0 = inBase[(size_t)(blk + 1) * TBF_BLK + threadIdx.x];
-			n1 = inBase[(size_t)(blk + 1) * TBF_BLK + threadIdx.x + NL];
-		}
 		/* a new parameter set (MIDI control functions) from this block on */
-		const int ws = rl (wsv, (int)blk);
+		const int ws = rl (wsv, blk_lane ((int)blk));
 		if (ws) {
 			const uint32_t* src = (const uint32_t*)(P.whSets + (ws - 1));
 			if (threadIdx.x < sizeof (tbf_wh_params) / 4)
@@ -2633,12 +2698,15 @@ k_whirl (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 		}
 		/* horn filter A may run ahead into the next block unless that one is bypassed or
 		 * changes its coefficients */
-		const int  nx      = (int)min (blk + 1, (uint32_t)NL - 1);
+		const int  nx      = blk_lane ((int)blk + 1);
 		const bool hasNext = more && !rl (byv, nx) && !rl (wsv, nx);
-		stage_whirl<W> (P, sm, rl (byv, (int)blk) != 0, rl (rvv, (int)blk), K, c0, c1, n0, hasNext, oL, oR);
+		stage_whirl<W> (P, sm, rl (byv, blk_lane ((int)blk)) != 0, rl (rvv, blk_lane ((int)blk)), K, c0, c1,
+		                inBase + (size_t)(more ? blk + 1 : blk) * TBF_BLK, n0, n1, hasNext, oL, oR, pend);
 		c0 = n0;
 		c1 = n1;
 	}
+	if (P.nBlocks > 0)
+		wh_flush (pend);
 	wave_sync ();
 	copy_words (S, &sm.st);
 	for (uint32_t i = threadIdx.x; i < 4u * W; i += NL)
@@ -2654,7 +2722,7 @@ extern "C" int tbf_launch_stage (const tbf_launch* P, int k, hipStream_t stream)
 		return 0;
 	if ((uint64_t)P->nBlocks * TBF_BLK > P->midStride)
 		return -22;
-	if ((k == 2 || k == 4 || k == 5) && P->nBlocks > NL) /* a launch's per-block controls sit one per lane */
+	if ((k == 2 || k == 4 || k == 5) && P->nBlocks > NL && P->ctlIdx) /* per-block controls one per lane (blk_lane) */
 		return -22;
 	const dim3 grid (P->nInst), block (NL);
 	const dim3 cgrid ((P->nInst + RVC_CB - 1) / RVC_CB), cblock (RVC_THREADS);

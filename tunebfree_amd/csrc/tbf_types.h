@@ -182,6 +182,14 @@ typedef struct tbf_rv_chan { /* one channel of the feedback network: k_rv_core w
  * and guards it with the dither state of that sample.  TBF_PD_HIST floats per instance,
  * indexed by absolute sample position mod TBF_PD_HIST, in the slab's line-12 region. */
 #define TBF_PD_HIST 1024
+/* blocks of a render chunk: a chunk with control deltas has at most 64 (TBF_CHUNK, the
+ * kernels keep a launch's per-block controls one per lane); a chunk without (every block
+ * plays each instance's current control) up to TBF_STEADY_MAX, so the per-launch state
+ * traffic (above all the reverb network's LDS rings) spreads over more samples */
+#define TBF_STEADY_MAX 256
+/* each reverb line of the slab starts on a 128-B boundary (16 doubles): a wave's 64
+ * consecutive doubles then cover exactly four whole cache lines */
+#define TBF_RING_ALIGN 16
 
 typedef struct tbf_rv_state { /* reverb: k_rv_pre / k_rv_core / k_rv_post */
 	int32_t     pdAge;        /* samples rendered, saturating at delayM (the predelay reads 0 before) */

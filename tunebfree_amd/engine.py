@@ -135,6 +135,15 @@ class Engine:
         _check(f(self._h, C.byref(w), C.byref(a), C.byref(s)))
         return {"wring_len": w.value, "max_ahead": a.value, "slab_len": s.value}
 
+    def chunks(self):
+        """Blocks per render chunk (tbf_debug_chunks): (with control deltas, without)."""
+        f = self._lib.tbf_debug_chunks
+        f.restype = C.c_int
+        f.argtypes = [C.c_void_p, _u32p, _u32p]
+        d, s = C.c_uint32(), C.c_uint32()
+        _check(f(self._h, C.byref(d), C.byref(s)))
+        return d.value, s.value
+
     def template(self, mts128=None, ratio9=None, seed=1):
         m = None if mts128 is None else np.ascontiguousarray(mts128, dtype=np.float64)
         r = None if ratio9 is None else np.ascontiguousarray(ratio9, dtype=np.float64)

@@ -4,8 +4,9 @@
 per GPU (configs[2] at N=1; configs[3] = 8 x 4096 at N=8, weak scaling), with
 max|err| vs the CPU chain.
 
-A "step" is one kernel pass over the batch: every instance renders `--blocks`
-128-sample blocks (default 64 = 8192 stereo samples per instance).  Inputs are
+A "step" is one render call over the batch: every instance renders `--blocks`
+128-sample blocks (default 256 = 32768 stereo samples, 0.68 s of audio, per instance: one
+steady chunk of the engine, i.e. one launch of each of the six stages).  Inputs are
 synthetic: instance i plays the "Jazz 1 all" registration (pgm/default.pgm:27-36)
 with overdrive character 0.5, reverb 0.1, rotary chorale, chord root 48+(i mod 24)
 + {0,4,7,12}; note-on lands at block 0 of the first warmup step.
@@ -48,7 +49,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=4096, help="instances per GPU")
-    ap.add_argument("--blocks", type=int, default=64, help="128-sample blocks per step")
+    ap.add_argument("--blocks", type=int, default=256,
+                    help="128-sample blocks per step (one render call; a steady chunk is up to 256 blocks)")
     ap.add_argument("--sr", type=float, default=None, help="sample rate (default 48000; 96000 for cfg5)")
     ap.add_argument("--workload", choices=("cfg3", "cfg2", "cfg5"), default="cfg3",
                     help="cfg3: BASELINE configs[2]/[3] (the metric's workload); cfg2: configs[1] (tonegen only, "

@@ -58,8 +58,8 @@ for s in $STEPS; do
 		;;
 	iso) run iso 300 python3 bench.py --isolated 1 --cpu-baseline 0 ;;
 	prof) # phase clocks of k_rv_core_lds and k_whirl (build variants from tools/*_prof_patch.py)
-		run rvl_prof 200 env TBF_LIB=tunebfree_amd/_variants/libtbf_rvlprof.so python3 tools/rvl_prof.py
-		run whirl_prof 200 env TBF_LIB=tunebfree_amd/_variants/libtbf_whprof.so python3 tools/whirl_prof.py ;;
+		run rvl_prof 200 env TBF_LIB=tunebfree_amd/_prof/libtbf_rvlprof.so python3 tools/rvl_prof.py
+		run whirl_prof 200 env TBF_LIB=tunebfree_amd/_prof/libtbf_whprof.so python3 tools/whirl_prof.py ;;
 	calib) # FETCH_SIZE / WRITE_SIZE of known streams: aligned and 64 B misaligned 8-B/lane reads and writes
 		run calib_f 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/calib_f" -o run --output-format csv -- python3 tools/calib_pmc.py 2 0,2,1,3
 		run calib_w 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/calib_w" -o run --output-format csv -- python3 tools/calib_pmc.py 2 0,2,1,3 ;;

@@ -37,7 +37,12 @@
 #define TG_SPLIT_MAX 8 /* k_tonegen block ranges (waves) per instance */
 #define TG_PCAP 128    /* a delta chunk's program entries staged in LDS per block (longer: read from HBM) */
 #define RV_WAVES 3
+#ifndef WH_WAVES
 #define WH_WAVES 3
+#endif
+#ifndef WH_RG
+#define WH_RG 4 /* k_whirl rings per motion group (4 or 2) */
+#endif
 /* wave priority raised (s_setprio 1) while a wave runs a serial chain, so the SIMD issues
  * the chain's dependent instructions ahead of other waves' lane-parallel work */
 #define PRIO_UP() __builtin_amdgcn_s_setprio (1)
@@ -2195,27 +2200,27 @@ __device__ __forceinline__ void motion_add (float* ring, int U, float a, float b
 	}
 }
 
-/* One pass of motion_add over all four rings (motion q of each), branch-free: every lane
- * reads its two slots of every ring, then every lane writes both, a lane that owns no slot
- * (or no slot t + 1) into its own sink entry.  So the four rings' reads go out together
+/* One pass of motion_add over a group of RG rings (motion q of each), branch-free: every
+ * lane reads its two slots of every ring, then every lane writes both, a lane that owns no
+ * slot (or no slot t + 1) into its own sink entry.  So the rings' reads go out together
  * and the pass costs one LDS round trip (per ring and motion, a branch on unit steps and
  * a read-modify-write of lane 63's slot t + 1 after the others' writes had cost up to two).
  * The same adds in the same order as motion_add. */
-template <int W>
-__device__ __forceinline__ void motion_pass4 (float (*ring)[W], float (*sink)[TBF_SUB], const int (&mu)[4][3],
-                                              const float (&ma)[4][3], const float (&mb)[4][3], const int q, int lane)
+template <int W, int RG>
+__device__ __forceinline__ void motion_pass (float (*ring)[W], float (*sink)[TBF_SUB], const int (&mu)[RG][3],
+                                             const float (&ma)[RG][3], const float (&mb)[RG][3], const int q, int lane)
 {
 	const uint32_t WM = (uint32_t)W - 1u;
-	MotionOwn      m[4];
-	float          v[4], w[4];
+	MotionOwn      m[RG];
+	float          v[RG], w[RG];
 #pragma unroll
-	for (int gi = 0; gi < 4; gi++) {
+	for (int gi = 0; gi < RG; gi++) {
 		m[gi] = motion_own (mu[gi][q], ma[gi][q], mb[gi][q], lane);
 		v[gi] = ring[gi][m[gi].t & WM];
 		w[gi] = ring[gi][(m[gi].t + 1) & WM];
 	}
 #pragma unroll
-	for (int gi = 0; gi < 4; gi++) {
+	for (int gi = 0; gi < RG; gi++) {
 		const float nv = motion_sum_t (m[gi], v[gi]);
 		const float nw = motion_sum_t1 (m[gi], w[gi]);
 		*(m[gi].first ? &ring[gi][m[gi].t & WM] : &sink[0][lane])                  = nv;
@@ -2452,18 +2457,18 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 		const float xd2v = (float)((0.4 * xd1v) + (0.4 * sm.xd1[n]));
 		wave_sync ();
 
-		/* ---- rings (HL, HR, DL, DR) in groups of 4: the group's motions first (their
+		/* ---- rings (HL, HR, DL, DR) in groups of WH_RG: the group's motions first (their
 		 * table loads in flight together), then each ring's ordered adds ---- */
 #pragma unroll
-		for (int r0 = 0; r0 < 4; r0 += 4) {
-			int   mu[4][3];
-			float ma[4][3], mb[4][3];
+		for (int r0 = 0; r0 < 4; r0 += WH_RG) {
+			int   mu[WH_RG][3];
+			float ma[WH_RG][3], mb[WH_RG][3];
 			/* the table positions of all 12 motions, then every table load (18) in flight
 			 * together, then the arithmetic: issued motion by motion, each motion's loads
 			 * were waited for before the next motion's were issued */
-			float h1v[4][3];
+			float h1v[WH_RG][3];
 #pragma unroll
-			for (int gi = 0; gi < 4; gi++)
+			for (int gi = 0; gi < WH_RG; gi++)
 #pragma unroll
 				for (int q = 0; q < 3; q++) {
 					const int p = ((r0 + gi) & 1) + 2 * q;
@@ -2472,11 +2477,11 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 					else /* DR_MOTION, src/whirl.cpp:1457 */
 						h1v[gi][q] = (float)(da * (unsigned int)16384 + K.hornPhase[p]);
 				}
-			f2u   dpv[4][3];
+			f2u   dpv[WH_RG][3];
 			f4u   b4v[2][3];
 			float b5v[2][3];
 #pragma unroll
-			for (int gi = 0; gi < 4; gi++)
+			for (int gi = 0; gi < WH_RG; gi++)
 #pragma unroll
 				for (int q = 0; q < 3; q++) {
 					const int      p   = ((r0 + gi) & 1) + 2 * q;
@@ -2495,11 +2500,13 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 			 * sub-block on; the second sub-block loads it again, so that every sub-block
 			 * issues the same memory operations in the same order and each wait is
 			 * counted exactly) and the previous sub-block's output stores */
-			nx0 = inNext[lane];
-			nx1 = inNext[lane + NL];
-			wh_flush (pend);
+			if (r0 == 0) {
+				nx0 = inNext[lane];
+				nx1 = inNext[lane + NL];
+				wh_flush (pend);
+			}
 #pragma unroll
-			for (int gi = 0; gi < 4; gi++) {
+			for (int gi = 0; gi < WH_RG; gi++) {
 				const int r = r0 + gi;
 #pragma unroll
 				for (int q = 0; q < 3; q++) {
@@ -2535,10 +2542,10 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 			 * >= 2 slots apart in source order at every sample (so passes farthest-first
 			 * keep the per-slot order: a farther motion reaches a slot only at earlier
 			 * samples) */
-			bool okr[4];
+			bool okr[WH_RG];
 			bool allOk = !(P.dbg & TBF_DEBUG_FORCE_SERIAL);
 #pragma unroll
-			for (int gi = 0; gi < 4; gi++) {
+			for (int gi = 0; gi < WH_RG; gi++) {
 				int ok = (mu[gi][1] >= mu[gi][0] + 2) && (mu[gi][2] >= mu[gi][1] + 2);
 #pragma unroll
 				for (int q = 0; q < 3; q++) {
@@ -2557,12 +2564,12 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 				 * (farthest motion first) updates all of them in one LDS round trip */
 #pragma unroll
 				for (int q = 2; q >= 0; q--) {
-					motion_pass4<W> (sm.wring, sm.sink, mu, ma, mb, q, lane);
+					motion_pass<W, WH_RG> (sm.wring + r0, sm.sink, mu, ma, mb, q, lane);
 					wave_sync ();
 				}
 			} else {
 #pragma unroll
-				for (int gi = 0; gi < 4; gi++) {
+				for (int gi = 0; gi < WH_RG; gi++) {
 					float* ring = sm.wring[r0 + gi];
 					if (okr[gi]) {
 						motion_add<W> (ring, mu[gi][2], ma[gi][2], mb[gi][2], lane);

@@ -420,8 +420,13 @@ def main():
             step_bytes = sum(algo[k] for k in kern)
             step_gbs = B * nsamp * step_bytes / (elapsed / a.steps) / 1e9  # per GPU
             ms = kern[dom]
-            roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            # the LDS-resident network moves far fewer bytes than the algorithm streams: what
+            # limits it is the latency and issue of its per-sample work, so `bound` names that,
+            # and the fraction of the HBM roofline the algorithmic bytes reach is kept beside it
+            lds_net = dom == "k_rv_core" and os.environ.get("TBF_RV_LDS", "1") != "0"
+            roof = {"bound": "latency" if lds_net else "hbm", "roofline": "hbm",
+                    "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": achieved / HBM_PEAK_GBS, "frac_algorithmic": achieved / HBM_PEAK_GBS, "traffic": traffic,
                     # the HBM bytes the kernel really moves (PMC) over the same time
                     "hbm_frac_actual": (traffic / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
                     "kernel": dom, "kernel_ms_per_launch": kern[dom],
@@ -432,14 +437,15 @@ def main():
                     "step_frac": step_gbs / HBM_PEAK_GBS,
                     "kernels_ms_per_launch": kern, "kernels_ms_isolated": kern_iso,
                     "reverb_core": ("k_rv_core_lds: a channel's 12 rings LDS-resident for the launch "
-                                    "(loaded and stored once per 64-block chunk), so its HBM traffic is "
+                                    "(loaded and stored once per launch: a steady chunk of up to 256 blocks), so its HBM traffic is "
                                     "far below the algorithmic ring bytes it is quoted against"
                                     if os.environ.get("TBF_RV_LDS", "1") != "0" else
                                     "k_rv_core: rings streamed through HBM every sample"),
-                    "limited_by": ("not HBM: latency of the per-sample network (LDS tap reads, two "
-                                   "barriers per 704-sample group) at one 12-wave workgroup per CU, and "
-                                   "waiting for whole CUs to drain beside the other stages (hbm_frac_actual)"
-                                   if dom == "k_rv_core" and os.environ.get("TBF_RV_LDS", "1") != "0" else None),
+                    "limited_by": ("not HBM: issue and latency of the per-sample network at one 12-wave "
+                                   "workgroup per CU (a read phase of sines, tap reads, interpolation and "
+                                   "Householder mix, then the ring writes, two barriers per 704-sample group; "
+                                   "tools/rvl_prof.py), plus its ring load and store per launch (hbm_frac_actual)"
+                                   if lds_net else None),
                     "timing": "HIP events on each launch's stream while neighbouring chunks' "
                               "kernels overlap (cross-chunk pipelining, as in the timed region)"}
         if roof is not None and bank_entries is not None and "k_tonegen" in kern:

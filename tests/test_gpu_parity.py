@@ -499,6 +499,80 @@ def test_gpu_device_front_end_note_chunks(oracle):
     assert max(eL, eR) <= TOL
 
 
+def test_gpu_device_front_end_param_events(oracle):
+    """Chunks of notes, drawbar moves (upper and bus drawbars, the percussion trigger bus
+    while percussion is on and off), vibrato switches and the percussion switches are
+    stepped on the device (k_front, §8(f) row 1): 1100 instances over 192 blocks, a
+    parameter event on most blocks of most instances.  Bit for bit against the host front
+    end (TBF_DEVICE_FRONT=0) and against the oracle for a sample.  (Drawbar settings stay
+    in 0..8: setDrawBar asserts that, src/tonegen.cpp:2741; the engine ignores others, and
+    test_control_cpu covers that.)"""
+    import os
+    import torch
+    import tunebfree_amd as T
+    from orc_bind import Template
+    n, nb = 1100, 192
+    seeds = [9000 + i for i in range(n)]
+    rows, oscen = [], [[] for _ in range(n)]
+
+    def ev(b, i, kind, a, v):
+        rows.append((b, i, 0 if kind == "note" else 1, a, float(v)))
+        oscen[i].append((b, kind, a, v))
+
+    for i in range(n):
+        for (k, a, v) in S.jazz1_params():
+            ev(0, i, k, a, v)
+        for k in S.chord_for(i):
+            ev(0, i, "note", k, 1)
+        for b in range(1, nb):
+            r = (i * 7 + b * 3) % 23
+            if r < 9:
+                ev(b, i, "param", S.P_DRAWBAR + r, (i + b) % 9)
+            elif r < 12:
+                ev(b, i, "param", S.P_BUS_DRAWBAR + 9 + (i + b) % 18, (i + 2 * b) % 9)  # lower / pedal buses
+            elif r == 12:
+                ev(b, i, "param", S.P_VIBRATO, (b // 12) % 2)
+            elif r == 13:
+                ev(b, i, "param", S.P_VIB_LOWER, (b // 17) % 2)
+            elif r == 14:
+                ev(b, i, "param", S.P_PERC, (b // 10) % 2)
+            elif r == 15:
+                ev(b, i, "param", S.P_PERC_HARM, (b // 13) % 2)
+            elif r == 16:
+                ev(b, i, "param", S.P_DRAWBAR + 8, (b % 9))  # the percussion trigger bus
+            if b % 5 == 0:
+                ev(b, i, "note", 55 + (i + b - 1) % 17, 0)
+                ev(b, i, "note", 55 + (i + b) % 17, 1)
+    rows.sort(key=lambda r: r[0])
+    outs = []
+    for front in (True, False):
+        if not front:
+            os.environ["TBF_DEVICE_FRONT"] = "0"
+        try:
+            eng = T.Engine(sample_rate=48000.0, device=0)
+        finally:
+            os.environ.pop("TBF_DEVICE_FRONT", None)
+        tid = eng.template(seed=7)
+        eng.add_instances([tid] * n, seeds)
+        evs = eng.events(rows)
+        L = torch.zeros((n, nb * 128), dtype=torch.float32, device="cuda")
+        R = torch.zeros_like(L)
+        eng.render_events_device(nb, evs, L.data_ptr(), R.data_ptr(), nb * 128)
+        eng.synchronize()
+        outs.append((L.cpu().numpy(), R.cpu().numpy()))
+        eng.close()
+        del L, R
+    assert np.array_equal(outs[0][0].view(np.uint32), outs[1][0].view(np.uint32))
+    assert np.array_equal(outs[0][1].view(np.uint32), outs[1][1].view(np.uint32))
+    sample = [0, 1, 2, 3, 550, n - 1]
+    tpl = Template(oracle, seed=7)
+    oL, oR, *_ = oracle_run(oracle, tpl, [seeds[i] for i in sample], [sorted(oscen[i], key=lambda r: r[0]) for i in sample], nb)
+    eL, xL = compare(outs[0][0][sample], oL)
+    eR, xR = compare(outs[0][1][sample], oR)
+    print(f"device front end (params) vs oracle: max|err| L={eL:.3g} R={eR:.3g} bit-exact {xL:.6f} {xR:.6f}")
+    assert max(eL, eR) <= TOL
+
+
 def test_gpu_steady_chunks(oracle):
     """A chunk in which no instance's control changes (every block plays each instance's
     current entry) runs up to TBF_STEADY_CHUNK blocks (default 256) per launch instead of

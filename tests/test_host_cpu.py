@@ -544,3 +544,26 @@ def test_bench_world2_dry_run_gloo():
         assert d["n_gpus"] == n and d["scaling"] == "weak" and d["value"] > 0
     assert two["dry_run"]["shard_rank0"] == [0, 5]
     assert two["dry_run"]["checksum"] == one["dry_run"]["checksum"]
+
+
+def test_drawbar_setting_out_of_range_ignored():
+    """setDrawBar asserts 0 <= setting < 9 (src/tonegen.cpp:2741); the engine ignores a
+    setting outside that (no drawbar change, no gain change), on the host front end and in
+    the device front end's packing (frontParam: setting 15 = ignored)."""
+    lib = T.load_library()
+    _bind_debug(lib)
+    eng = T.Engine(device=-1)
+    tid = eng.template(seed=7)
+    eng.add_instances([tid], [3])
+    for k in S.chord_for(0):
+        eng.note(0, k, 1)
+    before = [_engine_program(lib, eng, 0, False) for _ in range(3)][-1]
+    for bad in (9, 12):
+        eng.set_param(0, S.P_DRAWBAR + 2, bad)
+        eng.set_param(0, S.P_BUS_DRAWBAR + 11, bad)
+    after = [_engine_program(lib, eng, 0, False) for _ in range(3)][-1]
+    assert np.array_equal(before.view(np.uint32), after.view(np.uint32))
+    eng.set_param(0, S.P_DRAWBAR + 2, 3)
+    moved = [_engine_program(lib, eng, 0, False) for _ in range(3)][-1]
+    assert not np.array_equal(before.view(np.uint32), moved.view(np.uint32))
+    eng.close()

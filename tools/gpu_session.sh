@@ -11,7 +11,7 @@
 #   iso     the default bench with each kernel also timed alone (--isolated 1)
 #   bench   the default bench without the CPU leg
 #   ab:V=X  the default bench with environment switch V=X
-#   prof    k_rv_core_lds / k_whirl phase clocks (profiling build variants)
+#   prof    k_rv_core_lds / k_whirl / k_tonegen phase clocks (tools/build_prof.sh variants)
 #   calib   PMC byte counters on known aligned / misaligned streams
 set -u
 TAG=${1:-dev}; shift || true
@@ -59,7 +59,8 @@ for s in $STEPS; do
 	iso) run iso 300 python3 bench.py --isolated 1 --cpu-baseline 0 ;;
 	prof) # phase clocks of k_rv_core_lds and k_whirl (build variants from tools/*_prof_patch.py)
 		run rvl_prof 200 env TBF_LIB=tunebfree_amd/_prof/libtbf_rvlprof.so python3 tools/rvl_prof.py
-		run whirl_prof 200 env TBF_LIB=tunebfree_amd/_prof/libtbf_whprof.so python3 tools/whirl_prof.py ;;
+		run whirl_prof 200 env TBF_LIB=tunebfree_amd/_prof/libtbf_whprof.so python3 tools/whirl_prof.py
+		run tg_prof 200 env TBF_LIB=tunebfree_amd/_prof/libtbf_tgprof.so python3 tools/phase_prof.py --chain 1 ;;
 	calib) # FETCH_SIZE / WRITE_SIZE of known streams: aligned and 64 B misaligned 8-B/lane reads and writes
 		run calib_f 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/calib_f" -o run --output-format csv -- python3 tools/calib_pmc.py 2 0,2,1,3
 		run calib_w 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/calib_w" -o run --output-format csv -- python3 tools/calib_pmc.py 2 0,2,1,3 ;;

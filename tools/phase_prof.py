@@ -2,6 +2,7 @@
 (segment k ends at the k-th sync of its device functions, in source order).
 usage: TBF_LIB=<variant.so> python tools/phase_prof.py [--chain 0|1]"""
 import argparse
+import os
 import sys
 from pathlib import Path
 
@@ -19,7 +20,7 @@ def main():
     import bench
     import tunebfree_amd as T
     wl = bench.Workload("cfg3", 48000.0)
-    B, nb = 4096, 64
+    B, nb = 4096, int(os.environ.get("PROF_BLOCKS", "256"))
     eng = T.Engine(sample_rate=48000.0, device=0, chain=a.chain)
     bench.setup_instances(eng, wl, 0, B)
     outL = torch.empty((B, nb * 128), dtype=torch.float32, device="cuda")

@@ -4,19 +4,17 @@ segment between its syncs (a marker after every __syncthreads / wave_sync of the
 device functions) on lane 0 and writes them, as floats, over the first 32 output samples
 of instances 0..7 (tools/phase_prof.py reads them back).
 
-usage: python tools/phase_prof_patch.py {tonegen|whirl} OUT.hip"""
+usage: python tools/phase_prof_patch.py tonegen OUT.hip  (profile with tools/phase_prof.py --chain 1)"""
 import re
 import sys
 from pathlib import Path
 
 SRC = Path(__file__).resolve().parents[1] / "tunebfree_amd" / "csrc" / "tbf_render.hip"
 CFG = {
-    "tonegen": dict(lds="struct TgLds {", funcs=["__device__ void stage_tonegen (", "__device__ void stage_overdrive ("],
-                    kernel="k_tonegen (const tbf_launch P", end="\tcopy_words (S, &sm.st);\n}"),
-    "whirl": dict(lds="struct WhLds {", funcs=["__device__ void stage_whirl ("],
-                  kernel="k_whirl (const tbf_launch P", end="\t\twr[i] = (&sm.wring[0][0])[i];\n}"),
+    "tonegen": dict(lds="struct TgLds {", funcs=["__device__ void stage_tonegen ("],
+                    kernel="k_tonegen (const tbf_launch P", init_after="\tTgLds&              sm = smv[part];\n",
+                    end="\t\tfor (uint32_t i = lane; i < sizeof (tbf_tg_state) / 4; i += NL)\n\t\t\tdst[i] = src[i];\n\t}\n}"),
 }
-
 
 def main():
     which, out = sys.argv[1], sys.argv[2]
@@ -40,8 +38,7 @@ def main():
         body = re.sub(r"(__syncthreads|wave_sync) \(\);", mark, body)
         s = s[:a] + body + s[b:]
     a = s.index(c["kernel"])
-    b = s.index("__shared__", a)
-    b = s.index("\n", b) + 1
+    b = s.index(c["init_after"], a) + len(c["init_after"])
     s = s[:b] + "\n\tif (threadIdx.x < 32) sm.pp[threadIdx.x] = 0;\n\tif (threadIdx.x == 0) sm.pplast = __builtin_amdgcn_s_memtime ();" + s[b:]
     e = s.index(c["end"], a)
     s = s[:e] + c["end"][:-1] + ("\tif (inst < 8 && threadIdx.x < 32) P.outL[(size_t)inst * P.outStride + P.outOffset + "

@@ -3,6 +3,7 @@ tools/rvl_prof_patch.py: the bench workload (4096 instances, 64 blocks per step)
 with pipelining off (each kernel alone), cycles per (instance, channel) pair and per group.
 usage: TBF_LIB=<variant.so> python tools/rvl_prof.py"""
 import ctypes as C
+import os
 import sys
 from pathlib import Path
 
@@ -20,7 +21,7 @@ def main():
     import bench
     import tunebfree_amd as T
     wl = bench.Workload("cfg3", 48000.0)
-    B, nb, steps = 4096, 64, 3
+    B, nb, steps = 4096, int(os.environ.get("PROF_BLOCKS", "256")), 3
     eng = T.Engine(sample_rate=48000.0, device=0)
     bench.setup_instances(eng, wl, 0, B)
     lib = T.load_library()

@@ -34,17 +34,24 @@ def main():
     body = sub(body, "\tconst int      tid  = threadIdx.x;\n",
                "\tconst int      tid  = threadIdx.x;\n\tunsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};\n"
                "\tunsigned long long t0 = RVP_T (), t1;\n")
-    # the first two barriers (before the loop)
+    # the first two barriers (before the loops)
     body = sub(body, "\t__syncthreads ();\n\tint cntv", "\t__syncthreads ();\n\tt1 = RVP_T (); pt[0] += t1 - t0; t0 = t1;\n\tint cntv")
-    body = sub(body, "\t__syncthreads ();\n#pragma unroll 1\n\tfor (uint32_t g = 0; g < nGrp; g++) {\n",
-               "\t__syncthreads ();\n\tt1 = RVP_T (); pt[1] += t1 - t0; t0 = t1;\n#pragma unroll 1\n"
-               "\tfor (uint32_t g = 0; g < nGrp; g++) {\n\t\tpt[7]++;\n")
-    body = sub(body, "\t\t__syncthreads ();\n\t\t/* ---- write phase ---- */",
-               "\t\tt1 = RVP_T (); pt[2] += t1 - t0; t0 = t1;\n\t\t__syncthreads ();\n"
-               "\t\tt1 = RVP_T (); pt[3] += t1 - t0; t0 = t1;\n\t\t/* ---- write phase ---- */")
-    body = sub(body, "\t\tcw = wrap_slot (cw + TBF_SUB * RVL_G, dlyv);\n\t\t__syncthreads ();\n\t}\n",
-               "\t\tcw = wrap_slot (cw + TBF_SUB * RVL_G, dlyv);\n\t\tt1 = RVP_T (); pt[4] += t1 - t0; t0 = t1;\n"
-               "\t\t__syncthreads ();\n\t\tt1 = RVP_T (); pt[5] += t1 - t0; t0 = t1;\n\t}\n")
+    body = sub(body, "\t__syncthreads ();\n\t/* the workers and the planner run separate loops",
+               "\t__syncthreads ();\n\tt1 = RVP_T (); pt[1] += t1 - t0; t0 = t1;\n\t/* the workers and the planner run separate loops")
+    # the worker loop
+    body = sub(body, "\tif (w < RVL_G) {\n#pragma unroll 1\n\t\tfor (uint32_t g = 0; g < nGrp; g++) {\n",
+               "\tif (w < RVL_G) {\n#pragma unroll 1\n\t\tfor (uint32_t g = 0; g < nGrp; g++) {\n\t\t\tpt[7]++;\n")
+    body = sub(body, "\t\t\t__syncthreads ();\n\t\t\t/* ---- write phase ---- */",
+               "\t\t\tt1 = RVP_T (); pt[2] += t1 - t0; t0 = t1;\n\t\t\t__syncthreads ();\n"
+               "\t\t\tt1 = RVP_T (); pt[3] += t1 - t0; t0 = t1;\n\t\t\t/* ---- write phase ---- */")
+    body = sub(body, "\t\t\tcw = wrap_slot (cw + TBF_SUB * RVL_G, dlyv);\n\t\t\t__syncthreads ();\n\t\t}\n",
+               "\t\t\tcw = wrap_slot (cw + TBF_SUB * RVL_G, dlyv);\n\t\t\tt1 = RVP_T (); pt[4] += t1 - t0; t0 = t1;\n"
+               "\t\t\t__syncthreads ();\n\t\t\tt1 = RVP_T (); pt[5] += t1 - t0; t0 = t1;\n\t\t}\n")
+    # the planner loop: planning as the "read phase", its two barriers
+    body = sub(body, "\t\t\t__syncthreads ();\n\t\t\t__syncthreads ();\n\t\t}\n",
+               "\t\t\tpt[7]++;\n\t\t\tt1 = RVP_T (); pt[2] += t1 - t0; t0 = t1;\n\t\t\t__syncthreads ();\n"
+               "\t\t\tt1 = RVP_T (); pt[3] += t1 - t0; t0 = t1;\n\t\t\t__syncthreads ();\n"
+               "\t\t\tt1 = RVP_T (); pt[5] += t1 - t0; t0 = t1;\n\t\t}\n")
     body += ("\n\tt1 = RVP_T (); pt[6] += t1 - t0;\n"
              "\tif ((threadIdx.x & 63) == 0)\n\t\tfor (int k = 0; k < 8; k++)\n"
              "\t\t\tatomicAdd (&g_rvlprof[threadIdx.x >> 6][k], pt[k]);")

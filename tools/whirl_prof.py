@@ -1,6 +1,7 @@
 """Per-phase wave-clock cycles of k_whirl (profiling variant from tools/whirl_prof_patch.py):
 renders the bench workload with TBF_LIB pointing at the variant and prints each phase's
 cycles per block for instances 0..7.  usage: TBF_LIB=... python tools/whirl_prof.py"""
+import os
 import sys
 from pathlib import Path
 
@@ -18,7 +19,7 @@ def main():
     import bench
     import tunebfree_amd as T
     wl = bench.Workload("cfg3", 48000.0)
-    B, nb = 4096, 64
+    B, nb = 4096, int(os.environ.get("PROF_BLOCKS", "256"))
     eng = T.Engine(sample_rate=48000.0, device=0)
     bench.setup_instances(eng, wl, 0, B)
     outL = torch.empty((B, nb * 128), dtype=torch.float32, device="cuda")

@@ -27,7 +27,7 @@ s = ins_after(s, "\t\t\tsm.x2[i] = st.adx[2][(st.adi[2] + 3 - i) & 7];\n\t\t}\n\
 s = ins_after(s, "\t\t\twh_serial (ip, sm.tmp[lane], st.fz[lane], fa0, fa1, lane == 0 && sb + 1 == TBF_BLK / TBF_SUB);\n\t\t}\n\t\twave_sync ();", mark(3))
 s = ins_after(s, "\t\t\t\tst.drumAngle = okd ? d0 + (double)TBF_SUB * Dd : wrap1 (angBuf[2 * TBF_SUB - 1] + drumIncr);\n\t\t}\n\t\twave_sync ();", mark(4))
 s = ins_after(s, "\t\tconst float xd2v = (float)((0.4 * xd1v) + (0.4 * sm.xd1[n]));\n\t\twave_sync ();", mark(5))
-s = s.replace("\t\t\tbool     okr[4];", mark(6).replace("\n\t\t", "\n\t\t\t") + "\n\t\t\tbool     okr[4];")
+s = s.replace("\t\t\tbool okr[WH_RG];", mark(6).replace("\n\t\t", "\n\t\t\t") + "\n\t\t\tbool okr[WH_RG];")
 s = s.replace("\t\t/* ---- outputs (whirlProc2 outHL/outHR/outDL/outDR + whirlProc3 mix) ---- */",
               mark(7)[1:] + "\n\t\t/* ---- outputs (whirlProc2 outHL/outHR/outDL/outDR + whirlProc3 mix) ---- */")
 s = ins_after(s, "\t\t\tst.outpos = (st.outpos + TBF_SUB) & 2047u;\n\t\twave_sync ();", mark(8))

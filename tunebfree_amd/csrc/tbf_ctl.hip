@@ -444,17 +444,23 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_tgctl (
 		G->gain[lane] = sm.dbg[lane];
 }
 
-/* The device front end of a chunk whose events are all notes (src/tonegen.cpp:3096-3166
- * oscKeyOn / oscKeyOff, and the per-block step of TgControl::stepFront / mixCtl): one wave
- * per instance, lane 0 walking the instance's events in order from its key state at the
- * chunk start.  A key event updates activeKeys and the key counts and queues its messages;
- * a block with messages, or right after one (steadyPending), is stepped: it gets a control
- * delta (pool index nInst + inst * nBlocks + k) whose record k_tgctl turns into the entry
- * (the persistent entry with this block's keyCompTarget and percussion reset) and the
- * program.  Writes the records, the messages and the chunk's index table. */
+/* The device front end of a chunk whose events are notes, drawbar moves and the vibrato
+ * and percussion switches (src/tonegen.cpp:3096-3166 oscKeyOn / oscKeyOff, 2738-2756
+ * setDrawBar, 1678-1765 setPercEnabled / setPercFirst, src/vibrato.cpp routing; the
+ * per-block step of TgControl::stepFront / mixCtl): one wave per instance, lane 0 walking
+ * the instance's events in order from its front state at the chunk start.  A key event
+ * updates activeKeys and the key counts and queues its messages; a drawbar or percussion
+ * event updates the drawbar gains (the changed buses' (bus, gain) pairs go out with the
+ * block's record) and the drawbar-change flag; a switch updates the routing word.  A block
+ * with inputs (messages, a drawbar change or a routing change), or right after one
+ * (steadyPending), is stepped: it gets a control delta (pool index nInst + inst * nBlocks
+ * + k) whose record k_tgctl turns into the entry (the persistent entry with this block's
+ * keyCompTarget, percussion reset and routing) and the program.  Writes the records, the
+ * messages, the gain pairs and the chunk's index table. */
 __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_front (const tbf_launch P)
 {
 	__shared__ uint32_t keys[12];
+	__shared__ float    gl[27]; /* drawBarGain of the buses changed since the last step */
 	const int             lane = threadIdx.x;
 	const uint32_t        inst = blockIdx.x;
 	const uint32_t        n = P.nInst, nb = P.nBlocks;
@@ -467,18 +473,56 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_front (
 	uint32_t*      ctlIdx = (uint32_t*)P.ctlIdx;
 	uint16_t*      msgs   = (uint16_t*)P.msgs;
 	tbf_tgc_rec*   rec    = (tbf_tgc_rec*)P.rec;
+	float*         gains  = (float*)P.gains;
 	const float*   kct    = P.keyComp + (size_t)P.cst[inst].tpl * 128;
-	const uint32_t routing = P.ctl[inst].routing;
 	int            kdc = F.keyDown, ukc = F.upperDown;
 	bool           pending = F.pending != 0;
+	uint32_t       r = F.routing, oldR = F.routing, psb = F.percSendBus;
+	int            pe = F.percEnabled, restore = F.percTrigRestore;
+	const int      ptb = F.percTriggerBus;
+	uint32_t       gm = 0, dbc = 0, go = F.gainOff;
 	uint32_t       e = P.fevOff[inst], eEnd = P.fevOff[inst + 1];
 	uint32_t       mo = 2 * e; /* the instance's message slots: at most two per event */
 	uint32_t       idx = inst, k = 0;
+	/* drawBarLevel[bus][s] = (float)((float)s / 8.0) on every bus (TgControl::init) */
+	auto level = [] (uint32_t s) { return (float)((double)(float)s / 8.0); };
 	for (uint32_t b = 0; b < nb; b++) {
 		const uint32_t m0 = mo;
 		for (; e < eEnd && (P.fev[e] >> 16) == b; e++) {
-			const uint32_t v = P.fev[e], key = v & 0x0fffu;
-			const bool     on = (v >> 12) & 1u;
+			const uint32_t v = P.fev[e];
+			if (v & TBF_FEV_PARAM) {
+				const uint32_t op = (v >> 12) & 7u, bus = v & 31u, set = (v >> 5) & 15u;
+				const bool     fl = (v >> 9) & 1u;
+				if (op == TBF_FEV_DRAWBAR) {
+					if (set > 8)
+						continue; /* setDrawBar ignores settings > 8 */
+					dbc = 1;
+					if ((int)bus == ptb) {
+						restore = (int)set;
+						if (pe)
+							continue;
+					}
+					gl[bus] = level (set);
+					gm |= 1u << bus;
+				} else if (op == TBF_FEV_VIB_UPPER) {
+					r = fl ? (r | 0x02u) : (r & ~0x02u);
+				} else if (op == TBF_FEV_VIB_LOWER) {
+					r = fl ? (r | 0x01u) : (r & ~0x01u);
+				} else if (op == TBF_FEV_PERC) {
+					r = fl ? (r | 0x0Cu) : (r & ~0x0Cu);
+					if (-1 < ptb) {
+						gl[ptb] = fl ? 0.0f : level ((uint32_t)restore);
+						gm |= 1u << ptb;
+						dbc = 1;
+					}
+					pe = fl;
+				} else if (op == TBF_FEV_PERC_FIRST) {
+					psb = fl ? F.percSendBusA : F.percSendBusB;
+				}
+				continue;
+			}
+			const uint32_t key = v & 0x0fffu;
+			const bool     on  = (v >> 12) & 1u;
 			if (key >= 384) /* the host packs keys outside [0, MAX_KEYS) as 0x0fff: ignored (3098) */
 				continue;
 			const uint32_t w = key >> 5, bit = 1u << (key & 31);
@@ -497,22 +541,31 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_front (
 				msgs[mo++] = (uint16_t)(0x1000u | key);
 			}
 		}
-		const uint32_t nm = mo - m0;
-		if (nm > 0 || pending) {
-			const uint32_t d = inst * nb + k++;
+		const uint32_t nm  = mo - m0;
+		const bool     rcp = r != oldR;
+		if (nm > 0 || dbc || rcp || pending) {
+			const uint32_t d  = inst * nb + k++;
+			const uint32_t ng = (uint32_t)__builtin_popcount (gm);
 			tbf_tgc_rec    R;
 			R.msgOff        = m0;
 			R.nMsg          = nm;
-			R.gainOff       = 0;
+			R.gainOff       = ng ? go : 0;
 			R.full          = 0;
 			R.keyCompTarget = kct[kdc < 0 ? 0 : (kdc > 127 ? 127 : kdc)];
-			R.flags         = (uint8_t)(0x80u | (ukc == 0 ? 8u : 0u));
-			R.oldRouting    = (uint8_t)routing;
-			R.percSendBus   = (uint8_t)F.percSendBus;
-			R.pad           = 0;
-			rec[d]          = R;
-			idx             = n + d;
-			pending         = nm > 0;
+			R.flags         = (uint8_t)(0x80u | dbc | (rcp ? 2u : 0u) | (ng ? 4u : 0u) | (ukc == 0 ? 8u : 0u));
+			R.oldRouting    = (uint8_t)r;
+			R.percSendBus   = (uint8_t)psb;
+			R.pad           = (uint8_t)ng;
+			for (uint32_t m = gm; m; m &= m - 1) { /* the changed buses in bus order */
+				const uint32_t bus = (uint32_t)__builtin_ctz (m);
+				gains[go++]        = __uint_as_float (bus);
+				gains[go++]        = gl[bus];
+			}
+			rec[d]  = R;
+			idx     = n + d;
+			pending = nm > 0 || dbc || rcp;
+			oldR    = r;
+			gm = dbc = 0;
 		}
 		ctlIdx[(size_t)b * n + inst] = idx;
 	}

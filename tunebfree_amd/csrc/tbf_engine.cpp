@@ -1499,6 +1499,32 @@ static bool frontClean (const Instance& in)
 	       t.oldRouting == t.newRouting && t.gainsSent && t.gainMask == 0;
 }
 
+/* a parameter event the device front end steps (drawbars, the vibrato and percussion
+ * switches: they change only what a control record carries), as a TBF_FEV_* word without
+ * the block; 0 for any other */
+static uint32_t frontParam (const tbf_event& E)
+{
+	const int32_t idx = E.id;
+	const float   v   = (float)E.value;
+	int           bus = -1;
+	if (idx >= TBF_P_DRAWBAR_MIN && idx <= TBF_P_DRAWBAR_MAX)
+		bus = idx;
+	else if (idx >= TBF_P_BUS_DRAWBAR_BASE && idx < TBF_P_BUS_DRAWBAR_BASE + 27)
+		bus = idx - TBF_P_BUS_DRAWBAR_BASE;
+	if (bus >= 0) {
+		const unsigned st = (unsigned)rint (v); /* as tbf_set_param hands it to setDrawBar */
+		return TBF_FEV_PARAM | (TBF_FEV_DRAWBAR << 12) | ((st > 8 ? 15u : st) << 5) | (uint32_t)bus;
+	}
+	const uint32_t fl = (int)rint (v) != 0 ? 1u : 0u;
+	switch (idx) {
+		case TBF_P_VIBRATO: return TBF_FEV_PARAM | (TBF_FEV_VIB_UPPER << 12) | (fl << 9);
+		case TBF_P_VIBRATO_LOWER: return TBF_FEV_PARAM | (TBF_FEV_VIB_LOWER << 12) | (fl << 9);
+		case TBF_P_PERCUSSION: return TBF_FEV_PARAM | (TBF_FEV_PERC << 12) | (fl << 9);
+		case TBF_P_PERCUSSION_HARMONIC: return TBF_FEV_PARAM | (TBF_FEV_PERC_FIRST << 12) | (fl << 9);
+		default: return 0;
+	}
+}
+
 static bool frontEligible (tbf_engine* e, const tbf_event* ev, uint32_t evBeg, uint32_t evEnd)
 {
 	/* per instance once (an event list visits every instance's host state many times) */
@@ -1522,7 +1548,7 @@ static bool frontEligible (tbf_engine* e, const tbf_event* ev, uint32_t evBeg, u
 	parallelFor (T, [&] (uint32_t t) {
 		const uint32_t k0 = evBeg + std::min (nev, t * seg), k1 = evBeg + std::min (nev, (t + 1) * seg);
 		for (uint32_t k = k0; k < k1; k++)
-			if (ev[k].kind != TBF_EV_NOTE || !cl[ev[k].inst]) {
+			if ((ev[k].kind != TBF_EV_NOTE && !(ev[k].kind == TBF_EV_PARAM && frontParam (ev[k]))) || !cl[ev[k].inst]) {
 				ok[t] = 0;
 				return;
 			}
@@ -1545,6 +1571,7 @@ static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0
 		o.act.clear ();
 		o.ctlInst.clear ();
 		o.evs.clear ();
+		o.gainLocal = 0;
 	}
 	{ /* the events by instance range, in order (a parallel counting partition) */
 		const uint32_t        nev = evEnd - evBeg, seg = (nev + T - 1) / T;
@@ -1604,38 +1631,103 @@ static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0
 			for (int k = 0; k < 384; k++)
 				if (tg.activeKeys[k])
 					F.keys[k >> 5] |= 1u << (k & 31);
-			F.keyDown     = tg.keyDownCount;
-			F.upperDown   = (int32_t)tg.upperKeyCount;
-			F.pending     = tg.steadyPending ? 1u : 0u;
-			F.percSendBus = tg.percSendBus;
-			e->hFevOff[i] = wbase[t] + eo[i - i0];
-			uint32_t msgs = 0, last = 0;
+			F.keyDown         = tg.keyDownCount;
+			F.upperDown       = (int32_t)tg.upperKeyCount;
+			F.pending         = tg.steadyPending ? 1u : 0u;
+			F.percSendBus     = tg.percSendBus;
+			F.routing         = tg.oldRouting;
+			F.percEnabled     = tg.percEnabled ? 1 : 0;
+			F.percTrigRestore = tg.percTrigRestore;
+			F.percTriggerBus  = tg.percTriggerBus;
+			F.percSendBusA    = tg.percSendBusA;
+			F.percSendBusB    = tg.percSendBusB;
+			F.gainOff         = o.gainLocal; /* + the thread's base, below */
+			e->hFevOff[i]     = wbase[t] + eo[i - i0];
+			/* the host's front state takes the events too (it stays the truth for any later
+			 * host-stepped chunk): the same setters, block by block, and the same steps as
+			 * the device -- a block with inputs steps, and so does the one after it */
+			bool     stepped = F.pending != 0, pend = F.pending != 0;
+			uint32_t oldR = tg.oldRouting, ng = 0, msgsB = 0;
+			int      curB = -1;
+			auto     closeBlock = [&] () {
+                const bool rcp = tg.newRouting != oldR, in = msgsB > 0 || tg.drawBarChange || rcp;
+                ng += (uint32_t)__builtin_popcount (tg.gainMask);
+                stepped = stepped || in;
+                pend    = in;
+                oldR    = tg.newRouting;
+                tg.drawBarChange = 0;
+                tg.gainMask      = 0;
+                msgsB            = 0;
+			};
 			for (uint32_t j = eo[i - i0]; j < eo[i - i0 + 1]; j++) {
 				const tbf_event& E   = ev[es[j]];
 				const uint32_t   blk = E.block - b0;
-				const bool       on  = E.value != 0.0;
-				const bool       ok  = E.id >= 0 && E.id < 384; /* oscKeyOn/Off ignore keys >= MAX_KEYS */
+				if ((int)blk != curB) {
+					if (curB >= 0)
+						closeBlock ();
+					if (curB >= 0 ? blk > (uint32_t)curB + 1 : blk > 0)
+						pend = false; /* blocks without events between: the pending step is done */
+					curB = (int)blk;
+				}
+				if (E.kind == TBF_EV_PARAM) {
+					const uint32_t w = frontParam (E);
+					e->hFev[wbase[t] + j] = w | (blk << 16);
+					const float v = (float)E.value;
+					if (E.id >= 0 && E.id < 64)
+						in.params[E.id] = v;
+					const uint32_t op = (w >> 12) & 7u;
+					if (op == TBF_FEV_DRAWBAR)
+						tg.setDrawBar ((int)(w & 31u), (unsigned)rint (v));
+					else if (op == TBF_FEV_VIB_UPPER)
+						tg.setVibratoUpper ((int)rint (v));
+					else if (op == TBF_FEV_VIB_LOWER)
+						tg.setVibratoLower ((int)rint (v));
+					else if (op == TBF_FEV_PERC)
+						tg.setPercEnabled ((int)rint (v));
+					else
+						tg.setPercFirst ((int)rint (v));
+					continue;
+				}
+				const bool on = E.value != 0.0;
+				const bool ok = E.id >= 0 && E.id < 384; /* oscKeyOn/Off ignore keys >= MAX_KEYS */
 				e->hFev[wbase[t] + j] = (ok ? (uint32_t)E.id : 0x0fffu) | (on ? 1u << 12 : 0u) | (blk << 16);
-				const int m = ok ? tg.noteCount (E.id, on) : 0;
-				msgs += (uint32_t)m;
-				if (blk == want - 1)
-					last += (uint32_t)m;
+				msgsB += ok ? (uint32_t)tg.noteCount (E.id, on) : 0u;
 			}
-			if (msgs > 0 || F.pending) { /* stepped blocks: control deltas */
+			if (curB >= 0) {
+				closeBlock ();
+				if ((uint32_t)curB + 1 < want)
+					pend = false;
+			} else
+				pend = false; /* no events: block 0 takes the pending step */
+			o.gainLocal += 2 * ng;
+			tg.oldRouting = tg.newRouting;
+			if (stepped) { /* stepped blocks: control deltas */
 				e->stepped[i] = 1;
 				o.ctlInst.push_back (i);
 				e->chg[i] = 1;
 				const int kd = tg.keyDownCount;
 				e->hCtl[i].keyCompTarget  = tg.tpl->keyCompTable[kd < 0 ? 0 : (kd > 127 ? 127 : kd)];
 				e->hCtl[i].resetPercAtEnd = tg.upperKeyCount == 0;
+				e->hCtl[i].routing        = tg.oldRouting;
 			}
-			tg.steadyPending = last > 0;
+			const bool last = pend;
+			tg.steadyPending = last;
 			e->inAct[i]      = tg.steadyPending ? 1 : 0;
 			if (e->inAct[i])
 				o.act.push_back (i);
 		}
 	});
 	e->hFevOff[n] = wbase[T];
+	{ /* the gain-pair slots: each range's base */
+		std::vector<uint32_t> gb (T + 1, 0);
+		for (unsigned t = 0; t < T; t++)
+			gb[t + 1] = gb[t] + out[t].gainLocal;
+		e->frontGain = gb[T];
+		parallelFor (T, [&] (uint32_t t) {
+			for (uint32_t i = t * per; i < std::min (n, (t + 1) * per); i++)
+				e->hFront[i].gainOff += gb[t];
+		});
+	}
 	e->actList.clear ();
 	for (unsigned t = 0; t < T; t++) {
 		e->actList.insert (e->actList.end (), out[t].act.begin (), out[t].act.end ());
@@ -1919,7 +2011,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 				progEv = progEv || pe[t];
 			}
 		}
-		/* a chunk of note events only: the device front end */
+		/* a chunk of note, drawbar and switch events only (frontParam): the device front end */
 		bool dfront = false;
 		if (e->devCtl && dpipe && e->frontOn && !progEv && evEnd - evi >= 1024 && frontEligible (e, ev, evi, evEnd)) {
 			if ((rc = stepChunkFront (e, n, want, b0, ev, evi, evEnd, delta)))
@@ -2067,9 +2159,10 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			DevBuf<float>&       dgn  = rp ? e->dgainB : e->dgain;
 			DevBuf<uint32_t>&    dci  = rp ? e->dctlInstB : e->dctlInst;
 			DevBuf<tbf_seg_ctl>& dfl  = rp ? e->dfullB : e->dfull;
-			const size_t nRec = dfront ? (size_t)n * len : e->hRec.size ();
-			const size_t nMsg = dfront ? 2 * (size_t)e->hFevOff[n] : e->hMsg.size ();
-			if (drec.cap < nRec || dmsg.cap < nMsg || dci.cap < e->hDInst.size () || dgn.cap < e->hGain.size () ||
+			const size_t nRec  = dfront ? (size_t)n * len : e->hRec.size ();
+			const size_t nMsg  = dfront ? 2 * (size_t)e->hFevOff[n] : e->hMsg.size ();
+			const size_t nGain = dfront ? (size_t)e->frontGain : e->hGain.size ();
+			if (drec.cap < nRec || dmsg.cap < nMsg || dci.cap < e->hDInst.size () || dgn.cap < nGain ||
 			    dfl.cap < e->hFull.size ())
 			{
 				if (getenv ("TBF_DEBUG_HOST_PHASES"))
@@ -2077,7 +2170,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 				HIPCHK (hipDeviceSynchronize ()); /* growing: nothing may still read the old buffers */
 			}
 			if (drec.ensure (std::max<size_t> (nRec, 1)) || dmsg.ensure (std::max<size_t> (nMsg, 1)) ||
-			    dgn.ensure (std::max<size_t> (e->hGain.size (), 27)) ||
+			    dgn.ensure (std::max<size_t> (nGain, 27)) ||
 			    dci.ensure (e->hDInst.size ()) || dfl.ensure (std::max<size_t> (e->hFull.size (), 1)))
 				return fail (-12, "out of device memory (control records)");
 			if (dfront) {
@@ -2104,6 +2197,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 				P.keyComp = e->dkeyComp.p;
 				P.rec     = drec.p;
 				P.msgs    = dmsg.p;
+				P.gains   = dgn.p;
 				if ((rc = tbf_launch_front (&P, us)))
 					return fail (rc, std::string ("k_front launch failed: ") + hipGetErrorString (hipGetLastError ()));
 			}

@@ -223,6 +223,7 @@ struct tbf_engine {
 	/* device front end (k_front) for note-only chunks: per instance key state at the chunk
 	 * start, the instances' note events by instance, their offsets; by chunk parity */
 	bool                                    frontOn = true; /* TBF_DEVICE_FRONT=0 disables */
+	uint32_t                                frontGain = 0;  /* device front end: the chunk's gain-pair floats */
 	PinnedVec<tbf_front_state>              hFront, hFrontB;
 	PinnedVec<uint32_t>                     hFev, hFevB, hFevOff, hFevOffB;
 	DevBuf<tbf_front_state>                 dfront, dfrontB;
@@ -257,6 +258,7 @@ struct tbf_engine {
 		std::vector<uint32_t> act, ctlInst, evs, dInst, eoff, esort, efill;
 		std::vector<tbf_seg_ctl> fulls;
 		uint32_t              nd = 0;
+		uint32_t              gainLocal = 0; /* device front end: the range's gain-pair floats */
 		int                   rc = 0;
 		std::string           err; /* the worker's tbf_last_error text (it is thread-local) */
 	};

@@ -174,10 +174,12 @@ __device__ __forceinline__ void wave_sync ()
 }
 
 /* Whole-wave lane shifts by DPP (wave_shr:1 / wave_shl:1, GFX9 DPP controls 0x138 /
- * 0x130): lane i receives lane i-1 (shr) or i+1 (shl); the lane with no source keeps
- * its own value (callers mask it).  VALU-only, unlike __shfl_up/down (ds_bpermute). */
-__device__ __forceinline__ int lane_shr1 (int v) { return __builtin_amdgcn_update_dpp (v, v, 0x138, 0xF, 0xF, false); }
-__device__ __forceinline__ int lane_shl1 (int v) { return __builtin_amdgcn_update_dpp (v, v, 0x130, 0xF, 0xF, false); }
+ * 0x130): lane i receives lane i-1 (shr) or i+1 (shl); the lane with no source gets 0
+ * (bound_ctrl; callers mask it), so the shift is one v_mov_b32_dpp into a fresh register
+ * (keeping the old value needed a copy first).  VALU-only, unlike __shfl_up/down
+ * (ds_bpermute). */
+__device__ __forceinline__ int lane_shr1 (int v) { return __builtin_amdgcn_mov_dpp (v, 0x138, 0xF, 0xF, true); }
+__device__ __forceinline__ int lane_shl1 (int v) { return __builtin_amdgcn_mov_dpp (v, 0x130, 0xF, 0xF, true); }
 __device__ __forceinline__ float lane_shr1 (float v) { return __int_as_float (lane_shr1 (__float_as_int (v))); }
 __device__ __forceinline__ float lane_shl1 (float v) { return __int_as_float (lane_shl1 (__float_as_int (v))); }
 __device__ __forceinline__ double lane_shr1 (double v)
@@ -1446,19 +1448,29 @@ __device__ __forceinline__ void rvl_pair (const tbf_launch& P, const tbf_inst_co
 						}
 					}
 				}
-				double I[8];
+				/* every line's tap address first, then all eight tap-pair reads in flight
+				 * together, then the interpolations (a line's read was waited for before the
+				 * next line's address was formed) */
+				double I[8], fr[8], r0[8], r1[8];
+				int    wk[8];
 #pragma unroll
 				for (int l = 0; l < 8; l++) {
-					const double  off = (sn[l] + 1.0) * K.vibDepth;
-					const int     d   = RVL_DLY[l];
-					const double* rg  = sm.ring + RVL_LOFS[l];
-					const int     cn  = wrap_slot (rl (cw, l) + n + 1, d);
-					const int     wk  = (int)(cn + off); /* <= d + 5: the mirror covers wk + 1 */
-					const double  fr  = off - floor (off);
-					const double  r0 = rg[wk], r1 = rg[wk + 1];
-					double        x  = (r0 * (1 - fr));
-					x += (r1 * fr);
-					I[l] = (oneMB * x) + (r0 * K.blend);
+					const double off = (sn[l] + 1.0) * K.vibDepth;
+					const int    cn  = wrap_slot (rl (cw, l) + n + 1, RVL_DLY[l]);
+					wk[l]            = (int)(cn + off); /* <= d + 5: the mirror covers wk + 1 */
+					fr[l]            = off - floor (off);
+				}
+#pragma unroll
+				for (int l = 0; l < 8; l++) {
+					const double* rg = sm.ring + RVL_LOFS[l];
+					r0[l]            = rg[wk[l]];
+					r1[l]            = rg[wk[l] + 1];
+				}
+#pragma unroll
+				for (int l = 0; l < 8; l++) {
+					double x = (r0[l] * (1 - fr[l]));
+					x += (r1[l] * fr[l]);
+					I[l] = (oneMB * x) + (r0[l] * K.blend);
 				}
 				I[0]  = (I[0] * K.oneMinusAbsCm) + (I[4] * K.crossmod);
 				I[4]  = (I[4] * K.oneMinusAbsCm) + (I[0] * K.crossmod);
@@ -2161,27 +2173,26 @@ __device__ __forceinline__ MotionOwn motion_own (int U, float a, float b, int la
 	return m;
 }
 
-/* slot t: b of the group at t-1 (<= 2 samples, in order), then a of the group at t */
+/* slot t: b of the group at t-1 (<= 2 samples, in order), then a of the group at t.  A
+ * skipped add keeps v (v + 0 is not v for v = -0), so each optional add is a select of the
+ * sum, not a branch: the passes stay branch-free */
 __device__ __forceinline__ float motion_sum_t (const MotionOwn& m, float v)
 {
-	if (m.lead) {
-		if (m.lead2)
-			v += m.bp2;
-		v += m.bp1;
-	}
+	float t = v + m.bp2;
+	v       = (m.lead && m.lead2) ? t : v;
+	t       = v + m.bp1;
+	v       = m.lead ? t : v;
 	v += m.a;
-	if (m.pair)
-		v += m.an;
-	return v;
+	t = v + m.an;
+	return m.pair ? t : v;
 }
 
 /* slot t + 1 when no group sits there: b of this group */
 __device__ __forceinline__ float motion_sum_t1 (const MotionOwn& m, float w)
 {
 	w += m.b;
-	if (m.pair)
-		w += m.bn;
-	return w;
+	const float t = w + m.bn;
+	return m.pair ? t : w;
 }
 
 template <int W>

@@ -58,14 +58,33 @@ typedef struct tbf_tgc_rec {
 	uint8_t  pad;            /* flags & 4: the number of gain pairs */
 } tbf_tgc_rec;
 
-/* device front end (note-only chunks, k_front): an instance's key state at the chunk start */
+/* device front end (chunks of note, drawbar, vibrato-switch and percussion-switch events,
+ * k_front): an instance's tone-generator front state at the chunk start */
 typedef struct tbf_front_state {
-	uint32_t keys[12];    /* activeKeys, 384 bits */
-	int32_t  keyDown;     /* keyDownCount */
-	int32_t  upperDown;   /* upperKeyCount */
-	uint32_t pending;     /* steadyPending: the block before had inputs */
+	uint32_t keys[12];       /* activeKeys, 384 bits */
+	int32_t  keyDown;        /* keyDownCount */
+	int32_t  upperDown;      /* upperKeyCount */
+	uint32_t pending;        /* steadyPending: the block before had inputs */
 	uint32_t percSendBus;
+	uint32_t routing;        /* the routing word (oldRouting == newRouting at the chunk start) */
+	int32_t  percEnabled;
+	int32_t  percTrigRestore;
+	int32_t  percTriggerBus; /* < 0: none */
+	uint32_t percSendBusA, percSendBusB;
+	uint32_t gainOff;        /* the instance's slots for (bus, gain) pairs in gains (floats) */
 } tbf_front_state;
+
+/* a front-end event, 4 bytes: block << 16 | low 16 bits
+ *   note   key (12 bits; 0x0fff: outside [0, 384), ignored) | on << 12
+ *   param  0x8000 | op << 12 | flag << 9 | setting << 5 | bus, op:
+ *          TBF_FEV_DRAWBAR (setting 0..8, 15: out of range, ignored), TBF_FEV_VIB_UPPER /
+ *          TBF_FEV_VIB_LOWER / TBF_FEV_PERC (flag: on), TBF_FEV_PERC_FIRST (flag: first) */
+#define TBF_FEV_PARAM 0x8000u
+#define TBF_FEV_DRAWBAR 0u
+#define TBF_FEV_VIB_UPPER 1u
+#define TBF_FEV_VIB_LOWER 2u
+#define TBF_FEV_PERC 3u
+#define TBF_FEV_PERC_FIRST 4u
 
 /* one keyContrib element on the device (Contrib): a key's list is sorted by wheel, then
  * bus (compilePlayMatrix's insertion sort, src/tonegen.cpp:1183-1201) */
@@ -282,7 +301,7 @@ typedef struct tbf_launch {
 	const tbf_seg_ctl*    fulls;     /* the chunk's full control entries (tbf_tgc_rec.full) */
 	const tbf_front_state* front;    /* k_front: [inst] key state at the chunk start ... */
 	const uint32_t*       fevOff;    /* ... [inst + 1] offsets into fev ... */
-	const uint32_t*       fev;       /* ... an instance's note events in order: key | on << 12 | block << 16 */
+	const uint32_t*       fev;       /* ... an instance's events in order (TBF_FEV_*) */
 	const float*          keyComp;   /* [tpl][128] keyCompTable */
 	uint32_t              progBase;  /* program slot of delta d (pool index nInst + d): progBase + d * TBF_PROG_SLOT */
 } tbf_launch;

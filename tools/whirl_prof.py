@@ -9,9 +9,8 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "tests"))
 
-NAMES = {0: "stage input", 9: "block start (speed)", 1: "ring read/clear", 4: "angles", 5: "FILTER_C",
-         6: "motions (tables)", 7: "ring adds", 8: "outputs + carry", 11: "block end", 13: "output pipeline",
-         12: "barrier wait"}
+NAMES = {10: "block start", 9: "speed (lane 0)", 1: "ring read + staging", 3: "serial filters", 4: "filter outputs + angles",
+         5: "FILTER_C", 6: "motions (tables)", 7: "ring adds", 8: "outputs + carry"}
 
 
 def main():
@@ -33,7 +32,6 @@ def main():
     for k, nm in NAMES.items():
         print(f"{nm:26s} " + " ".join(f"{v / nb:8.0f}" for v in prof[:, k]) + f"   ({np.mean(prof[:, k] / tot) * 100:4.1f} %)")
     print(f"{'total per block':26s} " + " ".join(f"{v / nb:8.0f}" for v in tot))
-    print(f"filter wave (instance 0's slots): work {prof[0, 14] / nb:.0f}, barrier waits {prof[0, 15] / nb:.0f} per block")
 
 
 if __name__ == "__main__":

@@ -73,33 +73,6 @@ TBF_HD bool phase_run_cached (double v0, double d, int m, double& D, double& cD,
 	return true;
 }
 
-/* phase_run_cached for a step d that may change between runs (the rotor speeds ramp):
- * c = {d, D, lo, hi} of the last analysed run, reused while d is the same and the run stays
- * in that binade.  Same result as phase_run (v0, d, m, D). */
-TBF_HD bool phase_run_keyed (double v0, double d, int m, double& D, double (&c)[4])
-{
-	if (c[1] > 0.0 && d == c[0]) {
-		const double w = v0 + (double)m * c[1], a0 = fabs (v0), a1 = fabs (w);
-		if (a0 >= c[2] && a0 <= c[3] && a1 >= c[2] && a1 <= c[3] && ((v0 < 0) == (w < 0))) {
-			D = c[1];
-			return true;
-		}
-	}
-	c[1] = 0.0;
-	if (!phase_run (v0, d, m, D))
-		return false;
-	if (D > 0.0) {
-		int e;
-		frexp (v0, &e);
-		const double u = ldexp (1.0, e - 53);
-		c[0]           = d;
-		c[1]           = D;
-		c[2]           = ldexp (1.0, e - 1) + u;
-		c[3]           = ldexp (1.0, e) - u;
-	}
-	return true;
-}
-
 /* fmod (x, 1.0) for the rotor angle update (src/whirl.cpp:1428-1429): for x in [0, 2)
  * fmod is x or x - 1, the latter exact by Sterbenz; anything else takes libm. */
 TBF_HD double wrap1 (double x)

@@ -37,11 +37,14 @@
 #define TG_SPLIT_MAX 8 /* k_tonegen block ranges (waves) per instance */
 #define TG_PCAP 128    /* a delta chunk's program entries staged in LDS per block (longer: read from HBM) */
 #define RV_WAVES 3
-/* k_whirl instances (waves) per workgroup, by ring length: the workgroup's LDS (a W-float
- * ring per rotor channel and instance) fills most of a CU */
-constexpr int WH_NI (int W) { return W <= 512 ? 10 : (W <= 1024 ? 6 : 4); }
+/* k_whirl: 4 waves per SIMD (128 VGPRs, 9.8 KB of LDS: 16 instances per CU, so 4096 run
+ * at once on 256 CUs), motions and ring adds in 2 groups of 2 rings (4 rings per group
+ * need 168 VGPRs) */
+#ifndef WH_WAVES
+#define WH_WAVES 4
+#endif
 #ifndef WH_RG
-#define WH_RG 4 /* k_whirl rings per motion group (4 or 2) */
+#define WH_RG 2 /* k_whirl rings per motion group (4 or 2) */
 #endif
 /* wave priority raised (s_setprio 1) while a wave runs a serial chain, so the SIMD issues
  * the chain's dependent instructions ahead of other waves' lane-parallel work */
@@ -79,27 +82,20 @@ struct TgLds {
 };
 
 
-/* k_whirl: WH_NI instance waves and one filter wave per workgroup (see k_whirl) */
-template <int W>
-struct WhInst {
-	tbf_wh_state st;
-	float        wring[4][W];
-	float        xr[4][TBF_SUB];    /* input + 1e-14 of sub-block m in row m & 3 (staged 3 sub-blocks ahead) */
-	float        xf[TBF_SUB + 4];   /* horn B output: [0..3] the last 4 of the previous sub-block */
-	float        x1[TBF_SUB + 4];
-	float        x2[TBF_SUB + 4];
-	float        xd1[TBF_SUB + 1];
-	float        hb[2][TBF_SUB];    /* horn B output of sub-block m, row m & 1 (filter wave ->) */
-	float        dr[2][2][TBF_SUB]; /* drum ring outputs L / R of sub-block m, row m & 1 (-> filter wave) */
-	float        ds[2][2][TBF_SUB]; /* ... and their shelf outputs (filter wave ->) */
-	alignas (8) double ang[2][TBF_SUB]; /* the serial rotor-angle fallback's rows */
-	int32_t      bf[NL];            /* the launch's per-block control, entry b = block b: bypass | whSet << 1 */
-	int          brake;
-};
 template <int W>
 struct WhLds {
-	WhInst<W> in[WH_NI (W)];
-	float     ha[2][WH_NI (W)][TBF_SUB]; /* horn A output of sub-block m, row m & 1 (filter wave only) */
+	tbf_wh_state st;
+	float        wring[4][W];
+	float        xf[TBF_SUB + 4];
+	float        x1[TBF_SUB + 4];
+	float        x2[TBF_SUB + 4];
+	/* horn A rows by parity ap: ab[ap] takes the next sub-block's input and horn A filters
+	 * it in place (A runs one sub-block ahead), ab[ap ^ 1] holds A's output of this
+	 * sub-block, horn B's input */
+	float        ab[2][TBF_SUB];
+	int          brake;
+	int          aReady; /* ab[ap ^ 1] holds this sub-block's horn A output */
+	int          ap;
 };
 
 /* the control entry of instance `inst` for block `blk` of the chunk: events land at
@@ -185,6 +181,14 @@ __device__ __forceinline__ int lane_shr1 (int v) { return __builtin_amdgcn_mov_d
 __device__ __forceinline__ int lane_shl1 (int v) { return __builtin_amdgcn_mov_dpp (v, 0x130, 0xF, 0xF, true); }
 __device__ __forceinline__ float lane_shr1 (float v) { return __int_as_float (lane_shr1 (__float_as_int (v))); }
 __device__ __forceinline__ float lane_shl1 (float v) { return __int_as_float (lane_shl1 (__float_as_int (v))); }
+/* lane n receives lane n-1's v, lane 0 receives first: one DPP move with the old value
+ * (bound_ctrl off), so there is no select on the lane index -- a select lets the compiler
+ * put the DPP move under a branch that disables lane 0, and a DPP move reading a disabled
+ * lane gets 0 */
+__device__ __forceinline__ float lane_shr1_or (float v, float first)
+{
+	return __int_as_float (__builtin_amdgcn_update_dpp (__float_as_int (first), __float_as_int (v), 0x138, 0xF, 0xF, false));
+}
 __device__ __forceinline__ double lane_shr1 (double v)
 {
 	const unsigned long long u = __double_as_longlong (v);
@@ -2268,507 +2272,514 @@ __device__ __forceinline__ void motion_pass (float (*ring)[W], const int (&mu)[R
 	}
 }
 
-/* The filter wave of a k_whirl workgroup: the four DF2 filters of every instance of the
- * workgroup (EQ_IIR, src/whirl.cpp:1479-1485: horn A and horn B on the input, drum shelves
- * L and R on the drum rings' outputs, src/whirl.cpp:1603-1620), one filter chain per lane:
- * lane r WH_NI + j runs filter r of instance j.  Each is a serial recurrence of 64 steps per
- * sub-block; run by the instance waves, every step cost a whole wave instruction for one
- * lane's work.  At interval k (one barrier per interval) horn A filters sub-block k + 2,
- * horn B sub-block k + 1 (A's output of the interval before) and the shelves sub-block
- * k - 1 (the ring outputs the instance waves read at k - 1); the instance waves use horn
- * B's output of sub-block k at interval k and the shelves' at k + 1.  A lane takes a new
- * coefficient set (tbf_seg_ctl.whSet) at the first sub-block of the block that carries it,
- * and applies the block-end NaN scrub (src/whirl.cpp:1622-1627) after the last sub-block
- * of every block that is not bypassed; bypassed blocks leave its state alone. */
-template <int W>
-__device__ void whirl_filters (const tbf_launch& P, const tbf_inst_const* __restrict__ cst, WhLds<W>& sm, uint32_t inst0,
-                               int nj)
+/* one DF2 state recurrence (EQ_IIR, src/whirl.cpp:1479-1485) over a sub-block in one lane:
+ * temp[i] = (x[i] - a1 temp[i-1]) - a2 temp[i-2], written over x[i].  Element i of the row
+ * is r[i], or with WRAP r[(base + i) & m] (a ring window that wraps); read in groups of
+ * eight before their temps are written.  The outputs y = (temp b0 + b1 temp[-1]) + b2
+ * temp[-2] are lane-parallel afterwards (wh_outputs).  scrub applies the block-end NaN
+ * scrub (src/whirl.cpp:1622-1630) to the incoming state first. */
+template <bool WRAP>
+__device__ __forceinline__ void wh_serial (float* r, uint32_t base, uint32_t m, float* fz, float a1, float a2, bool scrub)
 {
-	constexpr int NI   = WH_NI (W);
-	const int     lane = threadIdx.x & (NL - 1);
-	const int     r = lane / NI, j = lane % NI;
-	const bool    act = r < 4 && j < nj;
-	const int     rr = act ? r : 0, jj = act ? j : 0;
-	WhInst<W>&    I  = sm.in[jj];
-	const tbf_inst_const& K = cst[inst0 + jj];
-	const int     nSub = (int)P.nBlocks * (TBF_BLK / TBF_SUB);
-	const int     off  = rr == 0 ? 2 : (rr == 1 ? 1 : -1); /* this lane's sub-block at interval k: k + off */
-	__syncthreads (); /* the instance waves staged the states and the first input */
-	float c[5];
+	float z0 = fz[0], z1 = fz[1];
+	if (scrub) {
+		if (isnan (z0))
+			z0 = 0.f;
+		if (isnan (z1))
+			z1 = 0.f;
+	}
+	for (int i0 = 0; i0 < TBF_SUB; i0 += 8) {
+		float xv[8];
 #pragma unroll
-	for (int q = 0; q < 5; q++)
-		c[q] = rr == 0 ? I.st.prm.hafw[q] : (rr == 1 ? I.st.prm.hbfw[q] : K.drf[q]);
-	float z0 = I.st.fz[rr][0], z1 = I.st.fz[rr][1];
-#pragma unroll 1
-	for (int k = -2; k <= nSub + 1; k++) {
-		const int m   = k + off;
-		const int bfv = I.bf[blk_lane (max (m, 0) / (TBF_BLK / TBF_SUB))];
-		if (act && m >= 0 && m < nSub) {
-			if (rr < 2 && (m & 1) == 0 && (bfv >> 1)) { /* a new set from this block on (bypassed or not) */
-				const tbf_wh_params& S = P.whSets[(bfv >> 1) - 1];
+		for (int k = 0; k < 8; k++)
+			xv[k] = WRAP ? r[(base + (uint32_t)(i0 + k)) & m] : r[i0 + k];
 #pragma unroll
-				for (int q = 0; q < 5; q++)
-					c[q] = rr == 0 ? S.hafw[q] : S.hbfw[q];
-			}
-			if (!(bfv & 1)) {
-				const float* ip = rr == 0 ? I.xr[m & 3] : (rr == 1 ? sm.ha[m & 1][jj] : I.dr[rr - 2][m & 1]);
-				float*       op = rr == 0 ? sm.ha[m & 1][jj] : (rr == 1 ? I.hb[m & 1] : I.ds[rr - 2][m & 1]);
-				PRIO_UP ();
-				for (int i0 = 0; i0 < TBF_SUB; i0 += 8) {
-					float xv[8], yv[8];
-#pragma unroll
-					for (int q = 0; q < 8; q++)
-						xv[q] = ip[i0 + q];
-#pragma unroll
-					for (int q = 0; q < 8; q++) {
-						const float t = xv[q] - (c[0] * z0) - (c[1] * z1);
-						yv[q]         = (t * c[2]) + (c[3] * z0) + (c[4] * z1);
-						z1            = z0;
-						z0            = t;
-					}
-#pragma unroll
-					for (int q = 0; q < 8; q++)
-						op[i0 + q] = yv[q];
-				}
-				PRIO_DOWN ();
-				if (m & 1) {
-					if (isnan (z0))
-						z0 = 0.f;
-					if (isnan (z1))
-						z1 = 0.f;
-				}
-			}
+		for (int k = 0; k < 8; k++) {
+			const float t = xv[k] - (a1 * z0) - (a2 * z1);
+			z1            = z0;
+			z0            = t;
+			xv[k]         = t;
 		}
-		__syncthreads ();
+#pragma unroll
+		for (int k = 0; k < 8; k++) {
+			if (WRAP)
+				r[(base + (uint32_t)(i0 + k)) & m] = xv[k];
+			else
+				r[i0 + k] = xv[k];
+		}
 	}
-	if (act) {
-		I.st.fz[rr][0] = z0;
-		I.st.fz[rr][1] = z1;
-	}
-	__syncthreads (); /* before the instance waves store the states */
+	fz[0] = z0;
+	fz[1] = z1;
 }
 
-/* One sub-block (64 samples) of whirlProc2 for one instance wave (src/whirl.cpp:1191-1638),
- * without the DF2 filters (whirl_filters): ring outputs at outpos, rotor angles,
- * reflection filters, horn and drum motions into the rings.  Returns the horn outputs
- * (hornLevel * ring + leak) of the sub-block's samples; the drum rings' outputs go to the
- * filter wave.  fl: the output stores of sub-block k - 2, issued behind the motion-table
- * loads (vmcnt retires in issue order: stores issued before the loads would be waited for
- * with them) */
+/* the filter outputs, lane n = sample n: t = temp[n], z0 / z1 = the state the pass started
+ * from (temp[-1], temp[-2]); the neighbours' temps by DPP lane shifts */
+__device__ __forceinline__ float wh_output (float t, float z0, float z1, const float* c)
+{
+	const float t1 = lane_shr1_or (t, z0);  /* temp[n-1] */
+	const float t2 = lane_shr1_or (t1, z1); /* temp[n-2] */
+	return (t * c[2]) + (c[3] * t1) + (c[4] * t2);
+}
+
+/* A sub-block's two output stores, held back until the next sub-block has issued its
+ * motion-table loads: vmcnt retires in issue order, so a store issued before a load is
+ * waited for with it, and every sub-block waits for its table loads (and every block for
+ * its input) -- with the stores issued first, each of those waits also waited out the
+ * previous stores' write latency. */
 struct WhOut {
 	float* l;
 	float* r;
 	float  vl, vr;
 };
 
+/* the held stores; unconditional (a store under a branch makes the wait counts after it
+ * unknown, and the compiler then waits for everything) */
 __device__ __forceinline__ void wh_flush (const WhOut& o)
 {
 	*o.l = o.vl;
 	*o.r = o.vr;
 }
 
+/* whirlProc2 (src/whirl.cpp:1191-1638) + whirlProc3 mic mix (1653-1681).  in0 / in1: this
+ * block's input (samples lane, lane + 64); the next block's is loaded from inNext into
+ * nx0 / nx1 during the first sub-block (inNext may be this block's own input when there
+ * is no next block: a harmless re-read) */
 template <int W>
-__device__ __forceinline__ void whirl_sub (const tbf_launch& P, WhInst<W>& I, const tbf_inst_const& K, const int k,
-                                           const WhOut& fl, float& hLo, float& hRo)
+__device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypass, const int revOpt, const tbf_inst_const& K,
+                             const float in0, const float in1, const float* __restrict__ inNext, float& nx0, float& nx1,
+                             const bool hasNext, float* __restrict__ oL, float* __restrict__ oR, WhOut& pend)
 {
-	const int     lane  = threadIdx.x & (NL - 1);
-	const int     n     = lane;
-	tbf_wh_state& st    = I.st;
+	const int     lane  = threadIdx.x;
+	tbf_wh_state& st    = sm.st;
 	const float*  hnFwd = P.whTab;
 	const float*  hnBwd = P.whTab + TBF_WH_TSTRIDE;
 	const float*  drFwd = P.whTab + 2 * TBF_WH_TSTRIDE;
 	const float*  drBwd = P.whTab + 3 * TBF_WH_TSTRIDE;
 	const float*  bfw   = P.whBw;
 	const float*  bbw   = P.whBw + 16384 * 5;
-	const uint32_t WM   = (uint32_t)W - 1u;
-	const double   hornIncr = st.hornIncr, drumIncr = st.drumIncr;
-	const uint32_t outpos   = (st.outpos + (uint32_t)n) & 2047u;
-	const int32_t  unwrap   = (int32_t)(st.outpos + (uint32_t)n - outpos); /* 0 or 2048 */
-	const float    xin      = I.xr[k & 3][n];
-	const float    xdp      = n == 0 ? st.z[2] : I.xr[k & 3][n - 1];
-	/* ring reads + clear at outpos: before this sub-block's writes, which land >= 79
-	 * slots ahead (src/whirl.cpp:1585-1600) */
-	const uint32_t o   = outpos & WM;
-	const float    hlv = I.wring[0][o], hrv = I.wring[1][o];
-	I.dr[0][k & 1][n]  = I.wring[2][o];
-	I.dr[1][k & 1][n]  = I.wring[3][o];
-	I.wring[0][o]      = 0.f;
-	I.wring[1][o]      = 0.f;
-	I.wring[2][o]      = 0.f;
-	I.wring[3][o]      = 0.f;
-	if (lane < 4) {
-		const int i = lane;
-		I.xf[i] = st.adx[0][(st.adi[0] + 3 - i) & 7];
-		I.x1[i] = st.adx[1][(st.adi[1] + 3 - i) & 7];
-		I.x2[i] = st.adx[2][(st.adi[2] + 3 - i) & 7];
+
+	if (bypass) {
+		/* whirlProc2 bypass (src/whirl.cpp:1197-1215) + whirlProc3 mix */
+		nx0 = inNext[lane];
+		nx1 = inNext[lane + NL];
+		wh_flush (pend);
+		oL[lane] = in0 * K.mic[0] + in0 * K.mic[1] + 0.f * K.mic[2] + 0.f * K.mic[3];
+		oR[lane] = in0 * K.mic[4] + in0 * K.mic[5] + 0.f * K.mic[6] + 0.f * K.mic[7];
+		/* the second sub-block's outputs become the held stores, so that the held
+		 * stores always carry the latest output of their lane (a later flush of an older
+		 * one would overwrite a newer value) */
+		pend.l  = oL + NL + lane;
+		pend.r  = oR + NL + lane;
+		pend.vl = in1 * K.mic[0] + in1 * K.mic[1] + 0.f * K.mic[2] + 0.f * K.mic[3];
+		pend.vr = in1 * K.mic[4] + in1 * K.mic[5] + 0.f * K.mic[6] + 0.f * K.mic[7];
+		return;
 	}
-	I.xf[4 + n] = I.hb[k & 1][n];
-	/* rotor angles, angle = fmod (angle + incr, 1) per sample (src/whirl.cpp:1428-1429):
-	 * inside one binade of the angle every sum lands on the same grid, so the run is
-	 * a0 + n D exactly (phase_run); otherwise lanes 1, 2 replay the recurrence */
-	double ha, da;
-	{
-		double*      angBuf = &I.ang[0][0];
-		double       Dh, Dd;
-		const double h0 = st.hornAngle, d0 = st.drumAngle;
-		const bool   frc = (P.dbg & TBF_DEBUG_FORCE_SERIAL) != 0;
-		double       ch[4], cd[4]; /* the cached run analyses (the frexp / division only on a change) */
+	if (lane == 0) {
+		int brake;
+		/* a control entry carrying a rotary selection is used for exactly one block */
+		whirl_speed (st, K, revOpt, brake);
+		sm.brake = brake;
+	}
+	wave_sync ();
+	const double   hornIncr = st.hornIncr, drumIncr = st.drumIncr;
+	const uint32_t WM       = (uint32_t)W - 1u;
+	/* the horn filters' coefficients of this block (the runtime set in the state); serial
+	 * filter coefficients: lane 0 horn A, lane 1 horn B, lanes 2-3 drum shelf */
+	float ha[5], hb[5];
 #pragma unroll
-		for (int q = 0; q < 4; q++) {
-			ch[q] = st.angRun[0][q];
-			cd[q] = st.angRun[1][q];
+	for (int j = 0; j < 5; j++) {
+		ha[j] = st.prm.hafw[j];
+		hb[j] = st.prm.hbfw[j];
+	}
+	/* a1, a2 of the serial lanes' recurrences: lane 0 horn A, lane 1 horn B, lanes 2-3 drum shelves */
+	const float fa0 = lane == 0 ? ha[0] : (lane == 1 ? hb[0] : K.drf[0]);
+	const float fa1 = lane == 0 ? ha[1] : (lane == 1 ? hb[1] : K.drf[1]);
+
+	for (int sb = 0; sb < TBF_BLK / TBF_SUB; sb++) {
+		const int      n      = lane;
+		const uint32_t outpos = (st.outpos + (uint32_t)n) & 2047u;
+		const int32_t  unwrap = (int32_t)(st.outpos + (uint32_t)n - outpos); /* 0 or 2048 */
+		const float    xin    = (float)((double)(sb == 0 ? in0 : in1) + 1e-14);
+		/* ring reads + clear at outpos: before this sub-block's writes, which land >= 79
+		 * slots ahead (src/whirl.cpp:1585-1600); the drum rings' outputs are read by the
+		 * shelves in place first */
+		const uint32_t o   = outpos & WM;
+		const float    hlv = sm.wring[0][o], hrv = sm.wring[1][o];
+		sm.wring[0][o]     = 0.f;
+		sm.wring[1][o]     = 0.f;
+		if (lane < 4) {
+			const int i = lane;
+			sm.xf[i] = st.adx[0][(st.adi[0] + 3 - i) & 7];
+			sm.x1[i] = st.adx[1][(st.adi[1] + 3 - i) & 7];
+			sm.x2[i] = st.adx[2][(st.adi[2] + 3 - i) & 7];
 		}
-		const bool okh = phase_run_keyed (h0, hornIncr, TBF_SUB, Dh, ch) && !frc;
-		const bool okd = phase_run_keyed (d0, drumIncr, TBF_SUB, Dd, cd) && !frc;
-		wave_sync (); /* every lane has read the start angles and the caches */
-		if (lane == 0)
+		/* DF2 biquads: horn B runs on horn A's output, so A runs one sub-block ahead and
+		 * one serial pass advances A over the next sub-block (lane 0), B over this one into
+		 * xf (lane 1) and the drum shelves over this one's ring outputs, in place (lanes 2,
+		 * 3).  A's own pass over this sub-block runs only when it is not ahead (launch
+		 * start, after a bypassed block or a new coefficient set). */
+		const int  ap    = sm.ap;
+		const bool aNext = sb + 1 < TBF_BLK / TBF_SUB || hasNext;
+		if (!sm.aReady)
+			sm.ab[ap ^ 1][n] = xin;
+		if (aNext)
+			sm.ab[ap][n] = (float)((double)(sb + 1 < TBF_BLK / TBF_SUB ? in1 : nx0) + 1e-14);
+		wave_sync ();
+		if (!sm.aReady) {
+			const float z0 = st.fz[0][0], z1 = st.fz[0][1];
+			if (lane == 0)
+				wh_serial<false> (sm.ab[ap ^ 1], 0u, 0u, st.fz[0], ha[0], ha[1], false);
+			wave_sync ();
+			sm.ab[ap ^ 1][n] = wh_output (sm.ab[ap ^ 1][n], z0, z1, ha);
+			wave_sync ();
+		}
+		/* the states the pass starts from (horn A's scrubbed when it crosses into the next block) */
+		const bool scrubA = sb + 1 == TBF_BLK / TBF_SUB;
+		float      zs[4][2];
 #pragma unroll
-			for (int q = 0; q < 4; q++) {
-				st.angRun[0][q] = ch[q];
-				st.angRun[1][q] = cd[q];
-			}
-		if (lane == 0 && !(okh && okd))
-			atomicOr (P.errFlags, (uint32_t)TBF_PATH_WH_ANGLE);
-		if ((lane == 1 && !okh) || (lane == 2 && !okd)) {
-			double       a   = lane == 1 ? h0 : d0;
-			const double inc = lane == 1 ? hornIncr : drumIncr;
-			double*      row = angBuf + (lane - 1) * TBF_SUB;
-			for (int i0 = 0; i0 < TBF_SUB; i0 += 8) {
-				double av[8];
-#pragma unroll
-				for (int q = 0; q < 8; q++) {
-					av[q] = a;
-					a     = wrap1 (a + inc);
+		for (int f = 0; f < 4; f++) {
+			zs[f][0] = st.fz[f][0];
+			zs[f][1] = st.fz[f][1];
+		}
+		if (scrubA) {
+			zs[0][0] = isnan (zs[0][0]) ? 0.f : zs[0][0];
+			zs[0][1] = isnan (zs[0][1]) ? 0.f : zs[0][1];
+		}
+		const uint32_t wb   = st.outpos & WM; /* the drum rings' window: wave-uniform */
+		const bool     wrap = wb + TBF_SUB > (uint32_t)W;
+		if (lane < 4 && (lane > 0 || aNext)) {
+			float* row = lane == 0 ? sm.ab[ap] : (lane == 1 ? sm.ab[ap ^ 1] : sm.wring[lane]);
+			if (wrap)
+				wh_serial<true> (row, lane < 2 ? 0u : wb, lane < 2 ? ~0u : WM, st.fz[lane], fa0, fa1, lane == 0 && scrubA);
+			else
+				wh_serial<false> (row + (lane < 2 ? 0u : wb), 0u, 0u, st.fz[lane], fa0, fa1, lane == 0 && scrubA);
+		}
+		wave_sync ();
+		/* the filter outputs: horn B -> xf, horn A of the next sub-block in place, the drum
+		 * shelves' (then the ring slots are cleared) */
+		sm.xf[4 + n] = wh_output (sm.ab[ap ^ 1][n], zs[1][0], zs[1][1], hb);
+		if (aNext)
+			sm.ab[ap][n] = wh_output (sm.ab[ap][n], zs[0][0], zs[0][1], ha);
+		const float dL = wh_output (sm.wring[2][o], zs[2][0], zs[2][1], K.drf);
+		const float dR = wh_output (sm.wring[3][o], zs[3][0], zs[3][1], K.drf);
+		sm.wring[2][o] = 0.f;
+		sm.wring[3][o] = 0.f;
+		if (lane == 0) {
+			sm.aReady = aNext;
+			sm.ap     = ap ^ 1;
+		}
+		/* rotor angles, angle = fmod (angle + incr, 1) per sample (src/whirl.cpp:1428-1429):
+		 * inside one binade of the angle every sum lands on the same grid, so the run is
+		 * a0 + n D exactly (phase_run); otherwise lanes 1, 2 replay the recurrence into
+		 * the (consumed) filter scratch */
+		double ha, da;
+		{
+			double       Dh, Dd;
+			const double h0 = st.hornAngle, d0 = st.drumAngle;
+			const bool   frc = (P.dbg & TBF_DEBUG_FORCE_SERIAL) != 0;
+			const bool   okh = phase_run (h0, hornIncr, TBF_SUB, Dh) && !frc;
+			const bool   okd = phase_run (d0, drumIncr, TBF_SUB, Dd) && !frc;
+			ha = h0 + (double)n * Dh;
+			da = d0 + (double)n * Dd;
+			double he = h0 + (double)TBF_SUB * Dh, de = d0 + (double)TBF_SUB * Dd;
+			if (!(okh && okd)) { /* wave-uniform: every lane replays the recurrence, lane n keeps step n */
+				if (lane == 0)
+					atomicOr (P.errFlags, (uint32_t)TBF_PATH_WH_ANGLE);
+				double a = h0, b = d0;
+				for (int i = 0; i < TBF_SUB; i++) {
+					if (!okh && n == i)
+						ha = a;
+					if (!okd && n == i)
+						da = b;
+					a = wrap1 (a + hornIncr);
+					b = wrap1 (b + drumIncr);
 				}
-#pragma unroll
-				for (int q = 0; q < 8; q++)
-					row[i0 + q] = av[q];
+				he = okh ? he : a;
+				de = okd ? de : b;
+			}
+			wave_sync (); /* every lane has read the start angles */
+			if (lane == 0) {
+				st.hornAngle = he;
+				st.drumAngle = de;
 			}
 		}
 		wave_sync ();
-		ha = okh ? h0 + (double)n * Dh : angBuf[n];
-		da = okd ? d0 + (double)n * Dd : angBuf[TBF_SUB + n];
-		if (lane == 1)
-			st.hornAngle = okh ? h0 + (double)TBF_SUB * Dh : wrap1 (angBuf[TBF_SUB - 1] + hornIncr);
-		if (lane == 2)
-			st.drumAngle = okd ? d0 + (double)TBF_SUB * Dd : wrap1 (angBuf[2 * TBF_SUB - 1] + drumIncr);
-	}
-	wave_sync ();
-	/* reflection filters FILTER_C (src/whirl.cpp:1472-1477), lane-parallel */
-	const float xf   = I.xf[n + 4];
-	const float xfp  = n == 0 ? st.z[0] : I.xf[n + 3];
-	const float x1v  = (float)((0.4 * xf) + (0.4 * xfp));
-	I.x1[n + 4]      = x1v;
-	const float xd1v = (float)((0.4 * xin) + (0.4 * xdp));
-	I.xd1[n + 1]     = xd1v;
-	if (lane == 0)
-		I.xd1[0] = st.z[3];
-	wave_sync ();
-	const float x1p  = n == 0 ? st.z[1] : I.x1[n + 3];
-	const float x2v  = (float)((0.4 * x1v) + (0.4 * x1p));
-	I.x2[n + 4]      = x2v;
-	const float xd2v = (float)((0.4 * xd1v) + (0.4 * I.xd1[n]));
-	wave_sync ();
+		/* reflection filters FILTER_C (src/whirl.cpp:1472-1477), lane-parallel */
+		const float xf   = sm.xf[n + 4];
+		const float xfp  = n == 0 ? st.z[0] : sm.xf[n + 3];
+		const float x1v  = (float)((0.4 * xf) + (0.4 * xfp));
+		sm.x1[n + 4]     = x1v;
+		const float xdp  = lane_shr1_or (xin, st.z[2]); /* the previous sample's input */
+		const float xd1v = (float)((0.4 * xin) + (0.4 * xdp));
+		wave_sync ();
+		const float x1p  = n == 0 ? st.z[1] : sm.x1[n + 3];
+		const float x2v  = (float)((0.4 * x1v) + (0.4 * x1p));
+		sm.x2[n + 4]     = x2v;
+		const float xd1p = lane_shr1_or (xd1v, st.z[3]);
+		const float xd2v = (float)((0.4 * xd1v) + (0.4 * xd1p));
+		wave_sync ();
 
-	/* ---- rings (HL, HR, DL, DR) in groups of WH_RG: the group's motions first (their
-	 * table loads in flight together), then each ring's ordered adds ---- */
+		/* ---- rings (HL, HR, DL, DR) in groups of WH_RG: the group's motions first (their
+		 * table loads in flight together), then each ring's ordered adds ---- */
 #pragma unroll
-	for (int r0 = 0; r0 < 4; r0 += WH_RG) {
-		int   mu[WH_RG][3];
-		float ma[WH_RG][3], mb[WH_RG][3];
-		/* the table positions of all 12 motions, then every table load (18) in flight
-		 * together, then the arithmetic: issued motion by motion, each motion's loads
-		 * were waited for before the next motion's were issued */
-		float h1v[WH_RG][3];
+		for (int r0 = 0; r0 < 4; r0 += WH_RG) {
+			int   mu[WH_RG][3];
+			float ma[WH_RG][3], mb[WH_RG][3];
+			/* the table positions of all 12 motions, then every table load (18) in flight
+			 * together, then the arithmetic: issued motion by motion, each motion's loads
+			 * were waited for before the next motion's were issued */
+			float h1v[WH_RG][3];
 #pragma unroll
-		for (int gi = 0; gi < WH_RG; gi++)
+			for (int gi = 0; gi < WH_RG; gi++)
 #pragma unroll
-			for (int q = 0; q < 3; q++) {
-				const int p = ((r0 + gi) & 1) + 2 * q;
-				if (r0 + gi < 2) /* HN_MOTION, src/whirl.cpp:1434 */
-					h1v[gi][q] = (float)((ha + ((p & 1) ? K.bwAng : K.fwAng)) * (unsigned int)16384 + K.hornPhase[p]);
-				else /* DR_MOTION, src/whirl.cpp:1457 */
-					h1v[gi][q] = (float)(da * (unsigned int)16384 + K.hornPhase[p]);
-			}
-		f2u   dpv[WH_RG][3];
-		f4u   b4v[2][3];
-		float b5v[2][3];
-#pragma unroll
-		for (int gi = 0; gi < WH_RG; gi++)
-#pragma unroll
-			for (int q = 0; q < 3; q++) {
-				const int      p   = ((r0 + gi) & 1) + 2 * q;
-				const bool     fwd = (p == 0 || p == 3 || p == 4);
-				const float*   dsp = r0 + gi < 2 ? (fwd ? hnFwd : hnBwd) : (fwd ? drFwd : drBwd);
-				const unsigned hl  = ((unsigned int)floorf (h1v[gi][q])) & 16383u;
-				dpv[gi][q]         = *(const f2u*)(dsp + hl); /* dsp[hl], dsp[(hl + 1) & 16383] */
-				if (r0 + gi < 2) {
-					const unsigned kk = ((unsigned int)roundf (h1v[gi][q])) & 16383u;
-					const float*   b  = (fwd ? bbw : bfw) + 5 * kk;
-					b4v[gi][q]        = *(const f4u*)b;
-					b5v[gi][q]        = b[4];
+				for (int q = 0; q < 3; q++) {
+					const int p = ((r0 + gi) & 1) + 2 * q;
+					if (r0 + gi < 2) /* HN_MOTION, src/whirl.cpp:1434 */
+						h1v[gi][q] = (float)((ha + ((p & 1) ? K.bwAng : K.fwAng)) * (unsigned int)16384 + K.hornPhase[p]);
+					else /* DR_MOTION, src/whirl.cpp:1457 */
+						h1v[gi][q] = (float)(da * (unsigned int)16384 + K.hornPhase[p]);
 				}
-			}
-		/* behind the table loads: the next block's input (used from the second
-		 * sub-block on; the second sub-block loads it again, so that every sub-block
-		 * issues the same memory operations in the same order and each wait is
-		 * counted exactly) and the previous sub-block's output stores */
-		if (r0 == 0)
-			wh_flush (fl);
+			f2u   dpv[WH_RG][3];
+			f4u   b4v[2][3];
+			float b5v[2][3];
 #pragma unroll
-		for (int gi = 0; gi < WH_RG; gi++) {
-			const int r = r0 + gi;
+			for (int gi = 0; gi < WH_RG; gi++)
 #pragma unroll
-			for (int q = 0; q < 3; q++) {
-				const int   p  = (r & 1) + 2 * q;
-				const float h1 = h1v[gi][q], hd = frac1 (h1);
-				const f2u   dp = dpv[gi][q];
-				const float intp = dp.x * (1.f - hd) + hd * dp.y;
-				float       xa, t;
-				if (r < 2) {
-					/* HN_MOTION, src/whirl.cpp:1432-1453 */
-					const float* hist = p < 2 ? I.xf : (p < 4 ? I.x1 : I.x2);
-					const f4u    b4   = b4v[gi][q];
-					t                 = K.hornSpacing[p] + intp + (float)outpos;
-					xa                = b4.x * hist[n + 4];
-					xa += b4.y * hist[n + 3];
-					xa += b4.z * hist[n + 2];
-					xa += b4.w * hist[n + 1];
-					xa += b5v[gi][q] * hist[n + 0];
-				} else {
-					/* DR_MOTION, src/whirl.cpp:1455-1469 */
-					xa = p < 2 ? xin : (p < 4 ? xd1v : xd2v);
-					t  = K.drumSpacing[p] + intp + (float)outpos;
+				for (int q = 0; q < 3; q++) {
+					const int      p   = ((r0 + gi) & 1) + 2 * q;
+					const bool     fwd = (p == 0 || p == 3 || p == 4);
+					const float*   dsp = r0 + gi < 2 ? (fwd ? hnFwd : hnBwd) : (fwd ? drFwd : drBwd);
+					const unsigned hl  = ((unsigned int)floorf (h1v[gi][q])) & 16383u;
+					dpv[gi][q]         = *(const f2u*)(dsp + hl); /* dsp[hl], dsp[(hl + 1) & 16383] */
+					if (r0 + gi < 2) {
+						const unsigned kk = ((unsigned int)roundf (h1v[gi][q])) & 16383u;
+						const float*   b  = (fwd ? bbw : bfw) + 5 * kk;
+						b4v[gi][q]        = *(const f4u*)b;
+						b5v[gi][q]        = b[4];
+					}
 				}
-				const float rr = floorf (t);
-				const float qq = xa * (t - rr);
-				mu[gi][q]      = (int32_t)((unsigned int)rr) + unwrap;
-				ma[gi][q]      = xa - qq;
-				mb[gi][q]      = qq;
+			/* behind the table loads: the next block's input (used from the second
+			 * sub-block on; the second sub-block loads it again, so that every sub-block
+			 * issues the same memory operations in the same order and each wait is
+			 * counted exactly) and the previous sub-block's output stores */
+			if (r0 == 0) {
+				nx0 = inNext[lane];
+				nx1 = inNext[lane + NL];
+				wh_flush (pend);
 			}
-		}
-		/* fast path preconditions (wave votes), per ring: each motion's slot
-		 * non-decreasing in n with groups of <= 2 equal slots, and the ring's motions
-		 * >= 2 slots apart in source order at every sample (so passes farthest-first
-		 * keep the per-slot order: a farther motion reaches a slot only at earlier
-		 * samples) */
-		bool okr[WH_RG];
-		bool allOk = !(P.dbg & TBF_DEBUG_FORCE_SERIAL);
-#pragma unroll
-		for (int gi = 0; gi < WH_RG; gi++) {
-			int ok = (mu[gi][1] >= mu[gi][0] + 2) && (mu[gi][2] >= mu[gi][1] + 2);
-#pragma unroll
-			for (int q = 0; q < 3; q++) {
-				const int up = lane_shr1 (mu[gi][q]);
-				const int un = lane_shl1 (mu[gi][q]);
-				if (lane > 0 && mu[gi][q] < up)
-					ok = 0;
-				if (lane > 0 && lane < NL - 1 && up == mu[gi][q] && un == mu[gi][q])
-					ok = 0;
-			}
-			okr[gi] = __all (ok) && !(P.dbg & TBF_DEBUG_FORCE_SERIAL);
-			allOk   = allOk && okr[gi];
-		}
-		if (allOk) {
-			/* every ring on its fast path: the rings are independent, so each pass
-			 * (farthest motion first) updates all of them in one LDS round trip */
-#pragma unroll
-			for (int q = 2; q >= 0; q--) {
-				motion_pass<W, WH_RG> (I.wring + r0, mu, ma, mb, q);
-				wave_sync ();
-			}
-		} else {
 #pragma unroll
 			for (int gi = 0; gi < WH_RG; gi++) {
-				float* ring = I.wring[r0 + gi];
-				if (okr[gi]) {
-					motion_add<W> (ring, mu[gi][2], ma[gi][2], mb[gi][2], lane);
+				const int r = r0 + gi;
+#pragma unroll
+				for (int q = 0; q < 3; q++) {
+					const int   p  = (r & 1) + 2 * q;
+					const float h1 = h1v[gi][q], hd = frac1 (h1);
+					const f2u   dp = dpv[gi][q];
+					const float intp = dp.x * (1.f - hd) + hd * dp.y;
+					float       xa, t;
+					if (r < 2) {
+						/* HN_MOTION, src/whirl.cpp:1432-1453 */
+						const float* hist = p < 2 ? sm.xf : (p < 4 ? sm.x1 : sm.x2);
+						const f4u    b4   = b4v[gi][q];
+						t                 = K.hornSpacing[p] + intp + (float)outpos;
+						xa                = b4.x * hist[n + 4];
+						xa += b4.y * hist[n + 3];
+						xa += b4.z * hist[n + 2];
+						xa += b4.w * hist[n + 1];
+						xa += b5v[gi][q] * hist[n + 0];
+					} else {
+						/* DR_MOTION, src/whirl.cpp:1455-1469 */
+						xa = p < 2 ? xin : (p < 4 ? xd1v : xd2v);
+						t  = K.drumSpacing[p] + intp + (float)outpos;
+					}
+					const float rr = floorf (t);
+					const float qq = xa * (t - rr);
+					mu[gi][q]      = (int32_t)((unsigned int)rr) + unwrap;
+					ma[gi][q]      = xa - qq;
+					mb[gi][q]      = qq;
+				}
+			}
+			/* fast path preconditions (wave votes), per ring: each motion's slot
+			 * non-decreasing in n with groups of <= 2 equal slots, and the ring's motions
+			 * >= 2 slots apart in source order at every sample (so passes farthest-first
+			 * keep the per-slot order: a farther motion reaches a slot only at earlier
+			 * samples) */
+			bool okr[WH_RG];
+			bool allOk = !(P.dbg & TBF_DEBUG_FORCE_SERIAL);
+#pragma unroll
+			for (int gi = 0; gi < WH_RG; gi++) {
+				int ok = (mu[gi][1] >= mu[gi][0] + 2) && (mu[gi][2] >= mu[gi][1] + 2);
+#pragma unroll
+				for (int q = 0; q < 3; q++) {
+					const int up = lane_shr1 (mu[gi][q]);
+					const int un = lane_shl1 (mu[gi][q]);
+					if (lane > 0 && mu[gi][q] < up)
+						ok = 0;
+					if (lane > 0 && lane < NL - 1 && up == mu[gi][q] && un == mu[gi][q])
+						ok = 0;
+				}
+				okr[gi] = __all (ok) && !(P.dbg & TBF_DEBUG_FORCE_SERIAL);
+				allOk   = allOk && okr[gi];
+			}
+			if (allOk) {
+				/* every ring on its fast path: the rings are independent, so each pass
+				 * (farthest motion first) updates all of them in one LDS round trip */
+#pragma unroll
+				for (int q = 2; q >= 0; q--) {
+					motion_pass<W, WH_RG> (sm.wring + r0, mu, ma, mb, q);
 					wave_sync ();
-					motion_add<W> (ring, mu[gi][1], ma[gi][1], mb[gi][1], lane);
-					wave_sync ();
-					motion_add<W> (ring, mu[gi][0], ma[gi][0], mb[gi][0], lane);
-					wave_sync ();
-				} else {
-					/* serial replay in the reference order: sample-major, motions in source order */
-					if (lane == 0)
-						atomicOr (P.errFlags, (uint32_t)TBF_PATH_WH_MOTION);
-					for (int i = 0; i < TBF_SUB; i++) {
-	#pragma unroll
-						for (int q = 0; q < 3; q++) {
-							const uint32_t sl = (uint32_t)__shfl (mu[gi][q], i) & WM;
-							const float    aa = __shfl (ma[gi][q], i);
-							const float    bb = __shfl (mb[gi][q], i);
-							if (lane == 0) {
-								ring[sl] += aa;
-								ring[(sl + 1) & WM] += bb;
+				}
+			} else {
+#pragma unroll
+				for (int gi = 0; gi < WH_RG; gi++) {
+					float* ring = sm.wring[r0 + gi];
+					if (okr[gi]) {
+						motion_add<W> (ring, mu[gi][2], ma[gi][2], mb[gi][2], lane);
+						wave_sync ();
+						motion_add<W> (ring, mu[gi][1], ma[gi][1], mb[gi][1], lane);
+						wave_sync ();
+						motion_add<W> (ring, mu[gi][0], ma[gi][0], mb[gi][0], lane);
+						wave_sync ();
+					} else {
+						/* serial replay in the reference order: sample-major, motions in source order */
+						if (lane == 0)
+							atomicOr (P.errFlags, (uint32_t)TBF_PATH_WH_MOTION);
+						for (int i = 0; i < TBF_SUB; i++) {
+		#pragma unroll
+							for (int q = 0; q < 3; q++) {
+								const uint32_t sl = (uint32_t)__shfl (mu[gi][q], i) & WM;
+								const float    aa = __shfl (ma[gi][q], i);
+								const float    bb = __shfl (mb[gi][q], i);
+								if (lane == 0) {
+									ring[sl] += aa;
+									ring[(sl + 1) & WM] += bb;
+								}
 							}
 						}
+						wave_sync ();
 					}
-					wave_sync ();
 				}
 			}
 		}
+		/* ---- outputs (whirlProc2 outHL/outHR/outDL/outDR + whirlProc3 mix) ---- */
+		{
+			const float leak = xf * K.leakage;
+			const float hL   = K.hornLevel * hlv + leak;
+			const float hR   = K.hornLevel * hrv + leak;
+			pend.l           = oL + sb * TBF_SUB + n;
+			pend.r           = oR + sb * TBF_SUB + n;
+			pend.vl          = hL * K.mic[0] + hR * K.mic[1] + dL * K.mic[2] + dR * K.mic[3];
+			pend.vr          = hL * K.mic[4] + hR * K.mic[5] + dL * K.mic[6] + dR * K.mic[7];
+		}
+		/* ---- carry filter taps and histories ---- */
+		if (lane == NL - 1) {
+			st.z[0] = xf;
+			st.z[1] = x1v;
+			st.z[2] = xin;
+			st.z[3] = xd1v;
+		}
+		wave_sync ();
+		if (lane < 24) { /* history k = lane / 8, entry j = lane % 8, one lane each */
+			const int    k = lane >> 3, j = lane & 7;
+			const float* h = k == 0 ? sm.xf : (k == 1 ? sm.x1 : sm.x2);
+			st.adx[k][(st.adi[k] + j) & 7] = h[4 + TBF_SUB - 1 - j];
+		}
+		if (lane == 0)
+			st.outpos = (st.outpos + TBF_SUB) & 2047u;
+		wave_sync ();
 	}
-	/* the horn outputs (whirlProc2 outHL / outHR); the drum outputs follow the shelves */
-	const float leak = xf * K.leakage;
-	hLo              = K.hornLevel * hlv + leak;
-	hRo              = K.hornLevel * hrv + leak;
-	/* ---- carry filter taps and histories ---- */
-	if (lane == NL - 1) {
-		st.z[0] = xf;
-		st.z[1] = x1v;
-		st.z[2] = xin;
-		st.z[3] = xd1v;
+	/* NaN scrub (src/whirl.cpp:1622-1630), a lane per value: lanes 0..7 the filter states
+	 * fz (horn A's only when it did not run ahead: then it got its scrub when it crossed
+	 * into the next block), lanes 8..11 z */
+	if (lane < 8) {
+		const int f = lane >> 1, j = lane & 1;
+		if ((f > 0 || !sm.aReady) && isnan (st.fz[f][j]))
+			st.fz[f][j] = 0.f;
+	} else if (lane < 12) {
+		if (isnan (st.z[lane - 8]))
+			st.z[lane - 8] = 0.f;
 	}
-	wave_sync ();
-	if (lane < 24) { /* history q = lane / 8, entry i = lane % 8, one lane each */
-		const int    q = lane >> 3, i = lane & 7;
-		const float* h = q == 0 ? I.xf : (q == 1 ? I.x1 : I.x2);
-		st.adx[q][(st.adi[q] + i) & 7] = h[4 + TBF_SUB - 1 - i];
+	if (lane == 0) {
+		if (sm.brake & 1) st.hornIncr = 0;
+		if (sm.brake & 2) st.drumIncr = 0;
 	}
-	if (lane == 0)
-		st.outpos = (st.outpos + TBF_SUB) & 2047u;
 	wave_sync ();
 }
 
 static_assert (sizeof (tbf_wh_params) % 4 == 0 && sizeof (tbf_wh_params) <= 4 * NL, "one dword per lane");
 
-/* whirlProc2 (src/whirl.cpp:1191-1638) + whirlProc3's mic mix (1653-1681): a workgroup of
- * WH_NI instance waves (one instance each) and one filter wave (whirl_filters), stepping
- * in intervals of one sub-block with one barrier each.  At interval k an instance wave
- * stages its input of sub-block k + 3 for the filter wave (loaded from HBM an interval
- * earlier), renders sub-block k (whirl_sub: horn B's output of k is ready) and stores the
- * output of sub-block k - 2 (the drum shelves' output of k - 2 is ready): so the launch
- * runs intervals -2 .. nSub + 1.  Bypassed blocks (whirlProc2's bypass, 1197-1215) pass
- * through the same output pipeline. */
 template <int W>
-__global__ void __launch_bounds__ (NL * (WH_NI (W) + 1))
+__global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL), amdgpu_waves_per_eu (W <= 512 ? WH_WAVES : (W <= 1024 ? 2 : 1))))
 k_whirl (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_seg_ctl* __restrict__ ctl)
 {
-	constexpr int NI = WH_NI (W);
 	__shared__ WhLds<W> sm;
-	const int      w     = __builtin_amdgcn_readfirstlane (threadIdx.x >> 6), lane = threadIdx.x & (NL - 1);
-	const uint32_t inst0 = P.instBase + blockIdx.x * NI;
-	if (inst0 >= P.nInst)
+	const uint32_t inst = blockIdx.x + P.instBase;
+	if (inst >= P.nInst)
 		return;
-	const int nj = (int)min ((uint32_t)NI, P.nInst - inst0);
-	if (w == NI) {
-		whirl_filters<W> (P, cst, sm, inst0, nj);
-		return;
+	const tbf_inst_const& K  = cst[inst];
+	tbf_wh_state*         S  = &P.st[inst].wh;
+	float*                wr = P.wring + (size_t)inst * 4 * W;
+	copy_words (&sm.st, S);
+	if (threadIdx.x == 0) {
+		sm.aReady = 0;
+		sm.ap     = 0;
 	}
-	const bool            live = w < nj;
-	const uint32_t        inst = inst0 + (live ? w : 0);
-	WhInst<W>&            I    = sm.in[w];
-	const tbf_inst_const& K    = cst[inst];
-	tbf_wh_state*         S    = &P.st[inst].wh;
-	float*                wr   = P.wring + (size_t)inst * 4 * W;
-	const int             nSub = (int)P.nBlocks * (TBF_BLK / TBF_SUB);
-	const float*          inB  = P.mid2 + (size_t)inst * P.midStride;
-	float*                oL   = P.outL + (size_t)inst * P.outStride + P.outOffset + lane;
-	float*                oR   = P.outR + (size_t)inst * P.outStride + P.outOffset + lane;
-	int                   rvv  = -1;
-	float                 xnx  = 0.f;
-	if (live) {
-		copy_words (&I.st, S);
-		for (uint32_t i = lane; i < 4u * W; i += NL)
-			(&I.wring[0][0])[i] = wr[i];
-		/* the launch's per-block control (bypass, coefficient set, rotary selection), lane
-		 * b = block b (<= 64 blocks; a longer launch has no deltas) */
-		int bfv = 0;
-		if ((uint32_t)lane < P.nBlocks) {
-			const tbf_seg_ctl& Gb = ctl_of (P, ctl, lane, inst);
-			bfv                   = (Gb.whBypass != 0) | (int)(Gb.whSet << 1);
-			rvv                   = Gb.whRevOption;
-		}
-		I.bf[lane]    = bfv;
-		I.xr[0][lane] = (float)((double)inB[lane] + 1e-14);
-		xnx           = inB[min (1, nSub - 1) * TBF_SUB + lane];
+	for (uint32_t i = threadIdx.x; i < 4u * W; i += NL)
+		(&sm.wring[0][0])[i] = wr[i];
+	wave_sync ();
+	/* the input (lane n: samples n and n + 64 of a block) is loaded one block ahead, in
+	 * the block's first sub-block behind its table loads (stage_whirl), so its latency
+	 * overlaps a whole sub-block and no wait for it waits for output stores */
+	const float* inBase = P.mid2 + (size_t)inst * P.midStride;
+	/* the launch's per-block control (bypass, rotary selection), lane b = block b (<= 64
+	 * blocks): read once, so no block waits on the two dependent control loads */
+	int byv = 0, rvv = -1, wsv = 0;
+	if (threadIdx.x < P.nBlocks) {
+		const tbf_seg_ctl& Gb = ctl_of (P, ctl, threadIdx.x, inst);
+		byv                   = Gb.whBypass != 0;
+		rvv                   = Gb.whRevOption;
+		wsv                   = (int)Gb.whSet;
 	}
-	__syncthreads ();
-	/* the output pipeline: sub-block k - 1 (a1, b1, p1) and k - 2 (a2, b2, p2): the horn
-	 * outputs, or (bypassed) the input twice; before the first output, the stores write 0
-	 * to the lane's first sample, which its real output overwrites later (same lane, same
+	float c0 = 0.f, c1 = 0.f;
+	if (P.nBlocks > 0) {
+		c0 = inBase[threadIdx.x];
+		c1 = inBase[threadIdx.x + NL];
+	}
+	/* before the first sub-block's outputs exist, the held store writes 0 to the first
+	 * output sample of the lane, which the real output overwrites later (same lane, same
 	 * address: in order) */
-	float a1 = 0.f, b1 = 0.f, a2 = 0.f, b2 = 0.f;
-	bool  p1 = false, p2 = false;
-#pragma unroll 1
-	for (int k = -2; k <= nSub + 1; k++) {
-		if (live) {
-			/* stage the input of sub-block k + 3, load k + 4's (clamped past the end) */
-			if (k + 3 < nSub)
-				I.xr[(k + 3) & 3][lane] = (float)((double)xnx + 1e-14);
-			xnx = inB[(size_t)min (k + 4, nSub - 1) * TBF_SUB + lane];
-			/* the output stores of sub-block k - 2 */
-			WhOut fl;
-			const int ko = max (k - 2, 0);
-			fl.l         = oL + (size_t)ko * TBF_SUB;
-			fl.r         = oR + (size_t)ko * TBF_SUB;
-			if (k - 2 < 0)
-				fl.vl = fl.vr = 0.f;
-			else if (p2) {
-				fl.vl = a2 * K.mic[0] + a2 * K.mic[1] + 0.f * K.mic[2] + 0.f * K.mic[3];
-				fl.vr = a2 * K.mic[4] + a2 * K.mic[5] + 0.f * K.mic[6] + 0.f * K.mic[7];
-			} else {
-				const float dL = I.ds[0][ko & 1][lane], dR = I.ds[1][ko & 1][lane];
-				fl.vl = a2 * K.mic[0] + b2 * K.mic[1] + dL * K.mic[2] + dR * K.mic[3];
-				fl.vr = a2 * K.mic[4] + b2 * K.mic[5] + dL * K.mic[6] + dR * K.mic[7];
-			}
-			float a0 = 0.f, b0 = 0.f;
-			bool  p0 = false;
-			if (k >= 0 && k < nSub) {
-				const int blk = k / (TBF_BLK / TBF_SUB), sb = k % (TBF_BLK / TBF_SUB);
-				const int bfv = I.bf[blk_lane (blk)];
-				p0            = (bfv & 1) != 0;
-				if (sb == 0) {
-					/* a new parameter set (MIDI control functions) from this block on */
-					if (bfv >> 1) {
-						const uint32_t* src = (const uint32_t*)(P.whSets + ((bfv >> 1) - 1));
-						if (lane < (int)(sizeof (tbf_wh_params) / 4))
-							((uint32_t*)&I.st.prm)[lane] = src[lane];
-						wave_sync ();
-					}
-					if (!p0 && lane == 0) {
-						int brake;
-						/* a control entry carrying a rotary selection is used for exactly one block */
-						whirl_speed (I.st, K, rl (rvv, blk_lane (blk)), brake);
-						I.brake = brake;
-					}
-					wave_sync ();
-				}
-				if (p0) {
-					wh_flush (fl);
-					a0 = inB[(size_t)k * TBF_SUB + lane]; /* whirlProc2's bypass: the input */
-				} else {
-					whirl_sub<W> (P, I, K, k, fl, a0, b0);
-					if (sb == TBF_BLK / TBF_SUB - 1) {
-						/* block end: NaN scrub of the reflection states (src/whirl.cpp:1628-1631),
-						 * the brake's speed reset */
-						if (lane < 4 && isnan (I.st.z[lane]))
-							I.st.z[lane] = 0.f;
-						if (lane == 0) {
-							if (I.brake & 1) I.st.hornIncr = 0;
-							if (I.brake & 2) I.st.drumIncr = 0;
-						}
-						wave_sync ();
-					}
-				}
-			} else
-				wh_flush (fl);
-			a2 = a1;
-			b2 = b1;
-			p2 = p1;
-			a1 = a0;
-			b1 = b0;
-			p1 = p0;
+	WhOut pend;
+	pend.l  = P.outL + (size_t)inst * P.outStride + P.outOffset + threadIdx.x;
+	pend.r  = P.outR + (size_t)inst * P.outStride + P.outOffset + threadIdx.x;
+	pend.vl = pend.vr = 0.f;
+	for (uint32_t blk = 0; blk < P.nBlocks; blk++) {
+		float*     oL = P.outL + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
+		float*     oR = P.outR + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
+		float      n0, n1;
+		const bool more = blk + 1 < P.nBlocks;
+		/* a new parameter set (MIDI control functions) from this block on */
+		const int ws = rl (wsv, blk_lane ((int)blk));
+		if (ws) {
+			const uint32_t* src = (const uint32_t*)(P.whSets + (ws - 1));
+			if (threadIdx.x < sizeof (tbf_wh_params) / 4)
+				((uint32_t*)&sm.st.prm)[threadIdx.x] = src[threadIdx.x];
+			wave_sync ();
 		}
-		__syncthreads ();
+		/* horn filter A may run ahead into the next block unless that one is bypassed or
+		 * changes its coefficients */
+		const int  nx      = blk_lane ((int)blk + 1);
+		const bool hasNext = more && !rl (byv, nx) && !rl (wsv, nx);
+		stage_whirl<W> (P, sm, rl (byv, blk_lane ((int)blk)) != 0, rl (rvv, blk_lane ((int)blk)), K, c0, c1,
+		                inBase + (size_t)(more ? blk + 1 : blk) * TBF_BLK, n0, n1, hasNext, oL, oR, pend);
+		c0 = n0;
+		c1 = n1;
 	}
-	__syncthreads (); /* the filter wave wrote its states */
-	if (live) {
-		copy_words (S, &I.st);
-		for (uint32_t i = lane; i < 4u * W; i += NL)
-			wr[i] = (&I.wring[0][0])[i];
-	}
+	if (P.nBlocks > 0)
+		wh_flush (pend);
+	wave_sync ();
+	copy_words (S, &sm.st);
+	for (uint32_t i = threadIdx.x; i < 4u * W; i += NL)
+		wr[i] = (&sm.wring[0][0])[i];
 }
 
 /* ------------------------------------------------------------------ launch */
@@ -2810,20 +2821,10 @@ extern "C" int tbf_launch_stage (const tbf_launch* P, int k, hipStream_t stream)
 	else if (k == 4)
 		hipLaunchKernelGGL (k_rv_post, cgrid, cblock, 0, stream, *P, P->cst, P->ctl);
 	else if (k == 5) {
-		/* WH_NI (W) instance waves + the filter wave per workgroup */
 		switch (P->wringLen) {
-			case 512:
-				hipLaunchKernelGGL (k_whirl<512>, dim3 ((P->nInst + WH_NI (512) - 1) / WH_NI (512)), dim3 (NL * (WH_NI (512) + 1)),
-				                    0, stream, *P, P->cst, P->ctl);
-				break;
-			case 1024:
-				hipLaunchKernelGGL (k_whirl<1024>, dim3 ((P->nInst + WH_NI (1024) - 1) / WH_NI (1024)),
-				                    dim3 (NL * (WH_NI (1024) + 1)), 0, stream, *P, P->cst, P->ctl);
-				break;
-			case 2048:
-				hipLaunchKernelGGL (k_whirl<2048>, dim3 ((P->nInst + WH_NI (2048) - 1) / WH_NI (2048)),
-				                    dim3 (NL * (WH_NI (2048) + 1)), 0, stream, *P, P->cst, P->ctl);
-				break;
+			case 512: hipLaunchKernelGGL (k_whirl<512>, grid, block, 0, stream, *P, P->cst, P->ctl); break;
+			case 1024: hipLaunchKernelGGL (k_whirl<1024>, grid, block, 0, stream, *P, P->cst, P->ctl); break;
+			case 2048: hipLaunchKernelGGL (k_whirl<2048>, grid, block, 0, stream, *P, P->cst, P->ctl); break;
 			default: return -22;
 		}
 	} else

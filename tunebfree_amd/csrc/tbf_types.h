@@ -230,7 +230,6 @@ typedef struct tbf_wh_state { /* whirl: k_whirl */
 	int32_t  adi[3];
 	int32_t  pad1[2];
 	tbf_wh_params prm; /* the current runtime parameters */
-	double   angRun[2][4]; /* k_whirl: the rotor angles' closed-form run analysis (phase_run_keyed) */
 } tbf_wh_state;
 
 typedef struct tbf_inst_state {

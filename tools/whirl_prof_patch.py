@@ -34,8 +34,8 @@ s = s.replace("\tif (lane == 0) {\n\t\tint brake;", mark(10)[1:].replace("\t\tif
 s = s.replace("\t\tsm.ap     = 0;\n\t}\n",
               "\t\tsm.ap     = 0;\n\t}\n\tif (threadIdx.x < 16) sm.wp[threadIdx.x] = 0;\n"
               "\tif (threadIdx.x == 0) sm.wplast = __builtin_amdgcn_s_memtime ();\n", 1)
-s = s.replace("\twave_sync ();\n\tcopy_words (S, &sm.st);\n\tfor (uint32_t i = threadIdx.x; i < 4u * W; i += NL)\n\t\twr[i] = (&sm.wring[0][0])[i];\n}",
-              "\twave_sync ();\n\tcopy_words (S, &sm.st);\n\tfor (uint32_t i = threadIdx.x; i < 4u * W; i += NL)\n\t\twr[i] = (&sm.wring[0][0])[i];\n"
+s = s.replace("\twave_sync ();\n\tcopy_words (S, &sm.st);\n\tfor (uint32_t i = threadIdx.x; i < 4u * W; i += NL)\n\t\twr[i] = sm.wring[i / W][i % W];\n}",
+              "\twave_sync ();\n\tcopy_words (S, &sm.st);\n\tfor (uint32_t i = threadIdx.x; i < 4u * W; i += NL)\n\t\twr[i] = sm.wring[i / W][i % W];\n"
               "\tif (inst < 8 && threadIdx.x < 16) P.outL[(size_t)inst * P.outStride + P.outOffset + threadIdx.x] = (float)sm.wp[threadIdx.x];\n}")
 assert s.count("sm.wp[") >= 11, s.count("sm.wp[")
 Path(sys.argv[1]).write_text(s)

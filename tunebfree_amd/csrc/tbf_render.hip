@@ -46,6 +46,9 @@
 #ifndef WH_RG
 #define WH_RG 2 /* k_whirl rings per motion group (4 or 2) */
 #endif
+#ifndef WH_PAD
+#define WH_PAD 1 /* floats after each LDS ring / horn-A row: rows of one serial pass on different banks */
+#endif
 /* wave priority raised (s_setprio 1) while a wave runs a serial chain, so the SIMD issues
  * the chain's dependent instructions ahead of other waves' lane-parallel work */
 #define PRIO_UP() __builtin_amdgcn_s_setprio (1)
@@ -85,14 +88,14 @@ struct TgLds {
 template <int W>
 struct WhLds {
 	tbf_wh_state st;
-	float        wring[4][W];
+	float        wring[4][W + WH_PAD]; /* rows padded: the serial lanes 2, 3 read rings 2, 3 at the same index */
 	float        xf[TBF_SUB + 4];
 	float        x1[TBF_SUB + 4];
 	float        x2[TBF_SUB + 4];
 	/* horn A rows by parity ap: ab[ap] takes the next sub-block's input and horn A filters
 	 * it in place (A runs one sub-block ahead), ab[ap ^ 1] holds A's output of this
 	 * sub-block, horn B's input */
-	float        ab[2][TBF_SUB];
+	float        ab[2][TBF_SUB + WH_PAD];
 	int          brake;
 	int          aReady; /* ab[ap ^ 1] holds this sub-block's horn A output */
 	int          ap;
@@ -2229,7 +2232,7 @@ __device__ __forceinline__ void motion_add (float* ring, int U, float a, float b
 __device__ __forceinline__ bool lane_in (uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64 (m); }
 
 template <int W, int RG>
-__device__ __forceinline__ void motion_pass (float (*ring)[W], const int (&mu)[RG][3], const float (&ma)[RG][3],
+__device__ __forceinline__ void motion_pass (float (*ring)[W + WH_PAD], const int (&mu)[RG][3], const float (&ma)[RG][3],
                                              const float (&mb)[RG][3], const int q)
 {
 	const uint32_t WM = (uint32_t)W - 1u;
@@ -2725,7 +2728,7 @@ k_whirl (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 		sm.ap     = 0;
 	}
 	for (uint32_t i = threadIdx.x; i < 4u * W; i += NL)
-		(&sm.wring[0][0])[i] = wr[i];
+		sm.wring[i / W][i % W] = wr[i];
 	wave_sync ();
 	/* the input (lane n: samples n and n + 64 of a block) is loaded one block ahead, in
 	 * the block's first sub-block behind its table loads (stage_whirl), so its latency
@@ -2779,7 +2782,7 @@ k_whirl (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 	wave_sync ();
 	copy_words (S, &sm.st);
 	for (uint32_t i = threadIdx.x; i < 4u * W; i += NL)
-		wr[i] = (&sm.wring[0][0])[i];
+		wr[i] = sm.wring[i / W][i % W];
 }
 
 /* ------------------------------------------------------------------ launch */

@@ -1485,13 +1485,14 @@ static int stepChunkParallel (tbf_engine* e, uint32_t n, uint32_t want, uint32_t
 	return 0;
 }
 
-/* Device front end: a chunk whose events are all notes, over instances whose control is
- * otherwise settled (no parameter, programme, rotor or whirl change pending, no drawbar or
- * routing step), is stepped by k_front on the device (csrc/tbf_ctl.hip): the messages, the
- * stepped blocks, the control records and the index table come from the instances' key
- * state at the chunk start and their note events.  The host only partitions the events
- * by instance and applies them to its own key state (the truth for any later host-stepped
- * chunk): no per-block step, no records, no index table. */
+/* Device front end: a chunk whose events are all notes or front-end parameters (drawbars,
+ * the vibrato and percussion switches: frontParam), over instances whose control is
+ * otherwise settled (no other parameter, programme, rotor or whirl change pending, no
+ * drawbar or routing step), is stepped by k_front on the device (csrc/tbf_ctl.hip): the
+ * messages, the stepped blocks, the control records and the index table come from the
+ * instances' front-end state at the chunk start and their events.  The host only
+ * partitions the events by instance and applies them to its own mirror state (the truth
+ * for any later host-stepped chunk): no records, no index table. */
 static bool frontClean (const Instance& in)
 {
 	const TgControl& t = in.tg;

@@ -303,45 +303,87 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 			}
 		};
 		/* groups of four entries: every load of a group (bank samples, envelope rows) is
-		 * issued before its arithmetic, the remainder one entry at a time */
-		auto group = [&] (int e, auto KC, auto EC) {
-			constexpr int  K  = decltype (KC)::value;
+		 * issued before its arithmetic, and the next group's loads before this group's
+		 * arithmetic (two register sets, A and B, alternating: a copy from one set to the
+		 * other at the loop's back edge would wait for the loads); the remainder one entry
+		 * at a time */
+		constexpr int K = 4;
+		struct Grp {
+			f2v xs[K], evs[K];
+		};
+		auto load = [&] (Grp& G, int e, auto EC) {
 			constexpr bool EN = decltype (EC)::value; /* the block has envelope entries */
-			f2v      xs[K], evs[K];
-			float    gg[K][6];
-			uint32_t ers[K];
 #pragma unroll
 			for (int k = 0; k < K; k++) {
 				const float* __restrict__ bp = P.bank + sm.u.ent.base[e + k];
-				xs[k]                        = f2v {bp[lane], bp[lane + NL]};
-				ent (e + k, gg[k], ers[k]);
+				G.xs[k]                      = f2v {bp[lane], bp[lane + NL]};
 				if constexpr (EN) { /* (a steady entry loads row 0 of the attack table: an L1 hit) */
-					const uint32_t env = ers[k] & 0xffu, row = (ers[k] >> 8) & 7u;
+					float    gg[6];
+					uint32_t er;
+					ent (e + k, gg, er);
+					const uint32_t env = er & 0xffu, row = (er >> 8) & 7u;
 					const float*   ep  = (env == 2 ? T->releaseEnv[row] : T->attackEnv[row]);
-					evs[k]             = f2v {ep[lane], ep[lane + NL]};
-				}
-			}
-#pragma unroll
-			for (int k = 0; k < K; k++) {
-				const float* g = gg[k];
-				if (EN && (ers[k] & 0xffu)) {
-					/* envelope entry x * (g + e (ng - g)) (src/tonegen.cpp:3640-3662) */
-					sw = sw + xs[k] * (g[0] + (evs[k] * (g[3] - g[0])));
-					vb = vb + xs[k] * (g[2] + (evs[k] * (g[5] - g[2])));
-					pc = pc + xs[k] * (g[1] + (evs[k] * (g[4] - g[1])));
-				} else { /* x * g (3667-3685) */
-					sw = sw + xs[k] * g[0];
-					vb = vb + xs[k] * g[2];
-					pc = pc + xs[k] * g[1];
+					G.evs[k]           = f2v {ep[lane], ep[lane + NL]};
 				}
 			}
 		};
+		auto compute = [&] (const Grp& G, int e, auto EC) {
+			constexpr bool EN = decltype (EC)::value;
+#pragma unroll
+			for (int k = 0; k < K; k++) {
+				float    g[6];
+				uint32_t er;
+				ent (e + k, g, er);
+				if (EN && (er & 0xffu)) {
+					/* envelope entry x * (g + e (ng - g)) (src/tonegen.cpp:3640-3662) */
+					sw = sw + G.xs[k] * (g[0] + (G.evs[k] * (g[3] - g[0])));
+					vb = vb + G.xs[k] * (g[2] + (G.evs[k] * (g[5] - g[2])));
+					pc = pc + G.xs[k] * (g[1] + (G.evs[k] * (g[4] - g[1])));
+				} else { /* x * g (3667-3685) */
+					sw = sw + G.xs[k] * g[0];
+					vb = vb + G.xs[k] * g[2];
+					pc = pc + G.xs[k] * g[1];
+				}
+			}
+		};
+		/* one entry: the remainder */
+		auto single = [&] (int e, auto EC) {
+			constexpr bool EN = decltype (EC)::value;
+			float          g[6];
+			uint32_t       er;
+			ent (e, g, er);
+			const float* __restrict__ bp = P.bank + sm.u.ent.base[e];
+			const f2v x                  = f2v {bp[lane], bp[lane + NL]};
+			if (EN && (er & 0xffu)) {
+				const uint32_t env = er & 0xffu, row = (er >> 8) & 7u;
+				const float*   ep  = (env == 2 ? T->releaseEnv[row] : T->attackEnv[row]);
+				const f2v      ev  = f2v {ep[lane], ep[lane + NL]};
+				sw                 = sw + x * (g[0] + (ev * (g[3] - g[0])));
+				vb                 = vb + x * (g[2] + (ev * (g[5] - g[2])));
+				pc                 = pc + x * (g[1] + (ev * (g[4] - g[1])));
+			} else {
+				sw = sw + x * g[0];
+				vb = vb + x * g[2];
+				pc = pc + x * g[1];
+			}
+		};
 		auto run = [&] (auto EC) {
-			int e = 0;
-			for (; e + 4 <= np; e += 4)
-				group (e, IntC<4> {}, EC);
-			for (; e < np; e++)
-				group (e, IntC<1> {}, EC);
+			const int nG = np / K;
+			Grp       A, B;
+			int       gi = 0;
+			if (nG > 0)
+				load (A, 0, EC);
+			for (; gi + 2 <= nG; gi += 2) {
+				load (B, K * (gi + 1), EC);
+				compute (A, K * gi, EC);
+				if (gi + 2 < nG)
+					load (A, K * (gi + 2), EC);
+				compute (B, K * (gi + 1), EC);
+			}
+			if (gi < nG)
+				compute (A, K * gi, EC);
+			for (int e = K * nG; e < np; e++)
+				single (e, EC);
 		};
 		if (anyEnv)
 			run (BoolC<true> {});

@@ -39,7 +39,7 @@ for s in $STEPS; do
 		run ffetch 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/ffetch" -o run --output-format csv -- python3 bench.py $NC
 		run fwrite 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/fwrite" -o run --output-format csv -- python3 bench.py $NC
 		run ftraffic 60 python3 tools/traffic_from_pmc.py "$OUT/ffetch" "$OUT/fwrite" --blocks ${BLOCKS:-256} --out "$OUT/traffic.json"
-		run fbench 900 python3 bench.py --traffic "$OUT/traffic.json"
+		run fbench 900 python3 bench.py --steps 20 --warmup 5 --traffic "$OUT/traffic.json"
 		cp "$OUT/fbench.log" "$OUT/bench.json"
 		;;
 	kpmc)
@@ -56,7 +56,7 @@ for s in $STEPS; do
 		run dense 500 python3 -u tools/dense_events.py --out "$OUT/dense_events.json"
 		run rt 300 python3 -u tools/rt_latency.py --out "$OUT/rt_latency.json"
 		;;
-	iso) run iso 300 python3 bench.py --isolated 1 --cpu-baseline 0 ;;
+	iso) run iso 300 python3 bench.py --steps 20 --warmup 5 --isolated 1 --cpu-baseline 0 ;;
 	prof) # phase clocks of k_rv_core_lds and k_whirl (build variants from tools/*_prof_patch.py)
 		run rvl_prof 200 env TBF_LIB=tunebfree_amd/_prof/libtbf_rvlprof.so python3 tools/rvl_prof.py
 		run whirl_prof 200 env TBF_LIB=tunebfree_amd/_prof/libtbf_whprof.so python3 tools/whirl_prof.py
@@ -65,6 +65,10 @@ for s in $STEPS; do
 		run calib_f 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/calib_f" -o run --output-format csv -- python3 tools/calib_pmc.py 2 0,2,1,3
 		run calib_w 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/calib_w" -o run --output-format csv -- python3 tools/calib_pmc.py 2 0,2,1,3 ;;
 	bench) run bench 300 python3 bench.py --cpu-baseline 0 ;;
+	fbench:*) # fbench:DIR -- the driver's bench (20 steps, 5 warmup) with DIR/traffic.json
+		d=${s#fbench:}
+		run fbench 900 python3 bench.py --steps 20 --warmup 5 --traffic "$d/traffic.json"
+		cp "$OUT/fbench.log" "$OUT/bench.json" ;;
 	ab:*) # ab:VAR=VALUE -- the default bench with one environment switch (A/B)
 		kv=${s#ab:}
 		run "ab_${kv//[^A-Za-z0-9_]/_}" 300 env "$kv" python3 bench.py --cpu-baseline 0 ;;

@@ -977,11 +977,17 @@ def test_gpu_device_templates_match_oracle_and_reference(oracle, sr):
     lib.tbf_debug_tables.restype = C.c_int
     lib.tbf_debug_tables.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
 
+    from orc_bind import Cfg, contrib_from
+    lib.tbf_debug_contrib.restype = C.c_int
+    lib.tbf_debug_contrib.argtypes = [C.c_void_p, C.c_uint32, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.c_uint32]
+
     def tables(tid):
         bank, lens = eng.template_bank(tid)
         a, r, k = np.zeros((9, 128), np.float32), np.zeros((9, 128), np.float32), np.zeros(128, np.float32)
         assert lib.tbf_debug_tables(eng._h, tid, a.ctypes.data, r.ctypes.data, k.ctypes.data) >= 0
-        return {"bank": bank, "lens": lens, "attack": a, "release": r, "keycomp": k}
+        contrib = contrib_from(lambda kk, w, b, lv, cap: lib.tbf_debug_contrib(eng._h, tid, kk, w, b, lv, cap))
+        return {"bank": bank, "lens": lens, "attack": a, "release": r, "keycomp": k, "contrib": contrib}
 
     def mts(nm):
         return None if tunings[nm] is None else np.asarray(tunings[nm], np.float64)
@@ -1006,7 +1012,7 @@ def test_gpu_device_templates_match_oracle_and_reference(oracle, sr):
         o = Template(oracle, sr=sr, mts128=mts(nm), seed=seed)
         ob, ol = o.bank()
         oa, orr, ok = o.envs()
-        want = {"bank": ob, "lens": ol, "attack": oa, "release": orr, "keycomp": ok}
+        want = {"bank": ob, "lens": ol, "attack": oa, "release": orr, "keycomp": ok, "contrib": o.contrib()}
         for key in want:
             assert np.array_equal(np.asarray(got[key]).view(np.uint32), np.asarray(want[key]).view(np.uint32)), \
                 (nm, seed, key)
@@ -1017,10 +1023,6 @@ def test_gpu_device_templates_match_oracle_and_reference(oracle, sr):
     eng.close()
     # the template cfg keys (envelope models, lengths, levels, x-precision; wheel EQ,
     # harmonics, the play matrix lists and levels) on the device path
-    from orc_bind import Cfg, contrib_from
-    lib.tbf_debug_contrib.restype = C.c_int
-    lib.tbf_debug_contrib.argtypes = [C.c_void_p, C.c_uint32, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
-                                      C.c_uint32]
     for p in [p for p in allpins if p["sr"] == sr and p.get("cfg")]:
         eng = T.Engine(sample_rate=sr, device=0)
         eng.config(S.CFG_SETS[p["cfg"]])
@@ -1039,6 +1041,62 @@ def test_gpu_device_templates_match_oracle_and_reference(oracle, sr):
             assert np.array_equal(np.asarray(v).view(np.uint32), np.asarray(want[key]).view(np.uint32)), (p["cfg"], key)
             assert hashlib.sha256(np.ascontiguousarray(v).tobytes()).hexdigest() == p[key], (p["cfg"], key)
         eng.close()
+
+
+def test_gpu_device_play_matrix_matches_host_builder():
+    """the play matrix built on the device (k_tpl_matrix in
+    tbf_templates_create: applyManualDefaults' nearest-wheel search, the pedal defaults,
+    the default crosstalk and compilePlayMatrix's cell sums, src/tonegen.cpp:707-879,
+    1061-1213) against the host builder (tbf_template_create, pinned to the reference's
+    compilePlayMatrix by tests/golden/template_pins.json), bit for bit over every key's
+    (wheel, bus, level) list: detuned tunings and bus ratios away from the defaults, with
+    the default cfg, the list keys (osc_lists) and the crosstalk / floor / minimum levels
+    (osc_models).  Also times a 64-template batch against TBF_HOST_MATRIX=1."""
+    import ctypes as C
+    import os
+    import time
+    import tunebfree_amd as T
+    from orc_bind import contrib_from
+    lib = T.load_library()
+    lib.tbf_debug_contrib.restype = C.c_int
+    lib.tbf_debug_contrib.argtypes = [C.c_void_p, C.c_uint32, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.c_uint32]
+    rng = np.random.default_rng(8)
+    tet = 440.0 * 2.0 ** ((np.arange(128) - 69) / 12.0)
+    base = np.array([0.5, 1.5, 1, 2, 3, 4, 5, 6, 8])
+    n = 8
+    M = tet[None] * 2.0 ** (rng.uniform(-40, 40, (n, 128)) / 1200.0)
+    M[1] = np.sort(tet * 2.0 ** (rng.uniform(-200, 200, 128) / 1200.0))  # far off the wheels
+    R = base[None] * 2.0 ** (rng.uniform(-60, 60, (n, 9)) / 1200.0)
+    R[2] = base                                                            # exact ratios
+    R[3, 4] = R[3, 3]                                                      # two buses alike
+    seeds = [900 + i for i in range(n)]
+    for cfgname in (None, "osc_lists", "osc_models"):
+        eng = T.Engine(sample_rate=48000.0, device=0)
+        if cfgname:
+            eng.config(S.CFG_SETS[cfgname])
+        dev = eng.templates(seeds, mts128=M, ratio9=R)
+        host = [eng.template(mts128=M[i], ratio9=R[i], seed=seeds[i]) for i in range(n)]
+        for i in range(n):
+            got, want = (contrib_from(lambda kk, w, b, lv, cap, t=t: lib.tbf_debug_contrib(eng._h, t, kk, w, b, lv, cap))
+                         for t in (dev[i], host[i]))
+            assert got.tobytes() == want.tobytes(), (cfgname, i)
+        eng.close()
+    eng = T.Engine(sample_rate=48000.0, device=0)
+    eng.templates([1])  # warm: first launch, allocations
+    ms = {}
+    for mode in ("device", "host"):
+        if mode == "host":
+            os.environ["TBF_HOST_MATRIX"] = "1"
+        try:
+            t0 = time.perf_counter()
+            eng.templates([2000 + i for i in range(64)])
+            ms[mode] = (time.perf_counter() - t0) * 1e3
+        finally:
+            os.environ.pop("TBF_HOST_MATRIX", None)
+    eng.close()
+    print(f"64 templates (bank + play matrix): {ms['device']:.1f} ms with the device play matrix, "
+          f"{ms['host']:.1f} ms with the host one")
 
 
 def test_gpu_pipelined_chunks_across_calls(oracle):

@@ -561,12 +561,16 @@ int tbf_templates_create (tbf_engine* e, uint32_t n, const double* mts128, const
 	std::vector<tbf_tpl_wheel>               wh ((size_t)n * TBF_NW);
 	uint64_t                                 sum = 0;
 	uint32_t                                 maxChunks = 0, maxLen = 0;
-	/* the rand-free tables of each template (frequencies, play matrix, wheel lengths and
-	 * spectra) and its rand() window, one template per host thread */
+	/* the play matrices on the device (k_tpl_matrix) unless TBF_HOST_MATRIX=1 (A/B: the
+	 * host builder of tbf_template_create, one template per host thread) */
+	const char* hm         = getenv ("TBF_HOST_MATRIX");
+	const bool  hostMatrix = hm && atoi (hm) != 0;
+	/* the rand-free tables of each template (frequencies, wheel lengths and spectra) and
+	 * its rand() window, one template per host thread */
 	parallelFor (n, [&] (uint32_t t) {
 		ts[t].reset (new TgTemplate ());
 		ts[t]->prepare (sr, mts128 ? mts128 + 128 * (size_t)t : nullptr, ratio9 ? ratio9 + 9 * (size_t)t : nullptr,
-		                e->conf);
+		                e->conf, hostMatrix);
 		uint32_t  W[31];
 		GlibcRand rnd (seeds[t]);
 		rnd.window (W);
@@ -597,9 +601,42 @@ int tbf_templates_create (tbf_engine* e, uint32_t n, const double* mts128, const
 	DevBuf<tbf_tpl_wheel> dWh;
 	DevBuf<uint8_t>       dLsb;
 	DevBuf<float>         dBank;
+	/* play matrix: the cfg-only inputs, each template's frequencies and bus ratios */
+	MatrixInputs          mi;
+	const size_t          nk = (size_t)n * 384;
+	std::vector<double>   fr, ra;
+	DevBuf<tbf_le>        dTm, dTp, dXt;
+	DevBuf<uint32_t>      dTmOff, dTpOff, dXtOff, dCnt, dOff;
+	DevBuf<float>         dTaper;
+	DevBuf<double>        dFr, dRa;
+	DevBuf<tbf_contrib>   dStage, dOut;
+	std::vector<uint32_t> hCnt, hOff;
+	std::vector<Contrib>  hOut;
+	if (!hostMatrix) {
+		mi.build (e->conf);
+		fr.resize ((size_t)n * TBF_NW);
+		ra.resize ((size_t)n * 9);
+		for (uint32_t t = 0; t < n; t++) {
+			memcpy (&fr[(size_t)t * TBF_NW], ts[t]->frequency, TBF_NW * sizeof (double));
+			memcpy (&ra[(size_t)t * 9], ts[t]->targetRatio, 9 * sizeof (double));
+		}
+		if (dTm.ensure (mi.tm.size ()) || dTp.ensure (mi.tp.size ()) || dXt.ensure (mi.xt.size ()) ||
+		    dTmOff.ensure (mi.tmOff.size ()) || dTpOff.ensure (mi.tpOff.size ()) || dXtOff.ensure (mi.xtOff.size ()) ||
+		    dTaper.ensure (128 * 9) || dFr.ensure (fr.size ()) || dRa.ensure (ra.size ()) || dCnt.ensure (nk) ||
+		    dOff.ensure (nk + 1) || dStage.ensure (nk * mi.cap) || dOut.ensure (nk * mi.cap))
+			return fail (-12, "device play matrix buffers");
+	}
+	auto releaseAll = [&] () {
+		dE.release (), dTot.release (), dBase.release (), dWh.release (), dLsb.release (), dBank.release ();
+		dTm.release (), dTp.release (), dXt.release (), dTmOff.release (), dTpOff.release (), dXtOff.release ();
+		dTaper.release (), dFr.release (), dRa.release (), dCnt.release (), dOff.release (), dStage.release ();
+		dOut.release ();
+	};
 	if (dE.ensure (E.size ()) || dTot.ensure (n) || dBase.ensure (n) || dWh.ensure (wh.size ()) || dLsb.ensure (sum) ||
-	    dBank.ensure (sum))
+	    dBank.ensure (sum)) {
+		releaseAll ();
 		return fail (-12, "device template buffers");
+	}
 	int rc = 0;
 	std::vector<float> hb (sum);
 	do {
@@ -615,17 +652,67 @@ int tbf_templates_create (tbf_engine* e, uint32_t n, const double* mts128, const
 			rc = fail (-5, "template kernels");
 			break;
 		}
+		if (!hostMatrix) {
+			auto up = [&] (void* d, const void* h, size_t bytes) {
+				return bytes == 0 || hipMemcpyAsync (d, h, bytes, hipMemcpyHostToDevice, s) == hipSuccess;
+			};
+			if (!up (dTm.p, mi.tm.data (), mi.tm.size () * sizeof (tbf_le)) ||
+			    !up (dTp.p, mi.tp.data (), mi.tp.size () * sizeof (tbf_le)) ||
+			    !up (dXt.p, mi.xt.data (), mi.xt.size () * sizeof (tbf_le)) ||
+			    !up (dTmOff.p, mi.tmOff.data (), mi.tmOff.size () * 4) ||
+			    !up (dTpOff.p, mi.tpOff.data (), mi.tpOff.size () * 4) ||
+			    !up (dXtOff.p, mi.xtOff.data (), mi.xtOff.size () * 4) || !up (dTaper.p, mi.taper, sizeof (mi.taper)) ||
+			    !up (dFr.p, fr.data (), fr.size () * 8) || !up (dRa.p, ra.data (), ra.size () * 8)) {
+				rc = fail (-5, "play matrix upload");
+				break;
+			}
+			const tbf_tpl_mx mx = {dTm.p,    dTmOff.p,    dTp.p,       dTpOff.p,    dXt.p, dXtOff.p,
+			                       dTaper.p, mi.wiringXT, mi.floor, mi.minLevel, mi.cap};
+			hCnt.resize (nk);
+			hOff.resize (nk + 1);
+			if (tbf_tpl_matrix_launch (n, &mx, dFr.p, dRa.p, dStage.p, dCnt.p, dOff.p, dOut.p, s)) {
+				rc = fail (-5, "play matrix kernels");
+				break;
+			}
+			if (hipMemcpyAsync (hCnt.data (), dCnt.p, nk * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+			    hipMemcpyAsync (hOff.data (), dOff.p, (nk + 1) * 4, hipMemcpyDeviceToHost, s) != hipSuccess) {
+				rc = fail (-5, "play matrix download");
+				break;
+			}
+		}
 		if (hipMemcpyAsync (hb.data (), dBank.p, sum * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
 		    hipStreamSynchronize (s) != hipSuccess) {
 			rc = fail (-5, "template download");
 			break;
 		}
+		if (!hostMatrix) {
+			for (size_t q = 0; q < nk; q++)
+				if (hCnt[q] > mi.cap) {
+					rc = fail (-5, "play matrix list longer than its staging");
+					break;
+				}
+			if (rc)
+				break;
+			static_assert (sizeof (Contrib) == sizeof (tbf_contrib), "Contrib is tbf_contrib's layout");
+			hOut.resize (hOff[nk]);
+			if ((hOff[nk] && hipMemcpyAsync (hOut.data (), dOut.p, hOff[nk] * sizeof (Contrib), hipMemcpyDeviceToHost,
+			                                 s) != hipSuccess) ||
+			    hipStreamSynchronize (s) != hipSuccess) {
+				rc = fail (-5, "play matrix download");
+				break;
+			}
+		}
 	} while (0);
-	dE.release (), dTot.release (), dBase.release (), dWh.release (), dLsb.release (), dBank.release ();
+	releaseAll ();
 	if (rc)
 		return rc;
 	parallelFor (n, [&] (uint32_t t) {
 		TgTemplate& T = *ts[t];
+		if (!hostMatrix)
+			for (int k = 0; k < 384; k++) {
+				const size_t q = (size_t)t * 384 + k;
+				T.keyContrib[k].assign (hOut.begin () + hOff[q], hOut.begin () + hOff[q + 1]);
+			}
 		T.bank.assign (hb.begin () + base[t], hb.begin () + base[t] + total[t]);
 		GlibcRand rnd (seeds[t]);
 		rnd.discard (T.total); /* the draws of the bank */

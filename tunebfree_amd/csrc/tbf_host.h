@@ -117,12 +117,25 @@ struct TgTemplate {
 	size_t                            total = 0; /* bank samples = rand() draws of the bank */
 	Config                            cfg; /* the osc.* template keys it was built with */
 	void build (double sr, const double* mts128, const double* ratio9, unsigned int seed, const Config& c);
-	/* the steps of build: prepare (tables, wheel lengths and spectra), synthHost (the
-	 * bank, one draw per sample), finish (key compression, envelopes: the draws after
-	 * the bank) */
-	void prepare (double sr, const double* mts128, const double* ratio9, const Config& c);
+	/* the steps of build: prepare (tables, play matrix unless matrix is false, wheel
+	 * lengths and spectra), synthHost (the bank, one draw per sample), finish (key
+	 * compression, envelopes: the draws after the bank) */
+	void prepare (double sr, const double* mts128, const double* ratio9, const Config& c, bool matrix = true);
 	void synthHost (GlibcRand& rnd);
 	void finish (GlibcRand& rnd);
+};
+
+/* the template-independent inputs of the play matrix for the device builder (k_tpl_matrix,
+ * tbf_tpl.hip): the terminal mix of applyDefaultConfiguration (src/tonegen.cpp:933-1003),
+ * the cfg's taper and crosstalk lists per key, the manual taper levels (taper (),
+ * 502-692), and the bound on a key's list length that sizes the device staging */
+struct MatrixInputs {
+	std::vector<tbf_le>   tm, tp, xt;          /* flattened lists */
+	std::vector<uint32_t> tmOff, tpOff, xtOff; /* TBF_NW + 2, 385, 385 offsets */
+	float                 taper[128][9];
+	double                wiringXT = 0, floor = 0, minLevel = 0;
+	uint32_t              cap = 0;
+	void build (const Config& c);
 };
 
 struct WhirlTables {

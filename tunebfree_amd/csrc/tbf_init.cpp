@@ -150,12 +150,11 @@ struct Le {
 	float fc;
 };
 
-/* src/tonegen.cpp:933-1213 applyDefaultConfiguration + compilePlayMatrix, over the cfg's
- * lists (t.cfg.lists: a key / terminal with its own list keeps it and gets no default) */
-static void playMatrix (TgTemplate& t)
+/* the cfg's lists (cf.lists: a key / terminal with its own list keeps it and gets no
+ * default) and the default terminal mix (src/tonegen.cpp:949-997) */
+static void matrixLists (const Config& cf, std::vector<Le>* terminalMix, std::vector<Le>* keyTaper,
+                         std::vector<Le>* keyCrosstalk)
 {
-	const Config&   cf = t.cfg;
-	std::vector<Le> terminalMix[TBF_NW + 1], keyTaper[384], keyCrosstalk[384];
 	for (const Config::ListEntry& e : cf.lists) {
 		if (e.kind == LE_TERMINAL)
 			terminalMix[e.idx].push_back ({e.sa, 0, e.fc});
@@ -189,6 +188,46 @@ static void playMatrix (TgTemplate& t)
 				}
 			}
 		}
+}
+
+void MatrixInputs::build (const Config& cf)
+{
+	std::vector<Le> terminalMix[TBF_NW + 1], keyTaper[384], keyCrosstalk[384];
+	matrixLists (cf, terminalMix, keyTaper, keyCrosstalk);
+	auto flat = [] (const std::vector<Le>* lists, int n, std::vector<tbf_le>& v, std::vector<uint32_t>& off) {
+		v.clear ();
+		off.assign (1, 0u);
+		size_t longest = 0;
+		for (int i = 0; i < n; i++) {
+			for (const Le& e : lists[i])
+				v.push_back ({e.sa, e.sb, e.fc});
+			off.push_back ((uint32_t)v.size ());
+			longest = std::max (longest, lists[i].size ());
+		}
+		return longest;
+	};
+	const size_t M = flat (terminalMix, TBF_NW + 1, tm, tmOff);
+	tmOff.push_back (tmOff.back ()); /* terminal TBF_NW + 1: none */
+	/* a key's events: its taper list (<= 9 defaults) and crosstalk list (<= 9 per taper
+	 * element by default), each element times its terminal's mix; cells <= wheels x buses */
+	const size_t T = std::max<size_t> (9, flat (keyTaper, 384, tp, tpOff));
+	const size_t X = std::max<size_t> (9 * T, flat (keyCrosstalk, 384, xt, xtOff));
+	cap            = (uint32_t)std::max<size_t> (1, std::min<size_t> ((size_t)TBF_NW * 27, (T + X) * M));
+	for (int k = 0; k < 128; k++)
+		for (int b = 0; b < 9; b++)
+			taper[k][b] = (float)tbf::taper (k, b);
+	wiringXT = cf.wiringXT;
+	floor    = cf.contribFloor;
+	minLevel = cf.contribMin;
+}
+
+/* src/tonegen.cpp:933-1213 applyDefaultConfiguration + compilePlayMatrix (the device
+ * builder k_tpl_matrix, tbf_tpl.hip, restates the same steps per key) */
+static void playMatrix (TgTemplate& t)
+{
+	const Config&   cf = t.cfg;
+	std::vector<Le> terminalMix[TBF_NW + 1], keyTaper[384], keyCrosstalk[384];
+	matrixLists (cf, terminalMix, keyTaper, keyCrosstalk);
 	/* applyManualDefaults (707-802) */
 	double of[TBF_NW + 1];
 	for (int i = 1; i <= TBF_NW; i++)
@@ -329,7 +368,7 @@ void TgTemplate::build (double rate, const double* mts128, const double* ratio9,
 	finish (rnd);
 }
 
-void TgTemplate::prepare (double rate, const double* mts128, const double* ratio9, const Config& c)
+void TgTemplate::prepare (double rate, const double* mts128, const double* ratio9, const Config& c, bool matrix)
 {
 	static const double defaultRatio[9] = {0.5, 1.5, 1, 2, 3, 4, 5, 6, 8};
 	sr     = rate;
@@ -344,7 +383,8 @@ void TgTemplate::prepare (double rate, const double* mts128, const double* ratio
 		targetRatio[i] = ratio9 ? ratio9[i] : defaultRatio[i];
 	for (auto& v : keyContrib)
 		v.clear ();
-	playMatrix (*this);
+	if (matrix)
+		playMatrix (*this);
 
 	/* initOscillators (1470-1630): wheel EQ (apply_CH_Spline 1240-1261 or the legacy
 	 * peak24 / peak46 damper curves 1223-1311), fitWave, the harmonics list (compile-time

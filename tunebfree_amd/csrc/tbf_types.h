@@ -93,6 +93,13 @@ typedef struct tbf_contrib {
 	float    level;
 } tbf_contrib;
 
+/* one element of a play-matrix list (struct _list_element, src/tonegen.cpp:444-450):
+ * terminal | wheel, bus, level -- the inputs of the device builder k_tpl_matrix */
+typedef struct tbf_le {
+	int16_t sa, sb;
+	float   fc;
+} tbf_le;
+
 /* per instance device control state (the runtime fields of struct b_tonegen that the
  * per-wheel control touches); aclPos1 = aclPos + 1 so that zeroed memory is the initial
  * state (no wheel in the list) */

@@ -46,6 +46,9 @@
 #ifndef WH_RG
 #define WH_RG 2 /* k_whirl rings per motion group (4 or 2) */
 #endif
+#ifndef WH_SERIAL_PIPE
+#define WH_SERIAL_PIPE 1 /* k_whirl serial passes: next group's reads ahead of this group's chain */
+#endif
 #ifndef WH_PAD
 #define WH_PAD 1 /* floats after each LDS ring / horn-A row: rows of one serial pass on different banks */
 #endif
@@ -616,15 +619,20 @@ k_tonegen (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl, const tbf_tp
  * it - 2, the waveshaper of tile it - 3; one barrier per iteration.  Every chain runs the
  * reference's operations in its order.  Tonegen-only chains (configs[1]) stop after the
  * products, which are then the output. */
+#ifndef MP_CB
 #define MP_CB 32                  /* instances per workgroup */
+#endif
 #define MP_T 32                   /* samples per tile: one per lane of a half-wave */
 #define MP_S (MP_T + 1)           /* row stride of the per-sample rows (odd: conflict-free columns) */
 #define MP_HS (MP_T / 2 + 1)      /* row stride of the high-pass rows (a chain's MP_T / 2 samples) */
+#ifndef MP_H
 #define MP_H 8                    /* helper waves */
+#endif
 #define MP_NTK (MP_CB / 2 / MP_H) /* helper tasks (instance pairs) per tile */
 #define MP_THREADS (NL * (2 + MP_H))
 #define MP_TPB (TBF_BLK / MP_T)   /* tiles per block */
-static_assert (2 * MP_CB == NL && 2 * MP_T == NL && MP_CB % (2 * MP_H) == 0, "k_mixpre geometry");
+static_assert (2 * MP_CB <= NL && 2 * MP_T == NL && MP_CB % (2 * MP_H) == 0, "k_mixpre geometry");
+#define MP_ROWS (2 * MP_CB + (2 * MP_CB < NL)) /* chain rows, + one that idle chain lanes write */
 
 /* one block's control of an instance as k_mixpre uses it, staged in LDS by the dither wave
  * a block ahead (so no global load sits on an iteration's path) */
@@ -659,11 +667,11 @@ __device__ __forceinline__ MpCtl mp_ctl (const tbf_seg_ctl& G)
 }
 
 struct MixPreLds {
-	float    g[2][2 * MP_CB][MP_S];  /* chase values before each sample, by tile parity: row 2j
+	float    g[2][MP_ROWS][MP_S];    /* chase values before each sample, by tile parity: row 2j
 	                                  * keyCompLevel, 2j + 1 percEnvGain of instance j */
-	double   x[4][2 * MP_CB][MP_HS]; /* preamp input (guarded), by tile mod 4: row 2j + q holds the
+	double   x[4][MP_ROWS][MP_HS];   /* preamp input (guarded), by tile mod 4: row 2j + q holds the
 	                                  * samples of instance j's high-pass chain q */
-	double   h[2][2 * MP_CB][MP_HS]; /* high-pass output, same rows, by tile parity */
+	double   h[2][MP_ROWS][MP_HS];   /* high-pass output, same rows, by tile parity */
 	uint32_t f[4][MP_CB][MP_S];      /* fpd before each sample (entry MP_T: after the tile), by tile mod 4 */
 	MpCtl    c[2][MP_CB];            /* the control of block b in slot b & 1 */
 };
@@ -712,8 +720,9 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 	if (!pre && __all (lane >= nj || P.mixFixed[inst0 + (lane < nj ? lane : 0)]))
 		return;
 	if (w == 0) {
-		const int      j = lane >> 1, q = lane & 1;
-		const bool     ok   = j < nj;
+		const int      cl = min (lane, MP_ROWS - 1); /* chain row (lanes past 2 MP_CB: the idle row) */
+		const int      j = min (lane >> 1, MP_CB - 1), q = lane & 1;
+		const bool     ok   = lane < 2 * MP_CB && j < nj;
 		tbf_mo_state*  M    = &P.st[inst0 + (ok ? j : 0)].mo;
 		float          v    = q ? M->percEnvGain : M->keyCompLevel;
 		double         iir  = q ? M->iirB : M->iirA;
@@ -733,7 +742,7 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 					rs  = q && (C.flags & MPF_RST);
 					rsv = C.reset;
 				}
-				float* row = sm.g[it & 1][lane];
+				float* row = sm.g[it & 1][cl];
 				if (__all ((v * m) + a == v)) { /* a fixed point on every lane (no percussion, the key
 				                                  * compression settled): the whole tile is v */
 #pragma unroll 8
@@ -765,8 +774,8 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 					ia             = C.iir;
 				}
 				if (hp) {
-					const double* xr = sm.x[th & 3][lane];
-					double*       hr = sm.h[th & 1][lane];
+					const double* xr = sm.x[th & 3][cl];
+					double*       hr = sm.h[th & 1][cl];
 					const double  om = 1.0 - ia;
 					PRIO_UP ();
 #pragma unroll
@@ -2333,6 +2342,42 @@ __device__ __forceinline__ void wh_serial (float* r, uint32_t base, uint32_t m, 
 		if (isnan (z1))
 			z1 = 0.f;
 	}
+#if WH_SERIAL_PIPE
+	/* two register sets of eight: the next group's reads are in flight while this group's
+	 * recurrence runs (the groups' elements are distinct, so no read passes a write of its
+	 * own element) */
+	auto ld = [&] (float (&v)[8], int i0) {
+#pragma unroll
+		for (int k = 0; k < 8; k++)
+			v[k] = WRAP ? r[(base + (uint32_t)(i0 + k)) & m] : r[i0 + k];
+	};
+	auto run = [&] (float (&v)[8], int i0) {
+#pragma unroll
+		for (int k = 0; k < 8; k++) {
+			const float t = v[k] - (a1 * z0) - (a2 * z1);
+			z1            = z0;
+			z0            = t;
+			v[k]          = t;
+		}
+#pragma unroll
+		for (int k = 0; k < 8; k++) {
+			if (WRAP)
+				r[(base + (uint32_t)(i0 + k)) & m] = v[k];
+			else
+				r[i0 + k] = v[k];
+		}
+	};
+	float xa[8], xb[8];
+	ld (xa, 0);
+#pragma unroll
+	for (int i0 = 0; i0 < TBF_SUB; i0 += 16) {
+		ld (xb, i0 + 8);
+		run (xa, i0);
+		if (i0 + 16 < TBF_SUB)
+			ld (xa, i0 + 16);
+		run (xb, i0 + 8);
+	}
+#else
 	for (int i0 = 0; i0 < TBF_SUB; i0 += 8) {
 		float xv[8];
 #pragma unroll
@@ -2353,6 +2398,7 @@ __device__ __forceinline__ void wh_serial (float* r, uint32_t base, uint32_t m, 
 				r[i0 + k] = xv[k];
 		}
 	}
+#endif
 	fz[0] = z0;
 	fz[1] = z1;
 }

@@ -246,6 +246,10 @@ int tbf_debug_device_program (tbf_engine* e, uint32_t inst, float* entries9, uin
  * (events, message queues, active lists, routing, per-block programmes) since the last
  * reset, and the blocks it covered */
 int tbf_debug_host_time (tbf_engine* e, int32_t reset, double* ms, uint64_t* blocks);
+/* self-check of the host worker pool the control plane's parallel sections run on: jobs
+ * of 1..40 tasks back to back (jobs of them), each task counted; returns the number of
+ * jobs in which a task ran other than exactly once (0: all good) */
+int tbf_debug_pool_check (uint32_t jobs);
 /* the cfg-derived HBM layout: the compact whirl ring window (512 / 1024 / 2048 samples
  * per ring, from the geometry's largest write-ahead) and the reverb slab length */
 int tbf_debug_layout (const tbf_engine* e, uint32_t* wring_len, float* max_ahead, uint32_t* slab_len);

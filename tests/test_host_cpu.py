@@ -567,3 +567,23 @@ def test_drawbar_setting_out_of_range_ignored():
     moved = [_engine_program(lib, eng, 0, False) for _ in range(3)][-1]
     assert not np.array_equal(before.view(np.uint32), moved.view(np.uint32))
     eng.close()
+
+
+def test_host_pool_runs_every_task_once():
+    """The host worker pool (HostPool, csrc/tbf_engine.cpp) behind the control plane's
+    parallel sections: a job ends when its tasks are done, and a worker woken late must
+    find that job's tasks taken rather than run a later job's twice.  20000 jobs of 1..40
+    tasks back to back, every task counted (tbf_debug_pool_check), with the pool at 16
+    threads."""
+    import os
+    import subprocess
+    import sys
+    code = ("import ctypes as C, tunebfree_amd as T; lib = T.load_library(); "
+            "lib.tbf_debug_pool_check.restype = C.c_int; lib.tbf_debug_pool_check.argtypes = [C.c_uint32]; "
+            "print(lib.tbf_debug_pool_check(20000))")
+    env = dict(os.environ, TBF_HOST_THREADS="16")
+    out = subprocess.run([sys.executable, "-c", code], env=env, cwd=str(ROOT), capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.strip().splitlines()[-1] == "0"
+

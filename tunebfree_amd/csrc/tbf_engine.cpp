@@ -277,8 +277,10 @@ static unsigned hostThreads ()
 }
 
 /* A persistent pool of hostThreads () - 1 workers (the caller is the last): a dense-event
- * chunk runs two parallel sections, and creating 16 threads for each cost ~0.3-0.8 ms.
- * One job at a time (the mutex), so engines driven from several host threads share it. */
+ * chunk runs several parallel sections, and creating 16 threads for each cost ~0.3-0.8 ms.
+ * One job at a time (the mutex), so engines driven from several host threads share it.
+ * A job ends when its tasks are done, not when every worker has woken: each job is its own
+ * object, so a worker the OS schedules late finds that job's tasks taken and leaves it. */
 class HostPool {
   public:
 	static HostPool& get ()
@@ -289,23 +291,28 @@ class HostPool {
 	void run (uint32_t n, const std::function<void (uint32_t)>& f)
 	{
 		std::lock_guard<std::mutex> job (jobM);
+		auto                        j = std::make_shared<Job> ();
+		j->fn                         = &f;
+		j->cnt                        = n;
 		{
 			std::lock_guard<std::mutex> g (m);
-			fn = &f;
-			cnt = n;
-			next.store (0);
-			busy = (int)th.size ();
+			cur = j;
 			gen++;
 		}
 		cv.notify_all ();
-		work ();
+		work (*j);
 		std::unique_lock<std::mutex> g (m);
-		done.wait (g, [&] { return busy == 0; });
-		fn = nullptr;
+		done.wait (g, [&] { return j->finished.load () == n; });
+		cur.reset ();
 	}
 	unsigned workers () const { return (unsigned)th.size () + 1; }
 
   private:
+	struct Job {
+		const std::function<void (uint32_t)>* fn  = nullptr;
+		uint32_t                              cnt = 0;
+		std::atomic<uint32_t>                 next {0}, finished {0};
+	};
 	HostPool ()
 	{
 		const unsigned nt = hostThreads ();
@@ -322,37 +329,39 @@ class HostPool {
 		for (auto& t : th)
 			t.join ();
 	}
-	void work ()
+	void work (Job& j)
 	{
-		for (uint32_t t; (t = next.fetch_add (1)) < cnt;)
-			(*fn) (t);
+		for (uint32_t t; (t = j.next.fetch_add (1)) < j.cnt;) {
+			(*j.fn) (t);
+			if (j.finished.fetch_add (1) + 1 == j.cnt) {
+				std::lock_guard<std::mutex> g (m);
+				done.notify_all ();
+			}
+		}
 	}
 	void loop ()
 	{
 		uint64_t seen = 0;
 		for (;;) {
+			std::shared_ptr<Job> j;
 			{
 				std::unique_lock<std::mutex> g (m);
 				cv.wait (g, [&] { return quit || gen != seen; });
 				if (quit)
 					return;
 				seen = gen;
+				j    = cur;
 			}
-			work ();
-			std::lock_guard<std::mutex> g (m);
-			if (--busy == 0)
-				done.notify_one ();
+			if (j)
+				work (*j);
 		}
 	}
-	std::vector<std::thread>             th;
-	std::mutex                           m, jobM;
-	std::condition_variable              cv, done;
-	const std::function<void (uint32_t)>* fn = nullptr;
-	uint32_t                             cnt = 0;
-	std::atomic<uint32_t>                next {0};
-	int                                  busy = 0;
-	uint64_t                             gen  = 0;
-	bool                                 quit = false;
+	std::vector<std::thread> th;
+	std::mutex               m, jobM;
+	std::condition_variable  cv, done;
+	std::shared_ptr<Job>     cur;
+	uint64_t                 gen  = 0;
+	bool                     quit = false;
 };
 
 /* run f(t) for t < n on up to hostThreads () threads */
@@ -1590,11 +1599,9 @@ static bool frontClean (const Instance& in)
 /* a parameter event the device front end steps (drawbars, the vibrato and percussion
  * switches: they change only what a control record carries), as a TBF_FEV_* word without
  * the block; 0 for any other */
-static uint32_t frontParam (const tbf_event& E)
+static uint32_t frontParam (int32_t idx, float v)
 {
-	const int32_t idx = E.id;
-	const float   v   = (float)E.value;
-	int           bus = -1;
+	int bus = -1;
 	if (idx >= TBF_P_DRAWBAR_MIN && idx <= TBF_P_DRAWBAR_MAX)
 		bus = idx;
 	else if (idx >= TBF_P_BUS_DRAWBAR_BASE && idx < TBF_P_BUS_DRAWBAR_BASE + 27)
@@ -1612,46 +1619,77 @@ static uint32_t frontParam (const tbf_event& E)
 		default: return 0;
 	}
 }
+static uint32_t frontParam (const tbf_event& E) { return frontParam (E.id, (float)E.value); }
 
-static bool frontEligible (tbf_engine* e, const tbf_event* ev, uint32_t evBeg, uint32_t evEnd)
+/* the instances' front-end cleanliness (e->fclean), once per chunk; false when an active
+ * instance is not clean (its pending step is the host's) */
+static bool frontCleanAll (tbf_engine* e)
 {
-	/* per instance once (an event list visits every instance's host state many times) */
 	const uint32_t        n  = (uint32_t)e->inst.size ();
 	std::vector<uint8_t>& cl = e->fclean;
 	cl.resize (n);
-	{
-		const unsigned T   = std::max (1u, std::min<unsigned> (hostThreads (), (n + 255) / 256));
-		const uint32_t per = (n + T - 1) / T;
-		parallelFor (T, [&] (uint32_t t) {
-			for (uint32_t i = t * per; i < std::min (n, (t + 1) * per); i++)
-				cl[i] = frontClean (e->inst[i]) ? 1 : 0;
-		});
-	}
+	const unsigned T   = std::max (1u, std::min<unsigned> (hostThreads (), (n + 255) / 256));
+	const uint32_t per = (n + T - 1) / T;
+	parallelFor (T, [&] (uint32_t t) {
+		for (uint32_t i = t * per; i < std::min (n, (t + 1) * per); i++)
+			cl[i] = frontClean (e->inst[i]) ? 1 : 0;
+	});
 	for (uint32_t i : e->actList)
 		if (!cl[i])
-			return false;
-	const unsigned    T   = std::max (1u, std::min (hostThreads (), (evEnd - evBeg + 32767) / 32768));
-	const uint32_t    nev = evEnd - evBeg, seg = (nev + T - 1) / T;
-	std::vector<char> ok (T, 1);
-	parallelFor (T, [&] (uint32_t t) {
-		const uint32_t k0 = evBeg + std::min (nev, t * seg), k1 = evBeg + std::min (nev, (t + 1) * seg);
-		for (uint32_t k = k0; k < k1; k++)
-			if ((ev[k].kind != TBF_EV_NOTE && !(ev[k].kind == TBF_EV_PARAM && frontParam (ev[k]))) || !cl[ev[k].inst]) {
-				ok[t] = 0;
-				return;
-			}
-	});
-	for (char c : ok)
-		if (!c)
 			return false;
 	return true;
 }
 
-static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0, const tbf_event* ev, uint32_t evBeg,
-                           uint32_t evEnd, bool& delta)
+/* One parallel pass over a chunk's events (sorted by block): a programme event among them,
+ * an event for a bad instance, and -- with cl, the instances' cleanliness -- whether the
+ * device front end takes them all (notes and frontParam kinds on clean instances), with
+ * the per-segment counts of stepChunkFront's partition by instance range.  (Three passes
+ * over the 24-B events used to do this: ~0.2 ms each at 524 k events.) */
+static void scanChunk (uint32_t n, const tbf_event* ev, uint32_t evBeg, uint32_t evEnd, const uint8_t* cl, bool& progEv,
+                       bool& bad, bool& front, ChunkScan& cs)
 {
-	const unsigned T   = std::max (1u, std::min<unsigned> (hostThreads (), (n + 255) / 256));
-	const uint32_t per = (n + T - 1) / T;
+	const uint32_t nev = evEnd - evBeg;
+	cs.T   = std::max (1u, std::min<unsigned> (hostThreads (), (n + 255) / 256));
+	cs.per = (n + cs.T - 1) / cs.T;
+	cs.Te  = std::max (1u, std::min (hostThreads (), (nev + 32767) / 32768));
+	cs.seg = (nev + cs.Te - 1) / cs.Te;
+	cs.cnt.assign (cl ? (size_t)cs.Te * cs.T : 0, 0u);
+	std::vector<char> pe (cs.Te, 0), bd (cs.Te, 0), fr (cs.Te, 0);
+	parallelFor (cs.Te, [&] (uint32_t sgm) {
+		const uint32_t k0 = evBeg + std::min (nev, sgm * cs.seg), k1 = evBeg + std::min (nev, (sgm + 1) * cs.seg);
+		bool           p = false, b = false, f = cl != nullptr; /* locals: the flags share a cache line */
+		uint32_t*      c = f ? cs.cnt.data () + (size_t)sgm * cs.T : nullptr;
+		for (uint32_t k = k0; k < k1; k++) {
+			const tbf_event& E = ev[k];
+			p                  = p || E.kind == TBF_EV_PROGRAM;
+			if (E.inst >= n) {
+				b = true;
+				f = false;
+				continue;
+			}
+			if (f) {
+				f = (E.kind == TBF_EV_NOTE || (E.kind == TBF_EV_PARAM && frontParam (E))) && cl[E.inst];
+				c[E.inst / cs.per]++;
+			}
+		}
+		pe[sgm] = p;
+		bd[sgm] = b;
+		fr[sgm] = f;
+	});
+	progEv = bad = false;
+	front        = cl != nullptr;
+	for (unsigned t = 0; t < cs.Te; t++) {
+		progEv = progEv || pe[t];
+		bad    = bad || bd[t];
+		front  = front && fr[t];
+	}
+}
+
+static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0, const tbf_event* ev, uint32_t evBeg,
+                           uint32_t evEnd, ChunkScan& cs, bool& delta)
+{
+	const unsigned T   = cs.T;
+	const uint32_t per = cs.per;
 	auto&          out = e->parStep;
 	const auto     f0  = std::chrono::steady_clock::now ();
 	out.resize (T);
@@ -1661,24 +1699,20 @@ static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0
 		o.evs.clear ();
 		o.gainLocal = 0;
 	}
-	{ /* the events by instance range, in order (a parallel counting partition) */
-		const uint32_t        nev = evEnd - evBeg, seg = (nev + T - 1) / T;
-		std::vector<uint32_t> cnt ((size_t)T * T, 0);
-		parallelFor (T, [&] (uint32_t sgm) {
-			const uint32_t k0 = evBeg + std::min (nev, sgm * seg), k1 = evBeg + std::min (nev, (sgm + 1) * seg);
-			for (uint32_t k = k0; k < k1; k++)
-				cnt[(size_t)sgm * T + ev[k].inst / per]++;
-		});
+	{ /* the events by instance range, in order (a parallel counting partition; the counts
+	   * per event segment come from scanChunk) */
+		const uint32_t         nev = evEnd - evBeg, seg = cs.seg;
+		std::vector<uint32_t>& cnt = cs.cnt;
 		for (unsigned t = 0; t < T; t++) {
 			uint32_t tot = 0;
-			for (unsigned sgm = 0; sgm < T; sgm++) {
+			for (unsigned sgm = 0; sgm < cs.Te; sgm++) {
 				const uint32_t c         = cnt[(size_t)sgm * T + t];
 				cnt[(size_t)sgm * T + t] = tot;
 				tot += c;
 			}
 			out[t].evs.resize (tot);
 		}
-		parallelFor (T, [&] (uint32_t sgm) {
+		parallelFor (cs.Te, [&] (uint32_t sgm) {
 			const uint32_t k0 = evBeg + std::min (nev, sgm * seg), k1 = evBeg + std::min (nev, (sgm + 1) * seg);
 			uint32_t*      at = cnt.data () + (size_t)sgm * T;
 			for (uint32_t k = k0; k < k1; k++) {
@@ -1694,23 +1728,31 @@ static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0
 	e->hFevOff.resize (n + 1);
 	e->hFev.resize (std::max<uint32_t> (wbase[T], 1));
 	e->hFront.resize (n);
+	const bool          dbgPh = getenv ("TBF_DEBUG_HOST_PHASES") != nullptr;
+	std::vector<double> thMs (dbgPh ? 3 * T : 0);
 	parallelFor (T, [&] (uint32_t t) {
+		const auto             g0 = std::chrono::steady_clock::now ();
 		tbf_engine::ParStep&   o  = out[t];
 		const uint32_t         i0 = t * per, i1 = std::min (n, i0 + per);
 		std::vector<uint32_t>& eo = o.eoff;
-		std::vector<uint32_t>& es = o.esort;
+		auto&                  es = o.erec;
 		eo.assign ((size_t)(i1 > i0 ? i1 - i0 : 0) + 1, 0);
 		for (uint32_t k : o.evs)
 			eo[ev[k].inst - i0 + 1]++;
 		for (uint32_t i = i0; i < i1; i++)
 			eo[i - i0 + 1] += eo[i - i0];
 		es.resize (o.evs.size ());
-		{
+		{ /* the events by instance as compact records (written while the range's events
+		   * are read in order, so the per-instance pass below reads them sequentially) */
 			std::vector<uint32_t>& fill = o.efill;
 			fill.assign (eo.begin (), eo.end () - 1);
-			for (uint32_t k : o.evs)
-				es[fill[ev[k].inst - i0]++] = k;
+			for (uint32_t k : o.evs) {
+				const tbf_event& E            = ev[k];
+				es[fill[E.inst - i0]++] = {E.block - b0, E.id, (float)E.value,
+				                           (E.kind == TBF_EV_PARAM ? 1u : 0u) | (E.value != 0.0 ? 2u : 0u)};
+			}
 		}
+		const auto g1 = std::chrono::steady_clock::now ();
 		for (uint32_t i = i0; i < i1; i++) {
 			Instance&        in = e->inst[i];
 			TgControl&       tg = in.tg;
@@ -1748,8 +1790,8 @@ static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0
                 msgsB            = 0;
 			};
 			for (uint32_t j = eo[i - i0]; j < eo[i - i0 + 1]; j++) {
-				const tbf_event& E   = ev[es[j]];
-				const uint32_t   blk = E.block - b0;
+				const auto&    E   = es[j];
+				const uint32_t blk = E.blk;
 				if ((int)blk != curB) {
 					if (curB >= 0)
 						closeBlock ();
@@ -1757,10 +1799,10 @@ static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0
 						pend = false; /* blocks without events between: the pending step is done */
 					curB = (int)blk;
 				}
-				if (E.kind == TBF_EV_PARAM) {
-					const uint32_t w = frontParam (E);
+				if (E.flag & 1u) {
+					const float    v = E.v;
+					const uint32_t w = frontParam (E.id, v);
 					e->hFev[wbase[t] + j] = w | (blk << 16);
-					const float v = (float)E.value;
 					if (E.id >= 0 && E.id < 64)
 						in.params[E.id] = v;
 					const uint32_t op = (w >> 12) & 7u;
@@ -1776,7 +1818,7 @@ static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0
 						tg.setPercFirst ((int)rint (v));
 					continue;
 				}
-				const bool on = E.value != 0.0;
+				const bool on = (E.flag & 2u) != 0;
 				const bool ok = E.id >= 0 && E.id < 384; /* oscKeyOn/Off ignore keys >= MAX_KEYS */
 				e->hFev[wbase[t] + j] = (ok ? (uint32_t)E.id : 0x0fffu) | (on ? 1u << 12 : 0u) | (blk << 16);
 				msgsB += ok ? (uint32_t)tg.noteCount (E.id, on) : 0u;
@@ -1804,6 +1846,12 @@ static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0
 			if (e->inAct[i])
 				o.act.push_back (i);
 		}
+		if (dbgPh) {
+			const auto g2 = std::chrono::steady_clock::now ();
+			thMs[3 * t]     = std::chrono::duration<double, std::milli> (g0 - f1).count (); /* start delay */
+			thMs[3 * t + 1] = std::chrono::duration<double, std::milli> (g1 - g0).count (); /* sort */
+			thMs[3 * t + 2] = std::chrono::duration<double, std::milli> (g2 - g1).count (); /* mirror */
+		}
 	});
 	e->hFevOff[n] = wbase[T];
 	{ /* the gain-pair slots: each range's base */
@@ -1827,6 +1875,14 @@ static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0
 		auto ms = [] (auto a, auto b) { return std::chrono::duration<double, std::milli> (b - a).count (); };
 		fprintf (stderr, "stepChunkFront T=%u: partition %.3f ms, instances %.3f ms\n", T, ms (f0, f1),
 		         ms (f1, std::chrono::steady_clock::now ()));
+		double mx[3] = {0, 0, 0}, sm[3] = {0, 0, 0};
+		for (unsigned t = 0; t < T; t++)
+			for (int q = 0; q < 3; q++) {
+				mx[q] = std::max (mx[q], thMs[3 * t + q]);
+				sm[q] += thMs[3 * t + q] / T;
+			}
+		fprintf (stderr, "  threads (mean / max ms): start %.3f / %.3f, sort %.3f / %.3f, mirror %.3f / %.3f\n", sm[0], mx[0],
+		         sm[1], mx[1], sm[2], mx[2]);
 	}
 	return 0;
 }
@@ -2077,32 +2133,17 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			}
 			evEnd = lo;
 		}
-		bool progEv = false;
-		{
-			const uint32_t    ne = evEnd - evi;
-			const unsigned    T  = std::max (1u, std::min (hostThreads (), (ne + 32767) / 32768));
-			const uint32_t    sg = (ne + T - 1) / T;
-			std::vector<char> pe (T, 0), bad (T, 0);
-			parallelFor (T, [&] (uint32_t t) {
-				const uint32_t k0 = evi + std::min (ne, t * sg), k1 = evi + std::min (ne, (t + 1) * sg);
-				bool           p = false, b = false; /* locals: the flags share a cache line */
-				for (uint32_t k = k0; k < k1; k++) {
-					p = p || ev[k].kind == TBF_EV_PROGRAM;
-					b = b || ev[k].inst >= n;
-				}
-				pe[t]  = p;
-				bad[t] = b;
-			});
-			for (unsigned t = 0; t < T; t++) {
-				if (bad[t])
-					return fail (-22, "event for a bad instance");
-				progEv = progEv || pe[t];
-			}
-		}
-		/* a chunk of note, drawbar and switch events only (frontParam): the device front end */
+		/* a chunk of note, drawbar and switch events only (frontParam) on clean instances: the
+		 * device front end */
+		bool       progEv = false, badEv = false, front = false;
+		const bool frontCand = e->devCtl && dpipe && e->frontOn && evEnd - evi >= 1024 && frontCleanAll (e);
+		ChunkScan& cs        = e->scan;
+		scanChunk (n, ev, evi, evEnd, frontCand ? e->fclean.data () : nullptr, progEv, badEv, front, cs);
+		if (badEv)
+			return fail (-22, "event for a bad instance");
 		bool dfront = false;
-		if (e->devCtl && dpipe && e->frontOn && !progEv && evEnd - evi >= 1024 && frontEligible (e, ev, evi, evEnd)) {
-			if ((rc = stepChunkFront (e, n, want, b0, ev, evi, evEnd, delta)))
+		if (frontCand && front && !progEv) {
+			if ((rc = stepChunkFront (e, n, want, b0, ev, evi, evEnd, cs, delta)))
 				return rc;
 			evi    = evEnd;
 			len    = want;
@@ -2583,6 +2624,27 @@ int tbf_debug_device_program (tbf_engine* e, uint32_t i, float* out, uint32_t ca
 		o[3] = p.sg; o[4] = p.pg; o[5] = p.vg; o[6] = p.nsg; o[7] = p.npg; o[8] = p.nvg;
 	}
 	return (int)np;
+}
+
+int tbf_debug_pool_check (uint32_t jobs)
+{
+	std::vector<std::atomic<int>> hits (64);
+	int                           bad = 0;
+	for (uint32_t it = 0; it < jobs; it++) {
+		const uint32_t n = 1 + (it * 7919u) % 40;
+		for (auto& h : hits)
+			h.store (0);
+		parallelFor (n, [&] (uint32_t t) {
+			hits[t].fetch_add (1);
+			if ((t & 7) == 0)
+				std::this_thread::yield ();
+		});
+		bool ok = true;
+		for (uint32_t i = 0; i < 64; i++)
+			ok = ok && hits[i].load () == (i < n ? 1 : 0);
+		bad += ok ? 0 : 1;
+	}
+	return bad;
 }
 
 int tbf_debug_host_time (tbf_engine* e, int32_t reset, double* ms, uint64_t* blocks)

@@ -140,6 +140,14 @@ struct PinnedVec {
 	}
 };
 
+/* a chunk's event scan (scanChunk, csrc/tbf_engine.cpp): instance ranges and event
+ * segments of the device front end's partition, with the per-segment counts */
+struct ChunkScan {
+	unsigned              T = 1, Te = 1; /* instance ranges, event segments */
+	uint32_t              per = 1, seg = 0;
+	std::vector<uint32_t> cnt; /* [Te][T] */
+};
+
 template <typename T>
 struct DevBuf {
 	T*     p   = nullptr;
@@ -232,6 +240,7 @@ struct tbf_engine {
 	DevBuf<uint32_t>                        dident;     /* 0 .. n-1: k_tgctl's grid over every instance */
 	std::vector<uint32_t>                   hIdent;
 	std::vector<uint8_t>                    fclean; /* per instance: no control change pending but notes */
+	ChunkScan                               scan;   /* the chunk's event scan (scanChunk) */
 	/* the other parity of the chunk staging (the previous chunk's, in flight), and the
 	 * events after each parity's uploads */
 	PinnedVec<tbf_seg_ctl>                  dCtlB, hCtlPin, hCtlPinB;
@@ -256,6 +265,14 @@ struct tbf_engine {
 		std::vector<float>    gains;
 		std::vector<tbf_wh_params> whs;
 		std::vector<uint32_t> act, ctlInst, evs, dInst, eoff, esort, efill;
+		/* a front-end chunk's events of the range, by instance: what the mirror pass reads */
+		struct FrontRec {
+			uint32_t blk;  /* block in the chunk */
+			int32_t  id;   /* key / parameter index */
+			float    v;    /* (float) value */
+			uint32_t flag; /* 1: parameter event, 2: value != 0 */
+		};
+		std::vector<FrontRec> erec;
 		std::vector<tbf_seg_ctl> fulls;
 		uint32_t              nd = 0;
 		uint32_t              gainLocal = 0; /* device front end: the range's gain-pair floats */

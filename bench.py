@@ -5,7 +5,7 @@ per GPU (configs[2] at N=1; configs[3] = 8 x 4096 at N=8, weak scaling), with
 max|err| vs the CPU chain.
 
 A "step" is one render call over the batch: every instance renders `--blocks`
-128-sample blocks (default 1024 = 131072 stereo samples, 2.73 s of audio, per instance: one
+128-sample blocks (default 2048 = 262144 stereo samples, 5.46 s of audio, per instance: one
 steady chunk of the engine, i.e. one launch of each of the six stages).  Inputs are
 synthetic: instance i plays the "Jazz 1 all" registration (pgm/default.pgm:27-36)
 with overdrive character 0.5, reverb 0.1, rotary chorale, chord root 48+(i mod 24)
@@ -49,8 +49,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=4096, help="instances per GPU")
-    ap.add_argument("--blocks", type=int, default=1024,
-                    help="128-sample blocks per step (one render call; a steady chunk is up to 1024 blocks)")
+    ap.add_argument("--blocks", type=int, default=2048,
+                    help="128-sample blocks per step (one render call; a steady chunk is up to 2048 blocks)")
     ap.add_argument("--sr", type=float, default=None, help="sample rate (default 48000; 96000 for cfg5)")
     ap.add_argument("--workload", choices=("cfg3", "cfg2", "cfg5"), default="cfg3",
                     help="cfg3: BASELINE configs[2]/[3] (the metric's workload); cfg2: configs[1] (tonegen only, "
@@ -357,7 +357,7 @@ def main():
 
     kern, kern_iso, max_err, exact, per_stage = {}, None, None, None, None
     # launch sets per step: the timed steps have no control deltas, so each chunk is up to the
-    # engine's steady chunk (TBF_STEADY_CHUNK, default TBF_STEADY_MAX = 1024 blocks; 64 with deltas)
+    # engine's steady chunk (TBF_STEADY_CHUNK, default TBF_STEADY_MAX = 2048 blocks; 64 with deltas)
     chunk = eng.chunks()[1] if not a.dry_run else 64
     launches = -(-a.blocks // chunk)
     ksteps = a.steps if a.kernel_steps is None else a.kernel_steps
@@ -440,7 +440,7 @@ def main():
                     "step_frac": step_gbs / HBM_PEAK_GBS,
                     "kernels_ms_per_launch": kern, "kernels_ms_isolated": kern_iso,
                     "reverb_core": ("k_rv_core_lds: a channel's 12 rings LDS-resident for the launch "
-                                    "(loaded and stored once per launch: a steady chunk of up to 1024 blocks), so its HBM traffic is "
+                                    "(loaded and stored once per launch: a steady chunk of up to 2048 blocks), so its HBM traffic is "
                                     "far below the algorithmic ring bytes it is quoted against"
                                     if os.environ.get("TBF_RV_LDS", "1") != "0" else
                                     "k_rv_core: rings streamed through HBM every sample"),

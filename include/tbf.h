@@ -253,7 +253,7 @@ int tbf_debug_pool_check (uint32_t jobs);
 /* the cfg-derived HBM layout: the compact whirl ring window (512 / 1024 / 2048 samples
  * per ring, from the geometry's largest write-ahead) and the reverb slab length */
 int tbf_debug_layout (const tbf_engine* e, uint32_t* wring_len, float* max_ahead, uint32_t* slab_len);
-/* blocks per render chunk: with control deltas (64) and without (TBF_STEADY_CHUNK, up to 1024) */
+/* blocks per render chunk: with control deltas (64) and without (TBF_STEADY_CHUNK, up to 2048) */
 int tbf_debug_chunks (const tbf_engine* e, uint32_t* delta_blocks, uint32_t* steady_blocks);
 /* test hook: set the reverb vibrato phase of line 0..7 of channel ch (b_reverb vib[ch][line],
  * src/reverb.cpp:479-496) of an instance, effective from the next block; parity tests use

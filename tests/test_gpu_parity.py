@@ -575,17 +575,17 @@ def test_gpu_device_front_end_param_events(oracle):
 
 def test_gpu_steady_chunks(oracle):
     """A chunk in which no instance's control changes (every block plays each instance's
-    current entry) runs up to TBF_STEADY_CHUNK blocks (default TBF_STEADY_MAX = 1024) per
+    current entry) runs up to TBF_STEADY_CHUNK blocks (default TBF_STEADY_MAX = 2048) per
     launch instead of 64, and ends at the next event's block.  Events at blocks 0..48
     (chords, drawbars, rotary, a note-off), then a reverb change and a whirl bypass toggle
-    at blocks 300 / 330 / 340 inside one 450-block call, and a second call of 1100 blocks
-    (one whole 1024-block chunk and a remainder): bit for bit the render of 64-block chunks
+    at blocks 300 / 330 / 340 inside one 450-block call, and a second call of 2100 blocks
+    (one whole 2048-block chunk and a remainder): bit for bit the render of 64-block chunks
     (TBF_STEADY_CHUNK=64), and the oracle."""
     import os
     import torch
     import tunebfree_amd as T
     from orc_bind import Template
-    n, nb1, nb2 = 48, 450, 1100
+    n, nb1, nb2 = 48, 450, 2100
     seeds = [5000 + i for i in range(n)]
     oscen = [S.event_scenario(i) if i % 2 else S.bench_scenario(i) for i in range(n)]
     for i in (3, 10):

@@ -38,7 +38,7 @@ for s in $STEPS; do
 		run fsum 60 python3 tools/kernel_stats.py "$(find "$OUT/fstats" -name 'run_kernel_trace.csv' | head -1)" --out "$OUT/kernel_stats_full.json"
 		run ffetch 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/ffetch" -o run --output-format csv -- python3 bench.py $NC
 		run fwrite 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/fwrite" -o run --output-format csv -- python3 bench.py $NC
-		run ftraffic 60 python3 tools/traffic_from_pmc.py "$OUT/ffetch" "$OUT/fwrite" --blocks ${BLOCKS:-1024} --out "$OUT/traffic.json"
+		run ftraffic 60 python3 tools/traffic_from_pmc.py "$OUT/ffetch" "$OUT/fwrite" --blocks ${BLOCKS:-2048} --out "$OUT/traffic.json"
 		run fbench 900 python3 bench.py --steps 20 --warmup 5 --traffic "$OUT/traffic.json"
 		cp "$OUT/fbench.log" "$OUT/bench.json"
 		;;

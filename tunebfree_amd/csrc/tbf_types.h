@@ -213,7 +213,7 @@ typedef struct tbf_rv_chan { /* one channel of the feedback network: k_rv_core w
  * plays each instance's current control) up to TBF_STEADY_MAX, so the per-launch state
  * traffic (above all the reverb network's LDS rings) spreads over more samples */
 #ifndef TBF_STEADY_MAX
-#define TBF_STEADY_MAX 1024
+#define TBF_STEADY_MAX 2048
 #endif
 /* each reverb line of the slab starts on a 128-B boundary (16 doubles): a wave's 64
  * consecutive doubles then cover exactly four whole cache lines */

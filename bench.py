@@ -32,15 +32,22 @@ sys.path.insert(0, str(ROOT / "tests"))
 #   k_rv_pre  = the predelay line M x 2 ch x 16 B                      =  32 B
 #   k_whirl   = L/R float32 output                                     =   8 B
 # The implementation's inter-stage streams (mid0/mid1/rvA/rvB/mid2) are NOT algorithmic; they
-# show up in the PMC `traffic` figure instead.  Step total: 424 B.
+# show up in the PMC bytes instead.  Step total: 424 B (step_frac, the north_star's figure).
 ALGO_BYTES = {"k_tonegen": 0, "k_mixpre": 0, "k_rv_pre": 32, "k_rv_core": 384, "k_rv_post": 0, "k_whirl": 8}
-DOMINANT = "k_rv_core"  # the HBM-streaming kernel the roofline is quoted for
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# Ceilings (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters and constants):
+HBM_PEAK_GBS = 8000.0  # HBM3E 8.0 TB/s spec
+CLOCK_GHZ = 2.4        # max clock
+SIMDS = 256 * 4        # 256 CUs x 4 SIMD-32
+# VALU issue cost of a wave64 instruction on a SIMD-32, in cycles: 2 for FP32 / integer;
+# FP64 add / mul / fma at half the FP32 rate (78.6 vs 157.3 TFLOP/s): 4; an FP32
+# transcendental (v_exp / v_sin / v_rcp ...) 2x a plain op: 4; an FP64 one: 16 (quarter of FP64)
+VALU_CYC = {"base": 2.0, "f64": 4.0, "trans32": 4.0, "trans64": 16.0}
+VALU_PEAK_TOPS = SIMDS * CLOCK_GHZ * 1e9 / VALU_CYC["base"] * 64 / 1e12  # 78.6 T lane-ops/s (FP32 rate)
 # MI355X_MICROARCH.md, LDS/L2 gather table: rows shared by every workgroup of an XCD come
 # from its L2 at 16.8-18.8 TB/s chip-wide (measured); the tonegen-only workload's wave-bank
 # gathers are that pattern (one shared bank, every instance reading the same wheels)
 L2_PEAK_GBS = 18800.0
-TRAFFIC_JSON = ROOT / "profiles" / "traffic.json"  # written by tools/traffic_from_pmc.py
+PMC_JSON = ROOT / "profiles" / "kernel_pmc.json"  # written by tools/kernel_pmc.py
 
 
 def parse():
@@ -61,9 +68,13 @@ def parse():
     ap.add_argument("--cpu-instances", type=int, default=128)
     ap.add_argument("--cpu-blocks", type=int, default=12000)
     ap.add_argument("--chain", type=int, default=0, help="0 full chain; 1/2/3 stage taps (profiling only)")
-    ap.add_argument("--isolated", type=int, default=0,
-                    help="also time each kernel alone (pipelining off); adds launches to a profiled run")
-    ap.add_argument("--traffic", default=str(TRAFFIC_JSON), help="PMC traffic JSON (tools/traffic_from_pmc.py)")
+    ap.add_argument("--isolated", type=int, default=3,
+                    help="steps timed with each kernel alone (pipelining off): the unloaded launch times "
+                         "the per-kernel roofline divides by (0: skip)")
+    ap.add_argument("--steady64", type=int, default=1,
+                    help="steps also timed with 64-block chunks (tbf_set_steady_chunk(64)): the figure of a "
+                         "workload with an event at least every 64 blocks, comparable with rounds 1-3")
+    ap.add_argument("--pmc", default=str(PMC_JSON), help="per-kernel PMC profile (tools/kernel_pmc.py)")
     ap.add_argument("--kernel-steps", type=int, default=None,
                     help="extra steps timed per kernel with HIP events for the roofline (default = --steps)")
     ap.add_argument("--stage-check", type=int, default=1,
@@ -273,6 +284,109 @@ def oracle_check(wl, rank_first, n_check, total_blocks, last_blocks, gpu_L, gpu_
     return err, exact, out
 
 
+def lib_hash():
+    import hashlib
+    import tunebfree_amd as T
+    return hashlib.sha256(Path(T.LIB_PATH).read_bytes()).hexdigest()[:16]
+
+
+def kernel_bounds(ms, pmc):
+    """One kernel against its two ceilings, from its unloaded launch time (ms) and its PMC
+    counts per launch (tools/kernel_pmc.py): HBM bytes / time against 8 TB/s, and VALU issue
+    cycles (instruction counts x their SIMD-32 issue cost) / time against every SIMD issuing
+    at 2.4 GHz.  Both fractions are of the whole chip."""
+    c = pmc["counters"]
+    row = {"kernel": pmc.get("kernel"), "ms_isolated": ms, "pmc_ms": pmc.get("pmc_ms")}
+    sec = ms * 1e-3
+    if "hbm_bytes" in pmc:
+        row["hbm_bytes"] = pmc["hbm_bytes"]
+        row["hbm_bytes_per_stereo_sample"] = pmc.get("hbm_bytes_per_stereo_sample")
+        row["hbm_gbs"] = pmc["hbm_bytes"] / sec / 1e9
+        row["hbm_frac"] = row["hbm_gbs"] / HBM_PEAK_GBS
+    if "SQ_INSTS_VALU" in c:
+        f64 = sum(c.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64"))
+        t32, t64 = c.get("SQ_INSTS_VALU_TRANS_F32", 0.0), c.get("SQ_INSTS_VALU_TRANS_F64", 0.0)
+        cyc = (VALU_CYC["base"] * c["SQ_INSTS_VALU"] + (VALU_CYC["f64"] - VALU_CYC["base"]) * f64
+               + (VALU_CYC["trans32"] - VALU_CYC["base"]) * t32 + (VALU_CYC["trans64"] - VALU_CYC["base"]) * t64)
+        row["valu_insts"] = c["SQ_INSTS_VALU"]
+        row["valu_issue_cycles"] = cyc
+        row["valu_tops"] = cyc / VALU_CYC["base"] * 64 / sec / 1e12
+        row["valu_frac"] = cyc / (SIMDS * CLOCK_GHZ * 1e9 * sec)
+    if c.get("SQ_WAVE_CYCLES"):
+        if "SQ_WAIT_ANY" in c:
+            row["wait_frac"] = c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"]  # waves parked (waitcnt / barrier)
+    if c.get("SQ_ACTIVE_INST_VALU") and "SQ_THREAD_CYCLES_VALU" in c:
+        row["lane_util"] = c["SQ_THREAD_CYCLES_VALU"] / (64.0 * c["SQ_ACTIVE_INST_VALU"])
+    if "clock_ghz" in pmc:
+        row["clock_ghz_profiled"] = pmc["clock_ghz"]
+    fr = {k: row[k + "_frac"] for k in ("hbm", "valu") if k + "_frac" in row}
+    row["bound"] = max(fr, key=fr.get) if fr else None
+    return row
+
+
+def roofline(a, B, nsamp, elapsed, samples_launch, launches, algo, kern, kern_iso, bank_entries):
+    """The bench line's roofline object: every kernel against the ceiling that binds it
+    (unloaded launch time, PMC bytes and VALU issue of the same build); the dominant kernel
+    (longest unloaded launch) in the top-level fields; the north_star's step-level HBM
+    fraction of the 424-B byte model beside it."""
+    pmc, pmc_note = None, None
+    if Path(a.pmc).exists():
+        pj = json.loads(Path(a.pmc).read_text())
+        wl = {"batch": B, "blocks": a.blocks, "sr": a.sr, "chain": a.chain}
+        if pj.get("workload") != wl:
+            pmc_note = f"{a.pmc}: another workload ({pj.get('workload')})"
+        else:
+            pmc = pj
+            if pj.get("build") != lib_hash():
+                pmc_note = f"{a.pmc}: profiled on build {pj.get('build')}, this library is {lib_hash()}"
+    step_bytes = sum(algo[k] for k in kern)
+    step_gbs = B * nsamp * step_bytes / (elapsed / a.steps) / 1e9  # per GPU
+    times = kern_iso or kern
+    rows = {}
+    for k, ms in times.items():
+        if pmc and k in pmc["kernels"]:
+            rows[k] = kernel_bounds(ms, pmc["kernels"][k])
+        else:
+            rows[k] = {"ms_isolated": ms if kern_iso else None}
+        rows[k]["ms_as_rendered"] = kern.get(k)
+        rows[k]["algorithmic_bytes_per_stereo_sample"] = algo.get(k, 0)
+    dom = max(times, key=times.get)
+    d = rows[dom]
+    roof = {"kernel": dom, "kernel_ms_isolated": times[dom] if kern_iso else None,
+            "bound": d.get("bound"), "achieved": None, "peak": None, "unit": None, "frac": None,
+            "traffic": d.get("hbm_bytes"),
+            "hbm_frac": d.get("hbm_frac"), "valu_frac": d.get("valu_frac"),
+            "algorithmic_bytes_per_launch": samples_launch * algo.get(dom, 0),
+            "algorithmic_hbm_frac": samples_launch * algo.get(dom, 0) / (times[dom] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "launches_per_step": launches,
+            "step_bytes_per_stereo_sample": step_bytes, "step_gbs_per_gpu": step_gbs,
+            "step_frac": step_gbs / HBM_PEAK_GBS,
+            "kernels": rows,
+            "pmc_source": (pmc or {}).get("source"), "pmc_build": (pmc or {}).get("build"),
+            "pmc_build_match": bool(pmc) and pmc.get("build") == lib_hash(), "pmc_note": pmc_note,
+            "method": "each kernel's unloaded launch time (every kernel alone, pipelining off, HIP events on "
+                      "its stream) against its own ceilings: HBM = PMC FETCH_SIZE x 2 + WRITE_SIZE bytes per "
+                      "launch / time vs 8 TB/s; VALU = SQ_INSTS_VALU (+ FP64 / transcendental issue cost) x "
+                      "SIMD-32 cycles / time vs 1024 SIMDs at 2.4 GHz; bound = the larger; the dominant "
+                      "kernel = the longest unloaded launch"}
+    if d.get("bound") == "hbm":
+        roof.update({"achieved": d["hbm_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": d["hbm_frac"]})
+    elif d.get("bound") == "valu":
+        roof.update({"achieved": d["valu_tops"], "peak": VALU_PEAK_TOPS, "unit": "T lane-ops/s (FP32-rate)",
+                     "frac": d["valu_frac"]})
+    if bank_entries is not None and "k_tonegen" in times:
+        # tonegen only (configs[1]) is L2-bound (SURVEY.md s8(d)): every program entry of a
+        # block gathers one wheel's 128 samples from the shared bank, 4 B per entry and sample
+        l2b = 4.0 * bank_entries
+        l2a = samples_launch * l2b / (times["k_tonegen"] * 1e-3) / 1e9
+        roof["l2"] = {"kernel": "k_tonegen", "achieved": l2a, "peak": L2_PEAK_GBS, "unit": "GB/s",
+                      "frac": l2a / L2_PEAK_GBS, "bytes_per_stereo_sample": l2b,
+                      "bank_entries_per_block": bank_entries,
+                      "note": "tonegen only: the wave-bank gathers, 4 B x program entries per sample, from the "
+                              "shared L2-resident bank; HBM moves only the 8 B output"}
+    return roof
+
+
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -355,7 +469,7 @@ def main():
     total_samples = world * a.batch * nsamp * a.steps  # every rank's instances (shard sums to world * batch)
     value = total_samples / elapsed
 
-    kern, kern_iso, max_err, exact, per_stage = {}, None, None, None, None
+    kern, kern_iso, max_err, exact, per_stage, steady64 = {}, None, None, None, None, None
     # launch sets per step: the timed steps have no control deltas, so each chunk is up to the
     # engine's steady chunk (TBF_STEADY_CHUNK, default TBF_STEADY_MAX = 2048 blocks; 64 with deltas)
     chunk = eng.chunks()[1] if not a.dry_run else 64
@@ -373,16 +487,35 @@ def main():
         kt = eng.kernel_times()
         eng.kernel_times(False)
         kern = {k: v[0] / v[1] for k, v in kt.items() if v[1]}
-        if a.isolated:  # each kernel alone on the GPU (pipelining off): per-kernel tuning
+        extra_blocks = ksteps * a.blocks
+        if a.isolated:  # each kernel alone on the GPU (pipelining off): the unloaded launch times
             eng.kernel_times("serial")
-            for _ in range(ksteps):
+            for _ in range(a.isolated):
                 step()
             torch.cuda.synchronize()
             kt = eng.kernel_times()
             eng.kernel_times(False)
             kern_iso = {k: v[0] / v[1] for k, v in kt.items() if v[1]}
+            extra_blocks += a.isolated * a.blocks
+        if a.steady64 and a.blocks > 64:
+            # the same steps in 64-block chunks (every launch 64 blocks, as a workload with an
+            # event at least every 64 blocks renders): one warmup step, then a.steady64 timed
+            eng.set_steady_chunk(64)
+            step()
+            sync()
+            t64 = time.perf_counter()
+            for _ in range(a.steady64):
+                step()
+            sync()
+            t64 = time.perf_counter() - t64
+            eng.set_steady_chunk(2048)
+            steady64 = {"ms_per_64_blocks": t64 / a.steady64 / (a.blocks / 64) * 1e3,
+                        "value": B * nsamp * a.steady64 / t64, "steps": a.steady64,
+                        "note": "rank-local: the same render with every chunk 64 blocks long "
+                                "(tbf_set_steady_chunk(64); rounds 1-3 measured this step)"}
+            extra_blocks += (1 + a.steady64) * a.blocks
         # parity on the last step (first --check instances of this rank), per stage
-        total_blocks = (a.warmup + a.steps + ksteps * (2 if a.isolated else 1)) * a.blocks
+        total_blocks = (a.warmup + a.steps) * a.blocks + extra_blocks
         if a.check:
             gL = outL[: a.check].cpu().numpy()
             gR = outR[: a.check].cpu().numpy()
@@ -408,58 +541,8 @@ def main():
         algo = dict(ALGO_BYTES)
         if a.chain == 1:  # tonegen only: k_mixpre writes L and R (8 B); bank reads are L2-resident
             algo["k_mixpre"] = 8
-        roof = None
-        if kern:
-            dom = DOMINANT if DOMINANT in kern else max(kern, key=kern.get)
-            achieved = samples_launch * algo[dom] / (kern[dom] * 1e-3) / 1e9
-            traffic, traffic_src = None, None
-            if Path(a.traffic).exists():
-                tj = json.loads(Path(a.traffic).read_text())
-                if tj.get("workload") == {"batch": B, "blocks": a.blocks, "sr": a.sr, "chain": a.chain} \
-                        and dom in tj.get("kernels", {}):
-                    traffic = tj["kernels"][dom]["bytes_per_launch"]
-                    traffic_src = tj.get("source")
-            # the algorithmic bytes of the kernels this chain mode runs (424 B for the full chain)
-            step_bytes = sum(algo[k] for k in kern)
-            step_gbs = B * nsamp * step_bytes / (elapsed / a.steps) / 1e9  # per GPU
-            ms = kern[dom]
-            # the LDS-resident network moves far fewer bytes than the algorithm streams: what
-            # limits it is the latency and issue of its per-sample work, so `bound` names that,
-            # and the fraction of the HBM roofline the algorithmic bytes reach is kept beside it
-            lds_net = dom == "k_rv_core" and os.environ.get("TBF_RV_LDS", "1") != "0"
-            roof = {"bound": "latency" if lds_net else "hbm", "roofline": "hbm",
-                    "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": achieved / HBM_PEAK_GBS, "frac_algorithmic": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                    # the HBM bytes the kernel really moves (PMC) over the same time
-                    "hbm_frac_actual": (traffic / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
-                    "kernel": dom, "kernel_ms_per_launch": kern[dom],
-                    "algorithmic_bytes_per_launch": samples_launch * algo[dom],
-                    "bytes_per_stereo_sample": algo[dom], "traffic_source": traffic_src,
-                    "launches_per_step": launches,
-                    "step_bytes_per_stereo_sample": step_bytes, "step_gbs_per_gpu": step_gbs,
-                    "step_frac": step_gbs / HBM_PEAK_GBS,
-                    "kernels_ms_per_launch": kern, "kernels_ms_isolated": kern_iso,
-                    "reverb_core": ("k_rv_core_lds: a channel's 12 rings LDS-resident for the launch "
-                                    "(loaded and stored once per launch: a steady chunk of up to 2048 blocks), so its HBM traffic is "
-                                    "far below the algorithmic ring bytes it is quoted against"
-                                    if os.environ.get("TBF_RV_LDS", "1") != "0" else
-                                    "k_rv_core: rings streamed through HBM every sample"),
-                    "limited_by": ("not HBM: issue and latency of the per-sample network at one 12-wave "
-                                   "workgroup per CU (a read phase of sines, tap reads, interpolation and "
-                                   "Householder mix, then the ring writes, two barriers per 704-sample group; "
-                                   "tools/rvl_prof.py), plus its ring load and store per launch (hbm_frac_actual)"
-                                   if lds_net else None),
-                    "timing": "HIP events on each launch's stream while neighbouring chunks' "
-                              "kernels overlap (cross-chunk pipelining, as in the timed region)"}
-        if roof is not None and bank_entries is not None and "k_tonegen" in kern:
-            l2b = 4.0 * bank_entries  # L2 bytes per (mono = stereo) sample
-            l2a = samples_launch * l2b / (kern["k_tonegen"] * 1e-3) / 1e9
-            roof.update({"bound": "l2", "achieved": l2a, "peak": L2_PEAK_GBS, "frac": l2a / L2_PEAK_GBS,
-                         "kernel": "k_tonegen", "kernel_ms_per_launch": kern["k_tonegen"],
-                         "algorithmic_bytes_per_launch": samples_launch * l2b, "bytes_per_stereo_sample": l2b,
-                         "bank_entries_per_block": bank_entries,
-                         "note": "tonegen only: the wave-bank gathers, 4 B x program entries per sample, "
-                                 "from the shared L2-resident bank; HBM moves only the 8 B output"})
+        roof = roofline(a, B, nsamp, elapsed, samples_launch, launches, algo, kern, kern_iso, bank_entries) \
+            if kern else None
         cpu = cpu_baseline(a.cpu_instances, a.cpu_blocks, a.sr) \
             if (a.cpu_baseline and world == 1 and a.workload == "cfg3" and not a.dry_run) else None
         line = {
@@ -473,6 +556,7 @@ def main():
             "max_err": max_err, "bit_exact_frac": exact, "checked_instances": a.check,
             "max_err_per_stage": per_stage,
             "roofline": roof,
+            "steady64": steady64,
             "cpu_baseline": cpu,
         }
         if a.dry_run:

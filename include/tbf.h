@@ -255,6 +255,18 @@ int tbf_debug_pool_check (uint32_t jobs);
 int tbf_debug_layout (const tbf_engine* e, uint32_t* wring_len, float* max_ahead, uint32_t* slab_len);
 /* blocks per render chunk: with control deltas (64) and without (TBF_STEADY_CHUNK, up to 2048) */
 int tbf_debug_chunks (const tbf_engine* e, uint32_t* delta_blocks, uint32_t* steady_blocks);
+/* chunks with events since the engine was created, by the front end that stepped them:
+ * the device's (k_front) and the host's */
+int tbf_debug_front_chunks (const tbf_engine* e, uint64_t* device_chunks, uint64_t* host_chunks);
+/* the longest render chunk without control deltas, in blocks (64 .. 2048, default 2048).
+ * The stage buffers hold one chunk per instance (about 68 B per instance and sample at the
+ * default stage groups: 73 GB at 4096 instances and 2048 blocks, 9.1 GB at 256 blocks) and
+ * grow to the longest chunk a call makes, so this bounds the engine's HBM footprint; longer
+ * chunks spread each launch's state traffic over more samples.  The
+ * engine lowers it by itself when the device cannot hold the buffers.  Takes effect at the
+ * next render (buffers larger than the new value are freed then); returns the value in
+ * effect, or < 0 on error.  Renders are bit-identical at every value. */
+int tbf_set_steady_chunk (tbf_engine* e, uint32_t blocks);
 /* test hook: set the reverb vibrato phase of line 0..7 of channel ch (b_reverb vib[ch][line],
  * src/reverb.cpp:479-496) of an instance, effective from the next block; parity tests use
  * it to place a phase just below a power of two (a binade crossing inside a launch) */

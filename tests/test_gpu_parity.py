@@ -573,6 +573,99 @@ def test_gpu_device_front_end_param_events(oracle):
     assert max(eL, eR) <= TOL
 
 
+def test_gpu_device_front_end_effect_events(oracle):
+    """The effect setters on the device front end (k_front): rotary
+    speed (drum / horn -> useRevOption, src/whirl.cpp:174-235), overdrive on / off and
+    character (src/overdrive.cpp:387, 552-574), reverb mix (src/reverb.cpp:233), percussion
+    volume and decay (src/tonegen.cpp:1725-1765), swell, whirl bypass and the vibrato type,
+    mixed with notes and drawbars into >= 1024-event chunks over 1100 instances.  Every
+    chunk after the first (fresh instances start dirty) is stepped on the device, except
+    one with a character outside [0, 1] (the host front end, from the device chunks'
+    mirror state).  Bit for bit against TBF_DEVICE_FRONT=0 and the oracle."""
+    import os
+    import torch
+    import tunebfree_amd as T
+    from orc_bind import Template
+    n, nb = 1100, 256
+    seeds = [9500 + i for i in range(n)]
+    rows, oscen = [], [[] for _ in range(n)]
+
+    def ev(b, i, kind, a, v):
+        rows.append((b, i, 0 if kind == "note" else 1, a, float(v)))
+        oscen[i].append((b, kind, a, v))
+
+    for i in range(n):
+        for (k, a, v) in S.jazz1_params():
+            ev(0, i, k, a, v)
+        for k in S.chord_for(i):
+            ev(0, i, "note", k, 1)
+        for b in range(1, nb):
+            r = (i * 5 + b * 7) % 29
+            if r == 0:
+                ev(b, i, "param", S.P_DRUM, (b // 20 + i) % 3)
+            elif r == 1:
+                ev(b, i, "param", S.P_HORN, (b // 24 + i) % 3)
+            elif r == 2:
+                ev(b, i, "param", S.P_OVERDRIVE, (b // 30) % 2)
+            elif r == 3:
+                # character in [0, 1]; at block 200 instance 7 takes 1.5 (outside: the host front end)
+                ev(b, i, "param", S.P_CHARACTER, ((i + b) % 11) / 10.0)
+            elif r == 4:
+                ev(b, i, "param", S.P_REVERB, ((i * 3 + b) % 9) / 8.0)
+            elif r == 5:
+                ev(b, i, "param", S.P_PERC_VOL, (b // 16) % 2)
+            elif r == 6:
+                ev(b, i, "param", S.P_PERC_DECAY, (b // 18) % 2)
+            elif r == 7:
+                ev(b, i, "param", S.P_SWELL, ((i + 2 * b) % 17) / 16.0)
+            elif r == 8 and b % 64 == 8:
+                ev(b, i, "param", S.P_WHIRL_BYPASS, (b // 64) % 2)
+            elif r == 9:
+                ev(b, i, "param", S.P_VIBRATO_TYPE, (i + b) % 7)  # 6: ignored by setVibrato
+            elif r == 10:
+                ev(b, i, "param", S.P_DRAWBAR + (i + b) % 9, (i + b) % 9)
+            elif r == 11:
+                ev(b, i, "param", S.P_PERC, (b // 22) % 2)
+            if b % 6 == 0:
+                ev(b, i, "note", 55 + (i + b - 1) % 17, 0)
+                ev(b, i, "note", 55 + (i + b) % 17, 1)
+    ev(200, 7, "param", S.P_CHARACTER, 1.5)
+    rows.sort(key=lambda r: r[0])
+    for o in oscen:
+        o.sort(key=lambda r: r[0])
+    outs, chunks = [], []
+    for front in (True, False):
+        if not front:
+            os.environ["TBF_DEVICE_FRONT"] = "0"
+        try:
+            eng = T.Engine(sample_rate=48000.0, device=0)
+        finally:
+            os.environ.pop("TBF_DEVICE_FRONT", None)
+        tid = eng.template(seed=7)
+        eng.add_instances([tid] * n, seeds)
+        evs = eng.events(rows)
+        L = torch.zeros((n, nb * 128), dtype=torch.float32, device="cuda")
+        R = torch.zeros_like(L)
+        eng.render_events_device(nb, evs, L.data_ptr(), R.data_ptr(), nb * 128)
+        eng.synchronize()
+        outs.append((L.cpu().numpy(), R.cpu().numpy()))
+        chunks.append(eng.front_chunks())
+        eng.close()
+        del L, R
+    print(f"front-end chunks (device, host): device front on {chunks[0]}, off {chunks[1]}")
+    assert chunks[0][0] >= 2 and chunks[0][1] >= 2, chunks  # the first chunk and block 200's: host
+    assert chunks[1][0] == 0
+    assert np.array_equal(outs[0][0].view(np.uint32), outs[1][0].view(np.uint32))
+    assert np.array_equal(outs[0][1].view(np.uint32), outs[1][1].view(np.uint32))
+    sample = [0, 1, 2, 7, 550, n - 1]
+    tpl = Template(oracle, seed=7)
+    oL, oR, *_ = oracle_run(oracle, tpl, [seeds[i] for i in sample], [oscen[i] for i in sample], nb)
+    eL, xL = compare(outs[0][0][sample], oL)
+    eR, xR = compare(outs[0][1][sample], oR)
+    print(f"device front end (effects) vs oracle: max|err| L={eL:.3g} R={eR:.3g} bit-exact {xL:.6f} {xR:.6f}")
+    assert max(eL, eR) <= TOL
+
+
 def test_gpu_steady_chunks(oracle):
     """A chunk in which no instance's control changes (every block plays each instance's
     current entry) runs up to TBF_STEADY_CHUNK blocks (default TBF_STEADY_MAX = 2048) per

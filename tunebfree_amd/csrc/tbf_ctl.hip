@@ -315,7 +315,7 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_tgctl (
 			const uint32_t* src = (const uint32_t*)(fm ? P.fulls + (ff - 1) : P.ctl + inst);
 			uint32_t*       dst = (uint32_t*)((tbf_seg_ctl*)P.ctl + idx);
 			const uint32_t  pp  = km ? P.progBase + (ki - n) * (uint32_t)TBF_PROG_SLOT : P.ctl[inst].prog_off;
-			const bool      pat = R.full == 0;
+			const bool      pat = R.full == 0 || (R.flags & 0x10); /* 0x10: k_front's effect entry */
 #pragma unroll
 			for (int k = 0; k < (int)(sizeof (tbf_seg_ctl) / 4); k++) {
 				uint32_t v = src[k];
@@ -484,6 +484,14 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_front (
 	uint32_t       e = P.fevOff[inst], eEnd = P.fevOff[inst + 1];
 	uint32_t       mo = 2 * e; /* the instance's message slots: at most two per event */
 	uint32_t       idx = inst, k = 0;
+	/* the effect setters' fields: the instance's entry at the chunk start, changed in
+	 * registers; a block whose fields changed gets a full entry of its own */
+	tbf_seg_ctl    E = P.ctl[inst];
+	tbf_seg_ctl*   fulls = (tbf_seg_ctl*)P.fulls;
+	int            soft = F.percSoft != 0, fast = F.percFast != 0;
+	float          swell = F.swell;
+	bool           fx = false, revClear = false;
+	int            revPend = -1;
 	/* drawBarLevel[bus][s] = (float)((float)s / 8.0) on every bus (TgControl::init) */
 	auto level = [] (uint32_t s) { return (float)((double)(float)s / 8.0); };
 	for (uint32_t b = 0; b < nb; b++) {
@@ -493,6 +501,70 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_front (
 			if (v & TBF_FEV_PARAM) {
 				const uint32_t op = (v >> 12) & 7u, bus = v & 31u, set = (v >> 5) & 15u;
 				const bool     fl = (v >> 9) & 1u;
+				if (op == TBF_FEV_EFFECT) {
+					/* the CLAP setParam effect setters (src/clap.cpp:162-207), as tbf_set_param and
+					 * stepControl apply them to the instance's control entry */
+					const float x = P.fevVal[e];
+					fx            = true;
+					switch (bus) {
+						case TBF_FX_ROTOR: revPend = (int)x; break; /* used by this block only */
+						case TBF_FX_CLEAN: E.odClean = (uint32_t)(int)x; break;
+						case TBF_FX_CHARACTER: {
+							/* fsetCharacter's output level C (linseg in float), then the preamp's
+							 * per-block constants (src/overdrive.cpp:60-140; odCtlCompute) */
+							/* the reference's double tables, narrowed to float as tbf::setCharacter does */
+							const float Av[5] = {(float)0.0, (float)0.25, (float)0.50, (float)0.75, (float)1.00};
+							const float Cv[5] = {(float)1.0, (float)0.70, (float)0.25, (float)0.15, (float)0.13};
+							for (int q = 0; q < 4; q++)
+								if (x <= Av[q + 1]) {
+									const float a = Av[q], bb = Av[q + 1], p = Cv[q], qq = Cv[q + 1];
+									E.odOutput    = (double)(p + (x - a) * (qq - p) / (bb - a));
+									break;
+								}
+							double density = x * 4.0, out = fabs (density);
+							density        = density * fabs (density);
+							double count   = density;
+							int    iter    = 0;
+							while (count > 1.0 && iter < 64) { /* the host admits A in [0, 1]: <= 15 */
+								iter++;
+								count = count - 1.0;
+							}
+							while (out > 1.0)
+								out = out - 1.0;
+							E.odIter       = iter;
+							E.odOut        = out;
+							E.odDensityPos = density > 0 ? 1u : 0u;
+							break;
+						}
+						case TBF_FX_REVERB: E.rvWet = (double)x; break;
+						case TBF_FX_PERC_SOFT:
+						case TBF_FX_PERC_FAST:
+							if (bus == TBF_FX_PERC_SOFT) {
+								soft               = (int)x != 0;
+								E.percEnvGainReset = F.percReset[soft];
+								E.outputGain       = swell * F.percDrawbar[soft];
+							} else
+								fast = (int)x != 0;
+							E.percEnvGainDecay = F.percDecay[fast * 2 + soft];
+							break;
+						case TBF_FX_SWELL:
+							swell            = x;
+							E.swellPedalGain = swell;
+							E.outputGain     = swell * F.percDrawbar[soft];
+							break;
+						case TBF_FX_BYPASS: E.whBypass = (uint32_t)(int)x; break;
+						case TBF_FX_VIBTYPE: {
+							const int q = (int)x;
+							if (q >= 0 && q <= 5) {
+								E.vibTable = (uint32_t)(q / 2);
+								E.vibMixed = (uint32_t)(q & 1);
+							}
+							break;
+						}
+						default: fx = false; break;
+					}
+					continue;
+				}
 				if (op == TBF_FEV_DRAWBAR) {
 					if (set > 8)
 						continue; /* setDrawBar ignores settings > 8 */
@@ -541,9 +613,11 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_front (
 				msgs[mo++] = (uint16_t)(0x1000u | key);
 			}
 		}
-		const uint32_t nm  = mo - m0;
-		const bool     rcp = r != oldR;
-		if (nm > 0 || dbc || rcp || pending) {
+		const uint32_t nm   = mo - m0;
+		const bool     rcp  = r != oldR;
+		const bool     tgs  = nm > 0 || dbc || rcp || pending; /* a tone-generator step */
+		const bool     fxE  = fx || revPend >= 0 || revClear;  /* an entry with new effect fields */
+		if (tgs || fxE) {
 			const uint32_t d  = inst * nb + k++;
 			const uint32_t ng = (uint32_t)__builtin_popcount (gm);
 			tbf_tgc_rec    R;
@@ -552,7 +626,7 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_front (
 			R.gainOff       = ng ? go : 0;
 			R.full          = 0;
 			R.keyCompTarget = kct[kdc < 0 ? 0 : (kdc > 127 ? 127 : kdc)];
-			R.flags         = (uint8_t)(0x80u | dbc | (rcp ? 2u : 0u) | (ng ? 4u : 0u) | (ukc == 0 ? 8u : 0u));
+			R.flags         = (uint8_t)((tgs ? 0x80u | dbc | (rcp ? 2u : 0u) | (ng ? 4u : 0u) : 0u) | (ukc == 0 ? 8u : 0u));
 			R.oldRouting    = (uint8_t)r;
 			R.percSendBus   = (uint8_t)psb;
 			R.pad           = (uint8_t)ng;
@@ -561,11 +635,27 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_front (
 				gains[go++]        = __uint_as_float (bus);
 				gains[go++]        = gl[bus];
 			}
-			rec[d]  = R;
-			idx     = n + d;
-			pending = nm > 0 || dbc || rcp;
-			oldR    = r;
-			gm = dbc = 0;
+			if (fxE) {
+				/* a full entry with this block's effect fields; k_tgctl patches its key fields
+				 * and program from the record (flag 0x10) and every later delta of the chunk
+				 * starts from it.  A rotary selection is used by this block only: the next
+				 * block gets an entry without it. */
+				E.whRevOption = revPend;
+				E.whSet       = 0;
+				fulls[d]      = E;
+				R.full        = d + 1;
+				R.flags |= 0x10u;
+				revClear = revPend >= 0;
+				revPend  = -1;
+				fx       = false;
+			}
+			rec[d] = R;
+			idx    = n + d;
+			if (tgs) {
+				pending = nm > 0 || dbc || rcp;
+				oldR    = r;
+				gm = dbc = 0;
+			}
 		}
 		ctlIdx[(size_t)b * n + inst] = idx;
 	}

@@ -500,6 +500,8 @@ int tbf_engine_destroy (tbf_engine* e)
 	e->dfrontB.release ();
 	e->dfev.release ();
 	e->dfevB.release ();
+	e->dfval.release ();
+	e->dfvalB.release ();
 	e->dfoff.release ();
 	e->dfoffB.release ();
 	e->dkeyComp.release ();
@@ -1076,7 +1078,7 @@ static int growProg (tbf_engine* e, size_t entries, uint32_t keep)
 	if (keep && e->prog.p)
 		HIPCHK (hipMemcpy (np.p, e->prog.p, PERSIST (keep) * sizeof (tbf_prog_entry), hipMemcpyDeviceToDevice));
 	e->prog.release ();
-	e->prog = np;
+	e->prog = std::move (np);
 	return 0;
 }
 
@@ -1205,9 +1207,9 @@ static int ensureDevice (tbf_engine* e)
 		e->st.release ();
 		e->wring.release ();
 		e->rslab.release ();
-		e->st    = nst;
-		e->wring = nwr;
-		e->rslab = nsl;
+		e->st    = std::move (nst);
+		e->wring = std::move (nwr);
+		e->rslab = std::move (nsl);
 		std::vector<tbf_inst_const> k (n);
 		for (uint32_t i = 0; i < n; i++)
 			k[i] = e->inst[i].k;
@@ -1227,7 +1229,7 @@ static int ensureDevice (tbf_engine* e)
 				HIPCHK (hipMemcpy (ng.p, e->tgc.p, old * sizeof (tbf_tgc_state), hipMemcpyDeviceToDevice));
 			HIPCHK (hipMemset (ng.p + old, 0, (n - old) * sizeof (tbf_tgc_state)));
 			e->tgc.release ();
-			e->tgc = ng;
+			e->tgc = std::move (ng);
 		}
 		e->persistStale = true;
 		HIPCHK (hipMemcpy (e->cst.p, k.data (), n * sizeof (tbf_inst_const), hipMemcpyHostToDevice));
@@ -1593,14 +1595,35 @@ static bool frontClean (const Instance& in)
 {
 	const TgControl& t = in.tg;
 	return !in.ctlDirty && !in.progDirty && in.revOpt < 0 && !in.whDirty && t.msg.empty () && !t.drawBarChange &&
-	       t.oldRouting == t.newRouting && t.gainsSent && t.gainMask == 0;
+	       t.oldRouting == t.newRouting && t.gainsSent && t.gainMask == 0 &&
+	       /* the rotary option a drum / horn event derives stays an exact small integer */
+	       fabs (in.params[TBF_P_DRUM]) < 1e6 && fabs (in.params[TBF_P_HORN]) < 1e6;
 }
 
-/* a parameter event the device front end steps (drawbars, the vibrato and percussion
- * switches: they change only what a control record carries), as a TBF_FEV_* word without
- * the block; 0 for any other */
+/* a parameter event the device front end steps, as a TBF_FEV_* word without the block; 0
+ * for any other.  Drawbars and the vibrato and percussion switches change what a control
+ * record carries; the effect setters (rotary speed, overdrive on / character, reverb mix,
+ * percussion volume / decay, swell, whirl bypass, vibrato type: src/clap.cpp:162-207) the
+ * entry's effect fields (TBF_FEV_EFFECT, their values in fevVal).  Values the setters take
+ * outside their sane range (a character outside [0, 1], a swell outside [0, 2], huge or
+ * non-finite numbers) leave the chunk to the host front end. */
 static uint32_t frontParam (int32_t idx, float v)
 {
+	auto fx = [] (uint32_t k) { return TBF_FEV_PARAM | (TBF_FEV_EFFECT << 12) | k; };
+	const bool small = fabsf (v) < 1e6f; /* false for NaN too */
+	switch (idx) {
+		case TBF_P_DRUM:
+		case TBF_P_HORN: return small ? fx (TBF_FX_ROTOR) : 0;
+		case TBF_P_OVERDRIVE: return small ? fx (TBF_FX_CLEAN) : 0;
+		case TBF_P_CHARACTER: return v >= 0.0f && v <= 1.0f ? fx (TBF_FX_CHARACTER) : 0;
+		case TBF_P_REVERB: return std::isfinite (v) ? fx (TBF_FX_REVERB) : 0;
+		case TBF_P_PERCUSSION_VOLUME: return small ? fx (TBF_FX_PERC_SOFT) : 0;
+		case TBF_P_PERCUSSION_DECAY: return small ? fx (TBF_FX_PERC_FAST) : 0;
+		case TBF_P_SWELL: return v >= 0.0f && v <= 2.0f ? fx (TBF_FX_SWELL) : 0;
+		case TBF_P_WHIRL_BYPASS: return small ? fx (TBF_FX_BYPASS) : 0;
+		case TBF_P_VIBRATO_TYPE: return small ? fx (TBF_FX_VIBTYPE) : 0;
+		default: break;
+	}
 	int bus = -1;
 	if (idx >= TBF_P_DRAWBAR_MIN && idx <= TBF_P_DRAWBAR_MAX)
 		bus = idx;
@@ -1698,6 +1721,7 @@ static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0
 		o.ctlInst.clear ();
 		o.evs.clear ();
 		o.gainLocal = 0;
+		o.fx        = false;
 	}
 	{ /* the events by instance range, in order (a parallel counting partition; the counts
 	   * per event segment come from scanChunk) */
@@ -1727,6 +1751,7 @@ static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0
 		wbase[t + 1] = wbase[t] + (uint32_t)out[t].evs.size ();
 	e->hFevOff.resize (n + 1);
 	e->hFev.resize (std::max<uint32_t> (wbase[T], 1));
+	e->hFevVal.resize (std::max<uint32_t> (wbase[T], 1));
 	e->hFront.resize (n);
 	const bool          dbgPh = getenv ("TBF_DEBUG_HOST_PHASES") != nullptr;
 	std::vector<double> thMs (dbgPh ? 3 * T : 0);
@@ -1772,11 +1797,22 @@ static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0
 			F.percSendBusA    = tg.percSendBusA;
 			F.percSendBusB    = tg.percSendBusB;
 			F.gainOff         = o.gainLocal; /* + the thread's base, below */
+			F.percReset[0]    = tg.percEnvScaling * tg.percEnvGainResetNorm; /* as setPercVolume */
+			F.percReset[1]    = tg.percEnvScaling * tg.percEnvGainResetSoft;
+			F.percDrawbar[0]  = tg.percDrawbarNormalGain;
+			F.percDrawbar[1]  = tg.percDrawbarSoftGain;
+			F.percDecay[0]    = tg.percEnvGainDecaySlowNorm;
+			F.percDecay[1]    = tg.percEnvGainDecaySlowSoft;
+			F.percDecay[2]    = tg.percEnvGainDecayFastNorm;
+			F.percDecay[3]    = tg.percEnvGainDecayFastSoft;
+			F.percSoft        = tg.percIsSoft != 0;
+			F.percFast        = tg.percIsFast != 0;
+			F.swell           = tg.swellPedalGain;
 			e->hFevOff[i]     = wbase[t] + eo[i - i0];
 			/* the host's front state takes the events too (it stays the truth for any later
 			 * host-stepped chunk): the same setters, block by block, and the same steps as
 			 * the device -- a block with inputs steps, and so does the one after it */
-			bool     stepped = F.pending != 0, pend = F.pending != 0;
+			bool     stepped = F.pending != 0, pend = F.pending != 0, fxd = false;
 			uint32_t oldR = tg.oldRouting, ng = 0, msgsB = 0;
 			int      curB = -1;
 			auto     closeBlock = [&] () {
@@ -1806,6 +1842,58 @@ static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0
 					if (E.id >= 0 && E.id < 64)
 						in.params[E.id] = v;
 					const uint32_t op = (w >> 12) & 7u;
+					if (op == TBF_FEV_EFFECT) {
+						/* tbf_set_param's setter on the mirror, and the value k_front applies */
+						float x = 0.0f;
+						switch (w & 31u) {
+							case TBF_FX_ROTOR:
+								x = (float)(int)(floor (in.params[TBF_P_DRUM]) + 3 * floor (in.params[TBF_P_HORN]));
+								break;
+							case TBF_FX_CLEAN:
+								in.odClean = (int)rint (1.0f - v);
+								x          = (float)in.odClean;
+								break;
+							case TBF_FX_CHARACTER:
+								setCharacter (in, v);
+								x = v;
+								break;
+							case TBF_FX_REVERB:
+								in.rvG = v;
+								x      = v;
+								break;
+							case TBF_FX_PERC_SOFT: {
+								const int soft = (int)(1 - rint (v));
+								tg.setPercVolume (soft);
+								x = soft != 0 ? 1.0f : 0.0f;
+								break;
+							}
+							case TBF_FX_PERC_FAST: {
+								const int fast = (int)rint (v);
+								tg.setPercFast (fast);
+								x = fast != 0 ? 1.0f : 0.0f;
+								break;
+							}
+							case TBF_FX_SWELL: {
+								unsigned char u   = (unsigned char)rint (v * 127.0);
+								tg.swellPedalGain = (float)((tg.outputLevelTrim * ((double)u)) / 127.0);
+								x                 = tg.swellPedalGain;
+								break;
+							}
+							case TBF_FX_BYPASS:
+								in.whBypass = (int)rint (v);
+								x           = (float)in.whBypass;
+								break;
+							case TBF_FX_VIBTYPE: {
+								const int p = (int)floor (v);
+								tg.setVibratoFromInt (p);
+								x = (float)p;
+								break;
+							}
+						}
+						e->hFevVal[wbase[t] + j] = x;
+						fxd                      = true;
+						continue;
+					}
 					if (op == TBF_FEV_DRAWBAR)
 						tg.setDrawBar ((int)(w & 31u), (unsigned)rint (v));
 					else if (op == TBF_FEV_VIB_UPPER)
@@ -1831,6 +1919,26 @@ static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0
 				pend = false; /* no events: block 0 takes the pending step */
 			o.gainLocal += 2 * ng;
 			tg.oldRouting = tg.newRouting;
+			if (fxd) {
+				/* effect setters: the control entry the instance ends the chunk with (the
+				 * device wrote the chunk's own entries); the rotary option was a one-shot */
+				tbf_seg_ctl& c     = e->hCtl[i];
+				odCtl (in, e->cfg.sample_rate, c);
+				c.rvWet            = in.rvG;
+				c.whBypass         = (uint32_t)in.whBypass;
+				c.swellPedalGain   = tg.swellPedalGain;
+				c.outputGain       = tg.swellPedalGain * tg.percDrawbarGain;
+				c.percEnvGainDecay = tg.percEnvGainDecay;
+				c.percEnvGainReset = tg.percEnvGainReset;
+				c.vibTable         = tg.vibTable;
+				c.vibMixed         = tg.vibMixed;
+				c.whRevOption      = -1;
+				c.whSet            = 0;
+				in.revOpt          = -1;
+				in.ctlDirty        = false;
+				e->chg[i]          = 1;
+				o.fx               = true;
+			}
 			if (stepped) { /* stepped blocks: control deltas */
 				e->stepped[i] = 1;
 				o.ctlInst.push_back (i);
@@ -1871,6 +1979,8 @@ static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0
 			e->hCtlInst.push_back (i);
 	}
 	delta = !e->hCtlInst.empty ();
+	for (unsigned t = 0; t < T; t++)
+		delta = delta || out[t].fx;
 	if (getenv ("TBF_DEBUG_HOST_PHASES")) {
 		auto ms = [] (auto a, auto b) { return std::chrono::duration<double, std::milli> (b - a).count (); };
 		fprintf (stderr, "stepChunkFront T=%u: partition %.3f ms, instances %.3f ms\n", T, ms (f0, f1),
@@ -1885,6 +1995,63 @@ static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0
 		         sm[1], mx[1], sm[2], mx[2]);
 	}
 	return 0;
+}
+
+/* The inter-stage buffers for a call of nblocks blocks: each holds, per instance, one
+ * chunk of stageBlocks blocks -- a power of two from TBF_CHUNK up to steadyChunk, just
+ * enough for the longest chunk this call can make, so a caller that renders 64 blocks at a
+ * time never pays for 2048-block chunks (n x blocks x 128 x 68 B at the default stage
+ * groups: 73 GB at 4096 instances and 2048 blocks, 2.3 GB at 64).  They only grow (a
+ * different stride under chunks still in flight would be wrong), after every launch that
+ * may read them has finished.  When the device cannot hold them, the chunk halves down to
+ * TBF_CHUNK before the call fails, and steadyChunk stays at what fitted.  A buffer whose
+ * producer and every reader run on one stage-group stream is single: the next chunk's
+ * producer is ordered behind this chunk's readers by the stream (default groups {0,0,1,1,2,2}:
+ * mid0, rvA and mid2 single; mid1, rvB by chunk parity). */
+static int stageBuffers (tbf_engine* e, uint32_t n, uint32_t nblocks, hipStream_t s)
+{
+	uint32_t want = TBF_CHUNK;
+	while (want < nblocks && want < e->steadyChunk)
+		want *= 2;
+	want = std::min (want, std::max (e->steadyChunk, (uint32_t)TBF_CHUNK));
+	if (e->stageN == n && e->stageBlocks >= want && e->mid0.p)
+		return 0;
+	/* every launch that may read the old buffers: pipelined stages and the caller's stream */
+	if (int rc = drainStages (e))
+		return rc;
+	HIPCHK (hipStreamSynchronize (s));
+	HIPCHK (hipDeviceSynchronize ());
+	/* producer stage -> reader stages of mid0, mid1, rvA, rvB, mid2 */
+	static const int prod[5] = {0, 1, 2, 3, 4}, rd[5][2] = {{1, -1}, {2, 4}, {3, -1}, {4, -1}, {5, -1}};
+	for (int b = 0; b < 5; b++) {
+		bool dbl = false;
+		for (int r : rd[b])
+			dbl = dbl || (r >= 0 && e->grp[r] != e->grp[prod[b]]);
+		e->stageDbl[b] = dbl;
+	}
+	const bool rv = e->cfg.chain_mode != TBF_CHAIN_TONEGEN && e->cfg.chain_mode != TBF_CHAIN_TAP_PREAMP;
+	auto       k  = [&] (int b) { return (size_t)(e->stageDbl[b] ? 2 : 1); };
+	for (uint32_t blocks = want;;) {
+		e->mid0.release (), e->mid1.release (), e->mid2.release (), e->rvA.release (), e->rvB.release ();
+		const size_t need = (size_t)n * blocks * TBF_BLK;
+		const bool   ok   = !e->mid0.ensure (k (0) * 2 * need) &&
+		                (!rv || (!e->mid1.ensure (k (1) * need) && !e->mid2.ensure (k (4) * need) &&
+		                         !e->rvA.ensure (k (2) * 2 * need) && !e->rvB.ensure (k (3) * 2 * need)));
+		if (ok) {
+			e->stageBlocks = blocks;
+			e->stageN      = n;
+			if (blocks < want) /* the device could not hold longer chunks */
+				e->steadyChunk = blocks;
+			return 0;
+		}
+		(void)hipGetLastError (); /* the failed hipMalloc's error */
+		if (blocks <= TBF_CHUNK) {
+			e->mid0.release (), e->mid1.release (), e->mid2.release (), e->rvA.release (), e->rvB.release ();
+			e->stageBlocks = e->stageN = 0;
+			return fail (-12, "out of device memory (stage buffers)");
+		}
+		blocks = std::max (blocks / 2, (uint32_t)TBF_CHUNK);
+	}
 }
 
 static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, uint64_t stride, hipStream_t s,
@@ -1956,18 +2123,13 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 	if (e->cfg.chain_mode == TBF_CHAIN_TONEGEN && e->mixFixed.ensure (n))
 		return fail (-12, "out of device memory");
 	P.mixFixed = e->mixFixed.p;
-	/* inter-stage buffers: two sets, by chunk parity (see the pipelining below), each for
-	 * the longest chunk (a chunk without deltas, steadyChunk blocks) */
-	const size_t need = (size_t)n * e->steadyChunk * TBF_BLK;
-	if (e->mid0.ensure (2 * 2 * need))
-		return fail (-12, "out of device memory (stage buffers)");
-	if (e->cfg.chain_mode != TBF_CHAIN_TONEGEN && e->cfg.chain_mode != TBF_CHAIN_TAP_PREAMP) {
-		if (e->mid1.ensure (2 * need) || e->mid2.ensure (2 * need))
-			return fail (-12, "out of device memory (stage buffers)");
-		if (e->rvA.ensure (2 * 2 * need) || e->rvB.ensure (2 * 2 * need))
-			return fail (-12, "out of device memory (reverb stage buffers)");
-	}
-	P.midStride = (uint64_t)e->steadyChunk * TBF_BLK;
+	/* inter-stage buffers for the longest chunk this call makes (stageBuffers): single, or
+	 * two sets by chunk parity (see the pipelining below) */
+	if ((rc = stageBuffers (e, n, nblocks, s)))
+		return rc;
+	const size_t   need     = (size_t)n * e->stageBlocks * TBF_BLK;
+	const uint32_t maxChunk = std::min (e->steadyChunk, e->stageBlocks);
+	P.midStride             = (uint64_t)e->stageBlocks * TBF_BLK;
 	/* Cross-chunk pipelining.  Every stage is causal and keeps its own state, so stage k
 	 * of chunk c depends only on stage k-1 of chunk c and on stage k of chunk c-1, which
 	 * runs on the same stage-group stream; the stage buffers alternate by chunk parity.
@@ -1990,6 +2152,11 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			if (e->chg[i]) {
 				e->hCtl[i].whRevOption = -1;
 				e->hCtl[i].whSet       = 0;
+				/* a one-shot in the chunk's last block left the instance dirty only so that the
+				 * next block clears it: the entry it ends with is cleared here already */
+				Instance& in = e->inst[i];
+				if (in.ctlDirty && !in.progDirty && in.revOpt < 0 && !in.whDirty)
+					in.ctlDirty = false;
 				lo                     = std::min (lo, i);
 				hi                     = std::max (hi, i + 1);
 				e->chg[i]              = 0;
@@ -2014,10 +2181,11 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		/* host control for the chunk, block by block: entry indices per (block, instance),
 		 * new pool entries only where an instance's control changes */
 		uint32_t want = std::min<uint32_t> (TBF_CHUNK, nblocks - b0);
-		if (nblocks - b0 > TBF_CHUNK && e->steadyChunk > TBF_CHUNK && e->actList.empty () && !e->persistStale) {
+		if (nblocks - b0 > TBF_CHUNK && maxChunk > TBF_CHUNK && e->actList.empty () && !e->persistStale) {
 			/* no instance's control can change before the next event: a chunk without deltas,
-			 * up to steadyChunk blocks, ending at the next event's block */
-			uint32_t w = std::min (e->steadyChunk, nblocks - b0);
+			 * up to steadyChunk blocks (as far as the stage buffers reach), ending at the next
+			 * event's block */
+			uint32_t w = std::min (maxChunk, nblocks - b0);
 			if (evi < nev)
 				w = std::min (w, ev[evi].block > b0 ? ev[evi].block - b0 : 0u);
 			if (w > TBF_CHUNK)
@@ -2074,6 +2242,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			e->hFull.swap (e->hFullB);
 			e->hFront.swap (e->hFrontB);
 			e->hFev.swap (e->hFevB);
+			e->hFevVal.swap (e->hFevValB);
 			e->hFevOff.swap (e->hFevOffB);
 			e->hIdx.swap (e->hIdxB);
 			e->hCtlPin.swap (e->hCtlPinB);
@@ -2148,20 +2317,27 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			evi    = evEnd;
 			len    = want;
 			dfront = true;
+			e->frontChunks[0]++;
 			if (getenv ("TBF_DEBUG_HOST_PHASES"))
 				fprintf (stderr, "chunk %llu: device front end, %u note events\n", (unsigned long long)e->chunkSeq,
 				         e->hFevOff[n]);
 		}
-		/* many instances to step: active now, or touched by this chunk's events */
-		else if (e->devCtl && !progEv && e->parCtl && e->actList.size () + (evEnd - evi) >= 1024) {
-			if ((rc = stepChunkParallel (e, n, want, b0, ev, evi, evEnd, rp, delta)))
-				return rc;
-			evi = evEnd;
-			len = want;
+		else {
+			if (evEnd > evi)
+				e->frontChunks[1]++;
+			/* many instances to step: active now, or touched by this chunk's events */
+			if (e->devCtl && !progEv && e->parCtl && e->actList.size () + (evEnd - evi) >= 1024) {
+				if ((rc = stepChunkParallel (e, n, want, b0, ev, evi, evEnd, rp, delta)))
+					return rc;
+				evi = evEnd;
+				len = want;
+			}
 		}
 		for (; len < want; len++) {
 			if (!e->devCtl && e->dProg.size () + (size_t)n * SLOT > dprogCap && len > 0)
 				break; /* delta program pool full: end the chunk here */
+			if (delta && len >= TBF_CHUNK)
+				break; /* a chunk with deltas ends at TBF_CHUNK blocks, before the next block's events */
 			for (; evi < nev && ev[evi].block <= b0 + len; evi++) {
 				rc = applyEvent (e, ev[evi]);
 				if (rc)
@@ -2231,11 +2407,12 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		if (delta && len > TBF_CHUNK)
 			return fail (-5, "internal: a chunk with control deltas longer than 64 blocks");
 		const bool     piped   = pipe && (!delta || dpipe);
-		P.mid0 = e->mid0.p + 2 * bset * need;
-		P.mid1 = e->mid1.p ? e->mid1.p + bset * need : nullptr;
-		P.mid2 = e->mid2.p ? e->mid2.p + bset * need : nullptr;
-		P.rvA  = e->rvA.p ? e->rvA.p + 2 * bset * need : nullptr;
-		P.rvB  = e->rvB.p ? e->rvB.p + 2 * bset * need : nullptr;
+		auto at = [&] (int b) { return e->stageDbl[b] ? (size_t)bset * need : (size_t)0; };
+		P.mid0 = e->mid0.p + 2 * at (0);
+		P.mid1 = e->mid1.p ? e->mid1.p + at (1) : nullptr;
+		P.mid2 = e->mid2.p ? e->mid2.p + at (4) : nullptr;
+		P.rvA  = e->rvA.p ? e->rvA.p + 2 * at (2) : nullptr;
+		P.rvB  = e->rvB.p ? e->rvB.p + 2 * at (3) : nullptr;
 		if (!piped && (rc = joinStages (e, s)))
 			return rc;
 		if (delta) {
@@ -2292,24 +2469,28 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 			const size_t nMsg  = dfront ? 2 * (size_t)e->hFevOff[n] : e->hMsg.size ();
 			const size_t nGain = dfront ? (size_t)e->frontGain : e->hGain.size ();
 			if (drec.cap < nRec || dmsg.cap < nMsg || dci.cap < e->hDInst.size () || dgn.cap < nGain ||
-			    dfl.cap < e->hFull.size ())
+			    dfl.cap < (dfront ? (size_t)n * len : e->hFull.size ()))
 			{
 				if (getenv ("TBF_DEBUG_HOST_PHASES"))
 					fprintf (stderr, "chunk %llu: control record buffers grow (device sync)\n", (unsigned long long)e->chunkSeq);
 				HIPCHK (hipDeviceSynchronize ()); /* growing: nothing may still read the old buffers */
 			}
+			const size_t nFull = dfront ? (size_t)n * len : e->hFull.size (); /* k_front writes its effect entries */
 			if (drec.ensure (std::max<size_t> (nRec, 1)) || dmsg.ensure (std::max<size_t> (nMsg, 1)) ||
 			    dgn.ensure (std::max<size_t> (nGain, 27)) ||
-			    dci.ensure (e->hDInst.size ()) || dfl.ensure (std::max<size_t> (e->hFull.size (), 1)))
+			    dci.ensure (e->hDInst.size ()) || dfl.ensure (std::max<size_t> (nFull, 1)))
 				return fail (-12, "out of device memory (control records)");
 			if (dfront) {
 				/* k_front: the records, messages and index table from the key states and events */
 				DevBuf<tbf_front_state>& dfs = rp ? e->dfrontB : e->dfront;
 				DevBuf<uint32_t>&        dfe = rp ? e->dfevB : e->dfev;
 				DevBuf<uint32_t>&        dfo = rp ? e->dfoffB : e->dfoff;
-				if (dfs.cap < n || dfe.cap < e->hFev.size () || dfo.cap < (size_t)n + 1 || e->dident.cap < n)
+				DevBuf<float>&           dfv = rp ? e->dfvalB : e->dfval;
+				if (dfs.cap < n || dfe.cap < e->hFev.size () || dfv.cap < e->hFev.size () || dfo.cap < (size_t)n + 1 ||
+				    e->dident.cap < n)
 					HIPCHK (hipDeviceSynchronize ()); /* growing: nothing may still read the old buffers */
-				if (dfs.ensure (n) || dfe.ensure (e->hFev.size ()) || dfo.ensure ((size_t)n + 1) || e->dident.ensure (n))
+				if (dfs.ensure (n) || dfe.ensure (e->hFev.size ()) || dfv.ensure (e->hFev.size ()) ||
+				    dfo.ensure ((size_t)n + 1) || e->dident.ensure (n))
 					return fail (-12, "out of device memory (front end)");
 				if (e->hIdent.size () != n) {
 					e->hIdent.resize (n);
@@ -2320,8 +2501,11 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 				HIPCHK (hipMemcpyAsync (dfs.p, e->hFront.data (), (size_t)n * sizeof (tbf_front_state), hipMemcpyHostToDevice, us));
 				HIPCHK (hipMemcpyAsync (dfe.p, e->hFev.data (), e->hFev.size () * 4, hipMemcpyHostToDevice, us));
 				HIPCHK (hipMemcpyAsync (dfo.p, e->hFevOff.data (), ((size_t)n + 1) * 4, hipMemcpyHostToDevice, us));
+				HIPCHK (hipMemcpyAsync (dfv.p, e->hFevVal.data (), e->hFev.size () * 4, hipMemcpyHostToDevice, us));
 				P.front   = dfs.p;
 				P.fev     = dfe.p;
+				P.fevVal  = dfv.p;
+				P.fulls   = dfl.p;
 				P.fevOff  = dfo.p;
 				P.keyComp = e->dkeyComp.p;
 				P.rec     = drec.p;
@@ -2675,6 +2859,25 @@ int tbf_debug_chunks (const tbf_engine* e, uint32_t* delta_blocks, uint32_t* ste
 	if (delta_blocks) *delta_blocks = TBF_CHUNK;
 	if (steady_blocks) *steady_blocks = e->steadyChunk;
 	return 0;
+}
+
+int tbf_debug_front_chunks (const tbf_engine* e, uint64_t* device_chunks, uint64_t* host_chunks)
+{
+	if (!e)
+		return fail (-22, "null argument");
+	if (device_chunks) *device_chunks = e->frontChunks[0];
+	if (host_chunks) *host_chunks = e->frontChunks[1];
+	return 0;
+}
+
+int tbf_set_steady_chunk (tbf_engine* e, uint32_t blocks)
+{
+	if (!e)
+		return fail (-22, "null argument");
+	e->steadyChunk = std::min (std::max (blocks, (uint32_t)TBF_CHUNK), (uint32_t)TBF_STEADY_MAX);
+	if (e->stageBlocks > e->steadyChunk)
+		e->stageN = 0; /* reallocated (smaller) at the next render */
+	return (int)e->steadyChunk;
 }
 
 int tbf_debug_reverb_phase (tbf_engine* e, uint32_t i, int32_t ch, int32_t line, double value)

@@ -152,6 +152,21 @@ template <typename T>
 struct DevBuf {
 	T*     p   = nullptr;
 	size_t cap = 0;
+	DevBuf ()                         = default;
+	DevBuf (const DevBuf&)            = delete; /* one owner: the destructor frees */
+	DevBuf& operator= (const DevBuf&) = delete;
+	DevBuf& operator= (DevBuf&& o) noexcept /* takes o's buffer (frees its own) */
+	{
+		if (this != &o) {
+			release ();
+			p     = o.p;
+			cap   = o.cap;
+			o.p   = nullptr;
+			o.cap = 0;
+		}
+		return *this;
+	}
+	~DevBuf () { release (); }
 	int    ensure (size_t n)
 	{
 		if (n <= cap)
@@ -234,8 +249,10 @@ struct tbf_engine {
 	uint32_t                                frontGain = 0;  /* device front end: the chunk's gain-pair floats */
 	PinnedVec<tbf_front_state>              hFront, hFrontB;
 	PinnedVec<uint32_t>                     hFev, hFevB, hFevOff, hFevOffB;
+	PinnedVec<float>                        hFevVal, hFevValB; /* TBF_FEV_EFFECT events' values */
 	DevBuf<tbf_front_state>                 dfront, dfrontB;
 	DevBuf<uint32_t>                        dfev, dfevB, dfoff, dfoffB;
+	DevBuf<float>                           dfval, dfvalB;
 	DevBuf<float>                           dkeyComp;   /* [tpl][128] keyCompTable */
 	DevBuf<uint32_t>                        dident;     /* 0 .. n-1: k_tgctl's grid over every instance */
 	std::vector<uint32_t>                   hIdent;
@@ -276,6 +293,7 @@ struct tbf_engine {
 		std::vector<tbf_seg_ctl> fulls;
 		uint32_t              nd = 0;
 		uint32_t              gainLocal = 0; /* device front end: the range's gain-pair floats */
+		bool                  fx = false;    /* ... and whether an effect setter stepped an entry */
 		int                   rc = 0;
 		std::string           err; /* the worker's tbf_last_error text (it is thread-local) */
 	};
@@ -331,7 +349,16 @@ struct tbf_engine {
 	DevBuf<uint32_t>                        rvWork;           /* its work counter */
 	DevBuf<uint8_t>                         mixFixed;         /* tonegen only: k_tonegen wrote the output (tbf_launch.mixFixed) */
 	int                                     tgSplit  = -1;    /* k_tonegen block ranges (TBF_TG_SPLIT; -1: by batch size) */
-	uint32_t                                steadyChunk = TBF_STEADY_MAX; /* blocks per chunk without control deltas (TBF_STEADY_CHUNK) */
+	uint32_t                                steadyChunk = TBF_STEADY_MAX; /* blocks per chunk without control deltas (TBF_STEADY_CHUNK,
+	                                                                       * tbf_set_steady_chunk) */
+	/* the stage buffers as allocated (stageBuffers): blocks per chunk they hold (a power of two
+	 * from TBF_CHUNK up to steadyChunk, grown to the longest chunk a call can make, never past
+	 * what the device could allocate), for stageN instances; a buffer whose producer and
+	 * readers share a stage-group stream is single (dbl[] false), the others alternate by
+	 * chunk parity */
+	uint32_t                                stageBlocks = 0, stageN = 0;
+	uint64_t                                frontChunks[2] = {0, 0}; /* chunks with events: device, host front end */
+	bool                                    stageDbl[5] = {true, true, true, true, true}; /* mid0 mid1 rvA rvB mid2 */
 	/* programme table (.pgm), src/program.h:26 MAXPROGS; pgm.controller.offset */
 	std::vector<Programme>                  progs = std::vector<Programme> (129);
 	int                                     pgmOffset = 1;

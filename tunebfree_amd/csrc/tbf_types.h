@@ -72,19 +72,40 @@ typedef struct tbf_front_state {
 	int32_t  percTriggerBus; /* < 0: none */
 	uint32_t percSendBusA, percSendBusB;
 	uint32_t gainOff;        /* the instance's slots for (bus, gain) pairs in gains (floats) */
+	/* effect setters (TBF_FEV_EFFECT): the instance's percussion constants (percEnvScaling
+	 * applied, src/tonegen.cpp:1725-1765) and the switches and swell at the chunk start */
+	float    percReset[2];   /* percEnvGainReset, [isSoft] */
+	float    percDrawbar[2]; /* percDrawbarGain, [isSoft] */
+	float    percDecay[4];   /* percEnvGainDecay, [isFast * 2 + isSoft] */
+	int32_t  percSoft, percFast;
+	float    swell;          /* swellPedalGain */
+	uint32_t pad;
 } tbf_front_state;
 
 /* a front-end event, 4 bytes: block << 16 | low 16 bits
  *   note   key (12 bits; 0x0fff: outside [0, 384), ignored) | on << 12
  *   param  0x8000 | op << 12 | flag << 9 | setting << 5 | bus, op:
  *          TBF_FEV_DRAWBAR (setting 0..8, 15: out of range, ignored), TBF_FEV_VIB_UPPER /
- *          TBF_FEV_VIB_LOWER / TBF_FEV_PERC (flag: on), TBF_FEV_PERC_FIRST (flag: first) */
+ *          TBF_FEV_VIB_LOWER / TBF_FEV_PERC (flag: on), TBF_FEV_PERC_FIRST (flag: first),
+ *          TBF_FEV_EFFECT (bus = TBF_FX_*: a setter of the block's control entry; its value,
+ *          as the host derives it from the parameter, is fevVal[event]) */
 #define TBF_FEV_PARAM 0x8000u
 #define TBF_FEV_DRAWBAR 0u
 #define TBF_FEV_VIB_UPPER 1u
 #define TBF_FEV_VIB_LOWER 2u
 #define TBF_FEV_PERC 3u
 #define TBF_FEV_PERC_FIRST 4u
+#define TBF_FEV_EFFECT 5u
+/* effect setters (src/clap.cpp:162-207 setParam) and their fevVal */
+#define TBF_FX_ROTOR 0u      /* useRevOption (src/whirl.cpp:174-196): the option, a one-shot */
+#define TBF_FX_CLEAN 1u      /* setClean (src/overdrive.cpp:387): the clean flag */
+#define TBF_FX_CHARACTER 2u  /* fsetCharacter (src/overdrive.cpp:552-574): A in [0, 1] */
+#define TBF_FX_REVERB 3u     /* setReverbMix (src/reverb.cpp:233): G */
+#define TBF_FX_PERC_SOFT 4u  /* setPercussionVolume (src/tonegen.cpp:1740-1752): isSoft */
+#define TBF_FX_PERC_FAST 5u  /* setPercussionFast (1727-1732): isFast */
+#define TBF_FX_SWELL 6u      /* the swell pedal: swellPedalGain */
+#define TBF_FX_BYPASS 7u     /* whirl bypass */
+#define TBF_FX_VIBTYPE 8u    /* setVibrato knob (src/vibrato.cpp:97-129): 0..5 */
 
 /* one keyContrib element on the device (Contrib): a key's list is sorted by wheel, then
  * bus (compilePlayMatrix's insertion sort, src/tonegen.cpp:1183-1201) */
@@ -310,7 +331,8 @@ typedef struct tbf_launch {
 	const tbf_seg_ctl*    fulls;     /* the chunk's full control entries (tbf_tgc_rec.full) */
 	const tbf_front_state* front;    /* k_front: [inst] key state at the chunk start ... */
 	const uint32_t*       fevOff;    /* ... [inst + 1] offsets into fev ... */
-	const uint32_t*       fev;       /* ... an instance's events in order (TBF_FEV_*) */
+	const uint32_t*       fev;       /* ... an instance's events in order (TBF_FEV_*) ... */
+	const float*          fevVal;    /* ... and the values of its TBF_FEV_EFFECT events */
 	const float*          keyComp;   /* [tpl][128] keyCompTable */
 	uint32_t              progBase;  /* program slot of delta d (pool index nInst + d): progBase + d * TBF_PROG_SLOT */
 } tbf_launch;

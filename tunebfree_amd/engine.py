@@ -59,6 +59,7 @@ SIGNATURES = {
     "tbf_program_install": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32]),
     "tbf_program_name": (C.c_int, [C.c_void_p, C.c_uint32, C.c_char_p, C.c_uint32]),
     "tbf_midi_control_id": (C.c_int, [C.c_char_p]),
+    "tbf_set_steady_chunk": (C.c_int, [C.c_void_p, C.c_uint32]),
     "tbf_render_events": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                     C.c_uint64, C.c_void_p]),
 }
@@ -134,6 +135,19 @@ class Engine:
         w, a, s = C.c_uint32(), C.c_float(), C.c_uint32()
         _check(f(self._h, C.byref(w), C.byref(a), C.byref(s)))
         return {"wring_len": w.value, "max_ahead": a.value, "slab_len": s.value}
+
+    def front_chunks(self):
+        """tbf_debug_front_chunks: chunks with events stepped by (the device's, the host's) front end"""
+        f = self._lib.tbf_debug_front_chunks
+        f.restype, f.argtypes = C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]
+        d, h = C.c_uint64(), C.c_uint64()
+        _check(f(self._h, C.byref(d), C.byref(h)))
+        return d.value, h.value
+
+    def set_steady_chunk(self, blocks):
+        """tbf_set_steady_chunk: the longest chunk without control deltas (64..2048 blocks),
+        which bounds the stage buffers; returns the value in effect."""
+        return _check(self._lib.tbf_set_steady_chunk(self._h, int(blocks)))
 
     def chunks(self):
         """Blocks per render chunk (tbf_debug_chunks): (with control deltas, without)."""

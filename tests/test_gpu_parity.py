@@ -1693,3 +1693,37 @@ def test_gpu_add_instances_after_render_then_events(oracle, via_events):
         if max(e1, e2) > TOL:
             bad.append(i)
     assert not bad, bad
+
+
+def test_gpu_sin_fast_paths_are_ocml_bits():
+    """csrc/tbf_sin.h: the kernels' sin with wave-uniform fast paths (only the sine or only
+    the cosine polynomial of OCML's reduction when every lane of a wave has n = 0 or n = 1)
+    returns the device library's sin bit for bit: sorted inputs (uniform waves on both fast
+    paths), shuffled ones (mixed waves: the library path), negatives, the n = 0 / 1 / 2
+    boundaries, the preamp's clamp 1.57079633, signed zeros, subnormals, huge values
+    (Payne-Hanek), infinities and NaN (through tbf_debug_calibrate op 4)."""
+    import ctypes as C
+    import torch
+    import tunebfree_amd as T
+    lib = T.load_library()
+    lib.tbf_debug_calibrate.restype = C.c_int
+    lib.tbf_debug_calibrate.argtypes = [C.c_int32, C.c_void_p, C.c_uint64, C.c_void_p]
+    rng = np.random.default_rng(5)
+    q = np.pi / 4
+    sorted_ = np.sort(rng.uniform(0.0, 1.6, 1 << 18))
+    mixed = rng.permutation(sorted_)
+    edges = np.concatenate([np.nextafter(q, 0) - np.arange(64) * 1e-16, q + np.arange(64) * 1e-16,
+                            3 * q + np.arange(-64, 64) * 1e-16, np.full(64, 1.57079633),
+                            np.full(64, 0.0), np.full(64, -0.0), np.full(64, 5e-324), np.full(64, 1e-300)])
+    special = np.array([np.inf, -np.inf, np.nan, 1e300, -1e22, 2.0 ** 30, -(2.0 ** 30) + 1, 1e9, 3.0, -2.5] * 7,
+                       dtype=np.float64)
+    x = np.concatenate([sorted_, -sorted_, mixed, edges, special, rng.normal(0, 0.05, 1 << 16)])
+    n = len(x)
+    buf = torch.zeros(3 * n, dtype=torch.float64, device="cuda")
+    buf[:n] = torch.from_numpy(x).cuda()
+    assert lib.tbf_debug_calibrate(4, C.c_void_p(buf.data_ptr()), n, None) == 0
+    torch.cuda.synchronize()
+    out = buf.cpu().numpy()
+    fast, ref = out[n:2 * n], out[2 * n:]
+    same = fast.view(np.uint64) == ref.view(np.uint64)
+    assert same.all(), (x[~same][:8], fast[~same][:8], ref[~same][:8])

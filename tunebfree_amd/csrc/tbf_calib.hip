@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "tbf_sin.h"
+
 __global__ void __launch_bounds__ (256) tbf_calib_read_f64 (const double* __restrict__ p, uint64_t n,
                                                           double* __restrict__ sink)
 {
@@ -27,6 +29,17 @@ __global__ void __launch_bounds__ (256) tbf_calib_write_f64 (double* __restrict_
 		p[i] = (double)i;
 }
 
+/* test hook for tbf_sin (op 4): buf = n inputs, then tbf_sin of each, then sin of each */
+__global__ void __launch_bounds__ (256) tbf_check_sin (double* __restrict__ p, uint64_t n)
+{
+	const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n)
+		return;
+	const double x = p[i];
+	p[n + i]       = tbf_sin (x);
+	p[2 * n + i]   = sin (x);
+}
+
 extern "C" int tbf_launch_calibrate (int op, void* buf, uint64_t n, hipStream_t s)
 {
 	dim3 grid (4096), block (256);
@@ -38,6 +51,8 @@ extern "C" int tbf_launch_calibrate (int op, void* buf, uint64_t n, hipStream_t 
 		hipLaunchKernelGGL (tbf_calib_read_f64, grid, block, 0, s, (const double*)buf + 8, n - 8, (double*)buf);
 	else if (op == 3) /* the write, likewise misaligned */
 		hipLaunchKernelGGL (tbf_calib_write_f64, grid, block, 0, s, (double*)buf + 8, n - 8);
+	else if (op == 4) /* tbf_sin against sin: n inputs, buffer of 3 n doubles */
+		hipLaunchKernelGGL (tbf_check_sin, dim3 ((unsigned)((n + 255) / 256)), block, 0, s, (double*)buf, n);
 	else
 		return -22;
 	return hipGetLastError () == hipSuccess ? 0 : -5;

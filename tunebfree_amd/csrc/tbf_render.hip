@@ -29,6 +29,7 @@
 #include "../../include/tbf.h"
 #include "tbf_types.h"
 #include "tbf_exact.h"
+#include "tbf_sin.h"
 
 #define NL 64
 
@@ -622,6 +623,9 @@ k_tonegen (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl, const tbf_tp
 #ifndef MP_CB
 #define MP_CB 32                  /* instances per workgroup */
 #endif
+#ifndef MP_ABL
+#define MP_ABL 0 /* timing experiments (wrong output): 1 no waveshaper, 2 no serial chains, 3 no dither */
+#endif
 #define MP_T 32                   /* samples per tile: one per lane of a half-wave */
 #define MP_S (MP_T + 1)           /* row stride of the per-sample rows (odd: conflict-free columns) */
 #define MP_HS (MP_T / 2 + 1)      /* row stride of the high-pass rows (a chain's MP_T / 2 samples) */
@@ -685,13 +689,13 @@ __device__ __forceinline__ float preamp_shape (double x, double dry, const MpCtl
 		br = fabs (x) * 1.57079633;
 		if (br > 1.57079633)
 			br = 1.57079633;
-		br = sin (br);
+		br = tbf_sin (br);
 		x  = (x > 0.0) ? br : -br;
 	}
 	br = fabs (x) * 1.57079633;
 	if (br > 1.57079633)
 		br = 1.57079633;
-	br = (C.flags & MPF_DPOS) ? sin (br) : 1 - cos (br);
+	br = (C.flags & MPF_DPOS) ? tbf_sin (br) : 1 - cos (br);
 	if (x > 0)
 		x = (x * (1 - C.out)) + (br * C.out);
 	else
@@ -743,8 +747,12 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 					rsv = C.reset;
 				}
 				float* row = sm.g[it & 1][cl];
+#if MP_ABL == 2 /* timing experiment only (wrong output): no serial chase or high-pass */
+				if (true) {
+#else
 				if (__all ((v * m) + a == v)) { /* a fixed point on every lane (no percussion, the key
 				                                  * compression settled): the whole tile is v */
+#endif
 #pragma unroll 8
 					for (int k = 0; k < MP_T; k++)
 						row[k] = v;
@@ -773,7 +781,11 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 					hp             = !(C.flags & MPF_CLEAN);
 					ia             = C.iir;
 				}
+#if MP_ABL == 2
+				if (false) {
+#else
 				if (hp) {
+#endif
 					const double* xr = sm.x[th & 3][cl];
 					double*       hr = sm.h[th & 1][cl];
 					const double  om = 1.0 - ia;
@@ -826,9 +838,13 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 #pragma unroll 1
 		for (int it = 0; it < nIt; it++) {
 			if (lane < MP_CB) {
+#if MP_ABL == 3 /* timing experiment only (wrong output): no dither stream */
+				if (false) {
+#else
 				if (pre && it < nT) {
+#endif
 					if (it % MP_TPB == 0)
-						adv = !(sm.c[(it / MP_TPB) & 1][lane].flags & MPF_CLEAN);
+						adv =!(sm.c[(it / MP_TPB) & 1][lane].flags & MPF_CLEAN);
 					uint32_t* f = sm.f[it & 3][lane];
 #pragma unroll 8
 					for (int n = 0; n < MP_T; n++) {
@@ -891,7 +907,11 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 				const MpCtl& C  = sm.c[(kw / MP_TPB) & 1][jT[t]];
 				const double xd = sm.x[kw & 3][rT[t]][n >> 1];
 				float        y;
+#if MP_ABL == 1 /* timing experiment only (wrong output): helpers without the waveshaper */
+				if (true)
+#else
 				if (C.flags & MPF_CLEAN)
+#endif
 					y = (float)xd;
 				else
 					y = preamp_shape (sm.h[kw & 1][rT[t]][n >> 1], xd, C, sm.f[kw & 3][jT[t]][n + 1]);
@@ -1883,7 +1903,7 @@ k_rv_pre (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 #pragma unroll
 			for (int t = 0; t < RVC_NTK; t++)
 				if (h + t * RVC_H < nj)
-					ra[t][(size_t)k2 * RVC_T] = sin (sv[t] * rld (wetv[t], blk_lane ((k2 * RVC_T) / TBF_BLK)));
+					ra[t][(size_t)k2 * RVC_T] = tbf_sin (sv[t] * rld (wetv[t], blk_lane ((k2 * RVC_T) / TBF_BLK)));
 		}
 		__syncthreads ();
 	};
@@ -2518,8 +2538,10 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 		wave_sync ();
 		if (!sm.aReady) {
 			const float z0 = st.fz[0][0], z1 = st.fz[0][1];
+#ifndef WH_NO_SERIAL
 			if (lane == 0)
 				wh_serial<false> (sm.ab[ap ^ 1], 0u, 0u, st.fz[0], ha[0], ha[1], false);
+#endif
 			wave_sync ();
 			sm.ab[ap ^ 1][n] = wh_output (sm.ab[ap ^ 1][n], z0, z1, ha);
 			wave_sync ();
@@ -2538,7 +2560,11 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 		}
 		const uint32_t wb   = st.outpos & WM; /* the drum rings' window: wave-uniform */
 		const bool     wrap = wb + TBF_SUB > (uint32_t)W;
+#ifdef WH_NO_SERIAL /* timing experiment only (wrong output): k_whirl without its serial filter passes */
+		if (false) {
+#else
 		if (lane < 4 && (lane > 0 || aNext)) {
+#endif
 			float* row = lane == 0 ? sm.ab[ap] : (lane == 1 ? sm.ab[ap ^ 1] : sm.wring[lane]);
 			if (wrap)
 				wh_serial<true> (row, lane < 2 ? 0u : wb, lane < 2 ? ~0u : WM, st.fz[lane], fa0, fa1, lane == 0 && scrubA);

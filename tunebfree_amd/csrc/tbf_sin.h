@@ -1,0 +1,108 @@
+/*
+ * tbf_sin.h -- the device's double sin with wave-uniform fast paths.
+ *
+ * The render kernels take sin from the ROCm device library (OCML __ocml_sin_f64): the
+ * small-argument reduction __ocmlpriv_trigredsmall_f64 (n = rint (|x| 2/pi), a three-part
+ * Cody-Waite subtraction of n pi/2) and __ocmlpriv_sincosred2_f64, which evaluates BOTH the
+ * sine and the cosine polynomial of the reduced argument and selects one by n & 1.  The
+ * preamp's density waveshaper (src/overdrive.cpp:111-136) takes sin of |x| pi/2 clamped to
+ * [0, 1.57079633] four times per sample at character 0.5, and the reverb input stage
+ * (src/reverb.cpp:371) sin of a small value: there n is 0 or 1, and the samples of a wave
+ * mostly share it (at the bench's registration 99.9 / 94 / 71 / 56 % of 32-sample tiles for
+ * the four density sines).  So when every active lane of the wave has n == 0, only the sine
+ * polynomial of r = |x| (no reduction: trigredsmall gives hi = |x|, lo = +0 for n = 0) is
+ * evaluated; when every lane has n == 1, the reduction with n = 1 and only the cosine
+ * polynomial; otherwise OCML's sin itself.  Each path is OCML's sequence of operations for
+ * the lanes it serves (explicit fma where OCML has llvm.fma, plain operations elsewhere,
+ * compiled with -ffp-contract=off), so the result is OCML's bits on every path -- the same
+ * values the kernels produced with sin () (bit-identical to the oracle's glibc sin on every
+ * parity test; DESIGN.md section 2, licensed differences).  Constants are OCML's, given by
+ * their bit patterns.
+ */
+#ifndef TBF_SIN_H
+#define TBF_SIN_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define TBF_D(bits) __builtin_bit_cast (double, (uint64_t)(bits##ull))
+
+/* __ocmlpriv_trigredsmall_f64 for a given n: |x| - n pi/2 as hi + lo */
+__device__ __forceinline__ void tbf_trigred_small (double a, double n, double& hi, double& lo)
+{
+	const double r4  = __builtin_fma (n, TBF_D (0xBFF921FB54442D18), a);
+	const double r5  = __builtin_fma (n, TBF_D (0xBC91A62633145C00), r4);
+	const double m6  = n * TBF_D (0x3C91A62633145C00);
+	const double e8  = __builtin_fma (n, TBF_D (0x3C91A62633145C00), -m6);
+	const double r9  = r4 - m6;
+	const double r10 = r4 - r9;
+	const double r11 = r10 - m6;
+	const double r12 = r9 - r5;
+	const double r13 = r12 + r11;
+	const double r14 = r13 - e8;
+	const double r15 = __builtin_fma (n, TBF_D (0xB97B839A252049C0), r14);
+	hi               = r5 + r15;
+	const double r17 = hi - r5;
+	lo               = r15 - r17;
+}
+
+/* the sine half of __ocmlpriv_sincosred2_f64 (x = hi, y = lo) */
+__device__ __forceinline__ double tbf_sinred (double x, double y)
+{
+	const double x2  = x * x;
+	const double s18 = __builtin_fma (x2, TBF_D (0x3DE5E0B2F9A43BB8), TBF_D (0xBE5AE600B42FDFA7));
+	const double s19 = __builtin_fma (x2, s18, TBF_D (0x3EC71DE3796CDE01));
+	const double s20 = __builtin_fma (x2, s19, TBF_D (0xBF2A01A019E83E5C));
+	const double s21 = __builtin_fma (x2, s20, TBF_D (0x3F81111111110BB3));
+	const double x23 = x * (-x2);
+	const double s24 = y * 0.5;
+	const double s25 = __builtin_fma (x23, s21, s24);
+	const double s26 = __builtin_fma (x2, s25, -y);
+	const double s27 = __builtin_fma (x23, TBF_D (0xBFC5555555555555), s26);
+	return x - s27;
+}
+
+/* the cosine half of __ocmlpriv_sincosred2_f64 */
+__device__ __forceinline__ double tbf_cosred (double x, double y)
+{
+	const double x2  = x * x;
+	const double h   = x2 * 0.5;
+	const double c5  = 1.0 - h;
+	const double c6  = 1.0 - c5;
+	const double c7  = c6 - h;
+	const double x4  = x2 * x2;
+	const double p9  = __builtin_fma (x2, TBF_D (0xBDA907DB46CC5E42), TBF_D (0x3E21EEB69037AB78));
+	const double p10 = __builtin_fma (x2, p9, TBF_D (0xBE927E4FA17F65F6));
+	const double p11 = __builtin_fma (x2, p10, TBF_D (0x3EFA01A019F4EC90));
+	const double p12 = __builtin_fma (x2, p11, TBF_D (0xBF56C16C16C16967));
+	const double p13 = __builtin_fma (x2, p12, TBF_D (0x3FA5555555555555));
+	const double c15 = __builtin_fma (x, -y, c7);
+	const double c16 = __builtin_fma (x4, p13, c15);
+	return c5 + c16;
+}
+
+/* OCML's sign rule: the selected value's sign flipped when x is negative (n & 2 is 0 here) */
+__device__ __forceinline__ double tbf_sign_of (double r, double x)
+{
+	const uint64_t s = __builtin_bit_cast (uint64_t, x) & 0x8000000000000000ull;
+	return __builtin_bit_cast (double, __builtin_bit_cast (uint64_t, r) ^ s);
+}
+
+/* sin (x), OCML's bits, with the wave-uniform fast paths above */
+__device__ __forceinline__ double tbf_sin (double x)
+{
+	const double a = fabs (x);
+	const double n = __builtin_rint (a * TBF_D (0x3FE45F306DC9C883));
+	if (__all (n == 0.0))
+		return tbf_sign_of (tbf_sinred (a, 0.0), x);
+	if (__all (n == 1.0)) {
+		double hi, lo;
+		tbf_trigred_small (a, 1.0, hi, lo);
+		return tbf_sign_of (tbf_cosred (hi, lo), x);
+	}
+	return sin (x);
+}
+
+#undef TBF_D
+
+#endif

@@ -300,9 +300,10 @@ int tbf_debug_exact (int32_t op, const double* in3, double* out2, uint32_t n);
 int tbf_debug_kernel_times (tbf_engine* e, int32_t enable, double* ms6, uint32_t* count6);
 /* PMC calibration: op 0 streams n doubles from d_buf (8 B/lane reads, the reverb ring
  * pattern), op 1 writes them; ops 2 / 3 the same starting 64 B into a cache line (n >= 16);
- * op 4 (test hook for the kernels' sin, csrc/tbf_sin.h): d_buf holds n inputs followed by
- * room for 2 n results, tbf_sin of each then the library sin of each; enqueued on `stream`
- * (NULL = legacy default stream) */
+ * op 4 (test hook for csrc/tbf_sin.h): d_buf holds n inputs x followed by room for 6 n
+ * results: tbf_sin (x), sin (x), tbf_sin2's two results for (x, the input n / 2 further on),
+ * the asin fast path and asin (x clamped to [-1, 1]); enqueued on `stream` (NULL = legacy
+ * default stream) */
 int tbf_debug_calibrate (int32_t op, void* d_buf, uint64_t n_doubles, void* stream);
 
 #ifdef __cplusplus

@@ -1697,8 +1697,9 @@ def test_gpu_add_instances_after_render_then_events(oracle, via_events):
 
 def test_gpu_sin_fast_paths_are_ocml_bits():
     """csrc/tbf_sin.h: the kernels' sin with wave-uniform fast paths (only the sine or only
-    the cosine polynomial of OCML's reduction when every lane of a wave has n = 0 or n = 1)
-    returns the device library's sin bit for bit: sorted inputs (uniform waves on both fast
+    the cosine polynomial of OCML's reduction when every lane of a wave has n = 0 or n = 1,
+    OCML's small-argument path inline otherwise), the paired tbf_sin2 and the asin polynomial
+    branch return the device library's sin / asin bit for bit: sorted inputs (uniform waves on both fast
     paths), shuffled ones (mixed waves: the library path), negatives, the n = 0 / 1 / 2
     boundaries, the preamp's clamp 1.57079633, signed zeros, subnormals, huge values
     (Payne-Hanek), infinities and NaN (through tbf_debug_calibrate op 4)."""
@@ -1719,11 +1720,15 @@ def test_gpu_sin_fast_paths_are_ocml_bits():
                        dtype=np.float64)
     x = np.concatenate([sorted_, -sorted_, mixed, edges, special, rng.normal(0, 0.05, 1 << 16)])
     n = len(x)
-    buf = torch.zeros(3 * n, dtype=torch.float64, device="cuda")
+    buf = torch.zeros(7 * n, dtype=torch.float64, device="cuda")
     buf[:n] = torch.from_numpy(x).cuda()
     assert lib.tbf_debug_calibrate(4, C.c_void_p(buf.data_ptr()), n, None) == 0
     torch.cuda.synchronize()
-    out = buf.cpu().numpy()
-    fast, ref = out[n:2 * n], out[2 * n:]
-    same = fast.view(np.uint64) == ref.view(np.uint64)
-    assert same.all(), (x[~same][:8], fast[~same][:8], ref[~same][:8])
+    out = buf.cpu().numpy().reshape(7, n)
+    ref = out[2]
+    other = np.roll(ref, -(n // 2))  # sin of the input n / 2 further on
+    for name, got, want in (("tbf_sin", out[1], ref), ("tbf_sin2 first", out[3], ref),
+                            ("tbf_sin2 second", out[4], other), ("asin fast path", out[5], out[6])):
+        same = got.view(np.uint64) == want.view(np.uint64)
+        assert same.all(), (name, x[~same][:8], got[~same][:8], want[~same][:8])
+    assert np.mean(np.abs(np.clip(x, -1, 1)) < 0.5) > 0.3  # the asin fast path was exercised

@@ -68,9 +68,12 @@ def run(frames, periods, warmup, retune_every, tunings):
             (retune_times if retune_every and p % retune_every == 0 else times).append(dt * 1e3)
     eng.close()
     budget = frames / 48.0
+    third = max(1, len(times) // 3)
     out = {"frames": frames, "budget_ms": budget, "periods": len(times), "p50_ms": pct(times, 50),
            "p99_ms": pct(times, 99), "max_ms": float(max(times)), "mean_ms": float(np.mean(times)),
-           "over_budget": int(sum(t > budget for t in times))}
+           "over_budget": int(sum(t > budget for t in times)),
+           # drift inside the run: the p50 of its first and last thirds (a clock ramp shows here)
+           "p50_first_third_ms": pct(times[:third], 50), "p50_last_third_ms": pct(times[-third:], 50)}
     if retune_every:
         out.update({"retune_periods": len(retune_times), "retune_p50_ms": pct(retune_times, 50),
                     "retune_max_ms": float(max(retune_times)) if retune_times else None})
@@ -80,7 +83,10 @@ def run(frames, periods, warmup, retune_every, tunings):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--periods", type=int, default=3000)
-    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=1000)
+    ap.add_argument("--spin-ms", type=float, default=2000.0,
+                    help="a full-size render loop before the rows, so the GPU and host clocks are up "
+                         "(0: none -- the first row then pays the ramp)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     import torch
@@ -88,13 +94,26 @@ def main():
     torch.zeros(1, device="cuda")  # HIP runtime up before the engine (as bench.py)
     tunings = json.loads((ROOT / "tests" / "golden" / "tunings.json").read_text())
     import tunebfree_amd as T
+    if a.spin_ms > 0:
+        # the chip idles at a low clock: the first periods of a process ran at ~0.41 ms where
+        # the same periods later take ~0.22 (round 4's rt_latency.json); spin it up first
+        eng = T.Engine(sample_rate=48000.0, device=0)
+        tid = eng.template(seed=7)
+        eng.add_instances([tid] * 256, list(range(256)))
+        t0 = time.perf_counter()
+        while (time.perf_counter() - t0) * 1e3 < a.spin_ms:
+            eng.render(64)
+        eng.close()
     rows = []
     for frames in (128, 256):
         rows.append(run(frames, a.periods, a.warmup, 0, tunings))
         print(json.dumps(rows[-1]), flush=True)
         rows.append(dict(run(frames, a.periods, a.warmup, 50, tunings), mode="retune every 50 periods"))
         print(json.dumps(rows[-1]), flush=True)
+    rows.append(dict(run(128, a.periods, a.warmup, 0, tunings), mode="128 frames again, last"))
+    print(json.dumps(rows[-1]), flush=True)
     res = {"what": "tbf_synth_sound wall-clock per period, 1 instance, 48 kHz, full chain",
+           "spin_ms": a.spin_ms, "warmup_periods": a.warmup,
            "host": os.uname().nodename, "gpu": torch.cuda.get_device_name(0), "rows": rows}
     if a.out:
         Path(a.out).write_text(json.dumps(res, indent=1) + "\n")

@@ -29,7 +29,8 @@ __global__ void __launch_bounds__ (256) tbf_calib_write_f64 (double* __restrict_
 		p[i] = (double)i;
 }
 
-/* test hook for tbf_sin (op 4): buf = n inputs, then tbf_sin of each, then sin of each */
+/* test hook for tbf_sin.h (op 4): buf = n inputs x, then tbf_sin (x), sin (x), tbf_sin2 (x, x'),
+ * asin fast path, asin (7 n doubles; x' = the input n / 2 further on) */
 __global__ void __launch_bounds__ (256) tbf_check_sin (double* __restrict__ p, uint64_t n)
 {
 	const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -38,6 +39,16 @@ __global__ void __launch_bounds__ (256) tbf_check_sin (double* __restrict__ p, u
 	const double x = p[i];
 	p[n + i]       = tbf_sin (x);
 	p[2 * n + i]   = sin (x);
+	/* tbf_sin2 on (x, the input n / 2 further on): its results must be the same bits */
+	const double x2 = p[(i + n / 2) % n];
+	double       r0, r1;
+	tbf_sin2 (x, x2, r0, r1);
+	p[3 * n + i] = r0;
+	p[4 * n + i] = r1;
+	/* asin: the polynomial branch where every lane is inside it, else the library */
+	const double y = fmin (fmax (x, -1.0), 1.0);
+	p[5 * n + i]   = __all (fabs (y) < 0.5) ? tbf_asin_poly (y) : asin (y);
+	p[6 * n + i]   = asin (y);
 }
 
 extern "C" int tbf_launch_calibrate (int op, void* buf, uint64_t n, hipStream_t s)
@@ -51,7 +62,7 @@ extern "C" int tbf_launch_calibrate (int op, void* buf, uint64_t n, hipStream_t 
 		hipLaunchKernelGGL (tbf_calib_read_f64, grid, block, 0, s, (const double*)buf + 8, n - 8, (double*)buf);
 	else if (op == 3) /* the write, likewise misaligned */
 		hipLaunchKernelGGL (tbf_calib_write_f64, grid, block, 0, s, (double*)buf + 8, n - 8);
-	else if (op == 4) /* tbf_sin against sin: n inputs, buffer of 3 n doubles */
+	else if (op == 4) /* tbf_sin.h against the library: n inputs, buffer of 7 n doubles */
 		hipLaunchKernelGGL (tbf_check_sin, dim3 ((unsigned)((n + 255) / 256)), block, 0, s, (double*)buf, n);
 	else
 		return -22;

@@ -36,6 +36,9 @@
 /* occupancy targets (waves per SIMD); LDS and VGPR budgets are sized for them */
 #define TG_WAVES 4
 #define TG_SPLIT_MAX 8 /* k_tonegen block ranges (waves) per instance */
+#ifndef TG_ABL
+#define TG_ABL 0 /* timing experiments (wrong output): 1 bank reads from one row, 2 no scanner */
+#endif
 #define TG_PCAP 128    /* a delta chunk's program entries staged in LDS per block (longer: read from HBM) */
 #define RV_WAVES 3
 /* k_whirl: 4 waves per SIMD (128 VGPRs, 9.8 KB of LDS: 16 instances per CU, so 4096 run
@@ -319,7 +322,11 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 			constexpr bool EN = decltype (EC)::value; /* the block has envelope entries */
 #pragma unroll
 			for (int k = 0; k < K; k++) {
+#if TG_ABL == 1 /* timing experiment only (wrong output): every entry reads the bank's first row */
+				const float* __restrict__ bp = P.bank + (sm.u.ent.base[e + k] & 63u);
+#else
 				const float* __restrict__ bp = P.bank + sm.u.ent.base[e + k];
+#endif
 				G.xs[k]                      = f2v {bp[lane], bp[lane + NL]};
 				if constexpr (EN) { /* (a steady entry loads row 0 of the attack table: an L1 hit) */
 					float    gg[6];
@@ -408,7 +415,11 @@ __device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl
 
 	const uint32_t routing = G.routing;
 	/* vibrato scanner, src/vibrato.cpp:365-411 */
+#if TG_ABL == 2 /* timing experiment only (wrong output): no scanner */
+	if (false) {
+#else
 	if (routing & 0x03) {
+#endif
 		const uint32_t* otab  = P.vibTab + 2048u * G.vibTable;
 		const uint32_t  out0  = st.outPos;
 		const uint32_t  stat0 = st.stator;
@@ -614,7 +625,8 @@ k_tonegen (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl, const tbf_tp
  *              alternate samples, so each covers half a tile).  One FP64 instruction stream
  *              advances 64 chains; a wave per instance served 2.
  *   wave 1     the preamp's xorshift dither stream (fpd), lane j = instance j
- *   waves 2..  lane-parallel work, two instances per task (a half-wave each): the gain
+ *   waves 2..  lane-parallel work, one instance per task and wave (MP_WIDE: 64-sample tiles;
+ *              else two instances per task, a half-wave each, 32-sample tiles): the gain
  *              products, the denormal guard, the waveshaper, blend and dither, the stores
  * Iteration it: the chases of tile it, the products of tile it - 1, the high-pass of tile
  * it - 2, the waveshaper of tile it - 3; one barrier per iteration.  Every chain runs the
@@ -623,19 +635,41 @@ k_tonegen (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl, const tbf_tp
 #ifndef MP_CB
 #define MP_CB 32                  /* instances per workgroup */
 #endif
+#ifndef MP_PROF
+#define MP_PROF 0 /* profiling variant: s_memtime per role and section (tools/mp_prof.py) */
+#endif
 #ifndef MP_ABL
 #define MP_ABL 0 /* timing experiments (wrong output): 1 no waveshaper, 2 no serial chains, 3 no dither */
 #endif
+#ifndef MP_SIN_PAIRS
+#define MP_SIN_PAIRS 0 /* the density sines in pairs (tbf_sin2) instead of one vote for all tasks */
+#endif
+#ifndef MP_WIDE
+#define MP_WIDE 1 /* tiles of 64 samples, a helper task = one instance (0: 32, an instance pair) */
+#endif
+#if MP_WIDE
+/* a tile is a whole wave of samples: each iteration gives a CU 2048 samples of waveshaper
+ * work (four density sines each, chains of dependent FP64 operations), eight chains per
+ * SIMD instead of four, which the 32-sample tiles left latency-bound (tools/mp_prof.py) */
+#define MP_T 64
+#define MP_NTK (MP_CB / MP_H)     /* helper tasks (instances) per tile */
+#define MP_XR 3                   /* preamp-input rows by tile mod 3 (tiles it-1 .. it-3 alive) */
+#define MP_CR 4                   /* control slots by block mod 4 (two tiles per block) */
+#else
 #define MP_T 32                   /* samples per tile: one per lane of a half-wave */
+#define MP_NTK (MP_CB / 2 / MP_H) /* helper tasks (instance pairs) per tile */
+#define MP_XR 4
+#define MP_CR 2
+#endif
 #define MP_S (MP_T + 1)           /* row stride of the per-sample rows (odd: conflict-free columns) */
 #define MP_HS (MP_T / 2 + 1)      /* row stride of the high-pass rows (a chain's MP_T / 2 samples) */
 #ifndef MP_H
 #define MP_H 8                    /* helper waves */
 #endif
-#define MP_NTK (MP_CB / 2 / MP_H) /* helper tasks (instance pairs) per tile */
 #define MP_THREADS (NL * (2 + MP_H))
 #define MP_TPB (TBF_BLK / MP_T)   /* tiles per block */
-static_assert (2 * MP_CB <= NL && 2 * MP_T == NL && MP_CB % (2 * MP_H) == 0, "k_mixpre geometry");
+static_assert (2 * MP_CB <= NL && (MP_WIDE ? MP_T == NL && MP_CB % MP_H == 0 : 2 * MP_T == NL && MP_CB % (2 * MP_H) == 0),
+               "k_mixpre geometry");
 #define MP_ROWS (2 * MP_CB + (2 * MP_CB < NL)) /* chain rows, + one that idle chain lanes write */
 
 /* one block's control of an instance as k_mixpre uses it, staged in LDS by the dither wave
@@ -673,11 +707,11 @@ __device__ __forceinline__ MpCtl mp_ctl (const tbf_seg_ctl& G)
 struct MixPreLds {
 	float    g[2][MP_ROWS][MP_S];    /* chase values before each sample, by tile parity: row 2j
 	                                  * keyCompLevel, 2j + 1 percEnvGain of instance j */
-	double   x[4][MP_ROWS][MP_HS];   /* preamp input (guarded), by tile mod 4: row 2j + q holds the
-	                                  * samples of instance j's high-pass chain q */
+	double   x[MP_XR][MP_ROWS][MP_HS]; /* preamp input (guarded), by tile mod MP_XR: row 2j + q holds the
+	                                    * samples of instance j's high-pass chain q */
 	double   h[2][MP_ROWS][MP_HS];   /* high-pass output, same rows, by tile parity */
 	uint32_t f[4][MP_CB][MP_S];      /* fpd before each sample (entry MP_T: after the tile), by tile mod 4 */
-	MpCtl    c[2][MP_CB];            /* the control of block b in slot b & 1 */
+	MpCtl    c[MP_CR][MP_CB];        /* the control of block b in slot b mod MP_CR */
 };
 
 /* the preamp after its high-pass (src/overdrive.cpp:117-168): density waveshaper, output
@@ -705,6 +739,75 @@ __device__ __forceinline__ float preamp_shape (double x, double dry, const MpCtl
 	if (C.wet < 1.0)
 		x = (dry * C.dry) + (x * C.wet);
 	return (float)dither_add (x, f1);
+}
+
+/* preamp_shape of a helper's NT tasks at once: the density loops run side by side (to the
+ * largest iteration count of the wave; a task past its own count keeps its value) with the
+ * sines of a step under one wave vote (tbf_sin_n), so the tasks' FP64 dependency chains
+ * interleave: a lone density loop is four sines in a row, ~1.2 k cycles each at two waves
+ * per SIMD, latency-bound.  The same operations per task as preamp_shape. */
+template <int NT>
+__device__ __forceinline__ void preamp_shape_n (const double (&x0)[NT], const double (&dry)[NT], const MpCtl* const (&C)[NT],
+                                                const uint32_t (&f1)[NT], float (&y)[NT])
+{
+	double x[NT];
+	int    itm = 0;
+	bool   dpos = true;
+#pragma unroll
+	for (int t = 0; t < NT; t++) {
+		x[t] = x0[t];
+		itm  = max (itm, C[t]->iter);
+		dpos = dpos && (C[t]->flags & MPF_DPOS);
+	}
+	const int itw = wave_max (itm);
+	for (int c = 0; c < itw; c++) {
+		double br[NT];
+#pragma unroll
+		for (int t = 0; t < NT; t++) {
+			br[t] = fabs (x[t]) * 1.57079633;
+			if (br[t] > 1.57079633)
+				br[t] = 1.57079633;
+		}
+#if MP_SIN_PAIRS
+#pragma unroll
+		for (int t = 0; t < NT; t += 2)
+			tbf_sin2 (br[t], br[t + 1], br[t], br[t + 1]);
+#else
+		tbf_sin_n<NT> (br);
+#endif
+#pragma unroll
+		for (int t = 0; t < NT; t++)
+			if (c < C[t]->iter)
+				x[t] = (x[t] > 0.0) ? br[t] : -br[t];
+	}
+	double br[NT];
+#pragma unroll
+	for (int t = 0; t < NT; t++) {
+		br[t] = fabs (x[t]) * 1.57079633;
+		if (br[t] > 1.57079633)
+			br[t] = 1.57079633;
+	}
+	if (__all (dpos)) {
+		tbf_sin_n<NT> (br);
+	} else {
+#pragma unroll
+		for (int t = 0; t < NT; t++)
+			br[t] = (C[t]->flags & MPF_DPOS) ? tbf_sin (br[t]) : 1 - cos (br[t]);
+	}
+#pragma unroll
+	for (int t = 0; t < NT; t++) {
+		const MpCtl& K = *C[t];
+		double       v = x[t];
+		if (v > 0)
+			v = (v * (1 - K.out)) + (br[t] * K.out);
+		else
+			v = (v * (1 - K.out)) - (br[t] * K.out);
+		if (K.output < 1.0)
+			v *= K.output;
+		if (K.wet < 1.0)
+			v = (dry[t] * K.dry) + (v * K.wet);
+		y[t] = (float)dither_add (v, f1[t]);
+	}
 }
 
 __global__ void __launch_bounds__ (MP_THREADS)
@@ -736,11 +839,17 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 		bool   rs = false, hp = false;
 		double ia = 0.0;
 		__syncthreads ();
+#if MP_PROF
+		unsigned long long sw0 = 0, sb0 = 0;
+#endif
 #pragma unroll 1
 		for (int it = 0; it < nIt; it++) {
+#if MP_PROF
+			const unsigned long long _s0 = __builtin_amdgcn_s_memtime ();
+#endif
 			if (it < nT) {
 				if (it % MP_TPB == 0) {
-					const MpCtl& C = sm.c[(it / MP_TPB) & 1][j];
+					const MpCtl& C = sm.c[(it / MP_TPB) % MP_CR][j];
 					m   = q ? ((C.flags & MPF_PERC) ? C.decay : 1.f) : 1.f;
 					a   = q ? 0.f : (C.keyCompTarget - v) / (float)TBF_BLK; /* keyCompDelta at the block start */
 					rs  = q && (C.flags & MPF_RST);
@@ -777,7 +886,7 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 			const int th = it - 2; /* the high-pass (src/overdrive.cpp:104-115) of tile th */
 			if (pre && th >= 0 && th < nT) {
 				if (th % MP_TPB == 0) {
-					const MpCtl& C = sm.c[(th / MP_TPB) & 1][j];
+					const MpCtl& C = sm.c[(th / MP_TPB) % MP_CR][j];
 					hp             = !(C.flags & MPF_CLEAN);
 					ia             = C.iir;
 				}
@@ -786,7 +895,7 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 #else
 				if (hp) {
 #endif
-					const double* xr = sm.x[th & 3][cl];
+					const double* xr = sm.x[th % MP_XR][cl];
 					double*       hr = sm.h[th & 1][cl];
 					const double  om = 1.0 - ia;
 					PRIO_UP ();
@@ -805,8 +914,21 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 					PRIO_DOWN ();
 				}
 			}
+#if MP_PROF
+			const unsigned long long _s1 = __builtin_amdgcn_s_memtime ();
+			sw0 += _s1 - _s0;
+#endif
 			__syncthreads ();
+#if MP_PROF
+			sb0 += __builtin_amdgcn_s_memtime () - _s1;
+#endif
 		}
+#if MP_PROF
+		if (blockIdx.x == 0 && lane == 0) {
+			P.outL[P.outOffset + 8] = (float)(sw0 * 1e-3);
+			P.outL[P.outOffset + 9] = (float)(sb0 * 1e-3);
+		}
+#endif
 		if (ok) {
 			if (q) {
 				M->percEnvGain = v;
@@ -819,8 +941,8 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 		return;
 	}
 	if (w == 1) {
-		/* the control staging (block b into slot b & 1 at iteration 4 b - 1, from registers
-		 * loaded a block earlier) and the dither stream: it advances once per sample of every
+		/* the control staging (block b into slot b mod MP_CR at iteration MP_TPB b - 1, from
+		 * registers loaded a block earlier) and the dither stream: it advances once per sample of every
 		 * block the preamp runs (src/overdrive.cpp:153-159), f[n] = the state before sample
 		 * n's step */
 		const bool     ok   = lane < nj;
@@ -835,8 +957,14 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 		}
 		bool adv = false;
 		__syncthreads ();
+#if MP_PROF
+		unsigned long long dw0 = 0, db0 = 0;
+#endif
 #pragma unroll 1
 		for (int it = 0; it < nIt; it++) {
+#if MP_PROF
+			const unsigned long long _d0 = __builtin_amdgcn_s_memtime ();
+#endif
 			if (lane < MP_CB) {
 #if MP_ABL == 3 /* timing experiment only (wrong output): no dither stream */
 				if (false) {
@@ -844,7 +972,7 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 				if (pre && it < nT) {
 #endif
 					if (it % MP_TPB == 0)
-						adv =!(sm.c[(it / MP_TPB) & 1][lane].flags & MPF_CLEAN);
+						adv =!(sm.c[(it / MP_TPB) % MP_CR][lane].flags & MPF_CLEAN);
 					uint32_t* f = sm.f[it & 3][lane];
 #pragma unroll 8
 					for (int n = 0; n < MP_T; n++) {
@@ -855,21 +983,34 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 				}
 				const int b = (it + 1) / MP_TPB; /* the block starting at the next iteration */
 				if ((it + 1) % MP_TPB == 0 && b < nB) {
-					sm.c[b & 1][lane] = nxt;
+					sm.c[b % MP_CR][lane] = nxt;
 					nxt               = mp_ctl (ctl_of (P, ctl, (uint32_t)min (b + 1, nB - 1), inst));
 				}
 			}
+#if MP_PROF
+			const unsigned long long _d1 = __builtin_amdgcn_s_memtime ();
+			dw0 += _d1 - _d0;
+#endif
 			__syncthreads ();
+#if MP_PROF
+			db0 += __builtin_amdgcn_s_memtime () - _d1;
+#endif
 		}
+#if MP_PROF
+		if (blockIdx.x == 0 && lane == 0) {
+			P.outL[P.outOffset + 16] = (float)(dw0 * 1e-3);
+			P.outL[P.outOffset + 17] = (float)(db0 * 1e-3);
+		}
+#endif
 		if (ok && pre && lane < MP_CB)
 			M->odFpd = fs;
 		return;
 	}
-	/* helpers: task t = instances 2 (h + MP_H t) + {0, 1}, half-wave hj each; lane n of the
-	 * half-wave = sample n of the tile.  The (s, p) input is read two iterations before its
-	 * use, into two register sets alternating by iteration parity (the loop is unrolled by
-	 * two, so the sets stay static) */
-	const int     h = w - 2, hj = lane >> 5, n = lane & (MP_T - 1);
+	/* helpers: task t = instance h + MP_H t, lane n = sample n of the tile (MP_WIDE; else
+	 * instances 2 (h + MP_H t) + {0, 1}, half-wave hj each, lane n of the half-wave = sample n).
+	 * The (s, p) input is read two iterations before its use, into two register sets
+	 * alternating by iteration parity (the loop is unrolled by two, so the sets stay static) */
+	const int     h = w - 2, hj = MP_WIDE ? 0 : lane >> 5, n = lane & (MP_T - 1);
 	const float2* in[MP_NTK];
 	float*        o1[MP_NTK];
 	float*        oL[MP_NTK];
@@ -879,7 +1020,7 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 	float2        pS[2][MP_NTK];
 #pragma unroll
 	for (int t = 0; t < MP_NTK; t++) {
-		const int j       = 2 * (h + MP_H * t) + hj;
+		const int j       = MP_WIDE ? h + MP_H * t : 2 * (h + MP_H * t) + hj;
 		okT[t]            = j < nj;
 		jT[t]             = okT[t] ? j : nj - 1;
 		const uint32_t is = inst0 + jT[t];
@@ -895,26 +1036,65 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 		pS[1][t]          = in[t][(size_t)min (1, nT - 1) * MP_T];
 	}
 	const bool tap = P.chain == TBF_CHAIN_TAP_PREAMP;
+#if MP_PROF /* profiling variant only: s_memtime per helper section, written over instance 0's output */
+	unsigned long long pf[3] = {0, 0, 0};
+#define MP_T0() const unsigned long long _t0 = __builtin_amdgcn_s_memtime ()
+#define MP_TS(i, a) { asm volatile ("" ::: "memory"); const unsigned long long _t = __builtin_amdgcn_s_memtime (); pf[i] += _t - (a); }
+#else
+#define MP_T0()
+#define MP_TS(i, a)
+#endif
 	__syncthreads ();
 	auto step = [&] (const int it, float2 (&qS)[MP_NTK]) {
+		MP_T0 ();
 		/* the waveshaper of tile it - 3: high-pass output, dry input, the dither state after
 		 * the sample's step */
 		const int kw = it - 3;
 		if (pre && kw >= 0 && kw < nT) {
 			const size_t so = (size_t)kw * MP_T;
+#if MP_NTK > 1
+			/* the tasks' waveshapers side by side (preamp_shape_n) */
+			float ys[MP_NTK];
+			{
+				const MpCtl* Cp[MP_NTK];
+				double       xd[MP_NTK], xh[MP_NTK];
+				uint32_t     f1[MP_NTK];
+				bool         cl[MP_NTK];
+				bool         allCl = true;
+#pragma unroll
+				for (int t = 0; t < MP_NTK; t++) {
+					Cp[t] = &sm.c[(kw / MP_TPB) % MP_CR][jT[t]];
+					xd[t] = sm.x[kw % MP_XR][rT[t]][n >> 1];
+					xh[t] = sm.h[kw & 1][rT[t]][n >> 1];
+					f1[t] = sm.f[kw & 3][jT[t]][n + 1];
+#if MP_ABL == 1 /* timing experiment only (wrong output): helpers without the waveshaper */
+					cl[t] = true;
+#else
+					cl[t] = (Cp[t]->flags & MPF_CLEAN) != 0;
+#endif
+					allCl = allCl && cl[t];
+				}
+				if (!__all (allCl))
+					preamp_shape_n<MP_NTK> (xh, xd, Cp, f1, ys);
+#pragma unroll
+				for (int t = 0; t < MP_NTK; t++)
+					if (cl[t])
+						ys[t] = (float)xd[t];
+			}
+#endif
 #pragma unroll
 			for (int t = 0; t < MP_NTK; t++) {
-				const MpCtl& C  = sm.c[(kw / MP_TPB) & 1][jT[t]];
-				const double xd = sm.x[kw & 3][rT[t]][n >> 1];
-				float        y;
-#if MP_ABL == 1 /* timing experiment only (wrong output): helpers without the waveshaper */
-				if (true)
+#if MP_NTK > 1
+				const float y = ys[t];
 #else
+				const MpCtl& C  = sm.c[(kw / MP_TPB) % MP_CR][jT[t]];
+				const double xd = sm.x[kw % MP_XR][rT[t]][n >> 1];
+				float        y;
 				if (C.flags & MPF_CLEAN)
-#endif
 					y = (float)xd;
 				else
 					y = preamp_shape (sm.h[kw & 1][rT[t]][n >> 1], xd, C, sm.f[kw & 3][jT[t]][n + 1]);
+#endif
 				if (okT[t]) {
 					if (tap) {
 						oL[t][so] = y;
@@ -924,13 +1104,17 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 				}
 			}
 		}
+#if MP_PROF
+		const unsigned long long _t1 = __builtin_amdgcn_s_memtime ();
+		pf[0] += _t1 - _t0;
+#endif
 		/* the products of tile it - 1 (src/tonegen.cpp:3734-3777) and the preamp input:
 		 * denormal guard with the dither state before the sample (src/overdrive.cpp:95-100) */
 		const int kp = it - 1;
 		if (kp >= 0 && kp < nT) {
 #pragma unroll
 			for (int t = 0; t < MP_NTK; t++) {
-				const MpCtl& C  = sm.c[(kp / MP_TPB) & 1][jT[t]];
+				const MpCtl& C  = sm.c[(kp / MP_TPB) % MP_CR][jT[t]];
 				const float  kc = sm.g[kp & 1][2 * jT[t]][n];
 				const float  pe = sm.g[kp & 1][2 * jT[t] + 1][n];
 				const float2 sp = qS[t];
@@ -944,7 +1128,7 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 					double x = (double)y;
 					if (!(C.flags & MPF_CLEAN) && fabs (x) < 1.18e-23)
 						x = sm.f[kp & 3][jT[t]][n] * 1.18e-17;
-					sm.x[kp & 3][rT[t]][n >> 1] = x;
+					sm.x[kp % MP_XR][rT[t]][n >> 1] = x;
 				}
 			}
 		}
@@ -954,7 +1138,12 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 #pragma unroll
 		for (int t = 0; t < MP_NTK; t++)
 			qS[t] = in[t][(size_t)tl * MP_T];
+#if MP_PROF
+		const unsigned long long _t2 = __builtin_amdgcn_s_memtime ();
+		pf[1] += _t2 - _t1;
+#endif
 		__syncthreads ();
+		MP_TS (2, _t2);
 	};
 #pragma unroll 1
 	for (int it = 0; it < nIt; it += 2) {
@@ -962,6 +1151,13 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 		if (it + 1 < nIt)
 			step (it + 1, pS[0]);
 	}
+#if MP_PROF
+	if (blockIdx.x == 0 && h == 0 && lane == 0)
+		for (int i = 0; i < 3; i++)
+			P.outL[P.outOffset + i] = (float)(pf[i] * 1e-3);
+#endif
+#undef MP_T0
+#undef MP_TS
 }
 
 /* ================================================================== reverb */
@@ -1900,10 +2096,20 @@ k_rv_pre (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 		/* sin (x * wet) of tile it - 2 */
 		if (it >= 2) {
 			const int k2 = it - 2;
+			double    sx[RVC_NTK];
+#pragma unroll
+			for (int t = 0; t < RVC_NTK; t++)
+				sx[t] = sv[t] * rld (wetv[t], blk_lane ((k2 * RVC_T) / TBF_BLK));
+			/* the tasks' sines in pairs (tbf_sin2: their chains interleave) */
+#pragma unroll
+			for (int t = 0; t + 1 < RVC_NTK; t += 2)
+				tbf_sin2 (sx[t], sx[t + 1], sx[t], sx[t + 1]);
+			if (RVC_NTK & 1)
+				sx[RVC_NTK - 1] = tbf_sin (sx[RVC_NTK - 1]);
 #pragma unroll
 			for (int t = 0; t < RVC_NTK; t++)
 				if (h + t * RVC_H < nj)
-					ra[t][(size_t)k2 * RVC_T] = tbf_sin (sv[t] * rld (wetv[t], blk_lane ((k2 * RVC_T) / TBF_BLK)));
+					ra[t][(size_t)k2 * RVC_T] = sx[t];
 		}
 		__syncthreads ();
 	};
@@ -2079,14 +2285,27 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 			qIn[t] = in[t][(size_t)ti * RVC_T];
 		}
 		if (it >= 2 && it - 2 < nT) {
+			double y[RVC_NTK];
+			bool   small = true;
 #pragma unroll
 			for (int t = 0; t < RVC_NTK; t++) {
-				double y = av[t];
-				if (y > 1.0)
-					y = 1.0;
-				if (y < -1.0)
-					y = -1.0;
-				sm.z[b][2 * (h + t * RVC_H) + hc][n] = asin (y);
+				y[t] = av[t];
+				if (y[t] > 1.0)
+					y[t] = 1.0;
+				if (y[t] < -1.0)
+					y[t] = -1.0;
+				small = small && fabs (y[t]) < 0.5;
+			}
+			/* every task's value inside OCML asin's polynomial branch (the tap mix is small):
+			 * that branch alone, straight-line, so the tasks' chains interleave (tbf_sin.h) */
+			if (__all (small)) {
+#pragma unroll
+				for (int t = 0; t < RVC_NTK; t++)
+					sm.z[b][2 * (h + t * RVC_H) + hc][n] = tbf_asin_poly (y[t]);
+			} else {
+#pragma unroll
+				for (int t = 0; t < RVC_NTK; t++)
+					sm.z[b][2 * (h + t * RVC_H) + hc][n] = asin (y[t]);
 			}
 		}
 		if (it >= 4) {

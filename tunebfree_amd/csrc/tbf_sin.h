@@ -88,11 +88,27 @@ __device__ __forceinline__ double tbf_sign_of (double r, double x)
 	return __builtin_bit_cast (double, __builtin_bit_cast (uint64_t, r) ^ s);
 }
 
+/* __ocml_sin_f64 for |x| < 2^30 (the trigredsmall branch): both polynomials, the one n & 1
+ * selects, the sign flipped for n & 2 and for negative x */
+__device__ __forceinline__ double tbf_sin_small (double x, double a, double n)
+{
+	double hi, lo;
+	tbf_trigred_small (a, n, hi, lo);
+	const double   s = tbf_sinred (hi, lo), c = tbf_cosred (hi, lo);
+	const int      q = (int)n & 3;
+	const uint64_t r = __builtin_bit_cast (uint64_t, (q & 1) ? c : s);
+	const uint64_t f = (q > 1 ? 0x8000000000000000ull : 0ull) ^ (__builtin_bit_cast (uint64_t, x) & 0x8000000000000000ull);
+	return __builtin_bit_cast (double, r ^ f);
+}
+
+#define TBF_N(a) __builtin_rint ((a) * TBF_D (0x3FE45F306DC9C883))
+#define TBF_SMALL(a) ((a) < TBF_D (0x41D0000000000000)) /* 2^30; false for NaN (OCML's test) */
+
 /* sin (x), OCML's bits, with the wave-uniform fast paths above */
 __device__ __forceinline__ double tbf_sin (double x)
 {
 	const double a = fabs (x);
-	const double n = __builtin_rint (a * TBF_D (0x3FE45F306DC9C883));
+	const double n = TBF_N (a);
 	if (__all (n == 0.0))
 		return tbf_sign_of (tbf_sinred (a, 0.0), x);
 	if (__all (n == 1.0)) {
@@ -100,9 +116,95 @@ __device__ __forceinline__ double tbf_sin (double x)
 		tbf_trigred_small (a, 1.0, hi, lo);
 		return tbf_sign_of (tbf_cosred (hi, lo), x);
 	}
+	if (__all (TBF_SMALL (a)))
+		return tbf_sin_small (x, a, n);
 	return sin (x);
 }
 
+/* two independent sines at once: one wave vote for both, and straight-line code on every
+ * path, so the compiler interleaves the two dependency chains (a lone sine is a chain of
+ * ~20 dependent FP64 operations, latency-bound at two waves per SIMD) */
+__device__ __forceinline__ void tbf_sin2 (double x0, double x1, double& r0, double& r1)
+{
+	const double a0 = fabs (x0), a1 = fabs (x1);
+	const double n0 = TBF_N (a0), n1 = TBF_N (a1);
+	if (__all (n0 == 0.0 && n1 == 0.0)) {
+		r0 = tbf_sign_of (tbf_sinred (a0, 0.0), x0);
+		r1 = tbf_sign_of (tbf_sinred (a1, 0.0), x1);
+	} else if (__all (n0 == 1.0 && n1 == 1.0)) {
+		double h0, l0, h1, l1;
+		tbf_trigred_small (a0, 1.0, h0, l0);
+		tbf_trigred_small (a1, 1.0, h1, l1);
+		r0 = tbf_sign_of (tbf_cosred (h0, l0), x0);
+		r1 = tbf_sign_of (tbf_cosred (h1, l1), x1);
+	} else if (__all (TBF_SMALL (a0) && TBF_SMALL (a1))) {
+		r0 = tbf_sin_small (x0, a0, n0);
+		r1 = tbf_sin_small (x1, a1, n1);
+	} else {
+		r0 = sin (x0);
+		r1 = sin (x1);
+	}
+}
+
+/* N independent sines in place, one wave vote for all of them (tbf_sin2 for N values) */
+template <int N>
+__device__ __forceinline__ void tbf_sin_n (double (&x)[N])
+{
+	double a[N], n[N];
+	bool   z = true, o = true, sm = true;
+#pragma unroll
+	for (int i = 0; i < N; i++) {
+		a[i] = fabs (x[i]);
+		n[i] = TBF_N (a[i]);
+		z    = z && n[i] == 0.0;
+		o    = o && n[i] == 1.0;
+		sm   = sm && TBF_SMALL (a[i]);
+	}
+	if (__all (z)) {
+#pragma unroll
+		for (int i = 0; i < N; i++)
+			x[i] = tbf_sign_of (tbf_sinred (a[i], 0.0), x[i]);
+	} else if (__all (o)) {
+#pragma unroll
+		for (int i = 0; i < N; i++) {
+			double hi, lo;
+			tbf_trigred_small (a[i], 1.0, hi, lo);
+			x[i] = tbf_sign_of (tbf_cosred (hi, lo), x[i]);
+		}
+	} else if (__all (sm)) {
+#pragma unroll
+		for (int i = 0; i < N; i++)
+			x[i] = tbf_sin_small (x[i], a[i], n[i]);
+	} else {
+#pragma unroll
+		for (int i = 0; i < N; i++)
+			x[i] = sin (x[i]);
+	}
+}
+
+/* __ocml_asin_f64's |x| < 0.5 branch: the polynomial in x^2 */
+__device__ __forceinline__ double tbf_asin_poly (double x)
+{
+	const double a  = fabs (x);
+	const double t  = x * x;
+	double       p  = __builtin_fma (t, TBF_D (0x3FA059859FEA6A70), TBF_D (0xBF90A5A378A05EAF));
+	p               = __builtin_fma (t, p, TBF_D (0x3F94052137024D6A));
+	p               = __builtin_fma (t, p, TBF_D (0x3F7AB3A098A70509));
+	p               = __builtin_fma (t, p, TBF_D (0x3F88ED60A300C8D2));
+	p               = __builtin_fma (t, p, TBF_D (0x3F8C6FA84B77012B));
+	p               = __builtin_fma (t, p, TBF_D (0x3F91C6C111DCCB70));
+	p               = __builtin_fma (t, p, TBF_D (0x3F96E89F0A0ADACF));
+	p               = __builtin_fma (t, p, TBF_D (0x3F9F1C72C668963F));
+	p               = __builtin_fma (t, p, TBF_D (0x3FA6DB6DB41CE4BD));
+	p               = __builtin_fma (t, p, TBF_D (0x3FB333333336FD5B));
+	p               = __builtin_fma (t, p, TBF_D (0x3FC5555555555380));
+	const double s  = t * p;
+	const double r  = __builtin_fma (a, s, a);
+	return __builtin_copysign (r, x);
+}
+
+#undef TBF_SMALL
+#undef TBF_N
 #undef TBF_D
 
 #endif

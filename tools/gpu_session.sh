@@ -56,7 +56,12 @@ for s in $STEPS; do
 		run cfg5 300 python3 bench.py --workload cfg5 --cpu-baseline 0 --check 8
 		run dense 500 python3 -u tools/dense_events.py --out "$OUT/dense_events.json"
 		run rt 300 python3 -u tools/rt_latency.py --out "$OUT/rt_latency.json"
+		run rt_nospin 300 python3 -u tools/rt_latency.py --spin-ms 0 --warmup 200 --out "$OUT/rt_latency_nospin.json"
 		;;
+	steady) # the bench at 2048-block steps with the steady chunk capped (stage-buffer footprint vs speed)
+		for c in 256 512 1024 2048; do
+			run "steady$c" 400 env TBF_STEADY_CHUNK=$c python3 bench.py --cpu-baseline 0 --check 0 --stage-check 0 --steps 10 --warmup 3 --isolated 0 --steady64 0
+		done ;;
 	bench) run bench 300 python3 bench.py --cpu-baseline 0 ;;
 	bench2048x2) # two driver-length benches (A/B baseline on one box)
 		run bench_a 400 python3 bench.py --cpu-baseline 0 --steps 20 --warmup 5

@@ -471,7 +471,7 @@ def main():
 
     kern, kern_iso, max_err, exact, per_stage, steady64 = {}, None, None, None, None, None
     # launch sets per step: the timed steps have no control deltas, so each chunk is up to the
-    # engine's steady chunk (TBF_STEADY_CHUNK, default TBF_STEADY_MAX = 2048 blocks; 64 with deltas)
+    # engine's steady chunk (TBF_STEADY_CHUNK, default TBF_STEADY_DEFAULT = 512 blocks; 64 with deltas)
     chunk = eng.chunks()[1] if not a.dry_run else 64
     launches = -(-a.blocks // chunk)
     ksteps = a.steps if a.kernel_steps is None else a.kernel_steps
@@ -500,6 +500,7 @@ def main():
         if a.steady64 and a.blocks > 64:
             # the same steps in 64-block chunks (every launch 64 blocks, as a workload with an
             # event at least every 64 blocks renders): one warmup step, then a.steady64 timed
+            chunk0 = eng.chunks()[1]
             eng.set_steady_chunk(64)
             step()
             sync()
@@ -508,7 +509,7 @@ def main():
                 step()
             sync()
             t64 = time.perf_counter() - t64
-            eng.set_steady_chunk(2048)
+            eng.set_steady_chunk(chunk0)
             steady64 = {"ms_per_64_blocks": t64 / a.steady64 / (a.blocks / 64) * 1e3,
                         "value": B * nsamp * a.steady64 / t64, "steps": a.steady64,
                         "note": "rank-local: the same render with every chunk 64 blocks long "

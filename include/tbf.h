@@ -258,9 +258,9 @@ int tbf_debug_chunks (const tbf_engine* e, uint32_t* delta_blocks, uint32_t* ste
 /* chunks with events since the engine was created, by the front end that stepped them:
  * the device's (k_front) and the host's */
 int tbf_debug_front_chunks (const tbf_engine* e, uint64_t* device_chunks, uint64_t* host_chunks);
-/* the longest render chunk without control deltas, in blocks (64 .. 2048, default 2048).
- * The stage buffers hold one chunk per instance (about 68 B per instance and sample at the
- * default stage groups: 73 GB at 4096 instances and 2048 blocks, 9.1 GB at 256 blocks) and
+/* the longest render chunk without control deltas, in blocks (64 .. 2048, default 512).
+ * The stage buffers hold one chunk per instance (56 B per instance and sample at the
+ * default stage groups: 15 GB at 4096 instances and 512 blocks, 60 GB at 2048) and
  * grow to the longest chunk a call makes, so this bounds the engine's HBM footprint; longer
  * chunks spread each launch's state traffic over more samples.  The
  * engine lowers it by itself when the device cannot hold the buffers.  Takes effect at the

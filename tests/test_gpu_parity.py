@@ -668,12 +668,12 @@ def test_gpu_device_front_end_effect_events(oracle):
 
 def test_gpu_steady_chunks(oracle):
     """A chunk in which no instance's control changes (every block plays each instance's
-    current entry) runs up to TBF_STEADY_CHUNK blocks (default TBF_STEADY_MAX = 2048) per
+    current entry) runs up to TBF_STEADY_CHUNK blocks (default 512, at most 2048) per
     launch instead of 64, and ends at the next event's block.  Events at blocks 0..48
     (chords, drawbars, rotary, a note-off), then a reverb change and a whirl bypass toggle
     at blocks 300 / 330 / 340 inside one 450-block call, and a second call of 2100 blocks
-    (one whole 2048-block chunk and a remainder): bit for bit the render of 64-block chunks
-    (TBF_STEADY_CHUNK=64), and the oracle."""
+    (four default 512-block chunks and a remainder; one 2048-block chunk at TBF_STEADY_CHUNK=2048):
+    bit for bit the render of 64-block chunks (TBF_STEADY_CHUNK=64), and the oracle."""
     import os
     import torch
     import tunebfree_amd as T
@@ -688,7 +688,7 @@ def test_gpu_steady_chunks(oracle):
     rows = sorted(((b, i, 0 if k == "note" else 1, a, float(v)) for i, sc in enumerate(oscen) for (b, k, a, v) in sc),
                   key=lambda r: r[0])
     outs = []
-    for steady in (None, "64"):
+    for steady in (None, "2048", "64"):
         if steady:
             os.environ["TBF_STEADY_CHUNK"] = steady
         try:
@@ -706,8 +706,9 @@ def test_gpu_steady_chunks(oracle):
         outs.append((L.cpu().numpy(), R.cpu().numpy()))
         eng.close()
         del L, R
-    assert np.array_equal(outs[0][0].view(np.uint32), outs[1][0].view(np.uint32))
-    assert np.array_equal(outs[0][1].view(np.uint32), outs[1][1].view(np.uint32))
+    for o in outs[:2]:
+        assert np.array_equal(o[0].view(np.uint32), outs[2][0].view(np.uint32))
+        assert np.array_equal(o[1].view(np.uint32), outs[2][1].view(np.uint32))
     sample = [0, 3, 5, 10, n - 1]
     tpl = Template(oracle, seed=7)
     oL, oR, *_ = oracle_run(oracle, tpl, [seeds[i] for i in sample], [sorted(oscen[i], key=lambda r: r[0]) for i in sample],

@@ -22,7 +22,9 @@ mark = lambda k: f"\n\t\tif (threadIdx.x == 0) {{ const unsigned long long _t = 
 # block start (whirl_speed) and per-sub-block phases
 s = ins_after(s, "\t\tsm.brake = brake;\n\t}\n\twave_sync ();", mark(9))
 s = ins_after(s, "\t\twave_sync ();\n\t\tif (!sm.aReady) {", mark(1).replace("\n\t\t", "\n\t\t\t"))
-s = ins_after(s, "\t\t\t\twh_serial<false> (row + (lane < 2 ? 0u : wb), 0u, 0u, st.fz[lane], fa0, fa1, lane == 0 && scrubA);\n\t\t}\n\t\twave_sync ();", mark(3))
+s = ins_after(s, "\t\t}\n\t\twave_sync ();\n\t\t/* the filter outputs: horn B -> xf", "", 1)
+s = s.replace("\t\t}\n\t\twave_sync ();\n\t\t/* the filter outputs: horn B -> xf",
+              "\t\t}\n\t\twave_sync ();" + mark(3) + "\n\t\t/* the filter outputs: horn B -> xf", 1)
 s = ins_after(s, "\t\t\t\tst.drumAngle = de;\n\t\t\t}\n\t\t}\n\t\twave_sync ();", mark(4))
 s = ins_after(s, "\t\tconst float xd2v = (float)((0.4 * xd1v) + (0.4 * xd1p));\n\t\twave_sync ();", mark(5))
 s = s.replace("\t\t\tbool okr[WH_RG];", mark(6).replace("\n\t\t", "\n\t\t\t") + "\n\t\t\tbool okr[WH_RG];")

@@ -2000,14 +2000,15 @@ static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0
 /* The inter-stage buffers for a call of nblocks blocks: each holds, per instance, one
  * chunk of stageBlocks blocks -- a power of two from TBF_CHUNK up to steadyChunk, just
  * enough for the longest chunk this call can make, so a caller that renders 64 blocks at a
- * time never pays for 2048-block chunks (n x blocks x 128 x 68 B at the default stage
- * groups: 73 GB at 4096 instances and 2048 blocks, 2.3 GB at 64).  They only grow (a
+ * time never pays for longer chunks (n x blocks x 128 x 56 B at the default stage
+ * groups: 15 GB at 4096 instances and the default 512-block chunks, 60 GB at 2048, 1.9 GB
+ * at 64).  They only grow (a
  * different stride under chunks still in flight would be wrong), after every launch that
  * may read them has finished.  When the device cannot hold them, the chunk halves down to
  * TBF_CHUNK before the call fails, and steadyChunk stays at what fitted.  A buffer whose
  * producer and every reader run on one stage-group stream is single: the next chunk's
- * producer is ordered behind this chunk's readers by the stream (default groups {0,0,1,1,2,2}:
- * mid0, rvA and mid2 single; mid1, rvB by chunk parity). */
+ * producer is ordered behind this chunk's readers by the stream (default groups {0,0,1,1,1,2}:
+ * mid0, rvA and rvB single; mid1, mid2 by chunk parity). */
 static int stageBuffers (tbf_engine* e, uint32_t n, uint32_t nblocks, hipStream_t s)
 {
 	uint32_t want = TBF_CHUNK;

@@ -342,15 +342,19 @@ struct tbf_engine {
 	uint64_t                                chunkSeq = 0;
 	bool                                    stagesBusy = false; /* pipelined work may be outstanding */
 	bool                                    pipeline = true;    /* TBF_PIPELINE=0 disables */
-	int                                     grp[TBF_NSTAGES] = {0, 0, 1, 1, 2, 2}; /* TBF_PIPE_GROUPS */
+	/* stage k's stream (TBF_PIPE_GROUPS): k_tonegen + k_mixpre | k_rv_pre + k_rv_core + k_rv_post |
+	 * k_whirl.  Against {0,0,1,1,2,2}: rvB single (its producer and reader share a stream),
+	 * mid2 by parity, 56 instead of 68 B per stereo sample, and the step 131.7 -> 128.3 ms
+	 * (profiles/r05/s20_groups) */
+	int                                     grp[TBF_NSTAGES] = {0, 0, 1, 1, 1, 2};
 	bool                                    rvLdsOn  = true;  /* k_rv_core_lds when the rings fit (TBF_RV_LDS=0: k_rv_core) */
 	bool                                    rvLdsFit = false; /* the instances' rings fit k_rv_core_lds */
 	uint32_t                                rvGrid   = 0;     /* k_rv_core_lds persistent workgroups (TBF_RV_PERSIST=0: one per pair) */
 	DevBuf<uint32_t>                        rvWork;           /* its work counter */
 	DevBuf<uint8_t>                         mixFixed;         /* tonegen only: k_tonegen wrote the output (tbf_launch.mixFixed) */
 	int                                     tgSplit  = -1;    /* k_tonegen block ranges (TBF_TG_SPLIT; -1: by batch size) */
-	uint32_t                                steadyChunk = TBF_STEADY_MAX; /* blocks per chunk without control deltas (TBF_STEADY_CHUNK,
-	                                                                       * tbf_set_steady_chunk) */
+	uint32_t                                steadyChunk = TBF_STEADY_DEFAULT; /* blocks per chunk without control deltas (TBF_STEADY_CHUNK,
+	                                                                           * tbf_set_steady_chunk) */
 	/* the stage buffers as allocated (stageBuffers): blocks per chunk they hold (a power of two
 	 * from TBF_CHUNK up to steadyChunk, grown to the longest chunk a call can make, never past
 	 * what the device could allocate), for stageN instances; a buffer whose producer and

@@ -38,7 +38,7 @@ TBF_HD bool phase_run (double v0, double d, int m, double& D)
 	frexp (v0, &e);
 	const double u  = ldexp (1.0, e - 53);
 	const double lo = ldexp (1.0, e - 1) + u, hi = ldexp (1.0, e) - u;
-	const double k  = d / u;
+	const double k  = ldexp (d, 53 - e); /* d / u: u is a power of two, so the same correctly rounded value without a division */
 	const double r  = rint (k);
 	if (fabs (k - r) == 0.5)
 		return false;

@@ -60,7 +60,9 @@
 #define WH_SERIAL_PIPE 1 /* k_whirl serial passes: next group's reads ahead of this group's chain */
 #endif
 #ifndef WH_PAD
-#define WH_PAD 1 /* floats after each LDS ring / horn-A row: rows of one serial pass on different banks */
+/* floats after each LDS ring / horn-A row: the rows of one serial pass 16-B aligned (its
+ * 4-sample reads and writes) and each lane's 16 B on banks of its own */
+#define WH_PAD 4
 #endif
 /* wave priority raised (s_setprio 1) while a wave runs a serial chain, so the SIMD issues
  * the chain's dependent instructions ahead of other waves' lane-parallel work */
@@ -101,14 +103,14 @@ struct TgLds {
 template <int W>
 struct WhLds {
 	tbf_wh_state st;
-	float        wring[4][W + WH_PAD]; /* rows padded: the serial lanes 2, 3 read rings 2, 3 at the same index */
+	alignas (16) float wring[4][W + WH_PAD]; /* rows padded: the serial lanes 2, 3 read rings 2, 3 at the same index */
 	float        xf[TBF_SUB + 4];
 	float        x1[TBF_SUB + 4];
 	float        x2[TBF_SUB + 4];
 	/* horn A rows by parity ap: ab[ap] takes the next sub-block's input and horn A filters
 	 * it in place (A runs one sub-block ahead), ab[ap ^ 1] holds A's output of this
 	 * sub-block, horn B's input */
-	float        ab[2][TBF_SUB + WH_PAD];
+	alignas (16) float ab[2][TBF_SUB + WH_PAD];
 	int          brake;
 	int          aReady; /* ab[ap ^ 1] holds this sub-block's horn A output */
 	int          ap;
@@ -2595,16 +2597,17 @@ __device__ __forceinline__ void motion_add (float* ring, int U, float a, float b
 /* One pass of motion_add over a group of RG rings (motion q of each): every lane reads its
  * two slots of every ring, then the owners write them.  So the rings' reads go out
  * together and the pass costs one LDS round trip.  The owner and neighbour relations of
- * motion_own are lane masks here: two compares against the previous lane's slot give
- * eq (U_n == U_n-1) and s1 (U_n == U_n-1 + 1), and every other relation is a shift of
- * those (pair: eq of the next lane, lead2: eq of the previous one, own2: s1 of the lane
- * after the group), so they cost scalar instructions and the selects take them as lane
- * masks.  The same adds in the same order as motion_add. */
+ * motion_own are lane masks here: the fast path's precondition vote already compared each
+ * slot with the previous lane's, eqm (U_n == U_n-1) and s1m (U_n == U_n-1 + 1), and every
+ * other relation is a shift of those (pair: eq of the next lane, lead2: eq of the previous
+ * one, own2: s1 of the lane after the group), so they cost scalar instructions and the
+ * selects take them as lane masks.  The same adds in the same order as motion_add. */
 __device__ __forceinline__ bool lane_in (uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64 (m); }
 
 template <int W, int RG>
 __device__ __forceinline__ void motion_pass (float (*ring)[W + WH_PAD], const int (&mu)[RG][3], const float (&ma)[RG][3],
-                                             const float (&mb)[RG][3], const int q)
+                                             const float (&mb)[RG][3], const uint64_t (&eqm)[RG][3],
+                                             const uint64_t (&s1m)[RG][3], const int q)
 {
 	const uint32_t WM = (uint32_t)W - 1u;
 	uint32_t       i0[RG], i1[RG];
@@ -2618,24 +2621,18 @@ __device__ __forceinline__ void motion_pass (float (*ring)[W + WH_PAD], const in
 	}
 #pragma unroll
 	for (int gi = 0; gi < RG; gi++) {
-		const int      U    = mu[gi][q];
-		const int      Up   = lane_shr1 (U);
-		const uint64_t eq   = __ballot (U == Up) & ~1ull; /* lane 0 has no previous sample */
-		const uint64_t s1   = __ballot (U == Up + 1) & ~1ull;
+		const uint64_t eq = eqm[gi][q], s1 = s1m[gi][q];
 		const uint64_t pair = eq >> 1, lead = s1, lead2 = eq << 1;
 		const uint64_t own2 = ~((pair & (s1 >> 2)) | (~pair & (s1 >> 1)));
 		const float    a = ma[gi][q], b = mb[gi][q];
 		const float    bp1 = lane_shr1 (b), bp2 = lane_shr1 (bp1), an = lane_shl1 (a), bn = lane_shl1 (b);
-		/* slot t: b of the group at t - 1 (<= 2 samples, in order), then a of the group at t;
-		 * a skipped add keeps the value (v + 0 is not v for v = -0): selects, not adds of 0 */
-		float x  = v[gi] + bp2;
-		float nv = lane_in (lead & lead2) ? x : v[gi];
-		x        = nv + bp1;
-		nv       = lane_in (lead) ? x : nv;
+		float          x  = v[gi] + bp2;
+		float          nv = lane_in (lead & lead2) ? x : v[gi];
+		x                 = nv + bp1;
+		nv                = lane_in (lead) ? x : nv;
 		nv += a;
 		x  = nv + an;
 		nv = lane_in (pair) ? x : nv;
-		/* slot t + 1 when no group sits there: b of this group */
 		float nw = w[gi] + b;
 		x        = nw + bn;
 		nw       = lane_in (pair) ? x : nw;
@@ -2719,6 +2716,51 @@ __device__ __forceinline__ void wh_serial (float* r, uint32_t base, uint32_t m, 
 		}
 	}
 #endif
+	fz[0] = z0;
+	fz[1] = z1;
+}
+
+/* wh_serial<false> on a 16-B aligned row, 4 samples per LDS read / write (ds_read_b128 /
+ * ds_write_b128: 32 LDS instructions per pass instead of 128); the same operations in the
+ * same order, the next group of 8 read while this one's recurrence runs */
+__device__ __forceinline__ void wh_serial_v (float* r, float* fz, float a1, float a2, bool scrub)
+{
+	float z0 = fz[0], z1 = fz[1];
+	if (scrub) {
+		if (isnan (z0))
+			z0 = 0.f;
+		if (isnan (z1))
+			z1 = 0.f;
+	}
+	PRIO_UP ();
+	float4* r4  = (float4*)r;
+	auto    run = [&] (float4 (&v)[2], int g) {
+		float x[8] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
+#pragma unroll
+		for (int k = 0; k < 8; k++) {
+			const float t = x[k] - (a1 * z0) - (a2 * z1);
+			z1            = z0;
+			z0            = t;
+			x[k]          = t;
+		}
+		r4[2 * g]     = make_float4 (x[0], x[1], x[2], x[3]);
+		r4[2 * g + 1] = make_float4 (x[4], x[5], x[6], x[7]);
+	};
+	float4 xa[2], xb[2];
+	xa[0] = r4[0];
+	xa[1] = r4[1];
+#pragma unroll
+	for (int g = 0; g < TBF_SUB / 8; g += 2) {
+		xb[0] = r4[2 * g + 2];
+		xb[1] = r4[2 * g + 3];
+		run (xa, g);
+		if (g + 2 < TBF_SUB / 8) {
+			xa[0] = r4[2 * g + 4];
+			xa[1] = r4[2 * g + 5];
+		}
+		run (xb, g + 1);
+	}
+	PRIO_DOWN ();
 	fz[0] = z0;
 	fz[1] = z1;
 }
@@ -2840,7 +2882,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 			const float z0 = st.fz[0][0], z1 = st.fz[0][1];
 #ifndef WH_NO_SERIAL
 			if (lane == 0)
-				wh_serial<false> (sm.ab[ap ^ 1], 0u, 0u, st.fz[0], ha[0], ha[1], false);
+				wh_serial_v (sm.ab[ap ^ 1], st.fz[0], ha[0], ha[1], false);
 #endif
 			wave_sync ();
 			sm.ab[ap ^ 1][n] = wh_output (sm.ab[ap ^ 1][n], z0, z1, ha);
@@ -2869,7 +2911,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 			if (wrap)
 				wh_serial<true> (row, lane < 2 ? 0u : wb, lane < 2 ? ~0u : WM, st.fz[lane], fa0, fa1, lane == 0 && scrubA);
 			else
-				wh_serial<false> (row + (lane < 2 ? 0u : wb), 0u, 0u, st.fz[lane], fa0, fa1, lane == 0 && scrubA);
+				wh_serial_v (row + (lane < 2 ? 0u : wb), st.fz[lane], fa0, fa1, lane == 0 && scrubA);
 		}
 		wave_sync ();
 		/* the filter outputs: horn B -> xf, horn A of the next sub-block in place, the drum
@@ -2951,10 +2993,12 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 #pragma unroll
 				for (int q = 0; q < 3; q++) {
 					const int p = ((r0 + gi) & 1) + 2 * q;
+					/* x 16384 is exact (a power of two), so one fma rounds once where the
+					 * reference's multiply-then-add rounds once: the same double */
 					if (r0 + gi < 2) /* HN_MOTION, src/whirl.cpp:1434 */
-						h1v[gi][q] = (float)((ha + ((p & 1) ? K.bwAng : K.fwAng)) * (unsigned int)16384 + K.hornPhase[p]);
+						h1v[gi][q] = (float)__builtin_fma (ha + ((p & 1) ? K.bwAng : K.fwAng), 16384.0, (double)K.hornPhase[p]);
 					else /* DR_MOTION, src/whirl.cpp:1457 */
-						h1v[gi][q] = (float)(da * (unsigned int)16384 + K.hornPhase[p]);
+						h1v[gi][q] = (float)__builtin_fma (da, 16384.0, (double)K.hornPhase[p]);
 				}
 			f2u   dpv[WH_RG][3];
 			f4u   b4v[2][3];
@@ -3023,19 +3067,24 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 			 * samples) */
 			bool okr[WH_RG];
 			bool allOk = !(P.dbg & TBF_DEBUG_FORCE_SERIAL);
+			/* as wave ballots, whose masks the passes reuse: eq (slot == previous lane's),
+			 * s1 (slot == previous lane's + 1); monotone = no lane below its predecessor,
+			 * groups <= 2 = no two consecutive eq bits */
+			uint64_t eqm[WH_RG][3], s1m[WH_RG][3];
 #pragma unroll
 			for (int gi = 0; gi < WH_RG; gi++) {
-				int ok = (mu[gi][1] >= mu[gi][0] + 2) && (mu[gi][2] >= mu[gi][1] + 2);
+				const bool ok = (mu[gi][1] >= mu[gi][0] + 2) && (mu[gi][2] >= mu[gi][1] + 2);
+				uint64_t   bad = ~__ballot (ok);
 #pragma unroll
 				for (int q = 0; q < 3; q++) {
-					const int up = lane_shr1 (mu[gi][q]);
-					const int un = lane_shl1 (mu[gi][q]);
-					if (lane > 0 && mu[gi][q] < up)
-						ok = 0;
-					if (lane > 0 && lane < NL - 1 && up == mu[gi][q] && un == mu[gi][q])
-						ok = 0;
+					const int      U  = mu[gi][q];
+					const int      Up = lane_shr1 (U);
+					const uint64_t e  = __ballot (U == Up) & ~1ull; /* lane 0 has no previous sample */
+					bad |= (__ballot (U < Up) & ~1ull) | (e & (e >> 1));
+					eqm[gi][q] = e;
+					s1m[gi][q] = __ballot (U == Up + 1) & ~1ull;
 				}
-				okr[gi] = __all (ok) && !(P.dbg & TBF_DEBUG_FORCE_SERIAL);
+				okr[gi] = bad == 0 && !(P.dbg & TBF_DEBUG_FORCE_SERIAL);
 				allOk   = allOk && okr[gi];
 			}
 			if (allOk) {
@@ -3043,7 +3092,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 				 * (farthest motion first) updates all of them in one LDS round trip */
 #pragma unroll
 				for (int q = 2; q >= 0; q--) {
-					motion_pass<W, WH_RG> (sm.wring + r0, mu, ma, mb, q);
+					motion_pass<W, WH_RG> (sm.wring + r0, mu, ma, mb, eqm, s1m, q);
 					wave_sync ();
 				}
 			} else {

@@ -236,6 +236,12 @@ typedef struct tbf_rv_chan { /* one channel of the feedback network: k_rv_core w
 #ifndef TBF_STEADY_MAX
 #define TBF_STEADY_MAX 2048
 #endif
+/* the default: 512 blocks keep the stage buffers at 15 GB for 4096 instances (56 B per
+ * stereo sample, tbf_engine.cpp stageBuffers) at the speed of 2048-block chunks (128.6 vs
+ * 128.3 ms per 2048-block step, profiles/r05/s20_groups) */
+#ifndef TBF_STEADY_DEFAULT
+#define TBF_STEADY_DEFAULT 512
+#endif
 /* each reverb line of the slab starts on a 128-B boundary (16 doubles): a wave's 64
  * consecutive doubles then cover exactly four whole cache lines */
 #define TBF_RING_ALIGN 16

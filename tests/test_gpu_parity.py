@@ -666,6 +666,74 @@ def test_gpu_device_front_end_effect_events(oracle):
     assert max(eL, eR) <= TOL
 
 
+def test_gpu_device_front_end_small_chunks(oracle):
+    """The device front end's event gate (TBF_FRONT_MIN, default 64 events per chunk): 96
+    instances with a note change, a drawbar move and a reverb / rotary setter now and then,
+    so chunks 1 and 2 carry ~420 events each.  Those step on the device (k_front), bit for
+    bit like TBF_DEVICE_FRONT=0 and the oracle; a chunk under the gate steps on the host."""
+    import os
+    import torch
+    import tunebfree_amd as T
+    from orc_bind import Template
+    n, nb = 96, 256
+    seeds = [7700 + i for i in range(n)]
+    rows, oscen = [], [[] for _ in range(n)]
+
+    def ev(b, i, kind, a, v):
+        rows.append((b, i, 0 if kind == "note" else 1, a, float(v)))
+        oscen[i].append((b, kind, a, v))
+
+    for i in range(n):
+        for (k, a, v) in S.jazz1_params():
+            ev(0, i, k, a, v)
+        for k in S.chord_for(i):
+            ev(0, i, "note", k, 1)
+        for b in range(1, 192):
+            if (b + i) % 40 == 0:
+                ev(b, i, "note", 60 + (b // 40 + i) % 12, 0)
+                ev(b, i, "note", 61 + (b // 40 + i) % 12, 1)
+            if (b * 3 + i) % 97 == 0:
+                ev(b, i, "param", S.P_DRAWBAR + (i + b) % 9, (i + b) % 9)
+            if (b * 5 + i) % 131 == 0:
+                ev(b, i, "param", S.P_REVERB if i % 2 else S.P_DRUM, (b % 3) / 2.0 if i % 2 else (b // 50) % 3)
+    ev(250, 3, "note", 40, 1)  # the last chunk: a lone event, under the gate
+    rows.sort(key=lambda r: r[0])
+    for o in oscen:
+        o.sort(key=lambda r: r[0])
+    per_chunk = np.bincount([r[0] // 64 for r in rows], minlength=4)
+    assert (per_chunk[1:3] >= 64).all() and per_chunk[3] < 64, per_chunk
+    outs, chunks = [], []
+    for front in (True, False):
+        if not front:
+            os.environ["TBF_DEVICE_FRONT"] = "0"
+        try:
+            eng = T.Engine(sample_rate=48000.0, device=0)
+        finally:
+            os.environ.pop("TBF_DEVICE_FRONT", None)
+        tid = eng.template(seed=7)
+        eng.add_instances([tid] * n, seeds)
+        evs = eng.events(rows)
+        L = torch.zeros((n, nb * 128), dtype=torch.float32, device="cuda")
+        R = torch.zeros_like(L)
+        eng.render_events_device(nb, evs, L.data_ptr(), R.data_ptr(), nb * 128)
+        eng.synchronize()
+        outs.append((L.cpu().numpy(), R.cpu().numpy()))
+        chunks.append(eng.front_chunks())
+        eng.close()
+        del L, R
+    print(f"front-end chunks (device, host): device front on {chunks[0]}, off {chunks[1]}")
+    assert chunks[0][0] >= 2 and chunks[1][0] == 0, chunks
+    assert np.array_equal(outs[0][0].view(np.uint32), outs[1][0].view(np.uint32))
+    assert np.array_equal(outs[0][1].view(np.uint32), outs[1][1].view(np.uint32))
+    sample = [0, 3, 41, n - 1]
+    tpl = Template(oracle, seed=7)
+    oL, oR, *_ = oracle_run(oracle, tpl, [seeds[i] for i in sample], [oscen[i] for i in sample], nb)
+    eL, xL = compare(outs[0][0][sample], oL)
+    eR, xR = compare(outs[0][1][sample], oR)
+    print(f"small device front-end chunks vs oracle: max|err| L={eL:.3g} R={eR:.3g} bit-exact {xL:.6f} {xR:.6f}")
+    assert max(eL, eR) <= TOL
+
+
 def test_gpu_steady_chunks(oracle):
     """A chunk in which no instance's control changes (every block plays each instance's
     current entry) runs up to TBF_STEADY_CHUNK blocks (default 512, at most 2048) per

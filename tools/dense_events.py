@@ -8,6 +8,8 @@ chord)?  One step = one tbf_render_events call of 64 blocks; modes:
   every8   each instance changes its chord every 8 blocks (2 x 4 note events)
   dense    each instance releases one key and presses another on EVERY block
   params   each instance moves a drawbar on every block (no key change)
+  sparseN  N instances (of the batch) change one note at the step's first block (2 N
+           events: the size range of the device front end's event gate, TBF_FRONT_MIN)
 
 For each: wall ms/step (HIP-synchronized), host control ms/step (tbf_debug_host_time),
 time inside the tbf_render_events calls per step (host control + enqueueing + any wait),
@@ -51,6 +53,14 @@ def events_for(mode, B, blocks, step):
                     ev.append((b, i, T.engine.EV_NOTE, k, 0.0))
                 for k in S.chord_for(i + t):
                     ev.append((b, i, T.engine.EV_NOTE, k, 1.0))
+    elif mode.startswith("sparse"):
+        m = int(mode[6:])
+        for i in range(m):
+            j = (step * m + i) % B
+            t = step
+            ev.append((0, j, T.engine.EV_NOTE, 62 + (t - 1) % 12, 0.0))
+            ev.append((0, j, T.engine.EV_NOTE, 62 + t % 12, 1.0))
+        ev.sort(key=lambda r: r[0])
     elif mode == "params":
         for b in range(blocks):
             for i in range(B):

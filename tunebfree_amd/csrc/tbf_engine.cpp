@@ -422,8 +422,29 @@ int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
 					pg++;
 			}
 		}
-		for (int g = 0; g <= e->grp[TBF_NSTAGES - 1]; g++)
-			HIPCHK (hipStreamCreateWithFlags (&e->gs[g], hipStreamNonBlocking));
+		/* stage-group stream priorities (TBF_GROUP_PRIO="p0,p1,...": HIP stream priorities,
+		 * lower = higher, clamped to the device's range; default: the reverb group high).
+		 * The reverb group is the step's critical path (k_rv_pre -> k_rv_core_lds ->
+		 * k_rv_post, ~65 ms alone per 2048 blocks against ~46 for k_tonegen + k_mixpre and ~37
+		 * for k_whirl); at equal priority the other groups' workgroups took the CUs first
+		 * and k_rv_pre ran 4x slower than alone (tools/timeline.py, profiles/r05/s23) */
+		int pLeast = 0, pGreatest = 0;
+		HIPCHK (hipDeviceGetStreamPriorityRange (&pLeast, &pGreatest));
+		int prio[TBF_NSTAGES] = {0, 0, 0, 0, 0, 0};
+		if (e->grp[2] == e->grp[3] && e->grp[3] == e->grp[4] && e->grp[2] != e->grp[1] && e->grp[4] != e->grp[5])
+			prio[e->grp[2]] = pGreatest;
+		if (const char* gp = getenv ("TBF_GROUP_PRIO"))
+			for (int g = 0; g < TBF_NSTAGES && *gp; g++) {
+				prio[g] = atoi (gp);
+				while (*gp && *gp != ',')
+					gp++;
+				if (*gp == ',')
+					gp++;
+			}
+		for (int g = 0; g <= e->grp[TBF_NSTAGES - 1]; g++) {
+			const int p = std::min (std::max (prio[g], std::min (pLeast, pGreatest)), std::max (pLeast, pGreatest));
+			HIPCHK (hipStreamCreateWithPriority (&e->gs[g], hipStreamNonBlocking, p));
+		}
 		for (int k = 0; k < TBF_NSTAGES; k++) {
 			HIPCHK (hipEventCreateWithFlags (&e->sdone[k], hipEventDisableTiming));
 			for (int p = 0; p < 4; p++)
@@ -457,6 +478,10 @@ int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
 		e->parCtl      = !(hs && hs[0] == '1');
 		const char* df = getenv ("TBF_DEVICE_FRONT"); /* 0: note-only chunks step on the host too (A/B) */
 		e->frontOn     = !(df && df[0] == '0');
+		if (const char* sp = getenv ("TBF_WHIRL_SPLIT")) /* 1: k_whirl_split (two waves per instance) */
+			e->whSplit = sp[0] != '0';
+		if (const char* fm = getenv ("TBF_FRONT_MIN")) /* events a chunk needs for the device front end */
+			e->frontMin = (uint32_t)std::max (atoi (fm), 1);
 	}
 	if (int rc = buildShared (e.get ()))
 		return rc;
@@ -1666,22 +1691,27 @@ static bool frontCleanAll (tbf_engine* e)
 /* One parallel pass over a chunk's events (sorted by block): a programme event among them,
  * an event for a bad instance, and -- with cl, the instances' cleanliness -- whether the
  * device front end takes them all (notes and frontParam kinds on clean instances), with
- * the per-segment counts of stepChunkFront's partition by instance range.  (Three passes
- * over the 24-B events used to do this: ~0.2 ms each at 524 k events.) */
-static void scanChunk (uint32_t n, const tbf_event* ev, uint32_t evBeg, uint32_t evEnd, const uint8_t* cl, bool& progEv,
-                       bool& bad, bool& front, ChunkScan& cs)
+ * the events as compact records bucketed by (segment, instance range) for stepChunkFront.
+ * (Three passes over the 24-B events used to do this: ~0.2 ms each at 524 k events; then a
+ * scan, a partition and a gather by instance, ~0.3 ms each.) */
+static void scanChunk (uint32_t n, uint32_t b0, const tbf_event* ev, uint32_t evBeg, uint32_t evEnd, const uint8_t* cl,
+                       bool& progEv, bool& bad, bool& front, ChunkScan& cs)
 {
 	const uint32_t nev = evEnd - evBeg;
 	cs.T   = std::max (1u, std::min<unsigned> (hostThreads (), (n + 255) / 256));
 	cs.per = (n + cs.T - 1) / cs.T;
 	cs.Te  = std::max (1u, std::min (hostThreads (), (nev + 32767) / 32768));
 	cs.seg = (nev + cs.Te - 1) / cs.Te;
-	cs.cnt.assign (cl ? (size_t)cs.Te * cs.T : 0, 0u);
+	if (cl && cs.bucket.size () < (size_t)cs.Te * cs.T)
+		cs.bucket.resize ((size_t)cs.Te * cs.T);
 	std::vector<char> pe (cs.Te, 0), bd (cs.Te, 0), fr (cs.Te, 0);
 	parallelFor (cs.Te, [&] (uint32_t sgm) {
 		const uint32_t k0 = evBeg + std::min (nev, sgm * cs.seg), k1 = evBeg + std::min (nev, (sgm + 1) * cs.seg);
 		bool           p = false, b = false, f = cl != nullptr; /* locals: the flags share a cache line */
-		uint32_t*      c = f ? cs.cnt.data () + (size_t)sgm * cs.T : nullptr;
+		std::vector<ChunkScan::Rec>* bk = f ? cs.bucket.data () + (size_t)sgm * cs.T : nullptr;
+		if (f)
+			for (unsigned t = 0; t < cs.T; t++)
+				bk[t].clear ();
 		for (uint32_t k = k0; k < k1; k++) {
 			const tbf_event& E = ev[k];
 			p                  = p || E.kind == TBF_EV_PROGRAM;
@@ -1692,7 +1722,9 @@ static void scanChunk (uint32_t n, const tbf_event* ev, uint32_t evBeg, uint32_t
 			}
 			if (f) {
 				f = (E.kind == TBF_EV_NOTE || (E.kind == TBF_EV_PARAM && frontParam (E))) && cl[E.inst];
-				c[E.inst / cs.per]++;
+				bk[E.inst / cs.per].push_back ({E.inst, (E.block - b0) << 2 | (E.kind == TBF_EV_PARAM ? 1u : 0u) |
+				                                            (E.value != 0.0 ? 2u : 0u),
+				                                E.id, (float)E.value});
 			}
 		}
 		pe[sgm] = p;
@@ -1723,32 +1755,15 @@ static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0
 		o.gainLocal = 0;
 		o.fx        = false;
 	}
-	{ /* the events by instance range, in order (a parallel counting partition; the counts
-	   * per event segment come from scanChunk) */
-		const uint32_t         nev = evEnd - evBeg, seg = cs.seg;
-		std::vector<uint32_t>& cnt = cs.cnt;
-		for (unsigned t = 0; t < T; t++) {
-			uint32_t tot = 0;
-			for (unsigned sgm = 0; sgm < cs.Te; sgm++) {
-				const uint32_t c         = cnt[(size_t)sgm * T + t];
-				cnt[(size_t)sgm * T + t] = tot;
-				tot += c;
-			}
-			out[t].evs.resize (tot);
-		}
-		parallelFor (cs.Te, [&] (uint32_t sgm) {
-			const uint32_t k0 = evBeg + std::min (nev, sgm * seg), k1 = evBeg + std::min (nev, (sgm + 1) * seg);
-			uint32_t*      at = cnt.data () + (size_t)sgm * T;
-			for (uint32_t k = k0; k < k1; k++) {
-				const uint32_t t = ev[k].inst / per;
-				out[t].evs[at[t]++] = k;
-			}
-		});
-	}
+	/* the events by instance range come from scanChunk's buckets, in event order */
 	const auto            f1 = std::chrono::steady_clock::now ();
 	std::vector<uint32_t> wbase (T + 1, 0);
-	for (unsigned t = 0; t < T; t++)
-		wbase[t + 1] = wbase[t] + (uint32_t)out[t].evs.size ();
+	for (unsigned t = 0; t < T; t++) {
+		size_t c = 0;
+		for (unsigned sgm = 0; sgm < cs.Te; sgm++)
+			c += cs.bucket[(size_t)sgm * T + t].size ();
+		wbase[t + 1] = wbase[t] + (uint32_t)c;
+	}
 	e->hFevOff.resize (n + 1);
 	e->hFev.resize (std::max<uint32_t> (wbase[T], 1));
 	e->hFevVal.resize (std::max<uint32_t> (wbase[T], 1));
@@ -1762,20 +1777,19 @@ static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0
 		std::vector<uint32_t>& eo = o.eoff;
 		auto&                  es = o.erec;
 		eo.assign ((size_t)(i1 > i0 ? i1 - i0 : 0) + 1, 0);
-		for (uint32_t k : o.evs)
-			eo[ev[k].inst - i0 + 1]++;
+		for (unsigned sgm = 0; sgm < cs.Te; sgm++)
+			for (const ChunkScan::Rec& r : cs.bucket[(size_t)sgm * T + t])
+				eo[r.inst - i0 + 1]++;
 		for (uint32_t i = i0; i < i1; i++)
 			eo[i - i0 + 1] += eo[i - i0];
-		es.resize (o.evs.size ());
-		{ /* the events by instance as compact records (written while the range's events
-		   * are read in order, so the per-instance pass below reads them sequentially) */
+		es.resize (wbase[t + 1] - wbase[t]);
+		{ /* the range's events by instance (a stable counting sort of its buckets, read in
+		   * order, so the per-instance pass below reads them sequentially) */
 			std::vector<uint32_t>& fill = o.efill;
 			fill.assign (eo.begin (), eo.end () - 1);
-			for (uint32_t k : o.evs) {
-				const tbf_event& E            = ev[k];
-				es[fill[E.inst - i0]++] = {E.block - b0, E.id, (float)E.value,
-				                           (E.kind == TBF_EV_PARAM ? 1u : 0u) | (E.value != 0.0 ? 2u : 0u)};
-			}
+			for (unsigned sgm = 0; sgm < cs.Te; sgm++)
+				for (const ChunkScan::Rec& r : cs.bucket[(size_t)sgm * T + t])
+					es[fill[r.inst - i0]++] = {r.bf >> 2, r.id, r.v, r.bf & 3u};
 		}
 		const auto g1 = std::chrono::steady_clock::now ();
 		for (uint32_t i = i0; i < i1; i++) {
@@ -1783,9 +1797,8 @@ static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0
 			TgControl&       tg = in.tg;
 			tbf_front_state& F  = e->hFront[i];
 			memset (&F, 0, sizeof (F));
-			for (int k = 0; k < 384; k++)
-				if (tg.activeKeys[k])
-					F.keys[k >> 5] |= 1u << (k & 31);
+			static_assert (sizeof (F.keys) == sizeof (tg.keyBits), "384 key bits");
+			memcpy (F.keys, tg.keyBits, sizeof (F.keys));
 			F.keyDown         = tg.keyDownCount;
 			F.upperDown       = (int32_t)tg.upperKeyCount;
 			F.pending         = tg.steadyPending ? 1u : 0u;
@@ -2118,6 +2131,7 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 	P.slabLen   = e->slabLen;
 	P.errFlags  = e->err.p;
 	P.dbg       = e->cfg.debug_flags;
+	P.whSplit   = e->whSplit ? 1u : 0u;
 	P.rvLds     = e->rvLdsOn && e->rvLdsFit;
 	P.rvGrid    = e->rvGrid;
 	P.rvWork    = e->rvWork.p;
@@ -2306,9 +2320,9 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		/* a chunk of note, drawbar and switch events only (frontParam) on clean instances: the
 		 * device front end */
 		bool       progEv = false, badEv = false, front = false;
-		const bool frontCand = e->devCtl && dpipe && e->frontOn && evEnd - evi >= 1024 && frontCleanAll (e);
+		const bool frontCand = e->devCtl && dpipe && e->frontOn && evEnd - evi >= e->frontMin && frontCleanAll (e);
 		ChunkScan& cs        = e->scan;
-		scanChunk (n, ev, evi, evEnd, frontCand ? e->fclean.data () : nullptr, progEv, badEv, front, cs);
+		scanChunk (n, b0, ev, evi, evEnd, frontCand ? e->fclean.data () : nullptr, progEv, badEv, front, cs);
 		if (badEv)
 			return fail (-22, "event for a bad instance");
 		bool dfront = false;

@@ -145,7 +145,15 @@ struct PinnedVec {
 struct ChunkScan {
 	unsigned              T = 1, Te = 1; /* instance ranges, event segments */
 	uint32_t              per = 1, seg = 0;
-	std::vector<uint32_t> cnt; /* [Te][T] */
+	/* the events of segment s for instance range t, in order, as compact records (written by
+	 * the scan itself, so the front end never reads the 24-B events again): bucket s T + t */
+	struct Rec {
+		uint32_t inst;
+		uint32_t bf; /* block in the chunk << 2 | 1: parameter event | 2: value != 0 */
+		int32_t  id;
+		float    v;
+	};
+	std::vector<std::vector<Rec>> bucket;
 };
 
 template <typename T>
@@ -272,6 +280,8 @@ struct tbf_engine {
 	 * parity; region p's persistent entries are refreshed from hCtl when they are older
 	 * than its version (ctlVer counts the changes of hCtl) */
 	uint64_t                                ctlVer = 1, regionVer[2] = {0, 0};
+	bool                                    whSplit = false; /* k_whirl_split (TBF_WHIRL_SPLIT=1) instead of k_whirl */
+	uint32_t                                frontMin = 64; /* events a chunk needs for the device front end (TBF_FRONT_MIN; 64: profiles/r05/s23) */
 	bool                                    parCtl = true; /* TBF_HOST_SERIAL=1 steps serially */
 	/* threaded host control (stepChunkParallel): per worker, kept between chunks so the
 	 * buffers stay allocated; worker t writes its deltas straight into the staging at pool

@@ -192,7 +192,7 @@ struct TgControl {
 	unsigned          newRouting = 0, oldRouting = 0;
 	unsigned          percSendBus = 4, percSendBusA = 3, percSendBusB = 4;
 	float             swellPedalGain = 0.07f, outputLevelTrim = 0.07f;
-	unsigned          activeKeys[384];
+	uint32_t          keyBits[12]; /* activeKeys[384] (src/tonegen.cpp:3096-3166) as bits */
 	float             drawBarGain[27];
 	float             drawBarLevel[27][9];
 	uint16_t          drawBarChange = 0;
@@ -214,6 +214,9 @@ struct TgControl {
 	/* keyOn / keyOff without queueing the messages (the device front end derives them):
 	 * returns the number of messages the key event makes */
 	int noteCount (int key, bool on);
+	bool keyActive (int key) const { return (keyBits[key >> 5] >> (key & 31)) & 1u; }
+	void keySet (int key) { keyBits[key >> 5] |= 1u << (key & 31); }
+	void keyClear (int key) { keyBits[key >> 5] &= ~(1u << (key & 31)); }
 	void setDrawBar (int bus, unsigned setting);
 	void setVibratoUpper (int on);
 	void setVibratoLower (int on);

@@ -817,7 +817,7 @@ void TgControl::init (const TgTemplate* t, const Config& c)
 	percEnvGainResetNorm = c.percEnvGainResetNorm;
 	percEnvGainResetSoft = c.percEnvGainResetSoft;
 	percEnvScaling       = c.percEnvScaling;
-	memset (activeKeys, 0, sizeof (activeKeys));
+	memset (keyBits, 0, sizeof (keyBits));
 	memset (drawBarGain, 0, sizeof (drawBarGain));
 	for (int i = 0; i < 27; i++)
 		for (int s = 0; s < 9; s++) {
@@ -842,9 +842,9 @@ void TgControl::init (const TgTemplate* t, const Config& c)
 /* src/tonegen.cpp:3096-3166 */
 void TgControl::keyOff (int key)
 {
-	if (key < 0 || key >= 384 || !activeKeys[key])
+	if (key < 0 || key >= 384 || !keyActive (key))
 		return;
-	activeKeys[key] = 0;
+	keyClear (key);
 	if (key < 128)
 		upperKeyCount--;
 	keyDownCount--;
@@ -855,9 +855,9 @@ void TgControl::keyOn (int key)
 {
 	if (key < 0 || key >= 384)
 		return;
-	if (activeKeys[key])
+	if (keyActive (key))
 		keyOff (key);
-	activeKeys[key] = 1;
+	keySet (key);
 	if (key < 128)
 		upperKeyCount++;
 	keyDownCount++;
@@ -869,15 +869,15 @@ int TgControl::noteCount (int key, bool on)
 	if (key < 0 || key >= 384)
 		return 0;
 	int m = 0;
-	if (activeKeys[key]) { /* keyOff, or keyOn's release of a held key first */
-		activeKeys[key] = 0;
+	if (keyActive (key)) { /* keyOff, or keyOn's release of a held key first */
+		keyClear (key);
 		if (key < 128)
 			upperKeyCount--;
 		keyDownCount--;
 		m++;
 	}
 	if (on) {
-		activeKeys[key] = 1;
+		keySet (key);
 		if (key < 128)
 			upperKeyCount++;
 		keyDownCount++;

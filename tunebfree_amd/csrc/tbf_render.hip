@@ -3248,6 +3248,547 @@ k_whirl (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 		wr[i] = sm.wring[i / W][i % W];
 }
 
+/* ------------------------------------------------------------------ k_whirl_split
+ * k_whirl with two waves per instance: the horn wave (rings HL, HR: horn filters A / B,
+ * FILTER_C on the horn signal, the six HN_MOTIONs, the outputs and mic mix) and the drum
+ * wave (rings DL, DR: the drum shelves, FILTER_C on the input, the six DR_MOTIONs).  The
+ * two halves of whirlProc2 share nothing within a block but the drum outputs dL / dR,
+ * which the drum wave leaves in its ring slots at outpos (just consumed by the shelves)
+ * and the horn wave reads after one workgroup barrier per sub-block; the drum wave clears
+ * those slots after the next barrier, before its own adds of that sub-block (the adds land
+ * >= 79 slots ahead and the ring holds write-ahead + 68 slots, so an add of sub-block k + 1
+ * may wrap into window k only after it is cleared).  Each rotor's speed update is its own
+ * half of whirl_speed.  So every instance is two waves of about half the instructions, 8
+ * waves per SIMD at the 512-sample ring (a latency-bound kernel: one wave alone per SIMD ran
+ * 7.1 ms per 512 blocks against 9.4 at 4 per SIMD, profiles/r05/s26), and the same
+ * operations in the same order as k_whirl. */
+
+#ifndef WHS_WAVES
+#define WHS_WAVES 8 /* k_whirl_split waves per SIMD at the 512-sample ring (8: all 4096 instances at once) */
+#endif
+/* a wave-uniform value moved to scalar registers */
+__device__ __forceinline__ float sgpr_f (float v) { return __int_as_float (__builtin_amdgcn_readfirstlane (__float_as_int (v))); }
+__device__ __forceinline__ double sgpr_d (double v)
+{
+	const unsigned long long u = __double_as_longlong (v);
+	const unsigned long long lo = (unsigned)__builtin_amdgcn_readfirstlane ((int)(unsigned)u);
+	const unsigned long long hi = (unsigned)__builtin_amdgcn_readfirstlane ((int)(unsigned)(u >> 32));
+	return __longlong_as_double ((long long)(lo | (hi << 32)));
+}
+
+/* one rotor's half of whirl_speed (src/whirl.cpp:174-235, 1219-1374): the horn's or the
+ * drum's fields only; brake = 1 when its brake engaged */
+template <bool HORN>
+__device__ void whirl_speed_rotor (tbf_wh_state& st, const tbf_inst_const& K, int revOpt, int& brake)
+{
+	double       angle = HORN ? st.hornAngle : st.drumAngle, incr = HORN ? st.hornIncr : st.drumIncr;
+	double       target = HORN ? st.hornTarget : st.drumTarget;
+	int          acdc   = HORN ? st.hornAcDc : st.drumAcDc;
+	const double brakePos = HORN ? st.prm.hnBrakePos : st.prm.drBrakePos;
+	if (revOpt >= 0) {
+		const int i = revOpt % 9;
+		target      = HORN ? K.revHorn[i] : K.revDrum[i];
+		if (incr < target)
+			acdc = 1;
+		else if (target < incr)
+			acdc = -1;
+	}
+	if (acdc) {
+		int flywheel = 0;
+		if (brakePos > 0 && target == 0 && incr > 0 && incr < (HORN ? K.hnHardstop : K.drHardstop)) {
+			const double targetPos = HORN ? fmod (1.25 - brakePos, 1.0) : fmod (brakePos + .75, 1.0);
+			if (fabs (angle - targetPos) < (2.0 / 16384)) {
+				angle = targetPos;
+				incr  = 0;
+			} else {
+				const float diffinc = (float)(fmod (1. + targetPos - angle, 1.0) / (float)TBF_BLK);
+				if (incr > diffinc)
+					incr = diffinc;
+				else if (incr < K.minspeed)
+					incr = K.minspeed;
+				flywheel = 1;
+			}
+		}
+		if (!flywheel) {
+			const double l = acdc > 0 ? st.prm.lAcc[HORN ? 0 : 2] : st.prm.lAcc[HORN ? 1 : 3];
+			incr += (1 - l) * (target - incr);
+		}
+		if (fabs (target - incr) < K.deadzone) {
+			acdc = 0;
+			incr = target;
+		}
+	}
+	brake = 0;
+	if (brakePos > 0) {
+		const double targetPos = HORN ? fmod (1.25 - brakePos, 1.0) : fmod (brakePos + .75, 1.0);
+		if (!acdc && incr == 0 && angle != targetPos) {
+			brake = 1;
+			if (fabs (angle - targetPos) < (2.0 / 16384)) {
+				angle = targetPos;
+			} else {
+				incr = fmod (1. + targetPos - angle, 1.0) / (float)TBF_BLK;
+				if (incr > (HORN ? K.hnLimit : K.drLimit))
+					incr = HORN ? K.hnLimit : K.drLimit;
+			}
+		}
+	}
+	if (HORN) {
+		st.hornAngle  = angle;
+		st.hornIncr   = incr;
+		st.hornTarget = target;
+		st.hornAcDc   = acdc;
+	} else {
+		st.drumAngle  = angle;
+		st.drumIncr   = incr;
+		st.drumTarget = target;
+		st.drumAcDc   = acdc;
+	}
+}
+
+/* a rotor's angles over a sub-block: lane n gets the angle of sample n (phase_run's closed
+ * form, or the literal fmod recurrence replayed); the angle after the sub-block is stored */
+__device__ __forceinline__ double wh_angles (const tbf_launch& P, double& stAngle, const double incr, const int n)
+{
+	double       D;
+	const double a0 = stAngle;
+	const bool   ok = phase_run (a0, incr, TBF_SUB, D) && !(P.dbg & TBF_DEBUG_FORCE_SERIAL);
+	double       an = a0 + (double)n * D, ae = a0 + (double)TBF_SUB * D;
+	if (!ok) { /* wave-uniform: every lane replays the recurrence, lane n keeps step n */
+		if (n == 0)
+			atomicOr (P.errFlags, (uint32_t)TBF_PATH_WH_ANGLE);
+		double a = a0;
+		for (int i = 0; i < TBF_SUB; i++) {
+			if (n == i)
+				an = a;
+			a = wrap1 (a + incr);
+		}
+		ae = a;
+	}
+	wave_sync (); /* every lane has read the start angle */
+	if (n == 0)
+		stAngle = ae;
+	wave_sync ();
+	return an;
+}
+
+/* the three motions of one ring (HORN: HL or HR, else DL or DR; gi = the ring's channel)
+ * and their ordered adds: k_whirl's ring group for one ring, so that a wave holds one
+ * ring's motions at a time (the split kernel's waves have 64 VGPRs) */
+template <int W, bool HORN>
+__device__ __forceinline__ void wh_ring (const tbf_launch& P, WhLds<W>& sm, const tbf_inst_const& K, const double hb,
+                                         const int gi, const uint32_t outpos, const int32_t unwrap, const float xin,
+                                         const float xd1v, const float xd2v)
+{
+	const int      n  = threadIdx.x & (NL - 1), lane = n;
+	const uint32_t WM = (uint32_t)W - 1u;
+	const float*   tF = P.whTab + (HORN ? 0 : 2) * TBF_WH_TSTRIDE;
+	const float*   tB = tF + TBF_WH_TSTRIDE;
+	float*         ring = sm.wring[(HORN ? 0 : 2) + gi];
+	int            mu[1][3];
+	float          ma[1][3], mb[1][3], h1v[3];
+#pragma unroll
+	for (int q = 0; q < 3; q++) { /* HN_MOTION src/whirl.cpp:1434 / DR_MOTION 1457, the fma exact (see k_whirl) */
+		/* the phase converted here: hoisted out of the sub-block loop, the six converted
+		 * doubles held 12 VGPRs across it and spilled */
+		int ph = K.hornPhase[gi + 2 * q];
+		asm volatile ("" : "+s"(ph));
+		h1v[q] = (float)__builtin_fma (hb, 16384.0, (double)ph);
+	}
+	f2u   dpv[3];
+	f4u   b4v[3];
+	float b5v[3];
+#pragma unroll
+	for (int q = 0; q < 3; q++) {
+		const int      p   = gi + 2 * q;
+		const bool     fwd = (p == 0 || p == 3 || p == 4);
+		const unsigned hl  = ((unsigned int)floorf (h1v[q])) & 16383u;
+		dpv[q]             = *(const f2u*)((fwd ? tF : tB) + hl); /* tab[hl], tab[(hl + 1) & 16383] */
+		if (HORN) {
+			const unsigned kk = ((unsigned int)roundf (h1v[q])) & 16383u;
+			const float*   b  = (fwd ? P.whBw + 16384 * 5 : P.whBw) + 5 * kk;
+			b4v[q]            = *(const f4u*)b;
+			b5v[q]            = b[4];
+		}
+	}
+#pragma unroll
+	for (int q = 0; q < 3; q++) {
+		const int   p    = gi + 2 * q;
+		const float hd   = frac1 (h1v[q]);
+		const float intp = dpv[q].x * (1.f - hd) + hd * dpv[q].y;
+		float       xa, t;
+		if (HORN) { /* HN_MOTION, src/whirl.cpp:1432-1453 */
+			const float* hist = p < 2 ? sm.xf : (p < 4 ? sm.x1 : sm.x2);
+			t                 = K.hornSpacing[p] + intp + (float)outpos;
+			xa                = b4v[q].x * hist[n + 4];
+			xa += b4v[q].y * hist[n + 3];
+			xa += b4v[q].z * hist[n + 2];
+			xa += b4v[q].w * hist[n + 1];
+			xa += b5v[q] * hist[n + 0];
+		} else { /* DR_MOTION, src/whirl.cpp:1455-1469 */
+			xa = p < 2 ? xin : (p < 4 ? xd1v : xd2v);
+			t  = K.drumSpacing[p] + intp + (float)outpos;
+		}
+		const float rr = floorf (t);
+		const float qq = xa * (t - rr);
+		mu[0][q]       = (int32_t)((unsigned int)rr) + unwrap;
+		ma[0][q]       = xa - qq;
+		mb[0][q]       = qq;
+	}
+	/* the fast path's preconditions as wave ballots whose masks the passes reuse (k_whirl) */
+	const bool ok  = (mu[0][1] >= mu[0][0] + 2) && (mu[0][2] >= mu[0][1] + 2);
+	uint64_t   bad = ~__ballot (ok);
+	uint64_t   eqm[1][3], s1m[1][3];
+#pragma unroll
+	for (int q = 0; q < 3; q++) {
+		const int      U  = mu[0][q];
+		const int      Up = lane_shr1 (U);
+		const uint64_t e  = __ballot (U == Up) & ~1ull;
+		bad |= (__ballot (U < Up) & ~1ull) | (e & (e >> 1));
+		eqm[0][q] = e;
+		s1m[0][q] = __ballot (U == Up + 1) & ~1ull;
+	}
+	if (bad == 0 && !(P.dbg & TBF_DEBUG_FORCE_SERIAL)) {
+#pragma unroll
+		for (int q = 2; q >= 0; q--) {
+			motion_pass<W, 1> (reinterpret_cast<float (*)[W + WH_PAD]> (ring), mu, ma, mb, eqm, s1m, q);
+			wave_sync ();
+		}
+		return;
+	}
+	/* the serial replay in the reference order: sample-major, motions in source order */
+	{
+		if (lane == 0)
+			atomicOr (P.errFlags, (uint32_t)TBF_PATH_WH_MOTION);
+		for (int i = 0; i < TBF_SUB; i++) {
+#pragma unroll
+			for (int q = 0; q < 3; q++) {
+				const uint32_t sl = (uint32_t)__shfl (mu[0][q], i) & WM;
+				const float    aa = __shfl (ma[0][q], i);
+				const float    bb = __shfl (mb[0][q], i);
+				if (lane == 0) {
+					ring[sl] += aa;
+					ring[(sl + 1) & WM] += bb;
+				}
+			}
+		}
+		wave_sync ();
+	}
+}
+
+/* the horn wave's block (whirlProc2's horn half + whirlProc3 mix): outputs via the held stores */
+template <int W>
+__device__ void whirl_horn (const tbf_launch& P, WhLds<W>& sm, const bool bypass, const int revOpt, const tbf_inst_const& K,
+                            const float in0, const float in1, const float* __restrict__ inNext, float& nx0, float& nx1,
+                            const bool hasNext, float* __restrict__ oL, float* __restrict__ oR, WhOut& pend, uint32_t& opos)
+{
+	const int     lane = threadIdx.x & (NL - 1), n = lane;
+	tbf_wh_state& st   = sm.st;
+	if (bypass) {
+		/* whirlProc2 bypass (src/whirl.cpp:1197-1215) + whirlProc3 mix (see stage_whirl) */
+		nx0 = inNext[lane];
+		nx1 = inNext[lane + NL];
+		wh_flush (pend);
+		oL[lane] = in0 * K.mic[0] + in0 * K.mic[1] + 0.f * K.mic[2] + 0.f * K.mic[3];
+		oR[lane] = in0 * K.mic[4] + in0 * K.mic[5] + 0.f * K.mic[6] + 0.f * K.mic[7];
+		pend.l   = oL + NL + lane;
+		pend.r   = oR + NL + lane;
+		pend.vl  = in1 * K.mic[0] + in1 * K.mic[1] + 0.f * K.mic[2] + 0.f * K.mic[3];
+		pend.vr  = in1 * K.mic[4] + in1 * K.mic[5] + 0.f * K.mic[6] + 0.f * K.mic[7];
+		return;
+	}
+	int brake = 0;
+	if (lane == 0) /* a control entry carrying a rotary selection is used for exactly one block */
+		whirl_speed_rotor<true> (st, K, revOpt, brake);
+	brake = __builtin_amdgcn_readfirstlane (brake);
+	wave_sync ();
+	/* wave-uniform values in scalar registers (the split kernel's waves have 64 VGPRs) */
+	const double   hornIncr = sgpr_d (st.hornIncr);
+	const uint32_t WM       = (uint32_t)W - 1u;
+	float          ha[5], hb[5];
+#pragma unroll
+	for (int j = 0; j < 5; j++) {
+		ha[j] = sgpr_f (st.prm.hafw[j]);
+		hb[j] = sgpr_f (st.prm.hbfw[j]);
+	}
+	/* serial lanes: 0 horn A (over the next sub-block), 1 horn B (over this one) */
+	const float fa0 = lane == 0 ? ha[0] : hb[0];
+	const float fa1 = lane == 0 ? ha[1] : hb[1];
+	for (int sb = 0; sb < TBF_BLK / TBF_SUB; sb++) {
+		const uint32_t outpos = (opos + (uint32_t)n) & 2047u;
+		const int32_t  unwrap = (int32_t)(opos + (uint32_t)n - outpos); /* 0 or 2048 */
+		const float    xin    = (float)((double)(sb == 0 ? in0 : in1) + 1e-14);
+		const uint32_t o      = outpos & WM;
+		const float    hlv = sm.wring[0][o], hrv = sm.wring[1][o];
+		sm.wring[0][o]     = 0.f;
+		sm.wring[1][o]     = 0.f;
+		if (lane < 4) {
+			const int i = lane;
+			sm.xf[i]    = st.adx[0][(st.adi[0] + 3 - i) & 7];
+			sm.x1[i]    = st.adx[1][(st.adi[1] + 3 - i) & 7];
+			sm.x2[i]    = st.adx[2][(st.adi[2] + 3 - i) & 7];
+		}
+		/* horn A runs one sub-block ahead (see stage_whirl) */
+		const int  ap    = sm.ap;
+		const bool aNext = sb + 1 < TBF_BLK / TBF_SUB || hasNext;
+		if (!sm.aReady)
+			sm.ab[ap ^ 1][n] = xin;
+		if (aNext)
+			sm.ab[ap][n] = (float)((double)(sb + 1 < TBF_BLK / TBF_SUB ? in1 : nx0) + 1e-14);
+		wave_sync ();
+		if (!sm.aReady) {
+			const float z0 = st.fz[0][0], z1 = st.fz[0][1];
+			if (lane == 0)
+				wh_serial_v (sm.ab[ap ^ 1], st.fz[0], ha[0], ha[1], false);
+			wave_sync ();
+			sm.ab[ap ^ 1][n] = wh_output (sm.ab[ap ^ 1][n], z0, z1, ha);
+			wave_sync ();
+		}
+		const bool scrubA = sb + 1 == TBF_BLK / TBF_SUB;
+		float      zs[2][2];
+#pragma unroll
+		for (int f = 0; f < 2; f++) {
+			zs[f][0] = st.fz[f][0];
+			zs[f][1] = st.fz[f][1];
+		}
+		if (scrubA) {
+			zs[0][0] = isnan (zs[0][0]) ? 0.f : zs[0][0];
+			zs[0][1] = isnan (zs[0][1]) ? 0.f : zs[0][1];
+		}
+		if (lane < 2 && (lane > 0 || aNext))
+			wh_serial_v (lane == 0 ? sm.ab[ap] : sm.ab[ap ^ 1], st.fz[lane], fa0, fa1, lane == 0 && scrubA);
+		wave_sync ();
+		sm.xf[4 + n] = wh_output (sm.ab[ap ^ 1][n], zs[1][0], zs[1][1], hb);
+		if (aNext)
+			sm.ab[ap][n] = wh_output (sm.ab[ap][n], zs[0][0], zs[0][1], ha);
+		if (lane == 0) {
+			sm.aReady = aNext;
+			sm.ap     = ap ^ 1;
+		}
+		const double ang = wh_angles (P, st.hornAngle, hornIncr, n);
+		/* FILTER_C on the horn signal (src/whirl.cpp:1472-1477) */
+		const float xf  = sm.xf[n + 4];
+		const float xfp = n == 0 ? st.z[0] : sm.xf[n + 3];
+		const float x1v = (float)((0.4 * xf) + (0.4 * xfp));
+		sm.x1[n + 4]    = x1v;
+		wave_sync ();
+		const float x1p = n == 0 ? st.z[1] : sm.x1[n + 3];
+		const float x2v = (float)((0.4 * x1v) + (0.4 * x1p));
+		sm.x2[n + 4]    = x2v;
+		wave_sync ();
+		/* behind this sub-block's loads: the next block's input and the held output stores */
+		nx0 = inNext[lane];
+		nx1 = inNext[lane + NL];
+		wh_flush (pend);
+		wh_ring<W, true> (P, sm, K, ang + K.fwAng, 0, outpos, unwrap, xin, 0.f, 0.f);
+		wh_ring<W, true> (P, sm, K, ang + K.bwAng, 1, outpos, unwrap, xin, 0.f, 0.f);
+		/* the drum wave's dL / dR of this sub-block, left in its ring slots at outpos */
+		__syncthreads ();
+		const float dL = sm.wring[2][o], dR = sm.wring[3][o];
+		{
+			const float leak = xf * K.leakage;
+			const float hL   = K.hornLevel * hlv + leak;
+			const float hR   = K.hornLevel * hrv + leak;
+			pend.l           = oL + sb * TBF_SUB + n;
+			pend.r           = oR + sb * TBF_SUB + n;
+			pend.vl          = hL * K.mic[0] + hR * K.mic[1] + dL * K.mic[2] + dR * K.mic[3];
+			pend.vr          = hL * K.mic[4] + hR * K.mic[5] + dL * K.mic[6] + dR * K.mic[7];
+		}
+		if (lane == NL - 1) {
+			st.z[0] = xf;
+			st.z[1] = x1v;
+		}
+		wave_sync ();
+		if (lane < 24) { /* history k = lane / 8, entry j = lane % 8, one lane each */
+			const int    k = lane >> 3, j = lane & 7;
+			const float* h = k == 0 ? sm.xf : (k == 1 ? sm.x1 : sm.x2);
+			st.adx[k][(st.adi[k] + j) & 7] = h[4 + TBF_SUB - 1 - j];
+		}
+		opos = (opos + TBF_SUB) & 2047u;
+		wave_sync ();
+	}
+	/* NaN scrub (src/whirl.cpp:1622-1630): the horn filters' states (horn A's only when it did
+	 * not run ahead) and z[0..1]; the brake */
+	if (lane < 4) {
+		const int f = lane >> 1, j = lane & 1;
+		if ((f > 0 || !sm.aReady) && isnan (st.fz[f][j]))
+			st.fz[f][j] = 0.f;
+	} else if (lane < 6) {
+		if (isnan (st.z[lane - 4]))
+			st.z[lane - 4] = 0.f;
+	}
+	if (lane == 0 && brake)
+		st.hornIncr = 0;
+	wave_sync ();
+}
+
+/* the drum wave's block (whirlProc2's drum half): dL / dR into the ring slots at outpos */
+template <int W>
+__device__ void whirl_drum (const tbf_launch& P, WhLds<W>& sm, const bool bypass, const int revOpt, const tbf_inst_const& K,
+                            const float in0, const float in1, const float* __restrict__ inNext, float& nx0, float& nx1,
+                            uint32_t& opos, int& clr)
+{
+	const int     lane = threadIdx.x & (NL - 1), n = lane;
+	tbf_wh_state& st   = sm.st;
+	if (bypass) {
+		nx0 = inNext[lane];
+		nx1 = inNext[lane + NL];
+		return;
+	}
+	int brake = 0;
+	if (lane == 0)
+		whirl_speed_rotor<false> (st, K, revOpt, brake);
+	brake = __builtin_amdgcn_readfirstlane (brake);
+	wave_sync ();
+	const double   drumIncr = sgpr_d (st.drumIncr);
+	const uint32_t WM       = (uint32_t)W - 1u;
+	for (int sb = 0; sb < TBF_BLK / TBF_SUB; sb++) {
+		const uint32_t outpos = (opos + (uint32_t)n) & 2047u;
+		const int32_t  unwrap = (int32_t)(opos + (uint32_t)n - outpos);
+		const float    xin    = (float)((double)(sb == 0 ? in0 : in1) + 1e-14);
+		const uint32_t o      = outpos & WM;
+		/* the shelves over this sub-block's ring outputs, in place (lanes 0, 1: DL, DR) */
+		const float z20 = st.fz[2][0], z21 = st.fz[2][1], z30 = st.fz[3][0], z31 = st.fz[3][1];
+		const uint32_t wb   = opos & WM; /* wave-uniform */
+		const bool     wrap = wb + TBF_SUB > (uint32_t)W;
+		if (lane < 2) {
+			float* row = sm.wring[2 + lane];
+			if (wrap)
+				wh_serial<true> (row, wb, WM, st.fz[2 + lane], K.drf[0], K.drf[1], false);
+			else
+				wh_serial_v (row + wb, st.fz[2 + lane], K.drf[0], K.drf[1], false);
+		}
+		wave_sync ();
+		const float dL = wh_output (sm.wring[2][o], z20, z21, K.drf);
+		const float dR = wh_output (sm.wring[3][o], z30, z31, K.drf);
+		sm.wring[2][o] = dL; /* handed to the horn wave */
+		sm.wring[3][o] = dR;
+		__syncthreads ();
+		/* the previous window: the horn wave has read it (it reached this barrier after) */
+		if (clr >= 0) {
+			sm.wring[2][((uint32_t)clr + (uint32_t)n) & WM] = 0.f;
+			sm.wring[3][((uint32_t)clr + (uint32_t)n) & WM] = 0.f;
+		}
+		clr = (int)wb;
+		const double ang = wh_angles (P, st.drumAngle, drumIncr, n);
+		/* FILTER_C on the input (src/whirl.cpp:1472-1477), by lane shifts */
+		const float xdp  = lane_shr1_or (xin, st.z[2]);
+		const float xd1v = (float)((0.4 * xin) + (0.4 * xdp));
+		const float xd1p = lane_shr1_or (xd1v, st.z[3]);
+		const float xd2v = (float)((0.4 * xd1v) + (0.4 * xd1p));
+		nx0 = inNext[lane];
+		nx1 = inNext[lane + NL];
+		wh_ring<W, false> (P, sm, K, ang, 0, outpos, unwrap, xin, xd1v, xd2v);
+		wh_ring<W, false> (P, sm, K, ang, 1, outpos, unwrap, xin, xd1v, xd2v);
+		if (lane == NL - 1) {
+			st.z[2] = xin;
+			st.z[3] = xd1v;
+		}
+		opos = (opos + TBF_SUB) & 2047u;
+		wave_sync ();
+	}
+	if (lane < 4) {
+		const int f = 2 + (lane >> 1), j = lane & 1;
+		if (isnan (st.fz[f][j]))
+			st.fz[f][j] = 0.f;
+	} else if (lane < 6) {
+		if (isnan (st.z[lane - 2]))
+			st.z[lane - 2] = 0.f;
+	}
+	if (lane == 0 && brake)
+		st.drumIncr = 0;
+	wave_sync ();
+}
+
+template <int W>
+__global__ void __attribute__ ((amdgpu_flat_work_group_size (2 * NL, 2 * NL),
+                                amdgpu_waves_per_eu (W <= 512 ? WHS_WAVES : (W <= 1024 ? 4 : 2))))
+k_whirl_split (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_seg_ctl* __restrict__ ctl)
+{
+	__shared__ WhLds<W> sm;
+	const uint32_t inst = blockIdx.x + P.instBase;
+	if (inst >= P.nInst)
+		return;
+	const int             tid  = threadIdx.x, lane = tid & (NL - 1);
+	const bool            horn = __builtin_amdgcn_readfirstlane (tid >> 6) == 0;
+	const tbf_inst_const& K    = cst[inst];
+	tbf_wh_state*         S    = &P.st[inst].wh;
+	float*                wr   = P.wring + (size_t)inst * 4 * W;
+	for (uint32_t i = (uint32_t)tid; i < sizeof (tbf_wh_state) / 4; i += 2 * NL)
+		((uint32_t*)&sm.st)[i] = ((const uint32_t*)S)[i];
+	if (tid == 0) {
+		sm.aReady = 0;
+		sm.ap     = 0;
+	}
+	for (uint32_t i = (uint32_t)tid; i < 4u * W; i += 2 * NL)
+		sm.wring[i / W][i % W] = wr[i];
+	__syncthreads ();
+	uint32_t     opos   = sm.st.outpos;
+	const float* inBase = P.mid2 + (size_t)inst * P.midStride;
+	int          byv = 0, rvv = -1, wsv = 0;
+	if (lane < (int)P.nBlocks) {
+		const tbf_seg_ctl& Gb = ctl_of (P, ctl, (uint32_t)lane, inst);
+		byv                   = Gb.whBypass != 0;
+		rvv                   = Gb.whRevOption;
+		wsv                   = (int)Gb.whSet;
+	}
+	float c0 = 0.f, c1 = 0.f;
+	if (P.nBlocks > 0) {
+		c0 = inBase[lane];
+		c1 = inBase[lane + NL];
+	}
+	WhOut pend;
+	pend.l  = P.outL + (size_t)inst * P.outStride + P.outOffset + lane;
+	pend.r  = P.outR + (size_t)inst * P.outStride + P.outOffset + lane;
+	pend.vl = pend.vr = 0.f;
+	int clr = -1; /* drum wave: the window whose dL / dR slots await clearing */
+	for (uint32_t blk = 0; blk < P.nBlocks; blk++) {
+		float*     oL = P.outL + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
+		float*     oR = P.outR + (size_t)inst * P.outStride + P.outOffset + (size_t)blk * TBF_BLK;
+		float      n0, n1;
+		const bool more = blk + 1 < P.nBlocks;
+		/* a new parameter set from this block on: both waves copy it (the same words; the
+		 * other wave is past its last read of the old set, k_whirl_split's barriers) */
+		const int ws = rl (wsv, blk_lane ((int)blk));
+		if (ws) {
+			const uint32_t* src = (const uint32_t*)(P.whSets + (ws - 1));
+			if (lane < (int)(sizeof (tbf_wh_params) / 4))
+				((uint32_t*)&sm.st.prm)[lane] = src[lane];
+			wave_sync ();
+		}
+		const int   nx      = blk_lane ((int)blk + 1);
+		const bool  hasNext = more && !rl (byv, nx) && !rl (wsv, nx);
+		const bool  byp     = rl (byv, blk_lane ((int)blk)) != 0;
+		const int   rev     = rl (rvv, blk_lane ((int)blk));
+		const float* inNext = inBase + (size_t)(more ? blk + 1 : blk) * TBF_BLK;
+#ifndef WHS_ONLY
+		if (horn)
+			whirl_horn<W> (P, sm, byp, rev, K, c0, c1, inNext, n0, n1, hasNext, oL, oR, pend, opos);
+		else
+			whirl_drum<W> (P, sm, byp, rev, K, c0, c1, inNext, n0, n1, opos, clr);
+#elif WHS_ONLY == 1
+		whirl_horn<W> (P, sm, byp, rev, K, c0, c1, inNext, n0, n1, hasNext, oL, oR, pend, opos);
+#else
+		whirl_drum<W> (P, sm, byp, rev, K, c0, c1, inNext, n0, n1, opos, clr);
+#endif
+		c0 = n0;
+		c1 = n1;
+	}
+	if (horn && P.nBlocks > 0)
+		wh_flush (pend);
+	__syncthreads (); /* the horn wave has read the last window's dL / dR */
+	if (!horn && clr >= 0) {
+		sm.wring[2][((uint32_t)clr + (uint32_t)lane) & (uint32_t)(W - 1)] = 0.f;
+		sm.wring[3][((uint32_t)clr + (uint32_t)lane) & (uint32_t)(W - 1)] = 0.f;
+	}
+	if (horn && lane == 0)
+		sm.st.outpos = opos;
+	__syncthreads ();
+	for (uint32_t i = (uint32_t)tid; i < sizeof (tbf_wh_state) / 4; i += 2 * NL)
+		((uint32_t*)S)[i] = ((const uint32_t*)&sm.st)[i];
+	for (uint32_t i = (uint32_t)tid; i < 4u * W; i += 2 * NL)
+		wr[i] = sm.wring[i / W][i % W];
+}
+
 /* ------------------------------------------------------------------ launch */
 /* stage k (0 k_tonegen, 1 k_mixpre, 2 k_rv_pre, 3 k_rv_core, 4 k_rv_post, 5 k_whirl) of one
  * launch chunk; the chain mode decides which stages run (tbf_chain_stages) */
@@ -3287,6 +3828,15 @@ extern "C" int tbf_launch_stage (const tbf_launch* P, int k, hipStream_t stream)
 	else if (k == 4)
 		hipLaunchKernelGGL (k_rv_post, cgrid, cblock, 0, stream, *P, P->cst, P->ctl);
 	else if (k == 5) {
+		if (P->whSplit) {
+			const dim3 sblock (2 * NL);
+			switch (P->wringLen) {
+				case 512: hipLaunchKernelGGL (k_whirl_split<512>, grid, sblock, 0, stream, *P, P->cst, P->ctl); break;
+				case 1024: hipLaunchKernelGGL (k_whirl_split<1024>, grid, sblock, 0, stream, *P, P->cst, P->ctl); break;
+				case 2048: hipLaunchKernelGGL (k_whirl_split<2048>, grid, sblock, 0, stream, *P, P->cst, P->ctl); break;
+				default: return -22;
+			}
+		} else
 		switch (P->wringLen) {
 			case 512: hipLaunchKernelGGL (k_whirl<512>, grid, block, 0, stream, *P, P->cst, P->ctl); break;
 			case 1024: hipLaunchKernelGGL (k_whirl<1024>, grid, block, 0, stream, *P, P->cst, P->ctl); break;

@@ -317,6 +317,7 @@ typedef struct tbf_launch {
 	uint32_t              instBase;
 	uint32_t              slabLen;
 	uint32_t              dbg;       /* TBF_DEBUG_* bits of tbf_engine_config.debug_flags */
+	uint32_t              whSplit;   /* k_whirl_split (two waves per instance) instead of k_whirl */
 	uint32_t*             errFlags;  /* TBF_PATH_* bits: which rare paths a launch took */
 	/* device-side control (k_tgctl) */
 	tbf_tgc_state*        tgc;       /* [inst] */

@@ -1490,6 +1490,66 @@ def test_gpu_whirl_control_functions(oracle):
     eng.close()
 
 
+@pytest.mark.parametrize("rate", [48000.0, 96000.0])
+def test_gpu_whirl_split_kernel(oracle, rate):
+    """k_whirl_split (two waves per instance: the horn and the drum halves of whirlProc2,
+    dL / dR handed over in the drum rings' consumed slots) against k_whirl, bit for bit,
+    over the whirl-control script (rotor stop / fast / brake / slow, filter and speed
+    setters, a bypass toggle) at 48 kHz (ring of 512 samples) and 96 kHz (1024), with and
+    without forced serial replays; and against the oracle.  (The engine picks k_whirl_split
+    by itself at rings > 512 samples or <= 1 instance per CU, TBF_WHIRL_SPLIT=0 / 1 force
+    either; most GPU tests here run small batches, so they run k_whirl_split.)"""
+    import os
+    import torch
+    import tunebfree_amd as T
+    n, nb = 24, 150
+    seeds = [6100 + i for i in range(n)]
+    scens = [S.whirl_control_scenario(i) for i in range(n)]
+    for i in range(0, n, 5):
+        scens[i] = sorted(scens[i] + [(90, "param", S.P_WHIRL_BYPASS, 1), (97, "param", S.P_WHIRL_BYPASS, 0)],
+                          key=lambda r: r[0])
+    outs = {}
+    for split in ("0", "1"):
+        for dbg in (0, 1):
+            os.environ["TBF_WHIRL_SPLIT"] = split
+            try:
+                eng = T.Engine(sample_rate=rate, device=0, debug_flags=dbg)
+            finally:
+                os.environ.pop("TBF_WHIRL_SPLIT", None)
+            tid = eng.template(seed=7)
+            eng.add_instances([tid] * n, seeds)
+            rows = []
+            for i, sc in enumerate(scens):
+                for (b, kind, a, v) in sc:
+                    if kind == "note":
+                        rows.append((b, i, 0, a, float(v)))
+                    elif kind == "control":
+                        rows.append((b, i, 2, eng.control_id(a), float(v)))
+                    else:
+                        rows.append((b, i, 1, a, float(v)))
+            rows.sort(key=lambda r: r[0])
+            L = torch.zeros((n, nb * 128), dtype=torch.float32, device="cuda")
+            R = torch.zeros_like(L)
+            eng.render_events_device(nb, eng.events(rows), L.data_ptr(), R.data_ptr(), nb * 128)
+            eng.synchronize()
+            outs[(split, dbg)] = (L.cpu().numpy(), R.cpu().numpy())
+            eng.close()
+            del L, R
+    ref = outs[("0", 0)]
+    for k, o in outs.items():
+        assert np.array_equal(o[0].view(np.uint32), ref[0].view(np.uint32)), k
+        assert np.array_equal(o[1].view(np.uint32), ref[1].view(np.uint32)), k
+    if rate == 48000.0:
+        from orc_bind import Template
+        sample = [0, 5, 13, n - 1]
+        tpl = Template(oracle, seed=7)
+        oL, oR, *_ = oracle_run(oracle, tpl, [seeds[i] for i in sample], [scens[i] for i in sample], nb)
+        eL, xL = compare(outs[("1", 0)][0][sample], oL)
+        eR, xR = compare(outs[("1", 0)][1][sample], oR)
+        print(f"k_whirl_split vs oracle: max|err| L={eL:.3g} R={eR:.3g} bit-exact {xL:.6f} {xR:.6f}")
+        assert max(eL, eR) <= TOL
+
+
 def test_gpu_whirl_control_events_threaded(oracle):
     """The same control functions as TBF_EV_CONTROL events inside one render of 72 blocks
     (across the 64-block chunk edge) for 1100 instances: the threaded host front end

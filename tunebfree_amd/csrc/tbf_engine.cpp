@@ -478,8 +478,9 @@ int tbf_engine_create (const tbf_engine_config* cfg, tbf_engine** out)
 		e->parCtl      = !(hs && hs[0] == '1');
 		const char* df = getenv ("TBF_DEVICE_FRONT"); /* 0: note-only chunks step on the host too (A/B) */
 		e->frontOn     = !(df && df[0] == '0');
-		if (const char* sp = getenv ("TBF_WHIRL_SPLIT")) /* 1: k_whirl_split (two waves per instance) */
-			e->whSplit = sp[0] != '0';
+		if (const char* sp = getenv ("TBF_WHIRL_SPLIT")) /* 0 / 1: k_whirl / k_whirl_split always */
+			e->whSplit = sp[0] != '0' ? 1 : 0;
+		e->nCU = (uint32_t)std::max (ncu, 1);
 		if (const char* fm = getenv ("TBF_FRONT_MIN")) /* events a chunk needs for the device front end */
 			e->frontMin = (uint32_t)std::max (atoi (fm), 1);
 	}
@@ -2131,7 +2132,8 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 	P.slabLen   = e->slabLen;
 	P.errFlags  = e->err.p;
 	P.dbg       = e->cfg.debug_flags;
-	P.whSplit   = e->whSplit ? 1u : 0u;
+	/* k_whirl_split where it keeps more waves per SIMD than k_whirl (tbf_render.hip) */
+	P.whSplit = e->whSplit >= 0 ? (uint32_t)e->whSplit : (e->wringLen > 512 || n <= e->nCU) ? 1u : 0u;
 	P.rvLds     = e->rvLdsOn && e->rvLdsFit;
 	P.rvGrid    = e->rvGrid;
 	P.rvWork    = e->rvWork.p;

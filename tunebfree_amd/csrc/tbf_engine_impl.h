@@ -280,7 +280,8 @@ struct tbf_engine {
 	 * parity; region p's persistent entries are refreshed from hCtl when they are older
 	 * than its version (ctlVer counts the changes of hCtl) */
 	uint64_t                                ctlVer = 1, regionVer[2] = {0, 0};
-	bool                                    whSplit = false; /* k_whirl_split (TBF_WHIRL_SPLIT=1) instead of k_whirl */
+	int                                     whSplit = -1; /* k_whirl_split: -1 at rings > 512 or <= 1 instance per CU, 0 / 1 (TBF_WHIRL_SPLIT) */
+	uint32_t                                nCU     = 256; /* the device's CUs */
 	uint32_t                                frontMin = 64; /* events a chunk needs for the device front end (TBF_FRONT_MIN; 64: profiles/r05/s23) */
 	bool                                    parCtl = true; /* TBF_HOST_SERIAL=1 steps serially */
 	/* threaded host control (stepChunkParallel): per worker, kept between chunks so the

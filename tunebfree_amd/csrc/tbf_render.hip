@@ -3258,13 +3258,20 @@ k_whirl (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
  * those slots after the next barrier, before its own adds of that sub-block (the adds land
  * >= 79 slots ahead and the ring holds write-ahead + 68 slots, so an add of sub-block k + 1
  * may wrap into window k only after it is cleared).  Each rotor's speed update is its own
- * half of whirl_speed.  So every instance is two waves of about half the instructions, 8
- * waves per SIMD at the 512-sample ring (a latency-bound kernel: one wave alone per SIMD ran
- * 7.1 ms per 512 blocks against 9.4 at 4 per SIMD, profiles/r05/s26), and the same
- * operations in the same order as k_whirl. */
+ * half of whirl_speed.  So every instance is two waves of about half the instructions
+ * (a latency-bound kernel: one wave alone per SIMD ran 7.1 ms per 512 blocks against 9.4
+ * at 4 per SIMD, profiles/r05/s26), and the same operations in the same order as k_whirl.
+ * The engine launches it where it wins as rendered: rings of 1024 or 2048 samples (k_whirl's
+ * LDS leaves it 2 / 1 waves per SIMD; the 96 kHz bench 156.4 -> 151.5 ms per step) and at
+ * most one instance per CU (real-time periods: 128 frames p50 0.213 -> 0.208 ms).  Alone it
+ * is faster up to 8 instances per CU too (6.34 vs 7.20 ms per 512 blocks at 2048 instances),
+ * but rendered beside the other stages the 2048-instance step went 77.6 -> 91.3 ms; at 4096
+ * k_whirl's 4 waves per SIMD win outright (9.4 against 14.5 ms in two rounds).
+ * profiles/r05/s29, s30. */
 
 #ifndef WHS_WAVES
-#define WHS_WAVES 8 /* k_whirl_split waves per SIMD at the 512-sample ring (8: all 4096 instances at once) */
+#define WHS_WAVES 4 /* k_whirl_split waves per SIMD at the 512-sample ring: 128 VGPRs, 8 instances per CU (at 8
+                      * per SIMD, 64 VGPRs, all 4096 at once but with spills in the sub-block loop: slower) */
 #endif
 /* a wave-uniform value moved to scalar registers */
 __device__ __forceinline__ float sgpr_f (float v) { return __int_as_float (__builtin_amdgcn_readfirstlane (__float_as_int (v))); }

@@ -1703,16 +1703,15 @@ static void scanChunk (uint32_t n, uint32_t b0, const tbf_event* ev, uint32_t ev
 	cs.per = (n + cs.T - 1) / cs.T;
 	cs.Te  = std::max (1u, std::min (hostThreads (), (nev + 32767) / 32768));
 	cs.seg = (nev + cs.Te - 1) / cs.Te;
-	if (cl && cs.bucket.size () < (size_t)cs.Te * cs.T)
-		cs.bucket.resize ((size_t)cs.Te * cs.T);
+	if (cl) {
+		cs.rec.resize (std::max<uint32_t> (nev, 1));
+		cs.boff.resize ((size_t)cs.Te * (cs.T + 1));
+	}
 	std::vector<char> pe (cs.Te, 0), bd (cs.Te, 0), fr (cs.Te, 0);
 	parallelFor (cs.Te, [&] (uint32_t sgm) {
 		const uint32_t k0 = evBeg + std::min (nev, sgm * cs.seg), k1 = evBeg + std::min (nev, (sgm + 1) * cs.seg);
 		bool           p = false, b = false, f = cl != nullptr; /* locals: the flags share a cache line */
-		std::vector<ChunkScan::Rec>* bk = f ? cs.bucket.data () + (size_t)sgm * cs.T : nullptr;
-		if (f)
-			for (unsigned t = 0; t < cs.T; t++)
-				bk[t].clear ();
+		uint32_t       c[17] = {};                               /* events per instance range (T <= 16) */
 		for (uint32_t k = k0; k < k1; k++) {
 			const tbf_event& E = ev[k];
 			p                  = p || E.kind == TBF_EV_PROGRAM;
@@ -1723,9 +1722,23 @@ static void scanChunk (uint32_t n, uint32_t b0, const tbf_event* ev, uint32_t ev
 			}
 			if (f) {
 				f = (E.kind == TBF_EV_NOTE || (E.kind == TBF_EV_PARAM && frontParam (E))) && cl[E.inst];
-				bk[E.inst / cs.per].push_back ({E.inst, (E.block - b0) << 2 | (E.kind == TBF_EV_PARAM ? 1u : 0u) |
-				                                            (E.value != 0.0 ? 2u : 0u),
-				                                E.id, (float)E.value});
+				c[E.inst / cs.per]++;
+			}
+		}
+		if (f) { /* the records, by range, into this segment's own part of rec (no shared lines) */
+			uint32_t* bo = cs.boff.data () + (size_t)sgm * (cs.T + 1);
+			uint32_t  at[16];
+			bo[0] = k0 - evBeg;
+			for (unsigned t = 0; t < cs.T; t++) {
+				at[t]     = bo[t];
+				bo[t + 1] = bo[t] + c[t];
+			}
+			ChunkScan::Rec* rec = cs.rec.data ();
+			for (uint32_t k = k0; k < k1; k++) {
+				const tbf_event& E = ev[k];
+				rec[at[E.inst / cs.per]++] = {E.inst, (E.block - b0) << 2 | (E.kind == TBF_EV_PARAM ? 1u : 0u) |
+				                                          (E.value != 0.0 ? 2u : 0u),
+				                              E.id, (float)E.value};
 			}
 		}
 		pe[sgm] = p;
@@ -1759,10 +1772,11 @@ static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0
 	/* the events by instance range come from scanChunk's buckets, in event order */
 	const auto            f1 = std::chrono::steady_clock::now ();
 	std::vector<uint32_t> wbase (T + 1, 0);
+	auto seg = [&] (unsigned sgm, unsigned t) { return cs.boff.data () + (size_t)sgm * (T + 1) + t; };
 	for (unsigned t = 0; t < T; t++) {
 		size_t c = 0;
 		for (unsigned sgm = 0; sgm < cs.Te; sgm++)
-			c += cs.bucket[(size_t)sgm * T + t].size ();
+			c += seg (sgm, t)[1] - seg (sgm, t)[0];
 		wbase[t + 1] = wbase[t] + (uint32_t)c;
 	}
 	e->hFevOff.resize (n + 1);
@@ -1779,8 +1793,8 @@ static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0
 		auto&                  es = o.erec;
 		eo.assign ((size_t)(i1 > i0 ? i1 - i0 : 0) + 1, 0);
 		for (unsigned sgm = 0; sgm < cs.Te; sgm++)
-			for (const ChunkScan::Rec& r : cs.bucket[(size_t)sgm * T + t])
-				eo[r.inst - i0 + 1]++;
+			for (uint32_t k = seg (sgm, t)[0]; k < seg (sgm, t)[1]; k++)
+				eo[cs.rec[k].inst - i0 + 1]++;
 		for (uint32_t i = i0; i < i1; i++)
 			eo[i - i0 + 1] += eo[i - i0];
 		es.resize (wbase[t + 1] - wbase[t]);
@@ -1789,8 +1803,10 @@ static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0
 			std::vector<uint32_t>& fill = o.efill;
 			fill.assign (eo.begin (), eo.end () - 1);
 			for (unsigned sgm = 0; sgm < cs.Te; sgm++)
-				for (const ChunkScan::Rec& r : cs.bucket[(size_t)sgm * T + t])
+				for (uint32_t k = seg (sgm, t)[0]; k < seg (sgm, t)[1]; k++) {
+					const ChunkScan::Rec& r = cs.rec[k];
 					es[fill[r.inst - i0]++] = {r.bf >> 2, r.id, r.v, r.bf & 3u};
+				}
 		}
 		const auto g1 = std::chrono::steady_clock::now ();
 		for (uint32_t i = i0; i < i1; i++) {
@@ -2324,7 +2340,12 @@ static int renderImpl (tbf_engine* e, uint32_t nblocks, float* dL, float* dR, ui
 		bool       progEv = false, badEv = false, front = false;
 		const bool frontCand = e->devCtl && dpipe && e->frontOn && evEnd - evi >= e->frontMin && frontCleanAll (e);
 		ChunkScan& cs        = e->scan;
+		const auto sc0       = std::chrono::steady_clock::now ();
 		scanChunk (n, b0, ev, evi, evEnd, frontCand ? e->fclean.data () : nullptr, progEv, badEv, front, cs);
+		if (getenv ("TBF_DEBUG_HOST_PHASES"))
+			fprintf (stderr, "chunk %llu: clean %.3f ms, scan %.3f ms (%u events)\n", (unsigned long long)e->chunkSeq,
+			         std::chrono::duration<double, std::milli> (sc0 - hc0).count (),
+			         std::chrono::duration<double, std::milli> (std::chrono::steady_clock::now () - sc0).count (), evEnd - evi);
 		if (badEv)
 			return fail (-22, "event for a bad instance");
 		bool dfront = false;

@@ -146,14 +146,16 @@ struct ChunkScan {
 	unsigned              T = 1, Te = 1; /* instance ranges, event segments */
 	uint32_t              per = 1, seg = 0;
 	/* the events of segment s for instance range t, in order, as compact records (written by
-	 * the scan itself, so the front end never reads the 24-B events again): bucket s T + t */
+	 * the scan itself, so the front end never reads the 24-B events again): rec[boff[s (T +
+	 * 1) + t] .. boff[s (T + 1) + t + 1]), inside segment s's own part of rec */
 	struct Rec {
 		uint32_t inst;
 		uint32_t bf; /* block in the chunk << 2 | 1: parameter event | 2: value != 0 */
 		int32_t  id;
 		float    v;
 	};
-	std::vector<std::vector<Rec>> bucket;
+	std::vector<Rec>      rec;
+	std::vector<uint32_t> boff;
 };
 
 template <typename T>

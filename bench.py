@@ -290,18 +290,19 @@ def lib_hash():
     return hashlib.sha256(Path(T.LIB_PATH).read_bytes()).hexdigest()[:16]
 
 
-def kernel_bounds(ms, pmc):
+def kernel_bounds(ms, pmc, scale=1.0):
     """One kernel against its two ceilings, from its unloaded launch time (ms) and its PMC
-    counts per launch (tools/kernel_pmc.py): HBM bytes / time against 8 TB/s, and VALU issue
-    cycles (instruction counts x their SIMD-32 issue cost) / time against every SIMD issuing
-    at 2.4 GHz.  Both fractions are of the whole chip."""
-    c = pmc["counters"]
+    counts per launch (tools/kernel_pmc.py), scaled by `scale` from the profiled launch's
+    samples to the timed launch's: HBM bytes / time against 8 TB/s, and VALU issue cycles
+    (instruction counts x their SIMD-32 issue cost) / time against every SIMD issuing at
+    2.4 GHz.  Both fractions are of the whole chip."""
+    c = {k: v * scale for k, v in pmc["counters"].items()}
     row = {"kernel": pmc.get("kernel"), "ms_isolated": ms, "pmc_ms": pmc.get("pmc_ms")}
     sec = ms * 1e-3
     if "hbm_bytes" in pmc:
-        row["hbm_bytes"] = pmc["hbm_bytes"]
+        row["hbm_bytes"] = pmc["hbm_bytes"] * scale
         row["hbm_bytes_per_stereo_sample"] = pmc.get("hbm_bytes_per_stereo_sample")
-        row["hbm_gbs"] = pmc["hbm_bytes"] / sec / 1e9
+        row["hbm_gbs"] = row["hbm_bytes"] / sec / 1e9
         row["hbm_frac"] = row["hbm_gbs"] / HBM_PEAK_GBS
     if "SQ_INSTS_VALU" in c:
         f64 = sum(c.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64"))
@@ -345,7 +346,7 @@ def roofline(a, B, nsamp, elapsed, samples_launch, launches, algo, kern, kern_is
     rows = {}
     for k, ms in times.items():
         if pmc and k in pmc["kernels"]:
-            rows[k] = kernel_bounds(ms, pmc["kernels"][k])
+            rows[k] = kernel_bounds(ms, pmc["kernels"][k], samples_launch / pmc["samples_per_launch"])
         else:
             rows[k] = {"ms_isolated": ms if kern_iso else None}
         rows[k]["ms_as_rendered"] = kern.get(k)
@@ -356,8 +357,9 @@ def roofline(a, B, nsamp, elapsed, samples_launch, launches, algo, kern, kern_is
             "bound": d.get("bound"), "achieved": None, "peak": None, "unit": None, "frac": None,
             "traffic": d.get("hbm_bytes"),
             "hbm_frac": d.get("hbm_frac"), "valu_frac": d.get("valu_frac"),
+            # the 424-B model's bytes for this kernel's launch (no fraction: k_rv_core_lds keeps its
+            # 384 B per sample of line traffic in LDS, so they would read above the HBM peak)
             "algorithmic_bytes_per_launch": samples_launch * algo.get(dom, 0),
-            "algorithmic_hbm_frac": samples_launch * algo.get(dom, 0) / (times[dom] * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "launches_per_step": launches,
             "step_bytes_per_stereo_sample": step_bytes, "step_gbs_per_gpu": step_gbs,
             "step_frac": step_gbs / HBM_PEAK_GBS,

@@ -46,7 +46,7 @@ for s in $STEPS; do
 		run pwrite 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pwrite" -o run --output-format csv -- python3 bench.py $PB
 		run psqa 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE GRBM_COUNT -d "$OUT/psqa" -o run --output-format csv -- python3 bench.py $PB
 		run psqb 300 rocprofv3 --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 $T32 SQ_WAIT_INST_ANY SQ_ACTIVE_INST_LDS SQ_BUSY_CYCLES -d "$OUT/psqb" -o run --output-format csv -- python3 bench.py $PB
-		run psum 60 python3 tools/kernel_pmc.py "$OUT/pfetch" "$OUT/pwrite" "$OUT/psqa" "$OUT/psqb" --blocks ${BLOCKS:-2048} --out "$OUT/kernel_pmc.json"
+		run psum 60 python3 tools/kernel_pmc.py "$OUT/pfetch" "$OUT/pwrite" "$OUT/psqa" "$OUT/psqb" --blocks ${BLOCKS:-2048} --launch-blocks ${LAUNCH_BLOCKS:-512} --out "$OUT/kernel_pmc.json"
 		;;
 	fbench) # the driver's bench (20 steps, 5 warmup) with this session's PMC profile
 		run fbench 900 python3 bench.py --steps 20 --warmup 5 --pmc "$OUT/kernel_pmc.json"

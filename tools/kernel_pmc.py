@@ -8,8 +8,12 @@ bench.py reads the output (profiles/kernel_pmc.json) and divides the per-launch 
 each kernel's unloaded launch time, measured live, to report every kernel against the
 ceiling that binds it (HBM bytes, VALU issue) -- only when the build hash matches.
 
+The counters are per launch, so per --launch-blocks blocks (the engine's steady chunk the
+profiled bench rendered in; bench.py scales them to the launches it times).
+
 usage: python tools/kernel_pmc.py PASS_DIR [PASS_DIR ...] --batch 4096 --blocks 2048 \
-           --sr 48000 --chain 0 --lib tunebfree_amd/libtbf.so --out profiles/kernel_pmc.json"""
+           --launch-blocks 512 --sr 48000 --chain 0 --lib tunebfree_amd/libtbf.so \
+           --out profiles/kernel_pmc.json"""
 import argparse
 import csv
 import hashlib
@@ -58,6 +62,7 @@ def main():
     ap.add_argument("dirs", nargs="+")
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--blocks", type=int, default=2048)
+    ap.add_argument("--launch-blocks", type=int, default=None, help="blocks per launch (default: --blocks)")
     ap.add_argument("--sr", type=float, default=48000.0)
     ap.add_argument("--chain", type=int, default=0)
     ap.add_argument("--lib", default="tunebfree_amd/libtbf.so")
@@ -78,10 +83,11 @@ def main():
             durs[st].append(ms)
             for c, v in cs.items():
                 per[st][c].append(v)
-    samples = a.batch * a.blocks * 128
+    lb = a.launch_blocks or a.blocks
+    samples = a.batch * lb * 128
     res = {"build": lib_hash(a.lib), "lib": a.lib,
            "workload": {"batch": a.batch, "blocks": a.blocks, "sr": a.sr, "chain": a.chain},
-           "samples_per_launch": samples, "fetch_scale": FETCH_SCALE, "write_scale": WRITE_SCALE,
+           "launch_blocks": lb, "samples_per_launch": samples, "fetch_scale": FETCH_SCALE, "write_scale": WRITE_SCALE,
            "source": "rocprofv3 --pmc passes: " + ", ".join(a.dirs),
            "units": "per launch (median over full-size launches); FETCH/WRITE in bytes after the scale; "
                     "SQ_*_CYCLES and SQ_WAIT_*/SQ_ACTIVE_* in quad-cycles summed over waves; "

@@ -2220,10 +2220,19 @@ k_rv_pre (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 	}
 }
 
+/* k_rv_post's chain block: RVP_CB instances per workgroup (k_rv_pre keeps RVC_CB) */
+#ifndef RVP_CB
+#define RVP_CB 16 /* 256 workgroups: all CUs (32 per workgroup: step 129.7 -> 127.5 ms at 16, profiles/r05/s37) */
+#endif
+#define RVP_NC (2 * RVP_CB)
+#define RVP_ROWS (RVP_NC + (RVP_NC < NL)) /* chain rows, + one that the idle chain lanes use */
+#define RVP_NTK (RVP_CB / RVC_H)
+static_assert (RVP_CB % RVC_H == 0 && RVP_NC <= NL, "k_rv_post chain-block geometry");
+
 struct RvPostLds {
-	double   y[2][RVC_NC][RVC_S]; /* tap mix -> biquadB output, in place */
-	double   z[2][RVC_NC][RVC_S]; /* asin output -> biquadC output, in place */
-	uint32_t f[2][RVC_NC][RVC_S]; /* fpdL / fpdR before each sample (entry RVC_T: after the tile) */
+	double   y[2][RVP_ROWS][RVC_S]; /* tap mix -> biquadB output, in place */
+	double   z[2][RVP_ROWS][RVC_S]; /* asin output -> biquadC output, in place */
+	uint32_t f[2][RVP_ROWS][RVC_S]; /* fpdL / fpdR before each sample (entry RVC_T: after the tile) */
 };
 
 /* biquadB, clamp + asin, biquadC, dry mix, dither, (L + R) / sqrt 2 (src/reverb.cpp:733-787)
@@ -2234,14 +2243,15 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 {
 	__shared__ RvPostLds sm;
 	const int      w = __builtin_amdgcn_readfirstlane (threadIdx.x >> 6), lane = threadIdx.x & (NL - 1);
-	const uint32_t inst0 = P.instBase + blockIdx.x * RVC_CB;
+	const uint32_t inst0 = P.instBase + blockIdx.x * RVP_CB;
 	if (inst0 >= P.nInst)
 		return;
-	const int     nj  = (int)min ((uint32_t)RVC_CB, P.nInst - inst0);
+	const int     nj  = (int)min ((uint32_t)RVP_CB, P.nInst - inst0);
 	const int     nT  = (int)P.nBlocks * (TBF_BLK / RVC_T);
 	const int     nIt = nT + 4;
 	const int     cj = lane >> 1, cc = lane & 1;
 	const bool    cok = cj < nj;
+	const int     crow = lane < RVP_NC ? lane : RVP_NC; /* chain lanes past the block's chains: the idle row */
 	tbf_rv_state* CS  = &P.st[inst0 + (cok ? cj : 0)].rv;
 	if (w == 0) {
 		/* biquadB of tile it - 1 and biquadC of tile it - 3, two chains per lane in one
@@ -2254,8 +2264,8 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 #pragma unroll 1
 		for (int it = 0; it < nIt; it++) {
 			const bool doB = it >= 1 && it - 1 < nT, doC = it >= 3 && it - 3 < nT;
-			double*    rb  = sm.y[(it - 1) & 1][lane];
-			double*    rc  = sm.z[(it - 1) & 1][lane];
+			double*    rb  = sm.y[(it - 1) & 1][crow];
+			double*    rc  = sm.z[(it - 1) & 1][crow];
 			if (doB && doC) {
 				double* const row[2] = {rb, rc};
 				rvc_serial<2> (row, c, s);
@@ -2290,7 +2300,7 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 #pragma unroll 1
 		for (int it = 0; it < nIt; it++) {
 			if (it >= 3 && it - 3 < nT)
-				rvc_dither_row (sm.f[(it - 3) & 1][lane], fs);
+				rvc_dither_row (sm.f[(it - 3) & 1][crow], fs);
 			__syncthreads ();
 		}
 		if (cok) {
@@ -2305,13 +2315,13 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 	 * parity (see k_rv_pre) */
 	const bool   tap = P.chain == TBF_CHAIN_TAP_REVERB;
 	const int    h = w - 2, hc = lane >> 5, n = lane & (RVC_T - 1);
-	double       pB[2][RVC_NTK], wetv[RVC_NTK];
-	float        pIn[2][RVC_NTK];
-	const double* rb[RVC_NTK];
-	const float*  in[RVC_NTK];
-	float*        out[RVC_NTK];
+	double       pB[2][RVP_NTK], wetv[RVP_NTK];
+	float        pIn[2][RVP_NTK];
+	const double* rb[RVP_NTK];
+	const float*  in[RVP_NTK];
+	float*        out[RVP_NTK];
 #pragma unroll
-	for (int t = 0; t < RVC_NTK; t++) {
+	for (int t = 0; t < RVP_NTK; t++) {
 		const int      j    = h + t * RVC_H;
 		const uint32_t inst = inst0 + (j < nj ? j : nj - 1);
 		rb[t]     = rv_buf (P.rvB, P, inst, hc) + n;
@@ -2324,15 +2334,15 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 		pIn[0][t] = pIn[1][t] = 0.f;
 	}
 	__syncthreads ();
-	auto step = [&] (const int it, double (&qB)[RVC_NTK], float (&qIn)[RVC_NTK]) {
+	auto step = [&] (const int it, double (&qB)[RVP_NTK], float (&qIn)[RVP_NTK]) {
 		const int b = it & 1; /* tiles it, it - 2 and it - 4 share the buffers */
 		/* output of tile it - 4: dry mix, dither, mono sum (src/reverb.cpp:766-787); the
 		 * half-waves hold L and R, and 0.7071 (L + R) == 0.7071 (R + L) */
-		float yv[RVC_NTK];
+		float yv[RVP_NTK];
 		if (it >= 4) {
 			const int ob = blk_lane (((it - 4) * RVC_T) / TBF_BLK);
 #pragma unroll
-			for (int t = 0; t < RVC_NTK; t++) {
+			for (int t = 0; t < RVP_NTK; t++) {
 				const double wet = rld (wetv[t], ob);
 				const int    r   = 2 * (h + t * RVC_H) + hc;
 				double       x   = sm.z[b][r][n];
@@ -2349,13 +2359,13 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 		}
 		/* clamp + asin of tile it - 2 (src/reverb.cpp:743-751); the tap mix of tile it,
 		 * which reuses the biquadB buffer, after the reads */
-		double av[RVC_NTK];
+		double av[RVP_NTK];
 #pragma unroll
-		for (int t = 0; t < RVC_NTK; t++)
+		for (int t = 0; t < RVP_NTK; t++)
 			av[t] = sm.y[b][2 * (h + t * RVC_H) + hc][n];
 		if (it < nT) {
 #pragma unroll
-			for (int t = 0; t < RVC_NTK; t++)
+			for (int t = 0; t < RVP_NTK; t++)
 				sm.y[b][2 * (h + t * RVC_H) + hc][n] = qB[t];
 		}
 		/* HBM reads into the set just consumed (indices clamped, so the loads need no
@@ -2363,15 +2373,15 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 		 * iteration it + 2) */
 		const int tb = min (it + 2, nT - 1), ti = max (0, min (it - 2, nT - 1));
 #pragma unroll
-		for (int t = 0; t < RVC_NTK; t++) {
+		for (int t = 0; t < RVP_NTK; t++) {
 			qB[t]  = rb[t][(size_t)tb * RVC_T];
 			qIn[t] = in[t][(size_t)ti * RVC_T];
 		}
 		if (it >= 2 && it - 2 < nT) {
-			double y[RVC_NTK];
+			double y[RVP_NTK];
 			bool   small = true;
 #pragma unroll
-			for (int t = 0; t < RVC_NTK; t++) {
+			for (int t = 0; t < RVP_NTK; t++) {
 				y[t] = av[t];
 				if (y[t] > 1.0)
 					y[t] = 1.0;
@@ -2383,18 +2393,18 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 			 * that branch alone, straight-line, so the tasks' chains interleave (tbf_sin.h) */
 			if (__all (small)) {
 #pragma unroll
-				for (int t = 0; t < RVC_NTK; t++)
+				for (int t = 0; t < RVP_NTK; t++)
 					sm.z[b][2 * (h + t * RVC_H) + hc][n] = tbf_asin_poly (y[t]);
 			} else {
 #pragma unroll
-				for (int t = 0; t < RVC_NTK; t++)
+				for (int t = 0; t < RVP_NTK; t++)
 					sm.z[b][2 * (h + t * RVC_H) + hc][n] = asin (y[t]);
 			}
 		}
 		if (it >= 4) {
 			const size_t so = (size_t)(it - 4) * RVC_T;
 #pragma unroll
-			for (int t = 0; t < RVC_NTK; t++)
+			for (int t = 0; t < RVP_NTK; t++)
 				if (h + t * RVC_H < nj && (tap || hc == 0))
 					out[t][so] = yv[t];
 		}
@@ -3833,7 +3843,7 @@ extern "C" int tbf_launch_stage (const tbf_launch* P, int k, hipStream_t stream)
 		} else
 			hipLaunchKernelGGL (k_rv_core, dim3 (2 * P->nInst), block, 0, stream, *P, P->cst);
 	else if (k == 4)
-		hipLaunchKernelGGL (k_rv_post, cgrid, cblock, 0, stream, *P, P->cst, P->ctl);
+		hipLaunchKernelGGL (k_rv_post, dim3 ((P->nInst + RVP_CB - 1) / RVP_CB), cblock, 0, stream, *P, P->cst, P->ctl);
 	else if (k == 5) {
 		if (P->whSplit) {
 			const dim3 sblock (2 * NL);

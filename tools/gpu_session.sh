@@ -8,7 +8,11 @@
 #   pmc     per-kernel PMC profile (FETCH_SIZE, WRITE_SIZE, two SQ passes: separate runs) ->
 #           kernel_pmc.json, which bench.py's roofline reads
 #   fbench  the driver's bench (20 steps, 5 warmup) with that profile
-#   cfg     secondary lines: configs[1] at 256 instances, configs[4] shape, dense events
+#   cfg     secondary lines: configs[1] at 256 instances, configs[4] shape, dense events, RT latency
+#   steady  the bench with the steady chunk capped at 256 .. 2048 blocks (footprint vs speed)
+#   front   the device front end's event gate (sparse / dense modes) and its host phases
+#   split   k_whirl vs k_whirl_split (96 kHz, 2048 instances, RT periods)
+#   wscale  unloaded kernel times at 4096 / 2048 / 1024 instances
 #   bench   the default bench without the CPU leg
 #   ab:V=X  the default bench with environment switch V=X
 #   prof    k_rv_core_lds / k_whirl / k_tonegen phase clocks (tools/build_prof.sh variants)
@@ -36,6 +40,9 @@ for s in $STEPS; do
 	full)
 		run fstats 300 rocprofv3 --kernel-trace --stats -d "$OUT/fstats" -o run --output-format csv -- python3 bench.py $NC
 		run fsum 60 python3 tools/kernel_stats.py "$(find "$OUT/fstats" -name 'run_kernel_trace.csv' | head -1)" --out "$OUT/kernel_stats_full.json"
+		# the concurrency profile of the timed steps alone (no kernel-time, isolated or steady64 passes)
+		run tstats 300 rocprofv3 --kernel-trace -d "$OUT/tstats" -o run --output-format csv -- python3 bench.py $NC --steps 12 --warmup 3 --isolated 0 --steady64 0 --kernel-steps 0
+		run tline 60 python3 tools/timeline.py "$(find "$OUT/tstats" -name 'run_kernel_trace.csv' | head -1)" --out "$OUT/timeline.json"
 		;;
 	pmc) # the per-kernel PMC profile bench.py's roofline reads: FETCH_SIZE, WRITE_SIZE and two
 		# SQ passes (each its own run), full-size launches, then tools/kernel_pmc.py
@@ -61,6 +68,21 @@ for s in $STEPS; do
 	steady) # the bench at 2048-block steps with the steady chunk capped (stage-buffer footprint vs speed)
 		for c in 256 512 1024 2048; do
 			run "steady$c" 400 env TBF_STEADY_CHUNK=$c python3 bench.py --cpu-baseline 0 --check 0 --stage-check 0 --steps 10 --warmup 3 --isolated 0 --steady64 0
+		done ;;
+	front) # the device front end: sparse and dense modes at two event gates, then its host phases
+		for fm in 1024 64; do
+			run "front_fm$fm" 400 env TBF_FRONT_MIN=$fm python3 -u tools/dense_events.py --modes sparse256,sparse64,every8,dense --out "$OUT/dense_fm$fm.json"
+		done
+		run front_phases 300 env TBF_DEBUG_HOST_PHASES=1 python3 -u tools/dense_events.py --modes dense --steps 4 --warmup 2 ;;
+	split) # k_whirl against k_whirl_split: 96 kHz, 2048 instances, real-time periods
+		for sp in 0 1; do
+			run "split${sp}_cfg5" 300 env TBF_WHIRL_SPLIT=$sp python3 bench.py --workload cfg5 --cpu-baseline 0 --check 4 --steps 3 --warmup 1 --steady64 0 --isolated 2
+			run "split${sp}_b2048" 300 env TBF_WHIRL_SPLIT=$sp python3 bench.py --batch 2048 --cpu-baseline 0 --check 4 --steps 5 --warmup 2 --steady64 0 --isolated 2
+			run "split${sp}_rt" 300 env TBF_WHIRL_SPLIT=$sp python3 -u tools/rt_latency.py --out "$OUT/rt_split$sp.json"
+		done ;;
+	wscale) # unloaded kernel times at 4096 / 2048 / 1024 instances (waves per SIMD vs latency)
+		for b in 4096 2048 1024; do
+			run "wscale$b" 300 python3 bench.py --batch $b --cpu-baseline 0 --check 0 --stage-check 0 --steps 3 --warmup 1 --isolated 2 --steady64 0
 		done ;;
 	bench) run bench 300 python3 bench.py --cpu-baseline 0 ;;
 	bench2048x2) # two driver-length benches (A/B baseline on one box)

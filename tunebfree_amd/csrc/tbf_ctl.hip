@@ -39,10 +39,12 @@
 #define NW TBF_NW
 
 /* the per-wheel arrays, staged in dynamic LDS for the launch's wheel count P.ctlNw (the
- * largest wheel any play matrix names, + 1: 92 for the tonewheel organ, so ~13 KB and
- * about 11 workgroups per CU instead of 4 at TBF_NW + 1) */
+ * largest wheel any play matrix names, + 1: 184 for the tonewheel organ with its
+ * crosstalk wheels, 35 B a wheel, so ~6.4 KB + CtlLds: 16 workgroups per CU, and the
+ * bench's 4096 instances in one round).  The bus levels ([nw][27] floats, 20 KB at 184
+ * wheels: 5 workgroups per CU, four rounds, when they were staged here too) stay in the
+ * instance's tbf_tgc_state in HBM, read and written in place (ctl_bl_load). */
 struct CtlW {
-	float*    bl;      /* [nw][27] bus levels */
 	float*    sums;    /* [nw][6]  routed sums */
 	int32_t*  ref;     /* [nw] */
 	uint16_t* list;    /* [nw] activeOscList */
@@ -51,25 +53,23 @@ struct CtlW {
 	uint8_t*  rf;      /* [nw] */
 };
 #define CTL_MSGCAP 256 /* a launch's messages prefetched into LDS (more: read per block) */
+#define FR_CAP 1024    /* k_front: an instance's events staged in LDS (more: read from HBM) */
 
 struct CtlLds {
 	float    dbg[27];
-	uint32_t L;
-	uint32_t nrem;
 	uint32_t mc0[CTL_MSGCAP], mc1[CTL_MSGCAP]; /* each message's keyContrib range */
 	uint16_t msg[CTL_MSGCAP];
 };
 
 __host__ __device__ constexpr size_t ctl_wbytes (uint32_t nw)
 {
-	return (size_t)nw * (27 * 4 + 6 * 4 + 4 + 2 + 2 + 2 + 1);
+	return (size_t)nw * (6 * 4 + 4 + 2 + 2 + 2 + 1);
 }
 
 __device__ __forceinline__ CtlW ctl_carve (uint8_t* p, uint32_t nw)
 {
 	CtlW w;
-	w.bl      = (float*)p;
-	w.sums    = w.bl + (size_t)nw * 27;
+	w.sums    = (float*)p;
 	w.ref     = (int32_t*)(w.sums + (size_t)nw * 6);
 	w.list    = (uint16_t*)(w.ref + nw);
 	w.acl1    = (int16_t*)(w.list + nw);
@@ -80,6 +80,20 @@ __device__ __forceinline__ CtlW ctl_carve (uint8_t* p, uint32_t nw)
 
 __device__ __forceinline__ uint64_t lanemask_lt () { return (1ull << threadIdx.x) - 1ull; }
 
+/* TBF_CTL_PROF (A/B builds only): shader-clock cycles per k_tgctl phase, printed by a few
+ * workgroups */
+#ifdef TBF_CTL_PROF
+#define CTL_T(v) const uint64_t v = __builtin_amdgcn_s_memtime ()
+#define CTL_ACC(acc, t0) acc += __builtin_amdgcn_s_memtime () - (t0)
+#define CTL_PARAM , uint64_t (&pt)[4]
+#define CTL_ARG , pt
+#else
+#define CTL_T(v)
+#define CTL_ACC(acc, t0)
+#define CTL_PARAM
+#define CTL_ARG
+#endif
+
 /* the workgroup is one wave: LDS accesses of a wave execute in issue order, so a read
  * after a write sees it; only the compiler must not move LDS accesses across this point
  * (a __syncthreads also waited for every outstanding global store: the program stores) */
@@ -89,77 +103,136 @@ __device__ __forceinline__ void wave_sync ()
 	__builtin_amdgcn_wave_barrier ();
 }
 
-/* one key message (src/tonegen.cpp:3270-3322) */
-__device__ void ctl_message (CtlLds& sm, const CtlW& W, const tbf_contrib* __restrict__ kc, uint32_t c0, uint32_t c1,
-                             bool on)
+/* the same for LDS accesses whose data flow stays within a lane or goes through wave-uniform
+ * registers: only the compiler's order matters */
+__device__ __forceinline__ void lds_order () { __asm__ __volatile__ ("" ::: "memory"); }
+
+/* A bus level, read at the device's coherence point (L2, not the CU's L1), since another
+ * lane of the wave may have written it in an earlier message: the wave's vector memory
+ * instructions reach L2 in issue order, so the read follows the write. */
+__device__ __forceinline__ float ctl_bl_load (const float* p)
 {
-	const int lane = threadIdx.x;
-	for (uint32_t base = c0; base < c1; base += NL) {
-		const uint32_t e     = base + lane;
-		const bool     valid = e < c1;
-		uint32_t       w = 0, bus = 0;
-		float          lev  = 0.f;
-		bool           lead = false;
-		if (valid) {
-			const tbf_contrib c = kc[e];
-			w                   = c.wheel;
-			bus                 = c.bus;
-			lev                 = c.level;
-			lead                = (e == c0) || kc[e - 1].wheel != w;
+	return __hip_atomic_load (p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+/* One pass of a key message (src/tonegen.cpp:3270-3322): the entries base + lane of the
+ * key's keyContrib range [c0, c1), packed as wheel | bus << 16 | lead << 24 with the level;
+ * a message's first CTL_PG passes are loaded together, a message ahead of their use, so
+ * the contribution table's load latency hides behind the message before. */
+#define CTL_PG 4 /* passes per load group: keyContrib lists of up to 256 entries in one */
+
+struct CtlGroup {
+	uint32_t wb[CTL_PG]; /* the entry's wheel | bus << 16 (lanes past the range: entry 0's or the last's) */
+	uint32_t pw[CTL_PG]; /* the wheel of the entry before it */
+	float    lev[CTL_PG];
+};
+
+__device__ __forceinline__ CtlGroup ctl_group_load (const tbf_contrib* __restrict__ kc, uint32_t c0, uint32_t c1,
+                                                    uint32_t g0)
+{
+	/* every lane loads (an index clamped into the range, or entry 0), so the group's loads
+	 * issue back to back without exec-mask branches */
+	/* nothing here consumes the loaded data: the loads stay in flight until the group is
+	 * applied, after the wait for the bus levels of the message before */
+	CtlGroup g;
+#pragma unroll
+	for (int q = 0; q < CTL_PG; q++) {
+		const uint32_t    e  = g0 + (uint32_t)(q * NL) + threadIdx.x;
+		const uint32_t    ec = e < c1 ? e : (c1 > c0 ? c1 - 1 : 0u); /* contrib holds >= 1 entry */
+		const tbf_contrib c  = kc[ec];
+		g.wb[q]              = (uint32_t)c.wheel | ((uint32_t)c.bus << 16);
+		g.lev[q]             = c.level;
+		g.pw[q]              = kc[ec > c0 ? ec - 1 : ec].wheel;
+	}
+	return g;
+}
+
+/* A wheel group's part in a pass runs from its first lane to the next group's first lane
+ * (or the pass end); lane 0 continues a group begun in the previous pass.  The owner's
+ * reference count, flags and list position are read in one batch, then written; L (the
+ * list end) is wave-uniform in a scalar register.  b: the entry's bus level as loaded. */
+__device__ __forceinline__ void ctl_pass_apply (const CtlW& W, float* __restrict__ gbl, uint32_t wb, uint32_t pw, float lev,
+                                                float b, uint32_t e, uint32_t c0, uint32_t nval, bool on, uint32_t& L)
+{
+	const int      lane  = threadIdx.x;
+	const uint32_t w     = wb & 0xFFFFu, bus = wb >> 16;
+	const bool     valid = (uint32_t)lane < nval;
+	const bool     lead  = valid && (e == c0 || pw != w);
+	const uint64_t ld    = __ballot (lead);
+	const uint64_t after = (lane + 1 < NL) ? (ld >> (lane + 1)) : 0ull;
+	const uint32_t next  = after ? (uint32_t)(lane + 1 + __builtin_ctzll (after)) : nval;
+	const bool     owner = valid && (lead || lane == 0);
+	const int      part  = (int)(next - (uint32_t)lane);
+	const uint32_t wr    = valid ? w : 0u; /* the reads unconditional, from a valid index */
+	const int      r0    = W.ref[wr];
+	const uint32_t f0    = W.rf[wr];
+	const int      a0    = W.acl1[wr];
+	if (valid)
+		gbl[w * 27 + bus] = on ? b + lev : b - lev;
+	bool join = false;
+	if (owner) {
+		int      r1;
+		uint32_t f1;
+		if (on) {
+			r1 = r0 + part;
+			if (lead && r0 == 0) {
+				f1   = 0x0006;
+				join = a0 == 0;
+			} else
+				f1 = f0 | 0x0004;
+		} else {
+			r1 = r0 - part;
+			f1 = r1 == 0 ? 0x0005 : (f0 | 0x0004);
 		}
-		/* a wheel group's part in this pass: from its first lane to the next group's first
-		 * lane (or the pass end); lane 0 continues a group begun in the previous pass */
-		const uint64_t ld    = __ballot (lead);
-		const uint32_t nval  = c1 - base < (uint32_t)NL ? c1 - base : (uint32_t)NL;
-		const uint64_t after = (lane + 1 < NL) ? (ld >> (lane + 1)) : 0ull;
-		const uint32_t next  = after ? (uint32_t)(lane + 1 + __builtin_ctzll (after)) : nval;
-		const bool     owner = valid && (lead || lane == 0);
-		const int      part  = (int)(next - (uint32_t)lane);
-		bool           join  = false;
-		if (valid) {
-			float* bl = &W.bl[w * 27 + bus];
-			*bl       = on ? *bl + lev : *bl - lev;
+		W.ref[w] = r1;
+		W.rf[w]  = (uint8_t)f1;
+	}
+	const uint64_t jb = __ballot (join);
+	if (join) {
+		const uint32_t pos = L + (uint32_t)__builtin_popcountll (jb & lanemask_lt ());
+		W.list[pos]        = (uint16_t)w;
+		W.acl1[w]          = (int16_t)(pos + 1);
+	}
+	L += (uint32_t)__builtin_popcountll (jb);
+	lds_order ();
+}
+
+/* one key message whose first load group g is loaded: per group, the bus levels of all its
+ * entries are read together (each (wheel, bus) appears once in a key's list), then the
+ * passes applied in order */
+__device__ __forceinline__ void ctl_message (const CtlW& W, float* __restrict__ gbl, const tbf_contrib* __restrict__ kc,
+                                             uint32_t c0, uint32_t c1, bool on, CtlGroup g, uint32_t& L)
+{
+	for (uint32_t g0 = c0; g0 < c1; g0 += CTL_PG * NL) {
+		if (g0 != c0)
+			g = ctl_group_load (kc, c0, c1, g0);
+		float b[CTL_PG];
+#pragma unroll
+		for (int q = 0; q < CTL_PG; q++) /* every lane: lanes past the range read a valid entry's level */
+			b[q] = ctl_bl_load (gbl + (g.wb[q] & 0xFFFFu) * 27 + (g.wb[q] >> 16));
+#pragma unroll
+		for (int q = 0; q < CTL_PG; q++) {
+			const uint32_t base = g0 + (uint32_t)(q * NL);
+			if (base < c1)
+				ctl_pass_apply (W, gbl, g.wb[q], g.pw[q], g.lev[q], b[q], base + threadIdx.x, c0,
+				                c1 - base < (uint32_t)NL ? c1 - base : (uint32_t)NL, on, L);
 		}
-		if (owner) {
-			const int r0 = W.ref[w];
-			if (on) {
-				if (lead && r0 == 0) {
-					W.rf[w] = 0x0006;
-					join    = W.acl1[w] == 0;
-				} else {
-					W.rf[w] |= 0x0004;
-				}
-				W.ref[w] = r0 + part;
-			} else {
-				const int r1 = r0 - part;
-				W.ref[w]     = r1;
-				W.rf[w]      = r1 == 0 ? 0x0005 : (W.rf[w] | 0x0004);
-			}
-		}
-		const uint64_t jb = __ballot (join);
-		const uint32_t L  = __builtin_amdgcn_readfirstlane (sm.L);
-		if (join) {
-			const uint32_t pos = L + (uint32_t)__builtin_popcountll (jb & lanemask_lt ());
-			W.list[pos]        = (uint16_t)w;
-			W.acl1[w]          = (int16_t)(pos + 1);
-		}
-		wave_sync ();
-		if (lane == 0)
-			sm.L = L + (uint32_t)__builtin_popcountll (jb);
-		wave_sync ();
 	}
 }
 
 /* the active-list loop and the removals of one block (src/tonegen.cpp:3333-3594); writes
  * the program (header + one entry per active wheel) at out */
-__device__ void ctl_block (CtlLds& sm, const CtlW& W, uint32_t flags, uint32_t routing, uint32_t percSendBus,
-                           tbf_prog_entry* __restrict__ out)
+__device__ void ctl_block (CtlLds& sm, const CtlW& W, const float* __restrict__ gbl, uint32_t flags, uint32_t routing,
+                           uint32_t percSendBus, tbf_prog_entry* __restrict__ out, uint32_t& L CTL_PARAM)
 {
+	CTL_T (q0);
 	const int      lane      = threadIdx.x;
-	const uint32_t L0        = __builtin_amdgcn_readfirstlane (sm.L);
+	const uint32_t L0        = L;
 	const bool     dbChange  = (flags & 1) != 0;
 	const bool     recompute = (flags & 2) != 0;
 	uint32_t       nrem      = 0;
+	uint64_t       rb0       = 0; /* the first pass's removals */
+	uint32_t       on0       = 0; /* and its lanes' wheels */
 	for (uint32_t base = 0; base < L0; base += NL) {
 		const uint32_t i     = base + lane;
 		const bool     valid = i < L0;
@@ -194,8 +267,12 @@ __device__ void ctl_block (CtlLds& sm, const CtlW& W, uint32_t flags, uint32_t r
 				}
 				bool reroute = false;
 				if ((rf & 0x0004) || dbChange) {
-					const float* bl  = W.bl + on * 27;
-					float        sum = 0.0f;
+					const float* blp = gbl + on * 27;
+					float        bl[27];
+#pragma unroll
+					for (int d = 0; d < 27; d++)
+						bl[d] = ctl_bl_load (blp + d);
+					float sum = 0.0f;
 					for (int d = 0; d < 9; d++)
 						sum += bl[d] * sm.dbg[d];
 					sumUpper = sum;
@@ -210,7 +287,7 @@ __device__ void ctl_block (CtlLds& sm, const CtlW& W, uint32_t flags, uint32_t r
 					reroute  = true;
 				}
 				if (reroute || recompute) {
-					sumPercn = (routing & 0x0C) ? W.bl[on * 27 + percSendBus] : 0.0f;
+					sumPercn = (routing & 0x0C) ? ctl_bl_load (gbl + on * 27 + percSendBus) : 0.0f;
 					sumScanr = 0.0f;
 					sumSwell = sumPedal;
 					if (routing & 0x02)
@@ -240,38 +317,61 @@ __device__ void ctl_block (CtlLds& sm, const CtlW& W, uint32_t flags, uint32_t r
 			out[1 + i] = E;
 		}
 		const uint64_t rb = __ballot (rem);
-		if (rem)
-			W.removed[nrem + (uint32_t)__builtin_popcountll (rb & lanemask_lt ())] = (uint16_t)on;
+		if (base == 0) {
+			rb0 = rb;
+			on0 = on;
+		} else if (rem)
+			W.removed[nrem - (uint32_t)__builtin_popcountll (rb0) + (uint32_t)__builtin_popcountll (rb & lanemask_lt ())] =
+				(uint16_t)on;
 		nrem += (uint32_t)__builtin_popcountll (rb);
 	}
-	wave_sync ();
+	CTL_ACC (pt[0], q0);
+	CTL_T (q1);
 	if (lane == 0) {
 		tbf_prog_entry H = {};
 		H.wheel          = 0xFFFF;
 		H.pad            = L0;
 		out[0]           = H;
 	}
-	/* the removals (3576-3594): in order, each swapped with the list's last entry (lane 0;
-	 * a register-held list with ballot lookups measured slower) */
-	uint32_t L = L0;
-	if (lane == 0) {
-		for (uint32_t r = 0; r < nrem; r++) {
+	/* the removals (3576-3594): in order, each swapped with the list's last entry, by lane 0
+	 * (a register-held list with readlane / lane-select swaps measured slower, 500 k against
+	 * 330 k cycles a wave under dense events); the first pass's victims come from their
+	 * lanes' registers, later passes' (lists over 64 wheels) through LDS.  The list and
+	 * positions go through LDS in issue order: one read batch per removal. */
+	lds_order ();
+	const uint32_t n0 = (uint32_t)__builtin_popcountll (rb0);
+	uint32_t       Lr = L0;
+	for (uint64_t m = rb0; m; m &= m - 1) {
+		const uint32_t vic = (uint32_t)__builtin_amdgcn_readlane ((int)on0, __builtin_ctzll (m));
+		Lr--;
+		if (lane == 0) {
+			const int      act = W.acl1[vic] - 1;
+			const uint32_t mov = W.list[Lr];
+			W.acl1[vic]        = 0;
+			if (0 < Lr && mov != vic) {
+				W.list[act] = (uint16_t)mov;
+				W.acl1[mov] = (int16_t)(act + 1);
+			}
+		}
+		lds_order ();
+	}
+	if (lane == 0)
+		for (uint32_t r = 0; r < nrem - n0; r++) {
 			const uint32_t vic = W.removed[r];
 			const int      act = W.acl1[vic] - 1;
 			W.acl1[vic]        = 0;
-			L--;
-			if (0 < L) {
-				const uint32_t mov = W.list[L];
+			Lr--;
+			if (0 < Lr) {
+				const uint32_t mov = W.list[Lr];
 				if (mov != vic) {
-					W.list[act]  = (uint16_t)mov;
+					W.list[act] = (uint16_t)mov;
 					W.acl1[mov] = (int16_t)(act + 1);
 				}
 			}
 		}
-	}
-	if (lane == 0)
-		sm.L = L;
-	wave_sync ();
+	L = L0 - nrem;
+	lds_order ();
+	CTL_ACC (pt[1], q1);
 }
 
 /* One wave per instance with control deltas in the chunk.  The chunk's per-block inputs
@@ -289,6 +389,10 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_tgctl (
 	__shared__ CtlLds         sm;
 	extern __shared__ uint8_t wdyn[];
 	const int                 lane = threadIdx.x;
+#ifdef TBF_CTL_PROF
+	const uint64_t pr_rt0 = __builtin_amdgcn_s_memrealtime ();
+	CTL_T (pr_c0);
+#endif
 	const uint32_t            nw   = P.ctlNw;
 	const CtlW                W    = ctl_carve (wdyn, nw);
 	const uint32_t            inst = P.ctlInst[blockIdx.x];
@@ -316,9 +420,14 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_tgctl (
 			uint32_t*       dst = (uint32_t*)((tbf_seg_ctl*)P.ctl + idx);
 			const uint32_t  pp  = km ? P.progBase + (ki - n) * (uint32_t)TBF_PROG_SLOT : P.ctl[inst].prog_off;
 			const bool      pat = R.full == 0 || (R.flags & 0x10); /* 0x10: k_front's effect entry */
+			constexpr int NWD = (int)(sizeof (tbf_seg_ctl) / 4);
+			uint32_t      wd[NWD]; /* all loads before the stores (src and dst share the pool) */
 #pragma unroll
-			for (int k = 0; k < (int)(sizeof (tbf_seg_ctl) / 4); k++) {
-				uint32_t v = src[k];
+			for (int k = 0; k < NWD; k++)
+				wd[k] = src[k];
+#pragma unroll
+			for (int k = 0; k < NWD; k++) {
+				uint32_t v = wd[k];
 				if (pat) {
 					if (k == (int)(offsetof (tbf_seg_ctl, prog_off) / 4))
 						v = pp;
@@ -333,6 +442,10 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_tgctl (
 			}
 		}
 	}
+#ifdef TBF_CTL_PROF
+	uint64_t pr_stage = 0, pr_msg = 0, pr_blk = 0, pr_end = 0, pt[4] = {0, 0, 0, 0};
+	CTL_T (pr_k0);
+#endif
 	const uint32_t poff = P.progBase + (idx - n) * (uint32_t)TBF_PROG_SLOT; /* a stepped delta's program */
 	const bool     stepped = isNew && (R.flags & 0x80);
 	const uint64_t todo0   = __ballot (stepped);
@@ -348,8 +461,6 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_tgctl (
 	const uint32_t M  = (uint32_t)__shfl ((int)mpos, NL - 1);
 	mpos -= nm;
 	const bool     pre = M <= CTL_MSGCAP;
-	for (size_t i = lane; i < (size_t)nw * 27; i += NL)
-		W.bl[i] = (&G->busLevel[0][0])[i];
 	for (size_t i = lane; i < (size_t)nw * 6; i += NL)
 		W.sums[i] = (&G->sums[0][0])[i];
 	for (uint32_t w = lane; w < nw; w += NL) {
@@ -358,8 +469,7 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_tgctl (
 		W.acl1[w] = G->aclPos1[w];
 		W.rf[w]   = G->rflags[w];
 	}
-	if (lane == 0)
-		sm.L = G->listEnd;
+	uint32_t L = __builtin_amdgcn_readfirstlane (G->listEnd); /* activeOscLEnd, wave-uniform */
 	if (lane < 27)
 		sm.dbg[lane] = G->gain[lane];
 	if (pre)
@@ -374,6 +484,13 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_tgctl (
 		}
 		wave_sync ();
 	}
+	/* the first pass of the next message (in launch order: blocks ascending, each block's
+	 * messages at its prefix offset), loaded one message ahead */
+	float* const gbl = &G->busLevel[0][0];
+	CtlGroup     pf  = {};
+	if (pre && M > 0)
+		pf = ctl_group_load (P.contrib, sm.mc0[0], sm.mc1[0], sm.mc0[0]);
+	CTL_ACC (pr_stage, pr_k0);
 	int64_t  last = -1; /* prog_off of the last program written */
 	uint64_t todo = todo0;
 	while (todo) {
@@ -389,30 +506,37 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_tgctl (
 			}
 			wave_sync ();
 		}
+		CTL_T (pr_m0);
 		const uint32_t bm = (uint32_t)__builtin_amdgcn_readlane ((int)nm, b);
 		const uint32_t bp = (uint32_t)__builtin_amdgcn_readlane ((int)mpos, b);
 		const uint32_t bo = (uint32_t)__builtin_amdgcn_readlane ((int)R.msgOff, b);
 		for (uint32_t m = 0; m < bm; m++) {
-			uint32_t msg, c0, c1;
 			if (pre) {
-				msg = sm.msg[bp + m];
-				c0  = sm.mc0[bp + m];
-				c1  = sm.mc1[bp + m];
+				const uint32_t j   = bp + m;
+				const uint32_t msg = sm.msg[j], c0 = sm.mc0[j], c1 = sm.mc1[j];
+				const CtlGroup cur = pf;
+				if (j + 1 < M)
+					pf = ctl_group_load (P.contrib, sm.mc0[j + 1], sm.mc1[j + 1], sm.mc0[j + 1]);
+				/* keys outside [0, 384) have the empty range */
+				ctl_message (W, gbl, P.contrib, c0, c1, (msg & 0xf000u) == 0x1000u, cur, L);
 			} else {
-				msg                = P.msgs[bo + m];
-				const uint32_t kn0 = msg & 0x0fffu;
-				c0                 = kn0 < 384 ? coff[kn0] : 0u;
-				c1                 = kn0 < 384 ? coff[kn0 + 1] : 0u;
+				const uint32_t msg = P.msgs[bo + m], kn0 = msg & 0x0fffu;
+				if (kn0 >= 384)
+					continue;
+				const uint32_t c0 = coff[kn0], c1 = coff[kn0 + 1];
+				ctl_message (W, gbl, P.contrib, c0, c1, (msg & 0xf000u) == 0x1000u, ctl_group_load (P.contrib, c0, c1, c0),
+				             L);
 			}
-			if ((msg & 0x0fffu) >= 384)
-				continue;
-			ctl_message (sm, W, P.contrib, c0, c1, (msg & 0xf000u) == 0x1000u);
 		}
+		CTL_ACC (pr_msg, pr_m0);
+		CTL_T (pr_b0);
 		const uint32_t off = (uint32_t)__builtin_amdgcn_readlane ((int)poff, b);
-		ctl_block (sm, W, flags, (uint32_t)__builtin_amdgcn_readlane ((int)R.oldRouting, b),
-		           (uint32_t)__builtin_amdgcn_readlane ((int)R.percSendBus, b), (tbf_prog_entry*)P.prog + off);
+		ctl_block (sm, W, gbl, flags, (uint32_t)__builtin_amdgcn_readlane ((int)R.oldRouting, b),
+		           (uint32_t)__builtin_amdgcn_readlane ((int)R.percSendBus, b), (tbf_prog_entry*)P.prog + off, L CTL_ARG);
 		last = off;
+		CTL_ACC (pr_blk, pr_b0);
 	}
+	CTL_T (pr_e0);
 	/* the instance's last program becomes its persistent one, in the slot after the current
 	 * persistent entry's (mod TBF_PROG_PSLOTS; the host advances its entry the same way
 	 * after the chunk) */
@@ -428,8 +552,6 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_tgctl (
 			d[k] = src[k];
 	}
 	wave_sync ();
-	for (size_t i = lane; i < (size_t)nw * 27; i += NL)
-		(&G->busLevel[0][0])[i] = W.bl[i];
 	for (size_t i = lane; i < (size_t)nw * 6; i += NL)
 		(&G->sums[0][0])[i] = W.sums[i];
 	for (uint32_t w = lane; w < nw; w += NL) {
@@ -439,9 +561,16 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_tgctl (
 		G->rflags[w]   = W.rf[w];
 	}
 	if (lane == 0)
-		G->listEnd = sm.L;
+		G->listEnd = L;
 	if (lane < 27)
 		G->gain[lane] = sm.dbg[lane];
+#ifdef TBF_CTL_PROF
+	CTL_ACC (pr_end, pr_e0);
+	if (lane == 0 && (blockIdx.x & 255) == 0)
+		printf ("ctlprof wg %u blocks %d L %u pre %lu stage %lu msg %lu blk %lu (pass %lu rem %lu) end %lu total %lu rt0 %lu rt1 %lu\n",
+		        blockIdx.x, __builtin_popcountll (todo0), L, pr_k0 - pr_c0, pr_stage, pr_msg, pr_blk, pt[0], pt[1], pr_end,
+		        __builtin_amdgcn_s_memtime () - pr_c0, pr_rt0, __builtin_amdgcn_s_memrealtime ());
+#endif
 }
 
 /* The device front end of a chunk whose events are notes, drawbar moves and the vibrato
@@ -461,27 +590,46 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_front (
 {
 	__shared__ uint32_t keys[12];
 	__shared__ float    gl[27]; /* drawBarGain of the buses changed since the last step */
+	/* the instance's events (their first FR_CAP), its key-compression table and the effect
+	 * values, read lane-parallel up front: lane 0's walk then waits on LDS, not on one
+	 * dependent global load per event */
+	__shared__ uint32_t fevs[FR_CAP];
+	__shared__ float    fvals[FR_CAP];
+	__shared__ float    kcs[128];
 	const int             lane = threadIdx.x;
 	const uint32_t        inst = blockIdx.x;
 	const uint32_t        n = P.nInst, nb = P.nBlocks;
 	const tbf_front_state& F   = P.front[inst];
+	const uint32_t        e0 = P.fevOff[inst], eEnd = P.fevOff[inst + 1];
 	if (lane < 12)
 		keys[lane] = F.keys[lane];
+	{
+		const float* kt = P.keyComp + (size_t)P.cst[inst].tpl * 128;
+		kcs[lane]       = kt[lane];
+		kcs[lane + NL]  = kt[lane + NL];
+		const uint32_t ne = eEnd - e0 < FR_CAP ? eEnd - e0 : FR_CAP;
+		for (uint32_t i = lane; i < ne; i += NL) {
+			const uint32_t v = P.fev[e0 + i];
+			fevs[i]          = v;
+			fvals[i]         = (v & TBF_FEV_PARAM) ? P.fevVal[e0 + i] : 0.f;
+		}
+	}
 	wave_sync ();
 	if (lane != 0)
 		return;
+	auto fev = [&] (uint32_t e) { return e - e0 < FR_CAP ? fevs[e - e0] : P.fev[e]; };
+	auto fval = [&] (uint32_t e) { return e - e0 < FR_CAP ? fvals[e - e0] : P.fevVal[e]; };
 	uint32_t*      ctlIdx = (uint32_t*)P.ctlIdx;
 	uint16_t*      msgs   = (uint16_t*)P.msgs;
 	tbf_tgc_rec*   rec    = (tbf_tgc_rec*)P.rec;
 	float*         gains  = (float*)P.gains;
-	const float*   kct    = P.keyComp + (size_t)P.cst[inst].tpl * 128;
 	int            kdc = F.keyDown, ukc = F.upperDown;
 	bool           pending = F.pending != 0;
 	uint32_t       r = F.routing, oldR = F.routing, psb = F.percSendBus;
 	int            pe = F.percEnabled, restore = F.percTrigRestore;
 	const int      ptb = F.percTriggerBus;
 	uint32_t       gm = 0, dbc = 0, go = F.gainOff;
-	uint32_t       e = P.fevOff[inst], eEnd = P.fevOff[inst + 1];
+	uint32_t       e = e0;
 	uint32_t       mo = 2 * e; /* the instance's message slots: at most two per event */
 	uint32_t       idx = inst, k = 0;
 	/* the effect setters' fields: the instance's entry at the chunk start, changed in
@@ -496,15 +644,15 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_front (
 	auto level = [] (uint32_t s) { return (float)((double)(float)s / 8.0); };
 	for (uint32_t b = 0; b < nb; b++) {
 		const uint32_t m0 = mo;
-		for (; e < eEnd && (P.fev[e] >> 16) == b; e++) {
-			const uint32_t v = P.fev[e];
+		for (; e < eEnd && (fev (e) >> 16) == b; e++) {
+			const uint32_t v = fev (e);
 			if (v & TBF_FEV_PARAM) {
 				const uint32_t op = (v >> 12) & 7u, bus = v & 31u, set = (v >> 5) & 15u;
 				const bool     fl = (v >> 9) & 1u;
 				if (op == TBF_FEV_EFFECT) {
 					/* the CLAP setParam effect setters (src/clap.cpp:162-207), as tbf_set_param and
 					 * stepControl apply them to the instance's control entry */
-					const float x = P.fevVal[e];
+					const float x = fval (e);
 					fx            = true;
 					switch (bus) {
 						case TBF_FX_ROTOR: revPend = (int)x; break; /* used by this block only */
@@ -625,7 +773,7 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_front (
 			R.nMsg          = nm;
 			R.gainOff       = ng ? go : 0;
 			R.full          = 0;
-			R.keyCompTarget = kct[kdc < 0 ? 0 : (kdc > 127 ? 127 : kdc)];
+			R.keyCompTarget = kcs[kdc < 0 ? 0 : (kdc > 127 ? 127 : kdc)];
 			R.flags         = (uint8_t)((tgs ? 0x80u | dbc | (rcp ? 2u : 0u) | (ng ? 4u : 0u) : 0u) | (ukc == 0 ? 8u : 0u));
 			R.oldRouting    = (uint8_t)r;
 			R.percSendBus   = (uint8_t)psb;

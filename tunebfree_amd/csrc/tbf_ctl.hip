@@ -53,6 +53,9 @@ struct CtlW {
 	uint8_t*  rf;      /* [nw] */
 };
 #define CTL_MSGCAP 256 /* a launch's messages prefetched into LDS (more: read per block) */
+#ifndef CTL_ABL
+#define CTL_ABL 0 /* timing experiments (wrong output): 1 no bus-level loads or stores in the messages, 2 none in ctl_block */
+#endif
 #define FR_CAP 1024    /* k_front: an instance's events staged in LDS (more: read from HBM) */
 
 struct CtlLds {
@@ -115,6 +118,14 @@ __device__ __forceinline__ float ctl_bl_load (const float* p)
 	return __hip_atomic_load (p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+/* 16 B of a wheel's bus-level row the same way: a buffer load with the sc1 policy (bit 4 of
+ * the cache-policy operand on gfx950), through the instance's rows as a buffer resource */
+typedef unsigned int v4u __attribute__ ((ext_vector_type (4)));
+__device__ __forceinline__ v4u ctl_row_load (__amdgpu_buffer_rsrc_t r, uint32_t w, int q)
+{
+	return __builtin_amdgcn_raw_buffer_load_b128 (r, (int)(w * TBF_BL_ROW * 4u + 16u * (uint32_t)q), 0, 16);
+}
+
 /* One pass of a key message (src/tonegen.cpp:3270-3322): the entries base + lane of the
  * key's keyContrib range [c0, c1), packed as wheel | bus << 16 | lead << 24 with the level;
  * a message's first CTL_PG passes are loaded together, a message ahead of their use, so
@@ -167,8 +178,10 @@ __device__ __forceinline__ void ctl_pass_apply (const CtlW& W, float* __restrict
 	const int      r0    = W.ref[wr];
 	const uint32_t f0    = W.rf[wr];
 	const int      a0    = W.acl1[wr];
+#if CTL_ABL != 1
 	if (valid)
-		gbl[w * 27 + bus] = on ? b + lev : b - lev;
+		gbl[w * TBF_BL_ROW + bus] = on ? b + lev : b - lev;
+#endif
 	bool join = false;
 	if (owner) {
 		int      r1;
@@ -209,7 +222,11 @@ __device__ __forceinline__ void ctl_message (const CtlW& W, float* __restrict__ 
 		float b[CTL_PG];
 #pragma unroll
 		for (int q = 0; q < CTL_PG; q++) /* every lane: lanes past the range read a valid entry's level */
-			b[q] = ctl_bl_load (gbl + (g.wb[q] & 0xFFFFu) * 27 + (g.wb[q] >> 16));
+#if CTL_ABL == 1
+			b[q] = 0.f;
+#else
+			b[q] = ctl_bl_load (gbl + (g.wb[q] & 0xFFFFu) * TBF_BL_ROW + (g.wb[q] >> 16));
+#endif
 #pragma unroll
 		for (int q = 0; q < CTL_PG; q++) {
 			const uint32_t base = g0 + (uint32_t)(q * NL);
@@ -228,6 +245,9 @@ __device__ void ctl_block (CtlLds& sm, const CtlW& W, const float* __restrict__ 
 	CTL_T (q0);
 	const int      lane      = threadIdx.x;
 	const uint32_t L0        = L;
+	/* the instance's bus-level rows as a buffer resource (dword 3: gfx950's raw 32-bit format) */
+	const __amdgpu_buffer_rsrc_t blr =
+		__builtin_amdgcn_make_buffer_rsrc ((void*)gbl, (short)0, (int)((TBF_NW + 1) * TBF_BL_ROW * 4), 0x00020000);
 	const bool     dbChange  = (flags & 1) != 0;
 	const bool     recompute = (flags & 2) != 0;
 	uint32_t       nrem      = 0;
@@ -267,11 +287,19 @@ __device__ void ctl_block (CtlLds& sm, const CtlW& W, const float* __restrict__ 
 				}
 				bool reroute = false;
 				if ((rf & 0x0004) || dbChange) {
-					const float* blp = gbl + on * 27;
-					float        bl[27];
+					float bl[TBF_BL_ROW];
 #pragma unroll
-					for (int d = 0; d < 27; d++)
-						bl[d] = ctl_bl_load (blp + d);
+					for (int q = 0; q < TBF_BL_ROW / 4; q++) {
+#if CTL_ABL == 2
+						const v4u v = {q, q, q, q};
+#else
+						const v4u v = ctl_row_load (blr, on, q);
+#endif
+						bl[4 * q]     = __uint_as_float (v.x);
+						bl[4 * q + 1] = __uint_as_float (v.y);
+						bl[4 * q + 2] = __uint_as_float (v.z);
+						bl[4 * q + 3] = __uint_as_float (v.w);
+					}
 					float sum = 0.0f;
 					for (int d = 0; d < 9; d++)
 						sum += bl[d] * sm.dbg[d];
@@ -287,7 +315,7 @@ __device__ void ctl_block (CtlLds& sm, const CtlW& W, const float* __restrict__ 
 					reroute  = true;
 				}
 				if (reroute || recompute) {
-					sumPercn = (routing & 0x0C) ? ctl_bl_load (gbl + on * 27 + percSendBus) : 0.0f;
+					sumPercn = (routing & 0x0C) ? ctl_bl_load (gbl + on * TBF_BL_ROW + percSendBus) : 0.0f;
 					sumScanr = 0.0f;
 					sumSwell = sumPedal;
 					if (routing & 0x02)

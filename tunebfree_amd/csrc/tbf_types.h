@@ -121,11 +121,13 @@ typedef struct tbf_le {
 	float   fc;
 } tbf_le;
 
+#define TBF_BL_ROW 28 /* floats per wheel row of tbf_tgc_state.busLevel */
+
 /* per instance device control state (the runtime fields of struct b_tonegen that the
  * per-wheel control touches); aclPos1 = aclPos + 1 so that zeroed memory is the initial
  * state (no wheel in the list) */
-typedef struct tbf_tgc_state {
-	float    busLevel[TBF_NW + 1][27];
+typedef struct alignas (16) tbf_tgc_state {
+	float    busLevel[TBF_NW + 1][TBF_BL_ROW]; /* 27 buses, rows padded to 16 B (k_tgctl's 16-B row loads) */
 	float    sums[TBF_NW + 1][6]; /* sumUpper, sumLower, sumPedal, sumPercn, sumSwell, sumScanr */
 	int32_t  refCount[TBF_NW + 1];
 	uint16_t list[TBF_NW + 1];    /* activeOscList */

@@ -1738,6 +1738,85 @@ def test_gpu_device_control_programs(oracle, tunings, scen):
     eng.close()
 
 
+def test_gpu_device_control_large_clusters(oracle):
+    """k_tgctl's paths past its fast ones (tbf_ctl.hip): 12-key clusters released and
+    pressed on every block put 24 messages in a block and ~1500 in a 64-block launch (more
+    than the CTL_MSGCAP prefetched into LDS: read per block), a key's passes over its
+    keyContrib list in groups, active lists over 64 wheels (a second pass of the active-list
+    loop, its removals through LDS) and more than 64 wheels leaving at once (the serial
+    removal loop); lighter instances in the same launch keep the fast paths.  Device front
+    end, host front end (TBF_DEVICE_FRONT=0) and host control (TBF_HOST_CONTROL=1, no
+    k_tgctl) bit-identical, and the oracle for a sample."""
+    import os
+    import torch
+    import tunebfree_amd as T
+    from orc_bind import Template
+    n, nb = 48, 128
+    seeds = [8100 + i for i in range(n)]
+    rows, oscen = [], [[] for _ in range(n)]
+
+    def ev(b, i, kind, a, v):
+        rows.append((b, i, 0 if kind == "note" else 1, a, float(v)))
+        oscen[i].append((b, kind, a, v))
+
+    def cluster(i, t):
+        base = 36 + (3 * i + 5 * t) % 40
+        return [base + 2 * k for k in range(12)]
+
+    for i in range(n):
+        for (k, a, v) in S.jazz1_params():
+            ev(0, i, k, a, v)
+        heavy = i % 3 != 2
+        cur = cluster(i, 0) if heavy else S.chord_for(i)
+        for k in cur:
+            ev(0, i, "note", k, 1)
+        for b in range(1, nb):
+            if heavy:
+                if b % 16 == 15:  # everything released: over 64 wheels leave in one block
+                    for k in cur:
+                        ev(b, i, "note", k, 0)
+                    cur = []
+                    continue
+                nxt = cluster(i, b)
+                for k in cur:
+                    ev(b, i, "note", k, 0)
+                for k in nxt:
+                    ev(b, i, "note", k, 1)
+                cur = nxt
+            else:
+                ev(b, i, "note", 60 + (i + b - 1) % 12, 0)
+                ev(b, i, "note", 60 + (i + b) % 12, 1)
+    rows.sort(key=lambda r: r[0])
+    outs = []
+    for env in ({}, {"TBF_DEVICE_FRONT": "0"}, {"TBF_HOST_CONTROL": "1"}):
+        os.environ.update(env)
+        try:
+            eng = T.Engine(sample_rate=48000.0, device=0)
+        finally:
+            for k in env:
+                os.environ.pop(k, None)
+        tid = eng.template(seed=7)
+        eng.add_instances([tid] * n, seeds)
+        evs = eng.events(rows)
+        L = torch.zeros((n, nb * 128), dtype=torch.float32, device="cuda")
+        R = torch.zeros_like(L)
+        eng.render_events_device(nb, evs, L.data_ptr(), R.data_ptr(), nb * 128)
+        eng.synchronize()
+        outs.append((L.cpu().numpy(), R.cpu().numpy()))
+        eng.close()
+        del L, R
+    for o in outs[1:]:
+        assert np.array_equal(outs[0][0].view(np.uint32), o[0].view(np.uint32))
+        assert np.array_equal(outs[0][1].view(np.uint32), o[1].view(np.uint32))
+    sample = [0, 1, 2, 29]
+    tpl = Template(oracle, seed=7)
+    oL, oR, *_ = oracle_run(oracle, tpl, [seeds[i] for i in sample], [sorted(oscen[i], key=lambda r: r[0]) for i in sample], nb)
+    eL, xL = compare(outs[0][0][sample], oL)
+    eR, xR = compare(outs[0][1][sample], oR)
+    print(f"large clusters vs oracle: max|err| L={eL:.3g} R={eR:.3g} bit-exact {xL:.6f} {xR:.6f}")
+    assert max(eL, eR) <= TOL
+
+
 def test_gpu_reroute_without_key_events(oracle):
     """Drawbar / vibrato-routing / percussion changes while keys are held, with no key
     event in the block (scenarios.reroute_scenario): the new sums must take effect from

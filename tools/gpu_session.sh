@@ -16,6 +16,10 @@
 #   bench   the default bench without the CPU leg
 #   ab:V=X  the default bench with environment switch V=X
 #   prof    k_rv_core_lds / k_whirl / k_tonegen phase clocks (tools/build_prof.sh variants)
+#   ctlprof k_tgctl phase clocks under dense / every-8 events, with the bus-level traffic
+#           ablated (tools/build_prof.sh variants; the ablations' output is wrong)
+#   ctlab:LIB  same-box A/B of dense / every-8 events: the in-tree library against LIB,
+#           alternating, two runs each (LIB: a build of the round's start, for example)
 #   calib   PMC byte counters on known aligned / misaligned streams
 set -u
 TAG=${1:-dev}; shift || true
@@ -92,6 +96,16 @@ for s in $STEPS; do
 		run rvl_prof 200 env TBF_LIB=tunebfree_amd/_prof/libtbf_rvlprof.so python3 tools/rvl_prof.py
 		run whirl_prof 200 env TBF_LIB=tunebfree_amd/_prof/libtbf_whprof.so python3 tools/whirl_prof.py
 		run tg_prof 200 env TBF_LIB=tunebfree_amd/_prof/libtbf_tgprof.so python3 tools/phase_prof.py --chain 1 ;;
+	ctlprof) # printed by a few workgroups per launch: cycles of the stage, message, active-list and removal phases
+		for v in ctlprof ctlabl1 ctlabl2; do
+			run "$v" 200 env TBF_LIB=tunebfree_amd/_prof/libtbf_$v.so python3 -u tools/dense_events.py --modes dense,every8 --steps 2 --warmup 1
+		done ;;
+	ctlab:*)
+		lib=${s#ctlab:}
+		for r in 1 2; do
+			run "ctlab_base_$r" 200 env TBF_LIB=$lib python3 -u tools/dense_events.py --modes every8,dense --steps 8 --warmup 3
+			run "ctlab_new_$r" 200 python3 -u tools/dense_events.py --modes every8,dense --steps 8 --warmup 3
+		done ;;
 	calib) # FETCH_SIZE / WRITE_SIZE of known streams: aligned and 64 B misaligned 8-B/lane reads and writes
 		run calib_f 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/calib_f" -o run --output-format csv -- python3 tools/calib_pmc.py 2 0,2,1,3
 		run calib_w 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/calib_w" -o run --output-format csv -- python3 tools/calib_pmc.py 2 0,2,1,3 ;;

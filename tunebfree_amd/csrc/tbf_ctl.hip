@@ -291,7 +291,7 @@ __device__ void ctl_block (CtlLds& sm, const CtlW& W, const float* __restrict__ 
 #pragma unroll
 					for (int q = 0; q < TBF_BL_ROW / 4; q++) {
 #if CTL_ABL == 2
-						const v4u v = {q, q, q, q};
+						const v4u v = {(unsigned)q, (unsigned)q, (unsigned)q, (unsigned)q};
 #else
 						const v4u v = ctl_row_load (blr, on, q);
 #endif

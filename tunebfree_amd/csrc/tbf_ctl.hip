@@ -14,13 +14,15 @@
  * each stepped block a tbf_tgc_rec; this kernel owns the per-wheel state
  * (tbf_tgc_state, HBM) and writes the block's program where k_tonegen reads it.
  *
- * One wave per instance with stepped blocks in the chunk, blocks in order, the instance's
- * bus levels and routed sums staged in LDS for the launch (their read-modify-writes were
- * global round trips, one per message and list pass):
+ * One wave per instance with stepped blocks in the chunk, blocks in order; the instance's
+ * routed sums, reference counts, list and flags staged in LDS for the launch, its bus
+ * levels read and written in place in HBM (at 184 wheels they would take 20 KB of LDS a
+ * workgroup: four rounds of workgroups at 4096 instances instead of one):
  *   messages   in queue order; the key's keyContrib list (sorted by wheel, then bus) is
- *              spread over the lanes.  Each (wheel, bus) appears once per key, so the
- *              bus-level adds are lane-parallel and keep the reference's per-(wheel, bus)
- *              order; a wheel's reference-count / flag update is made once per wheel group
+ *              spread over the lanes, four passes of 64 entries loaded together a message
+ *              ahead.  Each (wheel, bus) appears once per key, so the bus-level adds are
+ *              lane-parallel (one read batch per group) and keep the reference's
+ *              per-(wheel, bus) order; a wheel's reference-count / flag update is made once per wheel group
  *              by its first lane, which gives what the reference's per-element sequence
  *              gives (first element sees the old count, the rest see it > 0); newly
  *              activated wheels join the list in element order (ballot ranks).

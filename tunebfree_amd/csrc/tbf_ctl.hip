@@ -58,7 +58,7 @@ struct CtlW {
 #ifndef CTL_ABL
 #define CTL_ABL 0 /* timing experiments (wrong output): 1 no bus-level loads or stores in the messages, 2 none in ctl_block */
 #endif
-#define FR_CAP 1024    /* k_front: an instance's events staged in LDS (more: read from HBM) */
+#define FR_CAP 8192    /* k_front: a wave's (64 instances') events staged in LDS (more: read from HBM) */
 
 struct CtlLds {
 	float    dbg[27];
@@ -606,8 +606,10 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_tgctl (
 /* The device front end of a chunk whose events are notes, drawbar moves and the vibrato
  * and percussion switches (src/tonegen.cpp:3096-3166 oscKeyOn / oscKeyOff, 2738-2756
  * setDrawBar, 1678-1765 setPercEnabled / setPercFirst, src/vibrato.cpp routing; the
- * per-block step of TgControl::stepFront / mixCtl): one wave per instance, lane 0 walking
- * the instance's events in order from its front state at the chunk start.  A key event
+ * per-block step of TgControl::stepFront / mixCtl): one lane per instance, 64 instances a
+ * wave, each lane walking its instance's events in order from its front state at the chunk
+ * start (one wave per instance with lane 0 walking, before: 4096 single-wave workgroups
+ * that waited for free wave slots behind the render stages).  A key event
  * updates activeKeys and the key counts and queues its messages; a drawbar or percussion
  * event updates the drawbar gains (the changed buses' (bus, gain) pairs go out with the
  * block's record) and the drawbar-change flag; a switch updates the routing word.  A block
@@ -618,37 +620,42 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_tgctl (
  * messages, the gain pairs and the chunk's index table. */
 __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_front (const tbf_launch P)
 {
-	__shared__ uint32_t keys[12];
-	__shared__ float    gl[27]; /* drawBarGain of the buses changed since the last step */
-	/* the instance's events (their first FR_CAP), its key-compression table and the effect
-	 * values, read lane-parallel up front: lane 0's walk then waits on LDS, not on one
-	 * dependent global load per event */
+	/* per lane (instance) i: activeKeys keys[w][i], the drawBarGain of the buses changed
+	 * since the last step gl[bus][i]; the wave's events (instances i0 .. i0 + 63 are
+	 * contiguous in fev, their first FR_CAP staged) and the first instance's template's
+	 * key-compression table, read lane-parallel up front so the walks wait on LDS, not on
+	 * one dependent global load per event */
+	__shared__ uint32_t keys[12][NL];
+	__shared__ float    gl[27][NL];
 	__shared__ uint32_t fevs[FR_CAP];
-	__shared__ float    fvals[FR_CAP];
 	__shared__ float    kcs[128];
 	const int             lane = threadIdx.x;
-	const uint32_t        inst = blockIdx.x;
 	const uint32_t        n = P.nInst, nb = P.nBlocks;
-	const tbf_front_state& F   = P.front[inst];
-	const uint32_t        e0 = P.fevOff[inst], eEnd = P.fevOff[inst + 1];
-	if (lane < 12)
-		keys[lane] = F.keys[lane];
+	const uint32_t        i0 = blockIdx.x * NL, iN = i0 + NL < n ? i0 + NL : n;
+	const uint32_t        inst = i0 + (uint32_t)lane;
+	const bool            act  = inst < n;
+	const tbf_front_state& F   = P.front[act ? inst : iN - 1];
+	const uint32_t        w0 = P.fevOff[i0], w1 = P.fevOff[iN];
+	const uint32_t        e0 = P.fevOff[act ? inst : iN - 1], eEnd = act ? P.fevOff[inst + 1] : e0;
+	const uint32_t        tpl0 = P.cst[i0].tpl;
+#pragma unroll
+	for (int w = 0; w < 12; w++)
+		keys[w][lane] = F.keys[w];
 	{
-		const float* kt = P.keyComp + (size_t)P.cst[inst].tpl * 128;
+		const float* kt = P.keyComp + (size_t)tpl0 * 128;
 		kcs[lane]       = kt[lane];
 		kcs[lane + NL]  = kt[lane + NL];
-		const uint32_t ne = eEnd - e0 < FR_CAP ? eEnd - e0 : FR_CAP;
-		for (uint32_t i = lane; i < ne; i += NL) {
-			const uint32_t v = P.fev[e0 + i];
-			fevs[i]          = v;
-			fvals[i]         = (v & TBF_FEV_PARAM) ? P.fevVal[e0 + i] : 0.f;
-		}
+		const uint32_t ne = w1 - w0 < FR_CAP ? w1 - w0 : FR_CAP;
+		for (uint32_t i = lane; i < ne; i += NL)
+			fevs[i] = P.fev[w0 + i];
 	}
 	wave_sync ();
-	if (lane != 0)
+	if (!act)
 		return;
-	auto fev = [&] (uint32_t e) { return e - e0 < FR_CAP ? fevs[e - e0] : P.fev[e]; };
-	auto fval = [&] (uint32_t e) { return e - e0 < FR_CAP ? fvals[e - e0] : P.fevVal[e]; };
+	auto fev = [&] (uint32_t e) { return e - w0 < FR_CAP ? fevs[e - w0] : P.fev[e]; };
+	const uint32_t tpl = P.cst[inst].tpl;
+	const float*   kct = P.keyComp + (size_t)tpl * 128;
+	auto kcomp = [&] (int i) { return tpl == tpl0 ? kcs[i] : kct[i]; };
 	uint32_t*      ctlIdx = (uint32_t*)P.ctlIdx;
 	uint16_t*      msgs   = (uint16_t*)P.msgs;
 	tbf_tgc_rec*   rec    = (tbf_tgc_rec*)P.rec;
@@ -682,7 +689,7 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_front (
 				if (op == TBF_FEV_EFFECT) {
 					/* the CLAP setParam effect setters (src/clap.cpp:162-207), as tbf_set_param and
 					 * stepControl apply them to the instance's control entry */
-					const float x = fval (e);
+					const float x = P.fevVal[e];
 					fx            = true;
 					switch (bus) {
 						case TBF_FX_ROTOR: revPend = (int)x; break; /* used by this block only */
@@ -752,7 +759,7 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_front (
 						if (pe)
 							continue;
 					}
-					gl[bus] = level (set);
+					gl[bus][lane] = level (set);
 					gm |= 1u << bus;
 				} else if (op == TBF_FEV_VIB_UPPER) {
 					r = fl ? (r | 0x02u) : (r & ~0x02u);
@@ -761,7 +768,7 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_front (
 				} else if (op == TBF_FEV_PERC) {
 					r = fl ? (r | 0x0Cu) : (r & ~0x0Cu);
 					if (-1 < ptb) {
-						gl[ptb] = fl ? 0.0f : level ((uint32_t)restore);
+						gl[ptb][lane] = fl ? 0.0f : level ((uint32_t)restore);
 						gm |= 1u << ptb;
 						dbc = 1;
 					}
@@ -776,15 +783,15 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_front (
 			if (key >= 384) /* the host packs keys outside [0, MAX_KEYS) as 0x0fff: ignored (3098) */
 				continue;
 			const uint32_t w = key >> 5, bit = 1u << (key & 31);
-			if (keys[w] & bit) { /* keyOff, or keyOn's release of a held key first */
-				keys[w] &= ~bit;
+			if (keys[w][lane] & bit) { /* keyOff, or keyOn's release of a held key first */
+				keys[w][lane] &= ~bit;
 				if (key < 128)
 					ukc--;
 				kdc--;
 				msgs[mo++] = (uint16_t)key;
 			}
 			if (on) {
-				keys[w] |= bit;
+				keys[w][lane] |= bit;
 				if (key < 128)
 					ukc++;
 				kdc++;
@@ -803,7 +810,7 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_front (
 			R.nMsg          = nm;
 			R.gainOff       = ng ? go : 0;
 			R.full          = 0;
-			R.keyCompTarget = kcs[kdc < 0 ? 0 : (kdc > 127 ? 127 : kdc)];
+			R.keyCompTarget = kcomp (kdc < 0 ? 0 : (kdc > 127 ? 127 : kdc));
 			R.flags         = (uint8_t)((tgs ? 0x80u | dbc | (rcp ? 2u : 0u) | (ng ? 4u : 0u) : 0u) | (ukc == 0 ? 8u : 0u));
 			R.oldRouting    = (uint8_t)r;
 			R.percSendBus   = (uint8_t)psb;
@@ -811,7 +818,7 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_front (
 			for (uint32_t m = gm; m; m &= m - 1) { /* the changed buses in bus order */
 				const uint32_t bus = (uint32_t)__builtin_ctz (m);
 				gains[go++]        = __uint_as_float (bus);
-				gains[go++]        = gl[bus];
+				gains[go++]        = gl[bus][lane];
 			}
 			if (fxE) {
 				/* a full entry with this block's effect fields; k_tgctl patches its key fields
@@ -843,7 +850,7 @@ extern "C" int tbf_launch_front (const tbf_launch* P, hipStream_t stream)
 {
 	if (P->nInst == 0 || P->nBlocks > NL || P->instBase != 0)
 		return -22;
-	hipLaunchKernelGGL (k_front, dim3 (P->nInst), dim3 (NL), 0, stream, *P);
+	hipLaunchKernelGGL (k_front, dim3 ((P->nInst + NL - 1) / NL), dim3 (NL), 0, stream, *P);
 	return hipGetLastError () == hipSuccess ? 0 : -5;
 }
 

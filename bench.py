@@ -389,11 +389,34 @@ def roofline(a, B, nsamp, elapsed, samples_launch, launches, algo, kern, kern_is
     return roof
 
 
+def launch_ranks(n):
+    """`bench.py --gpus N` with no launcher around it: start N ranks under
+    torch.distributed.run as a CHILD process (this process has not touched HIP: nothing
+    above imports torch.cuda or the engine), relay its output (rank 0's JSON line) and
+    return its exit code.  One rank per GPU; TBF_BENCH_ONE_DEVICE=1 puts every rank on
+    device 0 (the rehearsal on a one-GPU lease)."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", str(ROOT / "bench.py")] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.run(cmd, env=env, cwd=str(ROOT)).returncode
+
+
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a.gpus))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world} (launch one rank per GPU, or drop the "
+              f"launcher and let bench.py start the ranks itself)", file=sys.stderr)
+        sys.exit(2)
     import numpy as np
     import torch
     from tunebfree_amd.shard import shard
@@ -404,7 +427,13 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("gloo")
     if not a.dry_run:
-        torch.cuda.set_device(local if world > 1 else 0)
+        one_dev = os.environ.get("TBF_BENCH_ONE_DEVICE", "0") == "1"
+        ndev = torch.cuda.device_count()  # counts devices without initialising HIP on this image
+        if world > 1 and not one_dev and local >= ndev:
+            print(f"bench.py: rank {rank} (local {local}) has no GPU: {ndev} visible for {world} ranks "
+                  f"(TBF_BENCH_ONE_DEVICE=1 shares device 0 for a rehearsal)", file=sys.stderr)
+            sys.exit(2)
+        torch.cuda.set_device(0 if (world == 1 or one_dev) else local)
     import tunebfree_amd as T
 
     # weak scaling: --batch instances per GPU, world * batch in all, contiguous shards

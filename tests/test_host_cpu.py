@@ -544,6 +544,24 @@ def test_bench_world2_dry_run_gloo():
         assert d["n_gpus"] == n and d["scaling"] == "weak" and d["value"] > 0
     assert two["dry_run"]["shard_rank0"] == [0, 5]
     assert two["dry_run"]["checksum"] == one["dry_run"]["checksum"]
+    # the driver's command form: `bench.py --gpus 2` with no launcher starts the two ranks itself
+    self_launched = _bench_json(common + ["--gpus", "2", "--batch", "5"])
+    assert self_launched["n_gpus"] == 2
+    assert self_launched["dry_run"]["shard_rank0"] == [0, 5]
+    assert self_launched["dry_run"]["checksum"] == one["dry_run"]["checksum"]
+
+
+def test_bench_world_size_mismatch_fails():
+    """A launcher world size that differs from --gpus is an error (exit 2), not a silent
+    one-GPU run reported as N."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--dry-run", "1"],
+                         env=env, capture_output=True, text=True, timeout=120, cwd=str(ROOT))
+    assert out.returncode == 2, out.stderr[-2000:]
+    assert "WORLD_SIZE=1" in out.stderr and not [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
 
 
 def test_drawbar_setting_out_of_range_ignored():

@@ -42,7 +42,18 @@ SIMDS = 256 * 4        # 256 CUs x 4 SIMD-32
 # FP64 add / mul / fma at half the FP32 rate (78.6 vs 157.3 TFLOP/s): 4; an FP32
 # transcendental (v_exp / v_sin / v_rcp ...) 2x a plain op: 4; an FP64 one: 16 (quarter of FP64)
 VALU_CYC = {"base": 2.0, "f64": 4.0, "trans32": 4.0, "trans64": 16.0}
-VALU_PEAK_TOPS = SIMDS * CLOCK_GHZ * 1e9 / VALU_CYC["base"] * 64 / 1e12  # 78.6 T lane-ops/s (FP32 rate)
+VALU_CYC_SOURCE = "spec-derived (78.6 vs 157.3 TFLOP/s)"
+# measured on the box when available (tools/valu_calib.py: issue-bound probes of each
+# instruction kind, cycles per wave64 instruction per SIMD), replacing the spec-derived costs
+VALU_CALIB_JSON = ROOT / "profiles" / "valu_calib.json"
+if VALU_CALIB_JSON.exists():
+    try:
+        _vc = json.loads(VALU_CALIB_JSON.read_text())["valu_cyc"]
+        VALU_CYC = {k: round(float(_vc[k]), 2) for k in VALU_CYC}
+        VALU_CYC_SOURCE = f"measured: {VALU_CALIB_JSON.relative_to(ROOT)} (tools/valu_calib.py)"
+    except (KeyError, ValueError, TypeError):
+        pass
+VALU_PEAK_TOPS = SIMDS * CLOCK_GHZ * 1e9 / VALU_CYC["base"] * 64 / 1e12  # T lane-ops/s at the FP32 issue rate
 # MI355X_MICROARCH.md, LDS/L2 gather table: rows shared by every workgroup of an XCD come
 # from its L2 at 16.8-18.8 TB/s chip-wide (measured); the tonegen-only workload's wave-bank
 # gathers are that pattern (one shared bank, every instance reading the same wheels)
@@ -366,10 +377,11 @@ def roofline(a, B, nsamp, elapsed, samples_launch, launches, algo, kern, kern_is
             "kernels": rows,
             "pmc_source": (pmc or {}).get("source"), "pmc_build": (pmc or {}).get("build"),
             "pmc_build_match": bool(pmc) and pmc.get("build") == lib_hash(), "pmc_note": pmc_note,
+            "valu_issue_cycles": VALU_CYC, "valu_issue_cycles_source": VALU_CYC_SOURCE,
             "method": "each kernel's unloaded launch time (every kernel alone, pipelining off, HIP events on "
                       "its stream) against its own ceilings: HBM = PMC FETCH_SIZE x 2 + WRITE_SIZE bytes per "
                       "launch / time vs 8 TB/s; VALU = SQ_INSTS_VALU (+ FP64 / transcendental issue cost) x "
-                      "SIMD-32 cycles / time vs 1024 SIMDs at 2.4 GHz; bound = the larger; the dominant "
+                      "cycles (valu_issue_cycles) / time vs 1024 SIMDs at 2.4 GHz; bound = the larger; the dominant "
                       "kernel = the longest unloaded launch"}
     if d.get("bound") == "hbm":
         roof.update({"achieved": d["hbm_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": d["hbm_frac"]})

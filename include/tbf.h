@@ -263,9 +263,12 @@ int tbf_debug_front_chunks (const tbf_engine* e, uint64_t* device_chunks, uint64
  * default stage groups: 15 GB at 4096 instances and 512 blocks, 60 GB at 2048) and
  * grow to the longest chunk a call makes, so this bounds the engine's HBM footprint; longer
  * chunks spread each launch's state traffic over more samples.  The
- * engine lowers it by itself when the device cannot hold the buffers.  Takes effect at the
- * next render (buffers larger than the new value are freed then); returns the value in
- * effect, or < 0 on error.  Renders are bit-identical at every value. */
+ * value is clamped to what the device can hold for the instances added so far (halved
+ * until the buffers fit the free memory plus the buffers held now), and a render that
+ * still cannot allocate them halves it again (tbf_debug_chunks reports the value in
+ * effect).  Takes effect at the next render (buffers larger than the new value are freed
+ * then); returns the value in effect, or < 0 on error.  Renders are bit-identical at every
+ * value. */
 int tbf_set_steady_chunk (tbf_engine* e, uint32_t blocks);
 /* test hook: set the reverb vibrato phase of line 0..7 of channel ch (b_reverb vib[ch][line],
  * src/reverb.cpp:479-496) of an instance, effective from the next block; parity tests use

@@ -787,6 +787,63 @@ def test_gpu_steady_chunks(oracle):
     assert max(eL, eR) <= TOL
 
 
+def test_gpu_set_steady_chunk_at_runtime(oracle):
+    """tbf_set_steady_chunk between renders (bench.py toggles it): render, shrink to 64
+    blocks (the stage buffers freed and reallocated at a smaller stride), render, grow to
+    2048 and to 512 (reallocated larger, single and double sets re-derived), render: bit
+    for bit the same calls on an engine fixed at TBF_STEADY_CHUNK=64, and the oracle.  The
+    value returned is the one in effect (tbf_debug_chunks)."""
+    import ctypes as C
+    import os
+    import torch
+    import tunebfree_amd as T
+    from orc_bind import Template
+    lib = T.load_library()
+    lib.tbf_debug_chunks.restype = C.c_int
+    lib.tbf_debug_chunks.argtypes = [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+    n, steps = 24, (300, 130, 700, 520)
+    seeds = [7000 + i for i in range(n)]
+    scens = [S.bench_scenario(i) for i in range(n)]
+    total = sum(steps)
+    outs = []
+    for fixed in (False, True):
+        if fixed:
+            os.environ["TBF_STEADY_CHUNK"] = "64"
+        try:
+            eng = T.Engine(sample_rate=48000.0, device=0)
+        finally:
+            os.environ.pop("TBF_STEADY_CHUNK", None)
+        tid = eng.template(seed=7)
+        eng.add_instances([tid] * n, seeds)
+        for i, sc in enumerate(scens):
+            for (_, kind, a, v) in sc:
+                (eng.note if kind == "note" else eng.set_param)(i, a, v)
+        L = torch.zeros((n, total * 128), dtype=torch.float32, device="cuda")
+        R = torch.zeros_like(L)
+        off = 0
+        for k, nb in enumerate(steps):
+            if not fixed and k > 0:
+                want = (64, 2048, 512)[k - 1]
+                got = eng.set_steady_chunk(want)
+                sb = C.c_uint32()
+                assert lib.tbf_debug_chunks(eng._h, None, C.byref(sb)) == 0
+                assert got == sb.value and got == want, (got, sb.value, want)
+            eng.render_device(nb, L[:, off * 128:].data_ptr(), R[:, off * 128:].data_ptr(), total * 128)
+            off += nb
+        eng.synchronize()
+        outs.append((L.cpu().numpy(), R.cpu().numpy()))
+        eng.close()
+        del L, R
+    assert np.array_equal(outs[0][0].view(np.uint32), outs[1][0].view(np.uint32))
+    assert np.array_equal(outs[0][1].view(np.uint32), outs[1][1].view(np.uint32))
+    pick = [0, 11, n - 1]
+    oL, oR, *_ = oracle_run(oracle, Template(oracle, seed=7), [seeds[i] for i in pick], [scens[i] for i in pick], total)
+    eL, xL = compare(outs[0][0][pick], oL)
+    eR, xR = compare(outs[0][1][pick], oR)
+    print(f"set_steady_chunk at runtime vs oracle: max|err| L={eL:.3g} R={eR:.3g} bit-exact {xL:.6f} {xR:.6f}")
+    assert max(eL, eR) <= TOL
+
+
 def test_gpu_threaded_host_control_reports_errors():
     """A bad event met by a host worker (threaded front end, >= 1024 instances) fails the
     call with the worker's message, as the serial loop would (the message is thread-local)."""

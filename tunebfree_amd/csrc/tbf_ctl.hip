@@ -113,12 +113,24 @@ __device__ __forceinline__ void wave_sync ()
 __device__ __forceinline__ void lds_order () { __asm__ __volatile__ ("" ::: "memory"); }
 
 /* A bus level, read at the device's coherence point (L2, not the CU's L1), since another
- * lane of the wave may have written it in an earlier message: the wave's vector memory
- * instructions reach L2 in issue order, so the read follows the write. */
+ * lane of the wave may have written it in an earlier message.
+ * HARDWARE ASSUMPTION (not a promise of the AMDGPU memory model, which treats the lanes as
+ * separate threads): a wave's vector memory instructions leave the CU in issue order, and
+ * requests to one address go to one L2 channel, which serves them in arrival order; so a
+ * load issued after a store to the same address (any lane) reads the stored value.  Between
+ * the messages of a block nothing else orders them (a vmcnt(0) wait per message would also
+ * wait out the next message's contribution loads, issued a message ahead); ctl_block, once
+ * per block, waits for the block's stores first (ctl_store_fence).  Pinned by
+ * test_gpu_device_control_large_clusters (~1500 messages a launch, every bus level read back
+ * after another lane's store) and the dense device-front-end tests, bit for bit. */
 __device__ __forceinline__ float ctl_bl_load (const float* p)
 {
 	return __hip_atomic_load (p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+
+/* every vector memory operation of the wave so far complete (s_waitcnt vmcnt(0): on gfx9
+ * it counts stores too, so the bus levels the messages stored have reached L2) */
+__device__ __forceinline__ void ctl_store_fence () { __builtin_amdgcn_s_waitcnt (0x0F70); }
 
 /* 16 B of a wheel's bus-level row the same way: a buffer load with the sc1 policy (bit 4 of
  * the cache-policy operand on gfx950), through the instance's rows as a buffer resource */
@@ -252,6 +264,7 @@ __device__ void ctl_block (CtlLds& sm, const CtlW& W, const float* __restrict__ 
 		__builtin_amdgcn_make_buffer_rsrc ((void*)gbl, (short)0, (int)((TBF_NW + 1) * TBF_BL_ROW * 4), 0x00020000);
 	const bool     dbChange  = (flags & 1) != 0;
 	const bool     recompute = (flags & 2) != 0;
+	ctl_store_fence (); /* the messages' bus-level stores before the row loads below */
 	uint32_t       nrem      = 0;
 	uint64_t       rb0       = 0; /* the first pass's removals */
 	uint32_t       on0       = 0; /* and its lanes' wheels */
@@ -689,8 +702,11 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_front (
 				if (op == TBF_FEV_EFFECT) {
 					/* the CLAP setParam effect setters (src/clap.cpp:162-207), as tbf_set_param and
 					 * stepControl apply them to the instance's control entry */
-					const float x = P.fevVal[e];
-					fx            = true;
+					/* a known setter marks the entry full (fx); an unknown bus is skipped and leaves
+					 * fx as an earlier event of the block set it (frontParam emits none today) */
+					const float x  = P.fevVal[e];
+					const bool  kn = bus <= TBF_FX_VIBTYPE; /* TBF_FX_ROTOR .. TBF_FX_VIBTYPE (tbf_types.h) */
+					fx = fx || kn;
 					switch (bus) {
 						case TBF_FX_ROTOR: revPend = (int)x; break; /* used by this block only */
 						case TBF_FX_CLEAN: E.odClean = (uint32_t)(int)x; break;
@@ -746,7 +762,7 @@ __global__ void __attribute__ ((amdgpu_flat_work_group_size (NL, NL))) k_front (
 							}
 							break;
 						}
-						default: fx = false; break;
+						default: break;
 					}
 					continue;
 				}

@@ -5,6 +5,7 @@
  * changes.
  */
 #include <hip/hip_runtime.h>
+#include <assert.h>
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -263,7 +264,9 @@ static int buildShared (tbf_engine* e)
 }
 
 /* host worker threads for per-template work: the process's lease (OMP_NUM_THREADS, set
- * on the GPU boxes) or the hardware, at most 16 */
+ * on the GPU boxes) or the hardware, at most TBF_MAX_HOST_THREADS (scanChunk sizes its
+ * per-range stack arrays by it) */
+#define TBF_MAX_HOST_THREADS 16u
 static unsigned hostThreads ()
 {
 	unsigned    t   = std::thread::hardware_concurrency ();
@@ -273,7 +276,7 @@ static unsigned hostThreads ()
 		t = (unsigned)atoi (ht);
 	else if (omp && atoi (omp) > 0)
 		t = (unsigned)atoi (omp);
-	return std::max (1u, std::min (t, 16u));
+	return std::max (1u, std::min (t, TBF_MAX_HOST_THREADS));
 }
 
 /* A persistent pool of hostThreads () - 1 workers (the caller is the last): a dense-event
@@ -1700,6 +1703,7 @@ static void scanChunk (uint32_t n, uint32_t b0, const tbf_event* ev, uint32_t ev
 {
 	const uint32_t nev = evEnd - evBeg;
 	cs.T   = std::max (1u, std::min<unsigned> (hostThreads (), (n + 255) / 256));
+	assert (cs.T <= TBF_MAX_HOST_THREADS);
 	cs.per = (n + cs.T - 1) / cs.T;
 	cs.Te  = std::max (1u, std::min (hostThreads (), (nev + 32767) / 32768));
 	cs.seg = (nev + cs.Te - 1) / cs.Te;
@@ -1711,7 +1715,7 @@ static void scanChunk (uint32_t n, uint32_t b0, const tbf_event* ev, uint32_t ev
 	parallelFor (cs.Te, [&] (uint32_t sgm) {
 		const uint32_t k0 = evBeg + std::min (nev, sgm * cs.seg), k1 = evBeg + std::min (nev, (sgm + 1) * cs.seg);
 		bool           p = false, b = false, f = cl != nullptr; /* locals: the flags share a cache line */
-		uint32_t       c[17] = {};                               /* events per instance range (T <= 16) */
+		uint32_t       c[TBF_MAX_HOST_THREADS + 1] = {};         /* events per instance range (T <= TBF_MAX_HOST_THREADS) */
 		for (uint32_t k = k0; k < k1; k++) {
 			const tbf_event& E = ev[k];
 			p                  = p || E.kind == TBF_EV_PROGRAM;
@@ -1727,7 +1731,7 @@ static void scanChunk (uint32_t n, uint32_t b0, const tbf_event* ev, uint32_t ev
 		}
 		if (f) { /* the records, by range, into this segment's own part of rec (no shared lines) */
 			uint32_t* bo = cs.boff.data () + (size_t)sgm * (cs.T + 1);
-			uint32_t  at[16];
+			uint32_t  at[TBF_MAX_HOST_THREADS];
 			bo[0] = k0 - evBeg;
 			for (unsigned t = 0; t < cs.T; t++) {
 				at[t]     = bo[t];
@@ -2039,6 +2043,25 @@ static int stepChunkFront (tbf_engine* e, uint32_t n, uint32_t want, uint32_t b0
  * producer and every reader run on one stage-group stream is single: the next chunk's
  * producer is ordered behind this chunk's readers by the stream (default groups {0,0,1,1,1,2}:
  * mid0, rvA and rvB single; mid1, mid2 by chunk parity). */
+/* bytes of the stage buffers at n instances and chunks of `blocks` blocks (mid0 8 B, mid1 /
+ * mid2 4 B, rvA / rvB 16 B per sample, each doubled when it alternates by chunk parity) */
+static size_t stageFootprint (const tbf_engine* e, size_t n, uint32_t blocks)
+{
+	static const int prod[5] = {0, 1, 2, 3, 4}, rd[5][2] = {{1, -1}, {2, 4}, {3, -1}, {4, -1}, {5, -1}};
+	static const size_t per[5] = {8, 4, 16, 16, 4};
+	const bool rv = e->cfg.chain_mode != TBF_CHAIN_TONEGEN && e->cfg.chain_mode != TBF_CHAIN_TAP_PREAMP;
+	size_t sum = 0;
+	for (int b = 0; b < 5; b++) {
+		if (b > 0 && !rv)
+			break;
+		bool dbl = false;
+		for (int r : rd[b])
+			dbl = dbl || (r >= 0 && e->grp[r] != e->grp[prod[b]]);
+		sum += (dbl ? 2 : 1) * per[b];
+	}
+	return sum * n * blocks * TBF_BLK;
+}
+
 static int stageBuffers (tbf_engine* e, uint32_t n, uint32_t nblocks, hipStream_t s)
 {
 	uint32_t want = TBF_CHUNK;
@@ -2047,11 +2070,12 @@ static int stageBuffers (tbf_engine* e, uint32_t n, uint32_t nblocks, hipStream_
 	want = std::min (want, std::max (e->steadyChunk, (uint32_t)TBF_CHUNK));
 	if (e->stageN == n && e->stageBlocks >= want && e->mid0.p)
 		return 0;
-	/* every launch that may read the old buffers: pipelined stages and the caller's stream */
+	/* every launch that may read the old buffers: pipelined stages and the caller's stream
+	 * (the engine's own streams and s; no device-wide synchronization, which would also
+	 * wait for a caller's unrelated work on other streams) */
 	if (int rc = drainStages (e))
 		return rc;
 	HIPCHK (hipStreamSynchronize (s));
-	HIPCHK (hipDeviceSynchronize ());
 	/* producer stage -> reader stages of mid0, mid1, rvA, rvB, mid2 */
 	static const int prod[5] = {0, 1, 2, 3, 4}, rd[5][2] = {{1, -1}, {2, 4}, {3, -1}, {4, -1}, {5, -1}};
 	for (int b = 0; b < 5; b++) {
@@ -2913,6 +2937,19 @@ int tbf_set_steady_chunk (tbf_engine* e, uint32_t blocks)
 	if (!e)
 		return fail (-22, "null argument");
 	e->steadyChunk = std::min (std::max (blocks, (uint32_t)TBF_CHUNK), (uint32_t)TBF_STEADY_MAX);
+	/* clamped here to what the device can hold for the current instances (the stage
+	 * buffers' footprint against the free memory plus the buffers held now), so the value
+	 * returned is the one renders use; stageBuffers still halves it on an allocation failure */
+	const size_t n = e->inst.size ();
+	if (e->cfg.device >= 0 && n) {
+		size_t freeB = 0, totalB = 0;
+		if (hipSetDevice (e->cfg.device) == hipSuccess && hipMemGetInfo (&freeB, &totalB) == hipSuccess) {
+			const size_t held = (e->mid0.cap + e->mid1.cap + e->mid2.cap) * sizeof (float) + (e->rvA.cap + e->rvB.cap) * sizeof (double);
+			while (e->steadyChunk > TBF_CHUNK && stageFootprint (e, n, e->steadyChunk) > freeB + held)
+				e->steadyChunk /= 2;
+		} else
+			(void)hipGetLastError ();
+	}
 	if (e->stageBlocks > e->steadyChunk)
 		e->stageN = 0; /* reallocated (smaller) at the next render */
 	return (int)e->steadyChunk;

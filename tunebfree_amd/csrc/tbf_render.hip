@@ -1260,6 +1260,24 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 
 #define RV_WIN 72 /* tap window per line: 64 samples + max offset 2 * vibDepth (5.4) + 2 */
 
+/* sin (v0 + (n+1) D) by angle addition from the start phase's S = sin v0, C = cos v0 and the
+ * step rows sd = sin ((n+1) D), cm = 2 sin^2 ((n+1) D / 2): S + (C sd - S cm).  Not libm's
+ * bits either way (FP64 sines only need a few ulps; the float outputs
+ * are bit-identical); RVL_SINFMA forms C sd - S cm with one fma (3 FP64 instructions for 4:
+ * k_rv_core_lds 9.48 -> 9.42 ms alone per 512 blocks, profiles/r06/s2).  Every network
+ * kernel and path uses this one expression, so they agree however a render is split. */
+#ifndef RVL_SINFMA
+#define RVL_SINFMA 1
+#endif
+__device__ __forceinline__ double rv_sin_add (double S, double C, double sd, double cm)
+{
+#if RVL_SINFMA
+	return S + __builtin_fma (C, sd, -(S * cm));
+#else
+	return S + ((C * sd) - (S * cm));
+#endif
+}
+
 struct RvCoreLds {
 	tbf_rv_chan st;
 	double      win[8][RV_WIN];  /* tap windows of the sub-block: slots count+1 .. count+72 */
@@ -1381,7 +1399,7 @@ __device__ __forceinline__ double rv_core_tap (RvCoreLds& sm, const tbf_inst_con
 				sm.tabD[l] = D;
 		}
 		const double S = rld (Sx, l), C = rld (Cx, l);
-		s              = S + ((C * sm.sd[l][n]) - (S * sm.cm[l][n]));
+		s              = rv_sin_add (S, C, sm.sd[l][n], sm.cm[l][n]);
 	} else {
 		const double dl = K.vibDelta[l];
 		double       v  = rld (v0x, l);
@@ -1598,6 +1616,67 @@ __device__ __forceinline__ void rvl_write (double* rg, int i, int d, double v)
 		rg[i + d + 1] = v;
 }
 
+#ifndef RVL_SCAL
+#define RVL_SCAL 1 /* the workers' line counters in scalar registers, wraps as scalar branches (below) */
+#endif
+/* lane n's slot c + n of a line of delay D, wrapped past D (wrap_slot), for a wave-uniform c
+ * in [0, D + 1]: a sub-block wraps a line in about one of D / 64 groups, so the test is a
+ * scalar branch around the lanes' correction and the common case is one add */
+template <int D>
+__device__ __forceinline__ int rvl_slot (int c, int n)
+{
+	int s = c + n;
+	if (c > D - (NL - 1)) {
+		/* opaque to the optimizer, so the branch stays a branch (if-converted, the lanes'
+		 * compare and selects ran in every sub-block) */
+		__asm__ __volatile__ ("" : "+v"(s));
+		s -= (s > D) ? D + 1 : 0;
+	}
+	return s;
+}
+
+/* rvl_slot of tap line l (0..7) one past the worker's counter (the taps' count + 1) */
+__device__ __forceinline__ int rvl_slot_l (int l, const int (&cs)[12], int n)
+{
+	switch (l) { /* l is a constant after unrolling: the delay a template argument */
+		case 0: return rvl_slot<RVL_DLY[0]> (cs[0] + 1, n);
+		case 1: return rvl_slot<RVL_DLY[1]> (cs[1] + 1, n);
+		case 2: return rvl_slot<RVL_DLY[2]> (cs[2] + 1, n);
+		case 3: return rvl_slot<RVL_DLY[3]> (cs[3] + 1, n);
+		case 4: return rvl_slot<RVL_DLY[4]> (cs[4] + 1, n);
+		case 5: return rvl_slot<RVL_DLY[5]> (cs[5] + 1, n);
+		case 6: return rvl_slot<RVL_DLY[6]> (cs[6] + 1, n);
+		default: return rvl_slot<RVL_DLY[7]> (cs[7] + 1, n);
+	}
+}
+
+/* rvl_write at slot rvl_slot<D> (c, n): the mirror (slots below RVL_MIR) is possible only when
+ * c < RVL_MIR or the sub-block wraps, again a scalar test */
+template <int D>
+__device__ __forceinline__ void rvl_write_s (double* rg, int c, int n, double v)
+{
+	if (c >= RVL_MIR && c <= D - (NL - 1)) { /* the common case: no wrap, no mirror */
+		rg[c + n] = v;
+	} else {
+		int i = c + n;
+		__asm__ __volatile__ ("" : "+v"(i)); /* a branch, not selects (rvl_slot) */
+		i -= (i > D) ? D + 1 : 0;
+		rg[i] = v;
+		if (i < RVL_MIR)
+			rg[i + D + 1] = v;
+	}
+}
+
+/* lane n receives lane n-1's v, lane 0 receives first (FP64 lane_shr1_or: the DPP moves keep
+ * the old value in the lane with no source) */
+__device__ __forceinline__ double lane_shr1_or (double v, double first)
+{
+	const unsigned long long u = __double_as_longlong (v), f = __double_as_longlong (first);
+	const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp ((int)(unsigned)f, (int)(unsigned)u, 0x138, 0xF, 0xF, false);
+	const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp ((int)(unsigned)(f >> 32), (int)(unsigned)(u >> 32), 0x138, 0xF, 0xF, false);
+	return __longlong_as_double ((long long)(((unsigned long long)hi << 32) | lo));
+}
+
 /* the planner wave: the phase plan of group g into buffer b (start phases, closed-form
  * flags, sincos of the start phases, sine rows); st.vib advanced past the group.  It
  * depends only on the phases, so it runs while the workers process the group before. */
@@ -1758,6 +1837,16 @@ __device__ __forceinline__ void rvl_pair (const tbf_launch& P, const tbf_inst_co
 	/* the workers and the planner run separate loops with the same two barriers per group, so
 	 * the registers of one role are not held live across the other's code */
 	if (w < RVL_G) {
+#if RVL_SCAL
+		/* this worker's first slot of each line in the group, wave-uniform (SGPRs) */
+		int cs[12];
+#pragma unroll
+		for (int l = 0; l < 12; l++)
+			cs[l] = rl (cw, l);
+#define RVL_C(l) cs[l]
+#else
+#define RVL_C(l) rl (cw, l)
+#endif
 #pragma unroll 1
 		for (uint32_t g = 0; g < nGrp; g++) {
 			const int  nb  = (int)min ((uint32_t)RVL_G, nSub - g * RVL_G);
@@ -1784,7 +1873,7 @@ __device__ __forceinline__ void rvl_pair (const tbf_launch& P, const tbf_inst_co
 #pragma unroll
 					for (int l = 0; l < 8; l++) {
 						const double2 SC = sm.SC[par][w][l], q = sm.sc[par][l][n];
-						sn[l]            = SC.x + ((SC.y * q.x) - (SC.x * q.y));
+						sn[l]            = rv_sin_add (SC.x, SC.y, q.x, q.y);
 					}
 				} else {
 					const uint32_t ox = __builtin_amdgcn_readfirstlane (sm.okx[par][w]);
@@ -1792,13 +1881,13 @@ __device__ __forceinline__ void rvl_pair (const tbf_launch& P, const tbf_inst_co
 					for (int l = 0; l < 8; l++) {
 						if ((om >> l) & 1) {
 							const double2 SC = sm.SC[par][w][l], q = sm.sc[par][l][n];
-							sn[l]            = SC.x + ((SC.y * q.x) - (SC.x * q.y));
+							sn[l]            = rv_sin_add (SC.x, SC.y, q.x, q.y);
 						} else if ((ox >> l) & 1) { /* k_rv_core's rows for this step (rv_core_tap) */
 							const double2 SC = sm.SC[par][w][l];
 							const double  dn = (double)(n + 1) * sm.Dx[par][w][l]; /* exact */
 							const double  hh = sin (dn * 0.5);
 							const double  sd = sin (dn), cm = 2.0 * hh * hh;
-							sn[l]            = SC.x + ((SC.y * sd) - (SC.x * cm));
+							sn[l]            = rv_sin_add (SC.x, SC.y, sd, cm);
 						} else {
 							const double dl = rld (vdl, l);
 							double       v  = sm.v0[par][w][l];
@@ -1816,9 +1905,17 @@ __device__ __forceinline__ void rvl_pair (const tbf_launch& P, const tbf_inst_co
 #pragma unroll
 				for (int l = 0; l < 8; l++) {
 					const double off = (sn[l] + 1.0) * K.vibDepth;
+#if RVL_SCAL
+					const int cn = rvl_slot_l (l, cs, n);
+					wk[l]        = (int)(cn + off); /* <= d + 5: the mirror covers wk + 1 */
+					/* off >= 0, so off - floor (off) is exact (or off < 0 tiny, |off| >= 2.7 2^-53: one
+					 * rounding of off + 1, below 1): v_fract_f64's value */
+					fr[l] = __builtin_amdgcn_fract (off);
+#else
 					const int    cn  = wrap_slot (rl (cw, l) + n + 1, RVL_DLY[l]);
 					wk[l]            = (int)(cn + off); /* <= d + 5: the mirror covers wk + 1 */
 					fr[l]            = off - floor (off);
+#endif
 				}
 #pragma unroll
 				for (int l = 0; l < 8; l++) {
@@ -1845,7 +1942,7 @@ __device__ __forceinline__ void rvl_pair (const tbf_launch& P, const tbf_inst_co
 				mix = (I[0] + I[1] + I[2] + I[3] + I[4] + I[5] + I[6] + I[7]) / 8.0;
 #pragma unroll
 				for (int l = 8; l < 12; l++) {
-					const double old = sm.ring[RVL_LOFS[l] + rl (cw, l) + n + 1]; /* <= d + 64: mirror */
+					const double old = sm.ring[RVL_LOFS[l] + RVL_C (l) + n + 1]; /* <= d + 64: mirror */
 					double       a   = a0;
 					a -= old * 0.5;
 					apw[l - 8] = a;
@@ -1868,6 +1965,21 @@ __device__ __forceinline__ void rvl_pair (const tbf_launch& P, const tbf_inst_co
 #pragma unroll
 				for (int l = 0; l < 8; l++)
 					cprv[l] = cp[l];
+#if RVL_SCAL
+				rvl_write_s<RVL_DLY[8]> (sm.ring + RVL_LOFS[8], cs[8], n, apw[0]);
+				rvl_write_s<RVL_DLY[9]> (sm.ring + RVL_LOFS[9], cs[9], n, apw[1]);
+				rvl_write_s<RVL_DLY[10]> (sm.ring + RVL_LOFS[10], cs[10], n, apw[2]);
+				rvl_write_s<RVL_DLY[11]> (sm.ring + RVL_LOFS[11], cs[11], n, apw[3]);
+				/* feedback (n - 1): lane 0 takes the previous sub-block's last, the DPP move's old value */
+				rvl_write_s<RVL_DLY[0]> (sm.ring + RVL_LOFS[0], cs[0], n, ap[3] + lane_shr1_or (fb[0], cprv[0]));
+				rvl_write_s<RVL_DLY[1]> (sm.ring + RVL_LOFS[1], cs[1], n, ap[2] + lane_shr1_or (fb[1], cprv[1]));
+				rvl_write_s<RVL_DLY[2]> (sm.ring + RVL_LOFS[2], cs[2], n, ap[1] + lane_shr1_or (fb[2], cprv[2]));
+				rvl_write_s<RVL_DLY[3]> (sm.ring + RVL_LOFS[3], cs[3], n, ap[0] + lane_shr1_or (fb[3], cprv[3]));
+				rvl_write_s<RVL_DLY[4]> (sm.ring + RVL_LOFS[4], cs[4], n, ap[0] + lane_shr1_or (fb[4], cprv[4]));
+				rvl_write_s<RVL_DLY[5]> (sm.ring + RVL_LOFS[5], cs[5], n, ap[1] + lane_shr1_or (fb[5], cprv[5]));
+				rvl_write_s<RVL_DLY[6]> (sm.ring + RVL_LOFS[6], cs[6], n, ap[2] + lane_shr1_or (fb[6], cprv[6]));
+				rvl_write_s<RVL_DLY[7]> (sm.ring + RVL_LOFS[7], cs[7], n, ap[3] + lane_shr1_or (fb[7], cprv[7]));
+#else
 #pragma unroll
 				for (int l = 8; l < 12; l++)
 					rvl_write (sm.ring + RVL_LOFS[l], wrap_slot (rl (cw, l) + n, RVL_DLY[l]), RVL_DLY[l], apw[l - 8]);
@@ -1878,6 +1990,7 @@ __device__ __forceinline__ void rvl_pair (const tbf_launch& P, const tbf_inst_co
 					const double prev = n == 0 ? cprv[l] : up;
 					rvl_write (sm.ring + RVL_LOFS[l], wrap_slot (rl (cw, l) + n, RVL_DLY[l]), RVL_DLY[l], ap[srcAp[l]] + prev);
 				}
+#endif
 				/* the tap mix, stored at the start of the next group (see above) */
 				pmix = mix;
 				po   = o;
@@ -1886,8 +1999,14 @@ __device__ __forceinline__ void rvl_pair (const tbf_launch& P, const tbf_inst_co
 			a0  = a0n;
 			a0n = nxt;
 			cw = wrap_slot (cw + TBF_SUB * RVL_G, dlyv);
+#if RVL_SCAL
+#pragma unroll
+			for (int l = 0; l < 12; l++)
+				cs[l] = wrap_slot (cs[l] + TBF_SUB * RVL_G, RVL_DLY[l]);
+#endif
 			__syncthreads ();
 		}
+#undef RVL_C
 	} else {
 #pragma unroll 1
 		for (uint32_t g = 0; g < nGrp; g++) {

@@ -3090,7 +3090,7 @@ int tbf_debug_exact (int32_t op, const double* in, double* out, uint32_t n)
 
 int tbf_debug_calibrate (int32_t op, void* buf, uint64_t n, void* stream)
 {
-	if (!buf || op < 0 || op > 4 || n < 16)
+	if (!buf || op < 0 || op > 12 || n < 16)
 		return fail (-22, "bad arguments");
 	int rc = tbf_launch_calibrate (op, buf, n, (hipStream_t)stream);
 	return rc ? fail (rc, "calibration launch failed") : 0;

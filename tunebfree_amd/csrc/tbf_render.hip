@@ -302,7 +302,7 @@ __device__ __forceinline__ void tg_cache_store (const TgCache& c, TgLds& sm)
 }
 
 /* oscGenerateFragment core interpreter + vibratoProc + mixdown, src/tonegen.cpp:3607-3777 */
-__device__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl& G, const tbf_tpl_desc* T,
+__device__ __forceinline__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl& G, const tbf_tpl_desc* T,
                               float2* __restrict__ out, float* __restrict__ oL = nullptr, float* __restrict__ oR = nullptr,
                               float kc = 0.f, float pe = 0.f, TgCache* tc = nullptr)
 {
@@ -1616,6 +1616,9 @@ __device__ __forceinline__ void rvl_write (double* rg, int i, int d, double v)
 		rg[i + d + 1] = v;
 }
 
+#ifndef RVL_FAST2
+#define RVL_FAST2 1 /* tap index without the FP64 sum (a vote on the rare carry), allpass products as fmas (exact) */
+#endif
 #ifndef RVL_SCAL
 #define RVL_SCAL 1 /* the workers' line counters in scalar registers, wraps as scalar branches (below) */
 #endif
@@ -1902,21 +1905,44 @@ __device__ __forceinline__ void rvl_pair (const tbf_launch& P, const tbf_inst_co
 				 * next line's address was formed) */
 				double I[8], fr[8], r0[8], r1[8];
 				int    wk[8];
+#if RVL_SCAL && RVL_FAST2
+				double offv[8];
+				int    cnv[8];
+				bool   slow = false;
+#endif
 #pragma unroll
 				for (int l = 0; l < 8; l++) {
 					const double off = (sn[l] + 1.0) * K.vibDepth;
 #if RVL_SCAL
 					const int cn = rvl_slot_l (l, cs, n);
-					wk[l]        = (int)(cn + off); /* <= d + 5: the mirror covers wk + 1 */
 					/* off >= 0, so off - floor (off) is exact (or off < 0 tiny, |off| >= 2.7 2^-53: one
 					 * rounding of off + 1, below 1): v_fract_f64's value */
 					fr[l] = __builtin_amdgcn_fract (off);
+#if RVL_FAST2
+					/* (int)(cn + off) == cn + (int)off unless the sum's rounding (ulp <= 2^-42, the
+					 * sum < 2048) carries the fraction to the next integer, or off < 0: both need
+					 * fr >= 1 - 2^-21, i.e. fr's high word >= 0x3FEFFFFF (one integer compare);
+					 * such a wave recomputes the reference's expression below */
+					offv[l] = off;
+					cnv[l]  = cn;
+					wk[l]   = cn + (int)off;
+					slow    = slow || (uint32_t)(__double_as_longlong (fr[l]) >> 32) >= 0x3FEFFFFFu;
+#else
+					wk[l] = (int)(cn + off); /* <= d + 5: the mirror covers wk + 1 */
+#endif
 #else
 					const int    cn  = wrap_slot (rl (cw, l) + n + 1, RVL_DLY[l]);
 					wk[l]            = (int)(cn + off); /* <= d + 5: the mirror covers wk + 1 */
 					fr[l]            = off - floor (off);
 #endif
 				}
+#if RVL_SCAL && RVL_FAST2
+				if (__builtin_expect (__any (slow), 0)) {
+#pragma unroll
+					for (int l = 0; l < 8; l++)
+						wk[l] = (int)(cnv[l] + offv[l]);
+				}
+#endif
 #pragma unroll
 				for (int l = 0; l < 8; l++) {
 					const double* rg = sm.ring + RVL_LOFS[l];
@@ -1943,12 +1969,22 @@ __device__ __forceinline__ void rvl_pair (const tbf_launch& P, const tbf_inst_co
 #pragma unroll
 				for (int l = 8; l < 12; l++) {
 					const double old = sm.ring[RVL_LOFS[l] + RVL_C (l) + n + 1]; /* <= d + 64: mirror */
+#if RVL_FAST2
+					/* a0 - old 0.5 then (.) 0.5 + old: both products by 0.5 are exact unless an
+					 * operand is subnormal (< 2.2e-308; the input's denormal guard,
+					 * src/reverb.cpp:343-346, keeps the network's values above ~1e-25), so one fma
+					 * each gives the reference's values */
+					const double a = __builtin_fma (old, -0.5, a0);
+					apw[l - 8]     = a;
+					ap[l - 8]      = __builtin_fma (a, 0.5, old);
+#else
 					double       a   = a0;
 					a -= old * 0.5;
 					apw[l - 8] = a;
 					a *= 0.5;
 					a += old;
 					ap[l - 8] = a;
+#endif
 				}
 				if (n == NL - 1) {
 #pragma unroll
@@ -3002,6 +3038,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 		 * start, after a bypassed block or a new coefficient set). */
 		const int  ap    = sm.ap;
 		const bool aNext = sb + 1 < TBF_BLK / TBF_SUB || hasNext;
+#ifndef WH_ABL_HORN
 		if (!sm.aReady)
 			sm.ab[ap ^ 1][n] = xin;
 		if (aNext)
@@ -3017,6 +3054,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 			sm.ab[ap ^ 1][n] = wh_output (sm.ab[ap ^ 1][n], z0, z1, ha);
 			wave_sync ();
 		}
+#endif
 		/* the states the pass starts from (horn A's scrubbed when it crosses into the next block) */
 		const bool scrubA = sb + 1 == TBF_BLK / TBF_SUB;
 		float      zs[4][2];
@@ -3033,6 +3071,8 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 		const bool     wrap = wb + TBF_SUB > (uint32_t)W;
 #ifdef WH_NO_SERIAL /* timing experiment only (wrong output): k_whirl without its serial filter passes */
 		if (false) {
+#elif defined(WH_ABL_HORN) /* timing experiment only (wrong output): horn filters A, B not run in k_whirl */
+		if (lane >= 2 && lane < 4) {
 #else
 		if (lane < 4 && (lane > 0 || aNext)) {
 #endif
@@ -3045,9 +3085,13 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 		wave_sync ();
 		/* the filter outputs: horn B -> xf, horn A of the next sub-block in place, the drum
 		 * shelves' (then the ring slots are cleared) */
+#ifdef WH_ABL_HORN
+		sm.xf[4 + n] = xin;
+#else
 		sm.xf[4 + n] = wh_output (sm.ab[ap ^ 1][n], zs[1][0], zs[1][1], hb);
 		if (aNext)
 			sm.ab[ap][n] = wh_output (sm.ab[ap][n], zs[0][0], zs[0][1], ha);
+#endif
 		const float dL = wh_output (sm.wring[2][o], zs[2][0], zs[2][1], K.drf);
 		const float dR = wh_output (sm.wring[3][o], zs[3][0], zs[3][1], K.drf);
 		sm.wring[2][o] = 0.f;

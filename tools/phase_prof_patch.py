@@ -11,7 +11,7 @@ from pathlib import Path
 
 SRC = Path(__file__).resolve().parents[1] / "tunebfree_amd" / "csrc" / "tbf_render.hip"
 CFG = {
-    "tonegen": dict(lds="struct TgLds {", funcs=["__device__ void stage_tonegen ("],
+    "tonegen": dict(lds="struct TgLds {", funcs=["__device__ __forceinline__ void stage_tonegen ("],
                     kernel="k_tonegen (const tbf_launch P", init_after="\tTgLds&              sm = smv[part];\n",
                     end="\t\tfor (uint32_t i = lane; i < sizeof (tbf_tg_state) / 4; i += NL)\n\t\t\tdst[i] = src[i];\n\t}\n}"),
 }

@@ -39,14 +39,14 @@ def main():
     body = sub(body, "\t__syncthreads ();\n\t/* the workers and the planner run separate loops",
                "\t__syncthreads ();\n\tt1 = RVP_T (); pt[1] += t1 - t0; t0 = t1;\n\t/* the workers and the planner run separate loops")
     # the worker loop
-    body = sub(body, "\tif (w < RVL_G) {\n#pragma unroll 1\n\t\tfor (uint32_t g = 0; g < nGrp; g++) {\n",
-               "\tif (w < RVL_G) {\n#pragma unroll 1\n\t\tfor (uint32_t g = 0; g < nGrp; g++) {\n\t\t\tpt[7]++;\n")
+    body = sub(body, "#pragma unroll 1\n\t\tfor (uint32_t g = 0; g < nGrp; g++) {\n\t\t\tconst int  nb  =",
+               "#pragma unroll 1\n\t\tfor (uint32_t g = 0; g < nGrp; g++) {\n\t\t\tpt[7]++;\n\t\t\tconst int  nb  =")
     body = sub(body, "\t\t\t__syncthreads ();\n\t\t\t/* ---- write phase ---- */",
                "\t\t\tt1 = RVP_T (); pt[2] += t1 - t0; t0 = t1;\n\t\t\t__syncthreads ();\n"
                "\t\t\tt1 = RVP_T (); pt[3] += t1 - t0; t0 = t1;\n\t\t\t/* ---- write phase ---- */")
-    body = sub(body, "\t\t\tcw = wrap_slot (cw + TBF_SUB * RVL_G, dlyv);\n\t\t\t__syncthreads ();\n\t\t}\n",
-               "\t\t\tcw = wrap_slot (cw + TBF_SUB * RVL_G, dlyv);\n\t\t\tt1 = RVP_T (); pt[4] += t1 - t0; t0 = t1;\n"
-               "\t\t\t__syncthreads ();\n\t\t\tt1 = RVP_T (); pt[5] += t1 - t0; t0 = t1;\n\t\t}\n")
+    body = sub(body, "#endif\n\t\t\t__syncthreads ();\n\t\t}\n#undef RVL_C",
+               "#endif\n\t\t\tt1 = RVP_T (); pt[4] += t1 - t0; t0 = t1;\n"
+               "\t\t\t__syncthreads ();\n\t\t\tt1 = RVP_T (); pt[5] += t1 - t0; t0 = t1;\n\t\t}\n#undef RVL_C")
     # the planner loop: planning as the "read phase", its two barriers
     body = sub(body, "\t\t\t__syncthreads ();\n\t\t\t__syncthreads ();\n\t\t}\n",
                "\t\t\tpt[7]++;\n\t\t\tt1 = RVP_T (); pt[2] += t1 - t0; t0 = t1;\n\t\t\t__syncthreads ();\n"

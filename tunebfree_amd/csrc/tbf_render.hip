@@ -42,6 +42,9 @@
 #ifndef TG_LDS_ALL
 #define TG_LDS_ALL 1 /* entries staged in LDS for steady chunks too (their per-block scalar loads: 21.8 -> 18.8 ms with TG_CACHE) */
 #endif
+#ifndef TG_SCAN_PASS
+#define TG_SCAN_PASS 1 /* the vibrato scanner's scatter as two ordered-add passes (stage_tonegen) */
+#endif
 #ifndef TG_ABL
 #define TG_ABL 0 /* timing experiments (wrong output): 1 bank reads from one row, 2 no scanner */
 #endif
@@ -250,6 +253,82 @@ __device__ __forceinline__ float eq_iir (float c0, float c1, float c2, float c3,
 	z1         = z0;
 	z0         = temp;
 	return y;
+}
+
+/* One motion's ordered adds into a ring for a 64-sample sub-block (HN_MOTION /
+ * DR_MOTION, src/whirl.cpp:1432-1469): sample n adds a_n into slot U_n and b_n into
+ * slot U_n + 1, in sample order.  With U non-decreasing, the samples sharing a slot
+ * value form a group G(u) and slot t receives, in order, b of G(t-1) then a of G(t).
+ * Groups have at most 2 samples (checked by the caller), so the first lane of each
+ * group owns slot t = U (and slot t + 1 when no group sits at t + 1) and finds its
+ * neighbours' terms with lane shifts; owners never share a slot. */
+/* the owner lanes' slots and ordered sums of one motion (see motion_add) */
+struct MotionOwn {
+	bool     first, own2, pair, lead, lead2;
+	uint32_t t;
+	float    a, an, b, bn, bp1, bp2;
+};
+
+__device__ __forceinline__ MotionOwn motion_own (int U, float a, float b, int lane)
+{
+	MotionOwn m;
+	const int Up  = lane_shr1 (U);
+	const int Up2 = lane_shr1 (Up);
+	const int Un  = lane_shl1 (U);
+	const int Un2 = lane_shl1 (Un);
+	m.bp1         = lane_shr1 (b);
+	m.bp2         = lane_shr1 (m.bp1);
+	m.an          = lane_shl1 (a);
+	m.bn          = lane_shl1 (b);
+	m.a           = a;
+	m.b           = b;
+	m.t           = (uint32_t)U;
+	m.first       = lane == 0 || U != Up;
+	m.pair        = lane < NL - 1 && Un == U;
+	m.lead        = lane > 0 && Up == U - 1;
+	m.lead2       = lane > 1 && Up2 == Up;
+	const bool nextExists = m.pair ? lane < NL - 2 : lane < NL - 1;
+	const int  Unx        = m.pair ? Un2 : Un;
+	m.own2                = !nextExists || Unx != U + 1;
+	return m;
+}
+
+/* slot t: b of the group at t-1 (<= 2 samples, in order), then a of the group at t.  A
+ * skipped add keeps v (v + 0 is not v for v = -0), so each optional add is a select of the
+ * sum, not a branch: the passes stay branch-free */
+__device__ __forceinline__ float motion_sum_t (const MotionOwn& m, float v)
+{
+	float t = v + m.bp2;
+	v       = (m.lead && m.lead2) ? t : v;
+	t       = v + m.bp1;
+	v       = m.lead ? t : v;
+	v += m.a;
+	t = v + m.an;
+	return m.pair ? t : v;
+}
+
+/* slot t + 1 when no group sits there: b of this group */
+__device__ __forceinline__ float motion_sum_t1 (const MotionOwn& m, float w)
+{
+	w += m.b;
+	const float t = w + m.bn;
+	return m.pair ? t : w;
+}
+
+template <int W>
+__device__ __forceinline__ void motion_add (float* ring, int U, float a, float b, int lane)
+{
+	const uint32_t  WM = (uint32_t)W - 1u;
+	const MotionOwn m  = motion_own (U, a, b, lane);
+	if (m.first) {
+		/* both slots read before either is written (one LDS round trip): an owner's
+		 * slot t+1 is read but left alone when another group owns it */
+		const uint32_t i0 = m.t & WM, i1 = (m.t + 1) & WM;
+		const float    v = ring[i0], w = ring[i1];
+		ring[i0]         = motion_sum_t (m, v);
+		if (m.own2)
+			ring[i1] = motion_sum_t1 (m, w);
+	}
 }
 
 /* ================================================================== k_tonegen */
@@ -514,6 +593,44 @@ __device__ __forceinline__ void stage_tonegen (const tbf_launch& P, TgLds& sm, c
 			sm.u.v.vh[n] = n + (int)(((uint32_t)h - op) & 0x3FFu); /* slot offset from out0 */
 		}
 		wave_sync ();
+#if TG_SCAN_PASS
+		/* The scatter as two passes of ordered adds (motion_add, the whirl rings' owner
+		 * scheme): sample m adds x - g into slot out0 + vh[m] and g into the slot after, in
+		 * sample order; for non-decreasing slots with groups of <= 2 equal slots in a pass,
+		 * the first lane of each group owns its slot (and the next when no group sits
+		 * there) and takes its neighbours' terms by DPP, and the second pass (samples
+		 * 64..127) reads what the first wrote.  Then every output slot is read and cleared:
+		 * all writes land >= 1 slot ahead of the writing sample's own output slot, so an
+		 * output read after all of them sees exactly the earlier samples' (src/vibrato.cpp:
+		 * 380-409).  Preconditions (wave votes): 1 <= vh[m] - m <= 31 and the slots
+		 * non-decreasing over the block, no three equal in a row; lane 0 replays serially
+		 * otherwise.  (The ordered gather before this looped over each slot's candidate
+		 * samples: 30 % of the kernel's cycles, tools/phase_prof.py.) */
+		const int U0 = sm.u.v.vh[lane], U1 = sm.u.v.vh[lane + NL];
+		const float a0 = sm.u.v.va[lane], b0 = sm.u.v.vg[lane], a1 = sm.u.v.va[lane + NL], b1 = sm.u.v.vg[lane + NL];
+		int bad = (U0 - lane < 1 || U0 - lane > 31 || U1 - (lane + NL) < 1 || U1 - (lane + NL) > 31) ? 1 : 0;
+		{
+			const int      P0 = lane_shr1 (U0), P1 = lane_shr1 (U1), L63 = rl (U0, NL - 1);
+			const int      Pr1 = lane == 0 ? L63 : P1; /* sample lane + 63 */
+			const uint64_t e0  = __ballot (lane > 0 && U0 == P0), e1 = __ballot (U1 == Pr1 && lane > 0);
+			bad = bad || (lane > 0 && U0 < P0) || U1 < Pr1;
+			/* three equal in a row inside a pass: two consecutive eq bits */
+			bad = __any (bad) || (e0 & (e0 >> 1)) != 0 || (e1 & (e1 >> 1)) != 0 || (P.dbg & TBF_DEBUG_FORCE_SERIAL);
+		}
+		if (!bad) {
+			motion_add<TBF_VRING> (st.vring, (int)out0 + U0, a0, b0, lane);
+			wave_sync ();
+			motion_add<TBF_VRING> (st.vring, (int)out0 + U1, a1, b1, lane);
+			wave_sync ();
+			for (int k = 0; k < 2; k++) {
+				const int      wo   = lane + k * NL;
+				const uint32_t slot = (out0 + wo) & (TBF_VRING - 1);
+				const float    v    = st.vring[slot];
+				const float    x    = sm.vin[wo];
+				sm.u.v.vout[wo]     = G.vibMixed ? (x + v) * (float)0.7071067811865475 : v;
+				st.vring[slot]      = 0.f;
+			}
+#else
 		/* ordered gather: slot W_o collects, in sample order, x-g from samples with
 		 * H==W_o and g from samples with H+1==W_o; valid while H is non-decreasing and
 		 * within 32 ahead (checked; lane 0 replays serially otherwise) */
@@ -551,6 +668,7 @@ __device__ __forceinline__ void stage_tonegen (const tbf_launch& P, TgLds& sm, c
 					st.vring[slot] = v;
 				}
 			}
+#endif
 		} else {
 			if (lane == 0) {
 				atomicOr (P.errFlags, (uint32_t)TBF_PATH_VIB_SERIAL);
@@ -2192,6 +2310,46 @@ __device__ __forceinline__ void rvc_serial (double* const (&row)[Q], const doubl
 	PRIO_DOWN ();
 }
 
+/* One chain's biquad over a tile with its input products precomputed (src/reverb.cpp:733-741,
+ * 756-764): p0 = x c0, p1 = x c1, p2 = x c2 are the reference's rounded products, so
+ *   t = p0 + s7;  s7 = (p1 - t c3) + s8;  s8 = p2 - t c4
+ * is its recurrence bit for bit, six FP64 operations a step where rvc_bq has nine (the
+ * chain wave is issue-bound: tools/rvp_prof.py, profiles/r06/s5).  t goes over p0.  Groups
+ * of eight, the next group's products read while this group's steps run. */
+__device__ __forceinline__ void rvc_serial_p (double* r0, const double* r1, const double* r2, double c3, double c4, double& s7,
+                                              double& s8)
+{
+	PRIO_UP ();
+	double a0[8], a1[8], a2[8], b0[8], b1[8], b2[8];
+	auto ld = [&] (double (&x0)[8], double (&x1)[8], double (&x2)[8], int i0) {
+#pragma unroll
+		for (int k = 0; k < 8; k++) {
+			x0[k] = r0[i0 + k];
+			x1[k] = r1[i0 + k];
+			x2[k] = r2[i0 + k];
+		}
+	};
+	auto run = [&] (const double (&x0)[8], const double (&x1)[8], const double (&x2)[8], int i0) {
+#pragma unroll
+		for (int k = 0; k < 8; k++) {
+			const double t = x0[k] + s7;
+			s7             = (x1[k] - (t * c3)) + s8;
+			s8             = x2[k] - (t * c4);
+			r0[i0 + k]     = t;
+		}
+	};
+	ld (a0, a1, a2, 0);
+#pragma unroll
+	for (int i0 = 0; i0 < RVC_T; i0 += 16) {
+		ld (b0, b1, b2, i0 + 8);
+		run (a0, a1, a2, i0);
+		if (i0 + 16 < RVC_T)
+			ld (a0, a1, a2, i0 + 16);
+		run (b0, b1, b2, i0 + 8);
+	}
+	PRIO_DOWN ();
+}
+
 struct RvPreLds {
 	double   x[2][RVC_NC][RVC_S]; /* predelayed input -> biquadA output, in place */
 	uint32_t f[2][RVC_NC][RVC_S]; /* fpdL / fpdR of the sample delayM back (the predelay's input guard) */
@@ -2322,7 +2480,8 @@ k_rv_pre (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 				double    x = (double)qIn[t];
 				if (fabs (x) < 1.18e-23)
 					x = sm.f[b][r][n] * 1.18e-17;
-				sm.x[b][r][n] = age[t] + it * RVC_T + n >= dM[t] ? x : 0.0;
+				const double xv = age[t] + it * RVC_T + n >= dM[t] ? x : 0.0;
+				sm.x[b][r][n] = xv;
 			}
 		}
 		/* HBM reads of tile it + 2 into the set just consumed (clamped past the last tile:
@@ -2379,21 +2538,50 @@ k_rv_pre (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 #ifndef RVP_CB
 #define RVP_CB 16 /* 256 workgroups: all CUs (32 per workgroup: step 129.7 -> 127.5 ms at 16, profiles/r05/s37) */
 #endif
+#ifndef RVP_PROF
+#define RVP_PROF 0 /* profiling variant (never the product): s_memtime work / barrier clocks per role (tools/rvp_prof.py) */
+#endif
+#if RVP_PROF /* workgroup 0's serial, dither and first helper waves write k cycles over instance 0's first outputs (tap chain) */
+#define RVP_PROF_DECL() unsigned long long pw_ = 0, pb_ = 0, pa_ = 0, pc_ = 0
+#define RVP_T0() pa_ = __builtin_amdgcn_s_memtime ()
+#define RVP_T1() { asm volatile ("" ::: "memory"); pc_ = __builtin_amdgcn_s_memtime (); pw_ += pc_ - pa_; }
+#define RVP_T2() { asm volatile ("" ::: "memory"); pb_ += __builtin_amdgcn_s_memtime () - pc_; }
+#define RVP_PROF_OUT(i) { if (blockIdx.x == 0 && lane == 0) { P.outL[P.outOffset + (i)] = (float)(pw_ * 1e-3); P.outL[P.outOffset + (i) + 1] = (float)(pb_ * 1e-3); } }
+#else
+#define RVP_PROF_DECL()
+#define RVP_T0()
+#define RVP_T1()
+#define RVP_T2()
+#define RVP_PROF_OUT(i)
+#endif
 #define RVP_NC (2 * RVP_CB)
 #define RVP_ROWS (RVP_NC + (RVP_NC < NL)) /* chain rows, + one that the idle chain lanes use */
 #define RVP_NTK (RVP_CB / RVC_H)
 static_assert (RVP_CB % RVC_H == 0 && RVP_NC <= NL, "k_rv_post chain-block geometry");
 
+#ifndef RVP_SPLIT
+#define RVP_SPLIT 1 /* biquadB and biquadC chains on waves of their own, the x-products precomputed by the helpers */
+#endif
+#define RVP_SER (RVP_SPLIT ? 2 : 1)                 /* serial chain waves */
+#define RVP_THREADS (NL * (RVP_SER + 1 + RVC_H))    /* + the dither wave and the helpers */
+
 struct RvPostLds {
-	double   y[2][RVP_ROWS][RVC_S]; /* tap mix -> biquadB output, in place */
-	double   z[2][RVP_ROWS][RVC_S]; /* asin output -> biquadC output, in place */
+	double   y[2][RVP_ROWS][RVC_S]; /* tap mix -> biquadB output, in place (RVP_SPLIT: x c0 -> output) */
+	double   z[2][RVP_ROWS][RVC_S]; /* asin output -> biquadC output, in place (RVP_SPLIT: x c0 -> output) */
+#if RVP_SPLIT
+	double   y1[2][RVP_ROWS][RVC_S], y2[2][RVP_ROWS][RVC_S]; /* x c1, x c2 of the tap mix */
+	double   z1[2][RVP_ROWS][RVC_S], z2[2][RVP_ROWS][RVC_S]; /* x c1, x c2 of the asin output */
+#endif
 	uint32_t f[2][RVP_ROWS][RVC_S]; /* fpdL / fpdR before each sample (entry RVC_T: after the tile) */
 };
 
 /* biquadB, clamp + asin, biquadC, dry mix, dither, (L + R) / sqrt 2 (src/reverb.cpp:733-787)
  * -> mid2.  A tile is loaded at iteration k (its HBM reads issued at k - 2), biquadB at
- * k + 1, asin at k + 2, biquadC at k + 3, output at k + 4. */
-__global__ void __launch_bounds__ (RVC_THREADS)
+ * k + 1, asin at k + 2, biquadC at k + 3, output at k + 4.  RVP_SPLIT: wave 0 runs the
+ * biquadB chains, wave 1 the biquadC chains (one chain per lane each; one wave with both
+ * interleaved was the kernel's bound, 4.2 k cycles an iteration against 1.4 k for the
+ * helpers), wave 2 the dither streams, and the helpers write each input's three products. */
+__global__ void __launch_bounds__ (RVP_THREADS)
 k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_seg_ctl* __restrict__ ctl)
 {
 	__shared__ RvPostLds sm;
@@ -2408,6 +2596,39 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 	const bool    cok = cj < nj;
 	const int     crow = lane < RVP_NC ? lane : RVP_NC; /* chain lanes past the block's chains: the idle row */
 	tbf_rv_state* CS  = &P.st[inst0 + (cok ? cj : 0)].rv;
+#if RVP_SPLIT
+	if (w < 2) {
+		/* w 0: biquadB of tile it - 1 (rows y); w 1: biquadC of tile it - 3 (rows z) */
+		const tbf_inst_const& K  = cst[inst0 + (cok ? cj : 0)];
+		const int             q  = w + 1;
+		const double          c3 = K.bq[q][3], c4 = K.bq[q][4];
+		double                s7 = CS->bq[q][2 * cc], s8 = CS->bq[q][2 * cc + 1];
+		__syncthreads ();
+		RVP_PROF_DECL ();
+#pragma unroll 1
+		for (int it = 0; it < nIt; it++) {
+			RVP_T0 ();
+			const int tile = it - 1 - 2 * w;
+			if (tile >= 0 && tile < nT) {
+				const int pb = (it - 1) & 1;
+				if (w == 0)
+					rvc_serial_p (sm.y[pb][crow], sm.y1[pb][crow], sm.y2[pb][crow], c3, c4, s7, s8);
+				else
+					rvc_serial_p (sm.z[pb][crow], sm.z1[pb][crow], sm.z2[pb][crow], c3, c4, s7, s8);
+			}
+			RVP_T1 ();
+			__syncthreads ();
+			RVP_T2 ();
+		}
+		if (w == 0)
+			RVP_PROF_OUT (0);
+		if (cok) {
+			CS->bq[q][2 * cc]     = s7;
+			CS->bq[q][2 * cc + 1] = s8;
+		}
+		return;
+	}
+#else
 	if (w == 0) {
 		/* biquadB of tile it - 1 and biquadC of tile it - 3, two chains per lane in one
 		 * instruction stream */
@@ -2416,8 +2637,10 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 		                        {K.bq[2][0], K.bq[2][1], K.bq[2][2], K.bq[2][3], K.bq[2][4]}};
 		double s[2][2] = {{CS->bq[1][2 * cc], CS->bq[1][2 * cc + 1]}, {CS->bq[2][2 * cc], CS->bq[2][2 * cc + 1]}};
 		__syncthreads ();
+		RVP_PROF_DECL ();
 #pragma unroll 1
 		for (int it = 0; it < nIt; it++) {
+			RVP_T0 ();
 			const bool doB = it >= 1 && it - 1 < nT, doC = it >= 3 && it - 3 < nT;
 			double*    rb  = sm.y[(it - 1) & 1][crow];
 			double*    rc  = sm.z[(it - 1) & 1][crow];
@@ -2439,8 +2662,11 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 				s[1][0] = s1[0][0];
 				s[1][1] = s1[0][1];
 			}
+			RVP_T1 ();
 			__syncthreads ();
+			RVP_T2 ();
 		}
+		RVP_PROF_OUT (0);
 		if (cok) {
 			CS->bq[1][2 * cc]     = s[0][0];
 			CS->bq[1][2 * cc + 1] = s[0][1];
@@ -2449,15 +2675,21 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 		}
 		return;
 	}
-	if (w == 1) {
+#endif
+	if (w == RVP_SER) {
 		uint32_t fs = cc ? CS->fpdR2 : CS->fpdL2;
 		__syncthreads ();
+		RVP_PROF_DECL ();
 #pragma unroll 1
 		for (int it = 0; it < nIt; it++) {
+			RVP_T0 ();
 			if (it >= 3 && it - 3 < nT)
 				rvc_dither_row (sm.f[(it - 3) & 1][crow], fs);
+			RVP_T1 ();
 			__syncthreads ();
+			RVP_T2 ();
 		}
+		RVP_PROF_OUT (4);
 		if (cok) {
 			if (cc)
 				CS->fpdR2 = fs;
@@ -2469,12 +2701,15 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 	/* helpers: HBM reads two tiles ahead into two register sets alternating by iteration
 	 * parity (see k_rv_pre) */
 	const bool   tap = P.chain == TBF_CHAIN_TAP_REVERB;
-	const int    h = w - 2, hc = lane >> 5, n = lane & (RVC_T - 1);
+	const int    h = w - RVP_SER - 1, hc = lane >> 5, n = lane & (RVC_T - 1);
 	double       pB[2][RVP_NTK], wetv[RVP_NTK];
 	float        pIn[2][RVP_NTK];
 	const double* rb[RVP_NTK];
 	const float*  in[RVP_NTK];
 	float*        out[RVP_NTK];
+#if RVP_SPLIT
+	double       cB[RVP_NTK][3], cC[RVP_NTK][3]; /* the task's biquadB / biquadC input coefficients c0 c1 c2 */
+#endif
 #pragma unroll
 	for (int t = 0; t < RVP_NTK; t++) {
 		const int      j    = h + t * RVC_H;
@@ -2487,9 +2722,17 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 		pB[0][t]  = rb[t][0];
 		pB[1][t]  = rb[t][(size_t)min (1, nT - 1) * RVC_T];
 		pIn[0][t] = pIn[1][t] = 0.f;
+#if RVP_SPLIT
+		for (int k = 0; k < 3; k++) {
+			cB[t][k] = cst[inst].bq[1][k];
+			cC[t][k] = cst[inst].bq[2][k];
+		}
+#endif
 	}
 	__syncthreads ();
+	RVP_PROF_DECL ();
 	auto step = [&] (const int it, double (&qB)[RVP_NTK], float (&qIn)[RVP_NTK]) {
+		RVP_T0 ();
 		const int b = it & 1; /* tiles it, it - 2 and it - 4 share the buffers */
 		/* output of tile it - 4: dry mix, dither, mono sum (src/reverb.cpp:766-787); the
 		 * half-waves hold L and R, and 0.7071 (L + R) == 0.7071 (R + L) */
@@ -2520,8 +2763,16 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 			av[t] = sm.y[b][2 * (h + t * RVC_H) + hc][n];
 		if (it < nT) {
 #pragma unroll
-			for (int t = 0; t < RVP_NTK; t++)
-				sm.y[b][2 * (h + t * RVC_H) + hc][n] = qB[t];
+			for (int t = 0; t < RVP_NTK; t++) {
+				const int r = 2 * (h + t * RVC_H) + hc;
+#if RVP_SPLIT
+				sm.y[b][r][n]  = qB[t] * cB[t][0];
+				sm.y1[b][r][n] = qB[t] * cB[t][1];
+				sm.y2[b][r][n] = qB[t] * cB[t][2];
+#else
+				sm.y[b][r][n] = qB[t];
+#endif
+			}
 		}
 		/* HBM reads into the set just consumed (indices clamped, so the loads need no
 		 * branch): the tap mix of tile it + 2, the dry input of tile it - 2 (output at
@@ -2546,14 +2797,26 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 			}
 			/* every task's value inside OCML asin's polynomial branch (the tap mix is small):
 			 * that branch alone, straight-line, so the tasks' chains interleave (tbf_sin.h) */
+			double as[RVP_NTK];
 			if (__all (small)) {
 #pragma unroll
 				for (int t = 0; t < RVP_NTK; t++)
-					sm.z[b][2 * (h + t * RVC_H) + hc][n] = tbf_asin_poly (y[t]);
+					as[t] = tbf_asin_poly (y[t]);
 			} else {
 #pragma unroll
 				for (int t = 0; t < RVP_NTK; t++)
-					sm.z[b][2 * (h + t * RVC_H) + hc][n] = asin (y[t]);
+					as[t] = asin (y[t]);
+			}
+#pragma unroll
+			for (int t = 0; t < RVP_NTK; t++) {
+				const int r = 2 * (h + t * RVC_H) + hc;
+#if RVP_SPLIT
+				sm.z[b][r][n]  = as[t] * cC[t][0];
+				sm.z1[b][r][n] = as[t] * cC[t][1];
+				sm.z2[b][r][n] = as[t] * cC[t][2];
+#else
+				sm.z[b][r][n] = as[t];
+#endif
 			}
 		}
 		if (it >= 4) {
@@ -2563,7 +2826,9 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 				if (h + t * RVC_H < nj && (tap || hc == 0))
 					out[t][so] = yv[t];
 		}
+		RVP_T1 ();
 		__syncthreads ();
+		RVP_T2 ();
 	};
 #pragma unroll 1
 	for (int it = 0; it < nIt; it += 2) {
@@ -2571,6 +2836,8 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 		if (it + 1 < nIt)
 			step (it + 1, pB[1], pIn[1]);
 	}
+	if (h == 0)
+		RVP_PROF_OUT (8);
 }
 
 /* ================================================================== k_whirl */
@@ -2681,82 +2948,6 @@ __device__ void whirl_speed (tbf_wh_state& st, const tbf_inst_const& K, int revO
 	st.drumTarget = drumTarget;
 	st.hornAcDc   = hornAcDc;
 	st.drumAcDc   = drumAcDc;
-}
-
-/* One motion's ordered adds into a ring for a 64-sample sub-block (HN_MOTION /
- * DR_MOTION, src/whirl.cpp:1432-1469): sample n adds a_n into slot U_n and b_n into
- * slot U_n + 1, in sample order.  With U non-decreasing, the samples sharing a slot
- * value form a group G(u) and slot t receives, in order, b of G(t-1) then a of G(t).
- * Groups have at most 2 samples (checked by the caller), so the first lane of each
- * group owns slot t = U (and slot t + 1 when no group sits at t + 1) and finds its
- * neighbours' terms with lane shifts; owners never share a slot. */
-/* the owner lanes' slots and ordered sums of one motion (see motion_add) */
-struct MotionOwn {
-	bool     first, own2, pair, lead, lead2;
-	uint32_t t;
-	float    a, an, b, bn, bp1, bp2;
-};
-
-__device__ __forceinline__ MotionOwn motion_own (int U, float a, float b, int lane)
-{
-	MotionOwn m;
-	const int Up  = lane_shr1 (U);
-	const int Up2 = lane_shr1 (Up);
-	const int Un  = lane_shl1 (U);
-	const int Un2 = lane_shl1 (Un);
-	m.bp1         = lane_shr1 (b);
-	m.bp2         = lane_shr1 (m.bp1);
-	m.an          = lane_shl1 (a);
-	m.bn          = lane_shl1 (b);
-	m.a           = a;
-	m.b           = b;
-	m.t           = (uint32_t)U;
-	m.first       = lane == 0 || U != Up;
-	m.pair        = lane < NL - 1 && Un == U;
-	m.lead        = lane > 0 && Up == U - 1;
-	m.lead2       = lane > 1 && Up2 == Up;
-	const bool nextExists = m.pair ? lane < NL - 2 : lane < NL - 1;
-	const int  Unx        = m.pair ? Un2 : Un;
-	m.own2                = !nextExists || Unx != U + 1;
-	return m;
-}
-
-/* slot t: b of the group at t-1 (<= 2 samples, in order), then a of the group at t.  A
- * skipped add keeps v (v + 0 is not v for v = -0), so each optional add is a select of the
- * sum, not a branch: the passes stay branch-free */
-__device__ __forceinline__ float motion_sum_t (const MotionOwn& m, float v)
-{
-	float t = v + m.bp2;
-	v       = (m.lead && m.lead2) ? t : v;
-	t       = v + m.bp1;
-	v       = m.lead ? t : v;
-	v += m.a;
-	t = v + m.an;
-	return m.pair ? t : v;
-}
-
-/* slot t + 1 when no group sits there: b of this group */
-__device__ __forceinline__ float motion_sum_t1 (const MotionOwn& m, float w)
-{
-	w += m.b;
-	const float t = w + m.bn;
-	return m.pair ? t : w;
-}
-
-template <int W>
-__device__ __forceinline__ void motion_add (float* ring, int U, float a, float b, int lane)
-{
-	const uint32_t  WM = (uint32_t)W - 1u;
-	const MotionOwn m  = motion_own (U, a, b, lane);
-	if (m.first) {
-		/* both slots read before either is written (one LDS round trip): an owner's
-		 * slot t+1 is read but left alone when another group owns it */
-		const uint32_t i0 = m.t & WM, i1 = (m.t + 1) & WM;
-		const float    v = ring[i0], w = ring[i1];
-		ring[i0]         = motion_sum_t (m, v);
-		if (m.own2)
-			ring[i1] = motion_sum_t1 (m, w);
-	}
 }
 
 /* One pass of motion_add over a group of RG rings (motion q of each): every lane reads its
@@ -4006,7 +4197,7 @@ extern "C" int tbf_launch_stage (const tbf_launch* P, int k, hipStream_t stream)
 		} else
 			hipLaunchKernelGGL (k_rv_core, dim3 (2 * P->nInst), block, 0, stream, *P, P->cst);
 	else if (k == 4)
-		hipLaunchKernelGGL (k_rv_post, dim3 ((P->nInst + RVP_CB - 1) / RVP_CB), cblock, 0, stream, *P, P->cst, P->ctl);
+		hipLaunchKernelGGL (k_rv_post, dim3 ((P->nInst + RVP_CB - 1) / RVP_CB), dim3 (RVP_THREADS), 0, stream, *P, P->cst, P->ctl);
 	else if (k == 5) {
 		if (P->whSplit) {
 			const dim3 sblock (2 * NL);

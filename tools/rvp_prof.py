@@ -28,11 +28,15 @@ def main():
     for _ in range(3):
         eng.render_device(nb, L.data_ptr(), R.data_ptr(), nb * 128)
         eng.synchronize()
-    v = L[0, :10].cpu().numpy()
+    v = L[0, :64].cpu().numpy()
     it = nb * 4 + 4
     print(f"k_rv_post per iteration (cycles), {it} iterations:")
     for name, o in (("serial", 0), ("dither", 4), ("helper0", 8)):
         print(f"  {name:8s} work {v[o] * 1e3 / it:8.0f}  barrier {v[o + 1] * 1e3 / it:8.0f}")
+    print("every wave of workgroup 0 (wave: work / barrier cycles per iteration, SIMD):")
+    for w in range(11):
+        b = 16 + 3 * w
+        print(f"  wave {w:2d}: {v[b] * 1e3 / it:8.0f} / {v[b + 1] * 1e3 / it:8.0f}  SIMD {v[b + 2]:.0f}")
 
 
 if __name__ == "__main__":

@@ -1128,6 +1128,7 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 		if (blockIdx.x == 0 && lane == 0) {
 			P.outL[P.outOffset + 8] = (float)(sw0 * 1e-3);
 			P.outL[P.outOffset + 9] = (float)(sb0 * 1e-3);
+			P.outL[P.outOffset + 10] = (float)((__builtin_amdgcn_s_getreg ((31 << 11) | 4) >> 4) & 3);
 		}
 #endif
 		if (ok) {
@@ -1201,6 +1202,7 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 		if (blockIdx.x == 0 && lane == 0) {
 			P.outL[P.outOffset + 16] = (float)(dw0 * 1e-3);
 			P.outL[P.outOffset + 17] = (float)(db0 * 1e-3);
+			P.outL[P.outOffset + 18] = (float)((__builtin_amdgcn_s_getreg ((31 << 11) | 4) >> 4) & 3);
 		}
 #endif
 		if (ok && pre && lane < MP_CB)
@@ -1356,6 +1358,11 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 	if (blockIdx.x == 0 && h == 0 && lane == 0)
 		for (int i = 0; i < 3; i++)
 			P.outL[P.outOffset + i] = (float)(pf[i] * 1e-3);
+	if (blockIdx.x == 0 && lane == 0) { /* every helper: its sections and its SIMD (HW_ID bits 5:4) */
+		for (int i = 0; i < 3; i++)
+			P.outL[P.outOffset + 32 + 4 * h + i] = (float)(pf[i] * 1e-3);
+		P.outL[P.outOffset + 32 + 4 * h + 3] = (float)((__builtin_amdgcn_s_getreg ((31 << 11) | 4) >> 4) & 3);
+	}
 #endif
 #undef MP_T0
 #undef MP_TS
@@ -2546,7 +2553,10 @@ k_rv_pre (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 #define RVP_T0() pa_ = __builtin_amdgcn_s_memtime ()
 #define RVP_T1() { asm volatile ("" ::: "memory"); pc_ = __builtin_amdgcn_s_memtime (); pw_ += pc_ - pa_; }
 #define RVP_T2() { asm volatile ("" ::: "memory"); pb_ += __builtin_amdgcn_s_memtime () - pc_; }
-#define RVP_PROF_OUT(i) { if (blockIdx.x == 0 && lane == 0) { P.outL[P.outOffset + (i)] = (float)(pw_ * 1e-3); P.outL[P.outOffset + (i) + 1] = (float)(pb_ * 1e-3); } }
+#define RVP_PROF_OUT(i) { if (blockIdx.x == 0 && lane == 0) { \
+	if ((i) >= 0) { P.outL[P.outOffset + (i)] = (float)(pw_ * 1e-3); P.outL[P.outOffset + (i) + 1] = (float)(pb_ * 1e-3); } \
+	P.outL[P.outOffset + 16 + 3 * w] = (float)(pw_ * 1e-3); P.outL[P.outOffset + 17 + 3 * w] = (float)(pb_ * 1e-3); \
+	P.outL[P.outOffset + 18 + 3 * w] = (float)((__builtin_amdgcn_s_getreg ((31 << 11) | 4) >> 4) & 3); } }
 #else
 #define RVP_PROF_DECL()
 #define RVP_T0()
@@ -2620,8 +2630,7 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 			__syncthreads ();
 			RVP_T2 ();
 		}
-		if (w == 0)
-			RVP_PROF_OUT (0);
+		RVP_PROF_OUT (w == 0 ? 0 : -1);
 		if (cok) {
 			CS->bq[q][2 * cc]     = s7;
 			CS->bq[q][2 * cc + 1] = s8;
@@ -2836,8 +2845,7 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 		if (it + 1 < nIt)
 			step (it + 1, pB[1], pIn[1]);
 	}
-	if (h == 0)
-		RVP_PROF_OUT (8);
+	RVP_PROF_OUT (h == 0 ? 8 : -1);
 }
 
 /* ================================================================== k_whirl */

@@ -42,9 +42,6 @@
 #ifndef TG_LDS_ALL
 #define TG_LDS_ALL 1 /* entries staged in LDS for steady chunks too (their per-block scalar loads: 21.8 -> 18.8 ms with TG_CACHE) */
 #endif
-#ifndef TG_SCAN_PASS
-#define TG_SCAN_PASS 1 /* the vibrato scanner's scatter as two ordered-add passes (stage_tonegen) */
-#endif
 #ifndef TG_ABL
 #define TG_ABL 0 /* timing experiments (wrong output): 1 bank reads from one row, 2 no scanner */
 #endif
@@ -593,7 +590,6 @@ __device__ __forceinline__ void stage_tonegen (const tbf_launch& P, TgLds& sm, c
 			sm.u.v.vh[n] = n + (int)(((uint32_t)h - op) & 0x3FFu); /* slot offset from out0 */
 		}
 		wave_sync ();
-#if TG_SCAN_PASS
 		/* The scatter as two passes of ordered adds (motion_add, the whirl rings' owner
 		 * scheme): sample m adds x - g into slot out0 + vh[m] and g into the slot after, in
 		 * sample order; for non-decreasing slots with groups of <= 2 equal slots in a pass,
@@ -630,45 +626,6 @@ __device__ __forceinline__ void stage_tonegen (const tbf_launch& P, TgLds& sm, c
 				sm.u.v.vout[wo]     = G.vibMixed ? (x + v) * (float)0.7071067811865475 : v;
 				st.vring[slot]      = 0.f;
 			}
-#else
-		/* ordered gather: slot W_o collects, in sample order, x-g from samples with
-		 * H==W_o and g from samples with H+1==W_o; valid while H is non-decreasing and
-		 * within 32 ahead (checked; lane 0 replays serially otherwise) */
-		int bad = 0, dmn = 1 << 20, dmx = -(1 << 20);
-		for (int k = 0; k < 2; k++) {
-			const int n = lane + k * NL;
-			const int d = sm.u.v.vh[n] - n;
-			if (d < 1 || d > 31) bad = 1;
-			if (n > 0 && sm.u.v.vh[n] < sm.u.v.vh[n - 1]) bad = 1;
-			dmn = min (dmn, d);
-			dmx = max (dmx, d);
-		}
-		bad = __any (bad) || (P.dbg & TBF_DEBUG_FORCE_SERIAL);
-		dmn = wave_min (dmn);
-		dmx = wave_max (dmx);
-		if (!bad) {
-			/* sample m reaches slot wo iff m + d_m is wo or wo - 1: m in [wo-1-dmax, wo-dmin] */
-			for (int wo = lane; wo < TBF_BLK + 32; wo += NL) {
-				const uint32_t slot = (out0 + wo) & (TBF_VRING - 1);
-				float          v    = st.vring[slot];
-				const int      m0   = wo - 1 - dmx < 0 ? 0 : wo - 1 - dmx;
-				const int      m1   = wo - dmn > TBF_BLK - 1 ? TBF_BLK - 1 : wo - dmn;
-				for (int m = m0; m <= m1; m++) {
-					const int hm = sm.u.v.vh[m];
-					if (hm == wo)
-						v += sm.u.v.va[m];
-					else if (hm + 1 == wo)
-						v += sm.u.v.vg[m];
-				}
-				if (wo < TBF_BLK) {
-					const float x     = sm.vin[wo];
-					sm.u.v.vout[wo]   = G.vibMixed ? (x + v) * (float)0.7071067811865475 : v;
-					st.vring[slot]    = 0.f;
-				} else {
-					st.vring[slot] = v;
-				}
-			}
-#endif
 		} else {
 			if (lane == 0) {
 				atomicOr (P.errFlags, (uint32_t)TBF_PATH_VIB_SERIAL);
@@ -845,6 +802,10 @@ k_tonegen (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl, const tbf_tp
 #ifndef MP_SIN_PAIRS
 #define MP_SIN_PAIRS 0 /* the density sines in pairs (tbf_sin2) instead of one vote for all tasks */
 #endif
+#ifndef MP_PRIO
+#define MP_PRIO 0 /* the helpers raise their priority at the waveshaper's start and drop it after density
+                   * step MP_PRIO - 1, so the two helpers of a SIMD progress together instead of in age order */
+#endif
 #ifndef MP_WIDE
 #define MP_WIDE 1 /* tiles of 64 samples, a helper task = one instance (0: 32, an instance pair) */
 #endif
@@ -961,7 +922,14 @@ __device__ __forceinline__ void preamp_shape_n (const double (&x0)[NT], const do
 		dpos = dpos && (C[t]->flags & MPF_DPOS);
 	}
 	const int itw = wave_max (itm);
+#if MP_PRIO
+	__builtin_amdgcn_s_setprio (1);
+#endif
 	for (int c = 0; c < itw; c++) {
+#if MP_PRIO
+		if (c == MP_PRIO)
+			__builtin_amdgcn_s_setprio (0);
+#endif
 		double br[NT];
 #pragma unroll
 		for (int t = 0; t < NT; t++) {
@@ -981,6 +949,9 @@ __device__ __forceinline__ void preamp_shape_n (const double (&x0)[NT], const do
 			if (c < C[t]->iter)
 				x[t] = (x[t] > 0.0) ? br[t] : -br[t];
 	}
+#if MP_PRIO
+	__builtin_amdgcn_s_setprio (0);
+#endif
 	double br[NT];
 #pragma unroll
 	for (int t = 0; t < NT; t++) {
@@ -1744,6 +1715,11 @@ __device__ __forceinline__ void rvl_write (double* rg, int i, int d, double v)
 #ifndef RVL_FAST2
 #define RVL_FAST2 1 /* tap index without the FP64 sum (a vote on the rare carry), allpass products as fmas (exact) */
 #endif
+#ifndef RVL_PRIO
+#define RVL_PRIO 0 /* workers raise their priority at a phase start and drop it part-way, so the three workers
+                    * of a SIMD progress together instead of in age order (1: drop after the tap reads, 2: after
+                    * the Householder mix) */
+#endif
 #ifndef RVL_SCAL
 #define RVL_SCAL 1 /* the workers' line counters in scalar registers, wraps as scalar branches (below) */
 #endif
@@ -1993,6 +1969,9 @@ __device__ __forceinline__ void rvl_pair (const tbf_launch& P, const tbf_inst_co
 			if (pst)
 				rv_st (&bout[po], pmix);
 			if (act) {
+#if RVL_PRIO
+				__builtin_amdgcn_s_setprio (1);
+#endif
 				/* the lines' vibrato sines: closed form on every line (wave-uniform, the rule), or
 				 * per line the closed form or the literal recurrence and sin */
 				const uint32_t om = __builtin_amdgcn_readfirstlane (sm.okm[par][w]);
@@ -2074,6 +2053,9 @@ __device__ __forceinline__ void rvl_pair (const tbf_launch& P, const tbf_inst_co
 					r0[l]            = rg[wk[l]];
 					r1[l]            = rg[wk[l] + 1];
 				}
+#if RVL_PRIO == 1
+				__builtin_amdgcn_s_setprio (0);
+#endif
 #pragma unroll
 				for (int l = 0; l < 8; l++) {
 					double x = (r0[l] * (1 - fr[l]));
@@ -2091,6 +2073,9 @@ __device__ __forceinline__ void rvl_pair (const tbf_launch& P, const tbf_inst_co
 				fb[6] = (I[6] - (I[4] + I[5] + I[7])) * K.regen;
 				fb[7] = (I[7] - (I[4] + I[5] + I[6])) * K.regen;
 				mix = (I[0] + I[1] + I[2] + I[3] + I[4] + I[5] + I[6] + I[7]) / 8.0;
+#if RVL_PRIO == 2
+				__builtin_amdgcn_s_setprio (0);
+#endif
 #pragma unroll
 				for (int l = 8; l < 12; l++) {
 					const double old = sm.ring[RVL_LOFS[l] + RVL_C (l) + n + 1]; /* <= d + 64: mirror */
@@ -2120,6 +2105,9 @@ __device__ __forceinline__ void rvl_pair (const tbf_launch& P, const tbf_inst_co
 			__syncthreads ();
 			/* ---- write phase ---- */
 			if (act) {
+#if RVL_PRIO
+				__builtin_amdgcn_s_setprio (1);
+#endif
 				/* the previous sub-block's last feedback, all 8 lines read before any ring write */
 				const double* cp = w == 0 ? sm.carry[par ^ 1][RVL_G - 1] : sm.carry[par][w - 1];
 				double        cprv[8];
@@ -2134,6 +2122,9 @@ __device__ __forceinline__ void rvl_pair (const tbf_launch& P, const tbf_inst_co
 				/* feedback (n - 1): lane 0 takes the previous sub-block's last, the DPP move's old value */
 				rvl_write_s<RVL_DLY[0]> (sm.ring + RVL_LOFS[0], cs[0], n, ap[3] + lane_shr1_or (fb[0], cprv[0]));
 				rvl_write_s<RVL_DLY[1]> (sm.ring + RVL_LOFS[1], cs[1], n, ap[2] + lane_shr1_or (fb[1], cprv[1]));
+#if RVL_PRIO
+				__builtin_amdgcn_s_setprio (0);
+#endif
 				rvl_write_s<RVL_DLY[2]> (sm.ring + RVL_LOFS[2], cs[2], n, ap[1] + lane_shr1_or (fb[2], cprv[2]));
 				rvl_write_s<RVL_DLY[3]> (sm.ring + RVL_LOFS[3], cs[3], n, ap[0] + lane_shr1_or (fb[3], cprv[3]));
 				rvl_write_s<RVL_DLY[4]> (sm.ring + RVL_LOFS[4], cs[4], n, ap[0] + lane_shr1_or (fb[4], cprv[4]));
@@ -2564,30 +2555,28 @@ k_rv_pre (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 #define RVP_T2()
 #define RVP_PROF_OUT(i)
 #endif
+#ifndef RVP_H
+#define RVP_H 8 /* helper waves */
+#endif
 #define RVP_NC (2 * RVP_CB)
 #define RVP_ROWS (RVP_NC + (RVP_NC < NL)) /* chain rows, + one that the idle chain lanes use */
-#define RVP_NTK (RVP_CB / RVC_H)
-static_assert (RVP_CB % RVC_H == 0 && RVP_NC <= NL, "k_rv_post chain-block geometry");
+#define RVP_NTK (RVP_CB / RVP_H)
+static_assert (RVP_CB % RVP_H == 0 && RVP_NC <= NL, "k_rv_post chain-block geometry");
 
-#ifndef RVP_SPLIT
-#define RVP_SPLIT 1 /* biquadB and biquadC chains on waves of their own, the x-products precomputed by the helpers */
-#endif
-#define RVP_SER (RVP_SPLIT ? 2 : 1)                 /* serial chain waves */
-#define RVP_THREADS (NL * (RVP_SER + 1 + RVC_H))    /* + the dither wave and the helpers */
+#define RVP_SER 2                                   /* serial chain waves (biquadB, biquadC) */
+#define RVP_THREADS (NL * (RVP_SER + 1 + RVP_H))    /* + the dither wave and the helpers */
 
 struct RvPostLds {
-	double   y[2][RVP_ROWS][RVC_S]; /* tap mix -> biquadB output, in place (RVP_SPLIT: x c0 -> output) */
-	double   z[2][RVP_ROWS][RVC_S]; /* asin output -> biquadC output, in place (RVP_SPLIT: x c0 -> output) */
-#if RVP_SPLIT
+	double   y[2][RVP_ROWS][RVC_S]; /* tap mix x c0 -> biquadB output, in place */
+	double   z[2][RVP_ROWS][RVC_S]; /* asin output x c0 -> biquadC output, in place */
 	double   y1[2][RVP_ROWS][RVC_S], y2[2][RVP_ROWS][RVC_S]; /* x c1, x c2 of the tap mix */
 	double   z1[2][RVP_ROWS][RVC_S], z2[2][RVP_ROWS][RVC_S]; /* x c1, x c2 of the asin output */
-#endif
 	uint32_t f[2][RVP_ROWS][RVC_S]; /* fpdL / fpdR before each sample (entry RVC_T: after the tile) */
 };
 
 /* biquadB, clamp + asin, biquadC, dry mix, dither, (L + R) / sqrt 2 (src/reverb.cpp:733-787)
  * -> mid2.  A tile is loaded at iteration k (its HBM reads issued at k - 2), biquadB at
- * k + 1, asin at k + 2, biquadC at k + 3, output at k + 4.  RVP_SPLIT: wave 0 runs the
+ * k + 1, asin at k + 2, biquadC at k + 3, output at k + 4.  Wave 0 runs the
  * biquadB chains, wave 1 the biquadC chains (one chain per lane each; one wave with both
  * interleaved was the kernel's bound, 4.2 k cycles an iteration against 1.4 k for the
  * helpers), wave 2 the dither streams, and the helpers write each input's three products. */
@@ -2606,7 +2595,6 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 	const bool    cok = cj < nj;
 	const int     crow = lane < RVP_NC ? lane : RVP_NC; /* chain lanes past the block's chains: the idle row */
 	tbf_rv_state* CS  = &P.st[inst0 + (cok ? cj : 0)].rv;
-#if RVP_SPLIT
 	if (w < 2) {
 		/* w 0: biquadB of tile it - 1 (rows y); w 1: biquadC of tile it - 3 (rows z) */
 		const tbf_inst_const& K  = cst[inst0 + (cok ? cj : 0)];
@@ -2637,54 +2625,6 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 		}
 		return;
 	}
-#else
-	if (w == 0) {
-		/* biquadB of tile it - 1 and biquadC of tile it - 3, two chains per lane in one
-		 * instruction stream */
-		const tbf_inst_const& K = cst[inst0 + (cok ? cj : 0)];
-		const double c[2][5] = {{K.bq[1][0], K.bq[1][1], K.bq[1][2], K.bq[1][3], K.bq[1][4]},
-		                        {K.bq[2][0], K.bq[2][1], K.bq[2][2], K.bq[2][3], K.bq[2][4]}};
-		double s[2][2] = {{CS->bq[1][2 * cc], CS->bq[1][2 * cc + 1]}, {CS->bq[2][2 * cc], CS->bq[2][2 * cc + 1]}};
-		__syncthreads ();
-		RVP_PROF_DECL ();
-#pragma unroll 1
-		for (int it = 0; it < nIt; it++) {
-			RVP_T0 ();
-			const bool doB = it >= 1 && it - 1 < nT, doC = it >= 3 && it - 3 < nT;
-			double*    rb  = sm.y[(it - 1) & 1][crow];
-			double*    rc  = sm.z[(it - 1) & 1][crow];
-			if (doB && doC) {
-				double* const row[2] = {rb, rc};
-				rvc_serial<2> (row, c, s);
-			} else if (doB) {
-				double* const row[1] = {rb};
-				const double  c1[1][5] = {{c[0][0], c[0][1], c[0][2], c[0][3], c[0][4]}};
-				double        s1[1][2] = {{s[0][0], s[0][1]}};
-				rvc_serial<1> (row, c1, s1);
-				s[0][0] = s1[0][0];
-				s[0][1] = s1[0][1];
-			} else if (doC) {
-				double* const row[1] = {rc};
-				const double  c1[1][5] = {{c[1][0], c[1][1], c[1][2], c[1][3], c[1][4]}};
-				double        s1[1][2] = {{s[1][0], s[1][1]}};
-				rvc_serial<1> (row, c1, s1);
-				s[1][0] = s1[0][0];
-				s[1][1] = s1[0][1];
-			}
-			RVP_T1 ();
-			__syncthreads ();
-			RVP_T2 ();
-		}
-		RVP_PROF_OUT (0);
-		if (cok) {
-			CS->bq[1][2 * cc]     = s[0][0];
-			CS->bq[1][2 * cc + 1] = s[0][1];
-			CS->bq[2][2 * cc]     = s[1][0];
-			CS->bq[2][2 * cc + 1] = s[1][1];
-		}
-		return;
-	}
-#endif
 	if (w == RVP_SER) {
 		uint32_t fs = cc ? CS->fpdR2 : CS->fpdL2;
 		__syncthreads ();
@@ -2716,12 +2656,10 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 	const double* rb[RVP_NTK];
 	const float*  in[RVP_NTK];
 	float*        out[RVP_NTK];
-#if RVP_SPLIT
 	double       cB[RVP_NTK][3], cC[RVP_NTK][3]; /* the task's biquadB / biquadC input coefficients c0 c1 c2 */
-#endif
 #pragma unroll
 	for (int t = 0; t < RVP_NTK; t++) {
-		const int      j    = h + t * RVC_H;
+		const int      j    = h + t * RVP_H;
 		const uint32_t inst = inst0 + (j < nj ? j : nj - 1);
 		rb[t]     = rv_buf (P.rvB, P, inst, hc) + n;
 		in[t]     = P.mid1 + (size_t)inst * P.midStride + n;
@@ -2731,12 +2669,10 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 		pB[0][t]  = rb[t][0];
 		pB[1][t]  = rb[t][(size_t)min (1, nT - 1) * RVC_T];
 		pIn[0][t] = pIn[1][t] = 0.f;
-#if RVP_SPLIT
 		for (int k = 0; k < 3; k++) {
 			cB[t][k] = cst[inst].bq[1][k];
 			cC[t][k] = cst[inst].bq[2][k];
 		}
-#endif
 	}
 	__syncthreads ();
 	RVP_PROF_DECL ();
@@ -2751,7 +2687,7 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 #pragma unroll
 			for (int t = 0; t < RVP_NTK; t++) {
 				const double wet = rld (wetv[t], ob);
-				const int    r   = 2 * (h + t * RVC_H) + hc;
+				const int    r   = 2 * (h + t * RVP_H) + hc;
 				double       x   = sm.z[b][r][n];
 				if (wet != 1.0) {
 					double dry = (double)qIn[t];
@@ -2769,18 +2705,14 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 		double av[RVP_NTK];
 #pragma unroll
 		for (int t = 0; t < RVP_NTK; t++)
-			av[t] = sm.y[b][2 * (h + t * RVC_H) + hc][n];
+			av[t] = sm.y[b][2 * (h + t * RVP_H) + hc][n];
 		if (it < nT) {
 #pragma unroll
 			for (int t = 0; t < RVP_NTK; t++) {
-				const int r = 2 * (h + t * RVC_H) + hc;
-#if RVP_SPLIT
+				const int r = 2 * (h + t * RVP_H) + hc;
 				sm.y[b][r][n]  = qB[t] * cB[t][0];
 				sm.y1[b][r][n] = qB[t] * cB[t][1];
 				sm.y2[b][r][n] = qB[t] * cB[t][2];
-#else
-				sm.y[b][r][n] = qB[t];
-#endif
 			}
 		}
 		/* HBM reads into the set just consumed (indices clamped, so the loads need no
@@ -2818,21 +2750,17 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 			}
 #pragma unroll
 			for (int t = 0; t < RVP_NTK; t++) {
-				const int r = 2 * (h + t * RVC_H) + hc;
-#if RVP_SPLIT
+				const int r = 2 * (h + t * RVP_H) + hc;
 				sm.z[b][r][n]  = as[t] * cC[t][0];
 				sm.z1[b][r][n] = as[t] * cC[t][1];
 				sm.z2[b][r][n] = as[t] * cC[t][2];
-#else
-				sm.z[b][r][n] = as[t];
-#endif
 			}
 		}
 		if (it >= 4) {
 			const size_t so = (size_t)(it - 4) * RVC_T;
 #pragma unroll
 			for (int t = 0; t < RVP_NTK; t++)
-				if (h + t * RVC_H < nj && (tap || hc == 0))
+				if (h + t * RVP_H < nj && (tap || hc == 0))
 					out[t][so] = yv[t];
 		}
 		RVP_T1 ();

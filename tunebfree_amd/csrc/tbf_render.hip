@@ -803,7 +803,7 @@ k_tonegen (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl, const tbf_tp
 #define MP_SIN_PAIRS 0 /* the density sines in pairs (tbf_sin2) instead of one vote for all tasks */
 #endif
 #ifndef MP_PRIO
-#define MP_PRIO 0 /* the helpers raise their priority at the waveshaper's start and drop it after density
+#define MP_PRIO 2 /* the helpers raise their priority at the waveshaper's start and drop it after density
                    * step MP_PRIO - 1, so the two helpers of a SIMD progress together instead of in age order */
 #endif
 #ifndef MP_WIDE
@@ -1716,7 +1716,7 @@ __device__ __forceinline__ void rvl_write (double* rg, int i, int d, double v)
 #define RVL_FAST2 1 /* tap index without the FP64 sum (a vote on the rare carry), allpass products as fmas (exact) */
 #endif
 #ifndef RVL_PRIO
-#define RVL_PRIO 0 /* workers raise their priority at a phase start and drop it part-way, so the three workers
+#define RVL_PRIO 1 /* workers raise their priority at a phase start and drop it part-way, so the three workers
                     * of a SIMD progress together instead of in age order (1: drop after the tap reads, 2: after
                     * the Householder mix) */
 #endif

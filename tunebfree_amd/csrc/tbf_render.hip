@@ -2351,13 +2351,6 @@ __device__ __forceinline__ void rvc_serial_p (double* r0, const double* r1, cons
 	PRIO_DOWN ();
 }
 
-#ifndef RVQ_PRIO
-#define RVQ_PRIO 0 /* k_rv_pre helpers: priority up at an iteration's start, down after the first sine pair
-                    * (the helpers of a SIMD progress together instead of in age order) */
-#endif
-#ifndef RVP_PRIO
-#define RVP_PRIO 0 /* k_rv_post helpers: priority up at an iteration's start, down before the asin */
-#endif
 struct RvPreLds {
 	double   x[2][RVC_NC][RVC_S]; /* predelayed input -> biquadA output, in place */
 	uint32_t f[2][RVC_NC][RVC_S]; /* fpdL / fpdR of the sample delayM back (the predelay's input guard) */
@@ -2472,9 +2465,6 @@ k_rv_pre (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 	}
 	__syncthreads ();
 	auto step = [&] (const int it, float (&qIn)[RVC_NTK]) {
-#if RVQ_PRIO
-		__builtin_amdgcn_s_setprio (1);
-#endif
 		const int b = it & 1; /* tiles it and it - 2 share the buffer */
 		double    sv[RVC_NTK];
 		/* the filtered tile it - 2, read before tile it overwrites it */
@@ -2512,10 +2502,6 @@ k_rv_pre (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 #pragma unroll
 			for (int t = 0; t + 1 < RVC_NTK; t += 2) {
 				tbf_sin2 (sx[t], sx[t + 1], sx[t], sx[t + 1]);
-#if RVQ_PRIO
-				if (t == 0)
-					__builtin_amdgcn_s_setprio (0);
-#endif
 			}
 			if (RVC_NTK & 1)
 				sx[RVC_NTK - 1] = tbf_sin (sx[RVC_NTK - 1]);
@@ -2524,9 +2510,6 @@ k_rv_pre (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 				if (h + t * RVC_H < nj)
 					ra[t][(size_t)k2 * RVC_T] = sx[t];
 		}
-#if RVQ_PRIO
-		__builtin_amdgcn_s_setprio (0);
-#endif
 		__syncthreads ();
 	};
 #pragma unroll 1
@@ -2699,9 +2682,6 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 	RVP_PROF_DECL ();
 	auto step = [&] (const int it, double (&qB)[RVP_NTK], float (&qIn)[RVP_NTK]) {
 		RVP_T0 ();
-#if RVP_PRIO
-		__builtin_amdgcn_s_setprio (1);
-#endif
 		const int b = it & 1; /* tiles it, it - 2 and it - 4 share the buffers */
 		/* output of tile it - 4: dry mix, dither, mono sum (src/reverb.cpp:766-787); the
 		 * half-waves hold L and R, and 0.7071 (L + R) == 0.7071 (R + L) */
@@ -2748,9 +2728,6 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 			qB[t]  = rb[t][(size_t)tb * RVC_T];
 			qIn[t] = in[t][(size_t)ti * RVC_T];
 		}
-#if RVP_PRIO
-		__builtin_amdgcn_s_setprio (0);
-#endif
 		if (it >= 2 && it - 2 < nT) {
 			double y[RVP_NTK];
 			bool   small = true;

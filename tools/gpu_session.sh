@@ -21,6 +21,8 @@
 #   ctlab:LIB  same-box A/B of dense / every-8 events: the in-tree library against LIB,
 #           alternating, two runs each (LIB: a build of the round's start, for example)
 #   calib   PMC byte counters on known aligned / misaligned streams
+#   smoke   __graft_entry__.smoke() (the driver's round-end check)
+#   world2  two bench ranks through bench.py's own launcher, both on device 0 (rehearsal)
 set -u
 TAG=${1:-dev}; shift || true
 STEPS=${*:-"tests pmc fbench full"}
@@ -109,6 +111,8 @@ for s in $STEPS; do
 	calib) # FETCH_SIZE / WRITE_SIZE of known streams: aligned and 64 B misaligned 8-B/lane reads and writes
 		run calib_f 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/calib_f" -o run --output-format csv -- python3 tools/calib_pmc.py 2 0,2,1,3
 		run calib_w 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/calib_w" -o run --output-format csv -- python3 tools/calib_pmc.py 2 0,2,1,3 ;;
+	smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
+	world2) run world2 400 env TBF_BENCH_ONE_DEVICE=1 python3 bench.py --gpus 2 --batch 1024 --cpu-baseline 0 --steps 3 --warmup 1 ;;
 	ab:*) # ab:VAR=VALUE -- the default bench with one environment switch (A/B)
 		kv=${s#ab:}
 		run "ab_${kv//[^A-Za-z0-9_]/_}" 300 env "$kv" python3 bench.py --cpu-baseline 0 ;;

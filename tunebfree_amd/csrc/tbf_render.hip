@@ -1720,6 +1720,14 @@ __device__ __forceinline__ void rvl_write (double* rg, int i, int d, double v)
                     * of a SIMD progress together instead of in age order (1: drop after the tap reads, 2: after
                     * the Householder mix) */
 #endif
+#ifndef RVL_EXPECT
+#define RVL_EXPECT 1 /* the ring wrap / mirror branches marked unlikely, so the common case falls through */
+#endif
+#if RVL_EXPECT
+#define RVL_RARE(x) __builtin_expect (!!(x), 0)
+#else
+#define RVL_RARE(x) (x)
+#endif
 #ifndef RVL_SCAL
 #define RVL_SCAL 1 /* the workers' line counters in scalar registers, wraps as scalar branches (below) */
 #endif
@@ -1730,7 +1738,7 @@ template <int D>
 __device__ __forceinline__ int rvl_slot (int c, int n)
 {
 	int s = c + n;
-	if (c > D - (NL - 1)) {
+	if (RVL_RARE (c > D - (NL - 1))) {
 		/* opaque to the optimizer, so the branch stays a branch (if-converted, the lanes'
 		 * compare and selects ran in every sub-block) */
 		__asm__ __volatile__ ("" : "+v"(s));
@@ -1759,7 +1767,7 @@ __device__ __forceinline__ int rvl_slot_l (int l, const int (&cs)[12], int n)
 template <int D>
 __device__ __forceinline__ void rvl_write_s (double* rg, int c, int n, double v)
 {
-	if (c >= RVL_MIR && c <= D - (NL - 1)) { /* the common case: no wrap, no mirror */
+	if (!RVL_RARE (c < RVL_MIR || c > D - (NL - 1))) { /* the common case: no wrap, no mirror */
 		rg[c + n] = v;
 	} else {
 		int i = c + n;

@@ -2751,7 +2751,7 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 			/* every task's value inside OCML asin's polynomial branch (the tap mix is small):
 			 * that branch alone, straight-line, so the tasks' chains interleave (tbf_sin.h) */
 			double as[RVP_NTK];
-			if (__all (small)) {
+			if (TBF_LIKELY (__all (small))) {
 #pragma unroll
 				for (int t = 0; t < RVP_NTK; t++)
 					as[t] = tbf_asin_poly (y[t]);
@@ -2789,6 +2789,15 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 }
 
 /* ================================================================== k_whirl */
+#ifndef WH_EXPECT
+#define WH_EXPECT 1 /* rare paths (bypass, horn A catching up, a wrapped drum window, the rotor-angle and
+                     * motion replays, a new parameter set) marked unlikely: the common case falls through */
+#endif
+#if WH_EXPECT
+#define WH_RARE(x) __builtin_expect (!!(x), 0)
+#else
+#define WH_RARE(x) (x)
+#endif
 __device__ void whirl_speed (tbf_wh_state& st, const tbf_inst_const& K, int revOpt, int& brake)
 {
 	/* the rotor state in registers: its LDS reads issued together, not one per branch */
@@ -3115,7 +3124,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 	const float*  bfw   = P.whBw;
 	const float*  bbw   = P.whBw + 16384 * 5;
 
-	if (bypass) {
+	if (WH_RARE (bypass)) {
 		/* whirlProc2 bypass (src/whirl.cpp:1197-1215) + whirlProc3 mix */
 		nx0 = inNext[lane];
 		nx1 = inNext[lane + NL];
@@ -3178,12 +3187,12 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 		const int  ap    = sm.ap;
 		const bool aNext = sb + 1 < TBF_BLK / TBF_SUB || hasNext;
 #ifndef WH_ABL_HORN
-		if (!sm.aReady)
+		if (WH_RARE (!sm.aReady))
 			sm.ab[ap ^ 1][n] = xin;
 		if (aNext)
 			sm.ab[ap][n] = (float)((double)(sb + 1 < TBF_BLK / TBF_SUB ? in1 : nx0) + 1e-14);
 		wave_sync ();
-		if (!sm.aReady) {
+		if (WH_RARE (!sm.aReady)) {
 			const float z0 = st.fz[0][0], z1 = st.fz[0][1];
 #ifndef WH_NO_SERIAL
 			if (lane == 0)
@@ -3216,7 +3225,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 		if (lane < 4 && (lane > 0 || aNext)) {
 #endif
 			float* row = lane == 0 ? sm.ab[ap] : (lane == 1 ? sm.ab[ap ^ 1] : sm.wring[lane]);
-			if (wrap)
+			if (WH_RARE (wrap))
 				wh_serial<true> (row, lane < 2 ? 0u : wb, lane < 2 ? ~0u : WM, st.fz[lane], fa0, fa1, lane == 0 && scrubA);
 			else
 				wh_serial_v (row + (lane < 2 ? 0u : wb), st.fz[lane], fa0, fa1, lane == 0 && scrubA);
@@ -3253,7 +3262,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 			ha = h0 + (double)n * Dh;
 			da = d0 + (double)n * Dd;
 			double he = h0 + (double)TBF_SUB * Dh, de = d0 + (double)TBF_SUB * Dd;
-			if (!(okh && okd)) { /* wave-uniform: every lane replays the recurrence, lane n keeps step n */
+			if (WH_RARE (!(okh && okd))) { /* wave-uniform: every lane replays the recurrence, lane n keeps step n */
 				if (lane == 0)
 					atomicOr (P.errFlags, (uint32_t)TBF_PATH_WH_ANGLE);
 				double a = h0, b = d0;
@@ -3399,7 +3408,7 @@ __device__ void stage_whirl (const tbf_launch& P, WhLds<W>& sm, const bool bypas
 				okr[gi] = bad == 0 && !(P.dbg & TBF_DEBUG_FORCE_SERIAL);
 				allOk   = allOk && okr[gi];
 			}
-			if (allOk) {
+			if (!WH_RARE (!allOk)) {
 				/* every ring on its fast path: the rings are independent, so each pass
 				 * (farthest motion first) updates all of them in one LDS round trip */
 #pragma unroll
@@ -3537,7 +3546,7 @@ k_whirl (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_s
 		const bool more = blk + 1 < P.nBlocks;
 		/* a new parameter set (MIDI control functions) from this block on */
 		const int ws = rl (wsv, blk_lane ((int)blk));
-		if (ws) {
+		if (WH_RARE (ws)) {
 			const uint32_t* src = (const uint32_t*)(P.whSets + (ws - 1));
 			if (threadIdx.x < sizeof (tbf_wh_params) / 4)
 				((uint32_t*)&sm.st.prm)[threadIdx.x] = src[threadIdx.x];

@@ -101,6 +101,17 @@ __device__ __forceinline__ double tbf_sin_small (double x, double a, double n)
 	return __builtin_bit_cast (double, r ^ f);
 }
 
+#ifndef SIN_EXPECT
+#define SIN_EXPECT 1 /* the first fast path (every lane's quadrant 0) likely, the library call for huge
+                      * arguments unlikely: the compiler lays the common path out as the fall-through */
+#endif
+#if SIN_EXPECT
+#define TBF_LIKELY(x) __builtin_expect (!!(x), 1)
+#define TBF_UNLIKELY(x) __builtin_expect (!!(x), 0)
+#else
+#define TBF_LIKELY(x) (x)
+#define TBF_UNLIKELY(x) (x)
+#endif
 #define TBF_N(a) __builtin_rint ((a) * TBF_D (0x3FE45F306DC9C883))
 #define TBF_SMALL(a) ((a) < TBF_D (0x41D0000000000000)) /* 2^30; false for NaN (OCML's test) */
 
@@ -109,14 +120,14 @@ __device__ __forceinline__ double tbf_sin (double x)
 {
 	const double a = fabs (x);
 	const double n = TBF_N (a);
-	if (__all (n == 0.0))
+	if (TBF_LIKELY (__all (n == 0.0)))
 		return tbf_sign_of (tbf_sinred (a, 0.0), x);
 	if (__all (n == 1.0)) {
 		double hi, lo;
 		tbf_trigred_small (a, 1.0, hi, lo);
 		return tbf_sign_of (tbf_cosred (hi, lo), x);
 	}
-	if (__all (TBF_SMALL (a)))
+	if (!TBF_UNLIKELY (!__all (TBF_SMALL (a))))
 		return tbf_sin_small (x, a, n);
 	return sin (x);
 }
@@ -128,7 +139,7 @@ __device__ __forceinline__ void tbf_sin2 (double x0, double x1, double& r0, doub
 {
 	const double a0 = fabs (x0), a1 = fabs (x1);
 	const double n0 = TBF_N (a0), n1 = TBF_N (a1);
-	if (__all (n0 == 0.0 && n1 == 0.0)) {
+	if (TBF_LIKELY (__all (n0 == 0.0 && n1 == 0.0))) {
 		r0 = tbf_sign_of (tbf_sinred (a0, 0.0), x0);
 		r1 = tbf_sign_of (tbf_sinred (a1, 0.0), x1);
 	} else if (__all (n0 == 1.0 && n1 == 1.0)) {
@@ -137,7 +148,7 @@ __device__ __forceinline__ void tbf_sin2 (double x0, double x1, double& r0, doub
 		tbf_trigred_small (a1, 1.0, h1, l1);
 		r0 = tbf_sign_of (tbf_cosred (h0, l0), x0);
 		r1 = tbf_sign_of (tbf_cosred (h1, l1), x1);
-	} else if (__all (TBF_SMALL (a0) && TBF_SMALL (a1))) {
+	} else if (!TBF_UNLIKELY (!__all (TBF_SMALL (a0) && TBF_SMALL (a1)))) {
 		r0 = tbf_sin_small (x0, a0, n0);
 		r1 = tbf_sin_small (x1, a1, n1);
 	} else {
@@ -160,7 +171,7 @@ __device__ __forceinline__ void tbf_sin_n (double (&x)[N])
 		o    = o && n[i] == 1.0;
 		sm   = sm && TBF_SMALL (a[i]);
 	}
-	if (__all (z)) {
+	if (TBF_LIKELY (__all (z))) {
 #pragma unroll
 		for (int i = 0; i < N; i++)
 			x[i] = tbf_sign_of (tbf_sinred (a[i], 0.0), x[i]);
@@ -171,7 +182,7 @@ __device__ __forceinline__ void tbf_sin_n (double (&x)[N])
 			tbf_trigred_small (a[i], 1.0, hi, lo);
 			x[i] = tbf_sign_of (tbf_cosred (hi, lo), x[i]);
 		}
-	} else if (__all (sm)) {
+	} else if (!TBF_UNLIKELY (!__all (sm))) {
 #pragma unroll
 		for (int i = 0; i < N; i++)
 			x[i] = tbf_sin_small (x[i], a[i], n[i]);

@@ -46,6 +46,12 @@
 #define TG_ABL 0 /* timing experiments (wrong output): 1 bank reads from one row, 2 no scanner */
 #endif
 #define TG_PCAP 128    /* a delta chunk's program entries staged in LDS per block (longer: read from HBM) */
+#ifndef TG_GRFL
+#define TG_GRFL 0 /* 1: the entries' gains moved to scalar registers (v_readfirstlane) after their LDS reads */
+#endif
+#ifndef TG_LCACHE
+#define TG_LCACHE 1 /* TG_CACHE's per-entry bank position, end and length in LDS, not in the lanes */
+#endif
 #define RV_WAVES 3
 /* k_whirl: 4 waves per SIMD (128 VGPRs, 9.8 KB of LDS: 16 instances per CU, so 4096 run
  * at once on 256 CUs), motions and ring adds in 2 groups of 2 rings (4 rings per group
@@ -79,6 +85,12 @@ template <int K> struct IntC {
 /* ------------------------------------------------------------------ LDS layouts */
 struct TgLds {
 	tbf_tg_state st;
+#if TG_LCACHE
+	/* TG_CACHE, entry e < 2 NL: bank index of the wheel's current sample, and the wave's end
+	 * and length in the bank (a block advances the index by TBF_BLK, less the length past
+	 * the end) */
+	uint32_t     cbase[2 * NL], cend[2 * NL], clen[2 * NL];
+#endif
 	float        swl[TBF_BLK];
 	float        vin[TBF_BLK];
 	float        prc[TBF_BLK];
@@ -339,9 +351,54 @@ struct TgCache {
 	bool     on;
 	int      np;
 	bool     anyEnv;
+#if !TG_LCACHE
 	uint32_t w[2], len[2], off[2], pos[2];
+#endif
 };
 
+#if TG_LCACHE
+/* The positions live in LDS (sm.cbase / cend / clen): held in the lanes, they were spilled
+ * around the interpreter, and each block's reload from scratch waited (vmcnt) for the
+ * previous block's output stores too. */
+__device__ __forceinline__ void tg_cache_load (TgCache& c, const tbf_launch& P, TgLds& sm, const tbf_seg_ctl& G,
+                                               const tbf_tpl_desc* T)
+{
+	const int             lane = threadIdx.x & (NL - 1);
+	const tbf_prog_entry* prog = P.prog + G.prog_off + 1;
+	c.np                       = (int)P.prog[G.prog_off].pad;
+	c.on                       = c.np <= 2 * NL;
+	int env                    = 0;
+#pragma unroll
+	for (int k = 0; k < 2; k++) {
+		const int e = lane + k * NL;
+		if (c.on && e < c.np) {
+			const uint32_t w = prog[e].wheel, len = T->len[w], off = T->off[w];
+			sm.cbase[e]      = off + sm.st.pos[w];
+			sm.cend[e]       = off + len;
+			sm.clen[e]       = len;
+			env |= prog[e].env != 0;
+		}
+	}
+	c.anyEnv = __any (env);
+}
+
+__device__ __forceinline__ void tg_cache_store (const TgCache& c, TgLds& sm, const tbf_launch& P, const tbf_seg_ctl& G,
+                                                const tbf_tpl_desc* T)
+{
+	const int             lane = threadIdx.x & (NL - 1);
+	const tbf_prog_entry* prog = P.prog + G.prog_off + 1;
+	if (!c.on)
+		return;
+#pragma unroll
+	for (int k = 0; k < 2; k++) {
+		const int e = lane + k * NL;
+		if (e < c.np) {
+			const uint32_t w = prog[e].wheel;
+			sm.st.pos[w]     = sm.cbase[e] - T->off[w];
+		}
+	}
+}
+#else
 __device__ __forceinline__ void tg_cache_load (TgCache& c, const tbf_launch& P, const TgLds& sm, const tbf_seg_ctl& G,
                                                const tbf_tpl_desc* T)
 {
@@ -376,6 +433,7 @@ __device__ __forceinline__ void tg_cache_store (const TgCache& c, TgLds& sm)
 		if (lane + k * NL < c.np)
 			sm.st.pos[c.w[k]] = c.pos[k];
 }
+#endif
 
 /* oscGenerateFragment core interpreter + vibratoProc + mixdown, src/tonegen.cpp:3607-3777 */
 __device__ __forceinline__ void stage_tonegen (const tbf_launch& P, TgLds& sm, const tbf_seg_ctl& G, const tbf_tpl_desc* T,
@@ -403,11 +461,17 @@ __device__ __forceinline__ void stage_tonegen (const tbf_launch& P, TgLds& sm, c
 		/* the launch's program, entries held in the lanes (TgCache) */
 #pragma unroll
 		for (int k = 0; k < 2; k++) {
-			const uint32_t pos = tc->pos[k], len = tc->len[k];
 			const int e = lane + k * NL;
 			if (e < np) {
+#if TG_LCACHE
+				const uint32_t b = sm.cbase[e], nb = b + TBF_BLK; /* off + pos, off + pos + TBF_BLK */
+				sm.u.ent.base[e] = b;
+				sm.cbase[e]      = (sm.cend[e] < nb) ? nb - sm.clen[e] : nb; /* (len < pos + TBF_BLK) as below */
+#else
+				const uint32_t pos = tc->pos[k], len = tc->len[k];
 				sm.u.ent.base[e] = tc->off[k] + pos;
 				tc->pos[k]       = (len < pos + TBF_BLK) ? pos + TBF_BLK - len : pos + TBF_BLK;
+#endif
 				if (lp) { /* the gains through LDS too (the scanner's rows overwrite them each block) */
 					const uint4 a = ((const uint4*)(prog + e))[0], b = ((const uint4*)(prog + e))[1];
 					sm.u.ent.g[e] = make_float4 (__uint_as_float (a.y), __uint_as_float (a.z), __uint_as_float (a.w), __uint_as_float (b.x));
@@ -452,8 +516,14 @@ __device__ __forceinline__ void stage_tonegen (const tbf_launch& P, TgLds& sm, c
 				 * is then a scalar branch, so a steady entry skips the envelope arithmetic */
 				const float4 a = sm.u.ent.g[e];
 				const float2 b = sm.u.ent.h[e];
+#if TG_GRFL
 				auto rfl = [] (float v) { return __int_as_float (__builtin_amdgcn_readfirstlane (__float_as_int (v))); };
 				g[0] = rfl (a.x); g[1] = rfl (a.y); g[2] = rfl (a.z); g[3] = rfl (a.w); g[4] = rfl (b.x); g[5] = rfl (b.y);
+#else
+				/* the gains stay in the lanes (every lane read the same LDS word): only the
+				 * envelope word needs to be scalar, for the branch */
+				g[0] = a.x; g[1] = a.y; g[2] = a.z; g[3] = a.w; g[4] = b.x; g[5] = b.y;
+#endif
 				er = (uint32_t)__builtin_amdgcn_readfirstlane ((int)sm.u.ent.er[e]);
 			} else {
 				const tbf_prog_entry& E = prog[e];
@@ -763,7 +833,11 @@ k_tonegen (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl, const tbf_tp
 			stage_tonegen (P, sm, ctl_of (P, ctl, blk, inst), T, o + (size_t)blk * TBF_BLK, nullptr, nullptr, 0.f, 0.f, &tc);
 	}
 	if (part == ns - 1) {
+#if TG_LCACHE
+		tg_cache_store (tc, sm, P, ctl_of (P, ctl, 0, inst), T);
+#else
 		tg_cache_store (tc, sm);
+#endif
 		wave_sync ();
 		const uint32_t* src = (const uint32_t*)&sm.st;
 		uint32_t*       dst = (uint32_t*)S;
@@ -2751,7 +2825,7 @@ k_rv_post (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf
 			/* every task's value inside OCML asin's polynomial branch (the tap mix is small):
 			 * that branch alone, straight-line, so the tasks' chains interleave (tbf_sin.h) */
 			double as[RVP_NTK];
-			if (TBF_LIKELY (__all (small))) {
+			if (__all (small)) {
 #pragma unroll
 				for (int t = 0; t < RVP_NTK; t++)
 					as[t] = tbf_asin_poly (y[t]);
@@ -3811,7 +3885,7 @@ __device__ void whirl_horn (const tbf_launch& P, WhLds<W>& sm, const bool bypass
 {
 	const int     lane = threadIdx.x & (NL - 1), n = lane;
 	tbf_wh_state& st   = sm.st;
-	if (bypass) {
+	if (WH_RARE (bypass)) {
 		/* whirlProc2 bypass (src/whirl.cpp:1197-1215) + whirlProc3 mix (see stage_whirl) */
 		nx0 = inNext[lane];
 		nx1 = inNext[lane + NL];
@@ -3858,12 +3932,12 @@ __device__ void whirl_horn (const tbf_launch& P, WhLds<W>& sm, const bool bypass
 		/* horn A runs one sub-block ahead (see stage_whirl) */
 		const int  ap    = sm.ap;
 		const bool aNext = sb + 1 < TBF_BLK / TBF_SUB || hasNext;
-		if (!sm.aReady)
+		if (WH_RARE (!sm.aReady))
 			sm.ab[ap ^ 1][n] = xin;
 		if (aNext)
 			sm.ab[ap][n] = (float)((double)(sb + 1 < TBF_BLK / TBF_SUB ? in1 : nx0) + 1e-14);
 		wave_sync ();
-		if (!sm.aReady) {
+		if (WH_RARE (!sm.aReady)) {
 			const float z0 = st.fz[0][0], z1 = st.fz[0][1];
 			if (lane == 0)
 				wh_serial_v (sm.ab[ap ^ 1], st.fz[0], ha[0], ha[1], false);
@@ -3957,7 +4031,7 @@ __device__ void whirl_drum (const tbf_launch& P, WhLds<W>& sm, const bool bypass
 {
 	const int     lane = threadIdx.x & (NL - 1), n = lane;
 	tbf_wh_state& st   = sm.st;
-	if (bypass) {
+	if (WH_RARE (bypass)) {
 		nx0 = inNext[lane];
 		nx1 = inNext[lane + NL];
 		return;
@@ -3980,7 +4054,7 @@ __device__ void whirl_drum (const tbf_launch& P, WhLds<W>& sm, const bool bypass
 		const bool     wrap = wb + TBF_SUB > (uint32_t)W;
 		if (lane < 2) {
 			float* row = sm.wring[2 + lane];
-			if (wrap)
+			if (WH_RARE (wrap))
 				wh_serial<true> (row, wb, WM, st.fz[2 + lane], K.drf[0], K.drf[1], false);
 			else
 				wh_serial_v (row + wb, st.fz[2 + lane], K.drf[0], K.drf[1], false);
@@ -4077,7 +4151,7 @@ k_whirl_split (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const
 		/* a new parameter set from this block on: both waves copy it (the same words; the
 		 * other wave is past its last read of the old set, k_whirl_split's barriers) */
 		const int ws = rl (wsv, blk_lane ((int)blk));
-		if (ws) {
+		if (WH_RARE (ws)) {
 			const uint32_t* src = (const uint32_t*)(P.whSets + (ws - 1));
 			if (lane < (int)(sizeof (tbf_wh_params) / 4))
 				((uint32_t*)&sm.st.prm)[lane] = src[lane];

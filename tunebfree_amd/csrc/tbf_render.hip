@@ -880,14 +880,6 @@ k_tonegen (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl, const tbf_tp
 #define MP_PRIO 2 /* the helpers raise their priority at the waveshaper's start and drop it after density
                    * step MP_PRIO - 1, so the two helpers of a SIMD progress together instead of in age order */
 #endif
-#ifndef MP_EXPECT
-#define MP_EXPECT 1 /* the preamp on and a positive density (the waveshaper's sine path) hinted likely */
-#endif
-#if MP_EXPECT
-#define MP_LIKELY(x) __builtin_expect (!!(x), 1)
-#else
-#define MP_LIKELY(x) (x)
-#endif
 #ifndef MP_WIDE
 #define MP_WIDE 1 /* tiles of 64 samples, a helper task = one instance (0: 32, an instance pair) */
 #endif
@@ -1041,7 +1033,7 @@ __device__ __forceinline__ void preamp_shape_n (const double (&x0)[NT], const do
 		if (br[t] > 1.57079633)
 			br[t] = 1.57079633;
 	}
-	if (MP_LIKELY (__all (dpos))) {
+	if (__all (dpos)) {
 		tbf_sin_n<NT> (br);
 	} else {
 #pragma unroll
@@ -1330,7 +1322,7 @@ k_mixpre (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl)
 #endif
 					allCl = allCl && cl[t];
 				}
-				if (MP_LIKELY (!__all (allCl)))
+				if (!__all (allCl))
 					preamp_shape_n<MP_NTK> (xh, xd, Cp, f1, ys);
 #pragma unroll
 				for (int t = 0; t < MP_NTK; t++)

@@ -865,7 +865,10 @@ k_tonegen (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl, const tbf_tp
  * reference's operations in its order.  Tonegen-only chains (configs[1]) stop after the
  * products, which are then the output. */
 #ifndef MP_CB
-#define MP_CB 32                  /* instances per workgroup */
+/* instances per workgroup: 28 with 14 helper waves (16 waves, 147 workgroups at 4096
+ * instances) hide more of the waveshaper's FP64 latency than 32 with 8 (10 waves, 128):
+ * alone 6.72 -> 5.23 ms per 512 blocks, the step 115.5 -> 113.7 ms (profiles/r06/s19) */
+#define MP_CB 28
 #endif
 #ifndef MP_PROF
 #define MP_PROF 0 /* profiling variant: s_memtime per role and section (tools/mp_prof.py) */
@@ -900,7 +903,7 @@ k_tonegen (const tbf_launch P, const tbf_seg_ctl* __restrict__ ctl, const tbf_tp
 #define MP_S (MP_T + 1)           /* row stride of the per-sample rows (odd: conflict-free columns) */
 #define MP_HS (MP_T / 2 + 1)      /* row stride of the high-pass rows (a chain's MP_T / 2 samples) */
 #ifndef MP_H
-#define MP_H 8                    /* helper waves */
+#define MP_H 14                   /* helper waves */
 #endif
 #define MP_THREADS (NL * (2 + MP_H))
 #define MP_TPB (TBF_BLK / MP_T)   /* tiles per block */

@@ -2317,22 +2317,22 @@ k_rv_core_lds (const tbf_launch P, const tbf_inst_const* __restrict__ cst)
  * A tile's stages advance one per iteration, with one barrier per iteration.  Every
  * chain runs the reference's operations in its order, so the bits are the reference's. */
 #ifndef RVC_CB
-#define RVC_CB 32 /* instances per workgroup */
+/* instances per workgroup: 28 with 14 helper waves (147 workgroups) against 32 with 8: k_rv_pre
+ * alone 2.79 -> 2.37 ms per 512 blocks, the step 113.6 -> 113.2 ms (profiles/r06/s21) */
+#define RVC_CB 28
 #endif
 #define RVC_NC (2 * RVC_CB)      /* chains per workgroup (<= 64: one per lane of wave 0) */
 #define RVC_T 32                 /* samples per tile: one per lane of a half-wave */
 #define RVC_S (RVC_T + 1)        /* LDS row stride (odd: conflict-free columns) */
 #ifndef RVC_H
-#define RVC_H 8 /* helper waves */
+#define RVC_H 14 /* helper waves */
 #endif
 #define RVC_TASKS RVC_CB          /* helper tasks per tile: one instance each */
 #define RVC_NTK (RVC_TASKS / RVC_H)
 static_assert (RVC_TASKS % RVC_H == 0, "helper tasks split evenly");
 #define RVC_THREADS (NL * (2 + RVC_H))
 static_assert (RVC_NC <= NL && RVC_T * 2 == NL && TBF_BLK % RVC_T == 0, "chain-block geometry");
-/* k_rv_pre's serial and dither waves address row `lane` of every chain array: one chain per
- * lane of the wave, no idle row (k_rv_post has one, RVP_ROWS) */
-static_assert (RVC_NC == NL, "k_rv_pre: a chain for every lane");
+#define RVC_ROWS (RVC_NC + (RVC_NC < NL)) /* chain rows, + one that the serial and dither waves' idle lanes use */
 
 /* one transposed-DF2 biquad step (biquadA/B/C, src/reverb.cpp:361-369, 733-741, 756-764) */
 __device__ __forceinline__ double rvc_bq (double x, double c0, double c1, double c2, double c3, double c4, double& s7,
@@ -2437,8 +2437,8 @@ __device__ __forceinline__ void rvc_serial_p (double* r0, const double* r1, cons
 }
 
 struct RvPreLds {
-	double   x[2][RVC_NC][RVC_S]; /* predelayed input -> biquadA output, in place */
-	uint32_t f[2][RVC_NC][RVC_S]; /* fpdL / fpdR of the sample delayM back (the predelay's input guard) */
+	double   x[2][RVC_ROWS][RVC_S]; /* predelayed input -> biquadA output, in place */
+	uint32_t f[2][RVC_ROWS][RVC_S]; /* fpdL / fpdR of the sample delayM back (the predelay's input guard) */
 };
 
 /* predelay, denormal guard, biquadA, sin (x * wet) (src/reverb.cpp:339-375) -> rvA.
@@ -2464,6 +2464,7 @@ k_rv_pre (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 	/* waves 0, 1: lane = chain 2 j + c */
 	const int     cj = lane >> 1, cc = lane & 1;
 	const bool    cok = cj < nj;
+	const int     crow = lane < RVC_NC ? lane : RVC_NC; /* chain lanes past the block's chains: the idle row */
 	tbf_rv_state* CS  = &P.st[inst0 + (cok ? cj : 0)].rv;
 	if (w == 0) {
 		const double* cf   = cst[inst0 + (cok ? cj : 0)].bq[0];
@@ -2473,7 +2474,7 @@ k_rv_pre (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 #pragma unroll 1
 		for (int it = 0; it < nIt; it++) {
 			if (it >= 1 && it - 1 < nT) { /* biquadA of tile it - 1 */
-				double* const row[1] = {sm.x[(it - 1) & 1][lane]};
+				double* const row[1] = {sm.x[(it - 1) & 1][crow]};
 				rvc_serial<1> (row, c, s);
 			}
 			__syncthreads ();
@@ -2492,7 +2493,7 @@ k_rv_pre (const tbf_launch P, const tbf_inst_const* __restrict__ cst, const tbf_
 		uint32_t  fs   = cc ? CS->fpdR : CS->fpdL;
 		auto      row  = [&] (int k) {
             const int lead = min (max (d - age0 - k * RVC_T, 0), RVC_T); /* samples with no input yet */
-            uint32_t* f    = sm.f[k & 1][lane];
+            uint32_t* f    = sm.f[k & 1][crow];
 #pragma unroll 8
             for (int n = 0; n < RVC_T; n++) {
                 f[n] = fs;
